@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Headline benchmark: learner SGD steps/sec (+ env frames/sec) for the Atari
+Nature-CNN DQN on 1..8 MI355X (BASELINE.json "metric").
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Per GPU (weak scaling): minibatch 32 from an HBM replay of synthetic 84x84x4
+uint8 frames, random-init Nature-CNN (VALID convs 32/64/64, FC512, A=6),
+RMSProp (TF semantics), MSE TD loss, target copy every 10k steps — one full
+SGD step per timed step (sample, gather, online+target forward, loss,
+backward, gradient all-reduce over RCCL when N > 1, optimizer, target
+predicate). The device actor (``--actor_envs``, default 1 env x update_freq 4
+frames per SGD step = the reference's 1:4 ratio) runs inside each timed step
+and writes its frames into the same replay.
+Prints ONE JSON line on rank 0; ``value`` = total SGD steps/s over all ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "learner SGD steps/sec + env frames/sec, Atari Nature-CNN DQN at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=500)
+    ap.add_argument('--warmup', type=int, default=50)
+    ap.add_argument('--network', default='nature')
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--backend', default='auto', choices=['auto', 'hip', 'torch'])
+    ap.add_argument('--replay', type=int, default=200000)
+    ap.add_argument('--actions', type=int, default=6)
+    ap.add_argument('--actor_envs', type=int, default=1)
+    ap.add_argument('--update_freq', type=int, default=4)
+    ap.add_argument('--graph', type=int, default=1)
+    ap.add_argument('--extra', default='', help='extra config flags, e.g. "--dueling --double_dqn"')
+    args = ap.parse_args()
+
+    import shlex
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import broadcast_flat, init_distributed
+    from dist_dqn_amd.replay import DeviceReplay
+
+    cfg = preset('nature' if args.network == 'nature' else 'atari', 'Pong-v0',
+                 '--minibatch_size=%d --dtype=%s --backend=%s --hip_graph=%d --replay_memory_capacity=%d '
+                 '--update_freq=%d --seed=0 %s' % (args.batch, args.dtype, args.backend, args.graph, args.replay,
+                                                    args.update_freq, args.extra))
+    if args.network not in ('nature', 'cnn'):
+        cfg = cfg.replace(network=args.network)
+    ctx = init_distributed(cfg, device='cuda')
+    dev = ctx.device
+    assert dev.type == 'cuda', 'bench.py needs a GPU'
+    net = Network.create_network(cfg, (84, 84, 4), args.actions, num_replicas=ctx.world_size, device=dev)
+    broadcast_flat(ctx, net.online.flat)
+    net.target.copy_from(net.online)
+    replay = DeviceReplay(cfg.replay_memory_capacity, (84, 84), 4, device=dev,
+                          prioritized=cfg.prioritized_replay, seed=ctx.rank)
+    replay.fill_synthetic(cfg.replay_memory_capacity, args.actions, seed=ctx.rank)
+    learner = Learner(net, replay, cfg, ctx)
+    actor = None
+    if args.actor_envs > 0:
+        from dist_dqn_amd.actors.device_actor import DeviceActor
+        actor = DeviceActor(net, replay, cfg, num_envs=args.actor_envs, steps_per_call=args.update_freq,
+                            seed=1000 + ctx.rank)
+
+    def step():
+        if actor is not None:
+            actor.step()
+        learner.step()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if ctx.enabled:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t)
+    loss = float(learner.loss)
+    if ctx.rank == 0:
+        sps = args.steps * ctx.world_size / el
+        frames = (args.actor_envs * args.update_freq) * args.steps * ctx.world_size / el
+        out = {
+            'metric': METRIC, 'value': round(sps, 2), 'unit': 'SGD steps/s (all GPUs)',
+            'n_gpus': ctx.world_size, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(1000.0 * el / args.steps, 4), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic (random uint8 84x84 frames, random init)',
+            'env_frames_per_sec': round(frames, 1),
+            'samples_per_sec': round(sps * args.batch, 1),
+            'config': {'model': 'nature-cnn' if args.network == 'nature' else args.network,
+                       'global_batch': args.batch * ctx.world_size, 'seq_len': None,
+                       'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
+                       'frames_per_state': 4, 'optimizer': 'rmsprop(tf)', 'executor': net.executor.name,
+                       'hip_graph': bool(args.graph), 'actor_envs': args.actor_envs,
+                       'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
+                       'num_actions': args.actions, 'extra': args.extra, 'final_loss': loss},
+        }
+        print(json.dumps(out), flush=True)
+    if ctx.enabled:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

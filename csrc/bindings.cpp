@@ -1,0 +1,230 @@
+// Python bindings of dist_dqn_amd._C: validates every operand on the host
+// (device, dtype, contiguity, shapes the kernels assume) and launches on the
+// current HIP stream, so the ops are captured correctly into HIP graphs.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "include/dqn_host.h"
+#include "include/dqn_kernels.h"
+#include "include/dqn_nets.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype: ", (t).scalar_type())
+#define CHECK_T(t, dt) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_DT(t, dt)
+
+template <typename T>
+T* ptr(const torch::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+void replay_sample_uniform(torch::Tensor size, torch::Tensor rng, torch::Tensor out) {
+  CHECK_T(size, torch::kInt32); CHECK_T(rng, torch::kInt64); CHECK_T(out, torch::kInt32);
+  TORCH_CHECK(out.numel() >= 1 && out.numel() <= 1024, "sample batch must be in [1, 1024]");
+  TORCH_CHECK(rng.numel() == 2, "rng state must be [seed, counter]");
+  c10::hip::HIPGuard g(out.device());
+  launch_replay_sample_uniform(ptr<int32_t>(size), ptr<int64_t>(rng), ptr<int32_t>(out), (int)out.numel(),
+                               cur_stream());
+}
+
+void replay_gather_frames(torch::Tensor frames, torch::Tensor state_idx, torch::Tensor next_idx,
+                          torch::Tensor idx, torch::Tensor s, torch::Tensor ns) {
+  CHECK_T(frames, torch::kUInt8); CHECK_T(state_idx, torch::kInt32); CHECK_T(next_idx, torch::kInt32);
+  CHECK_T(idx, torch::kInt32); CHECK_T(s, torch::kUInt8); CHECK_T(ns, torch::kUInt8);
+  TORCH_CHECK(frames.dim() == 3 && state_idx.dim() == 2, "frames [F,H,W], state_idx [C,k]");
+  const int K = (int)state_idx.size(1);
+  const int HW = (int)(frames.size(1) * frames.size(2));
+  const int B = (int)idx.numel();
+  TORCH_CHECK(K >= 1 && K <= 4, "frames_per_state must be 1..4");
+  TORCH_CHECK(HW % 4 == 0, "H*W must be a multiple of 4");
+  TORCH_CHECK(s.numel() == (int64_t)B * HW * K && ns.numel() == s.numel(), "output size mismatch");
+  c10::hip::HIPGuard g(frames.device());
+  launch_replay_gather_frames(ptr<uint8_t>(frames), ptr<int32_t>(state_idx), ptr<int32_t>(next_idx),
+                              ptr<int32_t>(idx), ptr<uint8_t>(s), ptr<uint8_t>(ns), B, HW, K, cur_stream());
+}
+
+void sumtree_set(torch::Tensor sum, torch::Tensor mn, torch::Tensor maxp, torch::Tensor idx, torch::Tensor td,
+                 double alpha, double eps, bool use_max, int64_t P) {
+  CHECK_T(sum, torch::kFloat32); CHECK_T(mn, torch::kFloat32); CHECK_T(maxp, torch::kFloat32);
+  CHECK_T(idx, torch::kInt32); CHECK_T(td, torch::kFloat32);
+  TORCH_CHECK(sum.numel() == 2 * P && mn.numel() == 2 * P, "tree size must be 2P");
+  TORCH_CHECK(use_max || td.numel() >= idx.numel(), "td must cover idx");
+  c10::hip::HIPGuard g(sum.device());
+  launch_sumtree_set(ptr<float>(sum), ptr<float>(mn), ptr<float>(maxp), ptr<int32_t>(idx), ptr<float>(td),
+                     (float)alpha, (float)eps, use_max ? 1 : 0, (int)idx.numel(), (int)P, cur_stream());
+}
+
+void sumtree_sample(torch::Tensor sum, torch::Tensor mn, torch::Tensor rng, torch::Tensor size, torch::Tensor beta,
+                    torch::Tensor idx_out, torch::Tensor w_out, int64_t P) {
+  CHECK_T(sum, torch::kFloat32); CHECK_T(mn, torch::kFloat32); CHECK_T(rng, torch::kInt64);
+  CHECK_T(size, torch::kInt32); CHECK_T(beta, torch::kFloat32); CHECK_T(idx_out, torch::kInt32);
+  CHECK_T(w_out, torch::kFloat32);
+  TORCH_CHECK(idx_out.numel() <= 1024 && w_out.numel() == idx_out.numel(), "PER batch must be <= 1024");
+  TORCH_CHECK(sum.numel() == 2 * P, "tree size must be 2P");
+  c10::hip::HIPGuard g(sum.device());
+  launch_sumtree_sample(ptr<float>(sum), ptr<float>(mn), ptr<int64_t>(rng), ptr<int32_t>(size), ptr<float>(beta),
+                        ptr<int32_t>(idx_out), ptr<float>(w_out), (int)idx_out.numel(), (int)P, cur_stream());
+}
+
+void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s0, torch::Tensor s1,
+                    torch::Tensor beta_pow, torch::Tensor ticket, double lr, double reg, int64_t reg_end,
+                    double grad_scale, torch::Tensor step, bool has_step, std::vector<double> hp) {
+  CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
+  CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
+  TORCH_CHECK(w.numel() % 4 == 0 && grad.numel() == w.numel(), "flat buffers must match and be /4");
+  TORCH_CHECK(s0.numel() == w.numel() || s0.data_ptr() == w.data_ptr(), "slot 0 size");
+  TORCH_CHECK(s1.numel() == w.numel() || s1.data_ptr() == w.data_ptr(), "slot 1 size");
+  TORCH_CHECK(reg_end % 4 == 0 && reg_end <= w.numel(), "reg_end");
+  TORCH_CHECK(hp.size() == 9, "9 hyper-parameters expected");
+  if (has_step) { CHECK_T(step, torch::kInt64); }
+  float h[9];
+  for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
+  c10::hip::HIPGuard g(w.device());
+  launch_optimizer_step((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1),
+                        ptr<float>(beta_pow), has_step ? ptr<int64_t>(step) : nullptr, ptr<int32_t>(ticket), h,
+                        (float)lr, (float)reg, (int)reg_end, (float)grad_scale, (int)w.numel(), cur_stream());
+}
+
+void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tensor step, int64_t freq,
+                   bool use_step) {
+  CHECK_T(dst, torch::kFloat32); CHECK_T(src, torch::kFloat32);
+  TORCH_CHECK(dst.numel() == src.numel() && dst.numel() % 4 == 0, "target/online size");
+  if (use_step) { CHECK_T(step, torch::kInt64); }
+  c10::hip::HIPGuard g(dst.device());
+  launch_target_update(ptr<float>(dst), ptr<float>(src), (float)tau, use_step ? ptr<int64_t>(step) : nullptr,
+                       (int)freq, (int)dst.numel(), cur_stream());
+}
+
+void td_loss_scalar(torch::Tensor q, torch::Tensor qn_t, c10::optional<torch::Tensor> qn_o, torch::Tensor act,
+                    torch::Tensor rew, torch::Tensor done, torch::Tensor gam, c10::optional<torch::Tensor> wts,
+                    torch::Tensor loss, torch::Tensor dq, torch::Tensor prio, bool huber, double delta) {
+  CHECK_T(q, torch::kFloat32); CHECK_T(qn_t, torch::kFloat32); CHECK_T(act, torch::kInt32);
+  CHECK_T(rew, torch::kFloat32); CHECK_T(done, torch::kFloat32); CHECK_T(gam, torch::kFloat32);
+  CHECK_T(loss, torch::kFloat32); CHECK_T(dq, torch::kFloat32); CHECK_T(prio, torch::kFloat32);
+  const int B = (int)q.size(0), A = (int)q.size(1);
+  TORCH_CHECK(B >= 1 && B <= 1024, "TD-loss batch must be in [1, 1024]");
+  TORCH_CHECK(qn_t.sizes() == q.sizes() && dq.sizes() == q.sizes(), "Q shapes");
+  TORCH_CHECK(act.numel() == B && rew.numel() == B && done.numel() == B && gam.numel() == B && prio.numel() == B,
+              "per-sample vectors must be [B]");
+  const float* qo = nullptr;
+  if (qn_o.has_value()) { CHECK_T((*qn_o), torch::kFloat32); TORCH_CHECK(qn_o->sizes() == q.sizes()); qo = ptr<float>(*qn_o); }
+  const float* w = nullptr;
+  if (wts.has_value()) { CHECK_T((*wts), torch::kFloat32); TORCH_CHECK(wts->numel() == B); w = ptr<float>(*wts); }
+  c10::hip::HIPGuard g(q.device());
+  launch_td_loss_scalar(ptr<float>(q), ptr<float>(qn_t), qo, ptr<int32_t>(act), ptr<float>(rew), ptr<float>(done),
+                        ptr<float>(gam), w, ptr<float>(loss), ptr<float>(dq), ptr<float>(prio), B, A, huber ? 1 : 0,
+                        (float)delta, cur_stream());
+}
+
+void td_loss_c51(torch::Tensor lg, torch::Tensor lgn_t, c10::optional<torch::Tensor> lgn_o, torch::Tensor act,
+                 torch::Tensor rew, torch::Tensor done, torch::Tensor gam, c10::optional<torch::Tensor> wts,
+                 torch::Tensor loss, torch::Tensor dlg, torch::Tensor prio, double vmin, double vmax) {
+  CHECK_T(lg, torch::kFloat32); CHECK_T(lgn_t, torch::kFloat32); CHECK_T(act, torch::kInt32);
+  CHECK_T(rew, torch::kFloat32); CHECK_T(done, torch::kFloat32); CHECK_T(gam, torch::kFloat32);
+  CHECK_T(loss, torch::kFloat32); CHECK_T(dlg, torch::kFloat32); CHECK_T(prio, torch::kFloat32);
+  TORCH_CHECK(lg.dim() == 3, "logits must be [B, A, N]");
+  const int B = (int)lg.size(0), A = (int)lg.size(1), N = (int)lg.size(2);
+  TORCH_CHECK(N >= 2 && N <= 64, "C51 atoms must be in [2, 64] (one wave per sample)");
+  TORCH_CHECK(lgn_t.sizes() == lg.sizes() && dlg.sizes() == lg.sizes(), "logit shapes");
+  TORCH_CHECK(act.numel() == B && rew.numel() == B && done.numel() == B && gam.numel() == B && prio.numel() == B);
+  const float* lo = nullptr;
+  if (lgn_o.has_value()) { CHECK_T((*lgn_o), torch::kFloat32); TORCH_CHECK(lgn_o->sizes() == lg.sizes()); lo = ptr<float>(*lgn_o); }
+  const float* w = nullptr;
+  if (wts.has_value()) { CHECK_T((*wts), torch::kFloat32); TORCH_CHECK(wts->numel() == B); w = ptr<float>(*wts); }
+  c10::hip::HIPGuard g(lg.device());
+  launch_td_loss_c51(ptr<float>(lg), ptr<float>(lgn_t), lo, ptr<int32_t>(act), ptr<float>(rew), ptr<float>(done),
+                     ptr<float>(gam), w, ptr<float>(loss), ptr<float>(dlg), ptr<float>(prio), B, A, N, (float)vmin,
+                     (float)vmax, cur_stream());
+}
+
+void preprocess_batch(torch::Tensor in, torch::Tensor out) {
+  CHECK_T(in, torch::kUInt8); CHECK_T(out, torch::kUInt8);
+  TORCH_CHECK(in.dim() == 4 && in.size(3) == 3 && out.dim() == 3 && out.size(0) == in.size(0), "shapes");
+  c10::hip::HIPGuard g(in.device());
+  launch_preprocess_batch(ptr<uint8_t>(in), ptr<uint8_t>(out), (int)in.size(0), (int)in.size(1), (int)in.size(2),
+                          (int)out.size(1), (int)out.size(2), cur_stream());
+}
+
+void preprocess_host(torch::Tensor in, torch::Tensor out) {
+  TORCH_CHECK(!in.is_cuda() && in.scalar_type() == torch::kUInt8 && in.is_contiguous() && in.dim() == 3 &&
+              in.size(2) == 3, "host RGB uint8 [H, W, 3]");
+  TORCH_CHECK(!out.is_cuda() && out.scalar_type() == torch::kUInt8 && out.is_contiguous() && out.dim() == 2);
+  dqn_preprocess_host(ptr<uint8_t>(in), (int)in.size(0), (int)in.size(1), ptr<uint8_t>(out), (int)out.size(0),
+                      (int)out.size(1));
+}
+
+void actor_step(torch::Tensor q, torch::Tensor frames, torch::Tensor stacks, torch::Tensor cursor,
+                torch::Tensor size_dev, torch::Tensor state_idx, torch::Tensor next_idx, torch::Tensor actions,
+                torch::Tensor rewards, torch::Tensor dones, torch::Tensor gammas, torch::Tensor eps, torch::Tensor rng,
+                torch::Tensor ticket, torch::Tensor frames_done, double gamma, double p_done) {
+  CHECK_T(q, torch::kFloat32); CHECK_T(frames, torch::kUInt8); CHECK_T(stacks, torch::kInt32);
+  CHECK_T(cursor, torch::kInt64); CHECK_T(size_dev, torch::kInt32); CHECK_T(state_idx, torch::kInt32);
+  CHECK_T(next_idx, torch::kInt32); CHECK_T(actions, torch::kInt32); CHECK_T(rewards, torch::kFloat32);
+  CHECK_T(dones, torch::kFloat32); CHECK_T(gammas, torch::kFloat32); CHECK_T(eps, torch::kFloat32);
+  CHECK_T(rng, torch::kInt64); CHECK_T(ticket, torch::kInt32); CHECK_T(frames_done, torch::kInt64);
+  const int E = (int)q.size(0), A = (int)q.size(1), K = (int)stacks.size(1);
+  const int F = (int)frames.size(0), HW = (int)(frames.size(1) * frames.size(2)), C = (int)state_idx.size(0);
+  TORCH_CHECK(stacks.size(0) == E && state_idx.size(1) == K, "stack shapes");
+  TORCH_CHECK(cursor.numel() == 3 && eps.numel() == 3 && rng.numel() == 2, "state vectors");
+  TORCH_CHECK(F >= 2 * C + K, "frame ring must hold 2C + k frames");
+  TORCH_CHECK(E >= 1 && E <= C, "env count");
+  c10::hip::HIPGuard g(q.device());
+  launch_actor_step(ptr<float>(q), ptr<uint8_t>(frames), ptr<int32_t>(stacks), ptr<int64_t>(cursor),
+                    ptr<int32_t>(size_dev), ptr<int32_t>(state_idx), ptr<int32_t>(next_idx), ptr<int32_t>(actions),
+                    ptr<float>(rewards), ptr<float>(dones), ptr<float>(gammas), ptr<float>(eps), ptr<int64_t>(rng),
+                    ptr<int32_t>(ticket), ptr<int64_t>(frames_done), E, A, K, HW, C, F, (float)gamma, (float)p_done,
+                    cur_stream());
+}
+
+void stack_states(torch::Tensor frames, torch::Tensor stacks, torch::Tensor out) {
+  CHECK_T(frames, torch::kUInt8); CHECK_T(stacks, torch::kInt32); CHECK_T(out, torch::kUInt8);
+  const int E = (int)stacks.size(0), K = (int)stacks.size(1), HW = (int)(frames.size(1) * frames.size(2));
+  TORCH_CHECK(out.numel() == (int64_t)E * HW * K, "out must be [E, H, W, K]");
+  c10::hip::HIPGuard g(frames.device());
+  launch_stack_states(ptr<uint8_t>(frames), ptr<int32_t>(stacks), ptr<uint8_t>(out), E, HW, K, cur_stream());
+}
+
+uint32_t crc32c(py::bytes data) {
+  std::string s = data;
+  return dqn_crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+}
+
+void ring_init(torch::Tensor buf, int64_t cap, int64_t rec) {
+  TORCH_CHECK(!buf.is_cuda() && buf.numel() >= (int64_t)dqn_ring_bytes(cap, rec), "ring buffer too small");
+  dqn_ring_init(ptr<uint8_t>(buf), cap, rec);
+}
+int64_t ring_push(torch::Tensor buf, torch::Tensor recs, int64_t n) {
+  return dqn_ring_push(ptr<uint8_t>(buf), ptr<uint8_t>(recs), n);
+}
+int64_t ring_pop(torch::Tensor buf, torch::Tensor out, int64_t max_n) {
+  return dqn_ring_pop(ptr<uint8_t>(buf), ptr<uint8_t>(out), max_n);
+}
+int64_t ring_size(torch::Tensor buf) { return dqn_ring_size(ptr<uint8_t>(buf)); }
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "dist_dqn_amd native extension (gfx950 HIP kernels + C++ host runtime)";
+  m.def("replay_sample_uniform", &replay_sample_uniform);
+  m.def("replay_gather_frames", &replay_gather_frames);
+  m.def("sumtree_set", &sumtree_set);
+  m.def("sumtree_sample", &sumtree_sample);
+  m.def("optimizer_step", &optimizer_step);
+  m.def("target_update", &target_update);
+  m.def("td_loss_scalar", &td_loss_scalar);
+  m.def("td_loss_c51", &td_loss_c51);
+  m.def("preprocess_batch", &preprocess_batch);
+  m.def("preprocess_host", &preprocess_host);
+  m.def("actor_step", &actor_step);
+  m.def("stack_states", &stack_states);
+  m.def("crc32c", &crc32c);
+  m.def("ring_bytes", [](int64_t cap, int64_t rec) { return (int64_t)dqn_ring_bytes(cap, rec); });
+  m.def("ring_init", &ring_init);
+  m.def("ring_push", &ring_push);
+  m.def("ring_pop", &ring_pop);
+  m.def("ring_size", &ring_size);
+  register_net_ops(m);
+}

@@ -1,0 +1,34 @@
+// Launchers for the gfx950 HIP kernels (raw pointers + stream; no torch types,
+// so the .hip translation units compile without the torch headers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, hipStream_t st);
+void launch_replay_gather_frames(const uint8_t* frames, const int32_t* state_idx, const int32_t* next_idx,
+                                 const int32_t* idx, uint8_t* s, uint8_t* ns, int B, int HW, int K,
+                                 hipStream_t st);
+void launch_sumtree_set(float* sum, float* mn, float* maxp, const int32_t* idx, const float* td, float alpha,
+                        float eps, int use_max, int n, int P, hipStream_t st);
+void launch_sumtree_sample(const float* sum, const float* mn, int64_t* rng, const int32_t* size,
+                           const float* beta, int32_t* idx_out, float* w_out, int B, int P, hipStream_t st);
+void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
+                           int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
+                           float grad_scale, int n, hipStream_t st);
+void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
+                          hipStream_t st);
+void launch_step_bump(int64_t* step, hipStream_t st);
+void launch_td_loss_scalar(const float* q, const float* qn_t, const float* qn_o, const int32_t* act,
+                           const float* rew, const float* done, const float* gam, const float* wts,
+                           float* loss, float* dq, float* prio, int B, int A, int huber, float delta,
+                           hipStream_t st);
+void launch_td_loss_c51(const float* lg, const float* lgn_t, const float* lgn_o, const int32_t* act,
+                        const float* rew, const float* done, const float* gam, const float* wts, float* loss,
+                        float* dlg, float* prio, int B, int A, int N, float vmin, float vmax, hipStream_t st);
+void launch_preprocess_batch(const uint8_t* in, uint8_t* out, int N, int Hs, int Ws, int H, int W, hipStream_t st);
+void launch_actor_step(const float* q, uint8_t* frames, int32_t* stacks, int64_t* cursor, int32_t* size_dev,
+                       int32_t* state_idx, int32_t* next_idx, int32_t* actions, float* rewards, float* dones,
+                       float* gammas, float* eps, int64_t* rng, int32_t* ticket, int64_t* frames_done, int E,
+                       int A, int K, int HW, int C, int F, float gamma, float p_done, hipStream_t st);
+void launch_stack_states(const uint8_t* frames, const int32_t* stacks, uint8_t* out, int E, int HW, int K,
+                         hipStream_t st);

@@ -1,0 +1,61 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of dist_dqn_amd.
+// Wave64 everywhere: lane = threadIdx.x & 63, reductions over 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define DQN_DEV __device__ __forceinline__
+
+namespace dqn {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u32x4 { uint32_t x, y, z, w; };
+
+DQN_DEV u32x4 philox(uint64_t key64, uint64_t ctr_hi, uint32_t ctr_lo0, uint32_t ctr_lo1) {
+  uint32_t k0 = (uint32_t)key64, k1 = (uint32_t)(key64 >> 32);
+  uint32_t c0 = ctr_lo0, c1 = ctr_lo1, c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+
+DQN_DEV float u01(uint32_t x) {  // [0, 1)
+  return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
+// ----------------------------------------------------------------- reductions
+DQN_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DQN_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// -------------------------------------------------------------------- bf16
+DQN_DEV uint16_t f2bf(float f) {  // round-to-nearest-even (NaN kept by the cast path)
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+DQN_DEV float bf2f(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+}  // namespace dqn

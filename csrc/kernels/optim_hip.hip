@@ -1,0 +1,164 @@
+#include "hip/hip_runtime.h"
+// Fused multi-tensor optimizer over the flat parameter buffer (TF-0.x exact).
+//
+// Reference: tf.train.{GradientDescent,Momentum,RMSProp,Adam,Adagrad,Adadelta,Ftrl}
+// Optimizer.minimize() colocated with the variables on the parameter server
+// (/root/reference/src/network.py:159-203) — one ApplyX op per variable plus
+// the separate L2 term in the loss (network.py:151-152,311,407).
+//
+// Here: ONE launch for all parameters; float4 vector loads; per element
+//   g = grad * grad_scale (+ reg * w for flat[:reg_end])   -- 1/world DP averaging folded in
+// then the TF update rule. Adam's beta powers (TF non-slot variables) are
+// read by every block and advanced by the LAST block to finish (arrival
+// ticket), together with global_step, so no extra launch is needed.
+#include "common.h"
+#include "../include/dqn_kernels.h"
+
+namespace dqn {
+
+struct OptHP {
+  float lr, reg, grad_scale;
+  float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
+  int reg_end;
+};
+
+template <int OP>
+DQN_DEV void update_one(float& w, float g, float& s0, float& s1, const OptHP& h, float lr_t) {
+  if constexpr (OP == 0) {            // sgd
+    w -= h.lr * g;
+  } else if constexpr (OP == 1) {     // momentum (non-Nesterov)
+    s0 = h.momentum * s0 + g;
+    w -= h.lr * s0;
+  } else if constexpr (OP == 2) {     // rmsprop: ms (init 1), mom
+    s0 = h.rho * s0 + (1.f - h.rho) * g * g;
+    s1 = h.rms_mom * s1 + h.lr * g / sqrtf(s0 + h.rms_eps);
+    w -= s1;
+  } else if constexpr (OP == 3) {     // adam (TF epsilon-hat form)
+    s0 = h.b1 * s0 + (1.f - h.b1) * g;
+    s1 = h.b2 * s1 + (1.f - h.b2) * g * g;
+    w -= lr_t * s0 / (sqrtf(s1) + h.adam_eps);
+  } else if constexpr (OP == 4) {     // adagrad (accumulator init 0.1)
+    s0 += g * g;
+    w -= h.lr * g / sqrtf(s0);
+  } else if constexpr (OP == 5) {     // adadelta
+    s0 = h.ad_rho * s0 + (1.f - h.ad_rho) * g * g;
+    const float upd = sqrtf(s1 + h.ad_eps) / sqrtf(s0 + h.ad_eps) * g;
+    s1 = h.ad_rho * s1 + (1.f - h.ad_rho) * upd * upd;
+    w -= h.lr * upd;
+  } else {                            // ftrl (lr_power -0.5, l1 = l2 = 0)
+    const float na = s0 + g * g;
+    s1 += g - (sqrtf(na) - sqrtf(s0)) / h.lr * w;
+    const float quad = sqrtf(na) / h.lr;
+    w = fabsf(s1) > 0.f ? -s1 / quad : 0.f;
+    s0 = na;
+  }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(256)
+optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __restrict__ s0,
+             float* __restrict__ s1, float* __restrict__ beta_pow, int64_t* __restrict__ step,
+             int32_t* __restrict__ ticket, OptHP h, int n4) {
+  float lr_t = h.lr;
+  if constexpr (OP == 3) {
+    const float b1p = beta_pow[0], b2p = beta_pow[1];
+    lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  }
+  float4* W = reinterpret_cast<float4*>(w);
+  const float4* G = reinterpret_cast<const float4*>(grad);
+  float4* S0 = reinterpret_cast<float4*>(s0);
+  float4* S1 = reinterpret_cast<float4*>(s1);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    float4 wv = W[i], gv = G[i];
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if constexpr (OP != 0) a = S0[i];
+    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6) b = S1[i];
+    const bool reg = (i * 4) < h.reg_end;       // reg_end is a multiple of 64
+    float ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    float aa[4] = {a.x, a.y, a.z, a.w}, bb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float g = gg[j] * h.grad_scale;
+      if (reg) g += h.reg * ww[j];
+      update_one<OP>(ww[j], g, aa[j], bb[j], h, lr_t);
+    }
+    W[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
+    if constexpr (OP != 0) S0[i] = make_float4(aa[0], aa[1], aa[2], aa[3]);
+    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6) S1[i] = make_float4(bb[0], bb[1], bb[2], bb[3]);
+  }
+  // last block advances global_step and (Adam) the beta powers. Every block
+  // read beta_pow above, before its ticket add, so the update cannot race.
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (int)gridDim.x - 1) {
+      if (step) step[0] += 1;
+      if constexpr (OP == 3) {
+        beta_pow[0] *= h.b1;
+        beta_pow[1] *= h.b2;
+      }
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// target <- tau * online + (1 - tau) * target, optionally only when step % freq == 0.
+__global__ void __launch_bounds__(256)
+target_update_kernel(float* __restrict__ dst, const float* __restrict__ src, float tau,
+                     const int64_t* __restrict__ step, int freq, int n4) {
+  if (step != nullptr && (step[0] % freq) != 0) return;
+  float4* D = reinterpret_cast<float4*>(dst);
+  const float4* S = reinterpret_cast<const float4*>(src);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    float4 s = S[i];
+    if (tau >= 1.f) {
+      D[i] = s;
+    } else {
+      float4 d = D[i];
+      const float k = 1.f - tau;
+      D[i] = make_float4(tau * s.x + k * d.x, tau * s.y + k * d.y, tau * s.z + k * d.z, tau * s.w + k * d.w);
+    }
+  }
+}
+
+__global__ void step_bump_kernel(int64_t* step) { step[0] += 1; }
+
+}  // namespace dqn
+
+using namespace dqn;
+
+static int grid_for(int n4) {
+  int g = (n4 + 255) / 256;
+  return g < 1 ? 1 : (g > 2048 ? 2048 : g);
+}
+
+void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
+                           int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
+                           float grad_scale, int n, hipStream_t st) {
+  OptHP h;
+  h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
+  h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
+  h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
+  const int n4 = n / 4;
+  dim3 grid(grid_for(n4)), block(256);
+  switch (op) {
+    case 0: hipLaunchKernelGGL(optim_kernel<0>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 1: hipLaunchKernelGGL(optim_kernel<1>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 2: hipLaunchKernelGGL(optim_kernel<2>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 3: hipLaunchKernelGGL(optim_kernel<3>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 4: hipLaunchKernelGGL(optim_kernel<4>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 5: hipLaunchKernelGGL(optim_kernel<5>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 6: hipLaunchKernelGGL(optim_kernel<6>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    default: break;
+  }
+}
+
+void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
+                          hipStream_t st) {
+  const int n4 = n / 4;
+  hipLaunchKernelGGL(target_update_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dst, src, tau, step,
+                     freq < 1 ? 1 : freq, n4);
+}
+
+void launch_step_bump(int64_t* step, hipStream_t st) {
+  hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(1), 0, st, step);
+}

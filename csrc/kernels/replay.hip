@@ -1,0 +1,116 @@
+// HBM replay kernels: uniform sampling without replacement + frame-stack gather.
+//
+// Reference: python `random.sample(deque, B)` + tuple partition + numpy stack
+// + feed_dict H2D (/root/reference/src/replay_memory.py:31-45,
+// /root/reference/src/dqn_agent.py:113-129,249-253). Here the sample is one
+// workgroup (B <= 1024 lanes, Philox4x32-10, counter advanced on the device so
+// graph replays draw fresh numbers) and the gather rebuilds the uint8 k-frame
+// stacks straight from the frame ring (frames stored once, not per state).
+#include "common.h"
+#include "../include/dqn_kernels.h"
+
+namespace dqn {
+
+__global__ void __launch_bounds__(1024)
+sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ rng,
+                      int32_t* __restrict__ out, int B) {
+  __shared__ int32_t cand[1024];
+  __shared__ int any_dup;
+  const int i = threadIdx.x;
+  const uint32_t n = (uint32_t)max(size_p[0], 1);
+  const uint64_t seed = (uint64_t)rng[0];
+  const uint64_t ctr = (uint64_t)rng[1];
+  uint32_t attempt = 0;
+  auto draw = [&]() -> int32_t {
+    u32x4 r = philox(seed, ctr, (uint32_t)i, attempt++);
+    return (int32_t)(((uint64_t)r.x * n) >> 32);
+  };
+  int32_t v = (i < B) ? draw() : -1;
+  const bool distinct_possible = n >= (uint32_t)B;
+  for (int round = 0; round < 64; ++round) {
+    if (i < 1024) cand[i] = v;
+    if (i == 0) any_dup = 0;
+    __syncthreads();
+    bool dup = false;
+    if (i < B && distinct_possible) {
+      for (int j = 0; j < i; ++j) dup |= (cand[j] == v);
+    }
+    if (dup) any_dup = 1;
+    __syncthreads();
+    if (!any_dup) break;
+    if (dup) v = draw();
+    __syncthreads();
+  }
+  if (i < B) out[i] = v;
+  if (i == 0) rng[1] = (int64_t)(ctr + 1);
+}
+
+// frames: [F, H, W] u8; state_idx: [C, k] i32; next_idx: [C] i32; idx: [B]
+// outputs s, ns: [B, H, W, k] u8 (NHWC, channel = frame in the stack).
+template <int K>
+__global__ void gather_frames_kernel(const uint8_t* __restrict__ frames, const int32_t* __restrict__ state_idx,
+                                     const int32_t* __restrict__ next_idx, const int32_t* __restrict__ idx,
+                                     uint8_t* __restrict__ s, uint8_t* __restrict__ ns, int B, int HW) {
+  // one thread = 4 consecutive pixels of one sample, both stacks
+  const int groups = HW / 4;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * groups) return;
+  const int b = t / groups, g = t - b * groups;
+  const int tr = idx[b];
+  int slots[K + 1];
+#pragma unroll
+  for (int c = 0; c < K; ++c) slots[c] = state_idx[(int64_t)tr * K + c];
+  slots[K] = next_idx[tr];
+  uint32_t px[K + 1];
+#pragma unroll
+  for (int c = 0; c <= K; ++c)
+    px[c] = *reinterpret_cast<const uint32_t*>(frames + (int64_t)slots[c] * HW + g * 4);
+  // transpose (K+1) frames x 4 pixels -> per pixel K channels
+  uint8_t* ds = s + ((int64_t)b * HW + g * 4) * K;
+  uint8_t* dn = ns + ((int64_t)b * HW + g * 4) * K;
+  if constexpr (K == 4) {
+    uint32_t ws[4], wn[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      ws[p] = wn[p] = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        ws[p] |= ((px[c] >> (8 * p)) & 0xffu) << (8 * c);
+        wn[p] |= ((px[c + 1] >> (8 * p)) & 0xffu) << (8 * c);
+      }
+    }
+    *reinterpret_cast<uint4*>(ds) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+    *reinterpret_cast<uint4*>(dn) = make_uint4(wn[0], wn[1], wn[2], wn[3]);
+  } else {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        ds[p * K + c] = (uint8_t)(px[c] >> (8 * p));
+        dn[p * K + c] = (uint8_t)(px[c + 1] >> (8 * p));
+      }
+    }
+  }
+}
+
+}  // namespace dqn
+
+using namespace dqn;
+
+void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, hipStream_t st) {
+  hipLaunchKernelGGL(sample_uniform_kernel, dim3(1), dim3(1024), 0, st, size, rng, out, B);
+}
+
+void launch_replay_gather_frames(const uint8_t* frames, const int32_t* state_idx, const int32_t* next_idx,
+                                 const int32_t* idx, uint8_t* s, uint8_t* ns, int B, int HW, int K,
+                                 hipStream_t st) {
+  const int total = B * (HW / 4);
+  dim3 grid((total + 255) / 256), block(256);
+  switch (K) {
+    case 1: hipLaunchKernelGGL(gather_frames_kernel<1>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
+    case 2: hipLaunchKernelGGL(gather_frames_kernel<2>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
+    case 3: hipLaunchKernelGGL(gather_frames_kernel<3>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
+    case 4: hipLaunchKernelGGL(gather_frames_kernel<4>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
+    default: break;  // host checks K in [1, 4]
+  }
+}

@@ -1,0 +1,129 @@
+"""Checkpoint / resume with the reference's layout.
+
+The reference relies on ``tf.train.Supervisor`` (`/root/reference/src/main.py:136-143`):
+every 600 s the chief saves all global variables to
+``<logdir>/model.ckpt-<global_step>`` plus a ``checkpoint`` index file, and
+``managed_session`` restores the latest one on start.
+
+Kept here:
+  * file names: ``<logdir>/checkpoint`` (text index in TF's
+    ``model_checkpoint_path: "..."`` format) and ``model.ckpt-<step>``;
+  * tensor names and layouts: TF variable names (``conv1/w`` ...), conv HWIO,
+    dense [in, out], NHWC flatten order, optimizer slots with TF slot names
+    (``conv1/w/RMSProp`` ...), ``global_step``; ``target/*`` only with
+    ``--disable_target_replication``.
+Storage is safetensors (no pickle; loads execute nothing). Not saved, as in
+the reference: replay, epsilon, local training_steps, stats; the agent
+re-syncs the target after restore. ``--save_agent_state`` adds an opt-in
+JSON sidecar with epsilon and training_steps.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import re
+import threading
+import time
+from typing import Dict, Optional
+
+import torch
+from safetensors.torch import load_file, save_file
+
+_INDEX = 'checkpoint'
+_PREFIX = 'model.ckpt'
+
+
+def _ckpt_path(logdir: str, step: int) -> str:
+    return os.path.join(logdir, '%s-%d' % (_PREFIX, step))
+
+
+def latest_checkpoint(logdir: str) -> Optional[str]:
+    idx = os.path.join(logdir, _INDEX)
+    if os.path.exists(idx):
+        with open(idx) as f:
+            for line in f:
+                m = re.match(r'model_checkpoint_path:\s*"(.*)"', line.strip())
+                if m:
+                    p = m.group(1)
+                    p = p if os.path.isabs(p) else os.path.join(logdir, p)
+                    if os.path.exists(p):
+                        return p
+    files = sorted(glob.glob(os.path.join(logdir, _PREFIX + '-*')),
+                   key=lambda p: int(re.findall(r'-(\d+)$', p)[0]) if re.findall(r'-(\d+)$', p) else -1)
+    files = [f for f in files if re.search(r'-\d+$', f)]
+    return files[-1] if files else None
+
+
+def save(logdir: str, tensors: Dict[str, torch.Tensor], step: int, max_to_keep: int = 5,
+         sidecar: Optional[dict] = None) -> str:
+    os.makedirs(logdir, exist_ok=True)
+    path = _ckpt_path(logdir, step)
+    tmp = path + '.tmp'
+    save_file({k: v.detach().cpu().contiguous() for k, v in tensors.items()}, tmp,
+              metadata={'format': 'dist_dqn_amd/tf-layout-v1', 'global_step': str(step)})
+    os.replace(tmp, path)
+    if sidecar is not None:
+        with open(path + '.agent.json', 'w') as f:
+            json.dump(sidecar, f)
+    kept = sorted(glob.glob(os.path.join(logdir, _PREFIX + '-*')))
+    kept = [k for k in kept if re.search(r'-\d+$', k)]
+    kept.sort(key=lambda p: int(re.findall(r'-(\d+)$', p)[0]))
+    for old in kept[:-max_to_keep] if max_to_keep > 0 else []:
+        for f in (old, old + '.agent.json'):
+            if os.path.exists(f):
+                os.remove(f)
+    kept = kept[-max_to_keep:] if max_to_keep > 0 else kept
+    with open(os.path.join(logdir, _INDEX + '.tmp'), 'w') as f:
+        f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
+        for k in kept:
+            f.write('all_model_checkpoint_paths: "%s"\n' % os.path.basename(k))
+    os.replace(os.path.join(logdir, _INDEX + '.tmp'), os.path.join(logdir, _INDEX))
+    return path
+
+
+def load(path: str) -> Dict[str, torch.Tensor]:
+    return load_file(path)
+
+
+def load_sidecar(path: str) -> Optional[dict]:
+    p = path + '.agent.json'
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+class CheckpointManager:
+    """Chief-only periodic saver (TF Supervisor's ``save_model_secs`` = 600 by default)."""
+
+    def __init__(self, logdir: str, network, is_chief: bool = True, save_secs: int = 600,
+                 max_to_keep: int = 5, agent_state_fn=None):
+        self.logdir = logdir
+        self.network = network
+        self.is_chief = is_chief
+        self.save_secs = save_secs
+        self.max_to_keep = max_to_keep
+        self.agent_state_fn = agent_state_fn
+        self._last = time.time()
+        self._lock = threading.Lock()
+
+    def restore(self) -> Optional[str]:
+        path = latest_checkpoint(self.logdir)
+        if path is None:
+            return None
+        self.network.load_state_dict(load(path))
+        return path
+
+    def maybe_save(self, force: bool = False) -> Optional[str]:
+        if not self.is_chief:
+            return None
+        now = time.time()
+        if not force and (self.save_secs <= 0 or now - self._last < self.save_secs):
+            return None
+        with self._lock:
+            self._last = now
+            sd = self.network.state_dict()
+            step = int(sd['global_step'])
+            side = self.agent_state_fn() if self.agent_state_fn else None
+            return save(self.logdir, sd, step, self.max_to_keep, side)

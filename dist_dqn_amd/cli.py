@@ -1,0 +1,82 @@
+"""Command line entry (reference `src/main.py`): ``python -m dist_dqn_amd <flags>``.
+
+Accepts every reference flag (see `config.py`). Launch modes:
+  * single process: ``python -m dist_dqn_amd --env=CartPole-v0 ...``;
+  * data parallel: ``torchrun --nproc-per-node N -m dist_dqn_amd ...`` (RCCL),
+    or reference-style ``--worker_hosts=h:p,h:p --task_id=i`` per process;
+  * ``--job=ps`` exits immediately (no parameter-server process is needed).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import sys
+from typing import Optional, Sequence
+
+import torch
+
+from .config import Config, parse_args
+
+log = logging.getLogger('dist_dqn_amd')
+
+
+def run_worker(config: Config):
+    """Reference `run_worker` (`src/main.py:100-167`) for one learner rank."""
+    from . import envs
+    from .agent import DQNAgent
+    from .learner import Learner
+    from .models.network import Network
+    from .parallel import broadcast_flat, init_distributed
+    from .replay import DeviceReplay, ReplayMemory
+    from .supervisor import RunSupervisor
+    from .utils.metrics import EpisodeMonitor, JsonlWriter
+
+    ctx = init_distributed(config)
+    seed = config.seed if config.seed is not None else 1234
+    torch.manual_seed(seed + ctx.rank)
+    env = envs.make(config.env, seed=seed + 1000 * ctx.rank)
+    input_shape = DQNAgent.get_input_shape(env, config)
+    network = Network.create_network(config.replace(seed=seed), input_shape, env.action_space.n,
+                                     num_replicas=ctx.world_size, device=ctx.device)
+    log.info('rank %d/%d device=%s executor=%s params=%d', ctx.rank, ctx.world_size, ctx.device,
+             network.executor.name, network.arch.num_params())
+
+    sv = RunSupervisor(is_chief=ctx.is_chief, logdir=config.logdir, network=network, rank=ctx.rank,
+                       world_size=ctx.world_size, save_secs=config.checkpoint_secs,
+                       max_to_keep=config.max_to_keep)
+    sv.prepare(broadcast_fn=lambda: broadcast_flat(ctx, network.online.flat))
+
+    use_device_replay = ctx.device.type == 'cuda' or ctx.enabled
+    if use_device_replay:
+        frames = config.resize_width > 0 and config.resize_height > 0
+        obs_shape = (config.resize_height, config.resize_width) if frames else tuple(env.observation_space.shape)
+        replay = DeviceReplay(config.replay_memory_capacity, obs_shape, config.frames_per_state if frames else 1,
+                              device=ctx.device, prioritized=config.prioritized_replay,
+                              alpha=config.per_alpha, seed=seed + ctx.rank)
+        session = Learner(network, replay, config, ctx)
+    else:
+        replay = ReplayMemory(config.replay_memory_capacity)
+        session = None
+    monitor = EpisodeMonitor(config.monitor_path, ctx.rank) if config.monitor else None
+    metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))
+    with sv.managed():
+        agent = DQNAgent(env, network, session, replay, config, enable_summary=ctx.is_chief,
+                         metrics=metrics, monitor=monitor)
+        sv.ckpt.agent_state_fn = agent.agent_state if config.save_agent_state else None
+        agent.train(config.num_episodes, config.max_steps_per_episode, sv)
+    return agent
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    config = parse_args(argv)
+    logging.basicConfig(level=getattr(logging, config.log_level.upper(), logging.INFO),
+                        format='%(asctime)s %(levelname)s %(name)s: %(message)s')
+    if config.job == 'ps':
+        log.warning('--job=ps: no parameter server is needed (synchronous RCCL data parallelism); exiting.')
+        return 0
+    run_worker(config)
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

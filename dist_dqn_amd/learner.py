@@ -1,0 +1,136 @@
+"""Device-resident learner step (reference `DQNAgent._train_minibatch`,
+`/root/reference/src/dqn_agent.py:108-143`).
+
+Reference per step: python `random.sample` over a deque, host partition,
+`session.run(target_q_output)` (H2D of next states, D2H of Q), host max,
+python loop building y / one-hot, `session.run(train_op)` (H2D 3.6 MB feed),
+optional summary, optional target assign — two host round trips per step.
+
+Here one step is, entirely on the GPU and with no host synchronisation:
+  sample (uniform w/o replacement, or PER sum-tree)  ->  gather uint8 stacks
+  -> online fwd(s) + target fwd(s') [+ online fwd(s') for Double DQN]
+  -> fused TD loss (+dQ)  ->  backward into the flat grad buffer
+  -> [RCCL all-reduce of the flat grad]  ->  fused optimizer (+global_step++)
+  -> [PER priority update]  ->  target copy/Polyak behind a device predicate.
+On the GPU the sequence is captured once into a HIP graph (via
+``torch.cuda.CUDAGraph``, which is hipGraph on ROCm) and replayed, so the
+per-step host cost is one graph launch. With world > 1 the collective sits
+between two captured graphs (pre: sample..backward, post: optimizer..target).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, Optional
+
+import torch
+
+from .models.network import Network
+from .ops import kernels
+from .parallel.dist import DistContext
+from .parallel.dp import GradAllReducer
+
+log = logging.getLogger(__name__)
+
+
+class Learner:
+    def __init__(self, network: Network, replay, config, ctx: Optional[DistContext] = None,
+                 use_graph: Optional[bool] = None):
+        self.net = network
+        self.replay = replay
+        self.config = config
+        self.ctx = ctx or DistContext(device=network.device)
+        self.device = network.device
+        B = config.minibatch_size
+        self.B = B
+        self.idx = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.weights = torch.ones(B, dtype=torch.float32, device=self.device)
+        self.prio = torch.zeros(B, dtype=torch.float32, device=self.device)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb, config.allreduce)
+        self.tau = min(1.0, float(config.target_update_tau))
+        self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
+        if use_graph is None:
+            use_graph = bool(config.hip_graph) and self.device.type == 'cuda'
+        self.use_graph = use_graph
+        self._graphs = None
+        self._warm = 0
+        self._noise_gen = None
+
+    # ------------------------------------------------------------ step body
+    def _sample_and_grad(self):
+        r = self.replay
+        if getattr(r, 'prioritized', False):
+            beta = torch.clamp(self.config.per_beta0 + (1.0 - self.config.per_beta0)
+                               * self.net.global_step.float() / max(1, self.config.per_beta_steps),
+                               max=1.0)
+            r.sample_prioritized(self.B, beta, self.idx, self.weights)
+        else:
+            r.sample_indices(self.B, self.idx)
+        batch = r.gather(self.idx)
+        if getattr(r, 'prioritized', False):
+            batch['weights'] = self.weights
+        self.net.reset_noise()
+        loss, prio = self.net.compute_grads(batch)
+        self.loss.copy_(loss.view(1))
+        self.prio.copy_(prio.view(-1))
+
+    def _apply(self):
+        cfg = self.config
+        self.net.apply_grads(self.reducer.scale)
+        if getattr(self.replay, 'prioritized', False):
+            self.replay.update_priorities(self.idx, self.prio, cfg.per_eps)
+        if self.tau < 1.0:
+            kernels.target_update(self.net.target.flat, self.net.online.flat, self.tau)
+        else:
+            # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).
+            # Under sync DP every rank's online params are bit-identical, so the local
+            # copy equals the reference's PS-owned target (--disable_target_replication).
+            kernels.target_update(self.net.target.flat, self.net.online.flat, 1.0,
+                                  self.net.global_step, cfg.target_update_freq)
+
+    def _eager_step(self):
+        self._sample_and_grad()
+        self.reducer.allreduce()
+        self._apply()
+
+    # ------------------------------------------------------------ graph
+    def _capture(self):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g_pre, g_post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            if self.ctx.enabled:
+                with torch.cuda.graph(g_pre, stream=s):
+                    self._sample_and_grad()
+                with torch.cuda.graph(g_post, stream=s):
+                    self._apply()
+                self._graphs = (g_pre, g_post)
+            else:
+                with torch.cuda.graph(g_pre, stream=s):
+                    self._sample_and_grad()
+                    self._apply()
+                self._graphs = (g_pre,)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+
+    # ------------------------------------------------------------- public
+    def step(self) -> torch.Tensor:
+        """One SGD step. Returns the (device) TD-loss tensor; no host sync."""
+        if not self.use_graph or (self._graphs is None and self._warm < 2):
+            # eager path; on the GPU the first two steps also warm up the
+            # allocator, kernels and RCCL communicators before capture
+            self._eager_step()
+            self._warm += 1
+        else:
+            if self._graphs is None:
+                torch.cuda.synchronize(self.device)
+                self._capture()      # records only; the replay below runs the step
+            self._graphs[0].replay()
+            if len(self._graphs) > 1:
+                self.reducer.allreduce()
+                self._graphs[1].replay()
+        self.train_steps += 1
+        return self.loss
+
+    def update_target_now(self):
+        """Unconditional target sync (reference `_update_target_network` at init, `dqn_agent.py:50`)."""
+        kernels.target_update(self.net.target.flat, self.net.online.flat, 1.0)

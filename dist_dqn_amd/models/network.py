@@ -1,0 +1,145 @@
+"""`Network`: the model/graph-builder layer (reference C4/C5/C8,
+`/root/reference/src/network.py:13-254`).
+
+The reference builds a TF graph and hands the agent graph handles
+(`q_output`, `target_q_output`, `train_op`, `target_update_ops`,
+`global_step`). Here those handles are methods over device-resident flat
+buffers:
+
+  reference handle            -> here
+  q_output                    -> q_values(x)
+  target_q_output             -> target_q_values(x)
+  train_op (+global_step++)   -> train_step(batch)  (= compute_grads + apply_grads)
+  target_update_ops           -> update_target()    (one D2D copy / Polyak kernel)
+  global_step                 -> global_step (device int64, advanced by the optimizer)
+
+Target parameters are always replicated per rank (reference default,
+`network.py:216-225`); `--disable_target_replication` makes rank 0 the owner
+and broadcasts it at update time (`parallel/dp.py`).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from .. import optim
+from ..ops import kernels
+from . import torch_net
+from .arch import ArchSpec, arch_from_config
+from .executor import TorchExecutor
+from .params import ParamStore
+
+
+def resolve_device(config) -> torch.device:
+    dev = getattr(config, 'device', 'auto')
+    if dev == 'auto':
+        dev = 'cuda' if torch.cuda.is_available() else 'cpu'
+    if dev == 'cuda':
+        return torch.device('cuda', torch.cuda.current_device())
+    return torch.device(dev)
+
+
+def make_executor(arch: ArchSpec, layout, config, device: torch.device):
+    backend = getattr(config, 'backend', 'auto')
+    kw = dict(input_scale=config.input_scale, loss=config.loss, huber_delta=config.huber_delta,
+              double_dqn=config.double_dqn)
+    if device.type == 'cuda' and backend in ('auto', 'hip'):
+        from ..ops.executor import HipExecutor, supports
+        if supports(arch):
+            return HipExecutor(arch, layout, dtype=config.dtype, **kw)
+        if backend == 'hip':
+            raise RuntimeError('HIP executor does not support %s' % (arch,))
+    return TorchExecutor(arch, layout, **kw)
+
+
+class Network:
+    def __init__(self, arch: ArchSpec, config, device=None, num_replicas: int = 1,
+                 ps_device=None, worker_device=None):
+        self.arch = arch
+        self.config = config
+        self.device = torch.device(device) if device is not None else resolve_device(config)
+        self.num_replicas = num_replicas
+        self.ps_device, self.worker_device = ps_device, worker_device
+        self.online = ParamStore(arch, self.device).init_(config.seed)
+        self.target = ParamStore(arch, self.device)
+        self.target.copy_from(self.online)
+        self.layout = self.online.layout
+        self.grad = torch.zeros_like(self.online.flat)
+        self.optimizer = optim.make_optimizer(config, self.layout, self.device)
+        self.global_step = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.executor = make_executor(arch, self.layout, config, self.device)
+        nz = torch_net.noise_size(arch)
+        self.noise = torch.zeros(nz, device=self.device) if nz else None
+        self.noise_target = torch.zeros(nz, device=self.device) if nz else None
+        self.last_loss = torch.zeros(1, device=self.device)
+
+    # -------------------------------------------------------------- factory
+    @staticmethod
+    def create_network(config, input_shape, num_actions, num_replicas=1, ps_device=None,
+                       worker_device=None, device=None) -> 'Network':
+        """Reference factory signature (`network.py:35-57`)."""
+        arch = arch_from_config(config, input_shape, num_actions)
+        return Network(arch, config, device=device, num_replicas=num_replicas,
+                       ps_device=ps_device, worker_device=worker_device)
+
+    # ------------------------------------------------------------ inference
+    def _to_dev(self, x):
+        if not torch.is_tensor(x):
+            import numpy as np
+            x = torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+        return x.to(self.device, non_blocking=True)
+
+    def q_values(self, x) -> torch.Tensor:
+        return self.executor.q_values(self.online.flat, self._to_dev(x), self.noise)
+
+    def target_q_values(self, x) -> torch.Tensor:
+        return self.executor.q_values(self.target.flat, self._to_dev(x), self.noise_target)
+
+    def reset_noise(self, generator=None):
+        if self.noise is not None:
+            self.noise.normal_(generator=generator)
+            self.noise_target.normal_(generator=generator)
+
+    # ------------------------------------------------------------- training
+    def compute_grads(self, batch: Dict[str, torch.Tensor]):
+        loss, prio = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
+                                                 self.noise, self.noise_target)
+        self.last_loss = loss
+        return loss, prio
+
+    def apply_grads(self, grad_scale: float = 1.0):
+        # global_step += 1 happens inside the (fused) optimizer step
+        self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step)
+
+    def train_step(self, batch: Dict[str, torch.Tensor], grad_scale: float = 1.0):
+        loss, prio = self.compute_grads(batch)
+        self.apply_grads(grad_scale)
+        return loss, prio
+
+    def update_target(self, tau: Optional[float] = None):
+        tau = self.config.target_update_tau if tau is None else tau
+        kernels.target_update(self.target.flat, self.online.flat, min(1.0, tau))
+
+    def total_loss(self) -> float:
+        """Reference `loss` summary value: TD loss + reg_param * sum 0.5||w||^2."""
+        reg = torch_net.reg_loss(self.layout, self.online.flat)
+        return float(self.last_loss) + self.config.reg_param * float(reg)
+
+    # ----------------------------------------------------------- checkpoint
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        sd = dict(self.online.state_dict())
+        sd.update(self.optimizer.state_dict())
+        sd['global_step'] = self.global_step.cpu().view(()).clone()
+        if self.config.disable_target_replication:
+            sd.update({'target/' + k: v for k, v in self.target.state_dict().items()})
+        return sd
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]):
+        self.online.load_state_dict(sd)
+        self.optimizer.load_state_dict(sd)
+        if 'global_step' in sd:
+            self.global_step.fill_(int(sd['global_step']))
+        tsd = {k[len('target/'):]: v for k, v in sd.items() if k.startswith('target/')}
+        if tsd:
+            self.target.load_state_dict(tsd)

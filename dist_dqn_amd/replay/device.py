@@ -1,0 +1,279 @@
+"""HBM-resident experience replay.
+
+The reference stores every transition as a Python tuple holding the full
+stacked state AND the full stacked next state (`/root/reference/src/replay_memory.py:22-23`,
+`/root/reference/src/dqn_agent.py:99`): 2 x 84x84x4 bytes per transition, 56 GB
+at the Atari capacity of 1M, re-fed to the GPU through ``feed_dict`` every
+step (3.6 MB of f32 per minibatch).
+
+Here the replay is a set of device tensors:
+  * ``frames``    uint8 [F, H, W]   — each observation frame stored ONCE;
+  * ``state_idx`` int32 [C, k]      — frame slots forming the state stack
+    (episode-start frames duplicated exactly like the reference FrameBuffer);
+  * ``next_idx``  int32 [C]         — slot of the newest frame of s'
+    (s' = state_idx[1:] + [next_idx]);
+  * ``actions`` int32, ``rewards`` f32, ``dones`` f32, ``gammas`` f32 [C]
+    (gammas = gamma^n of the stored n-step transition).
+Vector observations (CartPole) are stored directly as f32 [C, D] twice.
+
+Frame ring size F = 2C + k + 8: every transition writes one frame and at most
+one reset frame, so a valid transition's frames are never overwritten.
+1M transitions = 14 GB of frames — 5% of one MI355X's 288 GB HBM — so the
+default capacity per GPU can be far larger than the reference's.
+
+Writes are staged in pinned host memory and flushed as contiguous H2D copies
+on a side stream; sampling (uniform without replacement, or prioritized
+through the device sum-tree) and the gather that rebuilds the uint8 stacks
+run as HIP kernels inside the captured learner step (no host sync).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..ops import kernels
+
+
+class DeviceReplay:
+    def __init__(self, capacity: int, obs_shape: Sequence[int], frames_per_state: int = 1,
+                 device='cpu', num_actors: int = 1, prioritized: bool = False,
+                 alpha: float = 0.6, stage_size: int = 1024, seed: int = 0):
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.k = int(frames_per_state)
+        self.obs_shape = tuple(int(s) for s in obs_shape)
+        self.frame_mode = len(self.obs_shape) == 2
+        C = self.capacity
+        dev = self.device
+        if self.frame_mode:
+            H, W = self.obs_shape
+            self.num_frames = 2 * C + self.k + 8
+            self.frames = torch.zeros(self.num_frames, H, W, dtype=torch.uint8, device=dev)
+            self.state_idx = torch.zeros(C, self.k, dtype=torch.int32, device=dev)
+            self.next_idx = torch.zeros(C, dtype=torch.int32, device=dev)
+        else:
+            D = int(np.prod(self.obs_shape))
+            self.obs = torch.zeros(C, D, dtype=torch.float32, device=dev)
+            self.next_obs = torch.zeros(C, D, dtype=torch.float32, device=dev)
+        self.actions = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.rewards = torch.zeros(C, dtype=torch.float32, device=dev)
+        self.dones = torch.zeros(C, dtype=torch.float32, device=dev)
+        self.gammas = torch.ones(C, dtype=torch.float32, device=dev)
+        # size lives on the device so graph-captured sampling reads the live value
+        self.size_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        # RNG state for in-kernel Philox sampling: [seed, counter]
+        self.rng_state = torch.tensor([seed & 0x7fffffff, 0], dtype=torch.int64, device=dev)
+        self._size = 0
+        self._t_next = 0          # next transition slot
+        self._f_next = 0          # next frame slot
+        self.num_actors = num_actors
+        self._stacks: List[Optional[List[int]]] = [None] * num_actors
+        self._last_obs: List[Optional[np.ndarray]] = [None] * num_actors
+        self.prioritized = prioritized
+        self.alpha = alpha
+        if prioritized:
+            from .sumtree import DeviceSumTree
+            self.tree = DeviceSumTree(C, dev)
+        self._pin = self.device.type == 'cuda'
+        self._stage_size = stage_size
+        self._reset_stage()
+        self._copy_stream = torch.cuda.Stream(device=self.device) if self._pin else None
+        # device-side writers (DeviceActor) keep [t_next, f_next, size] on the GPU
+        self.cursor = None
+        self.device_writer = False
+
+    # ----------------------------------------------------------- staging
+    def _reset_stage(self):
+        self._st_frames: List[np.ndarray] = []
+        self._st_frame_first = self._f_next
+        self._st_trans: List[tuple] = []
+        self._st_trans_first = self._t_next
+
+    def _alloc_frame(self, frame) -> int:
+        # frame slots are handed out sequentially, so staged frames are one
+        # contiguous (wrap-split) range starting at _st_frame_first
+        slot = self._f_next
+        self._f_next = (self._f_next + 1) % self.num_frames
+        self._st_frames.append(np.asarray(frame, dtype=np.uint8))
+        return slot
+
+    def size(self) -> int:
+        if self.device_writer:
+            return int(self.size_dev[0])
+        return self._size
+
+    def __len__(self):
+        return self.size()
+
+    # ------------------------------------------------------------- write API
+    def begin_episode(self, obs, actor: int = 0):
+        """Start an episode: first frame duplicated k times (reference FrameBuffer semantics)."""
+        if self.frame_mode:
+            slot = self._alloc_frame(obs)
+            self._stacks[actor] = [slot] * self.k
+        else:
+            self._last_obs[actor] = np.asarray(obs, dtype=np.float32).reshape(-1)
+
+    def add_step(self, action: int, reward: float, next_obs, done: bool, actor: int = 0,
+                 gamma_n: float = 1.0):
+        """Append one transition whose state is the actor's current stack."""
+        if self.frame_mode:
+            st = self._stacks[actor]
+            assert st is not None, 'begin_episode() first'
+            slot = self._alloc_frame(next_obs)
+            self._st_trans.append((list(st), slot, int(action), float(reward), float(done), float(gamma_n)))
+            self._stacks[actor] = st[1:] + [slot]
+        else:
+            o = self._last_obs[actor]
+            n = np.asarray(next_obs, dtype=np.float32).reshape(-1)
+            self._st_trans.append((o, n, int(action), float(reward), float(done), float(gamma_n)))
+            self._last_obs[actor] = n
+        if len(self._st_trans) >= self._stage_size:
+            self.flush()
+
+    def add_transition(self, state_slots, next_slot, action, reward, done, gamma_n=1.0):
+        """Low-level add with explicit frame slots (n-step / Ape-X actors)."""
+        self._st_trans.append((list(state_slots), int(next_slot), int(action), float(reward),
+                               float(done), float(gamma_n)))
+        if len(self._st_trans) >= self._stage_size:
+            self.flush()
+
+    def write_frame(self, frame) -> int:
+        return self._alloc_frame(frame)
+
+    def flush(self):
+        """Copy staged frames/transitions into the device ring (contiguous, wrap-split)."""
+        assert not self.device_writer or not (self._st_frames or self._st_trans), \
+            'a replay is fed either by host staging or by device actors, not both'
+        if not self._st_frames and not self._st_trans:
+            return
+        if self._st_frames:
+            arr = np.stack(self._st_frames)
+            self._ring_copy(self.frames, self._st_frame_first, arr)
+        n = len(self._st_trans)
+        if n:
+            first = self._st_trans_first
+            if self.frame_mode:
+                sidx = np.array([t[0] for t in self._st_trans], dtype=np.int32).reshape(n, self.k)
+                nidx = np.array([t[1] for t in self._st_trans], dtype=np.int32)
+                self._ring_copy(self.state_idx, first, sidx)
+                self._ring_copy(self.next_idx, first, nidx)
+            else:
+                self._ring_copy(self.obs, first, np.stack([t[0] for t in self._st_trans]))
+                self._ring_copy(self.next_obs, first, np.stack([t[1] for t in self._st_trans]))
+            self._ring_copy(self.actions, first, np.array([t[2] for t in self._st_trans], dtype=np.int32))
+            self._ring_copy(self.rewards, first, np.array([t[3] for t in self._st_trans], dtype=np.float32))
+            self._ring_copy(self.dones, first, np.array([t[4] for t in self._st_trans], dtype=np.float32))
+            self._ring_copy(self.gammas, first, np.array([t[5] for t in self._st_trans], dtype=np.float32))
+            self._t_next = (first + n) % self.capacity
+            self._size = min(self.capacity, self._size + n)
+            if self.prioritized:
+                idx = (torch.arange(n, dtype=torch.int64) + first) % self.capacity
+                self.tree.set_max_priority(idx.to(self.device, torch.int32))
+        self._sync_copies()
+        self.size_dev.fill_(self._size)
+        self._reset_stage()
+
+    def _ring_copy(self, dst: torch.Tensor, first: int, src: np.ndarray):
+        cap = dst.shape[0]
+        n = src.shape[0]
+        t = torch.from_numpy(np.ascontiguousarray(src))
+        if self._pin:
+            t = t.pin_memory()
+        end = first + n
+        if end <= cap:
+            self._copy(dst[first:end], t)
+        else:
+            k = cap - first
+            self._copy(dst[first:], t[:k])
+            self._copy(dst[:end - cap], t[k:])
+
+    def _copy(self, dst, src):
+        if self._copy_stream is not None:
+            with torch.cuda.stream(self._copy_stream):
+                dst.copy_(src, non_blocking=True)
+                src.record_stream(self._copy_stream) if src.is_cuda else None
+        else:
+            dst.copy_(src)
+
+    def _sync_copies(self):
+        if self._copy_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._copy_stream)
+
+    # ------------------------------------------------------------- read API
+    def sample_indices(self, batch_size: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Uniform sample WITHOUT replacement (reference: random.sample), device-side."""
+        if out is None:
+            out = torch.empty(batch_size, dtype=torch.int32, device=self.device)
+        kernels.replay_sample_uniform(self.size_dev, self.rng_state, out)
+        return out
+
+    def sample_prioritized(self, batch_size: int, beta: torch.Tensor, idx_out=None, w_out=None):
+        if idx_out is None:
+            idx_out = torch.empty(batch_size, dtype=torch.int32, device=self.device)
+        if w_out is None:
+            w_out = torch.empty(batch_size, dtype=torch.float32, device=self.device)
+        self.tree.sample(self.rng_state, self.size_dev, beta, idx_out, w_out)
+        return idx_out, w_out
+
+    def update_priorities(self, idx: torch.Tensor, td_abs: torch.Tensor, eps: float = 1e-6):
+        self.tree.update(idx, td_abs, self.alpha, eps)
+
+    def gather(self, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Materialise a minibatch: states/next_states (uint8 NHWC stacks or f32 vectors)."""
+        out = {
+            'actions': self.actions.index_select(0, idx.long()),
+            'rewards': self.rewards.index_select(0, idx.long()),
+            'dones': self.dones.index_select(0, idx.long()),
+            'gammas': self.gammas.index_select(0, idx.long()),
+        }
+        if self.frame_mode:
+            out['states'], out['next_states'] = kernels.replay_gather_frames(
+                self.frames, self.state_idx, self.next_idx, idx)
+        else:
+            out['states'] = self.obs.index_select(0, idx.long())
+            out['next_states'] = self.next_obs.index_select(0, idx.long())
+        return out
+
+    def fill_synthetic(self, n: int, num_actions: int, seed: int = 0, episode_len: int = 500):
+        """Fill n transitions with synthetic random frames/rewards directly on the device
+        (benchmarks: "synthetic frames"). Episodes of ``episode_len`` steps with the reference's
+        duplicated first frame; frames are uniform random bytes."""
+        n = min(n, self.capacity)
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        if self.frame_mode:
+            nf = n + n // episode_len + self.k + 1
+            self.frames[:nf].random_(0, 256, generator=g)
+            t = torch.arange(n, device=self.device)
+            ep = t // episode_len
+            pos = t - ep * episode_len
+            first = ep * (episode_len + 1)                   # frame slot of each episode's reset frame
+            cur = first + pos                                # newest frame of state t
+            ks = torch.arange(self.k, device=self.device)
+            slots = cur.view(-1, 1) - (self.k - 1 - ks).view(1, -1)
+            slots = torch.maximum(slots, first.view(-1, 1))  # duplicate the episode's first frame
+            self.state_idx[:n] = slots.to(torch.int32)
+            self.next_idx[:n] = (cur + 1).to(torch.int32)
+            self._f_next = int(nf) % self.num_frames
+        else:
+            self.obs[:n].normal_(generator=g)
+            self.next_obs[:n].normal_(generator=g)
+        self.actions[:n].random_(0, num_actions, generator=g)
+        self.rewards[:n] = (torch.rand(n, device=self.device, generator=g) < 0.02).float()
+        self.dones[:n] = 0.0
+        if self.frame_mode:
+            self.dones[:n][(torch.arange(n, device=self.device) % episode_len) == episode_len - 1] = 1.0
+        self.gammas[:n] = 0.99
+        self._size = n
+        self._t_next = n % self.capacity
+        self.size_dev.fill_(n)
+        if self.prioritized:
+            self.tree.set_max_priority(torch.arange(n, dtype=torch.int32, device=self.device))
+
+    def nbytes(self) -> int:
+        ts = [self.actions, self.rewards, self.dones, self.gammas]
+        ts += [self.frames, self.state_idx, self.next_idx] if self.frame_mode else [self.obs, self.next_obs]
+        return sum(t.numel() * t.element_size() for t in ts)
