@@ -105,7 +105,7 @@ def main():
             'metric': METRIC, 'value': round(sps, 2), 'unit': 'SGD steps/s (all GPUs)',
             'n_gpus': ctx.world_size, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(1000.0 * el / args.steps, 4), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic (random uint8 84x84 frames, random init)',
+            'vs_baseline': None, 'dtype': getattr(net.executor, 'compute_dtype', 'fp32'), 'data': 'synthetic (random uint8 84x84 frames, random init)',
             'env_frames_per_sec': round(frames, 1),
             'samples_per_sec': round(sps * args.batch, 1),
             'config': {'model': 'nature-cnn' if args.network == 'nature' else args.network,

@@ -3,7 +3,8 @@
 // current HIP stream, so the ops are captured correctly into HIP graphs.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "include/dqn_host.h"
 #include "include/dqn_kernels.h"
@@ -11,7 +12,7 @@
 
 namespace {
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
@@ -25,7 +26,7 @@ void replay_sample_uniform(torch::Tensor size, torch::Tensor rng, torch::Tensor 
   CHECK_T(size, torch::kInt32); CHECK_T(rng, torch::kInt64); CHECK_T(out, torch::kInt32);
   TORCH_CHECK(out.numel() >= 1 && out.numel() <= 1024, "sample batch must be in [1, 1024]");
   TORCH_CHECK(rng.numel() == 2, "rng state must be [seed, counter]");
-  c10::hip::HIPGuard g(out.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
   launch_replay_sample_uniform(ptr<int32_t>(size), ptr<int64_t>(rng), ptr<int32_t>(out), (int)out.numel(),
                                cur_stream());
 }
@@ -41,7 +42,7 @@ void replay_gather_frames(torch::Tensor frames, torch::Tensor state_idx, torch::
   TORCH_CHECK(K >= 1 && K <= 4, "frames_per_state must be 1..4");
   TORCH_CHECK(HW % 4 == 0, "H*W must be a multiple of 4");
   TORCH_CHECK(s.numel() == (int64_t)B * HW * K && ns.numel() == s.numel(), "output size mismatch");
-  c10::hip::HIPGuard g(frames.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(frames.device());
   launch_replay_gather_frames(ptr<uint8_t>(frames), ptr<int32_t>(state_idx), ptr<int32_t>(next_idx),
                               ptr<int32_t>(idx), ptr<uint8_t>(s), ptr<uint8_t>(ns), B, HW, K, cur_stream());
 }
@@ -52,7 +53,7 @@ void sumtree_set(torch::Tensor sum, torch::Tensor mn, torch::Tensor maxp, torch:
   CHECK_T(idx, torch::kInt32); CHECK_T(td, torch::kFloat32);
   TORCH_CHECK(sum.numel() == 2 * P && mn.numel() == 2 * P, "tree size must be 2P");
   TORCH_CHECK(use_max || td.numel() >= idx.numel(), "td must cover idx");
-  c10::hip::HIPGuard g(sum.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(sum.device());
   launch_sumtree_set(ptr<float>(sum), ptr<float>(mn), ptr<float>(maxp), ptr<int32_t>(idx), ptr<float>(td),
                      (float)alpha, (float)eps, use_max ? 1 : 0, (int)idx.numel(), (int)P, cur_stream());
 }
@@ -64,7 +65,7 @@ void sumtree_sample(torch::Tensor sum, torch::Tensor mn, torch::Tensor rng, torc
   CHECK_T(w_out, torch::kFloat32);
   TORCH_CHECK(idx_out.numel() <= 1024 && w_out.numel() == idx_out.numel(), "PER batch must be <= 1024");
   TORCH_CHECK(sum.numel() == 2 * P, "tree size must be 2P");
-  c10::hip::HIPGuard g(sum.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(sum.device());
   launch_sumtree_sample(ptr<float>(sum), ptr<float>(mn), ptr<int64_t>(rng), ptr<int32_t>(size), ptr<float>(beta),
                         ptr<int32_t>(idx_out), ptr<float>(w_out), (int)idx_out.numel(), (int)P, cur_stream());
 }
@@ -82,7 +83,7 @@ void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tens
   if (has_step) { CHECK_T(step, torch::kInt64); }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
-  c10::hip::HIPGuard g(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
   launch_optimizer_step((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1),
                         ptr<float>(beta_pow), has_step ? ptr<int64_t>(step) : nullptr, ptr<int32_t>(ticket), h,
                         (float)lr, (float)reg, (int)reg_end, (float)grad_scale, (int)w.numel(), cur_stream());
@@ -93,7 +94,7 @@ void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tens
   CHECK_T(dst, torch::kFloat32); CHECK_T(src, torch::kFloat32);
   TORCH_CHECK(dst.numel() == src.numel() && dst.numel() % 4 == 0, "target/online size");
   if (use_step) { CHECK_T(step, torch::kInt64); }
-  c10::hip::HIPGuard g(dst.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dst.device());
   launch_target_update(ptr<float>(dst), ptr<float>(src), (float)tau, use_step ? ptr<int64_t>(step) : nullptr,
                        (int)freq, (int)dst.numel(), cur_stream());
 }
@@ -113,7 +114,7 @@ void td_loss_scalar(torch::Tensor q, torch::Tensor qn_t, c10::optional<torch::Te
   if (qn_o.has_value()) { CHECK_T((*qn_o), torch::kFloat32); TORCH_CHECK(qn_o->sizes() == q.sizes()); qo = ptr<float>(*qn_o); }
   const float* w = nullptr;
   if (wts.has_value()) { CHECK_T((*wts), torch::kFloat32); TORCH_CHECK(wts->numel() == B); w = ptr<float>(*wts); }
-  c10::hip::HIPGuard g(q.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   launch_td_loss_scalar(ptr<float>(q), ptr<float>(qn_t), qo, ptr<int32_t>(act), ptr<float>(rew), ptr<float>(done),
                         ptr<float>(gam), w, ptr<float>(loss), ptr<float>(dq), ptr<float>(prio), B, A, huber ? 1 : 0,
                         (float)delta, cur_stream());
@@ -134,7 +135,7 @@ void td_loss_c51(torch::Tensor lg, torch::Tensor lgn_t, c10::optional<torch::Ten
   if (lgn_o.has_value()) { CHECK_T((*lgn_o), torch::kFloat32); TORCH_CHECK(lgn_o->sizes() == lg.sizes()); lo = ptr<float>(*lgn_o); }
   const float* w = nullptr;
   if (wts.has_value()) { CHECK_T((*wts), torch::kFloat32); TORCH_CHECK(wts->numel() == B); w = ptr<float>(*wts); }
-  c10::hip::HIPGuard g(lg.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(lg.device());
   launch_td_loss_c51(ptr<float>(lg), ptr<float>(lgn_t), lo, ptr<int32_t>(act), ptr<float>(rew), ptr<float>(done),
                      ptr<float>(gam), w, ptr<float>(loss), ptr<float>(dlg), ptr<float>(prio), B, A, N, (float)vmin,
                      (float)vmax, cur_stream());
@@ -143,7 +144,7 @@ void td_loss_c51(torch::Tensor lg, torch::Tensor lgn_t, c10::optional<torch::Ten
 void preprocess_batch(torch::Tensor in, torch::Tensor out) {
   CHECK_T(in, torch::kUInt8); CHECK_T(out, torch::kUInt8);
   TORCH_CHECK(in.dim() == 4 && in.size(3) == 3 && out.dim() == 3 && out.size(0) == in.size(0), "shapes");
-  c10::hip::HIPGuard g(in.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
   launch_preprocess_batch(ptr<uint8_t>(in), ptr<uint8_t>(out), (int)in.size(0), (int)in.size(1), (int)in.size(2),
                           (int)out.size(1), (int)out.size(2), cur_stream());
 }
@@ -171,7 +172,7 @@ void actor_step(torch::Tensor q, torch::Tensor frames, torch::Tensor stacks, tor
   TORCH_CHECK(cursor.numel() == 3 && eps.numel() == 3 && rng.numel() == 2, "state vectors");
   TORCH_CHECK(F >= 2 * C + K, "frame ring must hold 2C + k frames");
   TORCH_CHECK(E >= 1 && E <= C, "env count");
-  c10::hip::HIPGuard g(q.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   launch_actor_step(ptr<float>(q), ptr<uint8_t>(frames), ptr<int32_t>(stacks), ptr<int64_t>(cursor),
                     ptr<int32_t>(size_dev), ptr<int32_t>(state_idx), ptr<int32_t>(next_idx), ptr<int32_t>(actions),
                     ptr<float>(rewards), ptr<float>(dones), ptr<float>(gammas), ptr<float>(eps), ptr<int64_t>(rng),
@@ -183,7 +184,7 @@ void stack_states(torch::Tensor frames, torch::Tensor stacks, torch::Tensor out)
   CHECK_T(frames, torch::kUInt8); CHECK_T(stacks, torch::kInt32); CHECK_T(out, torch::kUInt8);
   const int E = (int)stacks.size(0), K = (int)stacks.size(1), HW = (int)(frames.size(1) * frames.size(2));
   TORCH_CHECK(out.numel() == (int64_t)E * HW * K, "out must be [E, H, W, K]");
-  c10::hip::HIPGuard g(frames.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(frames.device());
   launch_stack_states(ptr<uint8_t>(frames), ptr<int32_t>(stacks), ptr<uint8_t>(out), E, HW, K, cur_stream());
 }
 

@@ -93,7 +93,9 @@ __global__ void __launch_bounds__(256) actor_step_kernel(ActorArgs a) {
   if (s_done) write_random_frame(a.frames + (int64_t)rslot * a.HW, a.HW, seed, ctr, 0x101u + 2u * e);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int tk = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed ticket: the last block only writes the cursor/eps/rng words that
+    // every block read at its start (see optim.hip for the same pattern)
+    const int tk = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tk == (int)gridDim.x - 1) {
       float eps = eps0;
       for (int i = 0; i < a.E && eps > eps_min; ++i) eps -= decay;

@@ -88,7 +88,10 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
   // last block advances global_step and (Adam) the beta powers. Every block
   // read beta_pow above, before its ticket add, so the update cannot race.
   if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed: the last arriver only WRITES beta_pow/step; every block's read of
+    // beta_pow completed (value consumed in the loop) before its ticket add.
+    // (An acq_rel agent atomic here costs an L2 writeback + invalidate per block.)
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {
       if (step) step[0] += 1;
       if constexpr (OP == 3) {

@@ -41,6 +41,38 @@ sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ 
     if (dup) v = draw();
     __syncthreads();
   }
+  // Rejection stalls when B is close to n (coupon collector): resolve what is
+  // left serially with an LDS bitmap (only reachable for small n).
+  __shared__ uint32_t used[2048];                  // 65536 bits
+  __shared__ int fix_needed;
+  if (i == 0) fix_needed = 0;
+  if (i < 1024) cand[i] = v;
+  __syncthreads();
+  bool dup = false;
+  if (i < B && distinct_possible) {
+    for (int j = 0; j < i; ++j) dup |= (cand[j] == v);
+    if (dup) fix_needed = 1;
+  }
+  __syncthreads();
+  if (fix_needed && n <= 65536u) {
+    for (int w = i; w < 2048; w += blockDim.x) used[w] = 0;
+    __syncthreads();
+    if (i < B && !dup) atomicOr(&used[v >> 5], 1u << (v & 31));
+    __syncthreads();
+    if (i == 0) {
+      for (int j = 0; j < B; ++j) {
+        bool dj = false;
+        for (int q = 0; q < j; ++q) dj |= (cand[q] == cand[j]);
+        if (!dj) continue;
+        uint32_t c = (uint32_t)cand[j];
+        while (used[c >> 5] & (1u << (c & 31))) c = (c + 1) % n;
+        used[c >> 5] |= 1u << (c & 31);
+        cand[j] = (int32_t)c;
+      }
+    }
+    __syncthreads();
+    if (i < B) v = cand[i];
+  }
   if (i < B) out[i] = v;
   if (i == 0) rng[1] = (int64_t)(ctr + 1);
 }

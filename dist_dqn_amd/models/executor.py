@@ -17,6 +17,7 @@ from .params import FlatLayout
 
 class TorchExecutor:
     name = 'torch'
+    compute_dtype = 'fp32'
 
     def __init__(self, arch: ArchSpec, layout: FlatLayout, input_scale: float = 1.0,
                  loss: str = 'mse', huber_delta: float = 1.0, double_dqn: bool = False):

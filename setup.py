@@ -1,39 +1,99 @@
-"""Build the in-tree native extension ``dist_dqn_amd/_C*.so`` for gfx950.
+"""Build the in-tree native extension ``dist_dqn_amd/_C<EXT_SUFFIX>`` for gfx950.
 
-    PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace
+    python setup.py build_ext --inplace        (or: python setup.py)
 
-HIP kernels (csrc/kernels/*.hip) include only the HIP headers and compile
-fast; torch headers are confined to the two binding translation units.
+A direct hipcc build (no hipify pass, no CUDA compatibility layer):
+  * csrc/kernels/*.hip   -> hipcc --offload-arch=gfx950 (HIP headers only: fast)
+  * csrc/host/*.cpp      -> g++ (C++ host runtime: preprocessing, SPSC rings, CRC32C)
+  * csrc/*bindings.cpp   -> hipcc host compile with the torch headers
+  * link                 -> hipcc -shared with libtorch / libamdhip64
+Objects go to build/ and are rebuilt when the source or any csrc header is newer.
 """
+import concurrent.futures as cf
 import glob
 import os
-
-from setuptools import setup
-
-os.environ.setdefault('PYTORCH_ROCM_ARCH', 'gfx950')
-from torch.utils.cpp_extension import BuildExtension, CUDAExtension  # noqa: E402
+import subprocess
+import sys
+import sysconfig
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
+HIPCC = os.path.join(os.environ.get('ROCM_PATH', '/opt/rocm'), 'bin', 'hipcc')
+BUILD = os.path.join(ROOT, 'build', 'obj')
+OUT = os.path.join(ROOT, 'dist_dqn_amd', '_C' + sysconfig.get_config_var('EXT_SUFFIX'))
 
 
-def rel(p):
-    return os.path.relpath(p, ROOT)
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths(device_type='cuda') if 'device_type' in ce.include_paths.__code__.co_varnames \
+        else ce.include_paths(cuda=True)
+    inc += [sysconfig.get_paths()['include']]
+    libdirs = ce.library_paths(device_type='cuda') if 'device_type' in ce.library_paths.__code__.co_varnames \
+        else ce.library_paths(cuda=True)
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    defs = ['-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1', '-DTORCH_API_INCLUDE_EXTENSION_H',
+            '-DTORCH_EXTENSION_NAME=_C', '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi]
+    return inc, libdirs, defs
 
 
-sources = ([rel(os.path.join(ROOT, 'csrc', 'bindings.cpp')), rel(os.path.join(ROOT, 'csrc', 'net_bindings.cpp'))]
-           + sorted(rel(p) for p in glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')))
-           + sorted(rel(p) for p in glob.glob(os.path.join(ROOT, 'csrc', 'host', '*.cpp'))))
+def _newer(src, obj, headers):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
 
-setup(
-    name='dist_dqn_amd',
-    version='0.1.0',
-    packages=['dist_dqn_amd'],
-    ext_modules=[CUDAExtension(
-        'dist_dqn_amd._C', sources,
-        include_dirs=[os.path.join(ROOT, 'csrc')],
-        extra_compile_args={
-            'cxx': ['-O3', '-std=c++17'],
-            'nvcc': ['-O3', '-std=c++17', '--offload-arch=gfx950', '-ffp-contract=fast'],
-        })],
-    cmdclass={'build_ext': BuildExtension.with_options(use_ninja=True)},
-)
+
+def build(verbose=False, jobs=None):
+    inc, libdirs, defs = _torch_flags()
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(ROOT, 'csrc', '**', '*.h'), recursive=True)
+    kern = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')))
+    host = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'host', '*.cpp')))
+    binds = sorted(glob.glob(os.path.join(ROOT, 'csrc', '*.cpp')))
+    cmds = []
+    objs = []
+    for src in kern:
+        obj = os.path.join(BUILD, os.path.basename(src) + '.o')
+        objs.append(obj)
+        cmd = [HIPCC, '-c', src, '-o', obj, '-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH,
+               '-ffp-contract=fast', '-I' + os.path.join(ROOT, 'csrc'), '-D__HIP_PLATFORM_AMD__=1']
+        if _newer(src, obj, headers):
+            cmds.append(cmd)
+    for src in host:
+        obj = os.path.join(BUILD, 'host_' + os.path.basename(src) + '.o')
+        objs.append(obj)
+        cmd = ['g++', '-c', src, '-o', obj, '-O3', '-std=c++17', '-fPIC', '-Wall']
+        if _newer(src, obj, headers):
+            cmds.append(cmd)
+    for src in binds:
+        obj = os.path.join(BUILD, 'bind_' + os.path.basename(src) + '.o')
+        objs.append(obj)
+        cmd = [HIPCC, '-c', src, '-o', obj, '-O2', '-std=c++17', '-fPIC', '-I' + os.path.join(ROOT, 'csrc')] + \
+              ['-I' + i for i in inc] + defs
+        if _newer(src, obj, headers):
+            cmds.append(cmd)
+
+    def run(cmd):
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError('compile failed: %s\n%s%s' % (' '.join(cmd), r.stdout, r.stderr))
+        return cmd[2] if len(cmd) > 2 else ''
+
+    jobs = jobs or int(os.environ.get('MAX_JOBS', min(16, os.cpu_count() or 4)))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for f in cf.as_completed([ex.submit(run, c) for c in cmds]):
+            f.result()
+    if cmds or not os.path.exists(OUT):
+        link = [HIPCC, '-shared', '-fPIC', '-o', OUT] + objs + ['-L' + d for d in libdirs] + \
+               ['-Wl,-rpath,' + d for d in libdirs] + \
+               ['-lc10', '-ltorch', '-ltorch_cpu', '-ltorch_python', '-lamdhip64', '-lc10_hip', '-ltorch_hip']
+        run(link)
+    return OUT
+
+
+if __name__ == '__main__':
+    args = [a for a in sys.argv[1:] if a not in ('build_ext', '--inplace')]
+    print(build(verbose='-v' in args))
