@@ -1,0 +1,70 @@
+// Argument structs + launchers of the Q-network kernels (csrc/kernels/qnet.hip).
+// Plain C++ (no torch types) so both the HIP TU and the torch binding TU include it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dqn {
+
+// One packing job: fp32 master tensor (TF layout) -> bf16 MFMA B-fragments
+// [K/32][N/16][64][8] (mode 0..2) or a contiguous fp32 copy (mode 3, biases).
+struct PackJob {
+  int src_off;   // element offset in the fp32 flat buffer
+  int K, N;      // logical B operand shape [K][N] (mode 3: K = length)
+  int dst_off;   // element offset (bf16 units) in the packed buffer
+  int dst_N16;   // n-tiles per k-step row of the destination (>= nt_off + N/16)
+  int nt_off;    // n-tile offset (concatenation along N)
+  int ks_off;    // k-step offset (concatenation along K)
+  int mode;      // 0 natural [K][N]; 1 conv dgrad (p0 taps, p1 CIN, p2 COUT); 2 dense transpose (p0 = OUT); 3 fp32 copy
+  int p0, p1, p2, pad;
+};
+
+// Implicit-GEMM arguments (up to 3 instances: online(s), target(s'), online(s')).
+struct ConvArgs {
+  const void* in[3];
+  const void* w[3];          // packed bf16 B fragments
+  const float* bias[3];
+  void* out[3];
+  const void* mask[3];       // ReLU mask source for dgrad epilogues
+  float scale[3];
+  int M, N, K, N16;          // GEMM shape; N16 = n-tiles per k-step of the packed B
+  int ldo;                   // output row stride (elements)
+  int IH, IW, OH, OW, pad_t, pad_l;
+};
+
+struct WgradArgs {
+  const void* dz;            // dZ rows [M][ldz] bf16 (gradient w.r.t. the layer pre-activation)
+  int ldz;
+  float* dw; float* db;      // columns [0, nsplit)
+  float* dw2; float* db2;    // columns [nsplit, N) (dueling concatenation), may be null
+  int nsplit, N;
+  int MC, KB, NB;            // rows per block, K-range per block, N-range per block
+  float scale;
+  int atomic;
+};
+
+struct HeadArgs {
+  int B, A, HID, dueling, huber, infer;
+  float delta;
+  const void* h[3];
+  const float* w[3]; const float* b[3];
+  const float* wv[3]; const float* bv[3];
+  const int32_t* act; const float* rew; const float* done; const float* gam; const float* wts;
+  float* loss; float* prio; float* q_out;
+  float* dw; float* db; float* dwv; float* dbv;
+  void* dh;
+};
+
+enum LayerKind {
+  L_NAT_CONV1_FWD = 1, L_NAT_CONV2_FWD = 2, L_NAT_CONV3_FWD = 3,
+  L_DENSE_FWD_RELU = 4, L_DENSE_FWD_F32 = 5, L_DENSE_DGRAD = 6,
+  L_NAT_CONV3_DGRAD = 7, L_NAT_CONV2_DGRAD = 8,
+};
+
+}  // namespace dqn
+
+void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int njobs, int max_threads,
+                 hipStream_t st);
+int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
+int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
+void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);

@@ -1,0 +1,546 @@
+// Q-network layer kernels for gfx950 (CDNA4): every GEMM-shaped op on the
+// bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate), wave64 tiles.
+//
+// Reference layers (TF 0.x ops, /root/reference/src/network.py:389-424):
+// conv2d + bias + relu (+ max_pool), matmul + bias (+ relu), and their
+// autodiff backward. Here:
+//   * pack_kernel      fp32 master weights (TF layouts) -> bf16 MFMA B-fragments
+//                      ([K/32][N/16][64 lanes][8]) for the forward and for dgrad;
+//   * igemm_kernel     implicit GEMM C[M][N] = A[M][K] B[K][N] with the A operand
+//                      produced on the fly by a loader (conv im2col from NHWC u8/bf16,
+//                      conv dgrad gather, dense rows) straight into registers and
+//                      B fragments read as one 16-byte load per lane; epilogues fuse
+//                      input scale + bias + ReLU (forward) or the ReLU mask (dgrad);
+//                      optional split-K across the waves of a block (LDS reduce);
+//   * wgrad_kernel     dW[K][N] = sum_m A[m][K]^T dZ[m][N] with both operands staged
+//                      transposed in LDS (padded rows: conflict-free ds_read_b128),
+//                      bias gradient fused, fp32 atomics only across M-chunks;
+//   * head_loss_kernel output layer + dueling combine + TD loss + dQ + head backward
+//                      (dW, db, dH masked by ReLU) in ONE workgroup.
+#include "common.h"
+#include "../include/dqn_nets_k.h"
+
+namespace dqn {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+
+DQN_DEV bfx8 zero8() {
+  bfx8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  return z;
+}
+
+DQN_DEV bfx8 u8x8_to_bf(uint32_t lo, uint32_t hi) {
+  bfx8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (__bf16)(float)((lo >> (8 * j)) & 0xffu);
+    r[4 + j] = (__bf16)(float)((hi >> (8 * j)) & 0xffu);
+  }
+  return r;
+}
+
+DQN_DEV f32x4 mfma16(const bfx8& a, const bfx8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ============================================================== weight packing
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src, __bf16* __restrict__ dst,
+                                                   const PackJob* __restrict__ jobs, const float* __restrict__ noise) {
+  const PackJob jb = jobs[blockIdx.y];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (jb.mode == 3) {                           // contiguous fp32 copy (bias concatenation)
+    if (t < jb.K) reinterpret_cast<float*>(dst + jb.dst_off)[t] = src[jb.src_off + t];
+    return;
+  }
+  const int K32 = (jb.K + 31) / 32, N16 = (jb.N + 15) / 16;
+  if (t >= K32 * N16 * 64) return;
+  const int l = t & 63, nt = (t >> 6) % N16, ks = (t >> 6) / N16;
+  const int n = nt * 16 + (l & 15);
+  bfx8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = ks * 32 + 8 * (l >> 4) + j;
+    float x = 0.f;
+    if (k < jb.K && n < jb.N) {
+      if (jb.mode == 0) {                       // natural [K][N] (conv HWIO fwd, dense fwd)
+        x = src[jb.src_off + (int64_t)k * jb.N + n];
+      } else if (jb.mode == 1) {                // conv dgrad: k=(tap, co), n=ci  <- W[tap][ci][co]
+        const int tap = k / jb.p2, co = k - tap * jb.p2;
+        x = src[jb.src_off + ((int64_t)tap * jb.p1 + n) * jb.p2 + co];
+      } else {                                  // dense transpose: k=o, n=i <- W[i][o] (OUT = p0)
+        x = src[jb.src_off + (int64_t)n * jb.p0 + k];
+      }
+    }
+    v[j] = (__bf16)x;
+  }
+  *reinterpret_cast<bfx8*>(dst + jb.dst_off + ((int64_t)((jb.ks_off + ks) * jb.dst_N16 + jb.nt_off + nt) * 64 + l) * 8) = v;
+}
+
+// ================================================================== A loaders
+// Each loader is built per (instance, row m) and returns the 8 consecutive
+// K-values [k0, k0+8) of row m as a bf16x8 MFMA A-fragment.
+template <typename Tin, int CIN, int KH, int KW, int S>
+struct ConvLoader {
+  const Tin* base;
+  int IH, IW, iy0, ix0;
+  bool ok;
+  DQN_DEV ConvLoader() {}
+  DQN_DEV ConvLoader(const ConvArgs& a, int inst, int m) {
+    const int ohw = a.OH * a.OW;
+    ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / ohw, r = mm - b * ohw, oy = r / a.OW, ox = r - oy * a.OW;
+    IH = a.IH; IW = a.IW;
+    iy0 = oy * S - a.pad_t;
+    ix0 = ox * S - a.pad_l;
+    base = reinterpret_cast<const Tin*>(a.in[inst]) + (int64_t)b * IH * IW * CIN;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    const int kh = k0 / (KW * CIN), rem = k0 - kh * (KW * CIN), kw = rem / CIN, ci = rem - kw * CIN;
+    const int iy = iy0 + kh, ix = ix0 + kw;
+    if constexpr (sizeof(Tin) == 1) {
+      static_assert(CIN == 4, "uint8 input path expects 4 stacked frames");
+      // 8 bytes = pixels (ix, ix+1) x 4 frames
+      uint32_t lo = 0, hi = 0;
+      if (iy >= 0 && iy < IH) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + (int64_t)iy * IW * CIN);
+        if (ix >= 0 && ix < IW) lo = row[ix];
+        if (ix + 1 >= 0 && ix + 1 < IW) hi = row[ix + 1];
+      }
+      return u8x8_to_bf(lo, hi);
+    } else {
+      if (iy < 0 || iy >= IH || ix < 0 || ix >= IW) return zero8();
+      return *reinterpret_cast<const bfx8*>(base + ((int64_t)iy * IW + ix) * CIN + ci);
+    }
+  }
+};
+
+// dgrad gather: row m = (b, iy, ix) of the conv INPUT, k = (kh, kw, co);
+// A[m][k] = dZ[b][oy][ox][co] where iy + pad_t - kh = S*oy (else 0).
+template <int COUT, int KH, int KW, int S>
+struct DgradLoader {
+  const __bf16* base;
+  int OH, OW, ty, tx;
+  bool ok;
+  DQN_DEV DgradLoader() {}
+  DQN_DEV DgradLoader(const ConvArgs& a, int inst, int m) {
+    const int ihw = a.IH * a.IW;
+    ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / ihw, r = mm - b * ihw, iy = r / a.IW, ix = r - iy * a.IW;
+    OH = a.OH; OW = a.OW;
+    ty = iy + a.pad_t;
+    tx = ix + a.pad_l;
+    base = reinterpret_cast<const __bf16*>(a.in[inst]) + (int64_t)b * OH * OW * COUT;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    const int tap = k0 / COUT, co = k0 - tap * COUT, kh = tap / KW, kw = tap - kh * KW;
+    const int ny = ty - kh, nx = tx - kw;
+    if (ny < 0 || nx < 0) return zero8();
+    const int oy = ny / S, ox = nx / S;
+    if (oy * S != ny || ox * S != nx || oy >= OH || ox >= OW) return zero8();
+    return *reinterpret_cast<const bfx8*>(base + ((int64_t)oy * OW + ox) * COUT + co);
+  }
+};
+
+struct DenseLoader {
+  const __bf16* row;
+  bool ok;
+  DQN_DEV DenseLoader() {}
+  DQN_DEV DenseLoader(const ConvArgs& a, int inst, int m) {
+    ok = m < a.M;
+    row = reinterpret_cast<const __bf16*>(a.in[inst]) + (int64_t)(ok ? m : 0) * a.K;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    return *reinterpret_cast<const bfx8*>(row + k0);
+  }
+};
+
+// ============================================================ implicit GEMM
+// Block = 4 waves = WM x WN x KSPLIT; wave tile = (MT*16) x (NT*16).
+// EPI: 0 = scale*acc + bias, ReLU, bf16 out; 1 = scale*acc + bias, fp32 out (no ReLU);
+//      2 = acc * (mask > 0), bf16 out (ReLU backward through the layer input).
+template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI>
+__global__ void __launch_bounds__(256) igemm_kernel(ConvArgs a) {
+  static_assert(WM * WN * KSPLIT == 4, "4 waves per block");
+  __shared__ float red[KSPLIT > 1 ? (KSPLIT - 1) * 64 * MT * NT * 4 : 1];
+  const int inst = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wk = wave % KSPLIT, wn = (wave / KSPLIT) % WN, wm = wave / (KSPLIT * WN);
+  const int m_base = blockIdx.x * (WM * MT * 16) + wm * MT * 16;
+  const int nt_base = blockIdx.y * (WN * NT) + wn * NT;
+  const int K32 = (a.K + 31) / 32;
+  const bfx8* __restrict__ Bp = reinterpret_cast<const bfx8*>(a.w[inst]);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // each lane owns row (lane & 15) of every m-tile and k-group (lane >> 4)
+  LD ld[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) ld[i] = LD(a, inst, m_base + i * 16 + (lane & 15));
+  const int kg = 8 * (lane >> 4);
+  const int ks_lo = (K32 * wk) / KSPLIT, ks_hi = (K32 * (wk + 1)) / KSPLIT;
+  for (int ks = ks_lo; ks < ks_hi; ++ks) {
+    bfx8 af[MT], bf[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) af[i] = ld[i].frag(ks * 32 + kg);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bf[j] = Bp[((int64_t)ks * a.N16 + nt_base + j) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+  }
+  if constexpr (KSPLIT > 1) {
+    // waves wk > 0 hand partial tiles to wk == 0 through LDS
+    const int slot = ((wm * WN + wn) * (KSPLIT - 1));
+    if (wk > 0) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            red[(((slot + wk - 1) * MT + i) * NT + j) * 256 + r * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (wk != 0) return;
+#pragma unroll
+    for (int s = 0; s < KSPLIT - 1; ++s)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += red[(((slot + s) * MT + i) * NT + j) * 256 + r * 64 + lane];
+  }
+  // epilogue: C/D layout col = lane & 15, row = 4*(lane >> 4) + r
+  const float scale = a.scale[inst];
+  const float* __restrict__ bias = a.bias[inst];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = (nt_base + j) * 16 + (lane & 15);
+    if (n >= a.N) continue;
+    const float bv = (EPI == 2 || bias == nullptr) ? 0.f : bias[n];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m_base + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= a.M) continue;
+        float v = acc[i][j][r];
+        const int64_t o = (int64_t)m * a.ldo + n;
+        if constexpr (EPI == 0) {
+          v = fmaxf(v * scale + bv, 0.f);
+          reinterpret_cast<__bf16*>(a.out[inst])[o] = (__bf16)v;
+        } else if constexpr (EPI == 1) {
+          reinterpret_cast<float*>(a.out[inst])[o] = v * scale + bv;
+        } else {
+          const float mk = (float)reinterpret_cast<const __bf16*>(a.mask[inst])[o];
+          reinterpret_cast<__bf16*>(a.out[inst])[o] = (__bf16)(mk > 0.f ? v : 0.f);
+        }
+      }
+    }
+  }
+}
+
+// ================================================================ weight grad
+// dW[k][n] (+)= scale * sum_{m in chunk} A[m][k] * dZ[m][n];  db[n] (+)= sum_m dZ[m][n]
+// grid: x = M-chunk, y = K-range (KB), z = N-range (NB). Operands for 32 rows
+// at a time are staged TRANSPOSED in LDS ([k][m], [n][m]) with 40-element
+// rows so each lane's 8 consecutive m are one conflict-free ds_read_b128.
+constexpr int WG_LDSROW = 40;
+constexpr int WG_MAXT = 12;   // output tiles per wave
+
+template <class LD>
+__global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 smem[];
+  __bf16* At = smem;                               // [KB][40]
+  __bf16* Zt = smem + g.KB * WG_LDSROW;            // [NB][40]
+  float* bsum = reinterpret_cast<float*>(Zt + g.NB * WG_LDSROW);  // [NB]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k_lo = blockIdx.y * g.KB, n_lo = blockIdx.z * g.NB;
+  const int m_lo = blockIdx.x * g.MC;
+  const int m_hi = min(a.M, m_lo + g.MC);
+  const int KT = g.KB / 16, NTt = g.NB / 16, tiles = KT * NTt;
+  f32x4 acc[WG_MAXT];
+#pragma unroll
+  for (int i = 0; i < WG_MAXT; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = g.db != nullptr && blockIdx.y == 0;
+  for (int t = threadIdx.x; t < g.NB; t += 256) bsum[t] = 0.f;
+  const __bf16* __restrict__ dz = reinterpret_cast<const __bf16*>(g.dz);
+  for (int m0 = m_lo; m0 < m_hi; m0 += 32) {
+    __syncthreads();
+    // stage dZ^T: 32 rows x NB cols (16-byte global loads)
+    for (int t = threadIdx.x; t < 32 * (g.NB / 8); t += 256) {
+      const int r = t / (g.NB / 8), c8 = (t - r * (g.NB / 8)) * 8;
+      const int m = m0 + r;
+      bfx8 v = zero8();
+      if (m < m_hi) v = *reinterpret_cast<const bfx8*>(dz + (int64_t)m * g.ldz + n_lo + c8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Zt[(c8 + j) * WG_LDSROW + r] = v[j];
+    }
+    // stage A^T: 32 rows x KB cols of the (implicit) A operand
+    for (int t = threadIdx.x; t < 32 * (g.KB / 8); t += 256) {
+      const int r = t / (g.KB / 8), c8 = (t - r * (g.KB / 8)) * 8;
+      const int m = m0 + r;
+      bfx8 v = zero8();
+      if (m < m_hi) {
+        LD ld(a, 0, m);
+        v = ld.frag(k_lo + c8);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) At[(c8 + j) * WG_LDSROW + r] = v[j];
+    }
+    __syncthreads();
+    if (do_bias) {
+      for (int n = threadIdx.x; n < g.NB; n += 256) {
+        float s = 0.f;
+        for (int r = 0; r < 32; ++r) s += (float)Zt[n * WG_LDSROW + r];
+        bsum[n] += s;
+      }
+    }
+    const int kg = 8 * (lane >> 4), row = lane & 15;
+#pragma unroll
+    for (int i = 0; i < WG_MAXT; ++i) {
+      const int tile = wave + 4 * i;
+      if (tile < tiles) {
+        const int kt = tile / NTt, nt = tile - kt * NTt;
+        const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * WG_LDSROW + kg);
+        const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * WG_LDSROW + kg);
+        acc[i] = mfma16(af, bf, acc[i]);
+      }
+    }
+  }
+  // epilogue: acc tile rows = k (4*(lane>>4)+r), cols = n (lane & 15)
+#pragma unroll
+  for (int i = 0; i < WG_MAXT; ++i) {
+    const int tile = wave + 4 * i;
+    if (tile < tiles) {
+      const int kt = tile / NTt, nt = tile - kt * NTt;
+      const int n = n_lo + nt * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k_lo + kt * 16 + 4 * (lane >> 4) + r;
+        if (k < a.K && n < g.N) {
+          float* p = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
+                                  : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
+          const float v = acc[i][r] * g.scale;
+          if (g.atomic) atomicAdd(p, v); else *p = v;
+        }
+      }
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    for (int n = threadIdx.x; n < g.NB; n += 256)
+      if (n_lo + n < g.N) {
+        const int nn = n_lo + n;
+        float* p = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        if (g.atomic) atomicAdd(p, bsum[n]); else *p = bsum[n];
+      }
+  }
+}
+
+// =========================================================== fused head + loss
+// Instances of the last hidden layer H (bf16): h[0] = online(s), h[1] = target(s'),
+// h[2] = online(s') (Double DQN). Plain: Q = H W + b. Dueling: H = [Hv | Ha],
+// Q = (Hv wv + bv) + (Ha Wa + ba) - mean_a(Ha Wa + ba).
+// Outputs: loss, prio[B], dW/db of the head (fp32, plain stores into the flat grad),
+// dH [B][HH] bf16 masked by ReLU (H > 0), Q of instance 0 (for logging).
+__global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  const int B = a.B, A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
+  float* q = hsm;                           // [3][B][A]
+  float* dq = q + 3 * B * A;                // [B][A]  dL/dQ
+  float* dv = dq + B * A;                   // [B]     dueling: dL/dV
+  float* red = dv + B;                      // [32]
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  // ---- 1. Q values (one thread per (inst, b, a) dot product, fp32 accumulate)
+  for (int t = tid; t < ninst * B * A; t += nth) {
+    const int inst = t / (B * A), r = t - inst * B * A, b = r / A, act = r - b * A;
+    const __bf16* h = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)b * HH;
+    const float* W = a.w[inst];              // plain: [HID][A]; dueling: advantage [HID][A]
+    float s = a.b[inst][act];
+    const __bf16* ha = a.dueling ? h + HID : h;
+    for (int k = 0; k < HID; k += 8) {
+      const bfx8 hv = *reinterpret_cast<const bfx8*>(ha + k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (float)hv[j] * W[(int64_t)(k + j) * A + act];
+    }
+    q[t] = s;
+  }
+  __syncthreads();
+  if (a.dueling) {
+    // value stream + mean-subtraction, one thread per (inst, b)
+    for (int t = tid; t < ninst * B; t += nth) {
+      const int inst = t / B, b = t - inst * B;
+      const __bf16* hv = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)b * HH;
+      const float* wv = a.wv[inst];
+      float v = a.bv[inst][0];
+      for (int k = 0; k < HID; ++k) v += (float)hv[k] * wv[k];
+      float mean = 0.f;
+      for (int i = 0; i < A; ++i) mean += q[(inst * B + b) * A + i];
+      mean /= (float)A;
+      for (int i = 0; i < A; ++i) q[(inst * B + b) * A + i] += v - mean;
+    }
+    __syncthreads();
+  }
+  if (a.infer) {                            // acting: Q of instance 0 only
+    for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
+    return;
+  }
+  // ---- 2. TD loss (one thread per sample)
+  float contrib = 0.f;
+  if (tid < B) {
+    const int b = tid;
+    const float* sel = q + ((ninst == 3 ? 2 : 1) * B + b) * A;
+    int best = 0;
+    float bvv = sel[0];
+    for (int i = 1; i < A; ++i) if (sel[i] > bvv) { bvv = sel[i]; best = i; }
+    const float nxt = q[(B + b) * A + best];
+    const float y = a.rew[b] + a.gam[b] * (1.f - a.done[b]) * nxt;
+    const int at = a.act[b];
+    const float d = q[b * A + at] - y;
+    const float w = a.wts != nullptr ? a.wts[b] : 1.f;
+    float per, dper;
+    if (a.huber) {
+      const float ad = fabsf(d);
+      per = ad <= a.delta ? 0.5f * d * d : a.delta * (ad - 0.5f * a.delta);
+      dper = ad <= a.delta ? d : copysignf(a.delta, d);
+    } else {
+      per = d * d;
+      dper = 2.f * d;
+    }
+    contrib = w * per;
+    const float gsc = w * dper / (float)B;
+    for (int i = 0; i < A; ++i) dq[b * A + i] = (i == at) ? gsc : 0.f;
+    if (a.dueling) {
+      // Q_i = V + A_i - mean(A): dV = sum_i dQ_i, dA_i = dQ_i - mean(dQ)
+      dv[b] = gsc;
+      for (int i = 0; i < A; ++i) dq[b * A + i] -= gsc / (float)A;
+    }
+    a.prio[b] = fabsf(d);
+  }
+  {
+    const float s = wave_sum(contrib);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+  }
+  if (a.q_out != nullptr)
+    for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int i = 0; i < (nth >> 6); ++i) s += red[i];
+    a.loss[0] = s / (float)B;
+  }
+  // ---- 3. head backward (online instance 0 only)
+  const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
+  __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
+  const __bf16* ha0 = a.dueling ? h0 + HID : h0;
+  const float* W0 = a.w[0];
+  for (int t = tid; t < HID * A; t += nth) {            // dW[k][i] = sum_b Ha[b][k] dA[b][i]
+    const int k = t / A, i = t - k * A;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += (float)ha0[(int64_t)b * HH + k] * dq[b * A + i];
+    a.dw[t] = s;
+  }
+  for (int i = tid; i < A; i += nth) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dq[b * A + i];
+    a.db[i] = s;
+  }
+  if (a.dueling) {
+    for (int k = tid; k < HID; k += nth) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += (float)h0[(int64_t)b * HH + k] * dv[b];
+      a.dwv[k] = s;
+    }
+    if (tid == 0) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += dv[b];
+      a.dbv[0] = s;
+    }
+  }
+  // dH[b][k] = (sum_i dA[b][i] W[k][i]) * (H > 0);   dueling value half: dV[b] * wv[k]
+  for (int t = tid; t < B * HH; t += nth) {
+    const int b = t / HH, k = t - b * HH;
+    float s = 0.f;
+    if (a.dueling && k < HID) {
+      s = dv[b] * a.wv[0][k];
+    } else {
+      const int kk = a.dueling ? k - HID : k;
+      for (int i = 0; i < A; ++i) s += dq[b * A + i] * W0[(int64_t)kk * A + i];
+    }
+    const float hval = (float)h0[t];
+    dh[t] = (__bf16)(hval > 0.f ? s : 0.f);
+  }
+}
+
+}  // namespace dqn
+
+using namespace dqn;
+
+// ------------------------------------------------------------------ launchers
+void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs, int max_threads, hipStream_t st) {
+  dim3 grid((max_threads + 255) / 256, njobs);
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, src, reinterpret_cast<__bf16*>(dst), jobs_dev,
+                     (const float*)nullptr);
+}
+
+#define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI)                                                     \
+  do {                                                                                                  \
+    dim3 grid((a.M + WM * MT * 16 - 1) / (WM * MT * 16), (a.N + WN * NT * 16 - 1) / (WN * NT * 16), ninst); \
+    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI>), grid, dim3(256), 0, st, a);         \
+  } while (0)
+
+using NatC1 = ConvLoader<uint8_t, 4, 8, 8, 4>;
+using NatC2 = ConvLoader<__bf16, 32, 4, 4, 2>;
+using NatC3 = ConvLoader<__bf16, 64, 3, 3, 1>;
+using NatD3 = DgradLoader<64, 3, 3, 1>;
+using NatD2 = DgradLoader<64, 4, 4, 2>;
+
+// layer kinds: see dqn_nets_k.h
+int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
+  switch (kind) {
+    // ---- forward, fused bias + ReLU, bf16 NHWC out
+    case L_NAT_CONV1_FWD: IGEMM_LAUNCH(NatC1, 1, 2, 4, 1, 1, 0); return 0;
+    case L_NAT_CONV2_FWD: IGEMM_LAUNCH(NatC2, 1, 4, 4, 1, 1, 0); return 0;
+    case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 2, 2, 2, 1, 0); return 0;
+    case L_DENSE_FWD_RELU: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 4, 0); return 0;
+    case L_DENSE_FWD_F32: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 4, 1); return 0;
+    // ---- backward data, ReLU mask of the layer input
+    case L_DENSE_DGRAD: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 4, 1, 2); return 0;
+    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH(NatD3, 1, 4, 4, 1, 1, 2); return 0;
+    case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH(NatD2, 1, 2, 4, 1, 1, 2); return 0;
+    default: return -1;
+  }
+}
+
+int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st) {
+  const int mchunks = (a.M + g.MC - 1) / g.MC;
+  dim3 grid(mchunks, (a.K + g.KB - 1) / g.KB, (g.N + g.NB - 1) / g.NB);
+  const size_t lds = (size_t)(g.KB + g.NB) * WG_LDSROW * 2 + (size_t)g.NB * 4;
+  switch (kind) {
+    case L_NAT_CONV1_FWD: hipLaunchKernelGGL(wgrad_kernel<NatC1>, grid, dim3(256), lds, st, a, g); return 0;
+    case L_NAT_CONV2_FWD: hipLaunchKernelGGL(wgrad_kernel<NatC2>, grid, dim3(256), lds, st, a, g); return 0;
+    case L_NAT_CONV3_FWD: hipLaunchKernelGGL(wgrad_kernel<NatC3>, grid, dim3(256), lds, st, a, g); return 0;
+    case L_DENSE_FWD_RELU: hipLaunchKernelGGL(wgrad_kernel<DenseLoader>, grid, dim3(256), lds, st, a, g); return 0;
+    default: return -1;
+  }
+}
+
+void launch_head_loss(const HeadArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)(4 * a.B * a.A + a.B + 32) * sizeof(float);
+  hipLaunchKernelGGL(head_loss_kernel, dim3(1), dim3(1024), lds, st, a);
+}

@@ -1,4 +1,99 @@
-// Bindings for the Q-network layer kernels (filled in by csrc/kernels/conv*.hip, dense*.hip).
-#include "include/dqn_nets.h"
+// Bindings for the Q-network kernels (csrc/kernels/qnet.hip).
+//
+// The Python executor (dist_dqn_amd/ops/executor.py) builds a static launch
+// plan once per (architecture, batch): it validates every buffer's shape,
+// dtype and device there, then hands raw device addresses to these entry
+// points, which only assemble the argument structs and launch on the current
+// HIP stream (so the whole step can be captured into one HIP graph).
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
-void register_net_ops(pybind11::module_& m) { (void)m; }
+#include "include/dqn_nets.h"
+#include "include/dqn_nets_k.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+template <typename T>
+T P(int64_t v) { return reinterpret_cast<T>(static_cast<intptr_t>(v)); }
+
+void pack(int64_t src, int64_t dst, int64_t jobs, int64_t njobs, int64_t max_threads) {
+  launch_pack(P<const float*>(src), P<void*>(dst), P<const dqn::PackJob*>(jobs), (int)njobs, (int)max_threads,
+              cur_stream());
+}
+
+dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_t>& w,
+                        const std::vector<int64_t>& bias, const std::vector<int64_t>& out,
+                        const std::vector<int64_t>& mask, const std::vector<double>& scale,
+                        const std::vector<int64_t>& d) {
+  TORCH_CHECK(d.size() == 11, "dims: M, N, K, N16, ldo, IH, IW, OH, OW, pad_t, pad_l");
+  TORCH_CHECK(in.size() >= 1 && in.size() <= 3, "1..3 instances");
+  dqn::ConvArgs a{};
+  for (size_t i = 0; i < in.size(); ++i) {
+    a.in[i] = P<const void*>(in[i]);
+    a.w[i] = i < w.size() ? P<const void*>(w[i]) : nullptr;
+    a.bias[i] = i < bias.size() ? P<const float*>(bias[i]) : nullptr;
+    a.out[i] = i < out.size() ? P<void*>(out[i]) : nullptr;
+    a.mask[i] = i < mask.size() ? P<const void*>(mask[i]) : nullptr;
+    a.scale[i] = i < scale.size() ? (float)scale[i] : 1.f;
+  }
+  a.M = (int)d[0]; a.N = (int)d[1]; a.K = (int)d[2]; a.N16 = (int)d[3]; a.ldo = (int)d[4];
+  a.IH = (int)d[5]; a.IW = (int)d[6]; a.OH = (int)d[7]; a.OW = (int)d[8]; a.pad_t = (int)d[9]; a.pad_l = (int)d[10];
+  return a;
+}
+
+void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_t> bias,
+           std::vector<int64_t> out, std::vector<int64_t> mask, std::vector<double> scale, std::vector<int64_t> dims) {
+  dqn::ConvArgs a = conv_args(in, w, bias, out, mask, scale, dims);
+  TORCH_CHECK(launch_igemm((int)kind, a, (int)in.size(), cur_stream()) == 0, "unknown igemm kind ", kind);
+}
+
+void wgrad(int64_t kind, int64_t in, std::vector<int64_t> dims, int64_t dz, int64_t ldz, int64_t dw, int64_t db,
+           int64_t dw2, int64_t db2, int64_t nsplit, int64_t N, int64_t MC, int64_t KB, int64_t NB, double scale,
+           bool atomic) {
+  dqn::ConvArgs a = conv_args({in}, {}, {}, {}, {}, {1.0}, dims);
+  dqn::WgradArgs g{};
+  g.dz = P<const void*>(dz); g.ldz = (int)ldz;
+  g.dw = P<float*>(dw); g.db = P<float*>(db); g.dw2 = P<float*>(dw2); g.db2 = P<float*>(db2);
+  g.nsplit = (int)nsplit; g.N = (int)N; g.MC = (int)MC; g.KB = (int)KB; g.NB = (int)NB;
+  g.scale = (float)scale; g.atomic = atomic ? 1 : 0;
+  TORCH_CHECK(KB % 16 == 0 && NB % 16 == 0 && MC % 32 == 0, "wgrad tiling");
+  TORCH_CHECK((KB / 16) * (NB / 16) <= 48, "wgrad: at most 48 output tiles per block");
+  TORCH_CHECK(launch_wgrad((int)kind, a, g, cur_stream()) == 0, "unknown wgrad kind ", kind);
+}
+
+void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
+               std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io) {
+  // ints: B, A, HID, dueling, huber, infer ; flts: delta
+  // io: act, rew, done, gam, wts, loss, prio, q_out, dw, db, dwv, dbv, dh
+  TORCH_CHECK(ints.size() == 6 && flts.size() == 1 && io.size() == 13, "head_loss args");
+  dqn::HeadArgs a{};
+  a.B = (int)ints[0]; a.A = (int)ints[1]; a.HID = (int)ints[2]; a.dueling = (int)ints[3]; a.huber = (int)ints[4];
+  a.infer = (int)ints[5];
+  a.delta = (float)flts[0];
+  TORCH_CHECK(a.HID % 8 == 0, "hidden size must be a multiple of 8");
+  for (size_t i = 0; i < 3; ++i) {
+    a.h[i] = i < h.size() ? P<const void*>(h[i]) : nullptr;
+    a.w[i] = i < w.size() ? P<const float*>(w[i]) : nullptr;
+    a.b[i] = i < b.size() ? P<const float*>(b[i]) : nullptr;
+    a.wv[i] = i < wv.size() ? P<const float*>(wv[i]) : nullptr;
+    a.bv[i] = i < bv.size() ? P<const float*>(bv[i]) : nullptr;
+  }
+  a.act = P<const int32_t*>(io[0]); a.rew = P<const float*>(io[1]); a.done = P<const float*>(io[2]);
+  a.gam = P<const float*>(io[3]); a.wts = P<const float*>(io[4]);
+  a.loss = P<float*>(io[5]); a.prio = P<float*>(io[6]); a.q_out = P<float*>(io[7]);
+  a.dw = P<float*>(io[8]); a.db = P<float*>(io[9]); a.dwv = P<float*>(io[10]); a.dbv = P<float*>(io[11]);
+  a.dh = P<void*>(io[12]);
+  launch_head_loss(a, cur_stream());
+}
+
+}  // namespace
+
+void register_net_ops(pybind11::module_& m) {
+  m.def("qnet_pack", &pack);
+  m.def("qnet_igemm", &igemm);
+  m.def("qnet_wgrad", &wgrad);
+  m.def("qnet_head_loss", &head_loss);
+  m.attr("PACK_JOB_INTS") = (int)(sizeof(dqn::PackJob) / sizeof(int));
+}

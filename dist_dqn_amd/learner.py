@@ -81,12 +81,14 @@ class Learner:
             self.replay.update_priorities(self.idx, self.prio, cfg.per_eps)
         if self.tau < 1.0:
             kernels.target_update(self.net.target.flat, self.net.online.flat, self.tau)
+            self.net.sync_target_copy(self.tau)
         else:
             # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).
             # Under sync DP every rank's online params are bit-identical, so the local
             # copy equals the reference's PS-owned target (--disable_target_replication).
             kernels.target_update(self.net.target.flat, self.net.online.flat, 1.0,
                                   self.net.global_step, cfg.target_update_freq)
+            self.net.sync_target_copy(1.0, self.net.global_step, cfg.target_update_freq)
 
     def _eager_step(self):
         self._sample_and_grad()
@@ -134,3 +136,4 @@ class Learner:
     def update_target_now(self):
         """Unconditional target sync (reference `_update_target_network` at init, `dqn_agent.py:50`)."""
         kernels.target_update(self.net.target.flat, self.net.online.flat, 1.0)
+        self.net.sync_target_copy(1.0)

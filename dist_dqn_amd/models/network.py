@@ -111,6 +111,16 @@ class Network:
     def apply_grads(self, grad_scale: float = 1.0):
         # global_step += 1 happens inside the (fused) optimizer step
         self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step)
+        self._repack()
+
+    def _repack(self):
+        if hasattr(self.executor, 'repack'):
+            self.executor.repack(self.online.flat)
+
+    def sync_target_copy(self, tau: float, step: Optional[torch.Tensor] = None, freq: int = 1):
+        """Executor-side refresh after ``target <- online`` (packed bf16 weights)."""
+        if hasattr(self.executor, 'sync_target'):
+            self.executor.sync_target(self.target.flat, self.online.flat, tau, step, freq)
 
     def train_step(self, batch: Dict[str, torch.Tensor], grad_scale: float = 1.0):
         loss, prio = self.compute_grads(batch)
@@ -120,6 +130,7 @@ class Network:
     def update_target(self, tau: Optional[float] = None):
         tau = self.config.target_update_tau if tau is None else tau
         kernels.target_update(self.target.flat, self.online.flat, min(1.0, tau))
+        self.sync_target_copy(min(1.0, tau))
 
     def total_loss(self) -> float:
         """Reference `loss` summary value: TD loss + reg_param * sum 0.5||w||^2."""
@@ -143,3 +154,6 @@ class Network:
         tsd = {k[len('target/'):]: v for k, v in sd.items() if k.startswith('target/')}
         if tsd:
             self.target.load_state_dict(tsd)
+        self._repack()
+        if hasattr(self.executor, 'repack'):
+            self.executor.repack(self.target.flat)

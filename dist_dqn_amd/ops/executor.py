@@ -1,13 +1,324 @@
-"""Fused HIP executor (placeholder until the conv/dense kernels land)."""
+"""Fused HIP executor: the Q-network forward / backward on hand-written
+gfx950 kernels (`csrc/kernels/qnet.hip`), bf16 MFMA with fp32 accumulation
+and fp32 master weights / gradients / optimizer state.
+
+One learner step = (after the replay sample+gather kernels)
+  conv1 fwd | conv2 fwd | conv3 fwd | fc fwd     (online(s), target(s')[, online(s')] as grid.z instances)
+  head+TD-loss+head-backward                     (one workgroup)
+  fc wgrad | fc dgrad | conv3 wgrad | conv3 dgrad | conv2 wgrad | conv2 dgrad | conv1 wgrad
+i.e. 11 kernels for the whole network + loss + gradient (the torch path runs
+~60 kernels for the same work). Weights are re-packed from the fp32 master
+buffer into bf16 MFMA B-fragments once per optimizer step (`repack`), and the
+target's packed copy is refreshed by a predicated copy when the target syncs.
+
+Supported: `nature` convs (84x84x{1..4}... frames packed as 4 uint8
+channels), plain or dueling scalar heads, MSE/Huber, Double DQN, PER weights.
+C51 / noisy heads fall back to the torch executor (`supports()`).
+"""
 from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _ext
+
+_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8)
 
 
 def supports(arch) -> bool:
-    return False
+    if arch.network != 'nature' or arch.distributional or arch.noisy:
+        return False
+    if tuple(arch.input_shape) != (84, 84, 4):
+        return False
+    return True
 
 
-class HipExecutor:  # pragma: no cover
+class _Job:
+    __slots__ = ('src_off', 'K', 'N', 'dst_off', 'dst_N16', 'nt_off', 'ks_off', 'mode', 'p0', 'p1', 'p2')
+
+    def __init__(self, **kw):
+        for k in self.__slots__:
+            setattr(self, k, kw.get(k, 0))
+
+    def ints(self):
+        return [self.src_off, self.K, self.N, self.dst_off, self.dst_N16, self.nt_off, self.ks_off, self.mode,
+                self.p0, self.p1, self.p2, 0]
+
+    def threads(self):
+        if self.mode == 3:
+            return self.K
+        return ((self.K + 31) // 32) * ((self.N + 15) // 16) * 64
+
+
+def _frag_elems(K, N):
+    return ((K + 31) // 32) * ((N + 15) // 16) * 512
+
+
+class HipExecutor:
     name = 'hip'
+    compute_dtype = 'bf16'
 
-    def __init__(self, *a, **k):
-        raise NotImplementedError
+    def __init__(self, arch, layout, dtype: str = 'bf16', input_scale: float = 1.0, loss: str = 'mse',
+                 huber_delta: float = 1.0, double_dqn: bool = False):
+        assert supports(arch), 'HIP executor: unsupported architecture'
+        self.ext = _ext.load(required=True)
+        self.arch, self.layout = arch, layout
+        self.input_scale = float(input_scale)
+        self.huber = loss == 'huber'
+        self.delta = float(huber_delta)
+        self.double = bool(double_dqn)
+        self.A = arch.num_actions
+        self.dueling = arch.dueling
+        fc = arch.value[0] if self.dueling else arch.head[0]
+        self.HID = fc.fout
+        self.HH = 2 * self.HID if self.dueling else self.HID
+        self.FLAT = arch.flat_features
+        self._plan_packing()
+        self._packed: Dict[int, torch.Tensor] = {}
+        self._ws: Dict[Tuple[int, int], dict] = {}
+
+    # ------------------------------------------------------------ packing
+    def _plan_packing(self):
+        lay, arch = self.layout, self.arch
+        off = 0
+        jobs = []
+        self.poff = {}
+
+        def add(key, K, N, entries):
+            nonlocal off
+            self.poff[key] = off
+            N16 = (N + 15) // 16
+            for e in entries:
+                jobs.append(_Job(dst_off=off, dst_N16=N16, **e))
+            off += _frag_elems(K, N)
+            off = (off + 255) // 256 * 256
+
+        for c in arch.convs:
+            K = c.k * c.k * c.cin
+            add(c.name + '/fwd', K, c.cout, [dict(src_off=lay.offsets[c.name + '/w'], K=K, N=c.cout, mode=0)])
+            if c.name != arch.convs[0].name:
+                Kd = c.k * c.k * c.cout
+                add(c.name + '/dgrad', Kd, c.cin,
+                    [dict(src_off=lay.offsets[c.name + '/w'], K=Kd, N=c.cin, mode=1, p0=c.k * c.k, p1=c.cin,
+                          p2=c.cout)])
+        F, H = self.FLAT, self.HID
+        if self.dueling:
+            fcs = [('value/fcl', 0), ('advantage/fcl', H)]
+        else:
+            fcs = [('fcl', 0)]
+        add('fc/fwd', F, self.HH, [dict(src_off=lay.offsets[n + '/w'], K=F, N=H, nt_off=o // 16, mode=0)
+                                    for n, o in fcs])
+        add('fc/dgrad', self.HH, F, [dict(src_off=lay.offsets[n + '/w'], K=H, N=F, ks_off=o // 32, mode=2, p0=H)
+                                      for n, o in fcs])
+        # concatenated fc bias (fp32, 2 bf16 slots per float)
+        self.poff['fc/bias'] = off
+        for n, o in fcs:
+            jobs.append(_Job(src_off=lay.offsets[n + '/b'], K=H, dst_off=off + 2 * o, mode=3))
+        off += 2 * self.HH
+        off = (off + 255) // 256 * 256
+        self.packed_elems = off
+        self.jobs = jobs
+        self._jobs_dev: Dict[torch.device, torch.Tensor] = {}
+        self._max_threads = max(j.threads() for j in jobs)
+
+    def _jobs_on(self, dev):
+        t = self._jobs_dev.get(dev)
+        if t is None:
+            ints = [v for j in self.jobs for v in j.ints()]
+            assert len(ints) == len(self.jobs) * self.ext.PACK_JOB_INTS
+            t = torch.tensor(ints, dtype=torch.int32, device=dev)
+            self._jobs_dev[dev] = t
+        return t
+
+    def packed(self, flat: torch.Tensor) -> torch.Tensor:
+        key = flat.data_ptr()
+        p = self._packed.get(key)
+        if p is None:
+            p = torch.zeros(self.packed_elems, dtype=torch.bfloat16, device=flat.device)
+            self._packed[key] = p
+            self.repack(flat)
+        return p
+
+    def repack(self, flat: torch.Tensor):
+        """fp32 master -> bf16 MFMA fragments (call after every optimizer step / load)."""
+        p = self._packed.get(flat.data_ptr())
+        if p is None:
+            self.packed(flat)
+            return
+        jobs = self._jobs_on(flat.device)
+        self.ext.qnet_pack(flat.data_ptr(), p.data_ptr(), jobs.data_ptr(), len(self.jobs), self._max_threads)
+
+    def sync_target(self, target: torch.Tensor, online: torch.Tensor, tau: float,
+                    step: Optional[torch.Tensor] = None, freq: int = 1):
+        """Refresh the target's packed copy after a target update of the fp32 master."""
+        from . import kernels
+        pt = self.packed(target)
+        if tau >= 1.0:
+            po = self.packed(online)
+            # bit-identical to repacking the copied fp32 weights; same device predicate
+            kernels.target_update(pt.view(torch.float32), po.view(torch.float32), 1.0, step, freq)
+        else:
+            self.repack(target)
+
+    # ---------------------------------------------------------- workspace
+    def _workspace(self, B: int, dev) -> dict:
+        key = (B, dev.index if dev.index is not None else 0)
+        ws = self._ws.get(key)
+        if ws is not None:
+            return ws
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        c1, c2, c3 = self.arch.convs
+        h1, w1 = c1.out_hw
+        h2, w2 = c2.out_hw
+        h3, w3 = c3.out_hw
+        ws = {
+            'x1': torch.zeros(3, B * h1 * w1 * c1.cout, **bf),
+            'x2': torch.zeros(3, B * h2 * w2 * c2.cout, **bf),
+            'x3': torch.zeros(3, B * h3 * w3 * c3.cout, **bf),
+            'h': torch.zeros(3, B * self.HH, **bf),
+            'dh': torch.zeros(B * self.HH, **bf),
+            'dz3': torch.zeros(B * self.FLAT, **bf),
+            'dz2': torch.zeros(B * h2 * w2 * c2.cout, **bf),
+            'dz1': torch.zeros(B * h1 * w1 * c1.cout, **bf),
+            'loss': torch.zeros(1, dtype=torch.float32, device=dev),
+            'prio': torch.zeros(B, dtype=torch.float32, device=dev),
+            'q': torch.zeros(B * self.A, dtype=torch.float32, device=dev),
+            'ones': torch.ones(B, dtype=torch.float32, device=dev),
+        }
+        self._ws[key] = ws
+        return ws
+
+    # ------------------------------------------------------------ forward
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst):
+        """conv1..fc for `ninst` instances; xs: uint8 NHWC inputs; returns nothing (ws['h'])."""
+        ext, lay = self.ext, self.layout
+        c1, c2, c3 = self.arch.convs
+        (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
+        bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
+        pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
+        rows = lambda t, i: t[i].data_ptr()
+        ext.qnet_igemm(_KIND['C1'], [x.data_ptr() for x in xs], pk('conv1/fwd'), bias('conv1/b'),
+                       [rows(ws['x1'], i) for i in range(ninst)], [], [self.input_scale] * ninst,
+                       [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1,
+                        0, 0])
+        ext.qnet_igemm(_KIND['C2'], [rows(ws['x1'], i) for i in range(ninst)], pk('conv2/fwd'), bias('conv2/b'),
+                       [rows(ws['x2'], i) for i in range(ninst)], [], [1.0] * ninst,
+                       [B * h2 * w2, c2.cout, c2.k * c2.k * c2.cin, c2.cout // 16, c2.cout, h1, w1, h2, w2, 0, 0])
+        ext.qnet_igemm(_KIND['C3'], [rows(ws['x2'], i) for i in range(ninst)], pk('conv3/fwd'), bias('conv3/b'),
+                       [rows(ws['x3'], i) for i in range(ninst)], [], [1.0] * ninst,
+                       [B * h3 * w3, c3.cout, c3.k * c3.k * c3.cin, c3.cout // 16, c3.cout, h2, w2, h3, w3, 0, 0])
+        fcb = [p.data_ptr() + 2 * self.poff['fc/bias'] for p in packs]
+        ext.qnet_igemm(_KIND['DFWD'], [rows(ws['x3'], i) for i in range(ninst)], pk('fc/fwd'), fcb,
+                       [rows(ws['h'], i) for i in range(ninst)], [], [1.0] * ninst,
+                       [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0])
+
+    def _head_ptrs(self, flats):
+        lay = self.layout
+        off = lambda f, n: f.data_ptr() + 4 * lay.offsets[n]
+        if self.dueling:
+            w = [off(f, 'advantage/output/w') for f in flats]
+            b = [off(f, 'advantage/output/b') for f in flats]
+            wv = [off(f, 'value/output/w') for f in flats]
+            bv = [off(f, 'value/output/b') for f in flats]
+        else:
+            w = [off(f, 'output/w') for f in flats]
+            b = [off(f, 'output/b') for f in flats]
+            wv, bv = [], []
+        return w, b, wv, bv
+
+    def _check_states(self, x):
+        assert x.dtype == torch.uint8 and x.is_contiguous() and tuple(x.shape[1:]) == (84, 84, 4), \
+            'HIP executor expects uint8 NHWC [B, 84, 84, 4] states, got %s %s' % (x.dtype, tuple(x.shape))
+
+    def forward(self, flat, x, noise=None):
+        return self.q_values(flat, x, noise)
+
+    def q_values(self, flat: torch.Tensor, x: torch.Tensor, noise=None) -> torch.Tensor:
+        x = x.contiguous()
+        self._check_states(x)
+        B = x.shape[0]
+        ws = self._workspace(B, x.device)
+        p = self.packed(flat)
+        self._fwd_trunk([x], [p], [flat], ws, B, 1)
+        w, b, wv, bv = self._head_ptrs([flat])
+        q = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
+        self.ext.qnet_head_loss([B, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],
+                                w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5)
+        return q
+
+    # ----------------------------------------------------------- training
+    def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
+                      grad_out: torch.Tensor, noise=None, noise_target=None):
+        ext, lay = self.ext, self.layout
+        s, ns = batch['states'], batch['next_states']
+        self._check_states(s)
+        self._check_states(ns)
+        B = s.shape[0]
+        assert B <= 1024
+        dev = s.device
+        ws = self._workspace(B, dev)
+        po, pt = self.packed(online), self.packed(target)
+        ninst = 3 if self.double else 2
+        xs = [s, ns, ns][:ninst]
+        packs = [po, pt, po][:ninst]
+        flats = [online, target, online][:ninst]
+        grad_out.zero_()
+        self._fwd_trunk(xs, packs, flats, ws, B, ninst)
+        # ---- fused head + TD loss + head backward
+        w, b, wv, bv = self._head_ptrs(flats)
+        g = lambda n: grad_out.data_ptr() + 4 * lay.offsets[n]
+        if self.dueling:
+            dw, db, dwv, dbv = g('advantage/output/w'), g('advantage/output/b'), g('value/output/w'), \
+                g('value/output/b')
+        else:
+            dw, db, dwv, dbv = g('output/w'), g('output/b'), 0, 0
+        act = batch['actions']
+        assert act.dtype == torch.int32 and act.numel() == B
+        rew, done, gam = (batch['rewards'].contiguous(), batch['dones'].contiguous(),
+                          batch['gammas'].contiguous())
+        wts = batch.get('weights')
+        ext.qnet_head_loss([B, self.A, self.HID, int(self.dueling), int(self.huber), 0], [self.delta],
+                           [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
+                           [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
+                            wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
+                            ws['q'].data_ptr(), dw, db, dwv, dbv, ws['dh'].data_ptr()])
+        # ---- backward (online instance 0 only)
+        c1, c2, c3 = self.arch.convs
+        (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
+        H, HH, F = self.HID, self.HH, self.FLAT
+        pko = lambda key: po.data_ptr() + 2 * self.poff[key]
+        x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
+        if self.dueling:
+            fw, fb, fw2, fb2 = g('value/fcl/w'), g('value/fcl/b'), g('advantage/fcl/w'), g('advantage/fcl/b')
+        else:
+            fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
+        mc_fc = (B + 31) // 32 * 32
+        # fc wgrad: dW[F][HH] = x3^T dh  (one M chunk -> plain stores)
+        ext.qnet_wgrad(_KIND['DFWD'], x3, [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0], ws['dh'].data_ptr(), HH,
+                       fw, fb, fw2, fb2, H, HH, mc_fc, 64, 128, 1.0, False)
+        # fc dgrad: dz3 = (dh W^T) * (x3 > 0)
+        ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()], [x3],
+                       [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
+        # conv3: wgrad (+bias), dgrad -> dz2 masked by x2
+        K3 = c3.k * c3.k * c3.cin
+        ext.qnet_wgrad(_KIND['C3'], x2, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
+                       ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout,
+                       256, 192, 64, 1.0, True)
+        ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [], [ws['dz2'].data_ptr()], [x2],
+                       [1.0], [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3,
+                               0, 0])
+        # conv2: wgrad, dgrad -> dz1 masked by x1
+        K2 = c2.k * c2.k * c2.cin
+        ext.qnet_wgrad(_KIND['C2'], x1, [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0],
+                       ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout, c2.cout,
+                       256, 128, 64, 1.0, True)
+        ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [], [ws['dz1'].data_ptr()], [x1],
+                       [1.0], [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
+                               0, 0])
+        # conv1: wgrad only (input scale folded in)
+        K1 = c1.k * c1.k * c1.cin
+        ext.qnet_wgrad(_KIND['C1'], s.data_ptr(), [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0],
+                       ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout, c1.cout,
+                       512, 128, 32, self.input_scale, True)
+        return ws['loss'], ws['prio']
