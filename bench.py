@@ -10,9 +10,10 @@ uint8 frames, random-init Nature-CNN (VALID convs 32/64/64, FC512, A=6),
 RMSProp (TF semantics), MSE TD loss, target copy every 10k steps — one full
 SGD step per timed step (sample, gather, online+target forward, loss,
 backward, gradient all-reduce over RCCL when N > 1, optimizer, target
-predicate). The device actor (``--actor_envs``, default 1 env x update_freq 4
-frames per SGD step = the reference's 1:4 ratio) runs inside each timed step
-and writes its frames into the same replay.
+predicate). The device actor runs inside each timed step and writes its
+frames into the same replay: ``--actor_envs`` envs x ``update_freq // envs``
+batched eps-greedy steps = update_freq (4) env frames per SGD step, the
+reference's 1:4 acting/learning ratio (`scripts/dqn_params.sh:38`).
 Prints ONE JSON line on rank 0; ``value`` = total SGD steps/s over all ranks.
 """
 from __future__ import annotations
@@ -43,7 +44,7 @@ def main():
     ap.add_argument('--backend', default='auto', choices=['auto', 'hip', 'torch'])
     ap.add_argument('--replay', type=int, default=200000)
     ap.add_argument('--actions', type=int, default=6)
-    ap.add_argument('--actor_envs', type=int, default=1)
+    ap.add_argument('--actor_envs', type=int, default=4)
     ap.add_argument('--update_freq', type=int, default=4)
     ap.add_argument('--graph', type=int, default=1)
     ap.add_argument('--extra', default='', help='extra config flags, e.g. "--dueling --double_dqn"')
@@ -75,7 +76,8 @@ def main():
     actor = None
     if args.actor_envs > 0:
         from dist_dqn_amd.actors.device_actor import DeviceActor
-        actor = DeviceActor(net, replay, cfg, num_envs=args.actor_envs, steps_per_call=args.update_freq,
+        actor = DeviceActor(net, replay, cfg, num_envs=args.actor_envs,
+                            steps_per_call=max(1, args.update_freq // args.actor_envs),
                             seed=1000 + ctx.rank)
 
     def step():
@@ -100,7 +102,7 @@ def main():
     loss = float(learner.loss)
     if ctx.rank == 0:
         sps = args.steps * ctx.world_size / el
-        frames = (args.actor_envs * args.update_freq) * args.steps * ctx.world_size / el
+        frames = (args.actor_envs * max(1, args.update_freq // args.actor_envs)) * args.steps * ctx.world_size / el
         out = {
             'metric': METRIC, 'value': round(sps, 2), 'unit': 'SGD steps/s (all GPUs)',
             'n_gpus': ctx.world_size, 'steps': args.steps, 'warmup': args.warmup,

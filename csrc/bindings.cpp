@@ -32,7 +32,19 @@ void replay_sample_uniform(torch::Tensor size, torch::Tensor rng, torch::Tensor 
 }
 
 void replay_gather_frames(torch::Tensor frames, torch::Tensor state_idx, torch::Tensor next_idx,
-                          torch::Tensor idx, torch::Tensor s, torch::Tensor ns) {
+                          torch::Tensor idx, torch::Tensor s, torch::Tensor ns,
+                          std::vector<torch::Tensor> scal) {
+  // scal: [] or [actions, rewards, dones, gammas (replay columns), a_out, r_out, d_out, g_out]
+  GatherScalars sc{};
+  if (!scal.empty()) {
+    TORCH_CHECK(scal.size() == 8, "scalars: 4 replay columns + 4 outputs");
+    for (auto& t : scal) { CHECK_DEV(t); CHECK_CONTIG(t); }
+    CHECK_DT(scal[0], torch::kInt32); CHECK_DT(scal[4], torch::kInt32);
+    for (int i : {1, 2, 3, 5, 6, 7}) CHECK_DT(scal[i], torch::kFloat32);
+    for (int i = 4; i < 8; ++i) TORCH_CHECK(scal[i].numel() == idx.numel(), "scalar output must be [B]");
+    sc = GatherScalars{ptr<int32_t>(scal[0]), ptr<float>(scal[1]), ptr<float>(scal[2]), ptr<float>(scal[3]),
+                       ptr<int32_t>(scal[4]), ptr<float>(scal[5]), ptr<float>(scal[6]), ptr<float>(scal[7])};
+  }
   CHECK_T(frames, torch::kUInt8); CHECK_T(state_idx, torch::kInt32); CHECK_T(next_idx, torch::kInt32);
   CHECK_T(idx, torch::kInt32); CHECK_T(s, torch::kUInt8); CHECK_T(ns, torch::kUInt8);
   TORCH_CHECK(frames.dim() == 3 && state_idx.dim() == 2, "frames [F,H,W], state_idx [C,k]");
@@ -44,7 +56,7 @@ void replay_gather_frames(torch::Tensor frames, torch::Tensor state_idx, torch::
   TORCH_CHECK(s.numel() == (int64_t)B * HW * K && ns.numel() == s.numel(), "output size mismatch");
   c10::hip::HIPGuardMasqueradingAsCUDA g(frames.device());
   launch_replay_gather_frames(ptr<uint8_t>(frames), ptr<int32_t>(state_idx), ptr<int32_t>(next_idx),
-                              ptr<int32_t>(idx), ptr<uint8_t>(s), ptr<uint8_t>(ns), B, HW, K, cur_stream());
+                              ptr<int32_t>(idx), ptr<uint8_t>(s), ptr<uint8_t>(ns), B, HW, K, sc, cur_stream());
 }
 
 void sumtree_set(torch::Tensor sum, torch::Tensor mn, torch::Tensor maxp, torch::Tensor idx, torch::Tensor td,

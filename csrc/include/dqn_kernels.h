@@ -5,9 +5,13 @@
 #include <stdint.h>
 
 void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, hipStream_t st);
+struct GatherScalars {   // optional per-sample scalar gather (a_out == nullptr: skip)
+  const int32_t* actions; const float* rewards; const float* dones; const float* gammas;
+  int32_t* a_out; float* r_out; float* d_out; float* g_out;
+};
 void launch_replay_gather_frames(const uint8_t* frames, const int32_t* state_idx, const int32_t* next_idx,
                                  const int32_t* idx, uint8_t* s, uint8_t* ns, int B, int HW, int K,
-                                 hipStream_t st);
+                                 const GatherScalars& sc, hipStream_t st);
 void launch_sumtree_set(float* sum, float* mn, float* maxp, const int32_t* idx, const float* td, float alpha,
                         float eps, int use_max, int n, int P, hipStream_t st);
 void launch_sumtree_sample(const float* sum, const float* mn, int64_t* rng, const int32_t* size,

@@ -47,6 +47,9 @@ struct HeadArgs {
   int B, A, HID, dueling, huber, infer;
   float delta;
   const void* h[3];
+  const void* pw[3];         // packed bf16 head fragments (plain output / advantage), [HID/32][N16][64][8]
+  const void* pwv[3];        // packed value-head fragments (dueling, N = 1)
+  int N16;                   // action n-tiles of pw
   const float* w[3]; const float* b[3];
   const float* wv[3]; const float* bv[3];
   const int32_t* act; const float* rew; const float* done; const float* gam; const float* wts;

@@ -162,12 +162,12 @@ struct DenseLoader {
 };
 
 // ============================================================ implicit GEMM
-// Block = 4 waves = WM x WN x KSPLIT; wave tile = (MT*16) x (NT*16).
+// Block = WM x WN x KSPLIT waves (4 or 8); wave tile = (MT*16) x (NT*16).
 // EPI: 0 = scale*acc + bias, ReLU, bf16 out; 1 = scale*acc + bias, fp32 out (no ReLU);
 //      2 = acc * (mask > 0), bf16 out (ReLU backward through the layer input).
 template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI>
-__global__ void __launch_bounds__(256) igemm_kernel(ConvArgs a) {
-  static_assert(WM * WN * KSPLIT == 4, "4 waves per block");
+__global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
+  static_assert(WM * WN * KSPLIT == 4 || WM * WN * KSPLIT == 8, "4 or 8 waves per block");
   __shared__ float red[KSPLIT > 1 ? (KSPLIT - 1) * 64 * MT * NT * 4 : 1];
   const int inst = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -189,7 +189,28 @@ __global__ void __launch_bounds__(256) igemm_kernel(ConvArgs a) {
   for (int i = 0; i < MT; ++i) ld[i] = LD(a, inst, m_base + i * 16 + (lane & 15));
   const int kg = 8 * (lane >> 4);
   const int ks_lo = (K32 * wk) / KSPLIT, ks_hi = (K32 * (wk + 1)) / KSPLIT;
-  for (int ks = ks_lo; ks < ks_hi; ++ks) {
+  // U k-steps per batch: all A/B fragment loads of the batch are issued before
+  // its MFMAs, so U x (MT + NT) global loads are in flight per wave (the loop
+  // is latency-bound at these sizes, not MFMA-bound).
+  constexpr int U = 4;
+  int ks = ks_lo;
+  for (; ks + U <= ks_hi; ks += U) {
+    bfx8 af[U][MT], bf[U][NT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[u][i] = ld[i].frag((ks + u) * 32 + kg);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[u][j] = Bp[((int64_t)(ks + u) * a.N16 + nt_base + j) * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[u][i], bf[u][j], acc[i][j]);
+  }
+  for (; ks < ks_hi; ++ks) {
     bfx8 af[MT], bf[NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) af[i] = ld[i].frag(ks * 32 + kg);
@@ -255,99 +276,92 @@ __global__ void __launch_bounds__(256) igemm_kernel(ConvArgs a) {
 
 // ================================================================ weight grad
 // dW[k][n] (+)= scale * sum_{m in chunk} A[m][k] * dZ[m][n];  db[n] (+)= sum_m dZ[m][n]
-// grid: x = M-chunk, y = K-range (KB), z = N-range (NB). Operands for 32 rows
-// at a time are staged TRANSPOSED in LDS ([k][m], [n][m]) with 40-element
-// rows so each lane's 8 consecutive m are one conflict-free ds_read_b128.
-constexpr int WG_LDSROW = 40;
-constexpr int WG_MAXT = 12;   // output tiles per wave
-
-template <class LD>
+// grid: x = M-chunk (MC rows), y = K-range (KB), z = N-range (NB). ONE staging
+// pass per block: all global loads of the chunk are issued first (register
+// staging), then written TRANSPOSED to LDS ([k][m], [n][m], rows padded by 8
+// elements) so each lane's 8 consecutive m are one ds_read_b128; then
+// (KB/16)x(NB/16) output tiles x MC/32 MFMA k-steps. fp32 atomics only when
+// more than one M-chunk contributes to a weight.
+template <class LD, int MC, int KB, int NB>
 __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
-  extern __shared__ __attribute__((aligned(16))) __bf16 smem[];
-  __bf16* At = smem;                               // [KB][40]
-  __bf16* Zt = smem + g.KB * WG_LDSROW;            // [NB][40]
-  float* bsum = reinterpret_cast<float*>(Zt + g.NB * WG_LDSROW);  // [NB]
+  constexpr int LR = MC + 8;
+  constexpr int TPR = 256 / MC;                  // threads per staged row
+  constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
+  constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
+  static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0, "tiling");
+  __shared__ __attribute__((aligned(16))) __bf16 At[KB * LR];
+  __shared__ __attribute__((aligned(16))) __bf16 Zt[NB * LR];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int k_lo = blockIdx.y * g.KB, n_lo = blockIdx.z * g.NB;
-  const int m_lo = blockIdx.x * g.MC;
-  const int m_hi = min(a.M, m_lo + g.MC);
-  const int KT = g.KB / 16, NTt = g.NB / 16, tiles = KT * NTt;
-  f32x4 acc[WG_MAXT];
+  const int m_lo = blockIdx.x * MC, k_lo = blockIdx.y * KB, n_lo = blockIdx.z * NB;
+  {
+    const int r = threadIdx.x % MC, p = threadIdx.x / MC;
+    const int m = m_lo + r;
+    const bool mok = m < a.M;
+    const __bf16* dz = reinterpret_cast<const __bf16*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
+    LD ld(a, 0, m);
+    bfx8 va[GA], vz[GZ];
 #pragma unroll
-  for (int i = 0; i < WG_MAXT; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = g.db != nullptr && blockIdx.y == 0;
-  for (int t = threadIdx.x; t < g.NB; t += 256) bsum[t] = 0.f;
-  const __bf16* __restrict__ dz = reinterpret_cast<const __bf16*>(g.dz);
-  for (int m0 = m_lo; m0 < m_hi; m0 += 32) {
-    __syncthreads();
-    // stage dZ^T: 32 rows x NB cols (16-byte global loads)
-    for (int t = threadIdx.x; t < 32 * (g.NB / 8); t += 256) {
-      const int r = t / (g.NB / 8), c8 = (t - r * (g.NB / 8)) * 8;
-      const int m = m0 + r;
-      bfx8 v = zero8();
-      if (m < m_hi) v = *reinterpret_cast<const bfx8*>(dz + (int64_t)m * g.ldz + n_lo + c8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Zt[(c8 + j) * WG_LDSROW + r] = v[j];
+    for (int i = 0; i < GA; ++i) {
+      const int k0 = k_lo + (p + i * TPR) * 8;
+      va[i] = k0 < a.K ? ld.frag(k0) : zero8();
     }
-    // stage A^T: 32 rows x KB cols of the (implicit) A operand
-    for (int t = threadIdx.x; t < 32 * (g.KB / 8); t += 256) {
-      const int r = t / (g.KB / 8), c8 = (t - r * (g.KB / 8)) * 8;
-      const int m = m0 + r;
-      bfx8 v = zero8();
-      if (m < m_hi) {
-        LD ld(a, 0, m);
-        v = ld.frag(k_lo + c8);
-      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) At[(c8 + j) * WG_LDSROW + r] = v[j];
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+      vz[i] = (mok && n_lo + c8 < g.N) ? *reinterpret_cast<const bfx8*>(dz + c8) : zero8();
     }
-    __syncthreads();
-    if (do_bias) {
-      for (int n = threadIdx.x; n < g.NB; n += 256) {
-        float s = 0.f;
-        for (int r = 0; r < 32; ++r) s += (float)Zt[n * WG_LDSROW + r];
-        bsum[n] += s;
-      }
-    }
-    const int kg = 8 * (lane >> 4), row = lane & 15;
 #pragma unroll
-    for (int i = 0; i < WG_MAXT; ++i) {
-      const int tile = wave + 4 * i;
-      if (tile < tiles) {
-        const int kt = tile / NTt, nt = tile - kt * NTt;
-        const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * WG_LDSROW + kg);
-        const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * WG_LDSROW + kg);
-        acc[i] = mfma16(af, bf, acc[i]);
+    for (int i = 0; i < GA; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + r] = va[i][j];
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[i][j];
+    }
+  }
+  __syncthreads();
+  const bool atomic = g.atomic != 0;
+  if (g.db != nullptr && blockIdx.y == 0) {
+    for (int n = threadIdx.x; n < NB; n += 256) {
+      float s = 0.f;
+      const __bf16* zr = Zt + n * LR;
+#pragma unroll 8
+      for (int r = 0; r < MC; ++r) s += (float)zr[r];
+      const int nn = n_lo + n;
+      if (nn < g.N) {
+        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        if (atomic) atomicAdd(pdb, s); else *pdb = s;
       }
     }
   }
-  // epilogue: acc tile rows = k (4*(lane>>4)+r), cols = n (lane & 15)
+  const int kg = 8 * (lane >> 4), row = lane & 15;
+  constexpr int NTt = NB / 16;
 #pragma unroll
-  for (int i = 0; i < WG_MAXT; ++i) {
+  for (int i = 0; i < PERW; ++i) {
     const int tile = wave + 4 * i;
-    if (tile < tiles) {
-      const int kt = tile / NTt, nt = tile - kt * NTt;
-      const int n = n_lo + nt * 16 + (lane & 15);
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = k_lo + kt * 16 + 4 * (lane >> 4) + r;
-        if (k < a.K && n < g.N) {
-          float* p = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
-                                  : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
-          const float v = acc[i][r] * g.scale;
-          if (g.atomic) atomicAdd(p, v); else *p = v;
-        }
+    for (int s = 0; s < KSTEPS; ++s) {
+      const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * LR + 32 * s + kg);
+      const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * LR + 32 * s + kg);
+      acc = mfma16(af, bf, acc);
+    }
+    const int n = n_lo + nt * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k_lo + kt * 16 + 4 * (lane >> 4) + r;
+      if (k < a.K && n < g.N) {
+        float* p = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
+                                : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
+        const float v = acc[r] * g.scale;
+        if (atomic) atomicAdd(p, v); else *p = v;
       }
     }
-  }
-  if (do_bias) {
-    __syncthreads();
-    for (int n = threadIdx.x; n < g.NB; n += 256)
-      if (n_lo + n < g.N) {
-        const int nn = n_lo + n;
-        float* p = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
-        if (g.atomic) atomicAdd(p, bsum[n]); else *p = bsum[n];
-      }
   }
 }
 
@@ -355,44 +369,67 @@ __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
 // Instances of the last hidden layer H (bf16): h[0] = online(s), h[1] = target(s'),
 // h[2] = online(s') (Double DQN). Plain: Q = H W + b. Dueling: H = [Hv | Ha],
 // Q = (Hv wv + bv) + (Ha Wa + ba) - mean_a(Ha Wa + ba).
-// Outputs: loss, prio[B], dW/db of the head (fp32, plain stores into the flat grad),
-// dH [B][HH] bf16 masked by ReLU (H > 0), Q of instance 0 (for logging).
+// Q tiles come from MFMA over packed head fragments (16 rows x 16 actions per
+// wave task); the TD loss, dQ and the head backward (dW, db, dH masked by
+// ReLU(H) > 0) follow in the same workgroup.
 __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   const int B = a.B, A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
   float* q = hsm;                           // [3][B][A]
-  float* dq = q + 3 * B * A;                // [B][A]  dL/dQ
+  float* vv = q + 3 * B * A;                // [3][B] dueling value stream
+  float* dq = vv + 3 * B;                   // [B][A]  dL/dQ (dueling: dL/dA)
   float* dv = dq + B * A;                   // [B]     dueling: dL/dV
   float* red = dv + B;                      // [32]
   const int tid = threadIdx.x, nth = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
   const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
-  // ---- 1. Q values (one thread per (inst, b, a) dot product, fp32 accumulate)
-  for (int t = tid; t < ninst * B * A; t += nth) {
-    const int inst = t / (B * A), r = t - inst * B * A, b = r / A, act = r - b * A;
-    const __bf16* h = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)b * HH;
-    const float* W = a.w[inst];              // plain: [HID][A]; dueling: advantage [HID][A]
-    float s = a.b[inst][act];
-    const __bf16* ha = a.dueling ? h + HID : h;
-    for (int k = 0; k < HID; k += 8) {
-      const bfx8 hv = *reinterpret_cast<const bfx8*>(ha + k);
+  // ---- 1. Q tiles on MFMA: task = (instance, 16-row tile)
+  const int mtiles = (B + 15) / 16, K32 = HID / 32;
+  for (int task = wave; task < ninst * mtiles; task += nwave) {
+    const int inst = task / mtiles, mt = task - inst * mtiles;
+    const int b_row = mt * 16 + (lane & 15);
+    const bool rok = b_row < B;
+    const __bf16* hrow = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)(rok ? b_row : 0) * HH;
+    const __bf16* ha = a.dueling ? hrow + HID : hrow;
+    const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
+    const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
+    const int kg = 8 * (lane >> 4);
+    for (int nt = 0; nt < a.N16; ++nt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accv = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < K32; ks += 4) {
+        bfx8 af[4], bf[4], avf[4], bvf[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += (float)hv[j] * W[(int64_t)(k + j) * A + act];
+        for (int u = 0; u < 4; ++u) {
+          af[u] = rok ? *reinterpret_cast<const bfx8*>(ha + (ks + u) * 32 + kg) : zero8();
+          bf[u] = pw[((ks + u) * a.N16 + nt) * 64 + lane];
+          if (a.dueling && nt == 0) {
+            avf[u] = rok ? *reinterpret_cast<const bfx8*>(hrow + (ks + u) * 32 + kg) : zero8();
+            bvf[u] = pv[(ks + u) * 64 + lane];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc = mfma16(af[u], bf[u], acc);
+          if (a.dueling && nt == 0) accv = mfma16(avf[u], bvf[u], accv);
+        }
+      }
+      const int act = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = mt * 16 + 4 * (lane >> 4) + r;
+        if (b < B && act < A) q[(inst * B + b) * A + act] = acc[r] + a.b[inst][act];
+        if (a.dueling && nt == 0 && (lane & 15) == 0 && b < B) vv[inst * B + b] = accv[r] + a.bv[inst][0];
+      }
     }
-    q[t] = s;
   }
   __syncthreads();
   if (a.dueling) {
-    // value stream + mean-subtraction, one thread per (inst, b)
     for (int t = tid; t < ninst * B; t += nth) {
-      const int inst = t / B, b = t - inst * B;
-      const __bf16* hv = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)b * HH;
-      const float* wv = a.wv[inst];
-      float v = a.bv[inst][0];
-      for (int k = 0; k < HID; ++k) v += (float)hv[k] * wv[k];
       float mean = 0.f;
-      for (int i = 0; i < A; ++i) mean += q[(inst * B + b) * A + i];
+      for (int i = 0; i < A; ++i) mean += q[t * A + i];
       mean /= (float)A;
-      for (int i = 0; i < A; ++i) q[(inst * B + b) * A + i] += v - mean;
+      const float v = vv[t];
+      for (int i = 0; i < A; ++i) q[t * A + i] += v - mean;
     }
     __syncthreads();
   }
@@ -434,26 +471,26 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
   }
   {
     const float s = wave_sum(contrib);
-    if ((tid & 63) == 0) red[tid >> 6] = s;
+    if (lane == 0) red[wave] = s;
   }
   if (a.q_out != nullptr)
     for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
   __syncthreads();
   if (tid == 0) {
     float s = 0.f;
-    for (int i = 0; i < (nth >> 6); ++i) s += red[i];
+    for (int i = 0; i < nwave; ++i) s += red[i];
     a.loss[0] = s / (float)B;
   }
-  // ---- 3. head backward (online instance 0 only)
+  // ---- 3. head backward (online instance 0 only); k fastest across threads -> coalesced H
   const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
-  __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
   const __bf16* ha0 = a.dueling ? h0 + HID : h0;
   const float* W0 = a.w[0];
+  __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
   for (int t = tid; t < HID * A; t += nth) {            // dW[k][i] = sum_b Ha[b][k] dA[b][i]
-    const int k = t / A, i = t - k * A;
+    const int i = t / HID, k = t - i * HID;
     float s = 0.f;
     for (int b = 0; b < B; ++b) s += (float)ha0[(int64_t)b * HH + k] * dq[b * A + i];
-    a.dw[t] = s;
+    a.dw[k * A + i] = s;
   }
   for (int i = tid; i < A; i += nth) {
     float s = 0.f;
@@ -501,7 +538,7 @@ void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs
 #define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI)                                                     \
   do {                                                                                                  \
     dim3 grid((a.M + WM * MT * 16 - 1) / (WM * MT * 16), (a.N + WN * NT * 16 - 1) / (WN * NT * 16), ninst); \
-    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI>), grid, dim3(256), 0, st, a);         \
+    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI>), grid, dim3(64 * WM * WN * KS), 0, st, a); \
   } while (0)
 
 using NatC1 = ConvLoader<uint8_t, 4, 8, 8, 4>;
@@ -510,37 +547,42 @@ using NatC3 = ConvLoader<__bf16, 64, 3, 3, 1>;
 using NatD3 = DgradLoader<64, 3, 3, 1>;
 using NatD2 = DgradLoader<64, 4, 4, 2>;
 
-// layer kinds: see dqn_nets_k.h
+// layer kinds: see dqn_nets_k.h.  Tiles: (MT, NT, WM, WN, KSPLIT, EPI)
 int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
   switch (kind) {
     // ---- forward, fused bias + ReLU, bf16 NHWC out
-    case L_NAT_CONV1_FWD: IGEMM_LAUNCH(NatC1, 1, 2, 4, 1, 1, 0); return 0;
-    case L_NAT_CONV2_FWD: IGEMM_LAUNCH(NatC2, 1, 4, 4, 1, 1, 0); return 0;
-    case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 2, 2, 2, 1, 0); return 0;
-    case L_DENSE_FWD_RELU: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 4, 0); return 0;
-    case L_DENSE_FWD_F32: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 4, 1); return 0;
+    case L_NAT_CONV1_FWD: IGEMM_LAUNCH(NatC1, 1, 2, 4, 1, 1, 0); return 0;       // K 256: 8 k-steps
+    case L_NAT_CONV2_FWD: IGEMM_LAUNCH(NatC2, 1, 4, 2, 1, 2, 0); return 0;       // K 512: split-K 2
+    case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 4, 2, 1, 2, 0); return 0;       // K 576: split-K 2
+    case L_DENSE_FWD_RELU: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 8, 0); return 0; // K 3136: split-K 8
+    case L_DENSE_FWD_F32: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 8, 1); return 0;
     // ---- backward data, ReLU mask of the layer input
-    case L_DENSE_DGRAD: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 4, 1, 2); return 0;
-    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH(NatD3, 1, 4, 4, 1, 1, 2); return 0;
-    case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH(NatD2, 1, 2, 4, 1, 1, 2); return 0;
+    case L_DENSE_DGRAD: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 2, 2, 2); return 0;   // K 512-1024
+    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH(NatD3, 1, 4, 2, 1, 2, 2); return 0;
+    case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH(NatD2, 1, 2, 2, 1, 2, 2); return 0;
     default: return -1;
   }
 }
 
+#define WGRAD_LAUNCH(LD, MC, KB, NB)                                                                   \
+  do {                                                                                                 \
+    dim3 grid((a.M + MC - 1) / MC, (a.K + KB - 1) / KB, (g.N + NB - 1) / NB);                          \
+    WgradArgs gg = g;                                                                                  \
+    gg.atomic = grid.x > 1 ? 1 : 0;                                                                    \
+    hipLaunchKernelGGL((wgrad_kernel<LD, MC, KB, NB>), grid, dim3(256), 0, st, a, gg);                 \
+  } while (0)
+
 int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st) {
-  const int mchunks = (a.M + g.MC - 1) / g.MC;
-  dim3 grid(mchunks, (a.K + g.KB - 1) / g.KB, (g.N + g.NB - 1) / g.NB);
-  const size_t lds = (size_t)(g.KB + g.NB) * WG_LDSROW * 2 + (size_t)g.NB * 4;
   switch (kind) {
-    case L_NAT_CONV1_FWD: hipLaunchKernelGGL(wgrad_kernel<NatC1>, grid, dim3(256), lds, st, a, g); return 0;
-    case L_NAT_CONV2_FWD: hipLaunchKernelGGL(wgrad_kernel<NatC2>, grid, dim3(256), lds, st, a, g); return 0;
-    case L_NAT_CONV3_FWD: hipLaunchKernelGGL(wgrad_kernel<NatC3>, grid, dim3(256), lds, st, a, g); return 0;
-    case L_DENSE_FWD_RELU: hipLaunchKernelGGL(wgrad_kernel<DenseLoader>, grid, dim3(256), lds, st, a, g); return 0;
+    case L_NAT_CONV1_FWD: WGRAD_LAUNCH(NatC1, 128, 256, 32); return 0;   // 100 chunks (B=32)
+    case L_NAT_CONV2_FWD: WGRAD_LAUNCH(NatC2, 128, 128, 64); return 0;   // 21 x 4 blocks
+    case L_NAT_CONV3_FWD: WGRAD_LAUNCH(NatC3, 128, 192, 64); return 0;   // 13 x 3 blocks
+    case L_DENSE_FWD_RELU: WGRAD_LAUNCH(DenseLoader, 32, 64, 128); return 0;
     default: return -1;
   }
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(4 * a.B * a.A + a.B + 32) * sizeof(float);
+  const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32) * sizeof(float);
   hipLaunchKernelGGL(head_loss_kernel, dim3(1), dim3(1024), lds, st, a);
 }

@@ -82,10 +82,18 @@ sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ 
 template <int K>
 __global__ void gather_frames_kernel(const uint8_t* __restrict__ frames, const int32_t* __restrict__ state_idx,
                                      const int32_t* __restrict__ next_idx, const int32_t* __restrict__ idx,
-                                     uint8_t* __restrict__ s, uint8_t* __restrict__ ns, int B, int HW) {
+                                     uint8_t* __restrict__ s, uint8_t* __restrict__ ns, int B, int HW,
+                                     GatherScalars sc) {
   // one thread = 4 consecutive pixels of one sample, both stacks
   const int groups = HW / 4;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sc.a_out != nullptr && t < B) {        // per-sample scalars ride along
+    const int tr = idx[t];
+    sc.a_out[t] = sc.actions[tr];
+    sc.r_out[t] = sc.rewards[tr];
+    sc.d_out[t] = sc.dones[tr];
+    sc.g_out[t] = sc.gammas[tr];
+  }
   if (t >= B * groups) return;
   const int b = t / groups, g = t - b * groups;
   const int tr = idx[b];
@@ -135,14 +143,14 @@ void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* ou
 
 void launch_replay_gather_frames(const uint8_t* frames, const int32_t* state_idx, const int32_t* next_idx,
                                  const int32_t* idx, uint8_t* s, uint8_t* ns, int B, int HW, int K,
-                                 hipStream_t st) {
+                                 const GatherScalars& sc, hipStream_t st) {
   const int total = B * (HW / 4);
   dim3 grid((total + 255) / 256), block(256);
   switch (K) {
-    case 1: hipLaunchKernelGGL(gather_frames_kernel<1>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
-    case 2: hipLaunchKernelGGL(gather_frames_kernel<2>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
-    case 3: hipLaunchKernelGGL(gather_frames_kernel<3>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
-    case 4: hipLaunchKernelGGL(gather_frames_kernel<4>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW); break;
+    case 1: hipLaunchKernelGGL(gather_frames_kernel<1>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW, sc); break;
+    case 2: hipLaunchKernelGGL(gather_frames_kernel<2>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW, sc); break;
+    case 3: hipLaunchKernelGGL(gather_frames_kernel<3>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW, sc); break;
+    case 4: hipLaunchKernelGGL(gather_frames_kernel<4>, grid, block, 0, st, frames, state_idx, next_idx, idx, s, ns, B, HW, sc); break;
     default: break;  // host checks K in [1, 4]
   }
 }

@@ -64,10 +64,13 @@ void wgrad(int64_t kind, int64_t in, std::vector<int64_t> dims, int64_t dz, int6
 }
 
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
-               std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io) {
+               std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
+               std::vector<int64_t> pw, std::vector<int64_t> pwv) {
   // ints: B, A, HID, dueling, huber, infer ; flts: delta
   // io: act, rew, done, gam, wts, loss, prio, q_out, dw, db, dwv, dbv, dh
   TORCH_CHECK(ints.size() == 6 && flts.size() == 1 && io.size() == 13, "head_loss args");
+  TORCH_CHECK(ints[1] >= 1 && ints[1] <= 32, "1..32 actions");
+  TORCH_CHECK(ints[2] % 128 == 0, "head hidden size must be a multiple of 128");
   dqn::HeadArgs a{};
   a.B = (int)ints[0]; a.A = (int)ints[1]; a.HID = (int)ints[2]; a.dueling = (int)ints[3]; a.huber = (int)ints[4];
   a.infer = (int)ints[5];
@@ -79,7 +82,10 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
     a.b[i] = i < b.size() ? P<const float*>(b[i]) : nullptr;
     a.wv[i] = i < wv.size() ? P<const float*>(wv[i]) : nullptr;
     a.bv[i] = i < bv.size() ? P<const float*>(bv[i]) : nullptr;
+    a.pw[i] = i < pw.size() ? P<const void*>(pw[i]) : nullptr;
+    a.pwv[i] = i < pwv.size() ? P<const void*>(pwv[i]) : nullptr;
   }
+  a.N16 = (a.A + 15) / 16;
   a.act = P<const int32_t*>(io[0]); a.rew = P<const float*>(io[1]); a.done = P<const float*>(io[2]);
   a.gam = P<const float*>(io[3]); a.wts = P<const float*>(io[4]);
   a.loss = P<float*>(io[5]); a.prio = P<float*>(io[6]); a.q_out = P<float*>(io[7]);

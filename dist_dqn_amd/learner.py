@@ -71,8 +71,9 @@ class Learner:
             batch['weights'] = self.weights
         self.net.reset_noise()
         loss, prio = self.net.compute_grads(batch)
-        self.loss.copy_(loss.view(1))
-        self.prio.copy_(prio.view(-1))
+        # keep references (static buffers under graph capture) instead of copies
+        self.loss = loss.view(1)
+        self.prio = prio.view(-1)
 
     def _apply(self):
         cfg = self.config

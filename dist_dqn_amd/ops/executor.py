@@ -111,6 +111,11 @@ class HipExecutor:
                                     for n, o in fcs])
         add('fc/dgrad', self.HH, F, [dict(src_off=lay.offsets[n + '/w'], K=H, N=F, ks_off=o // 32, mode=2, p0=H)
                                       for n, o in fcs])
+        # head (output layer) fragments for the MFMA Q tiles of the head kernel
+        hw = 'advantage/output/w' if self.dueling else 'output/w'
+        add('head/w', H, self.A, [dict(src_off=lay.offsets[hw], K=H, N=self.A, mode=0)])
+        if self.dueling:
+            add('head/v', H, 1, [dict(src_off=lay.offsets['value/output/w'], K=H, N=1, mode=0)])
         # concatenated fc bias (fp32, 2 bf16 slots per float)
         self.poff['fc/bias'] = off
         for n, o in fcs:
@@ -243,9 +248,15 @@ class HipExecutor:
         self._fwd_trunk([x], [p], [flat], ws, B, 1)
         w, b, wv, bv = self._head_ptrs([flat])
         q = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
+        pw, pwv = self._head_packs([p])
         self.ext.qnet_head_loss([B, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],
-                                w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5)
+                                w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv)
         return q
+
+    def _head_packs(self, packs):
+        pw = [p.data_ptr() + 2 * self.poff['head/w'] for p in packs]
+        pwv = [p.data_ptr() + 2 * self.poff['head/v'] for p in packs] if self.dueling else []
+        return pw, pwv
 
     # ----------------------------------------------------------- training
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
@@ -282,7 +293,7 @@ class HipExecutor:
                            [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
                            [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
                             wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
-                            ws['q'].data_ptr(), dw, db, dwv, dbv, ws['dh'].data_ptr()])
+                            ws['q'].data_ptr(), dw, db, dwv, dbv, ws['dh'].data_ptr()], *self._head_packs(packs))
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw

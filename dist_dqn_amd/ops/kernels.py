@@ -45,16 +45,26 @@ def replay_sample_uniform(size_dev: torch.Tensor, rng_state: torch.Tensor, out: 
 
 
 def replay_gather_frames(frames: torch.Tensor, state_idx: torch.Tensor, next_idx: torch.Tensor,
-                         idx: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Rebuild uint8 NHWC stacks: states [B,H,W,k], next_states [B,H,W,k]."""
+                         idx: torch.Tensor, out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                         scalars: Optional[list] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Rebuild uint8 NHWC stacks: states [B,H,W,k], next_states [B,H,W,k].
+
+    ``scalars`` = [actions, rewards, dones, gammas, a_out, r_out, d_out, g_out]
+    gathers the per-sample columns in the same launch (GPU path)."""
     ext = _hip(frames)
     B, k = idx.numel(), state_idx.shape[1]
     H, W = frames.shape[1], frames.shape[2]
     if ext is not None:
-        s = torch.empty(B, H, W, k, dtype=torch.uint8, device=frames.device)
-        ns = torch.empty_like(s)
-        ext.replay_gather_frames(frames, state_idx, next_idx, idx, s, ns)
+        if out is None:
+            s = torch.empty(B, H, W, k, dtype=torch.uint8, device=frames.device)
+            ns = torch.empty_like(s)
+        else:
+            s, ns = out
+        ext.replay_gather_frames(frames, state_idx, next_idx, idx, s, ns, scalars or [])
         return s, ns
+    if scalars:
+        for src, dst in zip(scalars[:4], scalars[4:]):
+            dst.copy_(src.index_select(0, idx.long()))
     si = state_idx.index_select(0, idx.long()).long()                       # [B, k]
     ni = torch.cat([si[:, 1:], next_idx.index_select(0, idx.long()).long().view(B, 1)], 1)
     s = frames.index_select(0, si.reshape(-1)).view(B, k, H, W).permute(0, 2, 3, 1).contiguous()

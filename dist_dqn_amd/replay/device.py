@@ -223,7 +223,30 @@ class DeviceReplay:
         self.tree.update(idx, td_abs, self.alpha, eps)
 
     def gather(self, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """Materialise a minibatch: states/next_states (uint8 NHWC stacks or f32 vectors)."""
+        """Materialise a minibatch: states/next_states (uint8 NHWC stacks or f32 vectors).
+
+        On the GPU the frame stacks and the per-sample columns come from ONE
+        gather launch into persistent per-batch-size buffers (graph-safe)."""
+        if self.frame_mode and self.device.type == 'cuda':
+            B = idx.numel()
+            buf = self._gather_bufs.get(B) if hasattr(self, '_gather_bufs') else None
+            if buf is None:
+                H, W = self.obs_shape
+                dev = self.device
+                buf = {'states': torch.empty(B, H, W, self.k, dtype=torch.uint8, device=dev),
+                       'next_states': torch.empty(B, H, W, self.k, dtype=torch.uint8, device=dev),
+                       'actions': torch.empty(B, dtype=torch.int32, device=dev),
+                       'rewards': torch.empty(B, dtype=torch.float32, device=dev),
+                       'dones': torch.empty(B, dtype=torch.float32, device=dev),
+                       'gammas': torch.empty(B, dtype=torch.float32, device=dev)}
+                if not hasattr(self, '_gather_bufs'):
+                    self._gather_bufs = {}
+                self._gather_bufs[B] = buf
+            kernels.replay_gather_frames(
+                self.frames, self.state_idx, self.next_idx, idx, (buf['states'], buf['next_states']),
+                [self.actions, self.rewards, self.dones, self.gammas,
+                 buf['actions'], buf['rewards'], buf['dones'], buf['gammas']])
+            return dict(buf)
         out = {
             'actions': self.actions.index_select(0, idx.long()),
             'rewards': self.rewards.index_select(0, idx.long()),

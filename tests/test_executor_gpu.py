@@ -26,7 +26,8 @@ def _setup(extra='', B=32, seed=0):
         'states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
         'next_states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
         'actions': torch.randint(0, 6, (B,), dtype=torch.int32, device=DEV, generator=g),
-        'rewards': torch.randn(B, device=DEV, generator=g),
+        # rewards dominate the TD error so bf16 rounding of Q does not cancel it away
+        'rewards': torch.randn(B, device=DEV, generator=g) * 5.0,
         'dones': (torch.rand(B, device=DEV, generator=g) < 0.2).float(),
         'gammas': torch.full((B,), 0.99, device=DEV),
     }
