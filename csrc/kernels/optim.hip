@@ -133,6 +133,13 @@ static int grid_for(int n4) {
   return g < 1 ? 1 : (g > 2048 ? 2048 : g);
 }
 
+// The optimizer's arrival ticket is one atomic word: keep the grid at one
+// block per CU (grid-stride) so the ticket sees <= 256 arrivals, not ~1.6k.
+static int grid_for_ticket(int n4) {
+  int g = (n4 + 255) / 256;
+  return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
+
 void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
                            int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
                            float grad_scale, int n, hipStream_t st) {
@@ -141,7 +148,7 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
   const int n4 = n / 4;
-  dim3 grid(grid_for(n4)), block(256);
+  dim3 grid(grid_for_ticket(n4)), block(256);
   switch (op) {
     case 0: hipLaunchKernelGGL(optim_kernel<0>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
     case 1: hipLaunchKernelGGL(optim_kernel<1>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;

@@ -168,7 +168,7 @@ struct DenseLoader {
 template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI>
 __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   static_assert(WM * WN * KSPLIT == 4 || WM * WN * KSPLIT == 8, "4 or 8 waves per block");
-  __shared__ float red[KSPLIT > 1 ? (KSPLIT - 1) * 64 * MT * NT * 4 : 1];
+  __shared__ float red[KSPLIT > 1 ? WM * WN * (KSPLIT - 1) * MT * NT * 256 : 1];
   const int inst = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wk = wave % KSPLIT, wn = (wave / KSPLIT) % WN, wm = wave / (KSPLIT * WN);
@@ -467,50 +467,53 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
       dv[b] = gsc;
       for (int i = 0; i < A; ++i) dq[b * A + i] -= gsc / (float)A;
     }
-    a.prio[b] = fabsf(d);
+    if (blockIdx.x == 0) a.prio[b] = fabsf(d);
   }
   {
     const float s = wave_sum(contrib);
     if (lane == 0) red[wave] = s;
   }
-  if (a.q_out != nullptr)
+  if (a.q_out != nullptr && blockIdx.x == 0)
     for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
   __syncthreads();
-  if (tid == 0) {
+  if (tid == 0 && blockIdx.x == 0) {
     float s = 0.f;
     for (int i = 0; i < nwave; ++i) s += red[i];
     a.loss[0] = s / (float)B;
   }
-  // ---- 3. head backward (online instance 0 only); k fastest across threads -> coalesced H
+  // ---- 3. head backward (online instance 0 only), partitioned over the grid's
+  // blocks (phases 1-2 above are recomputed by every block: cheap MFMA work);
+  // k fastest across threads -> coalesced H reads
+  const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
   const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
   const __bf16* ha0 = a.dueling ? h0 + HID : h0;
   const float* W0 = a.w[0];
   __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
-  for (int t = tid; t < HID * A; t += nth) {            // dW[k][i] = sum_b Ha[b][k] dA[b][i]
+  for (int t = gt; t < HID * A; t += gn) {              // dW[k][i] = sum_b Ha[b][k] dA[b][i]
     const int i = t / HID, k = t - i * HID;
     float s = 0.f;
     for (int b = 0; b < B; ++b) s += (float)ha0[(int64_t)b * HH + k] * dq[b * A + i];
     a.dw[k * A + i] = s;
   }
-  for (int i = tid; i < A; i += nth) {
+  for (int i = gt; i < A; i += gn) {
     float s = 0.f;
     for (int b = 0; b < B; ++b) s += dq[b * A + i];
     a.db[i] = s;
   }
   if (a.dueling) {
-    for (int k = tid; k < HID; k += nth) {
+    for (int k = gt; k < HID; k += gn) {
       float s = 0.f;
       for (int b = 0; b < B; ++b) s += (float)h0[(int64_t)b * HH + k] * dv[b];
       a.dwv[k] = s;
     }
-    if (tid == 0) {
+    if (gt == 0) {
       float s = 0.f;
       for (int b = 0; b < B; ++b) s += dv[b];
       a.dbv[0] = s;
     }
   }
   // dH[b][k] = (sum_i dA[b][i] W[k][i]) * (H > 0);   dueling value half: dV[b] * wv[k]
-  for (int t = tid; t < B * HH; t += nth) {
+  for (int t = gt; t < B * HH; t += gn) {
     const int b = t / HH, k = t - b * HH;
     float s = 0.f;
     if (a.dueling && k < HID) {
@@ -584,5 +587,6 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {
   const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32) * sizeof(float);
-  hipLaunchKernelGGL(head_loss_kernel, dim3(1), dim3(1024), lds, st, a);
+  // training: 8 blocks share the backward; acting (infer): one block
+  hipLaunchKernelGGL(head_loss_kernel, dim3(a.infer ? 1 : 8), dim3(1024), lds, st, a);
 }

@@ -166,6 +166,23 @@ class HipExecutor:
         else:
             self.repack(target)
 
+    # ------------------------------------------------------------ streams
+    def _side_stream(self, dev):
+        st = getattr(self, '_side', None)
+        if st is None or st.device != dev:
+            st = torch.cuda.Stream(device=dev)
+            self._side = st
+            self._events = {}
+        return st
+
+    def _event(self, name, stream):
+        ev = self._events.get(name)
+        if ev is None:
+            ev = torch.cuda.Event()
+            self._events[name] = ev
+        ev.record(stream)
+        return ev
+
     # ---------------------------------------------------------- workspace
     def _workspace(self, B: int, dev) -> dict:
         key = (B, dev.index if dev.index is not None else 0)
@@ -274,8 +291,18 @@ class HipExecutor:
         xs = [s, ns, ns][:ninst]
         packs = [po, pt, po][:ninst]
         flats = [online, target, online][:ninst]
-        grad_out.zero_()
+        # Two streams (= two parallel branches of the captured HIP graph):
+        # main: forward -> head -> fc/conv3/conv2 dgrad chain (critical path)
+        # side: grad zeroing (overlaps the forward) and every weight-gradient
+        #       kernel, each gated on the dgrad output it consumes.
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            grad_out.zero_()
+        ev_zero = self._event('zero', side)
         self._fwd_trunk(xs, packs, flats, ws, B, ninst)
+        main.wait_event(ev_zero)
         # ---- fused head + TD loss + head backward
         w, b, wv, bv = self._head_ptrs(flats)
         g = lambda n: grad_out.data_ptr() + 4 * lay.offsets[n]
@@ -305,31 +332,36 @@ class HipExecutor:
         else:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
         mc_fc = (B + 31) // 32 * 32
-        # fc wgrad: dW[F][HH] = x3^T dh  (one M chunk -> plain stores)
-        ext.qnet_wgrad(_KIND['DFWD'], x3, [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0], ws['dh'].data_ptr(), HH,
-                       fw, fb, fw2, fb2, H, HH, mc_fc, 64, 128, 1.0, False)
+        side.wait_event(self._event('head', main))
+        with torch.cuda.stream(side):
+            # fc wgrad: dW[F][HH] = x3^T dh, db = sum dh
+            ext.qnet_wgrad(_KIND['DFWD'], x3, [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0], ws['dh'].data_ptr(), HH,
+                           fw, fb, fw2, fb2, H, HH, mc_fc, 64, 128, 1.0, False)
         # fc dgrad: dz3 = (dh W^T) * (x3 > 0)
         ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()], [x3],
                        [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
-        # conv3: wgrad (+bias), dgrad -> dz2 masked by x2
+        side.wait_event(self._event('dz3', main))
         K3 = c3.k * c3.k * c3.cin
-        ext.qnet_wgrad(_KIND['C3'], x2, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
-                       ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout,
-                       256, 192, 64, 1.0, True)
+        with torch.cuda.stream(side):
+            ext.qnet_wgrad(_KIND['C3'], x2, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
+                           ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout,
+                           128, 192, 64, 1.0, True)
         ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [], [ws['dz2'].data_ptr()], [x2],
                        [1.0], [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3,
                                0, 0])
-        # conv2: wgrad, dgrad -> dz1 masked by x1
+        side.wait_event(self._event('dz2', main))
         K2 = c2.k * c2.k * c2.cin
-        ext.qnet_wgrad(_KIND['C2'], x1, [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0],
-                       ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout, c2.cout,
-                       256, 128, 64, 1.0, True)
+        with torch.cuda.stream(side):
+            ext.qnet_wgrad(_KIND['C2'], x1, [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0],
+                           ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout, c2.cout,
+                           128, 128, 64, 1.0, True)
         ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [], [ws['dz1'].data_ptr()], [x1],
                        [1.0], [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
                                0, 0])
-        # conv1: wgrad only (input scale folded in)
+        # conv1: wgrad only (input scale folded in); last kernel of the step, on main
         K1 = c1.k * c1.k * c1.cin
         ext.qnet_wgrad(_KIND['C1'], s.data_ptr(), [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0],
                        ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout, c1.cout,
-                       512, 128, 32, self.input_scale, True)
+                       128, 256, 32, self.input_scale, True)
+        main.wait_stream(side)
         return ws['loss'], ws['prio']
