@@ -22,13 +22,30 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUD
 template <typename T>
 T* ptr(const torch::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
 
-void replay_sample_uniform(torch::Tensor size, torch::Tensor rng, torch::Tensor out) {
+// [] or [state_idx, next_idx, actions, rewards, dones, gammas, a_out, r_out, d_out, g_out, st_slots, nx_slots]
+SampleOut sample_out(const std::vector<torch::Tensor>& v, int64_t B) {
+  SampleOut so{};
+  if (v.empty()) return so;
+  TORCH_CHECK(v.size() == 12, "sample outputs: 12 tensors");
+  for (auto& t : v) { CHECK_DEV(t); CHECK_CONTIG(t); }
+  for (int i : {0, 1, 2, 6, 10, 11}) CHECK_DT(v[i], torch::kInt32);
+  for (int i : {3, 4, 5, 7, 8, 9}) CHECK_DT(v[i], torch::kFloat32);
+  const int K = (int)v[0].size(1);
+  for (int i = 6; i < 10; ++i) TORCH_CHECK(v[i].numel() == B, "scalar outputs must be [B]");
+  TORCH_CHECK(v[10].numel() == B * K && v[11].numel() == B * K, "slot tables must be [B, K]");
+  so = SampleOut{ptr<int32_t>(v[0]), ptr<int32_t>(v[1]), K, ptr<int32_t>(v[2]), ptr<float>(v[3]),
+                 ptr<float>(v[4]), ptr<float>(v[5]), ptr<int32_t>(v[6]), ptr<float>(v[7]), ptr<float>(v[8]),
+                 ptr<float>(v[9]), ptr<int32_t>(v[10]), ptr<int32_t>(v[11])};
+  return so;
+}
+
+void replay_sample_uniform(torch::Tensor size, torch::Tensor rng, torch::Tensor out, std::vector<torch::Tensor> so) {
   CHECK_T(size, torch::kInt32); CHECK_T(rng, torch::kInt64); CHECK_T(out, torch::kInt32);
   TORCH_CHECK(out.numel() >= 1 && out.numel() <= 1024, "sample batch must be in [1, 1024]");
   TORCH_CHECK(rng.numel() == 2, "rng state must be [seed, counter]");
   c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
   launch_replay_sample_uniform(ptr<int32_t>(size), ptr<int64_t>(rng), ptr<int32_t>(out), (int)out.numel(),
-                               cur_stream());
+                               sample_out(so, out.numel()), cur_stream());
 }
 
 void replay_gather_frames(torch::Tensor frames, torch::Tensor state_idx, torch::Tensor next_idx,
@@ -71,7 +88,7 @@ void sumtree_set(torch::Tensor sum, torch::Tensor mn, torch::Tensor maxp, torch:
 }
 
 void sumtree_sample(torch::Tensor sum, torch::Tensor mn, torch::Tensor rng, torch::Tensor size, torch::Tensor beta,
-                    torch::Tensor idx_out, torch::Tensor w_out, int64_t P) {
+                    torch::Tensor idx_out, torch::Tensor w_out, int64_t P, std::vector<torch::Tensor> so) {
   CHECK_T(sum, torch::kFloat32); CHECK_T(mn, torch::kFloat32); CHECK_T(rng, torch::kInt64);
   CHECK_T(size, torch::kInt32); CHECK_T(beta, torch::kFloat32); CHECK_T(idx_out, torch::kInt32);
   CHECK_T(w_out, torch::kFloat32);
@@ -79,7 +96,8 @@ void sumtree_sample(torch::Tensor sum, torch::Tensor mn, torch::Tensor rng, torc
   TORCH_CHECK(sum.numel() == 2 * P, "tree size must be 2P");
   c10::hip::HIPGuardMasqueradingAsCUDA g(sum.device());
   launch_sumtree_sample(ptr<float>(sum), ptr<float>(mn), ptr<int64_t>(rng), ptr<int32_t>(size), ptr<float>(beta),
-                        ptr<int32_t>(idx_out), ptr<float>(w_out), (int)idx_out.numel(), (int)P, cur_stream());
+                        ptr<int32_t>(idx_out), ptr<float>(w_out), (int)idx_out.numel(), (int)P,
+                        sample_out(so, idx_out.numel()), cur_stream());
 }
 
 void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s0, torch::Tensor s1,
@@ -102,13 +120,22 @@ void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tens
 }
 
 void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tensor step, int64_t freq,
-                   bool use_step) {
+                   bool use_step, std::vector<torch::Tensor> extra) {
   CHECK_T(dst, torch::kFloat32); CHECK_T(src, torch::kFloat32);
   TORCH_CHECK(dst.numel() == src.numel() && dst.numel() % 4 == 0, "target/online size");
   if (use_step) { CHECK_T(step, torch::kInt64); }
   c10::hip::HIPGuardMasqueradingAsCUDA g(dst.device());
+  float* d2 = nullptr;
+  const float* s2 = nullptr;
+  int n2 = 0;
+  if (!extra.empty()) {   // second buffer pair in the same launch (packed bf16 weights, viewed as f32)
+    TORCH_CHECK(extra.size() == 2, "extra = [dst2, src2]");
+    CHECK_T(extra[0], torch::kFloat32); CHECK_T(extra[1], torch::kFloat32);
+    TORCH_CHECK(extra[0].numel() == extra[1].numel() && extra[0].numel() % 4 == 0, "extra pair size");
+    d2 = ptr<float>(extra[0]); s2 = ptr<float>(extra[1]); n2 = (int)extra[0].numel();
+  }
   launch_target_update(ptr<float>(dst), ptr<float>(src), (float)tau, use_step ? ptr<int64_t>(step) : nullptr,
-                       (int)freq, (int)dst.numel(), cur_stream());
+                       (int)freq, (int)dst.numel(), d2, s2, n2, cur_stream());
 }
 
 void td_loss_scalar(torch::Tensor q, torch::Tensor qn_t, c10::optional<torch::Tensor> qn_o, torch::Tensor act,

@@ -4,7 +4,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, hipStream_t st);
+// Optional outputs of the sampling kernels: per-sample scalars and the frame-slot
+// tables of s and s' (so conv1 can read the frame ring directly). st_slots == nullptr: skip.
+struct SampleOut {
+  const int32_t* state_idx; const int32_t* next_idx; int K;
+  const int32_t* actions; const float* rewards; const float* dones; const float* gammas;
+  int32_t* a_out; float* r_out; float* d_out; float* g_out;
+  int32_t* st_slots; int32_t* nx_slots;
+};
+void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, const SampleOut& so,
+                                  hipStream_t st);
 struct GatherScalars {   // optional per-sample scalar gather (a_out == nullptr: skip)
   const int32_t* actions; const float* rewards; const float* dones; const float* gammas;
   int32_t* a_out; float* r_out; float* d_out; float* g_out;
@@ -15,12 +24,13 @@ void launch_replay_gather_frames(const uint8_t* frames, const int32_t* state_idx
 void launch_sumtree_set(float* sum, float* mn, float* maxp, const int32_t* idx, const float* td, float alpha,
                         float eps, int use_max, int n, int P, hipStream_t st);
 void launch_sumtree_sample(const float* sum, const float* mn, int64_t* rng, const int32_t* size,
-                           const float* beta, int32_t* idx_out, float* w_out, int B, int P, hipStream_t st);
+                           const float* beta, int32_t* idx_out, float* w_out, int B, int P, const SampleOut& so,
+                           hipStream_t st);
 void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
                            int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
                            float grad_scale, int n, hipStream_t st);
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
-                          hipStream_t st);
+                          float* dst2, const float* src2, int n2, hipStream_t st);
 void launch_step_bump(int64_t* step, hipStream_t st);
 void launch_td_loss_scalar(const float* q, const float* qn_t, const float* qn_o, const int32_t* act,
                            const float* rew, const float* done, const float* gam, const float* wts,

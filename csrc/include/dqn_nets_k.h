@@ -30,6 +30,8 @@ struct ConvArgs {
   int M, N, K, N16;          // GEMM shape; N16 = n-tiles per k-step of the packed B
   int ldo;                   // output row stride (elements)
   int IH, IW, OH, OW, pad_t, pad_l;
+  const void* frames;        // frame ring [F][H*W] u8 for the frame-slot conv1 loader
+  int frame_hw;
 };
 
 struct WgradArgs {
@@ -41,6 +43,27 @@ struct WgradArgs {
   int MC, KB, NB;            // rows per block, K-range per block, N-range per block
   float scale;
   int atomic;
+};
+
+// Device actor step (eps-greedy + synthetic env + replay append), see actor.hip.
+struct ActorArgs {
+  const float* q;          // [E, A] online Q of the current states
+  uint8_t* frames;         // [F, HW]
+  int32_t* stacks;         // [E, K] frame slots of each env's current state
+  int64_t* cursor;         // [3]: next transition slot, next frame slot, size
+  int32_t* size_dev;       // [1]
+  int32_t* state_idx;      // [C, K]
+  int32_t* next_idx;       // [C]
+  int32_t* actions;        // [C]
+  float* rewards;          // [C]
+  float* dones;            // [C]
+  float* gammas;           // [C]
+  float* eps;              // [3]: eps, eps_min, decay
+  int64_t* rng;            // [2]
+  int32_t* ticket;         // [1]
+  int64_t* frames_done;    // [1] env-frame counter
+  int E, A, K, HW, C, F;
+  float gamma, p_done;
 };
 
 struct HeadArgs {
@@ -56,12 +79,16 @@ struct HeadArgs {
   float* loss; float* prio; float* q_out;
   float* dw; float* db; float* dwv; float* dbv;
   void* dh;
+  float* zero_ptr; int zero_n;   // grad range zeroed in-kernel (conv wgrads accumulate atomically)
+  int has_actor;                 // infer mode: run the fused actor step on the Q tile
+  ActorArgs actor;
 };
 
 enum LayerKind {
   L_NAT_CONV1_FWD = 1, L_NAT_CONV2_FWD = 2, L_NAT_CONV3_FWD = 3,
   L_DENSE_FWD_RELU = 4, L_DENSE_FWD_F32 = 5, L_DENSE_DGRAD = 6,
   L_NAT_CONV3_DGRAD = 7, L_NAT_CONV2_DGRAD = 8,
+  L_NAT_CONV1_FRAMES = 9,   // conv1 reading the frame ring through a [B][4] slot table
 };
 
 }  // namespace dqn

@@ -106,8 +106,14 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 // target <- tau * online + (1 - tau) * target, optionally only when step % freq == 0.
 __global__ void __launch_bounds__(256)
 target_update_kernel(float* __restrict__ dst, const float* __restrict__ src, float tau,
-                     const int64_t* __restrict__ step, int freq, int n4) {
+                     const int64_t* __restrict__ step, int freq, int n4, float* __restrict__ dst2,
+                     const float* __restrict__ src2, int n4b) {
   if (step != nullptr && (step[0] % freq) != 0) return;
+  if (dst2 != nullptr) {   // hard copy of a second buffer pair (packed bf16 weights)
+    float4* D2 = reinterpret_cast<float4*>(dst2);
+    const float4* S2 = reinterpret_cast<const float4*>(src2);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4b; i += gridDim.x * blockDim.x) D2[i] = S2[i];
+  }
   float4* D = reinterpret_cast<float4*>(dst);
   const float4* S = reinterpret_cast<const float4*>(src);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
@@ -162,10 +168,10 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
 }
 
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
-                          hipStream_t st) {
+                          float* dst2, const float* src2, int n2, hipStream_t st) {
   const int n4 = n / 4;
   hipLaunchKernelGGL(target_update_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dst, src, tau, step,
-                     freq < 1 ? 1 : freq, n4);
+                     freq < 1 ? 1 : freq, n4, dst2, src2, n2 / 4);
 }
 
 void launch_step_bump(int64_t* step, hipStream_t st) {

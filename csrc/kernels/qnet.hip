@@ -18,6 +18,7 @@
 //   * head_loss_kernel output layer + dueling combine + TD loss + dQ + head backward
 //                      (dW, db, dH masked by ReLU) in ONE workgroup.
 #include "common.h"
+#include "actor_dev.h"
 #include "../include/dqn_nets_k.h"
 
 namespace dqn {
@@ -115,6 +116,57 @@ struct ConvLoader {
       if (iy < 0 || iy >= IH || ix < 0 || ix >= IW) return zero8();
       return *reinterpret_cast<const bfx8*>(base + ((int64_t)iy * IW + ix) * CIN + ci);
     }
+  }
+};
+
+// conv1 straight from the replay's frame ring: row m = (b, oy, ox), k = (kh, kw, c)
+// with the 4 stacked frames of sample b given by a slot table slots[b][4]
+// (replay state_idx rows / actor stacks). Fuses the frame-stack gather into
+// the first layer: no materialised [B, 84, 84, 4] copy.
+template <int KH, int KW, int S>
+struct FrameLoader {
+  const uint8_t* fb[4];
+  int IH, IW, iy0, ix0;
+  bool ok;
+  DQN_DEV FrameLoader() {}
+  DQN_DEV FrameLoader(const ConvArgs& a, int inst, int m) {
+    const int ohw = a.OH * a.OW;
+    ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / ohw, r = mm - b * ohw, oy = r / a.OW, ox = r - oy * a.OW;
+    IH = a.IH; IW = a.IW;
+    iy0 = oy * S - a.pad_t;
+    ix0 = ox * S - a.pad_l;
+    const int4 sl = reinterpret_cast<const int4*>(a.in[inst])[b];
+    const uint8_t* fr = reinterpret_cast<const uint8_t*>(a.frames);
+    fb[0] = fr + (int64_t)sl.x * a.frame_hw;
+    fb[1] = fr + (int64_t)sl.y * a.frame_hw;
+    fb[2] = fr + (int64_t)sl.z * a.frame_hw;
+    fb[3] = fr + (int64_t)sl.w * a.frame_hw;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    const int kh = k0 / (KW * 4), kw = (k0 - kh * (KW * 4)) / 4;   // k0 % 8 == 0 -> kw even, c = 0
+    const int iy = iy0 + kh, ix = ix0 + kw;
+    bfx8 r = zero8();
+    if (iy < 0 || iy >= IH) return r;
+    const int off = iy * IW + ix;
+    const bool in0 = ix >= 0 && ix < IW, in1 = ix + 1 >= 0 && ix + 1 < IW;
+    if (in0 && in1 && ((off & 1) == 0)) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t v = *reinterpret_cast<const uint16_t*>(fb[c] + off);   // pixels ix, ix+1 of frame c
+        r[c] = (__bf16)(float)(v & 0xffu);
+        r[4 + c] = (__bf16)(float)(v >> 8);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (in0) r[c] = (__bf16)(float)fb[c][off];
+        if (in1) r[4 + c] = (__bf16)(float)fb[c][off + 1];
+      }
+    }
+    return r;
   }
 };
 
@@ -383,6 +435,12 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
   const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  // ---- 0. zero the gradient range the conv wgrads accumulate into (nothing in
+  //         this kernel touches it; saves a separate fill launch)
+  if (a.zero_ptr != nullptr) {
+    float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
+    for (int t = blockIdx.x * nth + tid; t < a.zero_n / 4; t += gridDim.x * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   // ---- 1. Q tiles on MFMA: task = (instance, 16-row tile)
   const int mtiles = (B + 15) / 16, K32 = HID / 32;
   for (int task = wave; task < ninst * mtiles; task += nwave) {
@@ -434,7 +492,9 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
     __syncthreads();
   }
   if (a.infer) {                            // acting: Q of instance 0 only
-    for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
+    if (a.q_out != nullptr)
+      for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
+    if (a.has_actor) actor_step_block(a.actor, q, reinterpret_cast<int*>(red + 32));
     return;
   }
   // ---- 2. TD loss (one thread per sample)
@@ -549,12 +609,14 @@ using NatC2 = ConvLoader<__bf16, 32, 4, 4, 2>;
 using NatC3 = ConvLoader<__bf16, 64, 3, 3, 1>;
 using NatD3 = DgradLoader<64, 3, 3, 1>;
 using NatD2 = DgradLoader<64, 4, 4, 2>;
+using NatF1 = FrameLoader<8, 8, 4>;
 
 // layer kinds: see dqn_nets_k.h.  Tiles: (MT, NT, WM, WN, KSPLIT, EPI)
 int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
   switch (kind) {
     // ---- forward, fused bias + ReLU, bf16 NHWC out
     case L_NAT_CONV1_FWD: IGEMM_LAUNCH(NatC1, 1, 2, 4, 1, 1, 0); return 0;       // K 256: 8 k-steps
+    case L_NAT_CONV1_FRAMES: IGEMM_LAUNCH(NatF1, 1, 2, 4, 1, 1, 0); return 0;
     case L_NAT_CONV2_FWD: IGEMM_LAUNCH(NatC2, 1, 4, 2, 1, 2, 0); return 0;       // K 512: split-K 2
     case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 4, 2, 1, 2, 0); return 0;       // K 576: split-K 2
     case L_DENSE_FWD_RELU: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 8, 0); return 0; // K 3136: split-K 8
@@ -578,6 +640,7 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
 int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st) {
   switch (kind) {
     case L_NAT_CONV1_FWD: WGRAD_LAUNCH(NatC1, 128, 256, 32); return 0;   // 100 chunks (B=32)
+    case L_NAT_CONV1_FRAMES: WGRAD_LAUNCH(NatF1, 128, 256, 32); return 0;
     case L_NAT_CONV2_FWD: WGRAD_LAUNCH(NatC2, 128, 128, 64); return 0;   // 21 x 4 blocks
     case L_NAT_CONV3_FWD: WGRAD_LAUNCH(NatC3, 128, 192, 64); return 0;   // 13 x 3 blocks
     case L_DENSE_FWD_RELU: WGRAD_LAUNCH(DenseLoader, 32, 64, 128); return 0;
@@ -586,7 +649,7 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32) * sizeof(float);
+  const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32 + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
   // training: 8 blocks share the backward; acting (infer): one block
   hipLaunchKernelGGL(head_loss_kernel, dim3(a.infer ? 1 : 8), dim3(1024), lds, st, a);
 }

@@ -11,9 +11,24 @@
 
 namespace dqn {
 
+DQN_DEV void write_sample_outputs(const SampleOut& so, int i, int tr) {
+  if (so.st_slots == nullptr) return;
+  so.a_out[i] = so.actions[tr];
+  so.r_out[i] = so.rewards[tr];
+  so.d_out[i] = so.dones[tr];
+  so.g_out[i] = so.gammas[tr];
+  const int K = so.K;
+  for (int c = 0; c < K; ++c) {
+    const int v = so.state_idx[(int64_t)tr * K + c];
+    so.st_slots[i * K + c] = v;
+    if (c > 0) so.nx_slots[i * K + c - 1] = v;
+  }
+  so.nx_slots[i * K + K - 1] = so.next_idx[tr];
+}
+
 __global__ void __launch_bounds__(1024)
 sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ rng,
-                      int32_t* __restrict__ out, int B) {
+                      int32_t* __restrict__ out, int B, SampleOut so) {
   __shared__ int32_t cand[1024];
   __shared__ int any_dup;
   const int i = threadIdx.x;
@@ -73,7 +88,10 @@ sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ 
     __syncthreads();
     if (i < B) v = cand[i];
   }
-  if (i < B) out[i] = v;
+  if (i < B) {
+    out[i] = v;
+    write_sample_outputs(so, i, v);
+  }
   if (i == 0) rng[1] = (int64_t)(ctr + 1);
 }
 
@@ -137,8 +155,9 @@ __global__ void gather_frames_kernel(const uint8_t* __restrict__ frames, const i
 
 using namespace dqn;
 
-void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, hipStream_t st) {
-  hipLaunchKernelGGL(sample_uniform_kernel, dim3(1), dim3(1024), 0, st, size, rng, out, B);
+void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, const SampleOut& so,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(sample_uniform_kernel, dim3(1), dim3(1024), 0, st, size, rng, out, B, so);
 }
 
 void launch_replay_gather_frames(const uint8_t* frames, const int32_t* state_idx, const int32_t* next_idx,

@@ -52,7 +52,7 @@ sumtree_set_kernel(float* __restrict__ sum, float* __restrict__ mn, float* __res
 __global__ void __launch_bounds__(1024) sumtree_sample_kernel(const float* __restrict__ sum, const float* __restrict__ mn,
                                       int64_t* __restrict__ rng, const int32_t* __restrict__ size_p,
                                       const float* __restrict__ beta_p, int32_t* __restrict__ idx_out,
-                                      float* __restrict__ w_out, int B, int P) {
+                                      float* __restrict__ w_out, int B, int P, SampleOut so) {
   const int i = threadIdx.x;
   const uint64_t seed = (uint64_t)rng[0], ctr = (uint64_t)rng[1];
   if (i < B) {
@@ -74,6 +74,19 @@ __global__ void __launch_bounds__(1024) sumtree_sample_kernel(const float* __res
     const float p = sum[P + leaf] / total;
     const float pmin = mn[1] / total;
     w_out[i] = powf((float)n * p, -beta) / powf((float)n * pmin, -beta);
+    if (so.st_slots != nullptr) {
+      so.a_out[i] = so.actions[leaf];
+      so.r_out[i] = so.rewards[leaf];
+      so.d_out[i] = so.dones[leaf];
+      so.g_out[i] = so.gammas[leaf];
+      const int K = so.K;
+      for (int c = 0; c < K; ++c) {
+        const int v = so.state_idx[(int64_t)leaf * K + c];
+        so.st_slots[i * K + c] = v;
+        if (c > 0) so.nx_slots[i * K + c - 1] = v;
+      }
+      so.nx_slots[i * K + K - 1] = so.next_idx[leaf];
+    }
   }
   __syncthreads();                      // every lane has read the counter
   if (threadIdx.x == 0) rng[1] = (int64_t)(ctr + 1);
@@ -92,8 +105,9 @@ void launch_sumtree_set(float* sum, float* mn, float* maxp, const int32_t* idx, 
 }
 
 void launch_sumtree_sample(const float* sum, const float* mn, int64_t* rng, const int32_t* size,
-                           const float* beta, int32_t* idx_out, float* w_out, int B, int P, hipStream_t st) {
+                           const float* beta, int32_t* idx_out, float* w_out, int B, int P, const SampleOut& so,
+                           hipStream_t st) {
   // one workgroup (host guarantees B <= 1024) so the rng counter update is ordered
   hipLaunchKernelGGL(sumtree_sample_kernel, dim3(1), dim3(1024), 0, st, sum, mn, rng, size, beta,
-                     idx_out, w_out, B, P);
+                     idx_out, w_out, B, P, so);
 }

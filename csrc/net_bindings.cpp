@@ -27,7 +27,7 @@ dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_
                         const std::vector<int64_t>& bias, const std::vector<int64_t>& out,
                         const std::vector<int64_t>& mask, const std::vector<double>& scale,
                         const std::vector<int64_t>& d) {
-  TORCH_CHECK(d.size() == 11, "dims: M, N, K, N16, ldo, IH, IW, OH, OW, pad_t, pad_l");
+  TORCH_CHECK(d.size() == 11 || d.size() == 13, "dims: M, N, K, N16, ldo, IH, IW, OH, OW, pad_t, pad_l[, frames, hw]");
   TORCH_CHECK(in.size() >= 1 && in.size() <= 3, "1..3 instances");
   dqn::ConvArgs a{};
   for (size_t i = 0; i < in.size(); ++i) {
@@ -40,6 +40,7 @@ dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_
   }
   a.M = (int)d[0]; a.N = (int)d[1]; a.K = (int)d[2]; a.N16 = (int)d[3]; a.ldo = (int)d[4];
   a.IH = (int)d[5]; a.IW = (int)d[6]; a.OH = (int)d[7]; a.OW = (int)d[8]; a.pad_t = (int)d[9]; a.pad_l = (int)d[10];
+  if (d.size() == 13) { a.frames = P<const void*>(d[11]); a.frame_hw = (int)d[12]; }
   return a;
 }
 
@@ -65,7 +66,8 @@ void wgrad(int64_t kind, int64_t in, std::vector<int64_t> dims, int64_t dz, int6
 
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
                std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
-               std::vector<int64_t> pw, std::vector<int64_t> pwv) {
+               std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
+               std::vector<int64_t> actor, std::vector<double> actor_f) {
   // ints: B, A, HID, dueling, huber, infer ; flts: delta
   // io: act, rew, done, gam, wts, loss, prio, q_out, dw, db, dwv, dbv, dh
   TORCH_CHECK(ints.size() == 6 && flts.size() == 1 && io.size() == 13, "head_loss args");
@@ -86,6 +88,25 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
     a.pwv[i] = i < pwv.size() ? P<const void*>(pwv[i]) : nullptr;
   }
   a.N16 = (a.A + 15) / 16;
+  if (!zero.empty()) {
+    TORCH_CHECK(zero.size() == 2 && zero[1] % 4 == 0 && zero[0] % 16 == 0, "zero = [ptr (16B aligned), n % 4 == 0]");
+    a.zero_ptr = P<float*>(zero[0]); a.zero_n = (int)zero[1];
+  }
+  if (!actor.empty()) {
+    // actor = 15 pointers (ActorArgs order, q unused) + E, A, K, HW, C, F ; actor_f = gamma, p_done
+    TORCH_CHECK(actor.size() == 21 && actor_f.size() == 2 && a.infer, "fused actor args");
+    dqn::ActorArgs& x = a.actor;
+    x.q = nullptr; x.frames = P<uint8_t*>(actor[1]); x.stacks = P<int32_t*>(actor[2]);
+    x.cursor = P<int64_t*>(actor[3]); x.size_dev = P<int32_t*>(actor[4]); x.state_idx = P<int32_t*>(actor[5]);
+    x.next_idx = P<int32_t*>(actor[6]); x.actions = P<int32_t*>(actor[7]); x.rewards = P<float*>(actor[8]);
+    x.dones = P<float*>(actor[9]); x.gammas = P<float*>(actor[10]); x.eps = P<float*>(actor[11]);
+    x.rng = P<int64_t*>(actor[12]); x.ticket = P<int32_t*>(actor[13]); x.frames_done = P<int64_t*>(actor[14]);
+    x.E = (int)actor[15]; x.A = (int)actor[16]; x.K = (int)actor[17]; x.HW = (int)actor[18]; x.C = (int)actor[19];
+    x.F = (int)actor[20]; x.gamma = (float)actor_f[0]; x.p_done = (float)actor_f[1];
+    TORCH_CHECK(x.E == a.B && x.A == a.A, "actor env batch must be the inference batch");
+    TORCH_CHECK(x.F >= 2 * x.C + x.K, "frame ring must hold 2C + k frames");
+    a.has_actor = 1;
+  }
   a.act = P<const int32_t*>(io[0]); a.rew = P<const float*>(io[1]); a.done = P<const float*>(io[2]);
   a.gam = P<const float*>(io[3]); a.wts = P<const float*>(io[4]);
   a.loss = P<float*>(io[5]); a.prio = P<float*>(io[6]); a.q_out = P<float*>(io[7]);

@@ -53,6 +53,17 @@ class DeviceActor:
 
     def _one(self):
         r = self.replay
+        ex = self.net.executor
+        if getattr(ex, 'consumes_slots', False) and self.E <= 64:
+            # 5 launches: conv1 reads the frame ring through the actors' stacks; the
+            # eps-greedy / env step / replay append run inside the head kernel
+            ptrs = [0] + [t.data_ptr() for t in (r.frames, self.stacks, r.cursor, r.size_dev, r.state_idx,
+                                                   r.next_idx, r.actions, r.rewards, r.dones, r.gammas, self.eps,
+                                                   self.rng, self.ticket, self.frames_done)]
+            ints = [self.E, self.net.arch.num_actions, r.k, r.frames.shape[1] * r.frames.shape[2], r.capacity,
+                    r.num_frames]
+            ex.act_fused(self.net.online.flat, r.frames, self.stacks, ptrs, ints, [self.gamma, self.p_done])
+            return
         self.ext.stack_states(r.frames, self.stacks, self.states)
         q = self.net.q_values(self.states).float().contiguous()
         self.ext.actor_step(q, r.frames, self.stacks, r.cursor, r.size_dev, r.state_idx, r.next_idx, r.actions,

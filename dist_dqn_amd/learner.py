@@ -59,16 +59,25 @@ class Learner:
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
         r = self.replay
-        if getattr(r, 'prioritized', False):
+        per = getattr(r, 'prioritized', False)
+        beta = None
+        if per:
             beta = torch.clamp(self.config.per_beta0 + (1.0 - self.config.per_beta0)
                                * self.net.global_step.float() / max(1, self.config.per_beta_steps),
                                max=1.0)
-            r.sample_prioritized(self.B, beta, self.idx, self.weights)
+        if (getattr(self.net.executor, 'consumes_slots', False) and getattr(r, 'frame_mode', False)
+                and self.device.type == 'cuda'):
+            # one launch: indices + scalars + frame-slot tables; conv1 reads the ring
+            batch = r.sample_slots(self.B, beta)
+            self.idx = batch['idx']
         else:
-            r.sample_indices(self.B, self.idx)
-        batch = r.gather(self.idx)
-        if getattr(r, 'prioritized', False):
-            batch['weights'] = self.weights
+            if per:
+                r.sample_prioritized(self.B, beta, self.idx, self.weights)
+            else:
+                r.sample_indices(self.B, self.idx)
+            batch = r.gather(self.idx)
+            if per:
+                batch['weights'] = self.weights
         self.net.reset_noise()
         loss, prio = self.net.compute_grads(batch)
         # keep references (static buffers under graph capture) instead of copies
@@ -87,9 +96,7 @@ class Learner:
             # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).
             # Under sync DP every rank's online params are bit-identical, so the local
             # copy equals the reference's PS-owned target (--disable_target_replication).
-            kernels.target_update(self.net.target.flat, self.net.online.flat, 1.0,
-                                  self.net.global_step, cfg.target_update_freq)
-            self.net.sync_target_copy(1.0, self.net.global_step, cfg.target_update_freq)
+            self.net.hard_target_update(self.net.global_step, cfg.target_update_freq)
 
     def _eager_step(self):
         self._sample_and_grad()

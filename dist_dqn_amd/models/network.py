@@ -117,6 +117,17 @@ class Network:
         if hasattr(self.executor, 'repack'):
             self.executor.repack(self.online.flat)
 
+    def hard_target_update(self, step: Optional[torch.Tensor] = None, freq: int = 1):
+        """target <- online when step % freq == 0 (device predicate); fp32 master and the
+        executor's packed copy move in ONE launch."""
+        ex = self.executor
+        if hasattr(ex, 'packed'):
+            pt, po = ex.packed(self.target.flat), ex.packed(self.online.flat)
+            kernels.target_update(self.target.flat, self.online.flat, 1.0, step, freq,
+                                  extra=(pt.view(torch.float32), po.view(torch.float32)))
+        else:
+            kernels.target_update(self.target.flat, self.online.flat, 1.0, step, freq)
+
     def sync_target_copy(self, tau: float, step: Optional[torch.Tensor] = None, freq: int = 1):
         """Executor-side refresh after ``target <- online`` (packed bf16 weights)."""
         if hasattr(self.executor, 'sync_target'):

@@ -23,7 +23,7 @@ import torch
 
 from . import _ext
 
-_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8)
+_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9)
 
 
 def supports(arch) -> bool:
@@ -58,6 +58,7 @@ def _frag_elems(K, N):
 class HipExecutor:
     name = 'hip'
     compute_dtype = 'bf16'
+    consumes_slots = True       # conv1 reads the replay frame ring through [B, 4] slot tables
 
     def __init__(self, arch, layout, dtype: str = 'bf16', input_scale: float = 1.0, loss: str = 'mse',
                  huber_delta: float = 1.0, double_dqn: bool = False):
@@ -77,6 +78,8 @@ class HipExecutor:
         self._plan_packing()
         self._packed: Dict[int, torch.Tensor] = {}
         self._ws: Dict[Tuple[int, int], dict] = {}
+        self.two_stream = False
+        self._events = {}
 
     # ------------------------------------------------------------ packing
     def _plan_packing(self):
@@ -212,18 +215,24 @@ class HipExecutor:
         return ws
 
     # ------------------------------------------------------------ forward
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst):
-        """conv1..fc for `ninst` instances; xs: uint8 NHWC inputs; returns nothing (ws['h'])."""
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None):
+        """conv1..fc for `ninst` instances -> ws['h'].
+
+        xs: uint8 NHWC [B, 84, 84, 4] inputs, or (frames given) int32 [B, 4] slot
+        tables into the frame ring ``frames`` [F, 84, 84] (fused gather)."""
         ext, lay = self.ext, self.layout
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
         bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
         pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
         rows = lambda t, i: t[i].data_ptr()
-        ext.qnet_igemm(_KIND['C1'], [x.data_ptr() for x in xs], pk('conv1/fwd'), bias('conv1/b'),
-                       [rows(ws['x1'], i) for i in range(ninst)], [], [self.input_scale] * ninst,
-                       [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1,
-                        0, 0])
+        d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
+        kind1 = _KIND['C1']
+        if frames is not None:
+            d1 += [frames.data_ptr(), 84 * 84]
+            kind1 = _KIND['F1']
+        ext.qnet_igemm(kind1, [x.data_ptr() for x in xs], pk('conv1/fwd'), bias('conv1/b'),
+                       [rows(ws['x1'], i) for i in range(ninst)], [], [self.input_scale] * ninst, d1)
         ext.qnet_igemm(_KIND['C2'], [rows(ws['x1'], i) for i in range(ninst)], pk('conv2/fwd'), bias('conv2/b'),
                        [rows(ws['x2'], i) for i in range(ninst)], [], [1.0] * ninst,
                        [B * h2 * w2, c2.cout, c2.k * c2.k * c2.cin, c2.cout // 16, c2.cout, h1, w1, h2, w2, 0, 0])
@@ -267,8 +276,23 @@ class HipExecutor:
         q = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
         pw, pwv = self._head_packs([p])
         self.ext.qnet_head_loss([B, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],
-                                w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv)
+                                w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv, [], [], [])
         return q
+
+    def act_fused(self, flat: torch.Tensor, frames: torch.Tensor, stacks: torch.Tensor, actor_ptrs, actor_ints,
+                  actor_f, q_out: Optional[torch.Tensor] = None):
+        """Acting step in 5 launches: conv1 (frame ring via the actors' slot stacks) ->
+        conv2 -> conv3 -> fc -> head with the eps-greedy/env/replay-append step fused."""
+        E = stacks.shape[0]
+        assert stacks.dtype == torch.int32 and stacks.is_contiguous() and stacks.shape[1] == 4
+        ws = self._workspace(E, frames.device)
+        p = self.packed(flat)
+        self._fwd_trunk([stacks], [p], [flat], ws, E, 1, frames=frames)
+        w, b, wv, bv = self._head_ptrs([flat])
+        pw, pwv = self._head_packs([p])
+        self.ext.qnet_head_loss([E, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],
+                                w, b, wv, bv, [0] * 7 + [q_out.data_ptr() if q_out is not None else 0] + [0] * 5,
+                                pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f))
 
     def _head_packs(self, packs):
         pw = [p.data_ptr() + 2 * self.poff['head/w'] for p in packs]
@@ -279,9 +303,15 @@ class HipExecutor:
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None):
         ext, lay = self.ext, self.layout
-        s, ns = batch['states'], batch['next_states']
-        self._check_states(s)
-        self._check_states(ns)
+        frames = batch.get('frames')
+        if frames is not None:             # slot batch: conv1 reads the replay frame ring directly
+            s, ns = batch['state_slots'], batch['next_slots']
+            assert s.dtype == torch.int32 and s.shape[1] == 4 and s.is_contiguous() and ns.is_contiguous()
+            assert frames.dtype == torch.uint8 and tuple(frames.shape[1:]) == (84, 84)
+        else:
+            s, ns = batch['states'], batch['next_states']
+            self._check_states(s)
+            self._check_states(ns)
         B = s.shape[0]
         assert B <= 1024
         dev = s.device
@@ -291,18 +321,29 @@ class HipExecutor:
         xs = [s, ns, ns][:ninst]
         packs = [po, pt, po][:ninst]
         flats = [online, target, online][:ninst]
+        # conv weight/bias grads are accumulated with atomics across M-chunks: the head
+        # kernel zeroes that range in-kernel; fc grads are plain stores while B <= 32
+        conv_lo = lay.offsets[self.arch.convs[0].name + '/w']
+        conv_hi = max(lay.offsets[c.name + '/b'] + c.cout for c in self.arch.convs)
+        conv_hi = (conv_hi + 3) // 4 * 4
+        zero_in_head = B <= 32 and not self.two_stream
         # Two streams (= two parallel branches of the captured HIP graph):
         # main: forward -> head -> fc/conv3/conv2 dgrad chain (critical path)
         # side: grad zeroing (overlaps the forward) and every weight-gradient
         #       kernel, each gated on the dgrad output it consumes.
+        # Measured on MI355X: the cross-stream waits cost more than the overlap
+        # gains at B=32 (3.9k vs 4.5k steps/s), so the side branch is off by default.
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            grad_out.zero_()
-        ev_zero = self._event('zero', side)
-        self._fwd_trunk(xs, packs, flats, ws, B, ninst)
-        main.wait_event(ev_zero)
+        side = self._side_stream(dev) if self.two_stream else main
+        if not zero_in_head:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                grad_out.zero_()
+            ev_zero = self._event('zero', side)
+        self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames)
+        if not zero_in_head:
+            main.wait_event(ev_zero)
+        zero = [grad_out.data_ptr() + 4 * conv_lo, conv_hi - conv_lo] if zero_in_head else []
         # ---- fused head + TD loss + head backward
         w, b, wv, bv = self._head_ptrs(flats)
         g = lambda n: grad_out.data_ptr() + 4 * lay.offsets[n]
@@ -320,7 +361,8 @@ class HipExecutor:
                            [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
                            [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
                             wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
-                            ws['q'].data_ptr(), dw, db, dwv, dbv, ws['dh'].data_ptr()], *self._head_packs(packs))
+                            ws['q'].data_ptr(), dw, db, dwv, dbv, ws['dh'].data_ptr()], *self._head_packs(packs),
+                           zero, [], [])
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
@@ -360,8 +402,12 @@ class HipExecutor:
                                0, 0])
         # conv1: wgrad only (input scale folded in); last kernel of the step, on main
         K1 = c1.k * c1.k * c1.cin
-        ext.qnet_wgrad(_KIND['C1'], s.data_ptr(), [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0],
-                       ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout, c1.cout,
-                       128, 256, 32, self.input_scale, True)
+        d1 = [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0]
+        kind1 = _KIND['C1']
+        if frames is not None:
+            d1 += [frames.data_ptr(), 84 * 84]
+            kind1 = _KIND['F1']
+        ext.qnet_wgrad(kind1, s.data_ptr(), d1, ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0,
+                       c1.cout, c1.cout, 128, 256, 32, self.input_scale, True)
         main.wait_stream(side)
         return ws['loss'], ws['prio']

@@ -28,11 +28,16 @@ def _cpu_gen(rng_state: torch.Tensor) -> torch.Generator:
 
 
 # --------------------------------------------------------------- replay ops
-def replay_sample_uniform(size_dev: torch.Tensor, rng_state: torch.Tensor, out: torch.Tensor):
-    """out[i] = distinct uniform indices in [0, size) (without replacement)."""
+def replay_sample_uniform(size_dev: torch.Tensor, rng_state: torch.Tensor, out: torch.Tensor,
+                          sample_out: Optional[list] = None):
+    """out[i] = distinct uniform indices in [0, size) (without replacement).
+
+    ``sample_out`` (GPU): [state_idx, next_idx, actions, rewards, dones, gammas,
+    a_out, r_out, d_out, g_out, st_slots, nx_slots] gathers the per-sample
+    scalars and the frame-slot tables of s / s' in the same launch."""
     ext = _hip(out)
     if ext is not None:
-        ext.replay_sample_uniform(size_dev, rng_state, out)
+        ext.replay_sample_uniform(size_dev, rng_state, out, sample_out or [])
         return out
     n = int(size_dev[0])
     g = _cpu_gen(rng_state)
@@ -98,11 +103,11 @@ def sumtree_set(tree, idx: torch.Tensor, td_abs: Optional[torch.Tensor], alpha: 
         tree.min[nodes] = torch.minimum(tree.min[2 * nodes], tree.min[2 * nodes + 1])
 
 
-def sumtree_sample(tree, rng_state, size_dev, beta, idx_out, w_out):
+def sumtree_sample(tree, rng_state, size_dev, beta, idx_out, w_out, sample_out: Optional[list] = None):
     """Stratified proportional sample + importance weights (max-normalised)."""
     ext = _hip(tree.sum)
     if ext is not None:
-        ext.sumtree_sample(tree.sum, tree.min, rng_state, size_dev, beta, idx_out, w_out, tree.P)
+        ext.sumtree_sample(tree.sum, tree.min, rng_state, size_dev, beta, idx_out, w_out, tree.P, sample_out or [])
         return
     B, P = idx_out.numel(), tree.P
     g = _cpu_gen(rng_state)
@@ -145,13 +150,18 @@ def optimizer_step(opt, param: torch.Tensor, grad: torch.Tensor, grad_scale: flo
 
 # ---------------------------------------------------------- target network
 def target_update(dst: torch.Tensor, src: torch.Tensor, tau: float,
-                  step: Optional[torch.Tensor] = None, freq: int = 1):
-    """dst = tau*src + (1-tau)*dst, executed only when step % freq == 0 (device predicate)."""
+                  step: Optional[torch.Tensor] = None, freq: int = 1, extra: Optional[tuple] = None):
+    """dst = tau*src + (1-tau)*dst, executed only when step % freq == 0 (device predicate).
+
+    ``extra`` = (dst2, src2): a second buffer pair hard-copied in the same launch
+    under the same predicate (the executor's packed bf16 weights)."""
     ext = _hip(dst)
     if ext is not None:
         ext.target_update(dst, src, float(tau), step if step is not None else src, int(freq),
-                          step is not None)
+                          step is not None, list(extra) if extra else [])
         return
+    if extra:
+        target_update(extra[0], extra[1], 1.0, step, freq)
     if step is not None and int(step) % freq != 0:
         return
     if tau >= 1.0:

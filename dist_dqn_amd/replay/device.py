@@ -219,6 +219,37 @@ class DeviceReplay:
         self.tree.sample(self.rng_state, self.size_dev, beta, idx_out, w_out)
         return idx_out, w_out
 
+    def sample_slots(self, batch_size: int, beta: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        """GPU fast path: ONE sampling launch returns indices, per-sample scalars and the
+        frame-slot tables of s and s' ([B, k] int32) — executors that read the frame ring
+        directly (the HIP executor's conv1) never materialise the uint8 stacks."""
+        assert self.frame_mode and self.device.type == 'cuda'
+        B = batch_size
+        if not hasattr(self, '_slot_bufs'):
+            self._slot_bufs = {}
+        buf = self._slot_bufs.get(B)
+        if buf is None:
+            dev = self.device
+            i32 = dict(dtype=torch.int32, device=dev)
+            f32 = dict(dtype=torch.float32, device=dev)
+            buf = {'idx': torch.zeros(B, **i32), 'weights': torch.ones(B, **f32),
+                   'actions': torch.zeros(B, **i32), 'rewards': torch.zeros(B, **f32),
+                   'dones': torch.zeros(B, **f32), 'gammas': torch.zeros(B, **f32),
+                   'state_slots': torch.zeros(B, self.k, **i32), 'next_slots': torch.zeros(B, self.k, **i32)}
+            self._slot_bufs[B] = buf
+        so = [self.state_idx, self.next_idx, self.actions, self.rewards, self.dones, self.gammas,
+              buf['actions'], buf['rewards'], buf['dones'], buf['gammas'], buf['state_slots'], buf['next_slots']]
+        if self.prioritized:
+            assert beta is not None
+            kernels.sumtree_sample(self.tree, self.rng_state, self.size_dev, beta, buf['idx'], buf['weights'], so)
+        else:
+            kernels.replay_sample_uniform(self.size_dev, self.rng_state, buf['idx'], so)
+        out = {k: buf[k] for k in ('idx', 'actions', 'rewards', 'dones', 'gammas', 'state_slots', 'next_slots')}
+        out['frames'] = self.frames
+        if self.prioritized:
+            out['weights'] = buf['weights']
+        return out
+
     def update_priorities(self, idx: torch.Tensor, td_abs: torch.Tensor, eps: float = 1e-6):
         self.tree.update(idx, td_abs, self.alpha, eps)
 
