@@ -1,0 +1,107 @@
+"""Data parallelism without a cluster: gloo process groups on the CPU (world 2-3).
+
+Replaces the reference's localhost PS/worker emulation (scripts/dqn_multi_gpu.sh)
+with torch.distributed ranks; checks the sync-DP invariants the RCCL path relies on:
+averaged gradients equal the big-batch gradient, replicas stay bit-identical,
+the chief's parameters reach every rank, and the reference cluster flags map to ranks.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(seed, B=6):
+    g = torch.Generator().manual_seed(seed)
+    return {'states': torch.randn(B, 4, generator=g), 'next_states': torch.randn(B, 4, generator=g),
+            'actions': torch.randint(0, 2, (B,), generator=g), 'rewards': torch.randn(B, generator=g),
+            'dones': (torch.rand(B, generator=g) < 0.3).float(), 'gammas': torch.full((B,), 0.9)}
+
+
+def _worker_grads(rank, world, port, tmpdir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import GradAllReducer, broadcast_flat, check_replicas_equal, init_distributed
+    cfg = parse_args(['--device=cpu', '--seed=%d' % (100 + rank), '--optimizer=rmsprop', '--lr=0.01'])
+    ctx = init_distributed(cfg, device='cpu')
+    assert ctx.world_size == world and ctx.rank == rank and ctx.backend == 'gloo'
+    net = Network.create_network(cfg, (4,), 2)
+    broadcast_flat(ctx, net.online.flat)          # chief init reaches every rank (reference M8)
+    net.target.copy_from(net.online)
+    assert check_replicas_equal(ctx, net.online.flat)
+    red = GradAllReducer(ctx, net.grad, bucket_mb=0.0005)   # force several buckets
+    assert len(red.buckets) > 1
+    for step in range(3):
+        net.compute_grads(_batch(1000 * step + rank))
+        red.allreduce()
+        g_avg = net.grad * red.scale
+        # reference: one process computing the gradient over the union of the batches
+        if rank == 0:
+            ref = Network.create_network(cfg, (4,), 2)
+            ref.online.flat.copy_(net.online.flat)
+            ref.target.flat.copy_(net.target.flat)
+            big = {k: torch.cat([_batch(1000 * step + r)[k] for r in range(world)]) for k in _batch(0)}
+            ref.compute_grads(big)
+            torch.testing.assert_close(g_avg, ref.grad, rtol=1e-5, atol=1e-7)
+        net.apply_grads(red.scale)
+        assert check_replicas_equal(ctx, net.online.flat)
+    assert int(net.global_step) == 3
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_dp_grads_equal_big_batch_and_replicas_stay_equal(tmp_path, world):
+    mp.spawn(_worker_grads, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+
+
+def _worker_learner(rank, world, port, tmpdir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import numpy as np
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import broadcast_flat, check_replicas_equal, init_distributed
+    from dist_dqn_amd.replay import DeviceReplay
+    cfg = parse_args(['--device=cpu', '--seed=5', '--network=cnn', '--optimizer=rmsprop', '--minibatch_size=4',
+                      '--target_update_freq=2', '--replay_memory_capacity=64'])
+    ctx = init_distributed(cfg, device='cpu')
+    net = Network.create_network(cfg, (84, 84, 4), 6)
+    broadcast_flat(ctx, net.online.flat)
+    net.target.copy_from(net.online)
+    rep = DeviceReplay(64, (84, 84), 4, device='cpu', seed=rank)
+    rep.fill_synthetic(64, 6, seed=rank, episode_len=16)    # different data per rank
+    ln = Learner(net, rep, cfg, ctx)
+    for _ in range(4):
+        ln.step()
+    assert check_replicas_equal(ctx, net.online.flat)
+    assert check_replicas_equal(ctx, net.target.flat)
+    assert int(net.global_step) == 4 and ln.train_steps == 4
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_learner_cnn_world2(tmp_path):
+    mp.spawn(_worker_learner, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def test_reference_cluster_flags_map_to_ranks(monkeypatch):
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.parallel.dist import _from_cluster_flags
+    cfg = parse_args(['--worker_hosts=localhost:8090,localhost:8091,localhost:8092', '--task_id=2',
+                      '--gpu_id=3'])
+    m = _from_cluster_flags(cfg)
+    assert m == dict(rank=2, world=3, addr='127.0.0.1', port='8090', local_rank=3)
+    assert _from_cluster_flags(parse_args([])) is None
