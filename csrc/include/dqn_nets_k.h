@@ -84,6 +84,17 @@ struct HeadArgs {
   ActorArgs actor;
 };
 
+// Fused per-sample Nature trunk (trunk.hip): conv1 -> conv2 -> conv3 in one launch.
+struct TrunkArgs {
+  const uint8_t* frames;           // frame ring [F][84*84] (slot path)
+  const int32_t* slots[3];         // [B][4] frame slots per instance (or nullptr -> states)
+  const uint8_t* states[3];        // [B][84][84][4] NHWC stacks per instance (materialised path)
+  const void* w1[3]; const void* w2[3]; const void* w3[3];   // packed bf16 fragments
+  const float* b1[3]; const float* b2[3]; const float* b3[3];
+  __bf16* x1[3]; __bf16* x2[3]; __bf16* x3[3];               // activations out ([B][...] NHWC)
+  float scale;                     // input scale folded into conv1
+};
+
 enum LayerKind {
   L_NAT_CONV1_FWD = 1, L_NAT_CONV2_FWD = 2, L_NAT_CONV3_FWD = 3,
   L_DENSE_FWD_RELU = 4, L_DENSE_FWD_F32 = 5, L_DENSE_DGRAD = 6,
@@ -98,3 +109,4 @@ void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int 
 int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
+void launch_trunk_fwd(const dqn::TrunkArgs& a, int B, int ninst, hipStream_t st);

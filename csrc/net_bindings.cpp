@@ -115,9 +115,30 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
   launch_head_loss(a, cur_stream());
 }
 
+// ptrs per instance (3 entries each, 0 = absent): slots, states, w1, w2, w3, b1, b2, b3, x1, x2, x3
+void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale) {
+  TORCH_CHECK(ptrs.size() == 33 && ninst >= 1 && ninst <= 3 && B >= 1, "trunk args");
+  dqn::TrunkArgs a{};
+  a.frames = P<const uint8_t*>(frames);
+  for (int i = 0; i < 3; ++i) {
+    a.slots[i] = P<const int32_t*>(ptrs[0 + i]);
+    a.states[i] = P<const uint8_t*>(ptrs[3 + i]);
+    a.w1[i] = P<const void*>(ptrs[6 + i]); a.w2[i] = P<const void*>(ptrs[9 + i]); a.w3[i] = P<const void*>(ptrs[12 + i]);
+    a.b1[i] = P<const float*>(ptrs[15 + i]); a.b2[i] = P<const float*>(ptrs[18 + i]); a.b3[i] = P<const float*>(ptrs[21 + i]);
+    a.x1[i] = P<__bf16*>(ptrs[24 + i]); a.x2[i] = P<__bf16*>(ptrs[27 + i]); a.x3[i] = P<__bf16*>(ptrs[30 + i]);
+    if (i < ninst) {
+      TORCH_CHECK((a.slots[i] != nullptr && a.frames != nullptr) || a.states[i] != nullptr, "trunk input");
+      TORCH_CHECK(a.w1[i] && a.w2[i] && a.w3[i] && a.b1[i] && a.b2[i] && a.b3[i] && a.x3[i], "trunk weights/out");
+    }
+  }
+  a.scale = (float)scale;
+  launch_trunk_fwd(a, (int)B, (int)ninst, cur_stream());
+}
+
 }  // namespace
 
 void register_net_ops(pybind11::module_& m) {
+  m.def("qnet_trunk", &trunk);
   m.def("qnet_pack", &pack);
   m.def("qnet_igemm", &igemm);
   m.def("qnet_wgrad", &wgrad);

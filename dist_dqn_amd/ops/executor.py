@@ -79,6 +79,7 @@ class HipExecutor:
         self._packed: Dict[int, torch.Tensor] = {}
         self._ws: Dict[Tuple[int, int], dict] = {}
         self.two_stream = False
+        self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -215,7 +216,7 @@ class HipExecutor:
         return ws
 
     # ------------------------------------------------------------ forward
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None):
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True):
         """conv1..fc for `ninst` instances -> ws['h'].
 
         xs: uint8 NHWC [B, 84, 84, 4] inputs, or (frames given) int32 [B, 4] slot
@@ -226,6 +227,19 @@ class HipExecutor:
         bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
         pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
         rows = lambda t, i: t[i].data_ptr()
+        if self.fused_trunk:
+            # ONE launch for conv1..conv3: a workgroup per (sample, instance), activations in LDS
+            pad = lambda v: list(v) + [0] * (3 - len(v))
+            slots = [x.data_ptr() for x in xs] if frames is not None else []
+            states = [] if frames is not None else [x.data_ptr() for x in xs]
+            ptrs = (pad(slots) + pad(states) + pad(pk('conv1/fwd')) + pad(pk('conv2/fwd')) + pad(pk('conv3/fwd'))
+                    + pad(bias('conv1/b')) + pad(bias('conv2/b')) + pad(bias('conv3/b'))
+                    # only the online(s) instance feeds the backward: the others skip x1/x2
+                    + pad([rows(ws['x1'], 0)] if keep_acts else []) + pad([rows(ws['x2'], 0)] if keep_acts else [])
+                    + pad([rows(ws['x3'], i) for i in range(ninst)]))
+            ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale)
+            self._fc_fwd(packs, ws, B, ninst)
+            return
         d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
         kind1 = _KIND['C1']
         if frames is not None:
@@ -239,10 +253,14 @@ class HipExecutor:
         ext.qnet_igemm(_KIND['C3'], [rows(ws['x2'], i) for i in range(ninst)], pk('conv3/fwd'), bias('conv3/b'),
                        [rows(ws['x3'], i) for i in range(ninst)], [], [1.0] * ninst,
                        [B * h3 * w3, c3.cout, c3.k * c3.k * c3.cin, c3.cout // 16, c3.cout, h2, w2, h3, w3, 0, 0])
+        self._fc_fwd(packs, ws, B, ninst)
+
+    def _fc_fwd(self, packs, ws, B, ninst):
         fcb = [p.data_ptr() + 2 * self.poff['fc/bias'] for p in packs]
-        ext.qnet_igemm(_KIND['DFWD'], [rows(ws['x3'], i) for i in range(ninst)], pk('fc/fwd'), fcb,
-                       [rows(ws['h'], i) for i in range(ninst)], [], [1.0] * ninst,
-                       [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0])
+        self.ext.qnet_igemm(_KIND['DFWD'], [ws['x3'][i].data_ptr() for i in range(ninst)],
+                            [p.data_ptr() + 2 * self.poff['fc/fwd'] for p in packs], fcb,
+                            [ws['h'][i].data_ptr() for i in range(ninst)], [], [1.0] * ninst,
+                            [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0])
 
     def _head_ptrs(self, flats):
         lay = self.layout
@@ -271,7 +289,7 @@ class HipExecutor:
         B = x.shape[0]
         ws = self._workspace(B, x.device)
         p = self.packed(flat)
-        self._fwd_trunk([x], [p], [flat], ws, B, 1)
+        self._fwd_trunk([x], [p], [flat], ws, B, 1, keep_acts=False)
         w, b, wv, bv = self._head_ptrs([flat])
         q = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
         pw, pwv = self._head_packs([p])
@@ -287,7 +305,7 @@ class HipExecutor:
         assert stacks.dtype == torch.int32 and stacks.is_contiguous() and stacks.shape[1] == 4
         ws = self._workspace(E, frames.device)
         p = self.packed(flat)
-        self._fwd_trunk([stacks], [p], [flat], ws, E, 1, frames=frames)
+        self._fwd_trunk([stacks], [p], [flat], ws, E, 1, frames=frames, keep_acts=False)
         w, b, wv, bv = self._head_ptrs([flat])
         pw, pwv = self._head_packs([p])
         self.ext.qnet_head_loss([E, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],

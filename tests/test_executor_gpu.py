@@ -90,3 +90,38 @@ def test_learner_step_graph_equals_eager():
         assert int(net.global_step) == 6
     # wgrad combines M-chunks with fp32 atomics (order-dependent last bits)
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('slots', [False, True])
+def test_fused_trunk_matches_layerwise(slots):
+    """trunk.hip (conv1..conv3 in one launch, activations in LDS) == the three
+    layer-wise implicit-GEMM launches, from NHWC stacks and from frame-ring slots."""
+    net, _, batch = _setup('', 16)
+    ex = net.executor
+    B = 16
+    g = torch.Generator(device=DEV).manual_seed(7)
+    frames = torch.randint(0, 256, (40, 84, 84), dtype=torch.uint8, device=DEV, generator=g)
+    sl = torch.randint(0, 40, (B, 4), dtype=torch.int32, device=DEV, generator=g)
+    x = batch['states'] if not slots else sl
+    fr = frames if slots else None
+    p, f = ex.packed(net.online.flat), net.online.flat
+    ws = ex._workspace(B, DEV)
+    outs = []
+    for fused in (False, True):
+        ex.fused_trunk = fused
+        for k in ('x1', 'x2', 'x3', 'h'):
+            ws[k].zero_()
+        ex._fwd_trunk([x, x], [p, p], [f, f], ws, B, 2, frames=fr)
+        torch.cuda.synchronize()
+        outs.append({k: ws[k][:2].clone() for k in ('x1', 'x2', 'x3', 'h')})
+    ex.fused_trunk = True
+    for k in ('x1', 'x2'):     # only the online instance keeps x1 / x2
+        torch.testing.assert_close(outs[1][k][0].float(), outs[0][k][0].float(), rtol=2e-2, atol=2e-2)
+    for k in ('x3', 'h'):
+        for i in range(2):
+            assert _rel(outs[1][k][i], outs[0][k][i]) < 1e-2, (k, i)
+    if slots:    # the slot path sees the same pixels as a materialised NHWC stack
+        st = frames[sl.long()].permute(0, 2, 3, 1).contiguous()
+        ex._fwd_trunk([st], [p], [f], ws, B, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(ws['x3'][0], outs[1]['x3'][0])
