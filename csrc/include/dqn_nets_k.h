@@ -93,6 +93,7 @@ struct TrunkArgs {
   const float* b1[3]; const float* b2[3]; const float* b3[3];
   __bf16* x1[3]; __bf16* x2[3]; __bf16* x3[3];               // activations out ([B][...] NHWC)
   float scale;                     // input scale folded into conv1
+  int64_t* prof;                   // optional [ninst][B][8] s_memtime phase stamps (profiling)
 };
 
 enum LayerKind {

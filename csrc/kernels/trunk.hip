@@ -38,184 +38,262 @@ DQN_DEV bfx8 tz8() {
   return z;
 }
 
+DQN_DEV f32x4 f4(const float4& v) { return f32x4{v.x, v.y, v.z, v.w}; }
+
+// ReLU + 4 floats -> 4 packed bf16 (8 bytes)
+DQN_DEV uint2 pack4(const f32x4& v) {
+  const __bf16 a = (__bf16)fmaxf(v[0], 0.f), b = (__bf16)fmaxf(v[1], 0.f);
+  const __bf16 c = (__bf16)fmaxf(v[2], 0.f), d = (__bf16)fmaxf(v[3], 0.f);
+  return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16),
+                    (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16));
+}
+
 DQN_DEV f32x4 tmfma(const bfx8& a, const bfx8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// conv1 A fragment for output pixel p (row of the GEMM), k0 = 8-aligned K index
-// (kh, kw..kw+1, 4 frames). fb[c] = base of frame c of this sample (slot path)
-// or nullptr with `nhwc` = the sample's [84][84][4] stack.
-DQN_DEV bfx8 conv1_frag(const uint8_t* const* fb, const uint8_t* nhwc, int p, int k0) {
-  using namespace trunk;
-  if (p >= R1) return tz8();
-  const int oy = p / O1, ox = p - oy * O1;
-  const int kh = k0 >> 5, kw = (k0 & 31) >> 2;
-  const int off = (oy * 4 + kh) * IW + ox * 4 + kw;     // pixel ix (even), ix + 1
-  bfx8 r;
-  if (nhwc != nullptr) {
-    const uint2 v = *reinterpret_cast<const uint2*>(nhwc + (int64_t)off * 4);
+// 4 pixels x 4 channels (one uint32 per channel plane, or one uint4 NHWC word
+// group) -> 4 NHWC bf16 pixels (32 B) in LDS.
+DQN_DEV uint32_t bfpair(uint32_t a, uint32_t b) {   // two integers 0..255 -> packed bf16 (exact)
+  const __bf16 x = (__bf16)(float)a, y = (__bf16)(float)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+
+DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, __bf16* dst) {
+  uint32_t o[8];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      r[c] = (__bf16)(float)((v.x >> (8 * c)) & 0xffu);
-      r[4 + c] = (__bf16)(float)((v.y >> (8 * c)) & 0xffu);
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint32_t v = *reinterpret_cast<const uint16_t*>(fb[c] + off);
-      r[c] = (__bf16)(float)(v & 0xffu);
-      r[4 + c] = (__bf16)(float)(v >> 8);
-    }
+  for (int i = 0; i < 4; ++i) {
+    const int sh = 8 * i;
+    o[2 * i] = bfpair((c0 >> sh) & 0xffu, (c1 >> sh) & 0xffu);
+    o[2 * i + 1] = bfpair((c2 >> sh) & 0xffu, (c3 >> sh) & 0xffu);
   }
-  return r;
+  reinterpret_cast<uint4*>(dst)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+  reinterpret_cast<uint4*>(dst)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// K-split partial-sum exchange: waves of k-half 1 park their fp32 accumulators
+// in LDS, waves of k-half 0 add them after the barrier.
+DQN_DEV void park(float* red, int slot, int lane, const f32x4& acc) {
+  reinterpret_cast<f32x4*>(red)[slot * 64 + lane] = acc;
+}
+DQN_DEV f32x4 unpark(const float* red, int slot, int lane, f32x4 acc) {
+  const f32x4 o = reinterpret_cast<const f32x4*>(red)[slot * 64 + lane];
+  return acc + o;
 }
 
 __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   using namespace trunk;
+  // xin: the sample as bf16 NHWC [84*84][4] (converted once); dead after conv1, so
+  // act2 and the conv2/conv3 K-split partials live in the same bytes afterwards.
+  __shared__ __attribute__((aligned(16))) __bf16 xin[HW * 4];
   __shared__ __attribute__((aligned(16))) __bf16 act1[R1 * L1];
-  __shared__ __attribute__((aligned(16))) __bf16 act2[R2 * L2];
+  __bf16* act2 = xin;
+  float* red = reinterpret_cast<float*>(xin + 6144);   // conv3 k-half partials, after act2 (R2 * L2 = 5832)
+  static_assert(R2 * L2 <= 6144 && 6144 * 2 + 4 * 4 * 1024 <= HW * 8, "act2 + partials fit xin");
   const int b = blockIdx.x, inst = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = lane & 15, kg = 8 * (lane >> 4);
-  const float scale = a.scale;
+  int64_t* prof = a.prof != nullptr && tid == 0 ? a.prof + ((int64_t)inst * gridDim.x + b) * 16 : nullptr;
+#define TRUNK_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
+  TRUNK_MARK(0);
 
-  // ---------------------------------------------------------------- conv1
-  const uint8_t* fb[4] = {nullptr, nullptr, nullptr, nullptr};
-  const uint8_t* nhwc = nullptr;
-  if (a.slots[inst] != nullptr) {
+  // ---------------------------------------------------------------- input loads (first)
+  // 1764 tasks of 4 pixels; a thread owns tasks tid + 512 j (j < 4)
+  constexpr int NT = HW / 4;
+  uint32_t in[4][4];
+  const bool slot_path = a.slots[inst] != nullptr;
+  if (slot_path) {
     const int4 sl = reinterpret_cast<const int4*>(a.slots[inst])[b];
-    fb[0] = a.frames + (int64_t)sl.x * HW;
-    fb[1] = a.frames + (int64_t)sl.y * HW;
-    fb[2] = a.frames + (int64_t)sl.z * HW;
-    fb[3] = a.frames + (int64_t)sl.w * HW;
+    const uint32_t* f0 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW);
+    const uint32_t* f1 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW);
+    const uint32_t* f2 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.z * HW);
+    const uint32_t* f3 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.w * HW);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 512 * j;
+      if (t < NT) { in[j][0] = f0[t]; in[j][1] = f1[t]; in[j][2] = f2[t]; in[j][3] = f3[t]; }
+    }
   } else {
-    nhwc = a.states[inst] + (int64_t)b * HW * 4;
+    const uint4* src = reinterpret_cast<const uint4*>(a.states[inst] + (int64_t)b * HW * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 512 * j;
+      if (t < NT) { const uint4 v = src[t]; in[j][0] = v.x; in[j][1] = v.y; in[j][2] = v.z; in[j][3] = v.w; }
+    }
   }
+
+  // Weight fragments (L2-resident packed bf16), held in VGPRs:
+  //   conv1 - every wave both n-tiles, all K (A fragments are read once per m-tile)
+  //   conv2 - wave owns n-tile (wave & 3), all K, m-tiles {wave>>2, +2, +4}
+  //   conv3 - wave owns n-tile (wave & 3) and k-half (wave >> 2); loaded after conv1
+  //           into the registers conv1 no longer needs.
+  const int nq = wave & 3, hi = wave >> 2;
+  bfx8 w1r[2][K1 / 32], w2r[K2 / 32];
+  const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
   {
     const bfx8* W1 = reinterpret_cast<const bfx8*>(a.w1[inst]);
-    const float* bias = a.b1[inst];
-    constexpr int MT = (R1 + 15) / 16;               // 25 m-tiles x 2 n-tiles (whole N per task)
-    for (int mt = wave; mt < MT; mt += 8) {
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-      const int p = mt * 16 + row;
+    const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
 #pragma unroll
-      for (int kb = 0; kb < K1 / 32; kb += 4) {
-        bfx8 af[4], b0[4], b1[4];
+    for (int ks = 0; ks < K1 / 32; ++ks) {
+      w1r[0][ks] = W1[(ks * 2 + 0) * 64 + lane];
+      w1r[1][ks] = W1[(ks * 2 + 1) * 64 + lane];
+    }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          af[u] = conv1_frag(fb, nhwc, p, (kb + u) * 32 + kg);
-          b0[u] = W1[((kb + u) * 2 + 0) * 64 + lane];
-          b1[u] = W1[((kb + u) * 2 + 1) * 64 + lane];
-        }
+    for (int ks = 0; ks < K2 / 32; ++ks) w2r[ks] = W2[(ks * 4 + nq) * 64 + lane];
+  }
+  // The MFMAs below run transposed (weights as the A operand): lane l then holds 4
+  // consecutive output channels 4*(l>>4)..+3 of pixel (l & 15) -> one 8-byte store.
+  const int cq = 4 * (lane >> 4);
+  const float4 bias1a = *reinterpret_cast<const float4*>(a.b1[inst] + cq);
+  const float4 bias1b = *reinterpret_cast<const float4*>(a.b1[inst] + 16 + cq);
+  const float4 bias2 = *reinterpret_cast<const float4*>(a.b2[inst] + nq * 16 + cq);
+  const float4 bias3 = *reinterpret_cast<const float4*>(a.b3[inst] + nq * 16 + cq);
+
+  // ---------------------------------------------------------------- u8 -> bf16 NHWC in LDS
+  if (slot_path) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc0 = tmfma(af[u], b0[u], acc0);
-          acc1 = tmfma(af[u], b1[u], acc1);
-        }
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 512 * j;
+      if (t < NT) planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], xin + 16 * t);
+    }
+  } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mt * 16 + 4 * (lane >> 4) + r;
-        if (m < R1) {
-          act1[m * L1 + row] = (__bf16)fmaxf(acc0[r] * scale + bias[row], 0.f);
-          act1[m * L1 + 16 + row] = (__bf16)fmaxf(acc1[r] * scale + bias[16 + row], 0.f);
-        }
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 512 * j;
+      if (t < NT) {   // NHWC word q = pixel 4t+q's 4 channels: transpose to planes then convert
+        uint32_t c[4];
+#pragma unroll
+        for (int ch = 0; ch < 4; ++ch)
+          c[ch] = ((in[j][0] >> 8 * ch) & 0xffu) | (((in[j][1] >> 8 * ch) & 0xffu) << 8) |
+                  (((in[j][2] >> 8 * ch) & 0xffu) << 16) | (((in[j][3] >> 8 * ch) & 0xffu) << 24);
+        planes_to_lds(c[0], c[1], c[2], c[3], xin + 16 * t);
       }
     }
   }
   __syncthreads();
-  // x1 -> global (backward masks / conv2 wgrad input), 16 B per thread
-  if (a.x1[inst] != nullptr) {
-    __bf16* x1 = a.x1[inst] + (int64_t)b * R1 * N1;
-    for (int t = threadIdx.x; t < R1 * N1 / 8; t += 512) {
-      const int m = t / (N1 / 8), c8 = (t - m * (N1 / 8)) * 8;
-      *reinterpret_cast<bfx8*>(x1 + m * N1 + c8) = *reinterpret_cast<const bfx8*>(act1 + m * L1 + c8);
+  TRUNK_MARK(1);
+
+  // ---------------------------------------------------------------- conv1 -> act1 (+x1)
+  // Every wave computes both n-tiles of its m-tiles (one LDS read per A fragment).
+  {
+    const float scale = a.scale;
+    const int kw = kg >> 2;                               // 0, 2, 4, 6: pixel pair of this lane
+    __bf16* x1 = a.x1[inst] != nullptr ? a.x1[inst] + (int64_t)b * R1 * N1 : nullptr;
+    auto load1 = [&](bfx8* f, int mt) {
+      const int p = mt * 16 + row, oy = p / O1, ox = p - oy * O1;
+      const __bf16* base = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
+#pragma unroll
+      for (int ks = 0; ks < K1 / 32; ++ks) f[ks] = *reinterpret_cast<const bfx8*>(base + ks * IW * 4);
+    };
+    constexpr int MT = R1 / 16, ITER = (MT + 7) / 8;      // 25 m-tiles (no tail) over 8 waves
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int mt = wave + 8 * i;
+      if (mt >= MT) break;                                // wave-uniform
+      bfx8 fa[K1 / 32];                                   // (single-buffered: VGPR budget)
+      load1(fa, mt);
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+      for (int ks = 0; ks < K1 / 32; ++ks) {              // k = (kh*8 + kw)*4 + c, kh = ks
+        c0 = tmfma(w1r[0][ks], fa[ks], c0);
+        c1 = tmfma(w1r[1][ks], fa[ks], c1);
+      }
+      const int p = mt * 16 + row;
+      const uint2 v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
+      *reinterpret_cast<uint2*>(act1 + p * L1 + cq) = v0;
+      *reinterpret_cast<uint2*>(act1 + p * L1 + 16 + cq) = v1;
+      if (x1 != nullptr) {   // conv2 wgrad input + ReLU mask of the backward
+        *reinterpret_cast<uint2*>(x1 + p * N1 + cq) = v0;
+        *reinterpret_cast<uint2*>(x1 + p * N1 + 16 + cq) = v1;
+      }
     }
   }
-  // ---------------------------------------------------------------- conv2
+  // conv3 fragments into the registers conv1 released (latency hidden by conv2)
+  bfx8 w3r[K3 / 64];
+#pragma unroll
+  for (int j = 0; j < K3 / 64; ++j) w3r[j] = W3[((hi * (K3 / 64) + j) * 4 + nq) * 64 + lane];
+  __syncthreads();
+  TRUNK_MARK(2);
+  // ---------------------------------------------------------------- conv2 -> act2 (+x2)
   {
-    const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
-    const float* bias = a.b2[inst];
-    constexpr int MT = (R2 + 15) / 16;               // 6 m-tiles x 2 n-tile pairs = 12 tasks
-    for (int task = wave; task < MT * 2; task += 8) {
-      const int mt = task >> 1, np = task & 1;
+    constexpr int KS = K2 / 32;                           // 16 k-steps
+    __bf16* x2 = a.x2[inst] != nullptr ? a.x2[inst] + (int64_t)b * R2 * N2 : nullptr;
+    auto load2 = [&](bfx8* f, int mt) {
       const int p = mt * 16 + row;
       const bool ok = p < R2;
       const int oy = ok ? p / O2 : 0, ox = ok ? p - oy * O2 : 0;
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-#pragma unroll 1
-      for (int kb = 0; kb < K2 / 32; kb += 4) {
-        bfx8 af[4], b0[4], b1[4];
+      const __bf16* base = act1 + ((oy * 2) * O1 + ox * 2) * L1 + kg;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k0 = (kb + u) * 32 + kg;             // k = (kh*4 + kw)*32 + ci
-          const int tap = k0 >> 5, ci = k0 & 31, kh = tap >> 2, kw = tap & 3;
-          af[u] = ok ? *reinterpret_cast<const bfx8*>(act1 + ((oy * 2 + kh) * O1 + ox * 2 + kw) * L1 + ci) : tz8();
-          b0[u] = W2[((kb + u) * 4 + np * 2 + 0) * 64 + lane];
-          b1[u] = W2[((kb + u) * 4 + np * 2 + 1) * 64 + lane];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc0 = tmfma(af[u], b0[u], acc0);
-          acc1 = tmfma(af[u], b1[u], acc1);
-        }
+      for (int ks = 0; ks < KS; ++ks) {                   // k = (kh*4 + kw)*32 + ci, tap = ks
+        const int kh = ks >> 2, kw = ks & 3;
+        f[ks] = ok ? *reinterpret_cast<const bfx8*>(base + (kh * O1 + kw) * L1) : tz8();
       }
-      const int n0 = np * 32 + row, n1 = np * 32 + 16 + row;
+    };
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mt * 16 + 4 * (lane >> 4) + r;
-        if (m < R2) {
-          act2[m * L2 + n0] = (__bf16)fmaxf(acc0[r] + bias[n0], 0.f);
-          act2[m * L2 + n1] = (__bf16)fmaxf(acc1[r] + bias[n1], 0.f);
-        }
+    for (int i = 0; i < 3; ++i) {                         // m-tiles hi, hi+2, hi+4 (6 = ceil(81/16))
+      const int mt = hi + 2 * i;
+      bfx8 fa[KS];
+      load2(fa, mt);
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) c = tmfma(w2r[ks], fa[ks], c);
+      const int p = mt * 16 + row;
+      if (p < R2) {
+        const uint2 v = pack4(c + f4(bias2));
+        *reinterpret_cast<uint2*>(act2 + p * L2 + nq * 16 + cq) = v;
+        if (x2 != nullptr) *reinterpret_cast<uint2*>(x2 + p * N2 + nq * 16 + cq) = v;
       }
     }
   }
   __syncthreads();
-  if (a.x2[inst] != nullptr) {
-    __bf16* x2 = a.x2[inst] + (int64_t)b * R2 * N2;
-    for (int t = threadIdx.x; t < R2 * N2 / 8; t += 512) {
-      const int m = t / (N2 / 8), c8 = (t - m * (N2 / 8)) * 8;
-      *reinterpret_cast<bfx8*>(x2 + m * N2 + c8) = *reinterpret_cast<const bfx8*>(act2 + m * L2 + c8);
-    }
-  }
-  // ---------------------------------------------------------------- conv3
+  TRUNK_MARK(6);
+  // ---------------------------------------------------------------- conv3 -> x3 (global)
   {
-    const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
-    const float* bias = a.b3[inst];
-    __bf16* x3 = a.x3[inst] + (int64_t)b * R3 * N3;
-    const int mt = wave >> 1, np = wave & 1;           // 4 m-tiles x 2 n-tile pairs = 8 tasks
-    const int p = mt * 16 + row;
-    const bool ok = p < R3;
-    const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-#pragma unroll 1
-    for (int kb = 0; kb < K3 / 32; kb += 6) {           // 18 k-steps = 3 batches of 6
-      bfx8 af[6], b0[6], b1[6];
+    constexpr int MT = (R3 + 15) / 16;                    // 4 m-tiles
+    constexpr int KJ = K3 / 64;                           // 9 k-steps per k-half
+    auto load3 = [&](bfx8* f, int mt) {
+      const int p = mt * 16 + row;
+      const bool ok = p < R3;
+      const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
+      const __bf16* base = act2 + (oy * O2 + ox) * L2 + kg;
 #pragma unroll
-      for (int u = 0; u < 6; ++u) {
-        const int k0 = (kb + u) * 32 + kg;               // k = (kh*3 + kw)*64 + ci
-        const int tap = k0 >> 6, ci = k0 & 63, kh = tap / 3, kw = tap - kh * 3;
-        af[u] = ok ? *reinterpret_cast<const bfx8*>(act2 + ((oy + kh) * O2 + ox + kw) * L2 + ci) : tz8();
-        b0[u] = W3[((kb + u) * 4 + np * 2 + 0) * 64 + lane];
-        b1[u] = W3[((kb + u) * 4 + np * 2 + 1) * 64 + lane];
+      for (int j = 0; j < KJ; ++j) {                      // k = (kh*3 + kw)*64 + ci
+        const int ks = hi * KJ + j, tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+        f[j] = ok ? *reinterpret_cast<const bfx8*>(base + (kh * O2 + kw) * L2 + (ks & 1) * 32) : tz8();
       }
+    };
+    f32x4 acc[MT];
+    bfx8 fa[2][KJ];
+    load3(fa[0], 0);
 #pragma unroll
-      for (int u = 0; u < 6; ++u) {
-        acc0 = tmfma(af[u], b0[u], acc0);
-        acc1 = tmfma(af[u], b1[u], acc1);
-      }
+    for (int mt = 0; mt < MT; ++mt) {
+      if (mt + 1 < MT) load3(fa[(mt + 1) & 1], mt + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < KJ; ++j) acc[mt] = tmfma(w3r[j], fa[mt & 1][j], acc[mt]);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    const int n0 = np * 32 + row, n1 = np * 32 + 16 + row;
+    TRUNK_MARK(8);
+    // k-half exchange: hi waves park fp32 partials in the (dead) input region
+    if (hi == 1) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = mt * 16 + 4 * (lane >> 4) + r;
-      if (m < R3) {
-        x3[m * N3 + n0] = (__bf16)fmaxf(acc0[r] + bias[n0], 0.f);
-        x3[m * N3 + n1] = (__bf16)fmaxf(acc1[r] + bias[n1], 0.f);
+      for (int mt = 0; mt < MT; ++mt) park(red, nq * MT + mt, lane, acc[mt]);
+    }
+    __syncthreads();
+    TRUNK_MARK(9);
+    if (hi == 0) {
+      __bf16* x3 = a.x3[inst] + (int64_t)b * R3 * N3;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 v = unpark(red, nq * MT + mt, lane, acc[mt]);
+        const int p = mt * 16 + row;
+        if (p < R3) *reinterpret_cast<uint2*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
       }
     }
   }
+  TRUNK_MARK(10);
+#undef TRUNK_MARK
 }
 
 }  // namespace dqn

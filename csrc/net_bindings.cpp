@@ -116,7 +116,7 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
 }
 
 // ptrs per instance (3 entries each, 0 = absent): slots, states, w1, w2, w3, b1, b2, b3, x1, x2, x3
-void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale) {
+void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale, int64_t prof) {
   TORCH_CHECK(ptrs.size() == 33 && ninst >= 1 && ninst <= 3 && B >= 1, "trunk args");
   dqn::TrunkArgs a{};
   a.frames = P<const uint8_t*>(frames);
@@ -132,13 +132,15 @@ void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, 
     }
   }
   a.scale = (float)scale;
+  a.prof = P<int64_t*>(prof);
   launch_trunk_fwd(a, (int)B, (int)ninst, cur_stream());
 }
 
 }  // namespace
 
 void register_net_ops(pybind11::module_& m) {
-  m.def("qnet_trunk", &trunk);
+  m.def("qnet_trunk", &trunk, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
+        pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("prof") = 0);
   m.def("qnet_pack", &pack);
   m.def("qnet_igemm", &igemm);
   m.def("qnet_wgrad", &wgrad);

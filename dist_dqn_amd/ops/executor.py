@@ -80,6 +80,7 @@ class HipExecutor:
         self._ws: Dict[Tuple[int, int], dict] = {}
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
+        self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -237,7 +238,8 @@ class HipExecutor:
                     # only the online(s) instance feeds the backward: the others skip x1/x2
                     + pad([rows(ws['x1'], 0)] if keep_acts else []) + pad([rows(ws['x2'], 0)] if keep_acts else [])
                     + pad([rows(ws['x3'], i) for i in range(ninst)]))
-            ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale)
+            prof = self.trunk_prof.data_ptr() if self.trunk_prof is not None else 0
+            ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale, prof)
             self._fc_fwd(packs, ws, B, ninst)
             return
         d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
