@@ -102,7 +102,8 @@ void sumtree_sample(torch::Tensor sum, torch::Tensor mn, torch::Tensor rng, torc
 
 void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s0, torch::Tensor s1,
                     torch::Tensor beta_pow, torch::Tensor ticket, double lr, double reg, int64_t reg_end,
-                    double grad_scale, torch::Tensor step, bool has_step, std::vector<double> hp) {
+                    double grad_scale, torch::Tensor step, bool has_step, std::vector<double> hp,
+                    c10::optional<torch::Tensor> target, int64_t target_freq) {
   CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
   CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
   TORCH_CHECK(w.numel() % 4 == 0 && grad.numel() == w.numel(), "flat buffers must match and be /4");
@@ -113,10 +114,17 @@ void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tens
   if (has_step) { CHECK_T(step, torch::kInt64); }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
+  float* tgt = nullptr;
+  if (target.has_value() && target->defined()) {   // fused hard target sync (needs the device step)
+    CHECK_T((*target), torch::kFloat32);
+    TORCH_CHECK(target->numel() == w.numel() && has_step && target_freq >= 1, "target sync args");
+    tgt = ptr<float>(*target);
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
   launch_optimizer_step((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1),
                         ptr<float>(beta_pow), has_step ? ptr<int64_t>(step) : nullptr, ptr<int32_t>(ticket), h,
-                        (float)lr, (float)reg, (int)reg_end, (float)grad_scale, (int)w.numel(), cur_stream());
+                        (float)lr, (float)reg, (int)reg_end, (float)grad_scale, (int)w.numel(), tgt,
+                        (int)target_freq, cur_stream());
 }
 
 void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tensor step, int64_t freq,
@@ -252,7 +260,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("replay_gather_frames", &replay_gather_frames);
   m.def("sumtree_set", &sumtree_set);
   m.def("sumtree_sample", &sumtree_sample);
-  m.def("optimizer_step", &optimizer_step);
+  m.def("optimizer_step", &optimizer_step, pybind11::arg("op"), pybind11::arg("w"), pybind11::arg("grad"),
+        pybind11::arg("s0"), pybind11::arg("s1"), pybind11::arg("beta_pow"), pybind11::arg("ticket"), pybind11::arg("lr"),
+        pybind11::arg("reg"), pybind11::arg("reg_end"), pybind11::arg("grad_scale"), pybind11::arg("step"),
+        pybind11::arg("has_step"), pybind11::arg("hp"), pybind11::arg("target") = pybind11::none(),
+        pybind11::arg("target_freq") = 1);
   m.def("target_update", &target_update);
   m.def("td_loss_scalar", &td_loss_scalar);
   m.def("td_loss_c51", &td_loss_c51);

@@ -106,7 +106,7 @@ enum LayerKind {
 }  // namespace dqn
 
 void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int njobs, int max_threads,
-                 hipStream_t st);
+                 void* dst2, const int64_t* step, int freq, hipStream_t st);
 int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);

@@ -57,8 +57,12 @@ template <int OP>
 __global__ void __launch_bounds__(256)
 optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __restrict__ s0,
              float* __restrict__ s1, float* __restrict__ beta_pow, int64_t* __restrict__ step,
-             int32_t* __restrict__ ticket, OptHP h, int n4) {
+             int32_t* __restrict__ ticket, OptHP h, int n4, float* __restrict__ tgt, int tfreq) {
   float lr_t = h.lr;
+  // fused hard target sync: this update makes global_step s+1; the reference copies
+  // target <- online after the train step when (s+1) % target_update_freq == 0
+  const bool sync = tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  float4* T = reinterpret_cast<float4*>(tgt);
   if constexpr (OP == 3) {
     const float b1p = beta_pow[0], b2p = beta_pow[1];
     lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
@@ -81,7 +85,9 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
       if (reg) g += h.reg * ww[j];
       update_one<OP>(ww[j], g, aa[j], bb[j], h, lr_t);
     }
-    W[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
+    const float4 nw = make_float4(ww[0], ww[1], ww[2], ww[3]);
+    W[i] = nw;
+    if (sync) T[i] = nw;
     if constexpr (OP != 0) S0[i] = make_float4(aa[0], aa[1], aa[2], aa[3]);
     if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6) S1[i] = make_float4(bb[0], bb[1], bb[2], bb[3]);
   }
@@ -148,7 +154,7 @@ static int grid_for_ticket(int n4) {
 
 void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
                            int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
-                           float grad_scale, int n, hipStream_t st) {
+                           float grad_scale, int n, float* tgt, int tfreq, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
@@ -156,13 +162,13 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
   const int n4 = n / 4;
   dim3 grid(grid_for_ticket(n4)), block(256);
   switch (op) {
-    case 0: hipLaunchKernelGGL(optim_kernel<0>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
-    case 1: hipLaunchKernelGGL(optim_kernel<1>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
-    case 2: hipLaunchKernelGGL(optim_kernel<2>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
-    case 3: hipLaunchKernelGGL(optim_kernel<3>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
-    case 4: hipLaunchKernelGGL(optim_kernel<4>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
-    case 5: hipLaunchKernelGGL(optim_kernel<5>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
-    case 6: hipLaunchKernelGGL(optim_kernel<6>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4); break;
+    case 0: hipLaunchKernelGGL(optim_kernel<0>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 1: hipLaunchKernelGGL(optim_kernel<1>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 2: hipLaunchKernelGGL(optim_kernel<2>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 3: hipLaunchKernelGGL(optim_kernel<3>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 4: hipLaunchKernelGGL(optim_kernel<4>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 5: hipLaunchKernelGGL(optim_kernel<5>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 6: hipLaunchKernelGGL(optim_kernel<6>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
     default: break;
   }
 }

@@ -47,12 +47,20 @@ DQN_DEV f32x4 mfma16(const bfx8& a, const bfx8& b, const f32x4& c) {
 }
 
 // ============================================================== weight packing
+// dst2 (optional): the target network's packed copy, written too when step % freq == 0
+// (the fused hard target sync: online was just copied to the target's fp32 master).
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src, __bf16* __restrict__ dst,
-                                                   const PackJob* __restrict__ jobs, const float* __restrict__ noise) {
+                                                   const PackJob* __restrict__ jobs, __bf16* __restrict__ dst2,
+                                                   const int64_t* __restrict__ step, int freq) {
   const PackJob jb = jobs[blockIdx.y];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool sync = dst2 != nullptr && step != nullptr && (step[0] % freq) == 0;
   if (jb.mode == 3) {                           // contiguous fp32 copy (bias concatenation)
-    if (t < jb.K) reinterpret_cast<float*>(dst + jb.dst_off)[t] = src[jb.src_off + t];
+    if (t < jb.K) {
+      const float x = src[jb.src_off + t];
+      reinterpret_cast<float*>(dst + jb.dst_off)[t] = x;
+      if (sync) reinterpret_cast<float*>(dst2 + jb.dst_off)[t] = x;
+    }
     return;
   }
   const int K32 = (jb.K + 31) / 32, N16 = (jb.N + 15) / 16;
@@ -76,7 +84,9 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src
     }
     v[j] = (__bf16)x;
   }
-  *reinterpret_cast<bfx8*>(dst + jb.dst_off + ((int64_t)((jb.ks_off + ks) * jb.dst_N16 + jb.nt_off + nt) * 64 + l) * 8) = v;
+  const int64_t o = jb.dst_off + ((int64_t)((jb.ks_off + ks) * jb.dst_N16 + jb.nt_off + nt) * 64 + l) * 8;
+  *reinterpret_cast<bfx8*>(dst + o) = v;
+  if (sync) *reinterpret_cast<bfx8*>(dst2 + o) = v;
 }
 
 // ================================================================== A loaders
@@ -592,10 +602,11 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
 using namespace dqn;
 
 // ------------------------------------------------------------------ launchers
-void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs, int max_threads, hipStream_t st) {
+void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs, int max_threads, void* dst2,
+                 const int64_t* step, int freq, hipStream_t st) {
   dim3 grid((max_threads + 255) / 256, njobs);
   hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, src, reinterpret_cast<__bf16*>(dst), jobs_dev,
-                     (const float*)nullptr);
+                     reinterpret_cast<__bf16*>(dst2), step, freq < 1 ? 1 : freq);
 }
 
 #define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI)                                                     \

@@ -18,9 +18,11 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUD
 template <typename T>
 T P(int64_t v) { return reinterpret_cast<T>(static_cast<intptr_t>(v)); }
 
-void pack(int64_t src, int64_t dst, int64_t jobs, int64_t njobs, int64_t max_threads) {
+void pack(int64_t src, int64_t dst, int64_t jobs, int64_t njobs, int64_t max_threads, int64_t dst2, int64_t step,
+          int64_t freq) {
+  TORCH_CHECK(dst2 == 0 || (step != 0 && freq >= 1), "pack: a second destination needs the device step");
   launch_pack(P<const float*>(src), P<void*>(dst), P<const dqn::PackJob*>(jobs), (int)njobs, (int)max_threads,
-              cur_stream());
+              P<void*>(dst2), P<const int64_t*>(step), (int)freq, cur_stream());
 }
 
 dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_t>& w,
@@ -141,7 +143,8 @@ void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, 
 void register_net_ops(pybind11::module_& m) {
   m.def("qnet_trunk", &trunk, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
         pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("prof") = 0);
-  m.def("qnet_pack", &pack);
+  m.def("qnet_pack", &pack, pybind11::arg("src"), pybind11::arg("dst"), pybind11::arg("jobs"), pybind11::arg("njobs"),
+        pybind11::arg("max_threads"), pybind11::arg("dst2") = 0, pybind11::arg("step") = 0, pybind11::arg("freq") = 1);
   m.def("qnet_igemm", &igemm);
   m.def("qnet_wgrad", &wgrad);
   m.def("qnet_head_loss", &head_loss);

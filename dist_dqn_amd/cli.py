@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import logging
 import os
+import random
 import sys
 from typing import Optional, Sequence
 
@@ -55,7 +56,7 @@ def run_worker(config: Config):
                               alpha=config.per_alpha, seed=seed + ctx.rank)
         session = Learner(network, replay, config, ctx)
     else:
-        replay = ReplayMemory(config.replay_memory_capacity)
+        replay = ReplayMemory(config.replay_memory_capacity, rng=random.Random(seed + 7919 * (ctx.rank + 1)))
         session = None
     monitor = EpisodeMonitor(config.monitor_path, ctx.rank) if config.monitor else None
     metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))

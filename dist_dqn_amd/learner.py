@@ -86,16 +86,18 @@ class Learner:
 
     def _apply(self):
         cfg = self.config
-        self.net.apply_grads(self.reducer.scale)
+        hard = self.tau >= 1.0
+        # hard target sync folded into the optimizer + repack launches when the backend can
+        fused = self.net.apply_grads(self.reducer.scale, target_freq=cfg.target_update_freq if hard else None)
         if getattr(self.replay, 'prioritized', False):
             self.replay.update_priorities(self.idx, self.prio, cfg.per_eps)
-        if self.tau < 1.0:
+        # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).
+        # Under sync DP every rank's online params are bit-identical, so the local
+        # copy equals the reference's PS-owned target (--disable_target_replication).
+        if not hard:
             kernels.target_update(self.net.target.flat, self.net.online.flat, self.tau)
             self.net.sync_target_copy(self.tau)
-        else:
-            # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).
-            # Under sync DP every rank's online params are bit-identical, so the local
-            # copy equals the reference's PS-owned target (--disable_target_replication).
+        elif not fused:
             self.net.hard_target_update(self.net.global_step, cfg.target_update_freq)
 
     def _eager_step(self):

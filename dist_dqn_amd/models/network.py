@@ -108,10 +108,24 @@ class Network:
         self.last_loss = loss
         return loss, prio
 
-    def apply_grads(self, grad_scale: float = 1.0):
-        # global_step += 1 happens inside the (fused) optimizer step
+    def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None) -> bool:
+        """Optimizer step (global_step += 1 inside it) + executor repack.
+
+        target_freq: also do the hard target sync (target <- online when the new
+        global_step % target_freq == 0, device predicate) inside those same two
+        launches. Returns True when it was fused that way; otherwise the caller
+        still owes the target update (``hard_target_update``)."""
+        ex = self.executor
+        fuse = (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
+                and hasattr(ex, 'packed'))
+        if fuse:
+            self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,
+                                target=self.target.flat, target_freq=int(target_freq))
+            ex.repack(self.online.flat, target=self.target.flat, step=self.global_step, freq=int(target_freq))
+            return True
         self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step)
         self._repack()
+        return False
 
     def _repack(self):
         if hasattr(self.executor, 'repack'):

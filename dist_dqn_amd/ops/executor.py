@@ -150,13 +150,25 @@ class HipExecutor:
             self.repack(flat)
         return p
 
-    def repack(self, flat: torch.Tensor):
-        """fp32 master -> bf16 MFMA fragments (call after every optimizer step / load)."""
+    def repack(self, flat: torch.Tensor, target: Optional[torch.Tensor] = None,
+               step: Optional[torch.Tensor] = None, freq: int = 1):
+        """fp32 master -> bf16 MFMA fragments (call after every optimizer step / load).
+
+        target/step/freq: also write the fragments into ``target``'s packed copy when
+        step % freq == 0 (device predicate; the fused hard target sync)."""
         p = self._packed.get(flat.data_ptr())
         if p is None:
             self.packed(flat)
-            return
+            if target is None:
+                return
+            p = self._packed[flat.data_ptr()]
         jobs = self._jobs_on(flat.device)
+        if target is not None:
+            assert step is not None and step.dtype == torch.int64 and step.device == flat.device
+            pt = self.packed(target)
+            self.ext.qnet_pack(flat.data_ptr(), p.data_ptr(), jobs.data_ptr(), len(self.jobs), self._max_threads,
+                               pt.data_ptr(), step.data_ptr(), int(freq))
+            return
         self.ext.qnet_pack(flat.data_ptr(), p.data_ptr(), jobs.data_ptr(), len(self.jobs), self._max_threads)
 
     def sync_target(self, target: torch.Tensor, online: torch.Tensor, tau: float,

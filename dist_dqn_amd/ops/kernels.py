@@ -131,7 +131,8 @@ def sumtree_sample(tree, rng_state, size_dev, beta, idx_out, w_out, sample_out: 
 
 # ------------------------------------------------------------- optimizer op
 def optimizer_step(opt, param: torch.Tensor, grad: torch.Tensor, grad_scale: float = 1.0,
-                   global_step: Optional[torch.Tensor] = None):
+                   global_step: Optional[torch.Tensor] = None, target: Optional[torch.Tensor] = None,
+                   target_freq: int = 1):
     ext = _ext.load(required=True)
     from ..optim import OPT_IDS
     hp = opt.hp
@@ -145,7 +146,8 @@ def optimizer_step(opt, param: torch.Tensor, grad: torch.Tensor, grad_scale: flo
                        global_step is not None, [float(hp['momentum']), float(hp['rho']),
                                            float(hp['rms_mom']), float(hp['rms_eps']),
                                            float(hp['b1']), float(hp['b2']), float(hp['adam_eps']),
-                                           float(hp['ad_rho']), float(hp['ad_eps'])])
+                                           float(hp['ad_rho']), float(hp['ad_eps'])],
+                       target, int(target_freq))
 
 
 # ---------------------------------------------------------- target network

@@ -86,11 +86,15 @@ class FlatOptimizer:
             self.beta_powers[1] = float(sd['beta2_power'])
 
     def step(self, param: torch.Tensor, grad: torch.Tensor, grad_scale: float = 1.0,
-             global_step: Optional[torch.Tensor] = None):
-        """param -= update(grad * grad_scale + reg * w) in place; global_step += 1."""
+             global_step: Optional[torch.Tensor] = None, target: Optional[torch.Tensor] = None,
+             target_freq: int = 1):
+        """param -= update(grad * grad_scale + reg * w) in place; global_step += 1.
+
+        target (HIP path): also copy the updated params into it when the new
+        global_step % target_freq == 0 (fused hard target sync)."""
         if param.is_cuda and self.backend != 'torch':
             from .ops import kernels
-            kernels.optimizer_step(self, param, grad, grad_scale, global_step)
+            kernels.optimizer_step(self, param, grad, grad_scale, global_step, target, target_freq)
         else:
             self.apply_torch(param, grad, grad_scale)
             if global_step is not None:

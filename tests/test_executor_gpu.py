@@ -125,3 +125,24 @@ def test_fused_trunk_matches_layerwise(slots):
         ex._fwd_trunk([st], [p], [f], ws, B, 1)
         torch.cuda.synchronize()
         assert torch.equal(ws['x3'][0], outs[1]['x3'][0])
+
+
+def test_fused_hard_target_sync():
+    """Optimizer + repack carry the hard target copy (device predicate on global_step)."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 --target_update_freq=3')
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+    rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
+    rep.fill_synthetic(4096, 6, seed=5)
+    ln = Learner(net, rep, cfg, use_graph=True)
+    ex = net.executor
+    for step in range(1, 8):
+        ln.step()
+        torch.cuda.synchronize()
+        same = torch.equal(net.target.flat, net.online.flat)
+        # bitwise (the packed buffer also holds fp32 bias copies: NaN patterns as bf16)
+        same_p = torch.equal(ex.packed(net.target.flat).view(torch.int16), ex.packed(net.online.flat).view(torch.int16))
+        assert same == same_p == (step % 3 == 0), step
