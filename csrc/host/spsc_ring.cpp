@@ -24,7 +24,7 @@ void dqn_ring_init(uint8_t* buf, uint64_t capacity, uint64_t record_bytes) {
   __atomic_store_n(u64(buf, kTail), 0, __ATOMIC_RELAXED);
   *u64(buf, kCap) = capacity;
   *u64(buf, kRec) = record_bytes;
-  __atomic_thread_fence(__ATOMIC_RELEASE);
+  // (published to other threads/processes by their creation, which happens after init)
 }
 
 int64_t dqn_ring_push(uint8_t* buf, const uint8_t* recs, int64_t n) {

@@ -11,3 +11,15 @@ void dqn_ring_init(uint8_t* buf, uint64_t capacity, uint64_t record_bytes);
 int64_t dqn_ring_push(uint8_t* buf, const uint8_t* recs, int64_t n);
 int64_t dqn_ring_pop(uint8_t* buf, uint8_t* out, int64_t max_n);
 int64_t dqn_ring_size(uint8_t* buf);
+
+// Actor <-> inference-server mailboxes (mailbox.cpp)
+int64_t dqn_mbox_stride(int64_t state_bytes);
+size_t dqn_mbox_region_bytes(int64_t n, int64_t state_bytes);
+void dqn_mbox_init(uint8_t* region, int64_t n, int64_t state_bytes);
+void dqn_mbox_set_stop(uint8_t* region, int64_t v);
+int64_t dqn_mbox_stopped(uint8_t* region);
+int64_t dqn_mbox_request(uint8_t* region, int64_t i, int64_t state_bytes, const uint8_t* state, int64_t timeout_us);
+int64_t dqn_mbox_collect(uint8_t* region, int64_t n, int64_t state_bytes, uint8_t* out_states, int32_t* out_ids,
+                         uint64_t* out_seq, int64_t max_batch);
+void dqn_mbox_respond(uint8_t* region, int64_t state_bytes, const int32_t* ids, const uint64_t* seq,
+                      const int32_t* actions, int64_t m);

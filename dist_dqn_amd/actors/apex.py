@@ -1,0 +1,405 @@
+"""Ape-X style distributed acting: many CPU actor processes, one GPU learner.
+
+Reference: one actor per worker process, acting inside the worker's own
+episode loop with a batch-1 `session.run` per greedy action against the PS
+parameters (`/root/reference/src/dqn_agent.py:72-107,155-189`).
+
+MI355X-native design:
+  * actors are plain numpy processes (no torch, no HIP): env step, C++ frame
+    preprocessing, per-actor fixed epsilon eps_i = base^(1 + alpha*i/(N-1))
+    (Ape-X), and — for greedy steps — a post into their inference MAILBOX;
+  * the learner process answers all pending mailboxes with ONE batched
+    forward on the GPU (``serve``) using the live online weights, so actors
+    never hold stale parameter copies and nothing is broadcast;
+  * transitions travel through a lock-free SPSC ring per actor in shared
+    memory (csrc/host/spsc_ring.cpp); ``drain`` moves them into the HBM
+    replay's pinned staging buffers, which flush as H2D copies on a side
+    stream (replay/device.py), frames stored once (slot stacks per actor);
+  * under data parallelism every rank runs its own pool into its own replay
+    shard (sharded replay; gradients all-reduced as usual).
+
+Shared memory is a file under /dev/shm mapped by every process (numpy.memmap),
+which keeps Python's SharedMemory resource tracker out of the actor lifecycle.
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import multiprocessing as mp
+import os
+import random
+import time
+import uuid
+from collections import deque
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+log = logging.getLogger(__name__)
+
+# transition record: 16-byte header + observation payload
+HEADER = np.dtype([('kind', 'u1'), ('done', 'u1'), ('pad', 'u2'), ('action', '<i4'), ('reward', '<f4'),
+                   ('ret', '<f4')])
+KIND_RESET, KIND_STEP = 0, 1
+assert HEADER.itemsize == 16
+
+
+def apex_epsilons(n: int, base: float = 0.4, alpha: float = 7.0) -> List[float]:
+    """Ape-X per-actor exploration rates eps_i = base^(1 + alpha * i / (n - 1))."""
+    if n == 1:
+        return [base]
+    return [base ** (1.0 + alpha * i / (n - 1)) for i in range(n)]
+
+
+@dataclasses.dataclass
+class ActorSpec:
+    index: int
+    env_id: str
+    seed: int
+    eps: float
+    frames_per_state: int
+    frame_hw: Optional[Sequence[int]]       # (H, W) for image envs, None for vector envs
+    obs_dim: int                            # vector envs: observation length
+    max_steps_per_episode: int
+    ring_path: str
+    ring_offset: int
+    ring_bytes: int
+    mbox_path: str
+    mbox_bytes: int
+    num_actors: int
+    record_bytes: int
+    state_bytes: int
+    reward_clip: float = 0.0
+    max_frames: int = 0                     # stop after this many env steps (0 = until told)
+
+
+def _map(path: str, nbytes: int, create: bool = False) -> np.memmap:
+    return np.memmap(path, dtype=np.uint8, mode='w+' if create else 'r+', shape=(nbytes,))
+
+
+def actor_main(spec: ActorSpec):
+    """Actor process body (spawned): numpy + ctypes only."""
+    from .. import envs
+    from ..native import load
+    lib = load()
+    ring_all = _map(spec.ring_path, spec.ring_offset + spec.ring_bytes)
+    ring = ring_all[spec.ring_offset:spec.ring_offset + spec.ring_bytes]
+    mbox = _map(spec.mbox_path, spec.mbox_bytes)
+    env = envs.make(spec.env_id, seed=spec.seed)
+    rng = random.Random(spec.seed)
+    n_act = env.action_space.n
+    k = spec.frames_per_state
+    image = spec.frame_hw is not None
+    rec = np.zeros(spec.record_bytes, dtype=np.uint8)
+    hdr = rec[:HEADER.itemsize].view(HEADER)
+    payload = rec[HEADER.itemsize:]
+    if image:
+        H, W = spec.frame_hw
+        frame = np.empty((H, W), dtype=np.uint8)
+        stack = np.zeros((H, W, k), dtype=np.uint8)
+
+    def observe(obs):
+        if image:
+            lib.preprocess(obs, H, W, out=frame)
+            payload[:] = frame.reshape(-1)
+            return frame
+        v = np.asarray(obs, dtype=np.float32).reshape(-1)
+        payload[:] = v.view(np.uint8)
+        return v
+
+    def push():
+        while lib.ring_push(ring, rec, 1) == 0:      # ring full: learner backpressure
+            if lib.mbox_stopped(mbox):
+                return False
+            time.sleep(0.0005)
+        return True
+
+    frames = 0
+    while not lib.mbox_stopped(mbox):
+        obs = observe(env.reset())
+        hdr['kind'], hdr['done'], hdr['action'], hdr['reward'], hdr['ret'] = KIND_RESET, 0, 0, 0.0, 0.0
+        if not push():
+            break
+        if image:
+            stack[:] = frame[:, :, None]               # first frame duplicated k times
+            state = stack
+        else:
+            state = obs.copy()
+        ret, steps, done = 0.0, 0, False
+        while not done and steps < spec.max_steps_per_episode:
+            if rng.random() < spec.eps:
+                a = rng.randrange(n_act)
+            else:
+                a = lib.mbox_request(mbox, spec.index, np.ascontiguousarray(state))
+                if a < 0:                             # stop requested while waiting
+                    return
+            obs, r, done, _ = env.step(a)
+            ret += r
+            steps += 1
+            frames += 1
+            if spec.reward_clip > 0:
+                r = float(np.clip(r, -spec.reward_clip, spec.reward_clip))
+            o = observe(obs)
+            hdr['kind'], hdr['done'], hdr['action'], hdr['reward'] = KIND_STEP, int(done), a, r
+            # episode return rides on the last record (for the learner's stats)
+            hdr['ret'] = ret if (done or steps >= spec.max_steps_per_episode) else np.float32('nan')
+            if not push():
+                return
+            if image:
+                stack[:, :, :-1] = stack[:, :, 1:]
+                stack[:, :, -1] = o
+            else:
+                state = o.copy()
+            if spec.max_frames and frames >= spec.max_frames:
+                return
+
+
+class ApexActorPool:
+    """Learner-side owner of the actor processes, their rings and mailboxes."""
+
+    def __init__(self, env_id: str, num_actors: int, frames_per_state: int, frame_hw: Optional[Sequence[int]],
+                 obs_dim: int, num_actions: int, max_steps_per_episode: int, seed: int = 0,
+                 eps_base: float = 0.4, eps_alpha: float = 7.0, ring_capacity: int = 1024,
+                 reward_clip: float = 0.0, max_frames_per_actor: int = 0, shm_dir: str = '/dev/shm',
+                 start_method: str = 'spawn', n_step: int = 1, gamma: float = 0.99):
+        from ..native import load
+        self.lib = load()
+        self.n = int(num_actors)
+        self.k = int(frames_per_state)
+        self.frame_hw = tuple(frame_hw) if frame_hw is not None else None
+        self.num_actions = num_actions
+        obs_bytes = (self.frame_hw[0] * self.frame_hw[1]) if self.frame_hw else 4 * obs_dim
+        self.obs_dim = obs_dim
+        self.record_bytes = HEADER.itemsize + obs_bytes
+        self.state_bytes = (obs_bytes * self.k) if self.frame_hw else obs_bytes
+        self.ring_capacity = ring_capacity
+        rb = self.lib.ring_bytes(ring_capacity, self.record_bytes)
+        self.ring_stride = (rb + 4095) // 4096 * 4096
+        tag = uuid.uuid4().hex[:12]
+        if not os.path.isdir(shm_dir):
+            shm_dir = '/tmp'
+        self.ring_path = os.path.join(shm_dir, 'dqn_apex_rings_%s' % tag)
+        self.mbox_path = os.path.join(shm_dir, 'dqn_apex_mbox_%s' % tag)
+        self.rings = _map(self.ring_path, self.ring_stride * self.n, create=True)
+        for i in range(self.n):
+            self.lib.ring_init(self.rings[i * self.ring_stride:(i + 1) * self.ring_stride], ring_capacity,
+                               self.record_bytes)
+        self.mbox_bytes = self.lib.mbox_region_bytes(self.n, self.state_bytes)
+        self.mbox = _map(self.mbox_path, self.mbox_bytes, create=True)
+        self.lib.mbox_init(self.mbox, self.n, self.state_bytes)
+        self.eps = apex_epsilons(self.n, eps_base, eps_alpha)
+        self.specs = [ActorSpec(i, env_id, seed + 7919 * (i + 1), self.eps[i], self.k, self.frame_hw, obs_dim,
+                                max_steps_per_episode, self.ring_path, i * self.ring_stride, rb, self.mbox_path,
+                                self.mbox_bytes, self.n, self.record_bytes, self.state_bytes, reward_clip,
+                                max_frames_per_actor)
+                      for i in range(self.n)]
+        self._ctx = mp.get_context(start_method)
+        self.procs: List[mp.Process] = []
+        # server buffers (pinned when a GPU learner asks for them: set_pinned)
+        self._states = np.zeros((self.n, self.state_bytes), dtype=np.uint8)
+        self._ids = np.zeros(self.n, dtype=np.int32)
+        self._seq = np.zeros(self.n, dtype=np.uint64)
+        self._acts = np.zeros(self.n, dtype=np.int32)
+        self._pop = np.zeros((ring_capacity, self.record_bytes), dtype=np.uint8)
+        self.n_step, self.gamma = int(n_step), float(gamma)
+        self._nstep = None
+        if self.n_step > 1:
+            from ..replay.nstep import NStepAccumulator
+            self._nstep = [NStepAccumulator(self.n_step, self.gamma) for _ in range(self.n)]
+        self.frames = 0                      # env steps ingested
+        self.episodes = 0
+        self.returns: deque = deque(maxlen=100)
+        self.served = 0                      # greedy actions answered
+        self._closed = False
+
+    # -------------------------------------------------------------- life
+    def start(self):
+        for s in self.specs:
+            p = self._ctx.Process(target=actor_main, args=(s,), daemon=True, name='apex-actor-%d' % s.index)
+            p.start()
+            self.procs.append(p)
+        return self
+
+    def alive(self) -> int:
+        return sum(p.is_alive() for p in self.procs)
+
+    def stop(self, timeout: float = 10.0):
+        if self._closed:
+            return
+        self.lib.mbox_set_stop(self.mbox, 1)
+        t0 = time.time()
+        for p in self.procs:
+            p.join(max(0.1, timeout - (time.time() - t0)))
+        for p in self.procs:            # exact processes we started, never a pattern
+            if p.is_alive():
+                p.terminate()
+                p.join(2.0)
+        self._closed = True
+        for path in (self.ring_path, self.mbox_path):
+            try:
+                os.unlink(path)
+            except FileNotFoundError:
+                pass
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    # ----------------------------------------------------------- serving
+    def serve(self, q_fn: Callable[[np.ndarray], np.ndarray], max_batch: Optional[int] = None) -> int:
+        """Answer every pending mailbox with ONE batched forward. q_fn maps a uint8/f32
+        state batch [m, ...] to actions [m] (int). Returns m."""
+        m = self.lib.mbox_collect(self.mbox, self.n, self.state_bytes, self._states, self._ids, self._seq,
+                                  max_batch or self.n)
+        if m == 0:
+            return 0
+        raw = self._states[:m]
+        if self.frame_hw:
+            batch = raw.reshape(m, self.frame_hw[0], self.frame_hw[1], self.k)
+        else:
+            batch = raw.view(np.float32).reshape(m, self.obs_dim)
+        self._acts[:m] = np.asarray(q_fn(batch), dtype=np.int32).reshape(-1)[:m]
+        self.lib.mbox_respond(self.mbox, self.state_bytes, self._ids, self._seq, self._acts, m)
+        self.served += m
+        return m
+
+    # ------------------------------------------------------------ ingest
+    def drain(self, replay, max_per_actor: Optional[int] = None) -> int:
+        """Move every actor's pending transitions into the replay's staging (then flush)."""
+        total = 0
+        hsz = HEADER.itemsize
+        cap = min(self.ring_capacity, max_per_actor or self.ring_capacity)
+        for i in range(self.n):
+            ring = self.rings[i * self.ring_stride:(i + 1) * self.ring_stride]
+            m = self.lib.ring_pop(ring, self._pop, cap)
+            if m == 0:
+                continue
+            hdrs = self._pop[:m, :hsz].copy().view(HEADER).reshape(m)
+            for j in range(m):
+                h = hdrs[j]
+                body = self._pop[j, hsz:]
+                obs = body.reshape(self.frame_hw) if self.frame_hw else body.view(np.float32)
+                if h['kind'] == KIND_RESET:
+                    replay.begin_episode(obs.copy(), actor=i)
+                    if self._nstep is not None:
+                        self._nstep[i].reset()
+                    continue
+                if self._nstep is not None:
+                    replay.add_step_nstep(self._nstep[i], int(h['action']), float(h['reward']), obs.copy(),
+                                          bool(h['done']), actor=i)
+                else:
+                    replay.add_step(int(h['action']), float(h['reward']), obs.copy(), bool(h['done']), actor=i,
+                                    gamma_n=self.gamma)
+                self.frames += 1
+                if not np.isnan(h['ret']):
+                    self.episodes += 1
+                    self.returns.append(float(h['ret']))
+            total += m
+        if total:
+            replay.flush()
+        return total
+
+
+class ApexTrainer:
+    """One learner rank of Ape-X: actor pool + inference thread + replay ingest + learner.
+
+    The learner keeps the reference's train cadence knob differently: actors run
+    free, and the learner takes an SGD step whenever the replay holds enough data
+    (Ape-X). ``actor_param_sync_freq`` > 0 makes the inference service act with a
+    parameter snapshot refreshed every that many learner steps (Ape-X actors'
+    periodic parameter pulls); 0 acts with the live online weights.
+    """
+
+    def __init__(self, network, replay, learner, pool: ApexActorPool, config, metrics=None):
+        import threading
+        import torch
+        self.torch = torch
+        self.net, self.replay, self.learner, self.pool = network, replay, learner, pool
+        self.config = config
+        self.metrics = metrics
+        self.device = network.device
+        self.sync_freq = int(config.actor_param_sync_freq)
+        self._snap = None
+        if self.sync_freq > 0:
+            self._snap = network.online.flat.clone()
+            self._refresh_snapshot()
+        self._stop = threading.Event()
+        self._lock = threading.Lock()       # one forward at a time vs the snapshot refresh
+        self._thread = threading.Thread(target=self._serve_loop, name='apex-inference', daemon=True)
+        self.serve_calls = 0
+
+    def _refresh_snapshot(self):
+        with self.torch.no_grad():
+            self._snap.copy_(self.net.online.flat)
+            if hasattr(self.net.executor, 'repack'):
+                self.net.executor.repack(self._snap)
+
+    def _q_actions(self, batch: np.ndarray) -> np.ndarray:
+        torch = self.torch
+        x = torch.from_numpy(batch)
+        if self.device.type == 'cuda':
+            x = x.pin_memory().to(self.device, non_blocking=True)
+        with self._lock, torch.no_grad():
+            if self._snap is not None:
+                q = self.net.executor.q_values(self._snap, x.contiguous())
+            else:
+                q = self.net.q_values(x)
+            return q.argmax(1).to(torch.int32).cpu().numpy()
+
+    def _serve_loop(self):
+        while not self._stop.is_set():
+            if self.pool.serve(self._q_actions) == 0:
+                time.sleep(0.0002)
+            else:
+                self.serve_calls += 1
+
+    def run(self, max_train_steps: int = 0, max_seconds: float = 0.0, supervisor=None, log_every: float = 10.0):
+        cfg = self.config
+        start = max(cfg.minibatch_size, cfg.replay_start_size)
+        self.pool.start()
+        self._thread.start()
+        t0 = last = time.time()
+        steps_at_last = frames_at_last = 0
+        try:
+            while True:
+                self.pool.drain(self.replay)
+                if self.replay.size() >= start:
+                    self.learner.step()
+                    if self._snap is not None and self.learner.train_steps % self.sync_freq == 0:
+                        with self._lock:
+                            self._refresh_snapshot()
+                else:
+                    time.sleep(0.001)
+                now = time.time()
+                if now - last >= log_every:
+                    dt = now - last
+                    sps = (self.learner.train_steps - steps_at_last) / dt
+                    fps = (self.pool.frames - frames_at_last) / dt
+                    mean = float(np.mean(self.pool.returns)) if self.pool.returns else 0.0
+                    log.info('apex: %d actors alive, frames %d (%.0f/s), sgd steps %d (%.1f/s), episodes %d, '
+                             'last-100 mean return %.2f, replay %d', self.pool.alive(), self.pool.frames, fps,
+                             self.learner.train_steps, sps, self.pool.episodes, mean, self.replay.size())
+                    if self.metrics is not None:
+                        self.metrics.write(kind='apex', frames=self.pool.frames, env_frames_per_sec=fps,
+                                           training_steps=self.learner.train_steps, sgd_steps_per_sec=sps,
+                                           episodes=self.pool.episodes, mean100=mean,
+                                           replay_size=self.replay.size(), actors_alive=self.pool.alive())
+                    last, steps_at_last, frames_at_last = now, self.learner.train_steps, self.pool.frames
+                if max_train_steps and self.learner.train_steps >= max_train_steps:
+                    break
+                if max_seconds and now - t0 >= max_seconds:
+                    break
+                if supervisor is not None and supervisor.should_stop():
+                    log.warning('Received signal to stop. Exiting Ape-X loop.')
+                    break
+                if self.pool.alive() == 0 and self.pool.procs:
+                    log.warning('all actors exited')
+                    self.pool.drain(self.replay)
+                    break
+        finally:
+            self._stop.set()
+            self._thread.join(5.0)
+            self.pool.stop()
+        return self

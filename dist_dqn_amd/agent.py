@@ -130,22 +130,7 @@ class DQNAgent:
                 self.replay_memory.add(s, a, R, ns, d)
 
     def _store_nstep_device(self, action, reward, next_frame, done):
-        rep = self.replay_memory
-        if rep.frame_mode:
-            st = list(rep._stacks[0])
-            slot = rep.write_frame(next_frame)
-            nxt = st[1:] + [slot]
-            rep._stacks[0] = nxt
-            for s, a, R, ns, d, g in self._nstep.push(st, action, reward, nxt, done):
-                rep.add_transition(s, ns[-1], a, R, d, g)
-        else:
-            prev = rep._last_obs[0]
-            cur = np.asarray(next_frame, dtype=np.float32).reshape(-1)
-            rep._last_obs[0] = cur
-            for s, a, R, ns, d, g in self._nstep.push(prev, action, reward, cur, done):
-                rep._st_trans.append((s, ns, int(a), float(R), float(d), float(g)))
-            if len(rep._st_trans) >= rep._stage_size:
-                rep.flush()
+        self.replay_memory.add_step_nstep(self._nstep, action, reward, next_frame, done)
 
     def train_episode(self, max_steps):
         state = self._begin_episode()

@@ -14,6 +14,7 @@ import random
 import sys
 from typing import Optional, Sequence
 
+import numpy as np
 import torch
 
 from .config import Config, parse_args
@@ -47,6 +48,8 @@ def run_worker(config: Config):
                        max_to_keep=config.max_to_keep)
     sv.prepare(broadcast_fn=lambda: broadcast_flat(ctx, network.online.flat))
 
+    if config.num_actors > 1:
+        return _run_apex(config, ctx, env, network, sv, seed)
     use_device_replay = ctx.device.type == 'cuda' or ctx.enabled
     if use_device_replay:
         frames = config.resize_width > 0 and config.resize_height > 0
@@ -66,6 +69,34 @@ def run_worker(config: Config):
         sv.ckpt.agent_state_fn = agent.agent_state if config.save_agent_state else None
         agent.train(config.num_episodes, config.max_steps_per_episode, sv)
     return agent
+
+
+def _run_apex(config: Config, ctx, env, network, sv, seed: int):
+    """Ape-X rank: ``--num_actors`` CPU actor processes feed this rank's HBM replay
+    shard; a batched GPU inference service answers their greedy actions."""
+    from .actors.apex import ApexActorPool, ApexTrainer
+    from .learner import Learner
+    from .replay import DeviceReplay
+    from .utils.metrics import JsonlWriter
+    frames = config.resize_width > 0 and config.resize_height > 0
+    hw = (config.resize_height, config.resize_width) if frames else None
+    obs_shape = hw if frames else tuple(env.observation_space.shape)
+    obs_dim = 0 if frames else int(np.prod(obs_shape))
+    replay = DeviceReplay(config.replay_memory_capacity, obs_shape, config.frames_per_state if frames else 1,
+                          device=ctx.device, num_actors=config.num_actors, prioritized=config.prioritized_replay,
+                          alpha=config.per_alpha, seed=seed + ctx.rank)
+    learner = Learner(network, replay, config, ctx)
+    learner.update_target_now()
+    pool = ApexActorPool(config.env, config.num_actors, config.frames_per_state if frames else 1, hw, obs_dim,
+                         env.action_space.n, config.max_steps_per_episode, seed=seed + 100003 * ctx.rank,
+                         eps_base=config.apex_eps_base, eps_alpha=config.apex_eps_alpha,
+                         ring_capacity=config.apex_ring, reward_clip=config.reward_clip,
+                         n_step=config.n_step, gamma=config.reward_discount)
+    metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))
+    with sv.managed():
+        trainer = ApexTrainer(network, replay, learner, pool, config, metrics=metrics)
+        trainer.run(max_train_steps=config.max_train_steps, supervisor=sv)
+    return trainer
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:

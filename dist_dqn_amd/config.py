@@ -128,7 +128,11 @@ def build_parser() -> argparse.ArgumentParser:
     a('--per_beta_steps', default=1000000, type=int)
     a('--per_eps', default=1e-6, type=float)
     a('--num_actors', default=1, type=int, help='Ape-X actor count')
-    a('--actor_param_sync_freq', default=400, type=int)
+    a('--actor_param_sync_freq', default=400, type=int,
+      help='Ape-X: learner steps between the inference service\'s parameter snapshots (0 = live weights)')
+    a('--apex_eps_base', default=0.4, type=float, help='Ape-X per-actor epsilon base')
+    a('--apex_eps_alpha', default=7.0, type=float, help='Ape-X per-actor epsilon exponent spread')
+    a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
     a('--allreduce', default='rccl', choices=['rccl', 'oneshot'])
     a('--grad_bucket_mb', default=4.0, type=float)
     a('--hip_graph', default=1, type=int, help='Capture the learner step in a HIP graph')
@@ -203,6 +207,9 @@ class Config:
     per_eps: float = 1e-6
     num_actors: int = 1
     actor_param_sync_freq: int = 400
+    apex_eps_base: float = 0.4
+    apex_eps_alpha: float = 7.0
+    apex_ring: int = 1024
     allreduce: str = 'rccl'
     grad_bucket_mb: float = 4.0
     hip_graph: int = 1

@@ -134,6 +134,27 @@ class DeviceReplay:
         if len(self._st_trans) >= self._stage_size:
             self.flush()
 
+    def add_step_nstep(self, acc, action: int, reward: float, next_obs, done: bool, actor: int = 0):
+        """add_step through an n-step accumulator (replay.nstep.NStepAccumulator) owned by
+        the caller, one per actor: frame stacks stay slot lists, so an n-step transition
+        costs no extra frame storage."""
+        if self.frame_mode:
+            st = self._stacks[actor]
+            assert st is not None, 'begin_episode() first'
+            slot = self.write_frame(next_obs)
+            nxt = st[1:] + [slot]
+            self._stacks[actor] = nxt
+            for s, a, R, ns, d, g in acc.push(list(st), action, reward, nxt, done):
+                self.add_transition(s, ns[-1], a, R, d, g)
+        else:
+            prev = self._last_obs[actor]
+            cur = np.asarray(next_obs, dtype=np.float32).reshape(-1)
+            self._last_obs[actor] = cur
+            for s, a, R, ns, d, g in acc.push(prev, action, reward, cur, done):
+                self._st_trans.append((s, ns, int(a), float(R), float(d), float(g)))
+            if len(self._st_trans) >= self._stage_size:
+                self.flush()
+
     def add_transition(self, state_slots, next_slot, action, reward, done, gamma_n=1.0):
         """Low-level add with explicit frame slots (n-step / Ape-X actors)."""
         self._st_trans.append((list(state_slots), int(next_slot), int(action), float(reward),

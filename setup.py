@@ -7,6 +7,8 @@ A direct hipcc build (no hipify pass, no CUDA compatibility layer):
   * csrc/host/*.cpp      -> g++ (C++ host runtime: preprocessing, SPSC rings, CRC32C)
   * csrc/*bindings.cpp   -> hipcc host compile with the torch headers
   * link                 -> hipcc -shared with libtorch / libamdhip64
+  * csrc/host/*.cpp also -> dist_dqn_amd/libdqn_host.so (no torch/HIP: loaded by
+                            CPU actor processes through ctypes)
 Objects go to build/ and are rebuilt when the source or any csrc header is newer.
 """
 import concurrent.futures as cf
@@ -21,6 +23,7 @@ ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 HIPCC = os.path.join(os.environ.get('ROCM_PATH', '/opt/rocm'), 'bin', 'hipcc')
 BUILD = os.path.join(ROOT, 'build', 'obj')
 OUT = os.path.join(ROOT, 'dist_dqn_amd', '_C' + sysconfig.get_config_var('EXT_SUFFIX'))
+HOST_OUT = os.path.join(ROOT, 'dist_dqn_amd', 'libdqn_host.so')   # torch-free host runtime (ctypes)
 
 
 def _torch_flags():
@@ -86,6 +89,9 @@ def build(verbose=False, jobs=None):
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for f in cf.as_completed([ex.submit(run, c) for c in cmds]):
             f.result()
+    host_objs = [o for o in objs if os.path.basename(o).startswith('host_')]
+    if cmds or not os.path.exists(HOST_OUT):
+        run(['g++', '-shared', '-fPIC', '-o', HOST_OUT] + host_objs + ['-lpthread'])
     if cmds or not os.path.exists(OUT):
         link = [HIPCC, '-shared', '-fPIC', '-o', OUT] + objs + ['-L' + d for d in libdirs] + \
                ['-Wl,-rpath,' + d for d in libdirs] + \

@@ -1,0 +1,114 @@
+"""Ape-X acting path: the torch-free host runtime
+(SPSC rings + inference mailboxes, also under ThreadSanitizer), the actor pool's
+processes / shared memory lifecycle, and end-to-end Ape-X training on the CPU."""
+import glob
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from dist_dqn_amd.actors.apex import HEADER, ApexActorPool, apex_epsilons
+from dist_dqn_amd.config import parse_args
+from dist_dqn_amd.native import load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_ring_roundtrip_and_backpressure():
+    L = load()
+    rec = 24
+    buf = np.zeros(L.ring_bytes(8, rec), dtype=np.uint8)
+    L.ring_init(buf, 8, rec)
+    recs = np.arange(10 * rec, dtype=np.uint8).reshape(10, rec)
+    assert L.ring_push(buf, recs, 10) == 8            # full after capacity
+    assert L.ring_size(buf) == 8
+    out = np.zeros((10, rec), dtype=np.uint8)
+    assert L.ring_pop(buf, out, 5) == 5
+    np.testing.assert_array_equal(out[:5], recs[:5])
+    assert L.ring_push(buf, recs[8:], 2) == 2          # wraps around
+    assert L.ring_pop(buf, out, 10) == 5
+    np.testing.assert_array_equal(out[:3], recs[5:8])
+    np.testing.assert_array_equal(out[3:5], recs[8:10])
+
+
+def test_mailbox_protocol_single_process():
+    L = load()
+    n, sb = 3, 8
+    region = np.zeros(L.mbox_region_bytes(n, sb), dtype=np.uint8)
+    L.mbox_init(region, n, sb)
+    st = np.full(sb, 5, dtype=np.uint8)
+    assert L.mbox_request(region, 1, st, timeout_us=1000) == -1      # nobody serves: timeout
+    states = np.zeros((n, sb), dtype=np.uint8)
+    ids, seq = np.zeros(n, np.int32), np.zeros(n, np.uint64)
+    m = L.mbox_collect(region, n, sb, states, ids, seq, n)
+    assert m == 1 and ids[0] == 1 and states[0, 0] == 5                # the posted request is pending
+    L.mbox_respond(region, sb, ids, seq, np.array([4], np.int32), 1)
+    assert L.mbox_collect(region, n, sb, states, ids, seq, n) == 0
+    L.mbox_set_stop(region, 1)
+    assert L.mbox_stopped(region) and L.mbox_request(region, 0, st) == -2
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+def test_host_runtime_under_thread_sanitizer(tmp_path):
+    exe = str(tmp_path / 'host_stress')
+    src = [os.path.join(ROOT, 'csrc', 'host', f) for f in ('tests/host_stress.cpp', 'spsc_ring.cpp', 'mailbox.cpp')]
+    r = subprocess.run(['g++', '-std=c++17', '-O1', '-g', '-fsanitize=thread', '-o', exe] + src + ['-lpthread'],
+                       capture_output=True, text=True)
+    if r.returncode != 0 and 'tsan' in (r.stderr + r.stdout).lower():
+        pytest.skip('ThreadSanitizer runtime unavailable')
+    assert r.returncode == 0, r.stderr
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, TSAN_OPTIONS='halt_on_error=1'))
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert 'ThreadSanitizer' not in run.stderr, run.stderr
+    assert 'ring errors 0, mailbox errors 0' in run.stdout
+
+
+def test_apex_epsilons():
+    e = apex_epsilons(8)
+    assert e[0] == pytest.approx(0.4) and e[-1] == pytest.approx(0.4 ** 8)
+    assert all(a > b for a, b in zip(e, e[1:]))
+
+
+def test_pool_serves_and_drains_image_actors():
+    """Synthetic Atari actors: C++ preprocessing, frame records, batched serving."""
+    from dist_dqn_amd.replay import DeviceReplay
+    pool = ApexActorPool('Pong-v0', 2, 4, (84, 84), 0, 6, max_steps_per_episode=50, seed=1,
+                         ring_capacity=64, max_frames_per_actor=120)
+    rep = DeviceReplay(1000, (84, 84), 4, device='cpu', num_actors=2)
+    seen = []
+
+    def q_fn(batch):
+        assert batch.shape[1:] == (84, 84, 4) and batch.dtype == np.uint8
+        seen.append(len(batch))
+        return np.zeros(len(batch), dtype=np.int64)
+
+    import time
+    with pool:
+        t0 = time.time()
+        while pool.frames < 240 and time.time() - t0 < 60:
+            pool.serve(q_fn)
+            pool.drain(rep)
+        paths = (pool.ring_path, pool.mbox_path)
+    assert pool.frames == 240 and rep.size() == 240          # every env step became a transition
+    assert pool.episodes >= 4 and pool.served > 0 and max(seen) >= 1
+    assert not any(os.path.exists(p) for p in paths)         # shared memory removed
+    # stacks are rebuilt from frame slots: s' of a transition == s of the next one (same episode)
+    st, nx = rep.state_idx.numpy(), rep.next_idx.numpy()
+    d = rep.dones.numpy()
+    i = int(np.argmax(d == 0))
+    assert list(st[i + 1]) == list(st[i, 1:]) + [nx[i]] or d[i]
+
+
+def test_apex_cartpole_end_to_end(tmp_path):
+    from dist_dqn_amd.cli import run_worker
+    cfg = parse_args(['--env=CartPole-v0', '--network=simple', '--optimizer=adam', '--lr=0.001',
+                      '--minibatch_size=32', '--num_actors=3', '--replay_memory_capacity=5000',
+                      '--max_train_steps=200', '--device=cpu', '--logdir=%s' % tmp_path, '--checkpoint_secs=0',
+                      '--replay_start_size=200', '--n_step=3', '--actor_param_sync_freq=50'])
+    tr = run_worker(cfg)
+    assert tr.learner.train_steps == 200 and tr.pool.frames >= 200
+    assert tr.pool.episodes > 0 and tr.pool.served > 0 and tr.pool.alive() == 0
+    assert not glob.glob(tr.pool.ring_path + '*')
