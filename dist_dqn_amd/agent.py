@@ -209,7 +209,7 @@ class DQNAgent:
             next_state = self.frame_buffer.get_state()
             self._store(state, action, reward, next_state, terminal, frame)
             state = next_state
-            if self._device_replay and self.replay_memory.size() + len(self.replay_memory._st_trans) >= prefill_size:
+            if self._device_replay and self.replay_memory.size() + self.replay_memory.staged() >= prefill_size:
                 self.replay_memory.flush()
         if self._device_replay:
             self.replay_memory.flush()

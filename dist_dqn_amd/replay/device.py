@@ -37,6 +37,45 @@ import torch
 from ..ops import kernels
 
 
+class _StageSet:
+    """Persistent host staging buffers (pinned when the replay is on the GPU), exposed
+    both as torch tensors (copy sources) and as numpy views (cheap per-step writes)."""
+
+    def __init__(self, rep: 'DeviceReplay', n: int):
+        pin = rep.device.type == 'cuda'
+
+        def buf(shape, dtype):
+            t = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+            return t, t.numpy()
+
+        if rep.frame_mode:
+            H, W = rep.obs_shape
+            # every transition writes one frame, a reset one more: <= 2 frames per transition
+            self.t_frames, self.frames = buf((2 * n + rep.k + 8, H, W), torch.uint8)
+            self.t_sidx, self.sidx = buf((n, rep.k), torch.int32)
+            self.t_nidx, self.nidx = buf((n,), torch.int32)
+        else:
+            self.t_frames, self.frames = buf((0,), torch.uint8)
+            D = int(np.prod(rep.obs_shape))
+            self.t_obs, self.obs = buf((n, D), torch.float32)
+            self.t_nobs, self.nobs = buf((n, D), torch.float32)
+        self.t_act, self.act = buf((n,), torch.int32)
+        self.t_rew, self.rew = buf((n,), torch.float32)
+        self.t_done, self.done = buf((n,), torch.float32)
+        self.t_gam, self.gam = buf((n,), torch.float32)
+        self.nf = self.nt = 0
+        self.event = None
+
+    def record(self, stream):
+        self.event = torch.cuda.Event()
+        self.event.record(stream)
+
+    def wait(self):
+        if self.event is not None:
+            self.event.synchronize()
+            self.event = None
+
+
 class DeviceReplay:
     def __init__(self, capacity: int, obs_shape: Sequence[int], frames_per_state: int = 1,
                  device='cpu', num_actors: int = 1, prioritized: bool = False,
@@ -79,26 +118,57 @@ class DeviceReplay:
             self.tree = DeviceSumTree(C, dev)
         self._pin = self.device.type == 'cuda'
         self._stage_size = stage_size
-        self._reset_stage()
         self._copy_stream = torch.cuda.Stream(device=self.device) if self._pin else None
+        # two persistent (pinned) staging sets: one fills while the other's H2D copies drain
+        self._sets = [_StageSet(self, stage_size) for _ in range(2 if self._pin else 1)]
+        self._cur = 0
+        self._reset_stage()
         # device-side writers (DeviceActor) keep [t_next, f_next, size] on the GPU
         self.cursor = None
         self.device_writer = False
 
     # ----------------------------------------------------------- staging
     def _reset_stage(self):
-        self._st_frames: List[np.ndarray] = []
+        st = self._sets[self._cur]
+        st.wait()                       # its previous H2D copies must be done before refilling
+        st.nf = st.nt = 0
         self._st_frame_first = self._f_next
-        self._st_trans: List[tuple] = []
         self._st_trans_first = self._t_next
+
+    @property
+    def _stage(self) -> '_StageSet':
+        return self._sets[self._cur]
 
     def _alloc_frame(self, frame) -> int:
         # frame slots are handed out sequentially, so staged frames are one
         # contiguous (wrap-split) range starting at _st_frame_first
+        st = self._stage
+        if st.nf == st.frames.shape[0]:
+            self.flush()
+            st = self._stage
+        st.frames[st.nf] = frame
+        st.nf += 1
         slot = self._f_next
         self._f_next = (self._f_next + 1) % self.num_frames
-        self._st_frames.append(np.asarray(frame, dtype=np.uint8))
         return slot
+
+    def _stage_transition(self, state, nxt, action, reward, done, gamma_n):
+        st = self._stage
+        i = st.nt
+        if self.frame_mode:
+            st.sidx[i] = state
+            st.nidx[i] = nxt
+        else:
+            st.obs[i] = state
+            st.nobs[i] = nxt
+        st.act[i], st.rew[i], st.done[i], st.gam[i] = action, reward, done, gamma_n
+        st.nt = i + 1
+        if st.nt == self._stage_size:
+            self.flush()
+
+    def staged(self) -> int:
+        """Transitions written but not yet flushed to the device."""
+        return self._stage.nt
 
     def size(self) -> int:
         if self.device_writer:
@@ -124,15 +194,13 @@ class DeviceReplay:
             st = self._stacks[actor]
             assert st is not None, 'begin_episode() first'
             slot = self._alloc_frame(next_obs)
-            self._st_trans.append((list(st), slot, int(action), float(reward), float(done), float(gamma_n)))
+            self._stage_transition(st, slot, action, reward, done, gamma_n)
             self._stacks[actor] = st[1:] + [slot]
         else:
             o = self._last_obs[actor]
             n = np.asarray(next_obs, dtype=np.float32).reshape(-1)
-            self._st_trans.append((o, n, int(action), float(reward), float(done), float(gamma_n)))
+            self._stage_transition(o, n, action, reward, done, gamma_n)
             self._last_obs[actor] = n
-        if len(self._st_trans) >= self._stage_size:
-            self.flush()
 
     def add_step_nstep(self, acc, action: int, reward: float, next_obs, done: bool, actor: int = 0):
         """add_step through an n-step accumulator (replay.nstep.NStepAccumulator) owned by
@@ -151,72 +219,68 @@ class DeviceReplay:
             cur = np.asarray(next_obs, dtype=np.float32).reshape(-1)
             self._last_obs[actor] = cur
             for s, a, R, ns, d, g in acc.push(prev, action, reward, cur, done):
-                self._st_trans.append((s, ns, int(a), float(R), float(d), float(g)))
-            if len(self._st_trans) >= self._stage_size:
-                self.flush()
+                self._stage_transition(s, ns, a, R, d, g)
 
     def add_transition(self, state_slots, next_slot, action, reward, done, gamma_n=1.0):
         """Low-level add with explicit frame slots (n-step / Ape-X actors)."""
-        self._st_trans.append((list(state_slots), int(next_slot), int(action), float(reward),
-                               float(done), float(gamma_n)))
-        if len(self._st_trans) >= self._stage_size:
-            self.flush()
+        self._stage_transition(state_slots, next_slot, action, reward, done, gamma_n)
 
     def write_frame(self, frame) -> int:
         return self._alloc_frame(frame)
 
     def flush(self):
-        """Copy staged frames/transitions into the device ring (contiguous, wrap-split)."""
-        assert not self.device_writer or not (self._st_frames or self._st_trans), \
+        """Copy staged frames/transitions into the device ring (contiguous, wrap-split)
+        as async H2D copies on the side stream, then switch staging sets."""
+        st = self._stage
+        assert not self.device_writer or not (st.nf or st.nt), \
             'a replay is fed either by host staging or by device actors, not both'
-        if not self._st_frames and not self._st_trans:
+        if not st.nf and not st.nt:
             return
-        if self._st_frames:
-            arr = np.stack(self._st_frames)
-            self._ring_copy(self.frames, self._st_frame_first, arr)
-        n = len(self._st_trans)
+        cs = self._copy_stream
+        if cs is not None:
+            cs.wait_stream(torch.cuda.current_stream(self.device))   # ring slots may still be read
+        if st.nf:
+            self._ring_copy(self.frames, self._st_frame_first, st.t_frames[:st.nf])
+        n = st.nt
         if n:
             first = self._st_trans_first
             if self.frame_mode:
-                sidx = np.array([t[0] for t in self._st_trans], dtype=np.int32).reshape(n, self.k)
-                nidx = np.array([t[1] for t in self._st_trans], dtype=np.int32)
-                self._ring_copy(self.state_idx, first, sidx)
-                self._ring_copy(self.next_idx, first, nidx)
+                self._ring_copy(self.state_idx, first, st.t_sidx[:n])
+                self._ring_copy(self.next_idx, first, st.t_nidx[:n])
             else:
-                self._ring_copy(self.obs, first, np.stack([t[0] for t in self._st_trans]))
-                self._ring_copy(self.next_obs, first, np.stack([t[1] for t in self._st_trans]))
-            self._ring_copy(self.actions, first, np.array([t[2] for t in self._st_trans], dtype=np.int32))
-            self._ring_copy(self.rewards, first, np.array([t[3] for t in self._st_trans], dtype=np.float32))
-            self._ring_copy(self.dones, first, np.array([t[4] for t in self._st_trans], dtype=np.float32))
-            self._ring_copy(self.gammas, first, np.array([t[5] for t in self._st_trans], dtype=np.float32))
+                self._ring_copy(self.obs, first, st.t_obs[:n])
+                self._ring_copy(self.next_obs, first, st.t_nobs[:n])
+            self._ring_copy(self.actions, first, st.t_act[:n])
+            self._ring_copy(self.rewards, first, st.t_rew[:n])
+            self._ring_copy(self.dones, first, st.t_done[:n])
+            self._ring_copy(self.gammas, first, st.t_gam[:n])
             self._t_next = (first + n) % self.capacity
             self._size = min(self.capacity, self._size + n)
             if self.prioritized:
                 idx = (torch.arange(n, dtype=torch.int64) + first) % self.capacity
                 self.tree.set_max_priority(idx.to(self.device, torch.int32))
+        if cs is not None:
+            st.record(cs)
         self._sync_copies()
         self.size_dev.fill_(self._size)
+        self._cur = (self._cur + 1) % len(self._sets)
         self._reset_stage()
 
-    def _ring_copy(self, dst: torch.Tensor, first: int, src: np.ndarray):
+    def _ring_copy(self, dst: torch.Tensor, first: int, src: torch.Tensor):
         cap = dst.shape[0]
         n = src.shape[0]
-        t = torch.from_numpy(np.ascontiguousarray(src))
-        if self._pin:
-            t = t.pin_memory()
         end = first + n
         if end <= cap:
-            self._copy(dst[first:end], t)
+            self._copy(dst[first:end], src)
         else:
             k = cap - first
-            self._copy(dst[first:], t[:k])
-            self._copy(dst[:end - cap], t[k:])
+            self._copy(dst[first:], src[:k])
+            self._copy(dst[:end - cap], src[k:])
 
     def _copy(self, dst, src):
         if self._copy_stream is not None:
             with torch.cuda.stream(self._copy_stream):
                 dst.copy_(src, non_blocking=True)
-                src.record_stream(self._copy_stream) if src.is_cuda else None
         else:
             dst.copy_(src)
 

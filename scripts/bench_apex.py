@@ -1,0 +1,59 @@
+"""Ape-X throughput (BASELINE.json config 4, single rank): N CPU actor processes
+(synthetic Atari, C++ preprocessing) -> SPSC rings -> HBM PER replay shard,
+batched GPU inference service, Double+Dueling n-step learner on the HIP executor.
+
+    python scripts/bench_apex.py --actors 16 --seconds 60
+
+Prints one JSON line: env frames/s (all actors), SGD steps/s, served batch stats.
+"""
+import argparse
+import json
+import logging
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--actors', type=int, default=min(16, os.cpu_count() or 4))
+    ap.add_argument('--seconds', type=float, default=60.0)
+    ap.add_argument('--capacity', type=int, default=200000)
+    ap.add_argument('--extra', default='')
+    args = ap.parse_args()
+    logging.basicConfig(level=logging.INFO, format='%(asctime)s %(name)s: %(message)s')
+    import torch
+    from dist_dqn_amd.actors.apex import ApexActorPool, ApexTrainer
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    dev = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
+    cfg = preset('apex', 'Pong-v0', '--num_actors=%d --replay_memory_capacity=%d --replay_start_size=2000 '
+                 '--logdir=%s %s' % (args.actors, args.capacity, tempfile.mkdtemp(), args.extra))
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=dev)
+    rep = DeviceReplay(cfg.replay_memory_capacity, (84, 84), 4, device=dev, num_actors=cfg.num_actors,
+                       prioritized=cfg.prioritized_replay, alpha=cfg.per_alpha, seed=1)
+    ln = Learner(net, rep, cfg)
+    pool = ApexActorPool(cfg.env, cfg.num_actors, 4, (84, 84), 0, 6, cfg.max_steps_per_episode, seed=1,
+                         eps_base=cfg.apex_eps_base, eps_alpha=cfg.apex_eps_alpha, ring_capacity=cfg.apex_ring,
+                         n_step=cfg.n_step, gamma=cfg.reward_discount)
+    tr = ApexTrainer(net, rep, ln, pool, cfg)
+    t0 = time.time()
+    tr.run(max_seconds=args.seconds, log_every=10.0)
+    wall = time.time() - t0
+    print(json.dumps({
+        'metric': 'Ape-X env frames/sec + learner SGD steps/sec (1 rank)', 'actors': cfg.num_actors,
+        'seconds': round(wall, 1), 'env_frames': pool.frames, 'env_frames_per_sec': round(pool.frames / wall, 1),
+        'sgd_steps': ln.train_steps, 'sgd_steps_per_sec': round(ln.train_steps / wall, 1),
+        'greedy_actions_served': pool.served, 'serve_calls': tr.serve_calls,
+        'mean_serve_batch': round(pool.served / max(1, tr.serve_calls), 2), 'executor': net.executor.name,
+        'config': 'apex preset: double+dueling, PER, n_step=3, nature-cnn', 'dtype': net.executor.compute_dtype,
+        'device': str(dev)}))
+
+
+if __name__ == '__main__':
+    main()

@@ -95,11 +95,12 @@ def test_pool_serves_and_drains_image_actors():
     assert pool.frames == 240 and rep.size() == 240          # every env step became a transition
     assert pool.episodes >= 4 and pool.served > 0 and max(seen) >= 1
     assert not any(os.path.exists(p) for p in paths)         # shared memory removed
-    # stacks are rebuilt from frame slots: s' of a transition == s of the next one (same episode)
-    st, nx = rep.state_idx.numpy(), rep.next_idx.numpy()
-    d = rep.dones.numpy()
-    i = int(np.argmax(d == 0))
-    assert list(st[i + 1]) == list(st[i, 1:]) + [nx[i]] or d[i]
+    # stacks are rebuilt from frame slots per actor: the s' of every transition that was
+    # followed by another step of its episode is the s of that later transition
+    st, nx = rep.state_idx.numpy()[:240], rep.next_idx.numpy()[:240]
+    states = {tuple(r) for r in st}
+    follow = [tuple(st[i, 1:]) + (nx[i],) in states for i in range(240)]
+    assert sum(follow) >= 240 - 2 * 4        # all but the last step of each (cut) episode
 
 
 def test_apex_cartpole_end_to_end(tmp_path):
