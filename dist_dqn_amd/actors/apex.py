@@ -349,13 +349,17 @@ class ApexTrainer:
             return q.argmax(1).to(torch.int32).cpu().numpy()
 
     def _serve_loop(self):
+        from ..utils.trace import trace
         while not self._stop.is_set():
-            if self.pool.serve(self._q_actions) == 0:
+            with trace('apex.serve'):
+                m = self.pool.serve(self._q_actions)
+            if m == 0:
                 time.sleep(0.0002)
             else:
                 self.serve_calls += 1
 
     def run(self, max_train_steps: int = 0, max_seconds: float = 0.0, supervisor=None, log_every: float = 10.0):
+        from ..utils.trace import trace
         cfg = self.config
         start = max(cfg.minibatch_size, cfg.replay_start_size)
         self.pool.start()
@@ -364,7 +368,8 @@ class ApexTrainer:
         steps_at_last = frames_at_last = 0
         try:
             while True:
-                self.pool.drain(self.replay)
+                with trace('apex.drain'):
+                    self.pool.drain(self.replay)
                 if self.replay.size() >= start:
                     self.learner.step()
                     if self._snap is not None and self.learner.train_steps % self.sync_freq == 0:

@@ -16,6 +16,7 @@ import torch
 
 from ..ops import _ext
 from ..replay.device import DeviceReplay
+from ..utils.trace import trace
 
 
 class DeviceActor:
@@ -75,6 +76,10 @@ class DeviceActor:
             self._one()
 
     def step(self):
+        with trace('actor.step'):
+            self._step()
+
+    def _step(self):
         if not self.use_graph or self._warm < 2:
             self._body()
             self._warm += 1

@@ -28,6 +28,7 @@ from .models.network import Network
 from .ops import kernels
 from .parallel.dist import DistContext
 from .parallel.dp import GradAllReducer
+from .utils.trace import trace
 
 log = logging.getLogger(__name__)
 
@@ -127,6 +128,10 @@ class Learner:
     # ------------------------------------------------------------- public
     def step(self) -> torch.Tensor:
         """One SGD step. Returns the (device) TD-loss tensor; no host sync."""
+        with trace('learner.step'):
+            return self._step()
+
+    def _step(self) -> torch.Tensor:
         if not self.use_graph or (self._graphs is None and self._warm < 2):
             # eager path; on the GPU the first two steps also warm up the
             # allocator, kernels and RCCL communicators before capture
@@ -138,7 +143,8 @@ class Learner:
                 self._capture()      # records only; the replay below runs the step
             self._graphs[0].replay()
             if len(self._graphs) > 1:
-                self.reducer.allreduce()
+                with trace('allreduce'):
+                    self.reducer.allreduce()
                 self._graphs[1].replay()
         self.train_steps += 1
         return self.loss
