@@ -82,6 +82,15 @@ struct HeadArgs {
   float* zero_ptr; int zero_n;   // grad range zeroed in-kernel (conv wgrads accumulate atomically)
   int has_actor;                 // infer mode: run the fused actor step on the Q tile
   ActorArgs actor;
+  int atoms;                     // C51 head (rainbow.hip): atoms per action, support [vmin, vmax]
+  float vmin, vmax;
+};
+
+// One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =
+// mu + sigma * f(noise[ein_off + k]) * f(noise[eout_off + n]); sigma_off < 0: plain
+// copy; ein_off < 0: bias (no input factor).
+struct NoisyJob {
+  int mu_off, sigma_off, K, N, ein_off, eout_off, pad0, pad1;
 };
 
 // Fused per-sample Nature trunk (trunk.hip): conv1 -> conv2 -> conv3 in one launch.
@@ -111,3 +120,9 @@ int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
 void launch_trunk_fwd(const dqn::TrunkArgs& a, int B, int ninst, hipStream_t st);
+void launch_c51_head(const dqn::HeadArgs& a, hipStream_t st);
+size_t c51_head_lds_bytes(const dqn::HeadArgs& a);
+void launch_noisy_mix(const float* flat, float* eff, const float* noise, const dqn::NoisyJob* jobs, int njobs,
+                      int max_elems, hipStream_t st);
+void launch_noisy_grad(float* grad, const float* noise, const dqn::NoisyJob* jobs, int njobs, int max_elems,
+                       hipStream_t st);

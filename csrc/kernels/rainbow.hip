@@ -1,0 +1,337 @@
+// Rainbow pieces of the HIP executor: the C51 distributional head and the
+// factorised-Gaussian noisy-layer parameter mix / gradient split.
+//
+// Reference: the reference has scalar heads only (/root/reference/src/network.py:401-409);
+// C51 (Bellemare et al. 2017) and noisy nets (Fortunato et al. 2018) are the
+// BASELINE.json config-5 extensions. Torch oracles: dist_dqn_amd/models/losses.py
+// (c51_loss, categorical_projection) and models/torch_net.py (_dense with noise).
+//
+//   c51_head_kernel   logits [B][A*N] (+ dueling value [B][N]) on MFMA for up to
+//                     3 instances, dueling combine per atom, softmax with one
+//                     wave64 per (sample, action) row (lanes = atoms, N <= 64),
+//                     Double-DQN action choice, categorical projection through
+//                     LDS float atomics, cross-entropy loss / priorities, and the
+//                     output-layer backward (dW, db, dWv, dbv, dH masked by ReLU).
+//                     Acting mode: Q = sum_n p_n z_n -> q_out / fused actor step.
+//   noisy_mix_kernel  eff = mu + sigma * f(eps_in) f(eps_out)^T (f(x) = sgn(x) sqrt|x|),
+//                     plain copy for deterministic tensors: the executor packs
+//                     and reads the effective parameters from `eff`.
+//   noisy_grad_kernel dL/dsigma = dL/dW_eff * f(eps_in) f(eps_out)^T (bias: * f(eps_out));
+//                     the conv/dense backward writes dL/dW_eff into the mu slots.
+#include "common.h"
+#include "actor_dev.h"
+#include "../include/dqn_nets_k.h"
+
+namespace dqn {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+
+DQN_DEV bfx8 rz8() {
+  bfx8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  return z;
+}
+
+// logits of one instance -> lg [B][NO] (+ vl [B][NA] for dueling), bias added
+DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int lane, int wave, int nwave) {
+  const int B = a.B, NA = a.atoms, NO = a.A * NA, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
+  const int N16 = (NO + 15) / 16, N16v = (NA + 15) / 16, mtiles = (B + 15) / 16, K32 = HID / 32;
+  const int ntask = mtiles * (N16 + (a.dueling ? N16v : 0));
+  const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
+  const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
+  const int kg = 8 * (lane >> 4);
+  for (int task = wave; task < ntask; task += nwave) {
+    const int mt = task % mtiles, t2 = task / mtiles;
+    const bool val = t2 >= N16;                              // dueling value-stream tile
+    const int nt = val ? t2 - N16 : t2;
+    const int b_row = mt * 16 + (lane & 15);
+    const bool rok = b_row < B;
+    const __bf16* hrow = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)(rok ? b_row : 0) * HH;
+    const __bf16* src = (a.dueling && !val) ? hrow + HID : hrow;  // [value | advantage] halves of h
+    const bfx8* W = val ? pv : pw;
+    const int n16 = val ? N16v : N16;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < K32; ks += 4) {
+      bfx8 af[4], bf[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        af[u] = rok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : rz8();
+        bf[u] = W[((ks + u) * n16 + nt) * 64 + lane];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bf[u], acc, 0, 0, 0);
+    }
+    const int col = nt * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = mt * 16 + 4 * (lane >> 4) + r;
+      if (b >= B) continue;
+      if (val) {
+        if (col < NA) vl[b * NA + col] = acc[r] + a.bv[inst][col];
+      } else if (col < NO) {
+        lg[b * NO + col] = acc[r] + a.b[inst][col];
+      }
+    }
+  }
+}
+
+// dueling combine per atom, then in-place softmax of every (b, a) row (one wave
+// per row, lane = atom). If logp != nullptr the log-probabilities of each
+// sample's TAKEN action row are kept there ([B][NA]).
+DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* logp, int tid, int nth, int lane,
+                         int wave, int nwave) {
+  const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
+  if (a.dueling) {
+    for (int t = tid; t < B * NA; t += nth) {
+      const int b = t / NA, n = t - b * NA;
+      float mean = 0.f;
+      for (int i = 0; i < A; ++i) mean += lg[b * NO + i * NA + n];
+      mean /= (float)A;
+      const float v = vl[b * NA + n] - mean;
+      for (int i = 0; i < A; ++i) lg[b * NO + i * NA + n] += v;
+    }
+    __syncthreads();
+  }
+  for (int row = wave; row < B * A; row += nwave) {
+    const int b = row / A, i = row - b * A;
+    float* r = lg + b * NO + i * NA;
+    const float x = lane < NA ? r[lane] : -INFINITY;
+    const float mx = wave_max(x);
+    const float e = lane < NA ? __expf(x - mx) : 0.f;
+    const float s = wave_sum(e);
+    if (lane < NA) {
+      r[lane] = e / s;
+      if (logp != nullptr && i == a.act[b]) logp[b * NA + lane] = (x - mx) - __logf(s);
+    }
+  }
+  __syncthreads();
+}
+
+DQN_DEV float c51_z(const HeadArgs& a, int n) {
+  return a.vmin + (a.vmax - a.vmin) * (float)n / (float)(a.atoms - 1);
+}
+
+__global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
+  float* lg = sm;                       // [B][NO] logits -> probabilities
+  float* vl = lg + B * NO;              // [B][NA] dueling value logits
+  float* mt = vl + B * NA;              // [B][NA] projected target distribution
+  float* lp = mt + B * NA;              // [B][NA] log p of the taken action (online s)
+  float* q = lp + B * NA;               // [B][A] expected Q (selection / acting)
+  float* red = q + B * A;               // [32]
+  int* astar = reinterpret_cast<int*>(red + 32);   // [B]
+  int* sdone = astar + B;               // [E] fused actor scratch
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
+  const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  if (a.zero_ptr != nullptr) {
+    float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
+    for (int t = blockIdx.x * nth + tid; t < a.zero_n / 4; t += gridDim.x * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto expected_q = [&]() {             // q[b][i] = sum_n p z_n  (one wave per row)
+    for (int row = wave; row < B * A; row += nwave) {
+      const float* r = lg + row * NA;
+      const float s = wave_sum(lane < NA ? r[lane] * c51_z(a, lane) : 0.f);
+      if (lane == 0) q[row] = s;
+    }
+    __syncthreads();
+  };
+  if (a.infer) {
+    c51_logits(a, 0, lg, vl, lane, wave, nwave);
+    __syncthreads();
+    c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
+    expected_q();
+    if (a.q_out != nullptr)
+      for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
+    if (a.has_actor) actor_step_block(a.actor, q, sdone);
+    return;
+  }
+  // ---- 1. action choice on s' (Double DQN: online net, else the target net)
+  const int sel = ninst == 3 ? 2 : 1;
+  c51_logits(a, sel, lg, vl, lane, wave, nwave);
+  __syncthreads();
+  c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
+  expected_q();
+  for (int b = tid; b < B; b += nth) {
+    int best = 0;
+    float bv = q[b * A];
+    for (int i = 1; i < A; ++i) if (q[b * A + i] > bv) { bv = q[b * A + i]; best = i; }
+    astar[b] = best;
+  }
+  __syncthreads();
+  // ---- 2. target distribution of a* projected onto the support
+  if (sel != 1) {
+    c51_logits(a, 1, lg, vl, lane, wave, nwave);
+    __syncthreads();
+    c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
+  }
+  for (int t = tid; t < B * NA; t += nth) mt[t] = 0.f;
+  __syncthreads();
+  {
+    const float dz = (a.vmax - a.vmin) / (float)(NA - 1);
+    for (int b = wave; b < B; b += nwave) {
+      if (lane < NA) {
+        const float p = lg[b * NO + astar[b] * NA + lane];
+        float tz = a.rew[b] + a.gam[b] * (1.f - a.done[b]) * c51_z(a, lane);
+        tz = fminf(fmaxf(tz, a.vmin), a.vmax);
+        const float bj = (tz - a.vmin) / dz;
+        const float lo = floorf(bj), hi = ceilf(bj);
+        const int l = (int)lo, u = (int)hi;
+        atomicAdd(&mt[b * NA + l], p * (hi - bj + (l == u ? 1.f : 0.f)));
+        atomicAdd(&mt[b * NA + u], p * (bj - lo));
+      }
+    }
+  }
+  // ---- 3. online distribution of (s, a): cross-entropy, d logits
+  __syncthreads();                      // projection reads of lg done, its atomics complete
+  c51_logits(a, 0, lg, vl, lane, wave, nwave);
+  __syncthreads();
+  c51_softmax(a, lg, vl, lp, tid, nth, lane, wave, nwave);
+  float contrib = 0.f;
+  for (int b = wave; b < B; b += nwave) {
+    const float ce = -wave_sum(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
+    const float w = a.wts != nullptr ? a.wts[b] : 1.f;
+    if (lane < NA) {   // d(mean w*CE)/d logit of the taken action = w/B (p - m); reuse lp for it
+      const float p = lg[b * NO + a.act[b] * NA + lane];
+      lp[b * NA + lane] = w / (float)B * (p - mt[b * NA + lane]);
+    }
+    if (lane == 0) {
+      contrib += w * ce;
+      if (blockIdx.x == 0) a.prio[b] = ce;
+    }
+  }
+  {
+    const float s = wave_sum(contrib);
+    if (lane == 0) red[wave] = s;
+  }
+  __syncthreads();
+  if (tid == 0 && blockIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < nwave; ++i) s += red[i];
+    a.loss[0] = s / (float)B;
+  }
+  // ---- 4. output-layer backward (online instance 0), partitioned over the blocks.
+  // g[b][n] = lp (d logit of the taken action); advantage/plain output j = i*NA + n:
+  //   dOut[b][j] = g[b][n] * ((i == act_b) - (dueling ? 1/A : 0)),  dV[b][n] = g[b][n]
+  const float inva = a.dueling ? 1.f / (float)A : 0.f;
+  auto dout = [&](int b, int j) {
+    const int i = j / NA, n = j - i * NA;
+    return lp[b * NA + n] * ((i == a.act[b] ? 1.f : 0.f) - inva);
+  };
+  const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
+  const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
+  const __bf16* ha0 = a.dueling ? h0 + HID : h0;
+  for (int t = gt; t < HID * NO; t += gn) {             // dW[k][j], k fastest -> coalesced h reads
+    const int j = t / HID, k = t - j * HID;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += (float)ha0[(int64_t)b * HH + k] * dout(b, j);
+    a.dw[(int64_t)k * NO + j] = s;
+  }
+  for (int j = gt; j < NO; j += gn) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dout(b, j);
+    a.db[j] = s;
+  }
+  if (a.dueling) {
+    for (int t = gt; t < HID * NA; t += gn) {
+      const int n = t / HID, k = t - n * HID;
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += (float)h0[(int64_t)b * HH + k] * lp[b * NA + n];
+      a.dwv[(int64_t)k * NA + n] = s;
+    }
+    for (int n = gt; n < NA; n += gn) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += lp[b * NA + n];
+      a.dbv[n] = s;
+    }
+  }
+  // dH[b][k] = (sum_j dOut[b][j] W[k][j] (+ sum_n dV[b][n] Wv[k][n])) * (H > 0)
+  __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
+  const float* W0 = a.w[0];
+  for (int t = gt; t < B * HH; t += gn) {
+    const int b = t / HH, k = t - b * HH;
+    float s = 0.f;
+    if (a.dueling && k < HID) {
+      const float* wv = a.wv[0] + (int64_t)k * NA;
+      for (int n = 0; n < NA; ++n) s += lp[b * NA + n] * wv[n];
+    } else {
+      const int kk = a.dueling ? k - HID : k;
+      const float* w = W0 + (int64_t)kk * NO;
+      const int at = a.act[b];
+      // dOut is nonzero on the taken action's atoms, and -g/A on every action (dueling)
+      float gsum = 0.f;
+      for (int n = 0; n < NA; ++n) {
+        const float g = lp[b * NA + n];
+        s += g * w[at * NA + n];
+        if (a.dueling) {
+          float col = 0.f;
+          for (int i = 0; i < A; ++i) col += w[i * NA + n];
+          gsum += g * col;
+        }
+      }
+      s -= inva * gsum;
+    }
+    const float hval = (float)h0[t];
+    dh[t] = (__bf16)(hval > 0.f ? s : 0.f);
+  }
+}
+
+// ------------------------------------------------------------------ noisy nets
+DQN_DEV float fnoise(float x) { return copysignf(sqrtf(fabsf(x)), x); }
+
+__global__ void __launch_bounds__(256) noisy_mix_kernel(const float* __restrict__ flat, float* __restrict__ eff,
+                                                        const float* __restrict__ noise,
+                                                        const NoisyJob* __restrict__ jobs) {
+  const NoisyJob j = jobs[blockIdx.y];
+  const int n = j.K * j.N;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    float v = flat[j.mu_off + t];
+    if (j.sigma_off >= 0 && noise != nullptr) {
+      const int k = t / j.N, c = t - k * j.N;
+      const float fin = j.ein_off >= 0 ? fnoise(noise[j.ein_off + k]) : 1.f;
+      v += flat[j.sigma_off + t] * fin * fnoise(noise[j.eout_off + c]);
+    }
+    eff[j.mu_off + t] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) noisy_grad_kernel(float* __restrict__ grad, const float* __restrict__ noise,
+                                                         const NoisyJob* __restrict__ jobs) {
+  const NoisyJob j = jobs[blockIdx.y];
+  if (j.sigma_off < 0) return;
+  const int n = j.K * j.N;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const int k = t / j.N, c = t - k * j.N;
+    const float fin = j.ein_off >= 0 ? fnoise(noise[j.ein_off + k]) : 1.f;
+    grad[j.sigma_off + t] = grad[j.mu_off + t] * fin * fnoise(noise[j.eout_off + c]);
+  }
+}
+
+}  // namespace dqn
+
+using namespace dqn;
+
+size_t c51_head_lds_bytes(const HeadArgs& a) {
+  const int B = a.B, NA = a.atoms, NO = a.A * NA;
+  return (size_t)(B * NO + 4 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
+}
+
+void launch_c51_head(const HeadArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(c51_head_kernel, dim3(a.infer ? 1 : 8), dim3(1024), c51_head_lds_bytes(a), st, a);
+}
+
+void launch_noisy_mix(const float* flat, float* eff, const float* noise, const NoisyJob* jobs, int njobs,
+                      int max_elems, hipStream_t st) {
+  int g = (max_elems + 255) / 256;
+  g = g < 1 ? 1 : (g > 512 ? 512 : g);
+  hipLaunchKernelGGL(noisy_mix_kernel, dim3(g, njobs), dim3(256), 0, st, flat, eff, noise, jobs);
+}
+
+void launch_noisy_grad(float* grad, const float* noise, const NoisyJob* jobs, int njobs, int max_elems,
+                       hipStream_t st) {
+  int g = (max_elems + 255) / 256;
+  g = g < 1 ? 1 : (g > 512 ? 512 : g);
+  hipLaunchKernelGGL(noisy_grad_kernel, dim3(g, njobs), dim3(256), 0, st, grad, noise, jobs);
+}

@@ -66,20 +66,20 @@ void wgrad(int64_t kind, int64_t in, std::vector<int64_t> dims, int64_t dz, int6
   TORCH_CHECK(launch_wgrad((int)kind, a, g, cur_stream()) == 0, "unknown wgrad kind ", kind);
 }
 
-void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
-               std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
-               std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
-               std::vector<int64_t> actor, std::vector<double> actor_f) {
-  // ints: B, A, HID, dueling, huber, infer ; flts: delta
+dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int64_t>& h,
+                        const std::vector<int64_t>& w, const std::vector<int64_t>& b, const std::vector<int64_t>& wv,
+                        const std::vector<int64_t>& bv, const std::vector<int64_t>& io, const std::vector<int64_t>& pw,
+                        const std::vector<int64_t>& pwv, const std::vector<int64_t>& zero,
+                        const std::vector<int64_t>& actor, const std::vector<double>& actor_f) {
+  // ints: B, A, HID, dueling, huber, infer
   // io: act, rew, done, gam, wts, loss, prio, q_out, dw, db, dwv, dbv, dh
-  TORCH_CHECK(ints.size() == 6 && flts.size() == 1 && io.size() == 13, "head_loss args");
+  TORCH_CHECK(ints.size() == 6 && io.size() == 13, "head args");
   TORCH_CHECK(ints[1] >= 1 && ints[1] <= 32, "1..32 actions");
   TORCH_CHECK(ints[2] % 128 == 0, "head hidden size must be a multiple of 128");
   dqn::HeadArgs a{};
   a.B = (int)ints[0]; a.A = (int)ints[1]; a.HID = (int)ints[2]; a.dueling = (int)ints[3]; a.huber = (int)ints[4];
   a.infer = (int)ints[5];
-  a.delta = (float)flts[0];
-  TORCH_CHECK(a.HID % 8 == 0, "hidden size must be a multiple of 8");
+  a.atoms = 1; a.vmin = 0.f; a.vmax = 0.f;
   for (size_t i = 0; i < 3; ++i) {
     a.h[i] = i < h.size() ? P<const void*>(h[i]) : nullptr;
     a.w[i] = i < w.size() ? P<const float*>(w[i]) : nullptr;
@@ -114,7 +114,42 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
   a.loss = P<float*>(io[5]); a.prio = P<float*>(io[6]); a.q_out = P<float*>(io[7]);
   a.dw = P<float*>(io[8]); a.db = P<float*>(io[9]); a.dwv = P<float*>(io[10]); a.dbv = P<float*>(io[11]);
   a.dh = P<void*>(io[12]);
+  return a;
+}
+
+void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
+               std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
+               std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
+               std::vector<int64_t> actor, std::vector<double> actor_f) {
+  TORCH_CHECK(flts.size() == 1, "flts = [huber delta]");
+  dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f);
+  a.delta = (float)flts[0];
   launch_head_loss(a, cur_stream());
+}
+
+// C51 head: ints as head_loss; dist = [atoms]; flts = [v_min, v_max]
+void c51_head(std::vector<int64_t> ints, std::vector<int64_t> dist, std::vector<double> flts, std::vector<int64_t> h,
+              std::vector<int64_t> w, std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv,
+              std::vector<int64_t> io, std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
+              std::vector<int64_t> actor, std::vector<double> actor_f) {
+  TORCH_CHECK(dist.size() == 1 && flts.size() == 2, "c51 args");
+  dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f);
+  a.atoms = (int)dist[0]; a.vmin = (float)flts[0]; a.vmax = (float)flts[1];
+  TORCH_CHECK(a.atoms >= 2 && a.atoms <= 64, "C51: 2..64 atoms (one wave64 lane per atom)");
+  TORCH_CHECK(a.vmax > a.vmin, "C51 support");
+  TORCH_CHECK(c51_head_lds_bytes(a) <= 160 * 1024, "C51 head: batch too large for one workgroup's LDS");
+  launch_c51_head(a, cur_stream());
+}
+
+void noisy_mix(int64_t flat, int64_t eff, int64_t noise, int64_t jobs, int64_t njobs, int64_t max_elems) {
+  launch_noisy_mix(P<const float*>(flat), P<float*>(eff), P<const float*>(noise), P<const dqn::NoisyJob*>(jobs),
+                   (int)njobs, (int)max_elems, cur_stream());
+}
+
+void noisy_grad(int64_t grad, int64_t noise, int64_t jobs, int64_t njobs, int64_t max_elems) {
+  TORCH_CHECK(noise != 0, "noisy_grad needs the noise vector");
+  launch_noisy_grad(P<float*>(grad), P<const float*>(noise), P<const dqn::NoisyJob*>(jobs), (int)njobs,
+                    (int)max_elems, cur_stream());
 }
 
 // ptrs per instance (3 entries each, 0 = absent): slots, states, w1, w2, w3, b1, b2, b3, x1, x2, x3
@@ -148,5 +183,9 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_igemm", &igemm);
   m.def("qnet_wgrad", &wgrad);
   m.def("qnet_head_loss", &head_loss);
+  m.def("qnet_c51_head", &c51_head);
+  m.def("qnet_noisy_mix", &noisy_mix);
+  m.def("qnet_noisy_grad", &noisy_grad);
+  m.attr("NOISY_JOB_INTS") = (int)(sizeof(dqn::NoisyJob) / sizeof(int));
   m.attr("PACK_JOB_INTS") = (int)(sizeof(dqn::PackJob) / sizeof(int));
 }

@@ -63,7 +63,8 @@ class DeviceActor:
                                                    self.rng, self.ticket, self.frames_done)]
             ints = [self.E, self.net.arch.num_actions, r.k, r.frames.shape[1] * r.frames.shape[2], r.capacity,
                     r.num_frames]
-            ex.act_fused(self.net.online.flat, r.frames, self.stacks, ptrs, ints, [self.gamma, self.p_done])
+            ex.act_fused(self.net.online.flat, r.frames, self.stacks, ptrs, ints, [self.gamma, self.p_done],
+                         noise=self.net.noise)
             return
         self.ext.stack_states(r.frames, self.stacks, self.states)
         q = self.net.q_values(self.states).float().contiguous()

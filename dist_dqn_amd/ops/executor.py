@@ -11,9 +11,11 @@ i.e. 11 kernels for the whole network + loss + gradient (the torch path runs
 buffer into bf16 MFMA B-fragments once per optimizer step (`repack`), and the
 target's packed copy is refreshed by a predicated copy when the target syncs.
 
-Supported: `nature` convs (84x84x{1..4}... frames packed as 4 uint8
-channels), plain or dueling scalar heads, MSE/Huber, Double DQN, PER weights.
-C51 / noisy heads fall back to the torch executor (`supports()`).
+Supported: `nature` convs (84x84x4 uint8 frames), plain or dueling heads,
+scalar (MSE/Huber) or C51 distributional (csrc/kernels/rainbow.hip), noisy
+dense layers (factorised Gaussian: effective weights mixed on the GPU, then
+packed; sigma gradients split from the mu gradients), Double DQN, PER weights.
+Other architectures (`simple`, the reference `cnn`) use the torch executor.
 """
 from __future__ import annotations
 
@@ -27,7 +29,9 @@ _KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9)
 
 
 def supports(arch) -> bool:
-    if arch.network != 'nature' or arch.distributional or arch.noisy:
+    if arch.network != 'nature':
+        return False
+    if arch.distributional and arch.atoms > 64:     # one wave64 lane per atom
         return False
     if tuple(arch.input_shape) != (84, 84, 4):
         return False
@@ -71,6 +75,11 @@ class HipExecutor:
         self.double = bool(double_dqn)
         self.A = arch.num_actions
         self.dueling = arch.dueling
+        self.dist = arch.distributional
+        self.atoms = arch.atoms if self.dist else 1
+        self.NO = self.A * self.atoms          # output-layer width (advantage / plain head)
+        self.noisy = arch.noisy
+        self._eff: Dict[int, torch.Tensor] = {}
         fc = arch.value[0] if self.dueling else arch.head[0]
         self.HID = fc.fout
         self.HH = 2 * self.HID if self.dueling else self.HID
@@ -118,9 +127,9 @@ class HipExecutor:
                                       for n, o in fcs])
         # head (output layer) fragments for the MFMA Q tiles of the head kernel
         hw = 'advantage/output/w' if self.dueling else 'output/w'
-        add('head/w', H, self.A, [dict(src_off=lay.offsets[hw], K=H, N=self.A, mode=0)])
+        add('head/w', H, self.NO, [dict(src_off=lay.offsets[hw], K=H, N=self.NO, mode=0)])
         if self.dueling:
-            add('head/v', H, 1, [dict(src_off=lay.offsets['value/output/w'], K=H, N=1, mode=0)])
+            add('head/v', H, self.atoms, [dict(src_off=lay.offsets['value/output/w'], K=H, N=self.atoms, mode=0)])
         # concatenated fc bias (fp32, 2 bf16 slots per float)
         self.poff['fc/bias'] = off
         for n, o in fcs:
@@ -131,6 +140,75 @@ class HipExecutor:
         self.jobs = jobs
         self._jobs_dev: Dict[torch.device, torch.Tensor] = {}
         self._max_threads = max(j.threads() for j in jobs)
+        self._plan_noisy()
+
+    def _plan_noisy(self):
+        """Mix jobs (rainbow.hip NoisyJob): every mu tensor -> the effective buffer;
+        noisy dense layers add sigma * f(eps_in) f(eps_out). Noise offsets follow
+        models/torch_net.forward (dense layers in arch.dense_layers() order)."""
+        self.noisy_jobs = []
+        if not self.noisy:
+            return
+        lay = self.layout
+        noff, dense = 0, {}
+        for d in self.arch.dense_layers():
+            if d.noisy:
+                dense[d.name] = (d, noff)
+                noff += d.fin + d.fout
+        for name in lay.names:
+            kind = lay.kinds[name]
+            if kind not in ('w', 'b'):
+                continue
+            layer = name.rsplit('/', 1)[0]
+            n = lay.numel(name)
+            if layer in dense:
+                d, o = dense[layer]
+                if kind == 'w':
+                    self.noisy_jobs.append([lay.offsets[name], lay.offsets[layer + '/w_sigma'], d.fin, d.fout, o,
+                                            o + d.fin, 0, 0])
+                else:
+                    self.noisy_jobs.append([lay.offsets[name], lay.offsets[layer + '/b_sigma'], 1, d.fout, -1,
+                                            o + d.fin, 0, 0])
+            else:
+                self.noisy_jobs.append([lay.offsets[name], -1, 1, n, -1, -1, 0, 0])
+        self._noisy_max = max(j[2] * j[3] for j in self.noisy_jobs)
+        self._noisy_dev: Dict[torch.device, torch.Tensor] = {}
+
+    def _noisy_jobs_on(self, dev):
+        t = self._noisy_dev.get(dev)
+        if t is None:
+            ints = [v for j in self.noisy_jobs for v in j]
+            assert len(ints) == len(self.noisy_jobs) * self.ext.NOISY_JOB_INTS
+            t = torch.tensor(ints, dtype=torch.int32, device=dev)
+            self._noisy_dev[dev] = t
+        return t
+
+    def effective(self, flat: torch.Tensor, noise: Optional[torch.Tensor], key: Optional[int] = None
+                  ) -> torch.Tensor:
+        """Noisy nets: eff = mu + sigma*f(e_in)f(e_out) for the noisy layers (mu elsewhere),
+        then packed into ``flat``'s fragment buffer. Returns the effective fp32 buffer the
+        kernels read biases / head weights from. No-op (returns flat) without noisy layers."""
+        if not self.noisy:
+            return flat
+        k = flat.data_ptr() if key is None else key
+        eff = self._eff.get(k)
+        if eff is None:
+            eff = torch.zeros_like(flat)
+            self._eff[k] = eff
+        jobs = self._noisy_jobs_on(flat.device)
+        self.ext.qnet_noisy_mix(flat.data_ptr(), eff.data_ptr(), noise.data_ptr() if noise is not None else 0,
+                                jobs.data_ptr(), len(self.noisy_jobs), self._noisy_max)
+        p = self.packed(flat) if key is None else self._packed_for(key, flat)
+        self.ext.qnet_pack(eff.data_ptr(), p.data_ptr(), self._jobs_on(flat.device).data_ptr(), len(self.jobs),
+                           self._max_threads)
+        return eff
+
+    def _packed_for(self, key: int, like: torch.Tensor) -> torch.Tensor:
+        p = self._packed.get(key)
+        if p is None:
+            p = torch.zeros(self.packed_elems, dtype=torch.bfloat16, device=like.device)
+            self._packed[key] = p
+        return p
 
     def _jobs_on(self, dev):
         t = self._jobs_dev.get(dev)
@@ -297,34 +375,46 @@ class HipExecutor:
     def forward(self, flat, x, noise=None):
         return self.q_values(flat, x, noise)
 
+    def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f):
+        """Output layer + loss (+ backward) launch: scalar head or the C51 head."""
+        if self.dist:
+            self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
+                                   wv, bv, io, pw, pwv, zero, actor, actor_f)
+        else:
+            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f)
+
     def q_values(self, flat: torch.Tensor, x: torch.Tensor, noise=None) -> torch.Tensor:
+        """Q [B, A] (C51: expected value of the return distribution)."""
         x = x.contiguous()
         self._check_states(x)
         B = x.shape[0]
         ws = self._workspace(B, x.device)
+        fl = self.effective(flat, noise)
         p = self.packed(flat)
-        self._fwd_trunk([x], [p], [flat], ws, B, 1, keep_acts=False)
-        w, b, wv, bv = self._head_ptrs([flat])
+        self._fwd_trunk([x], [p], [fl], ws, B, 1, keep_acts=False)
+        w, b, wv, bv = self._head_ptrs([fl])
         q = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
         pw, pwv = self._head_packs([p])
-        self.ext.qnet_head_loss([B, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],
-                                w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv, [], [], [])
+        self._head([B, self.A, self.HID, int(self.dueling), 0, 1], [ws['h'][0].data_ptr()],
+                   w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv, [], [], [])
         return q
 
     def act_fused(self, flat: torch.Tensor, frames: torch.Tensor, stacks: torch.Tensor, actor_ptrs, actor_ints,
-                  actor_f, q_out: Optional[torch.Tensor] = None):
-        """Acting step in 5 launches: conv1 (frame ring via the actors' slot stacks) ->
-        conv2 -> conv3 -> fc -> head with the eps-greedy/env/replay-append step fused."""
+                  actor_f, q_out: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None):
+        """Acting step in 3 launches: fused trunk (frame ring via the actors' slot stacks)
+        -> fc -> head with the eps-greedy/env/replay-append step fused (+2 for noisy nets:
+        parameter mix and repack under the acting noise)."""
         E = stacks.shape[0]
         assert stacks.dtype == torch.int32 and stacks.is_contiguous() and stacks.shape[1] == 4
         ws = self._workspace(E, frames.device)
+        fl = self.effective(flat, noise)
         p = self.packed(flat)
-        self._fwd_trunk([stacks], [p], [flat], ws, E, 1, frames=frames, keep_acts=False)
-        w, b, wv, bv = self._head_ptrs([flat])
+        self._fwd_trunk([stacks], [p], [fl], ws, E, 1, frames=frames, keep_acts=False)
+        w, b, wv, bv = self._head_ptrs([fl])
         pw, pwv = self._head_packs([p])
-        self.ext.qnet_head_loss([E, self.A, self.HID, int(self.dueling), 0, 1], [1.0], [ws['h'][0].data_ptr()],
-                                w, b, wv, bv, [0] * 7 + [q_out.data_ptr() if q_out is not None else 0] + [0] * 5,
-                                pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f))
+        self._head([E, self.A, self.HID, int(self.dueling), 0, 1], [ws['h'][0].data_ptr()],
+                   w, b, wv, bv, [0] * 7 + [q_out.data_ptr() if q_out is not None else 0] + [0] * 5,
+                   pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f))
 
     def _head_packs(self, packs):
         pw = [p.data_ptr() + 2 * self.poff['head/w'] for p in packs]
@@ -349,10 +439,12 @@ class HipExecutor:
         dev = s.device
         ws = self._workspace(B, dev)
         po, pt = self.packed(online), self.packed(target)
+        # noisy nets: effective weights under this step's noise (mixed + packed on the GPU)
+        eo, et = self.effective(online, noise), self.effective(target, noise_target)
         ninst = 3 if self.double else 2
         xs = [s, ns, ns][:ninst]
         packs = [po, pt, po][:ninst]
-        flats = [online, target, online][:ninst]
+        flats = [eo, et, eo][:ninst]
         # conv weight/bias grads are accumulated with atomics across M-chunks: the head
         # kernel zeroes that range in-kernel; fc grads are plain stores while B <= 32
         conv_lo = lay.offsets[self.arch.convs[0].name + '/w']
@@ -389,12 +481,12 @@ class HipExecutor:
         rew, done, gam = (batch['rewards'].contiguous(), batch['dones'].contiguous(),
                           batch['gammas'].contiguous())
         wts = batch.get('weights')
-        ext.qnet_head_loss([B, self.A, self.HID, int(self.dueling), int(self.huber), 0], [self.delta],
-                           [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
-                           [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
-                            wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
-                            ws['q'].data_ptr(), dw, db, dwv, dbv, ws['dh'].data_ptr()], *self._head_packs(packs),
-                           zero, [], [])
+        self._head([B, self.A, self.HID, int(self.dueling), int(self.huber), 0],
+                   [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
+                   [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
+                    wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
+                    ws['q'].data_ptr() if not self.dist else 0, dw, db, dwv, dbv, ws['dh'].data_ptr()],
+                   *self._head_packs(packs), zero, [], [])
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
@@ -441,5 +533,8 @@ class HipExecutor:
             kind1 = _KIND['F1']
         ext.qnet_wgrad(kind1, s.data_ptr(), d1, ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0,
                        c1.cout, c1.cout, 128, 256, 32, self.input_scale, True)
+        if self.noisy and noise is not None:       # dL/dsigma from dL/dW_eff (in the mu slots)
+            ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
+                                len(self.noisy_jobs), self._noisy_max)
         main.wait_stream(side)
         return ws['loss'], ws['prio']

@@ -20,6 +20,7 @@ def _setup(extra='', B=32, seed=0):
     net.target.flat.normal_(0.0, 0.03, generator=g)
     net.executor.repack(net.online.flat)
     net.executor.repack(net.target.flat)
+    net.reset_noise(generator=g)          # noisy nets: a fresh factorised noise sample
     oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
                            huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
     batch = {
@@ -38,24 +39,32 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
 
 
-@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber'])
+RAINBOW = '--distributional --noisy --dueling --double_dqn'
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', '--distributional', '--noisy --dueling',
+                                   RAINBOW])
 def test_q_values_match_oracle(extra):
     net, oracle, batch = _setup(extra)
     q = net.q_values(batch['states'])
-    q_ref = oracle.q_values(net.online.flat, batch['states'])
+    q_ref = oracle.q_values(net.online.flat, batch['states'], net.noise)
     assert _rel(q, q_ref) < 2e-2
 
 
 @pytest.mark.parametrize('extra,B,weighted', [('', 32, False), ('--dueling --double_dqn --loss=huber', 32, True),
-                                             ('', 7, False), ('--double_dqn', 64, False)])
+                                             ('', 7, False), ('--double_dqn', 64, False),
+                                             ('--distributional', 32, False), ('--noisy', 32, False),
+                                             (RAINBOW, 32, True), (RAINBOW, 13, False)])
 def test_loss_and_grad_match_oracle(extra, B, weighted):
     net, oracle, batch = _setup(extra, B)
     if weighted:
         batch['weights'] = torch.rand(B, device=DEV) + 0.5
     g_hip = torch.zeros_like(net.online.flat)
     g_ref = torch.zeros_like(net.online.flat)
-    loss, prio = net.executor.loss_and_grad(net.online.flat, net.target.flat, batch, g_hip)
-    loss_r, prio_r = oracle.loss_and_grad(net.online.flat, net.target.flat, batch, g_ref)
+    loss, prio = net.executor.loss_and_grad(net.online.flat, net.target.flat, batch, g_hip, net.noise,
+                                            net.noise_target)
+    loss_r, prio_r = oracle.loss_and_grad(net.online.flat, net.target.flat, batch, g_ref, net.noise,
+                                          net.noise_target)
     torch.cuda.synchronize()
     assert abs(float(loss) - float(loss_r)) / abs(float(loss_r)) < 3e-2
     assert _rel(prio, prio_r) < 3e-2
