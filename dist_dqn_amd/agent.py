@@ -154,7 +154,9 @@ class DQNAgent:
 
     # ---------------------------------------------------------- learner step
     def _train_minibatch(self, minibatch_size):
-        if self.replay_memory.size() < minibatch_size:
+        # device replay: staged (not yet flushed) transitions count, the flush below ships them
+        avail = self.replay_memory.size() + (self.replay_memory.staged() if self._device_replay else 0)
+        if avail < minibatch_size:
             return
         if self._device_replay:
             self.replay_memory.flush()

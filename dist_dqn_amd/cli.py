@@ -48,6 +48,8 @@ def run_worker(config: Config):
                        max_to_keep=config.max_to_keep)
     sv.prepare(broadcast_fn=lambda: broadcast_flat(ctx, network.online.flat))
 
+    if config.async_ps and ctx.enabled and ctx.rank == 0:
+        return _run_parameter_server(config, ctx, network, sv)
     if config.num_actors > 1:
         return _run_apex(config, ctx, env, network, sv, seed)
     use_device_replay = ctx.device.type == 'cuda' or ctx.enabled
@@ -57,7 +59,13 @@ def run_worker(config: Config):
         replay = DeviceReplay(config.replay_memory_capacity, obs_shape, config.frames_per_state if frames else 1,
                               device=ctx.device, prioritized=config.prioritized_replay,
                               alpha=config.per_alpha, seed=seed + ctx.rank)
-        session = Learner(network, replay, config, ctx)
+        ps = None
+        if config.async_ps and ctx.enabled:
+            from .parallel.async_ps import AsyncPSClient
+            ps = AsyncPSClient(ctx, network.online.flat)
+            ps.pull(network.online.flat, network.global_step)      # start from the PS parameters
+            network._repack()
+        session = Learner(network, replay, config, ctx, ps_client=ps)
     else:
         replay = ReplayMemory(config.replay_memory_capacity, rng=random.Random(seed + 7919 * (ctx.rank + 1)))
         session = None
@@ -67,8 +75,24 @@ def run_worker(config: Config):
         agent = DQNAgent(env, network, session, replay, config, enable_summary=ctx.is_chief,
                          metrics=metrics, monitor=monitor)
         sv.ckpt.agent_state_fn = agent.agent_state if config.save_agent_state else None
-        agent.train(config.num_episodes, config.max_steps_per_episode, sv)
+        try:
+            agent.train(config.num_episodes, config.max_steps_per_episode, sv)
+        finally:
+            if session is not None and session.ps is not None:
+                session.ps.close()
     return agent
+
+
+def _run_parameter_server(config: Config, ctx, network, sv):
+    """--async_ps rank 0: the parameter server (no env, no replay): applies every
+    worker's gradient push in arrival order and answers with fresh parameters."""
+    from .parallel.async_ps import AsyncPSServer
+    server = AsyncPSServer(ctx, network)
+    log.info('async PS on rank 0 serving %d workers', len(server.workers))
+    with sv.managed():
+        server.serve()
+    log.info('async PS done: %d updates %s', server.updates, server.per_worker)
+    return server
 
 
 def _run_apex(config: Config, ctx, env, network, sv, seed: int):

@@ -35,7 +35,7 @@ log = logging.getLogger(__name__)
 
 class Learner:
     def __init__(self, network: Network, replay, config, ctx: Optional[DistContext] = None,
-                 use_graph: Optional[bool] = None):
+                 use_graph: Optional[bool] = None, ps_client=None):
         self.net = network
         self.replay = replay
         self.config = config
@@ -56,6 +56,9 @@ class Learner:
         self._graphs = None
         self._warm = 0
         self._noise_gen = None
+        # --async_ps worker: gradients go to the rank-0 parameter server, which answers with
+        # its current parameters (parallel/async_ps.py); no local optimizer step
+        self.ps = ps_client
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -103,8 +106,22 @@ class Learner:
 
     def _eager_step(self):
         self._sample_and_grad()
+        if self.ps is not None:
+            self._ps_exchange()
+            return
         self.reducer.allreduce()
         self._apply()
+
+    def _ps_exchange(self):
+        """Async-PS worker: push grads, pull the PS parameters, repack; target cadence on
+        the LOCAL train-step count (reference `dqn_agent.py:143,215-222`)."""
+        with trace('ps.exchange'):
+            self.ps.exchange(self.net.grad, self.net.online.flat, self.net.global_step)
+        self.net._repack()
+        if self.tau < 1.0:
+            self.update_target_now(self.tau)
+        elif (self.train_steps + 1) % max(1, self.config.target_update_freq) == 0:
+            self.update_target_now()
 
     # ------------------------------------------------------------ graph
     def _capture(self):
@@ -112,7 +129,11 @@ class Learner:
         s.wait_stream(torch.cuda.current_stream(self.device))
         g_pre, g_post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
-            if self.ctx.enabled:
+            if self.ps is not None:          # post-exchange work is host-driven (eager)
+                with torch.cuda.graph(g_pre, stream=s):
+                    self._sample_and_grad()
+                self._graphs = (g_pre,)
+            elif self.ctx.enabled:
                 with torch.cuda.graph(g_pre, stream=s):
                     self._sample_and_grad()
                 with torch.cuda.graph(g_post, stream=s):
@@ -142,14 +163,16 @@ class Learner:
                 torch.cuda.synchronize(self.device)
                 self._capture()      # records only; the replay below runs the step
             self._graphs[0].replay()
-            if len(self._graphs) > 1:
+            if self.ps is not None:
+                self._ps_exchange()
+            elif len(self._graphs) > 1:
                 with trace('allreduce'):
                     self.reducer.allreduce()
                 self._graphs[1].replay()
         self.train_steps += 1
         return self.loss
 
-    def update_target_now(self):
+    def update_target_now(self, tau: float = 1.0):
         """Unconditional target sync (reference `_update_target_network` at init, `dqn_agent.py:50`)."""
-        kernels.target_update(self.net.target.flat, self.net.online.flat, 1.0)
-        self.net.sync_target_copy(1.0)
+        kernels.target_update(self.net.target.flat, self.net.online.flat, tau)
+        self.net.sync_target_copy(tau)

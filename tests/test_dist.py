@@ -105,3 +105,63 @@ def test_reference_cluster_flags_map_to_ranks(monkeypatch):
     m = _from_cluster_flags(cfg)
     assert m == dict(rank=2, world=3, addr='127.0.0.1', port='8090', local_rank=3)
     assert _from_cluster_flags(parse_args([])) is None
+
+
+def _worker_async(rank, world, port, tmpdir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import broadcast_flat, init_distributed
+    from dist_dqn_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
+    cfg = parse_args(['--device=cpu', '--seed=7', '--optimizer=sgd', '--lr=1.0', '--reg_param=0'])
+    ctx = init_distributed(cfg, device='cpu')
+    net = Network.create_network(cfg, (4,), 2)
+    broadcast_flat(ctx, net.online.flat)
+    init = net.online.flat.clone()
+    steps = 5
+    if rank == 0:
+        srv = AsyncPSServer(ctx, net)
+        assert srv.serve() == steps * (world - 1)
+        # SGD lr=1: every push of worker w subtracted w * ones, in whatever order they arrived
+        total = sum(w * steps for w in range(1, world))
+        torch.testing.assert_close(net.online.flat, init - total)
+        assert int(net.global_step) == steps * (world - 1)
+        assert srv.per_worker == {w: steps for w in range(1, world)}
+    else:
+        cli = AsyncPSClient(ctx, net.online.flat)
+        cli.pull(net.online.flat, net.global_step)
+        torch.testing.assert_close(net.online.flat, init)
+        seen = []
+        for _ in range(steps):
+            cli.exchange(torch.full_like(net.online.flat, float(rank)), net.online.flat, net.global_step)
+            seen.append(int(net.global_step))
+        assert seen == sorted(seen) and len(set(seen)) == steps    # PS step only moves forward
+        cli.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_parameter_server_arrival_order(tmp_path):
+    mp.spawn(_worker_async, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+
+
+def _worker_async_cli(rank, world, port, tmpdir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.cli import run_worker
+    from dist_dqn_amd.config import parse_args
+    cfg = parse_args(['--env=CartPole-v0', '--network=simple', '--device=cpu', '--seed=3', '--async_ps',
+                      '--optimizer=adam', '--minibatch_size=16', '--num_episodes=6', '--max_steps_per_episode=60',
+                      '--replay_memory_capacity=2000', '--target_update_freq=7', '--checkpoint_secs=0',
+                      '--logdir=%s/r%d' % (tmpdir, rank)])
+    out = run_worker(cfg)
+    if rank == 0:
+        assert out.updates > 0 and sum(out.per_worker.values()) == out.updates
+    else:
+        assert out.session.ps.pushes == out.training_steps > 0, (out.session.ps.pushes, out.training_steps)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_ps_training_cli_world3(tmp_path):
+    """--async_ps end to end: rank 0 serves, ranks 1-2 run the agent against it."""
+    mp.spawn(_worker_async_cli, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
