@@ -13,9 +13,9 @@ ARGS=${BENCH_ARGS:-"--steps 60 --warmup 10"}
 i=0
 for group in "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" \
              "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS" \
-             "FETCH_SIZE WRITE_SIZE"; do
+             "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i + 1))
-  timeout -k 10 400 rocprofv3 --pmc $group --kernel-trace -d "$OUT/pass$i" -o pass$i --output-format csv -- \
+  timeout -k 10 240 rocprofv3 --pmc $group --kernel-trace -d "$OUT/pass$i" -o pass$i --output-format csv -- \
       python3 "$REPO/bench.py" $ARGS > "$OUT/pass$i.log" 2>&1
   rc=$?
   echo "[pmc pass $i: $group] rc=$rc"
