@@ -52,15 +52,16 @@ DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int l
     const bfx8* W = val ? pv : pw;
     const int n16 = val ? N16v : N16;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < K32; ks += 4) {
-      bfx8 af[4], bf[4];
+    for (int ks = 0; ks < K32; ks += 8) {           // 8 k-steps of loads in flight per batch
+      bfx8 af[8], bf[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        af[u] = rok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : rz8();
-        bf[u] = W[((ks + u) * n16 + nt) * 64 + lane];
+      for (int u = 0; u < 8; ++u) {
+        const bool kok = ks + u < K32;
+        af[u] = rok && kok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : rz8();
+        bf[u] = kok ? W[((ks + u) * n16 + nt) * 64 + lane] : rz8();
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bf[u], acc, 0, 0, 0);
+      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bf[u], acc, 0, 0, 0);
     }
     const int col = nt * 16 + (lane & 15);
 #pragma unroll
@@ -212,70 +213,95 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     for (int i = 0; i < nwave; ++i) s += red[i];
     a.loss[0] = s / (float)B;
   }
-  // ---- 4. output-layer backward (online instance 0), partitioned over the blocks.
-  // g[b][n] = lp (d logit of the taken action); advantage/plain output j = i*NA + n:
-  //   dOut[b][j] = g[b][n] * ((i == act_b) - (dueling ? 1/A : 0)),  dV[b][n] = g[b][n]
+  // ---- 4. output-layer backward (online instance 0) on MFMA, tiles spread over every
+  // wave of every block. dOut[b][j] (j = i*NA + n) = g[b][n] * ((i == act_b) - 1/A dueling)
+  // goes to LDS (over the dead logits); g = lp; dV[b][n] = g[b][n].
   const float inva = a.dueling ? 1.f / (float)A : 0.f;
-  auto dout = [&](int b, int j) {
-    const int i = j / NA, n = j - i * NA;
-    return lp[b * NA + n] * ((i == a.act[b] ? 1.f : 0.f) - inva);
-  };
-  const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
-  const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
-  const __bf16* ha0 = a.dueling ? h0 + HID : h0;
-  for (int t = gt; t < HID * NO; t += gn) {             // dW[k][j], k fastest -> coalesced h reads
-    const int j = t / HID, k = t - j * HID;
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += (float)ha0[(int64_t)b * HH + k] * dout(b, j);
-    a.dw[(int64_t)k * NO + j] = s;
+  float* dout = lg;
+  for (int t = tid; t < B * NO; t += nth) {
+    const int b = t / NO, j = t - b * NO, i = j / NA, n = j - i * NA;
+    dout[t] = lp[b * NA + n] * ((i == a.act[b] ? 1.f : 0.f) - inva);
   }
+  __syncthreads();
+  const int gw = blockIdx.x * nwave + wave, GW = gridDim.x * nwave;
+  const int kg = 8 * (lane >> 4), l16 = lane & 15;
+  const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
+  const int KB = (B + 31) / 32;                 // k-steps over the batch
+  // (a) dW[k][j] = sum_b h[b][k] dOut[b][j]  (+ dWv with g): M = HID rows, N = outputs
+  {
+    const int MT = HID / 16, NT = (NO + 15) / 16, NTv = a.dueling ? (NA + 15) / 16 : 0;
+    for (int task = gw; task < MT * (NT + NTv); task += GW) {
+      const int mt = task % MT, t2 = task / MT;
+      const bool val = t2 >= NT;
+      const int nt = val ? t2 - NT : t2, ncol = val ? NA : NO;
+      const __bf16* hsrc = (a.dueling && !val) ? h0 + HID : h0;   // advantage half / value half
+      const float* bsrc = val ? lp : dout;
+      const int k = mt * 16 + l16, j = nt * 16 + l16;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kb = 0; kb < KB; ++kb) {
+        bfx8 af, bf;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int b = kb * 32 + kg + u;
+          af[u] = b < B ? hsrc[(int64_t)b * HH + k] : (__bf16)0.f;
+          bf[u] = (__bf16)(b < B && j < ncol ? bsrc[b * ncol + j] : 0.f);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
+      }
+      if (j < ncol) {
+        float* dst = val ? a.dwv : a.dw;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(int64_t)(mt * 16 + 4 * (lane >> 4) + r) * ncol + j] = acc[r];
+      }
+    }
+  }
+  // (b) dH[b][k] = (sum_j dOut[b][j] W[k][j]) * (h > 0); value half: sum_n g[b][n] Wv[k][n]
+  {
+    __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
+    const int MT = (B + 15) / 16, NT = HH / 16;
+    for (int task = gw; task < MT * NT; task += GW) {
+      const int mt = task % MT, nt = task / MT;
+      const int kcol0 = nt * 16;
+      const bool val = a.dueling && kcol0 < HID;
+      const int kk = (a.dueling && !val ? kcol0 - HID : kcol0) + l16;   // row of W / Wv
+      const int KD = val ? NA : NO;                                       // reduction length
+      const float* Wrow = val ? a.wv[0] + (int64_t)kk * NA : a.w[0] + (int64_t)kk * NO;
+      const float* asrc = val ? lp : dout;
+      const int b = mt * 16 + l16;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < (KD + 31) / 32; ++ks) {
+        bfx8 af, bf;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int jj = ks * 32 + kg + u;
+          af[u] = (__bf16)(b < B && jj < KD ? asrc[b * KD + jj] : 0.f);
+          bf[u] = (__bf16)(jj < KD ? Wrow[jj] : 0.f);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int bb = mt * 16 + 4 * (lane >> 4) + r;
+        if (bb < B) {
+          const int64_t o = (int64_t)bb * HH + kcol0 + l16;
+          dh[o] = (__bf16)((float)h0[o] > 0.f ? acc[r] : 0.f);
+        }
+      }
+    }
+  }
+  // (c) bias gradients
+  const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
   for (int j = gt; j < NO; j += gn) {
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dout(b, j);
+    for (int b = 0; b < B; ++b) s += dout[b * NO + j];
     a.db[j] = s;
   }
-  if (a.dueling) {
-    for (int t = gt; t < HID * NA; t += gn) {
-      const int n = t / HID, k = t - n * HID;
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += (float)h0[(int64_t)b * HH + k] * lp[b * NA + n];
-      a.dwv[(int64_t)k * NA + n] = s;
-    }
+  if (a.dueling)
     for (int n = gt; n < NA; n += gn) {
       float s = 0.f;
       for (int b = 0; b < B; ++b) s += lp[b * NA + n];
       a.dbv[n] = s;
     }
-  }
-  // dH[b][k] = (sum_j dOut[b][j] W[k][j] (+ sum_n dV[b][n] Wv[k][n])) * (H > 0)
-  __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
-  const float* W0 = a.w[0];
-  for (int t = gt; t < B * HH; t += gn) {
-    const int b = t / HH, k = t - b * HH;
-    float s = 0.f;
-    if (a.dueling && k < HID) {
-      const float* wv = a.wv[0] + (int64_t)k * NA;
-      for (int n = 0; n < NA; ++n) s += lp[b * NA + n] * wv[n];
-    } else {
-      const int kk = a.dueling ? k - HID : k;
-      const float* w = W0 + (int64_t)kk * NO;
-      const int at = a.act[b];
-      // dOut is nonzero on the taken action's atoms, and -g/A on every action (dueling)
-      float gsum = 0.f;
-      for (int n = 0; n < NA; ++n) {
-        const float g = lp[b * NA + n];
-        s += g * w[at * NA + n];
-        if (a.dueling) {
-          float col = 0.f;
-          for (int i = 0; i < A; ++i) col += w[i * NA + n];
-          gsum += g * col;
-        }
-      }
-      s -= inva * gsum;
-    }
-    const float hval = (float)h0[t];
-    dh[t] = (__bf16)(hval > 0.f ? s : 0.f);
-  }
 }
 
 // ------------------------------------------------------------------ noisy nets

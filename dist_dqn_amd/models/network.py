@@ -121,7 +121,10 @@ class Network:
         if fuse:
             self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,
                                 target=self.target.flat, target_freq=int(target_freq))
-            ex.repack(self.online.flat, target=self.target.flat, step=self.global_step, freq=int(target_freq))
+            # (noisy nets: every consumer re-mixes + repacks under its own noise sample)
+            if not getattr(ex, 'noisy', False):
+                ex.repack(self.online.flat, target=self.target.flat, step=self.global_step,
+                          freq=int(target_freq))
             return True
         self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step)
         self._repack()
