@@ -133,8 +133,11 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_eps_base', default=0.4, type=float, help='Ape-X per-actor epsilon base')
     a('--apex_eps_alpha', default=7.0, type=float, help='Ape-X per-actor epsilon exponent spread')
     a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
-    a('--allreduce', default='rccl', choices=['rccl', 'oneshot'])
-    a('--grad_bucket_mb', default=4.0, type=float)
+    a('--allreduce', default='rccl', choices=['rccl'], help='gradient all-reduce transport (RCCL over xGMI)')
+    a('--allreduce_dtype', default='fp32', choices=['fp32', 'bf16'],
+      help='wire dtype of the gradient all-reduce (bf16 halves the bytes; optimizer stays fp32)')
+    a('--grad_bucket_mb', default=64.0, type=float,
+      help='all-reduce bucket size; the default keeps the whole flat gradient in ONE collective')
     a('--hip_graph', default=1, type=int, help='Capture the learner step in a HIP graph')
     a('--checkpoint_secs', default=600, type=int)
     a('--max_to_keep', default=5, type=int)
@@ -211,7 +214,8 @@ class Config:
     apex_eps_alpha: float = 7.0
     apex_ring: int = 1024
     allreduce: str = 'rccl'
-    grad_bucket_mb: float = 4.0
+    allreduce_dtype: str = 'fp32'
+    grad_bucket_mb: float = 64.0
     hip_graph: int = 1
     checkpoint_secs: int = 600
     max_to_keep: int = 5

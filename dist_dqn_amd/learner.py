@@ -47,7 +47,8 @@ class Learner:
         self.weights = torch.ones(B, dtype=torch.float32, device=self.device)
         self.prio = torch.zeros(B, dtype=torch.float32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
-        self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb, config.allreduce)
+        self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb, config.allreduce,
+                                      config.allreduce_dtype)
         self.tau = min(1.0, float(config.target_update_tau))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:

@@ -9,13 +9,10 @@ so parameters stay bit-identical without any parameter traffic (reference
 messages M1/M2/M4/M6 disappear; only M3 = one gradient all-reduce remains).
 
 Gradient message sizing for xGMI: the reference `cnn` is
-0.58 MB fp32, Nature-CNN 6.7 MB. Buckets of ``grad_bucket_mb`` are issued in
-backward order (dense weights finish first) on a dedicated comm stream so
-they overlap the conv backward; small messages are latency-bound on the
-7-link point-to-point mesh, so the default is few, large buckets.
-
-``--allreduce=oneshot`` swaps RCCL for the custom one-shot IPC kernel
-(`parallel/oneshot.py`); RCCL stays the correctness oracle.
+0.58 MB fp32, Nature-CNN 6.7 MB. Messages this small are latency-bound on the
+7-link point-to-point mesh, so the default bucket holds the WHOLE flat
+gradient: one RCCL collective per SGD step. ``--allreduce_dtype=bf16`` sends
+bf16 on the wire (one cast kernel each way, fp32 master gradient kept).
 """
 from __future__ import annotations
 
@@ -28,8 +25,8 @@ from .dist import DistContext
 
 
 class GradAllReducer:
-    def __init__(self, ctx: DistContext, flat_grad: torch.Tensor, bucket_mb: float = 4.0,
-                 mode: str = 'rccl'):
+    def __init__(self, ctx: DistContext, flat_grad: torch.Tensor, bucket_mb: float = 64.0,
+                 mode: str = 'rccl', wire_dtype: str = 'fp32'):
         self.ctx = ctx
         self.flat = flat_grad
         self.mode = mode
@@ -39,10 +36,10 @@ class GradAllReducer:
         self.buckets: List[Tuple[int, int]] = [(o, min(n, o + per)) for o in range(0, n, per)]
         self.comm_stream = (torch.cuda.Stream(device=flat_grad.device)
                             if flat_grad.is_cuda and ctx.enabled else None)
-        self._oneshot = None
-        if mode == 'oneshot' and ctx.enabled and flat_grad.is_cuda:
-            from .oneshot import OneShotAllReduce
-            self._oneshot = OneShotAllReduce(ctx, flat_grad.numel())
+        assert mode == 'rccl', mode
+        self.wire = None
+        if wire_dtype == 'bf16' and ctx.enabled:
+            self.wire = torch.zeros(n, dtype=torch.bfloat16, device=flat_grad.device)
 
     @property
     def scale(self) -> float:
@@ -52,8 +49,11 @@ class GradAllReducer:
         """Blocking (stream-ordered) sum of the whole flat gradient."""
         if not self.ctx.enabled:
             return
-        if self._oneshot is not None:
-            self._oneshot(self.flat)
+        if self.wire is not None:
+            self.wire.copy_(self.flat)
+            for lo, hi in self.buckets:
+                dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.SUM)
+            self.flat.copy_(self.wire)
             return
         for lo, hi in self.buckets:
             dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM)

@@ -165,3 +165,24 @@ def _worker_async_cli(rank, world, port, tmpdir):
 def test_async_ps_training_cli_world3(tmp_path):
     """--async_ps end to end: rank 0 serves, ranks 1-2 run the agent against it."""
     mp.spawn(_worker_async_cli, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+
+
+def _worker_bf16_wire(rank, world, port, tmpdir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.parallel import GradAllReducer, init_distributed
+    ctx = init_distributed(parse_args(['--device=cpu']), device='cpu')
+    g = torch.Generator().manual_seed(rank)
+    flat = torch.randn(1000, generator=g)
+    ref = flat.clone()
+    dist.all_reduce(ref)
+    red = GradAllReducer(ctx, flat, wire_dtype='bf16')
+    assert len(red.buckets) == 1                      # default: ONE collective per step
+    red.allreduce()
+    torch.testing.assert_close(flat, ref, rtol=2e-2, atol=2e-2)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_bf16_wire(tmp_path):
+    mp.spawn(_worker_bf16_wire, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
