@@ -105,6 +105,15 @@ struct TrunkArgs {
   int64_t* prof;                   // optional [ninst][B][8] s_memtime phase stamps (profiling)
 };
 
+// Grouped weight-gradient launch (qnet.hip): up to 4 independent layers.
+struct WgradGroup {
+  ConvArgs a[4];
+  WgradArgs g[4];
+  int kind[4];
+  int nblk[4], gx[4], gy[4];     // filled by the launcher
+  int n;
+};
+
 enum LayerKind {
   L_NAT_CONV1_FWD = 1, L_NAT_CONV2_FWD = 2, L_NAT_CONV3_FWD = 3,
   L_DENSE_FWD_RELU = 4, L_DENSE_FWD_F32 = 5, L_DENSE_DGRAD = 6,
@@ -118,6 +127,7 @@ void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int 
                  void* dst2, const int64_t* step, int freq, hipStream_t st);
 int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
+int launch_wgrad_group(dqn::WgradGroup G, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
 void launch_trunk_fwd(const dqn::TrunkArgs& a, int B, int ninst, hipStream_t st);
 void launch_c51_head(const dqn::HeadArgs& a, hipStream_t st);

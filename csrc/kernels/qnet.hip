@@ -344,17 +344,26 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 // elements) so each lane's 8 consecutive m are one ds_read_b128; then
 // (KB/16)x(NB/16) output tiles x MC/32 MFMA k-steps. fp32 atomics only when
 // more than one M-chunk contributes to a weight.
+template <int MC, int KB, int NB>
+struct WgradTile {
+  static constexpr int LR = MC + 8;
+  static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(__bf16);
+};
+
+// Body shared by the per-layer launch and the grouped launch (one block = one
+// (M-chunk, K-range, N-range) tile; LDS passed in so a grouped kernel can carve
+// every member's staging from one buffer).
 template <class LD, int MC, int KB, int NB>
-__global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
+DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, __bf16* lds) {
   constexpr int LR = MC + 8;
   constexpr int TPR = 256 / MC;                  // threads per staged row
   constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
   constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
   static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0, "tiling");
-  __shared__ __attribute__((aligned(16))) __bf16 At[KB * LR];
-  __shared__ __attribute__((aligned(16))) __bf16 Zt[NB * LR];
+  __bf16* At = lds;
+  __bf16* Zt = lds + KB * LR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m_lo = blockIdx.x * MC, k_lo = blockIdx.y * KB, n_lo = blockIdx.z * NB;
+  const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
   {
     const int r = threadIdx.x % MC, p = threadIdx.x / MC;
     const int m = m_lo + r;
@@ -387,7 +396,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
   }
   __syncthreads();
   const bool atomic = g.atomic != 0;
-  if (g.db != nullptr && blockIdx.y == 0) {
+  if (g.db != nullptr && by == 0) {
     for (int n = threadIdx.x; n < NB; n += 256) {
       float s = 0.f;
       const __bf16* zr = Zt + n * LR;
@@ -425,6 +434,12 @@ __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
       }
     }
   }
+}
+
+template <class LD, int MC, int KB, int NB>
+__global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[WgradTile<MC, KB, NB>::lds_bytes / sizeof(__bf16)];
+  wgrad_block<LD, MC, KB, NB>(a, g, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
 // =========================================================== fused head + loss
@@ -657,6 +672,62 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
     case L_DENSE_FWD_RELU: WGRAD_LAUNCH(DenseLoader, 32, 64, 128); return 0;
     default: return -1;
   }
+}
+
+// ---- grouped weight gradients: every layer's wgrad in ONE launch (they are
+// independent once the dgrad chain produced all dZ). Block ranges per member,
+// longest member first; each block runs its member's wgrad_block.
+namespace dqn {
+template <class LD, int MC, int KB, int NB>
+DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, int gy, __bf16* lds) {
+  const int bx = b % gx, r = b / gx, by = r % gy, bz = r / gy;
+  wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
+}
+
+__global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 glds[];
+  int b = blockIdx.x, i = 0;
+  while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
+  switch (G.kind[i]) {
+    case L_NAT_CONV1_FWD: group_member<NatC1, 128, 256, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV1_FRAMES: group_member<NatF1, 128, 256, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV2_FWD: group_member<NatC2, 128, 128, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV3_FWD: group_member<NatC3, 128, 192, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_DENSE_FWD_RELU: group_member<DenseLoader, 32, 64, 128>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    default: break;
+  }
+}
+}  // namespace dqn
+
+static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
+  switch (kind) {
+    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = 128; KB = 256; NB = 32; break;
+    case L_NAT_CONV2_FWD: MC = 128; KB = 128; NB = 64; break;
+    case L_NAT_CONV3_FWD: MC = 128; KB = 192; NB = 64; break;
+    case L_DENSE_FWD_RELU: MC = 32; KB = 64; NB = 128; break;
+    default: return false;
+  }
+  lds = (size_t)(KB + NB) * (MC + 8) * sizeof(__bf16);
+  return true;
+}
+
+int launch_wgrad_group(WgradGroup G, hipStream_t st) {
+  int total = 0;
+  size_t lds = 0;
+  for (int i = 0; i < G.n; ++i) {
+    int MC, KB, NB;
+    size_t l;
+    if (!wgrad_tiles(G.kind[i], MC, KB, NB, l)) return -1;
+    G.gx[i] = (G.a[i].M + MC - 1) / MC;
+    G.gy[i] = (G.a[i].K + KB - 1) / KB;
+    const int gz = (G.g[i].N + NB - 1) / NB;
+    G.nblk[i] = G.gx[i] * G.gy[i] * gz;
+    G.g[i].atomic = G.gx[i] > 1 ? 1 : 0;
+    total += G.nblk[i];
+    lds = l > lds ? l : lds;
+  }
+  hipLaunchKernelGGL(wgrad_group_kernel, dim3(total), dim3(256), lds, st, G);
+  return 0;
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {

@@ -117,6 +117,26 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
   return a;
 }
 
+// members: per layer [kind, in, dz, ldz, dw, db, dw2, db2, nsplit, N] + dims (11 or 13) + scale
+void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vector<int64_t>> dims,
+                 std::vector<double> scales) {
+  TORCH_CHECK(members.size() >= 1 && members.size() <= 4 && dims.size() == members.size() &&
+              scales.size() == members.size(), "1..4 group members");
+  dqn::WgradGroup G{};
+  G.n = (int)members.size();
+  for (int i = 0; i < G.n; ++i) {
+    const auto& m = members[i];
+    TORCH_CHECK(m.size() == 10, "member = [kind, in, dz, ldz, dw, db, dw2, db2, nsplit, N]");
+    G.kind[i] = (int)m[0];
+    G.a[i] = conv_args({m[1]}, {}, {}, {}, {}, {1.0}, dims[i]);
+    dqn::WgradArgs& g = G.g[i];
+    g.dz = P<const void*>(m[2]); g.ldz = (int)m[3];
+    g.dw = P<float*>(m[4]); g.db = P<float*>(m[5]); g.dw2 = P<float*>(m[6]); g.db2 = P<float*>(m[7]);
+    g.nsplit = (int)m[8]; g.N = (int)m[9]; g.scale = (float)scales[i];
+  }
+  TORCH_CHECK(launch_wgrad_group(G, cur_stream()) == 0, "unknown wgrad kind in group");
+}
+
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
                std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
                std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
@@ -183,6 +203,7 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_igemm", &igemm);
   m.def("qnet_wgrad", &wgrad);
   m.def("qnet_head_loss", &head_loss);
+  m.def("qnet_wgrad_group", &wgrad_group);
   m.def("qnet_c51_head", &c51_head);
   m.def("qnet_noisy_mix", &noisy_mix);
   m.def("qnet_noisy_grad", &noisy_grad);

@@ -89,6 +89,7 @@ class HipExecutor:
         self._ws: Dict[Tuple[int, int], dict] = {}
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
+        self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self._events = {}
 
@@ -498,6 +499,37 @@ class HipExecutor:
         else:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
         mc_fc = (B + 31) // 32 * 32
+        K1, K2, K3 = c1.k * c1.k * c1.cin, c2.k * c2.k * c2.cin, c3.k * c3.k * c3.cin
+        d1 = [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0]
+        kind1 = _KIND['C1']
+        if frames is not None:
+            d1 += [frames.data_ptr(), 84 * 84]
+            kind1 = _KIND['F1']
+        # (fc wgrad members are plain stores only while one 32-row M-chunk covers the batch)
+        if self.grouped_wgrad and not self.two_stream and B <= 32:
+            # dgrad chain: dz3 = (dh W_fc^T)*(x3>0) -> dz2 -> dz1, then ONE grouped launch for
+            # the four weight gradients (conv1 first: the longest member)
+            ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()],
+                           [x3], [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
+            ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [], [ws['dz2'].data_ptr()],
+                           [x2], [1.0], [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2,
+                                         h3, w3, 0, 0])
+            ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [], [ws['dz1'].data_ptr()],
+                           [x1], [1.0], [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1,
+                                         h2, w2, 0, 0])
+            ext.qnet_wgrad_group(
+                [[kind1, s.data_ptr(), ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout,
+                  c1.cout],
+                 [_KIND['C3'], x2, ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout],
+                 [_KIND['C2'], x1, ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout, c2.cout],
+                 [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]],
+                [d1, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
+                 [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]],
+                [self.input_scale, 1.0, 1.0, 1.0])
+            if self.noisy and noise is not None:
+                ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
+                                    len(self.noisy_jobs), self._noisy_max)
+            return ws['loss'], ws['prio']
         side.wait_event(self._event('head', main))
         with torch.cuda.stream(side):
             # fc wgrad: dW[F][HH] = x3^T dh, db = sum dh
@@ -507,7 +539,6 @@ class HipExecutor:
         ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()], [x3],
                        [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
         side.wait_event(self._event('dz3', main))
-        K3 = c3.k * c3.k * c3.cin
         with torch.cuda.stream(side):
             ext.qnet_wgrad(_KIND['C3'], x2, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
                            ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout,
@@ -516,7 +547,6 @@ class HipExecutor:
                        [1.0], [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3,
                                0, 0])
         side.wait_event(self._event('dz2', main))
-        K2 = c2.k * c2.k * c2.cin
         with torch.cuda.stream(side):
             ext.qnet_wgrad(_KIND['C2'], x1, [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0],
                            ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout, c2.cout,
@@ -525,12 +555,6 @@ class HipExecutor:
                        [1.0], [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
                                0, 0])
         # conv1: wgrad only (input scale folded in); last kernel of the step, on main
-        K1 = c1.k * c1.k * c1.cin
-        d1 = [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0]
-        kind1 = _KIND['C1']
-        if frames is not None:
-            d1 += [frames.data_ptr(), 84 * 84]
-            kind1 = _KIND['F1']
         ext.qnet_wgrad(kind1, s.data_ptr(), d1, ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0,
                        c1.cout, c1.cout, 128, 256, 32, self.input_scale, True)
         if self.noisy and noise is not None:       # dL/dsigma from dL/dW_eff (in the mu slots)
