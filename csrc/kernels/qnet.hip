@@ -227,7 +227,7 @@ struct DenseLoader {
 // Block = WM x WN x KSPLIT waves (4 or 8); wave tile = (MT*16) x (NT*16).
 // EPI: 0 = scale*acc + bias, ReLU, bf16 out; 1 = scale*acc + bias, fp32 out (no ReLU);
 //      2 = acc * (mask > 0), bf16 out (ReLU backward through the layer input).
-template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI>
+template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U = 4>
 __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   static_assert(WM * WN * KSPLIT == 4 || WM * WN * KSPLIT == 8, "4 or 8 waves per block");
   __shared__ float red[KSPLIT > 1 ? WM * WN * (KSPLIT - 1) * MT * NT * 256 : 1];
@@ -253,17 +253,18 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   const int ks_lo = (K32 * wk) / KSPLIT, ks_hi = (K32 * (wk + 1)) / KSPLIT;
   // U k-steps per batch: all A/B fragment loads of the batch are issued before
   // its MFMAs, so U x (MT + NT) global loads are in flight per wave (the loop
-  // is latency-bound at these sizes, not MFMA-bound).
-  constexpr int U = 4;
-  int ks = ks_lo;
-  for (; ks + U <= ks_hi; ks += U) {
+  // is latency-bound at these sizes, not MFMA-bound). A partial last batch is
+  // predicated (zero fragments) instead of falling back to one step at a time;
+  // a U that covers the wave's whole K range pays the load latency once.
+  for (int ks = ks_lo; ks < ks_hi; ks += U) {
     bfx8 af[U][MT], bf[U][NT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      const bool kok = ks + u < ks_hi;
 #pragma unroll
-      for (int i = 0; i < MT; ++i) af[u][i] = ld[i].frag((ks + u) * 32 + kg);
+      for (int i = 0; i < MT; ++i) af[u][i] = kok ? ld[i].frag((ks + u) * 32 + kg) : zero8();
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bf[u][j] = Bp[((int64_t)(ks + u) * a.N16 + nt_base + j) * 64 + lane];
+      for (int j = 0; j < NT; ++j) bf[u][j] = kok ? Bp[((int64_t)(ks + u) * a.N16 + nt_base + j) * 64 + lane] : zero8();
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -271,17 +272,6 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[u][i], bf[u][j], acc[i][j]);
-  }
-  for (; ks < ks_hi; ++ks) {
-    bfx8 af[MT], bf[NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) af[i] = ld[i].frag(ks * 32 + kg);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) bf[j] = Bp[((int64_t)ks * a.N16 + nt_base + j) * 64 + lane];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
   }
   if constexpr (KSPLIT > 1) {
     // waves wk > 0 hand partial tiles to wk == 0 through LDS
@@ -624,11 +614,12 @@ void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs
                      reinterpret_cast<__bf16*>(dst2), step, freq < 1 ? 1 : freq);
 }
 
-#define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI)                                                     \
+#define IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, U)                                                \
   do {                                                                                                  \
     dim3 grid((a.M + WM * MT * 16 - 1) / (WM * MT * 16), (a.N + WN * NT * 16 - 1) / (WN * NT * 16), ninst); \
-    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI>), grid, dim3(64 * WM * WN * KS), 0, st, a); \
+    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI, U>), grid, dim3(64 * WM * WN * KS), 0, st, a); \
   } while (0)
+#define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI) IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, 4)
 
 using NatC1 = ConvLoader<uint8_t, 4, 8, 8, 4>;
 using NatC2 = ConvLoader<__bf16, 32, 4, 4, 2>;
@@ -645,12 +636,13 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case L_NAT_CONV1_FRAMES: IGEMM_LAUNCH(NatF1, 1, 2, 4, 1, 1, 0); return 0;
     case L_NAT_CONV2_FWD: IGEMM_LAUNCH(NatC2, 1, 4, 2, 1, 2, 0); return 0;       // K 512: split-K 2
     case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 4, 2, 1, 2, 0); return 0;       // K 576: split-K 2
-    case L_DENSE_FWD_RELU: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 8, 0); return 0; // K 3136: split-K 8
-    case L_DENSE_FWD_F32: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 1, 8, 1); return 0;
+    // K 3136 = 98 k-steps, split-K 8: one 13-step load batch per wave
+    case L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 0, 13); return 0;
+    case L_DENSE_FWD_F32: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 1, 13); return 0;
     // ---- backward data, ReLU mask of the layer input
-    case L_DENSE_DGRAD: IGEMM_LAUNCH(DenseLoader, 2, 1, 1, 2, 2, 2); return 0;   // K 512-1024
-    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH(NatD3, 1, 4, 2, 1, 2, 2); return 0;
-    case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH(NatD2, 1, 2, 2, 1, 2, 2); return 0;
+    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 2, 2, 2, 8); return 0;   // K 512-1024
+    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 4, 2, 1, 2, 2, 9); return 0;     // 18 k-steps
+    case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;     // 32 k-steps
     default: return -1;
   }
 }
