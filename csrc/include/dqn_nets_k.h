@@ -105,6 +105,25 @@ struct TrunkArgs {
   int64_t* prof;                   // optional [ninst][B][8] s_memtime phase stamps (profiling)
 };
 
+// Reference `cnn` (SAME convs + 2x2 max-pools), per-sample fused kernels (cnn.hip).
+struct CnnFwdArgs {
+  const uint8_t* frames;
+  const int32_t* slots[3];
+  const uint8_t* states[3];
+  const void* w1[3]; const void* w2[3]; const void* w3[3];   // packed bf16 fwd fragments
+  const float* b1[3]; const float* b2[3]; const float* b3[3];
+  __bf16* a1; __bf16* p1; __bf16* a2; __bf16* p2; __bf16* a3;  // instance 0, for the backward
+  __bf16* x3[3];                                               // [B][256] pooled fc inputs
+  float scale;
+};
+
+struct CnnBwdArgs {
+  const __bf16* dp3;                          // [B][256] d(pool3 out), masked by its ReLU
+  const __bf16* a1; const __bf16* a2; const __bf16* a3;   // post-ReLU pre-pool activations
+  const void* w3d; const void* w2d;           // packed conv3 / conv2 dgrad fragments
+  __bf16* dz1; __bf16* dz2; __bf16* dz3;      // d(conv pre-activation) for the wgrads
+};
+
 // Grouped weight-gradient launch (qnet.hip): up to 4 independent layers.
 struct WgradGroup {
   ConvArgs a[4];
@@ -128,6 +147,8 @@ void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int 
 int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
 int launch_wgrad_group(dqn::WgradGroup G, hipStream_t st);
+void launch_cnn_fwd(const dqn::CnnFwdArgs& a, int B, int ninst, hipStream_t st);
+void launch_cnn_bwd(const dqn::CnnBwdArgs& a, int B, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
 void launch_trunk_fwd(const dqn::TrunkArgs& a, int B, int ninst, hipStream_t st);
 void launch_c51_head(const dqn::HeadArgs& a, hipStream_t st);

@@ -1,0 +1,417 @@
+// The reference Q-network `cnn` (/root/reference/src/network.py:317-424): three
+// [conv SAME -> +bias -> ReLU -> max-pool 2x2/2 SAME] blocks, 84x84x4 ->
+// 21x21x32 -> 11x11x32 -> 6x6x64 -> 3x3x64 -> 3x3x64 -> 2x2x64 = 256 features.
+// Per-sample fused kernels (one workgroup = one sample), MFMA bf16 / fp32 acc:
+//
+//   cnn_fwd_kernel  stage the uint8 stack (frame-ring slots or NHWC) into LDS as a
+//                   zero-PADDED bf16 88x88x4 image (SAME padding costs no bounds
+//                   checks), conv1 -> a1 (LDS), pool1 -> padded p1 (LDS), conv2 ->
+//                   a2, pool2 -> padded p2, conv3 (k-split over 2 wave groups) -> a3,
+//                   pool3 -> the 256 fc inputs. Online(s) keeps a1/p1/a2/p2/a3 in
+//                   global memory for the backward; other instances write x3 only.
+//   cnn_bwd_kernel  from dp3 (fc dgrad, already masked by the pooled ReLU output):
+//                   pool3 backward (argmax recomputed, first max in row-major order
+//                   like the oracle's max_pool2d) + ReLU mask -> dz3, conv3 dgrad
+//                   (MFMA, packed dgrad fragments), pool2 backward -> dz2, conv2
+//                   dgrad, pool1 backward -> dz1. dz1/dz2/dz3 feed the grouped
+//                   weight-gradient launch (qnet.hip) with padded conv loaders.
+#include "common.h"
+#include "fused_util.h"
+#include "../include/dqn_nets_k.h"
+
+namespace dqn {
+namespace cnn {
+constexpr int IH = 84, HW = IH * IH, XP = 2, XW = IH + 2 * XP;   // padded input 88 x 88
+constexpr int O1 = 21, R1 = O1 * O1, N1 = 32, K1 = 256, L1 = N1 + 8;
+constexpr int Q1 = 11, P1W = Q1 + 3, LP1 = N1 + 8;                 // conv2 SAME pad: top/left 1, bottom/right 2
+constexpr int O2 = 6, R2 = O2 * O2, N2 = 64, K2 = 512, L2 = N2 + 8;
+constexpr int Q2 = 3, P2W = Q2 + 2, LP2 = N2 + 8;                  // conv3 SAME pad 1
+constexpr int O3 = 3, R3 = O3 * O3, N3 = 64, K3 = 576, L3 = N3 + 8;
+constexpr int Q3 = 2;                                               // pool3 (SAME, pad bottom/right 1)
+// LDS carve-up of the (dead after conv1) padded-input region, in bf16 elements
+constexpr int OFF_P1 = 0, OFF_A2 = OFF_P1 + P1W * P1W * LP1, OFF_P2 = OFF_A2 + R2 * L2,
+              OFF_A3 = OFF_P2 + P2W * P2W * LP2, OFF_RED = OFF_A3 + R3 * L3;
+static_assert((OFF_RED * 2) % 16 == 0 && OFF_RED + 2048 <= XW * XW * 4, "fwd LDS carve-up");
+}  // namespace cnn
+
+DQN_DEV bfx8 max8(bfx8 a, const bfx8& b) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = (float)b[j] > (float)a[j] ? b[j] : a[j];
+  return a;
+}
+
+__global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
+  using namespace cnn;
+  __shared__ __attribute__((aligned(16))) __bf16 xin[XW * XW * 4];
+  __shared__ __attribute__((aligned(16))) __bf16 a1[R1 * L1];
+  __bf16* p1p = xin + OFF_P1;
+  __bf16* a2 = xin + OFF_A2;
+  __bf16* p2p = xin + OFF_P2;
+  __bf16* a3 = xin + OFF_A3;
+  float* red = reinterpret_cast<float*>(xin + OFF_RED);
+  const int b = blockIdx.x, inst = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, kg = 8 * (lane >> 4), cq = 4 * (lane >> 4);
+  const bool keep = inst == 0 && a.a1 != nullptr;
+
+  // ---- input loads first (4 pixels x 4 channels per task), then weights / biases
+  constexpr int NT = HW / 4;
+  uint32_t in[4][4];
+  const bool slot_path = a.slots[inst] != nullptr;
+  if (slot_path) {
+    const int4 sl = reinterpret_cast<const int4*>(a.slots[inst])[b];
+    const uint32_t* f0 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW);
+    const uint32_t* f1 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW);
+    const uint32_t* f2 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.z * HW);
+    const uint32_t* f3 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.w * HW);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 512 * j;
+      if (t < NT) { in[j][0] = f0[t]; in[j][1] = f1[t]; in[j][2] = f2[t]; in[j][3] = f3[t]; }
+    }
+  } else {
+    const uint4* src = reinterpret_cast<const uint4*>(a.states[inst] + (int64_t)b * HW * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 512 * j;
+      if (t < NT) { const uint4 v = src[t]; in[j][0] = v.x; in[j][1] = v.y; in[j][2] = v.z; in[j][3] = v.w; }
+    }
+  }
+  const int nq = wave & 3, hi = wave >> 2;
+  bfx8 w1r[2][K1 / 32];
+  {
+    const bfx8* W1 = reinterpret_cast<const bfx8*>(a.w1[inst]);
+#pragma unroll
+    for (int ks = 0; ks < K1 / 32; ++ks) {
+      w1r[0][ks] = W1[(ks * 2 + 0) * 64 + lane];
+      w1r[1][ks] = W1[(ks * 2 + 1) * 64 + lane];
+    }
+  }
+  const float4 bias1a = *reinterpret_cast<const float4*>(a.b1[inst] + cq);
+  const float4 bias1b = *reinterpret_cast<const float4*>(a.b1[inst] + 16 + cq);
+  const float4 bias2 = *reinterpret_cast<const float4*>(a.b2[inst] + nq * 16 + cq);
+  const float4 bias3 = *reinterpret_cast<const float4*>(a.b3[inst] + nq * 16 + cq);
+
+  // ---- zero-padded bf16 NHWC image: interior from the loads, 2-pixel zero border
+  for (int t = tid; t < 4 * XW + 4 * IH; t += 512) {       // 688 border pixels
+    int y, x;
+    if (t < 4 * XW) { const int r = t / XW; y = r < 2 ? r : r + IH; x = t - r * XW; }
+    else { const int u = t - 4 * XW, r = u / 4, c = u - r * 4; y = r + XP; x = c < 2 ? c : c + IH; }
+    *reinterpret_cast<uint2*>(xin + (y * XW + x) * 4) = make_uint2(0u, 0u);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = tid + 512 * j;
+    if (t >= NT) continue;
+    const int y = (4 * t) / IH, x = 4 * t - y * IH;          // 4 consecutive pixels of one row
+    __bf16* dst = xin + ((y + XP) * XW + x + XP) * 4;
+    if (slot_path) {
+      planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], dst);
+    } else {
+      uint32_t c[4];
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch)
+        c[ch] = ((in[j][0] >> 8 * ch) & 0xffu) | (((in[j][1] >> 8 * ch) & 0xffu) << 8) |
+                (((in[j][2] >> 8 * ch) & 0xffu) << 16) | (((in[j][3] >> 8 * ch) & 0xffu) << 24);
+      planes_to_lds(c[0], c[1], c[2], c[3], dst);
+    }
+  }
+  __syncthreads();
+
+  // ---- conv1 (8x8/4 SAME) -> a1 = ReLU(scale*acc + b); both n-tiles per wave
+  {
+    const float scale = a.scale;
+    const int kw = kg >> 2;
+    __bf16* ga1 = keep ? a.a1 + (int64_t)b * R1 * N1 : nullptr;
+    for (int mt = wave; mt < (R1 + 15) / 16; mt += 8) {
+      const int p = mt * 16 + l16;
+      const bool ok = p < R1;
+      const int oy = ok ? p / O1 : 0, ox = ok ? p - oy * O1 : 0;
+      const __bf16* base = xin + ((oy * 4) * XW + ox * 4 + kw) * 4;
+      bfx8 fa[K1 / 32];
+#pragma unroll
+      for (int ks = 0; ks < K1 / 32; ++ks) fa[ks] = ok ? *reinterpret_cast<const bfx8*>(base + ks * XW * 4) : tz8();
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+      for (int ks = 0; ks < K1 / 32; ++ks) {
+        c0 = tmfma(w1r[0][ks], fa[ks], c0);
+        c1 = tmfma(w1r[1][ks], fa[ks], c1);
+      }
+      if (ok) {
+        const uint2 v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
+        *reinterpret_cast<uint2*>(a1 + p * L1 + cq) = v0;
+        *reinterpret_cast<uint2*>(a1 + p * L1 + 16 + cq) = v1;
+        if (ga1 != nullptr) {
+          *reinterpret_cast<uint2*>(ga1 + p * N1 + cq) = v0;
+          *reinterpret_cast<uint2*>(ga1 + p * N1 + 16 + cq) = v1;
+        }
+      }
+    }
+  }
+  // conv2 / conv3 fragments now (latency overlaps pool1)
+  bfx8 w2r[K2 / 32];
+  {
+    const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
+#pragma unroll
+    for (int ks = 0; ks < K2 / 32; ++ks) w2r[ks] = W2[(ks * 4 + nq) * 64 + lane];
+  }
+  __syncthreads();
+
+  // ---- pool1 (SAME 21 -> 11, bottom/right window cut) -> padded p1 (zero border)
+  for (int t = tid; t < Q1 * Q1 * 4; t += 512) {
+    const int pix = t >> 2, c8 = (t & 3) * 8, py = pix / Q1, px = pix - py * Q1;
+    bfx8 m = *reinterpret_cast<const bfx8*>(a1 + ((2 * py) * O1 + 2 * px) * L1 + c8);
+    if (2 * px + 1 < O1) m = max8(m, *reinterpret_cast<const bfx8*>(a1 + ((2 * py) * O1 + 2 * px + 1) * L1 + c8));
+    if (2 * py + 1 < O1) {
+      m = max8(m, *reinterpret_cast<const bfx8*>(a1 + ((2 * py + 1) * O1 + 2 * px) * L1 + c8));
+      if (2 * px + 1 < O1) m = max8(m, *reinterpret_cast<const bfx8*>(a1 + ((2 * py + 1) * O1 + 2 * px + 1) * L1 + c8));
+    }
+    *reinterpret_cast<bfx8*>(p1p + ((py + 1) * P1W + px + 1) * LP1 + c8) = m;
+    if (keep) *reinterpret_cast<bfx8*>(a.p1 + (int64_t)b * Q1 * Q1 * N1 + pix * N1 + c8) = m;
+  }
+  for (int t = tid; t < (P1W * P1W - Q1 * Q1) * 4; t += 512) {   // 75 border pixels x 4
+    const int bp = t >> 2, c8 = (t & 3) * 8;
+    int y, x;
+    if (bp < 3 * P1W) { const int r = bp / P1W; y = r == 0 ? 0 : Q1 + r; x = bp - r * P1W; }
+    else { const int u = bp - 3 * P1W, r = u / 3, c = u - r * 3; y = r + 1; x = c == 0 ? 0 : Q1 + c; }
+    *reinterpret_cast<bfx8*>(p1p + (y * P1W + x) * LP1 + c8) = tz8();
+  }
+  __syncthreads();
+
+  // ---- conv2 (4x4/2 SAME) -> a2: wave = n-tile (wave & 3), m-tiles {wave>>2, +2}
+  {
+    __bf16* ga2 = keep ? a.a2 + (int64_t)b * R2 * N2 : nullptr;
+    for (int mt = hi; mt < (R2 + 15) / 16; mt += 2) {
+      const int p = mt * 16 + l16;
+      const bool ok = p < R2;
+      const int oy = ok ? p / O2 : 0, ox = ok ? p - oy * O2 : 0;
+      const __bf16* base = p1p + ((oy * 2) * P1W + ox * 2) * LP1 + kg;
+      bfx8 fa[K2 / 32];
+#pragma unroll
+      for (int ks = 0; ks < K2 / 32; ++ks)                 // k = (kh*4 + kw)*32 + ci
+        fa[ks] = ok ? *reinterpret_cast<const bfx8*>(base + ((ks >> 2) * P1W + (ks & 3)) * LP1) : tz8();
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < K2 / 32; ++ks) c = tmfma(w2r[ks], fa[ks], c);
+      if (ok) {
+        const uint2 v = pack4(c + f4(bias2));
+        *reinterpret_cast<uint2*>(a2 + p * L2 + nq * 16 + cq) = v;
+        if (ga2 != nullptr) *reinterpret_cast<uint2*>(ga2 + p * N2 + nq * 16 + cq) = v;
+      }
+    }
+  }
+  bfx8 w3r[K3 / 64];
+  {
+    const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) w3r[j] = W3[((hi * (K3 / 64) + j) * 4 + nq) * 64 + lane];
+  }
+  __syncthreads();
+
+  // ---- pool2 (6 -> 3) -> padded p2
+  for (int t = tid; t < Q2 * Q2 * 8; t += 512) {
+    const int pix = t >> 3, c8 = (t & 7) * 8, py = pix / Q2, px = pix - py * Q2;
+    const __bf16* r0 = a2 + ((2 * py) * O2 + 2 * px) * L2 + c8;
+    bfx8 m = max8(*reinterpret_cast<const bfx8*>(r0), *reinterpret_cast<const bfx8*>(r0 + L2));
+    m = max8(m, *reinterpret_cast<const bfx8*>(r0 + O2 * L2));
+    m = max8(m, *reinterpret_cast<const bfx8*>(r0 + O2 * L2 + L2));
+    *reinterpret_cast<bfx8*>(p2p + ((py + 1) * P2W + px + 1) * LP2 + c8) = m;
+    if (keep) *reinterpret_cast<bfx8*>(a.p2 + (int64_t)b * Q2 * Q2 * N2 + pix * N2 + c8) = m;
+  }
+  for (int t = tid; t < (P2W * P2W - Q2 * Q2) * 8; t += 512) {   // 16 border pixels x 8
+    const int bp = t >> 3, c8 = (t & 7) * 8;
+    int y, x;
+    if (bp < 2 * P2W) { const int r = bp / P2W; y = r == 0 ? 0 : P2W - 1; x = bp - r * P2W; }
+    else { const int u = bp - 2 * P2W, r = u / 2; y = r + 1; x = (u & 1) ? P2W - 1 : 0; }
+    *reinterpret_cast<bfx8*>(p2p + (y * P2W + x) * LP2 + c8) = tz8();
+  }
+  __syncthreads();
+
+  // ---- conv3 (3x3/1 SAME) -> a3: wave = (n-tile, k-half), partials exchanged in LDS
+  {
+    const int p = l16;
+    const bool ok = p < R3;
+    const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
+    const __bf16* base = p2p + (oy * P2W + ox) * LP2 + kg;
+    bfx8 fa[K3 / 64];
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) {                    // k = (kh*3 + kw)*64 + ci
+      const int ks = hi * (K3 / 64) + j, tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+      fa[j] = ok ? *reinterpret_cast<const bfx8*>(base + (kh * P2W + kw) * LP2 + (ks & 1) * 32) : tz8();
+    }
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) c = tmfma(w3r[j], fa[j], c);
+    if (hi == 1) park(red, nq, lane, c);
+    __syncthreads();
+    if (hi == 0) {
+      c = unpark(red, nq, lane, c);
+      if (ok) {
+        const uint2 v = pack4(c + f4(bias3));
+        *reinterpret_cast<uint2*>(a3 + p * L3 + nq * 16 + cq) = v;
+        if (keep) *reinterpret_cast<uint2*>(a.a3 + (int64_t)b * R3 * N3 + p * N3 + nq * 16 + cq) = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- pool3 (SAME 3 -> 2, windows {0,1} and {2}) -> the 256 fc inputs (HWC order)
+  if (tid < Q3 * Q3 * 8) {
+    const int pix = tid >> 3, c8 = (tid & 7) * 8, py = pix / Q3, px = pix - py * Q3;
+    bfx8 m = *reinterpret_cast<const bfx8*>(a3 + ((2 * py) * O3 + 2 * px) * L3 + c8);
+    if (2 * px + 1 < O3) m = max8(m, *reinterpret_cast<const bfx8*>(a3 + ((2 * py) * O3 + 2 * px + 1) * L3 + c8));
+    if (2 * py + 1 < O3) {
+      m = max8(m, *reinterpret_cast<const bfx8*>(a3 + ((2 * py + 1) * O3 + 2 * px) * L3 + c8));
+      if (2 * px + 1 < O3) m = max8(m, *reinterpret_cast<const bfx8*>(a3 + ((2 * py + 1) * O3 + 2 * px + 1) * L3 + c8));
+    }
+    *reinterpret_cast<bfx8*>(a.x3[inst] + (int64_t)b * Q3 * Q3 * N3 + pix * N3 + c8) = m;
+  }
+}
+
+// ======================================================================= backward
+// position (y, x) of a pre-pool map is the argmax of its 2x2/2 window (first max in
+// row-major order over the valid cells) for channel c?
+DQN_DEV bool is_argmax(const __bf16* act, int OW, int OH, int L, int y, int x, int c) {
+  const int y0 = y & ~1, x0 = x & ~1;
+  float best = -INFINITY;
+  int by = y0, bx = x0;
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int yy = y0 + dy, xx = x0 + dx;
+      if (yy < OH && xx < OW) {
+        const float v = (float)act[(yy * OW + xx) * L + c];
+        if (v > best) { best = v; by = yy; bx = xx; }
+      }
+    }
+  return by == y && bx == x;
+}
+
+__global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
+  using namespace cnn;
+  __shared__ __attribute__((aligned(16))) __bf16 a1s[R1 * N1];
+  __shared__ __attribute__((aligned(16))) __bf16 a2s[R2 * N2];
+  __shared__ __attribute__((aligned(16))) __bf16 a3s[R3 * N3];
+  __shared__ __attribute__((aligned(16))) __bf16 dz3s[R3 * L3];
+  __shared__ __attribute__((aligned(16))) __bf16 dz2s[R2 * L2];
+  __shared__ __attribute__((aligned(16))) float dp3s[Q3 * Q3 * N3];
+  __shared__ __attribute__((aligned(16))) float dp2[Q2 * Q2 * N2];
+  __shared__ __attribute__((aligned(16))) float dp1[Q1 * Q1 * N1];
+  __shared__ __attribute__((aligned(16))) float red[4 * 256];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, kg = 8 * (lane >> 4);
+  const __bf16* ga1 = a.a1 + (int64_t)b * R1 * N1;
+  const __bf16* ga2 = a.a2 + (int64_t)b * R2 * N2;
+  const __bf16* ga3 = a.a3 + (int64_t)b * R3 * N3;
+  for (int t = tid; t < R1 * N1 / 8; t += 512)
+    reinterpret_cast<bfx8*>(a1s)[t] = reinterpret_cast<const bfx8*>(ga1)[t];
+  for (int t = tid; t < R2 * N2 / 8; t += 512)
+    reinterpret_cast<bfx8*>(a2s)[t] = reinterpret_cast<const bfx8*>(ga2)[t];
+  if (tid < R3 * N3 / 8) reinterpret_cast<bfx8*>(a3s)[tid] = reinterpret_cast<const bfx8*>(ga3)[tid];
+  if (tid < Q3 * Q3 * N3) dp3s[tid] = (float)a.dp3[(int64_t)b * Q3 * Q3 * N3 + tid];
+  __syncthreads();
+
+  // ---- pool3 backward + ReLU mask -> dz3 (LDS + global)
+  for (int t = tid; t < R3 * N3; t += 512) {
+    const int p = t / N3, c = t - p * N3, y = p / O3, x = p - y * O3;
+    const float av = (float)a3s[p * N3 + c];
+    float d = 0.f;
+    if (av > 0.f && is_argmax(a3s, O3, O3, N3, y, x, c)) d = dp3s[((y >> 1) * Q3 + (x >> 1)) * N3 + c];
+    dz3s[p * L3 + c] = (__bf16)d;
+    a.dz3[(int64_t)b * R3 * N3 + t] = (__bf16)d;
+  }
+  __syncthreads();
+
+  // ---- conv3 dgrad -> dp2 [9][64]: A gathers dz3 (SAME pad 1, stride 1), B = packed dgrad
+  {
+    const int nq = wave & 3, hi = wave >> 2;
+    const bfx8* W = reinterpret_cast<const bfx8*>(a.w3d);
+    const int m = l16;
+    const int iy = m / O3, ix = m - iy * O3;
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) {
+      const int ks = hi * (K3 / 64) + j, tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+      const int oy = iy + 1 - kh, ox = ix + 1 - kw, co = (ks & 1) * 32 + kg;
+      const bool ok = m < R3 && oy >= 0 && oy < O3 && ox >= 0 && ox < O3;
+      const bfx8 af = ok ? *reinterpret_cast<const bfx8*>(dz3s + (oy * O3 + ox) * L3 + co) : tz8();
+      c = tmfma(af, W[(ks * 4 + nq) * 64 + lane], c);
+    }
+    if (hi == 1) park(red, nq, lane, c);
+    __syncthreads();
+    if (hi == 0) {
+      c = unpark(red, nq, lane, c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = 4 * (lane >> 4) + r;
+        if (mm < R3) dp2[mm * N2 + nq * 16 + l16] = c[r];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- pool2 backward + mask -> dz2
+  for (int t = tid; t < R2 * N2; t += 512) {
+    const int p = t / N2, c = t - p * N2, y = p / O2, x = p - y * O2;
+    const float av = (float)a2s[p * N2 + c];
+    float d = 0.f;
+    if (av > 0.f && is_argmax(a2s, O2, O2, N2, y, x, c)) d = dp2[((y >> 1) * Q2 + (x >> 1)) * N2 + c];
+    dz2s[p * L2 + c] = (__bf16)d;
+    a.dz2[(int64_t)b * R2 * N2 + t] = (__bf16)d;
+  }
+  __syncthreads();
+
+  // ---- conv2 dgrad -> dp1 [121][32]: 8 m-tiles x 2 n-tiles, K = 16 taps x 64 (32 k-steps)
+  {
+    const bfx8* W = reinterpret_cast<const bfx8*>(a.w2d);
+    for (int task = wave; task < 16; task += 8) {
+      const int mt = task >> 1, nt = task & 1;
+      const int m = mt * 16 + l16;
+      const int iy = m / Q1, ix = m - iy * Q1;
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+      for (int k8 = 0; k8 < 32; k8 += 8) {
+        bfx8 af[8], bf[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int ks = k8 + u, tap = ks >> 1, kh = tap >> 2, kw = tap & 3, co = (ks & 1) * 32 + kg;
+          const int ny = iy + 1 - kh, nx = ix + 1 - kw;           // SAME pad_t = pad_l = 1, stride 2
+          const bool ok = m < Q1 * Q1 && ny >= 0 && nx >= 0 && !(ny & 1) && !(nx & 1) && (ny >> 1) < O2 &&
+                          (nx >> 1) < O2;
+          af[u] = ok ? *reinterpret_cast<const bfx8*>(dz2s + ((ny >> 1) * O2 + (nx >> 1)) * L2 + co) : tz8();
+          bf[u] = W[(ks * 2 + nt) * 64 + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c = tmfma(af[u], bf[u], c);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = mt * 16 + 4 * (lane >> 4) + r;
+        if (mm < Q1 * Q1) dp1[mm * N1 + nt * 16 + l16] = c[r];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- pool1 backward + mask -> dz1 (global only: the conv1 wgrad input)
+  __bf16* gdz1 = a.dz1 + (int64_t)b * R1 * N1;
+  for (int t = tid; t < R1 * N1; t += 512) {
+    const int p = t / N1, c = t - p * N1, y = p / O1, x = p - y * O1;
+    const float av = (float)a1s[p * N1 + c];
+    float d = 0.f;
+    if (av > 0.f && is_argmax(a1s, O1, O1, N1, y, x, c)) d = dp1[((y >> 1) * Q1 + (x >> 1)) * N1 + c];
+    gdz1[t] = (__bf16)d;
+  }
+}
+
+}  // namespace dqn
+
+using namespace dqn;
+
+void launch_cnn_fwd(const CnnFwdArgs& a, int B, int ninst, hipStream_t st) {
+  hipLaunchKernelGGL(cnn_fwd_kernel, dim3(B, ninst), dim3(512), 0, st, a);
+}
+
+void launch_cnn_bwd(const CnnBwdArgs& a, int B, hipStream_t st) {
+  hipLaunchKernelGGL(cnn_bwd_kernel, dim3(B), dim3(512), 0, st, a);
+}

@@ -17,11 +17,10 @@
 // x1 / x2 are also written to global (the backward's ReLU masks / wgrad inputs).
 // Everything is v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
 #include "common.h"
+#include "fused_util.h"
 #include "../include/dqn_nets_k.h"
 
 namespace dqn {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
 
 namespace trunk {
 constexpr int IH = 84, IW = 84, HW = IH * IW;
@@ -30,56 +29,6 @@ constexpr int O2 = 9, N2 = 64, K2 = 512, R2 = O2 * O2;        // conv2: 4x4/2
 constexpr int O3 = 7, N3 = 64, K3 = 576, R3 = O3 * O3;        // conv3: 3x3/1
 constexpr int L1 = N1 + 8, L2 = N2 + 8;                       // padded LDS rows (elements)
 }  // namespace trunk
-
-DQN_DEV bfx8 tz8() {
-  bfx8 z;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
-  return z;
-}
-
-DQN_DEV f32x4 f4(const float4& v) { return f32x4{v.x, v.y, v.z, v.w}; }
-
-// ReLU + 4 floats -> 4 packed bf16 (8 bytes)
-DQN_DEV uint2 pack4(const f32x4& v) {
-  const __bf16 a = (__bf16)fmaxf(v[0], 0.f), b = (__bf16)fmaxf(v[1], 0.f);
-  const __bf16 c = (__bf16)fmaxf(v[2], 0.f), d = (__bf16)fmaxf(v[3], 0.f);
-  return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16),
-                    (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16));
-}
-
-DQN_DEV f32x4 tmfma(const bfx8& a, const bfx8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// 4 pixels x 4 channels (one uint32 per channel plane, or one uint4 NHWC word
-// group) -> 4 NHWC bf16 pixels (32 B) in LDS.
-DQN_DEV uint32_t bfpair(uint32_t a, uint32_t b) {   // two integers 0..255 -> packed bf16 (exact)
-  const __bf16 x = (__bf16)(float)a, y = (__bf16)(float)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
-}
-
-DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, __bf16* dst) {
-  uint32_t o[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int sh = 8 * i;
-    o[2 * i] = bfpair((c0 >> sh) & 0xffu, (c1 >> sh) & 0xffu);
-    o[2 * i + 1] = bfpair((c2 >> sh) & 0xffu, (c3 >> sh) & 0xffu);
-  }
-  reinterpret_cast<uint4*>(dst)[0] = make_uint4(o[0], o[1], o[2], o[3]);
-  reinterpret_cast<uint4*>(dst)[1] = make_uint4(o[4], o[5], o[6], o[7]);
-}
-
-// K-split partial-sum exchange: waves of k-half 1 park their fp32 accumulators
-// in LDS, waves of k-half 0 add them after the barrier.
-DQN_DEV void park(float* red, int slot, int lane, const f32x4& acc) {
-  reinterpret_cast<f32x4*>(red)[slot * 64 + lane] = acc;
-}
-DQN_DEV f32x4 unpark(const float* red, int slot, int lane, f32x4 acc) {
-  const f32x4 o = reinterpret_cast<const f32x4*>(red)[slot * 64 + lane];
-  return acc + o;
-}
 
 __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   using namespace trunk;

@@ -137,6 +137,39 @@ void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vec
   TORCH_CHECK(launch_wgrad_group(G, cur_stream()) == 0, "unknown wgrad kind in group");
 }
 
+// ptrs: slots[3], states[3], w1[3], w2[3], w3[3], b1[3], b2[3], b3[3], x3[3], a1, p1, a2, p2, a3
+void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale) {
+  TORCH_CHECK(ptrs.size() == 32 && ninst >= 1 && ninst <= 3 && B >= 1, "cnn_fwd args");
+  dqn::CnnFwdArgs a{};
+  a.frames = P<const uint8_t*>(frames);
+  for (int i = 0; i < 3; ++i) {
+    a.slots[i] = P<const int32_t*>(ptrs[i]); a.states[i] = P<const uint8_t*>(ptrs[3 + i]);
+    a.w1[i] = P<const void*>(ptrs[6 + i]); a.w2[i] = P<const void*>(ptrs[9 + i]); a.w3[i] = P<const void*>(ptrs[12 + i]);
+    a.b1[i] = P<const float*>(ptrs[15 + i]); a.b2[i] = P<const float*>(ptrs[18 + i]); a.b3[i] = P<const float*>(ptrs[21 + i]);
+    a.x3[i] = P<__bf16*>(ptrs[24 + i]);
+    if (i < ninst) {
+      TORCH_CHECK((a.slots[i] != nullptr && a.frames != nullptr) || a.states[i] != nullptr, "cnn_fwd input");
+      TORCH_CHECK(a.w1[i] && a.w2[i] && a.w3[i] && a.b1[i] && a.b2[i] && a.b3[i] && a.x3[i], "cnn_fwd weights/out");
+    }
+  }
+  a.a1 = P<__bf16*>(ptrs[27]); a.p1 = P<__bf16*>(ptrs[28]); a.a2 = P<__bf16*>(ptrs[29]);
+  a.p2 = P<__bf16*>(ptrs[30]); a.a3 = P<__bf16*>(ptrs[31]);
+  TORCH_CHECK(a.a1 == nullptr || (a.p1 && a.a2 && a.p2 && a.a3), "cnn_fwd: keep all activations or none");
+  a.scale = (float)scale;
+  launch_cnn_fwd(a, (int)B, (int)ninst, cur_stream());
+}
+
+// ptrs: dp3, a1, a2, a3, w3d, w2d, dz1, dz2, dz3
+void cnn_bwd(std::vector<int64_t> ptrs, int64_t B) {
+  TORCH_CHECK(ptrs.size() == 9 && B >= 1, "cnn_bwd args");
+  for (auto p : ptrs) TORCH_CHECK(p != 0, "cnn_bwd: null pointer");
+  dqn::CnnBwdArgs a{};
+  a.dp3 = P<const __bf16*>(ptrs[0]); a.a1 = P<const __bf16*>(ptrs[1]); a.a2 = P<const __bf16*>(ptrs[2]);
+  a.a3 = P<const __bf16*>(ptrs[3]); a.w3d = P<const void*>(ptrs[4]); a.w2d = P<const void*>(ptrs[5]);
+  a.dz1 = P<__bf16*>(ptrs[6]); a.dz2 = P<__bf16*>(ptrs[7]); a.dz3 = P<__bf16*>(ptrs[8]);
+  launch_cnn_bwd(a, (int)B, cur_stream());
+}
+
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
                std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
                std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
@@ -204,6 +237,8 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_wgrad", &wgrad);
   m.def("qnet_head_loss", &head_loss);
   m.def("qnet_wgrad_group", &wgrad_group);
+  m.def("qnet_cnn_fwd", &cnn_fwd);
+  m.def("qnet_cnn_bwd", &cnn_bwd);
   m.def("qnet_c51_head", &c51_head);
   m.def("qnet_noisy_mix", &noisy_mix);
   m.def("qnet_noisy_grad", &noisy_grad);

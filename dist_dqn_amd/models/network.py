@@ -45,9 +45,9 @@ def make_executor(arch: ArchSpec, layout, config, device: torch.device):
     kw = dict(input_scale=config.input_scale, loss=config.loss, huber_delta=config.huber_delta,
               double_dqn=config.double_dqn)
     if device.type == 'cuda' and backend in ('auto', 'hip'):
-        from ..ops.executor import HipExecutor, supports
+        from ..ops.executor import make_hip_executor, supports
         if supports(arch):
-            return HipExecutor(arch, layout, dtype=config.dtype, **kw)
+            return make_hip_executor(arch, layout, dtype=config.dtype, **kw)
         if backend == 'hip':
             raise RuntimeError('HIP executor does not support %s' % (arch,))
     return TorchExecutor(arch, layout, **kw)

@@ -15,7 +15,8 @@ Supported: `nature` convs (84x84x4 uint8 frames), plain or dueling heads,
 scalar (MSE/Huber) or C51 distributional (csrc/kernels/rainbow.hip), noisy
 dense layers (factorised Gaussian: effective weights mixed on the GPU, then
 packed; sigma gradients split from the mu gradients), Double DQN, PER weights.
-Other architectures (`simple`, the reference `cnn`) use the torch executor.
+The reference `cnn` (SAME convs + max-pools) runs on the per-sample fused
+kernels of csrc/kernels/cnn.hip (`HipCnnExecutor`). `simple` uses torch.
 """
 from __future__ import annotations
 
@@ -29,7 +30,7 @@ _KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9)
 
 
 def supports(arch) -> bool:
-    if arch.network != 'nature':
+    if arch.network not in ('nature', 'cnn'):
         return False
     if arch.distributional and arch.atoms > 64:     # one wave64 lane per atom
         return False
@@ -493,11 +494,13 @@ class HipExecutor:
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
         H, HH, F = self.HID, self.HH, self.FLAT
         pko = lambda key: po.data_ptr() + 2 * self.poff[key]
-        x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         if self.dueling:
             fw, fb, fw2, fb2 = g('value/fcl/w'), g('value/fcl/b'), g('advantage/fcl/w'), g('advantage/fcl/b')
         else:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
+        if self.arch.network == 'cnn':
+            return self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev)
+        x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         mc_fc = (B + 31) // 32 * 32
         K1, K2, K3 = c1.k * c1.k * c1.cin, c2.k * c2.k * c2.cin, c3.k * c3.k * c3.cin
         d1 = [B * h1 * w1, c1.cout, K1, 0, 0, 84, 84, h1, w1, 0, 0]
@@ -562,3 +565,86 @@ class HipExecutor:
                                 len(self.noisy_jobs), self._noisy_max)
         main.wait_stream(side)
         return ws['loss'], ws['prio']
+
+
+class HipCnnExecutor(HipExecutor):
+    """The reference `cnn` (/root/reference/src/network.py:317-424) on HIP: fused
+    per-sample forward (conv/ReLU/max-pool x3 with the activations in LDS) and
+    backward (pool argmax routing + conv dgrads) kernels from csrc/kernels/cnn.hip,
+    plus the shared fc / head / grouped-wgrad / optimizer / pack kernels."""
+
+    def _workspace(self, B: int, dev) -> dict:
+        key = (B, dev.index if dev.index is not None else 0)
+        ws = self._ws.get(key)
+        if ws is not None:
+            return ws
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        ws = {
+            'x3': torch.zeros(3, B * self.FLAT, **bf),
+            'h': torch.zeros(3, B * self.HH, **bf),
+            'a1': torch.zeros(B * 441 * 32, **bf), 'p1': torch.zeros(B * 121 * 32, **bf),
+            'a2': torch.zeros(B * 36 * 64, **bf), 'p2': torch.zeros(B * 9 * 64, **bf),
+            'a3': torch.zeros(B * 9 * 64, **bf),
+            'dh': torch.zeros(B * self.HH, **bf), 'dz3': torch.zeros(B * self.FLAT, **bf),
+            'dc1': torch.zeros(B * 441 * 32, **bf), 'dc2': torch.zeros(B * 36 * 64, **bf),
+            'dc3': torch.zeros(B * 9 * 64, **bf),
+            'loss': torch.zeros(1, **f32), 'prio': torch.zeros(B, **f32), 'q': torch.zeros(B * self.A, **f32),
+            'ones': torch.ones(B, **f32),
+        }
+        self._ws[key] = ws
+        return ws
+
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True):
+        lay = self.layout
+        pad = lambda v: list(v) + [0] * (3 - len(v))
+        pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
+        bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
+        slots = [x.data_ptr() for x in xs] if frames is not None else []
+        states = [] if frames is not None else [x.data_ptr() for x in xs]
+        keep = [ws[k].data_ptr() for k in ('a1', 'p1', 'a2', 'p2', 'a3')] if keep_acts else [0] * 5
+        ptrs = (pad(slots) + pad(states) + pad(pk('conv1/fwd')) + pad(pk('conv2/fwd')) + pad(pk('conv3/fwd'))
+                + pad(bias('conv1/b')) + pad(bias('conv2/b')) + pad(bias('conv3/b'))
+                + pad([ws['x3'][i].data_ptr() for i in range(ninst)]) + keep)
+        self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale)
+        self._fc_fwd(packs, ws, B, ninst)
+
+    def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev):
+        ext = self.ext
+        F, HH, H = self.FLAT, self.HH, self.HID
+        pko = lambda key: po.data_ptr() + 2 * self.poff[key]
+        x3 = ws['x3'][0].data_ptr()
+        # dp3 = (dh W_fc^T) * (pooled conv3 output > 0)
+        ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()], [x3],
+                       [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
+        # pool / ReLU / conv dgrad chain per sample -> d(conv pre-activations)
+        ext.qnet_cnn_bwd([ws['dz3'].data_ptr(), ws['a1'].data_ptr(), ws['a2'].data_ptr(), ws['a3'].data_ptr(),
+                          pko('conv3/dgrad'), pko('conv2/dgrad'), ws['dc1'].data_ptr(), ws['dc2'].data_ptr(),
+                          ws['dc3'].data_ptr()], B)
+        c1, c2, c3 = self.arch.convs
+        t1, _, l1, _ = c1.pads()
+        t2, _, l2, _ = c2.pads()
+        t3, _, l3, _ = c3.pads()
+        d1 = [B * 441, c1.cout, c1.k * c1.k * c1.cin, 0, 0, 84, 84, 21, 21, t1, l1]
+        kind1 = _KIND['C1']
+        if frames is not None:
+            d1 += [frames.data_ptr(), 84 * 84]
+            kind1 = _KIND['F1']
+        ext.qnet_wgrad_group(
+            [[kind1, s.data_ptr(), ws['dc1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout, c1.cout],
+             [_KIND['C3'], ws['p2'].data_ptr(), ws['dc3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0,
+              c3.cout, c3.cout],
+             [_KIND['C2'], ws['p1'].data_ptr(), ws['dc2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0,
+              c2.cout, c2.cout],
+             [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]],
+            [d1, [B * 9, c3.cout, c3.k * c3.k * c3.cin, 0, 0, 3, 3, 3, 3, t3, l3],
+             [B * 36, c2.cout, c2.k * c2.k * c2.cin, 0, 0, 11, 11, 6, 6, t2, l2], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]],
+            [self.input_scale, 1.0, 1.0, 1.0])
+        if self.noisy and noise is not None:
+            ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
+                                len(self.noisy_jobs), self._noisy_max)
+        return ws['loss'], ws['prio']
+
+
+def make_hip_executor(arch, layout, **kw):
+    return (HipCnnExecutor if arch.network == 'cnn' else HipExecutor)(arch, layout, **kw)

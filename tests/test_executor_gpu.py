@@ -11,7 +11,10 @@ def _setup(extra='', B=32, seed=0):
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.models.executor import TorchExecutor
     from dist_dqn_amd.models.network import Network
-    cfg = preset('nature', 'Pong-v0', '--seed=%d --backend=hip %s' % (seed, extra))
+    # 'cnn:' prefix = the reference network (SAME convs + max-pools, no input scaling)
+    kind = 'atari' if extra.startswith('cnn:') else 'nature'
+    extra = extra[4:] if extra.startswith('cnn:') else extra
+    cfg = preset(kind, 'Pong-v0', '--seed=%d --backend=hip %s' % (seed, extra))
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     assert net.executor.name == 'hip'
     g = torch.Generator(device=DEV).manual_seed(seed)
@@ -43,7 +46,7 @@ RAINBOW = '--distributional --noisy --dueling --double_dqn'
 
 
 @pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', '--distributional', '--noisy --dueling',
-                                   RAINBOW])
+                                   RAINBOW, 'cnn:', 'cnn:--dueling'])
 def test_q_values_match_oracle(extra):
     net, oracle, batch = _setup(extra)
     q = net.q_values(batch['states'])
@@ -54,7 +57,9 @@ def test_q_values_match_oracle(extra):
 @pytest.mark.parametrize('extra,B,weighted', [('', 32, False), ('--dueling --double_dqn --loss=huber', 32, True),
                                              ('', 7, False), ('--double_dqn', 64, False),
                                              ('--distributional', 32, False), ('--noisy', 32, False),
-                                             (RAINBOW, 32, True), (RAINBOW, 13, False)])
+                                             (RAINBOW, 32, True), (RAINBOW, 13, False),
+                                             ('cnn:', 32, False), ('cnn:--dueling --double_dqn --loss=huber', 32, True),
+                                             ('cnn:', 7, False), ('cnn:--double_dqn', 64, False)])
 def test_loss_and_grad_match_oracle(extra, B, weighted):
     net, oracle, batch = _setup(extra, B)
     if weighted:
@@ -155,3 +160,45 @@ def test_fused_hard_target_sync():
         # bitwise (the packed buffer also holds fp32 bias copies: NaN patterns as bf16)
         same_p = torch.equal(ex.packed(net.target.flat).view(torch.int16), ex.packed(net.online.flat).view(torch.int16))
         assert same == same_p == (step % 3 == 0), step
+
+
+def test_cnn_slot_batch_equals_materialised_batch():
+    """Reference cnn: conv1 from frame-ring slots == from materialised NHWC stacks."""
+    net, _, batch = _setup('cnn:--double_dqn', 16)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    frames = torch.randint(0, 256, (64, 84, 84), dtype=torch.uint8, device=DEV, generator=g)
+    s = torch.randint(0, 64, (16, 4), dtype=torch.int32, device=DEV, generator=g)
+    ns = torch.randint(0, 64, (16, 4), dtype=torch.int32, device=DEV, generator=g)
+    mat = dict(batch, states=frames[s.long()].permute(0, 2, 3, 1).contiguous(),
+               next_states=frames[ns.long()].permute(0, 2, 3, 1).contiguous())
+    slot = {k: v for k, v in batch.items() if k not in ('states', 'next_states')}
+    slot.update(frames=frames, state_slots=s, next_slots=ns)
+    outs = []
+    for b in (mat, slot):
+        gr = torch.zeros_like(net.online.flat)
+        loss, prio = net.executor.loss_and_grad(net.online.flat, net.target.flat, b, gr)
+        torch.cuda.synchronize()
+        outs.append((loss.clone(), prio.clone(), gr))
+    torch.testing.assert_close(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[0][1], outs[1][1])
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-4, atol=1e-5)   # (fp32 atomics order)
+
+
+def test_cnn_learner_graph_equals_eager():
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    outs = []
+    for graph in (False, True):
+        cfg = preset('atari', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096')
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        assert net.executor.name == 'hip' and type(net.executor).__name__ == 'HipCnnExecutor'
+        rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
+        rep.fill_synthetic(4096, 6, seed=5)
+        ln = Learner(net, rep, cfg, use_graph=graph)
+        for _ in range(5):
+            ln.step()
+        torch.cuda.synchronize()
+        outs.append(net.online.flat.clone())
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-6)
