@@ -84,6 +84,9 @@ struct HeadArgs {
   ActorArgs actor;
   int atoms;                     // C51 head (rainbow.hip): atoms per action, support [vmin, vmax]
   float vmin, vmax;
+  int64_t* prof;                 // optional s_memtime phase stamps of block 0 (profiling)
+  const float* lgi[3];           // C51: precomputed logits [B][A*atoms] per instance (igemm, many CUs)
+  const float* vli[3];           // C51 dueling: precomputed value logits [B][atoms]
 };
 
 // One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =

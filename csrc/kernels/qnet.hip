@@ -215,7 +215,9 @@ struct DenseLoader {
   DQN_DEV DenseLoader() {}
   DQN_DEV DenseLoader(const ConvArgs& a, int inst, int m) {
     ok = m < a.M;
-    row = reinterpret_cast<const __bf16*>(a.in[inst]) + (int64_t)(ok ? m : 0) * a.K;
+    // row stride: a.IW when given (a K-wide slice of wider rows, e.g. one half of the
+    // dueling [value | advantage] hidden layer), else K
+    row = reinterpret_cast<const __bf16*>(a.in[inst]) + (int64_t)(ok ? m : 0) * (a.IW > 0 ? a.IW : a.K);
   }
   DQN_DEV bfx8 frag(int k0) const {
     if (!ok) return zero8();

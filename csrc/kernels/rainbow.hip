@@ -34,14 +34,17 @@ DQN_DEV bfx8 rz8() {
 }
 
 // logits of one instance -> lg [B][NO] (+ vl [B][NA] for dueling), bias added
-DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int lane, int wave, int nwave) {
+DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int lane, int wave, int nwave,
+                        int64_t* prof = nullptr) {
   const int B = a.B, NA = a.atoms, NO = a.A * NA, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
   const int N16 = (NO + 15) / 16, N16v = (NA + 15) / 16, mtiles = (B + 15) / 16, K32 = HID / 32;
   const int ntask = mtiles * (N16 + (a.dueling ? N16v : 0));
   const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
   const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
   const int kg = 8 * (lane >> 4);
+  int pi = 0;
   for (int task = wave; task < ntask; task += nwave) {
+    if (prof) prof[pi++] = (int64_t)__builtin_amdgcn_s_memtime();
     const int mt = task % mtiles, t2 = task / mtiles;
     const bool val = t2 >= N16;                              // dueling value-stream tile
     const int nt = val ? t2 - N16 : t2;
@@ -51,6 +54,8 @@ DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int l
     const __bf16* src = (a.dueling && !val) ? hrow + HID : hrow;  // [value | advantage] halves of h
     const bfx8* W = val ? pv : pw;
     const int n16 = val ? N16v : N16;
+    const int col0 = nt * 16 + (lane & 15);
+    const float bias_pre = val ? (col0 < NA ? a.bv[inst][col0] : 0.f) : (col0 < NO ? a.b[inst][col0] : 0.f);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < K32; ks += 8) {           // 8 k-steps of loads in flight per batch
       bfx8 af[8], bf[8];
@@ -64,22 +69,36 @@ DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int l
       for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bf[u], acc, 0, 0, 0);
     }
     const int col = nt * 16 + (lane & 15);
+    const float bias = bias_pre;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = mt * 16 + 4 * (lane >> 4) + r;
       if (b >= B) continue;
       if (val) {
-        if (col < NA) vl[b * NA + col] = acc[r] + a.bv[inst][col];
+        if (col < NA) vl[b * NA + col] = acc[r] + bias;
       } else if (col < NO) {
-        lg[b * NO + col] = acc[r] + a.b[inst][col];
+        lg[b * NO + col] = acc[r] + bias;
       }
     }
   }
+  if (prof) prof[pi++] = (int64_t)__builtin_amdgcn_s_memtime();
 }
 
-// dueling combine per atom, then in-place softmax of every (b, a) row (one wave
-// per row, lane = atom). If logp != nullptr the log-probabilities of each
-// sample's TAKEN action row are kept there ([B][NA]).
+// logits of one instance from the precomputed igemm outputs (global fp32) into LDS
+DQN_DEV void c51_load_logits(const HeadArgs& a, int inst, float* lg, float* vl, int tid, int nth) {
+  const int B = a.B, NA = a.atoms, NO = a.A * NA;
+  const float* src = a.lgi[inst];
+  for (int t = tid; t < B * NO; t += nth) lg[t] = src[t];
+  if (a.dueling) {
+    const float* sv = a.vli[inst];
+    for (int t = tid; t < B * NA; t += nth) vl[t] = sv[t];
+  }
+}
+
+// dueling combine per atom, then in-place softmax of every (b, a) row, ONE LANE PER
+// ROW (51-atom rows at an odd LDS stride: conflict-free, no cross-lane reductions).
+// If logp != nullptr the log-probabilities of each sample's TAKEN action row are
+// kept there ([B][NA]).
 DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* logp, int tid, int nth, int lane,
                          int wave, int nwave) {
   const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
@@ -94,16 +113,23 @@ DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* l
     }
     __syncthreads();
   }
-  for (int row = wave; row < B * A; row += nwave) {
+  for (int row = tid; row < B * A; row += nth) {
     const int b = row / A, i = row - b * A;
     float* r = lg + b * NO + i * NA;
-    const float x = lane < NA ? r[lane] : -INFINITY;
-    const float mx = wave_max(x);
-    const float e = lane < NA ? __expf(x - mx) : 0.f;
-    const float s = wave_sum(e);
-    if (lane < NA) {
-      r[lane] = e / s;
-      if (logp != nullptr && i == a.act[b]) logp[b * NA + lane] = (x - mx) - __logf(s);
+    float* lq = (logp != nullptr && i == a.act[b]) ? logp + b * NA : nullptr;
+    float mx = -INFINITY;
+    for (int n = 0; n < NA; ++n) mx = fmaxf(mx, r[n]);
+    float s = 0.f;
+    for (int n = 0; n < NA; ++n) {
+      const float x = r[n] - mx, e = __expf(x);
+      s += e;
+      r[n] = e;
+      if (lq) lq[n] = x;
+    }
+    const float inv = 1.f / s, ls = __logf(s);
+    for (int n = 0; n < NA; ++n) {
+      r[n] *= inv;
+      if (lq) lq[n] -= ls;
     }
   }
   __syncthreads();
@@ -127,20 +153,28 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
   const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  int64_t* prof = (a.prof != nullptr && blockIdx.x == 0 && tid == 0) ? a.prof : nullptr;
+#define C51_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
+  C51_MARK(0);
   if (a.zero_ptr != nullptr) {
     float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
     for (int t = blockIdx.x * nth + tid; t < a.zero_n / 4; t += gridDim.x * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  auto expected_q = [&]() {             // q[b][i] = sum_n p z_n  (one wave per row)
-    for (int row = wave; row < B * A; row += nwave) {
+  auto logits = [&](int inst) {          // precomputed (igemm) or in-block MFMA logits
+    if (a.lgi[inst] != nullptr) c51_load_logits(a, inst, lg, vl, tid, nth);
+    else c51_logits(a, inst, lg, vl, lane, wave, nwave);
+  };
+  auto expected_q = [&]() {             // q[b][i] = sum_n p z_n  (one lane per row)
+    for (int row = tid; row < B * A; row += nth) {
       const float* r = lg + row * NA;
-      const float s = wave_sum(lane < NA ? r[lane] * c51_z(a, lane) : 0.f);
-      if (lane == 0) q[row] = s;
+      float s = 0.f;
+      for (int n = 0; n < NA; ++n) s += r[n] * c51_z(a, n);
+      q[row] = s;
     }
     __syncthreads();
   };
   if (a.infer) {
-    c51_logits(a, 0, lg, vl, lane, wave, nwave);
+    logits(0);
     __syncthreads();
     c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
     expected_q();
@@ -151,10 +185,12 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   }
   // ---- 1. action choice on s' (Double DQN: online net, else the target net)
   const int sel = ninst == 3 ? 2 : 1;
-  c51_logits(a, sel, lg, vl, lane, wave, nwave);
+  logits(sel);
   __syncthreads();
+  C51_MARK(1);
   c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
   expected_q();
+  C51_MARK(2);
   for (int b = tid; b < B; b += nth) {
     int best = 0;
     float bv = q[b * A];
@@ -162,9 +198,10 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     astar[b] = best;
   }
   __syncthreads();
+  C51_MARK(3);
   // ---- 2. target distribution of a* projected onto the support
   if (sel != 1) {
-    c51_logits(a, 1, lg, vl, lane, wave, nwave);
+    logits(1);
     __syncthreads();
     c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
   }
@@ -185,9 +222,10 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
       }
     }
   }
+  C51_MARK(4);
   // ---- 3. online distribution of (s, a): cross-entropy, d logits
   __syncthreads();                      // projection reads of lg done, its atomics complete
-  c51_logits(a, 0, lg, vl, lane, wave, nwave);
+  logits(0);
   __syncthreads();
   c51_softmax(a, lg, vl, lp, tid, nth, lane, wave, nwave);
   float contrib = 0.f;
@@ -213,6 +251,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     for (int i = 0; i < nwave; ++i) s += red[i];
     a.loss[0] = s / (float)B;
   }
+  C51_MARK(5);
   // ---- 4. output-layer backward (online instance 0) on MFMA, tiles spread over every
   // wave of every block. dOut[b][j] (j = i*NA + n) = g[b][n] * ((i == act_b) - 1/A dueling)
   // goes to LDS (over the dead logits); g = lp; dV[b][n] = g[b][n].
@@ -255,6 +294,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
       }
     }
   }
+  C51_MARK(6);
   // (b) dH[b][k] = (sum_j dOut[b][j] W[k][j]) * (h > 0); value half: sum_n g[b][n] Wv[k][n]
   {
     __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
@@ -289,6 +329,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
       }
     }
   }
+  C51_MARK(7);
   // (c) bias gradients
   const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
   for (int j = gt; j < NO; j += gn) {
@@ -302,6 +343,8 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
       for (int b = 0; b < B; ++b) s += lp[b * NA + n];
       a.dbv[n] = s;
     }
+  C51_MARK(8);
+#undef C51_MARK
 }
 
 // ------------------------------------------------------------------ noisy nets

@@ -184,13 +184,19 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
 void c51_head(std::vector<int64_t> ints, std::vector<int64_t> dist, std::vector<double> flts, std::vector<int64_t> h,
               std::vector<int64_t> w, std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv,
               std::vector<int64_t> io, std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
-              std::vector<int64_t> actor, std::vector<double> actor_f) {
+              std::vector<int64_t> actor, std::vector<double> actor_f, int64_t prof, std::vector<int64_t> lg,
+              std::vector<int64_t> vl) {
   TORCH_CHECK(dist.size() == 1 && flts.size() == 2, "c51 args");
   dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f);
   a.atoms = (int)dist[0]; a.vmin = (float)flts[0]; a.vmax = (float)flts[1];
   TORCH_CHECK(a.atoms >= 2 && a.atoms <= 64, "C51: 2..64 atoms (one wave64 lane per atom)");
   TORCH_CHECK(a.vmax > a.vmin, "C51 support");
   TORCH_CHECK(c51_head_lds_bytes(a) <= 160 * 1024, "C51 head: batch too large for one workgroup's LDS");
+  a.prof = P<int64_t*>(prof);
+  TORCH_CHECK(lg.size() <= 3 && vl.size() <= 3, "c51: up to 3 precomputed logit buffers");
+  for (size_t i = 0; i < lg.size(); ++i) a.lgi[i] = P<const float*>(lg[i]);
+  for (size_t i = 0; i < vl.size(); ++i) a.vli[i] = P<const float*>(vl[i]);
+  TORCH_CHECK(lg.empty() || !a.dueling || vl.size() == lg.size(), "c51: dueling needs value logits too");
   launch_c51_head(a, cur_stream());
 }
 
@@ -239,7 +245,11 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_wgrad_group", &wgrad_group);
   m.def("qnet_cnn_fwd", &cnn_fwd);
   m.def("qnet_cnn_bwd", &cnn_bwd);
-  m.def("qnet_c51_head", &c51_head);
+  m.def("qnet_c51_head", &c51_head, pybind11::arg("ints"), pybind11::arg("dist"), pybind11::arg("flts"),
+        pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),
+        pybind11::arg("io"), pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),
+        pybind11::arg("actor_f"), pybind11::arg("prof") = 0, pybind11::arg("lg") = std::vector<int64_t>{},
+        pybind11::arg("vl") = std::vector<int64_t>{});
   m.def("qnet_noisy_mix", &noisy_mix);
   m.def("qnet_noisy_grad", &noisy_grad);
   m.attr("NOISY_JOB_INTS") = (int)(sizeof(dqn::NoisyJob) / sizeof(int));

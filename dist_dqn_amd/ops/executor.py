@@ -92,6 +92,7 @@ class HipExecutor:
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
+        self.head_prof = None       # int64 [16] C51 head phase stamps (scripts/probe_c51.py)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -377,11 +378,42 @@ class HipExecutor:
     def forward(self, flat, x, noise=None):
         return self.q_values(flat, x, noise)
 
+    def _c51_logits(self, hs, b, bv, pw, pwv):
+        """C51 logits of every instance as fp32 [B][A*atoms] (+ value [B][atoms]) on the
+        igemm kernel: spread over many CUs instead of re-streaming the 313 KB output
+        layer through one CU per head workgroup."""
+        B = self._c51_B
+        n = len(hs)
+        ws = self._c51_ws(B, n)
+        lg = [ws['lg'][i].data_ptr() for i in range(n)]
+        hsrc = [h + 2 * self.HID for h in hs] if self.dueling else list(hs)      # advantage half of [value | adv]
+        self.ext.qnet_igemm(_KIND['DF32'], hsrc, pw, b, lg, [], [1.0] * n,
+                            [B, self.NO, self.HID, (self.NO + 15) // 16, self.NO, 0, self.HH, 0, 0, 0, 0])
+        vl = []
+        if self.dueling:
+            vl = [ws['vl'][i].data_ptr() for i in range(n)]
+            self.ext.qnet_igemm(_KIND['DF32'], list(hs), pwv, bv, vl, [], [1.0] * n,
+                                [B, self.atoms, self.HID, (self.atoms + 15) // 16, self.atoms, 0, self.HH, 0, 0, 0, 0])
+        return lg, vl
+
+    def _c51_ws(self, B, n):
+        key = ('c51', B)
+        ws = self._ws.get(key)
+        if ws is None:
+            dev = self._c51_dev
+            ws = {'lg': torch.zeros(3, B * self.NO, dtype=torch.float32, device=dev),
+                  'vl': torch.zeros(3, B * self.atoms, dtype=torch.float32, device=dev)}
+            self._ws[key] = ws
+        return ws
+
     def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f):
         """Output layer + loss (+ backward) launch: scalar head or the C51 head."""
         if self.dist:
+            self._c51_B = ints[0]
+            lg, vl = self._c51_logits(hs, b, bv, pw, pwv)
+            prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
             self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
-                                   wv, bv, io, pw, pwv, zero, actor, actor_f)
+                                   wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl)
         else:
             self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f)
 
@@ -397,6 +429,7 @@ class HipExecutor:
         w, b, wv, bv = self._head_ptrs([fl])
         q = torch.empty(B, self.A, dtype=torch.float32, device=x.device)
         pw, pwv = self._head_packs([p])
+        self._c51_dev = x.device
         self._head([B, self.A, self.HID, int(self.dueling), 0, 1], [ws['h'][0].data_ptr()],
                    w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv, [], [], [])
         return q
@@ -414,6 +447,7 @@ class HipExecutor:
         self._fwd_trunk([stacks], [p], [fl], ws, E, 1, frames=frames, keep_acts=False)
         w, b, wv, bv = self._head_ptrs([fl])
         pw, pwv = self._head_packs([p])
+        self._c51_dev = frames.device
         self._head([E, self.A, self.HID, int(self.dueling), 0, 1], [ws['h'][0].data_ptr()],
                    w, b, wv, bv, [0] * 7 + [q_out.data_ptr() if q_out is not None else 0] + [0] * 5,
                    pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f))
@@ -483,6 +517,7 @@ class HipExecutor:
         rew, done, gam = (batch['rewards'].contiguous(), batch['dones'].contiguous(),
                           batch['gammas'].contiguous())
         wts = batch.get('weights')
+        self._c51_dev = dev
         self._head([B, self.A, self.HID, int(self.dueling), int(self.huber), 0],
                    [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
                    [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
