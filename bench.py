@@ -48,6 +48,8 @@ def main():
     ap.add_argument('--update_freq', type=int, default=4)
     ap.add_argument('--graph', type=int, default=1)
     ap.add_argument('--extra', default='', help='extra config flags, e.g. "--dueling --double_dqn"')
+    ap.add_argument('--fuse_acting', type=int, default=1,
+                    help='run the device actors\' step inside the learner step\'s launches when possible')
     args = ap.parse_args()
 
     import shlex
@@ -72,16 +74,17 @@ def main():
     replay = DeviceReplay(cfg.replay_memory_capacity, (84, 84), 4, device=dev,
                           prioritized=cfg.prioritized_replay, seed=ctx.rank)
     replay.fill_synthetic(cfg.replay_memory_capacity, args.actions, seed=ctx.rank)
-    learner = Learner(net, replay, cfg, ctx)
     actor = None
     if args.actor_envs > 0:
         from dist_dqn_amd.actors.device_actor import DeviceActor
         actor = DeviceActor(net, replay, cfg, num_envs=args.actor_envs,
                             steps_per_call=max(1, args.update_freq // args.actor_envs),
                             seed=1000 + ctx.rank)
+    fused = bool(args.fuse_acting) and actor is not None and actor.can_fuse(args.batch)
+    learner = Learner(net, replay, cfg, ctx, actor=actor if fused else None)
 
     def step():
-        if actor is not None:
+        if actor is not None and not fused:
             actor.step()
         learner.step()
 
@@ -115,6 +118,7 @@ def main():
                        'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
                        'frames_per_state': 4, 'optimizer': 'rmsprop(tf)', 'executor': net.executor.name,
                        'hip_graph': bool(args.graph), 'actor_envs': args.actor_envs,
+                       'acting': 'fused into the learner launches' if fused else 'separate launches',
                        'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
                        'num_actions': args.actions, 'extra': args.extra, 'final_loss': loss},
         }

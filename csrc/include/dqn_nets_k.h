@@ -6,6 +6,11 @@
 
 namespace dqn {
 
+// Up to 4 network instances per launch (grid.y / grid.z): online(s), target(s'),
+// online(s') for Double DQN, and the device actors' states when acting is fused
+// into the learner step.
+constexpr int kMaxInst = 4;
+
 // One packing job: fp32 master tensor (TF layout) -> bf16 MFMA B-fragments
 // [K/32][N/16][64][8] (mode 0..2) or a contiguous fp32 copy (mode 3, biases).
 struct PackJob {
@@ -21,12 +26,12 @@ struct PackJob {
 
 // Implicit-GEMM arguments (up to 3 instances: online(s), target(s'), online(s')).
 struct ConvArgs {
-  const void* in[3];
-  const void* w[3];          // packed bf16 B fragments
-  const float* bias[3];
-  void* out[3];
-  const void* mask[3];       // ReLU mask source for dgrad epilogues
-  float scale[3];
+  const void* in[kMaxInst];
+  const void* w[kMaxInst];          // packed bf16 B fragments
+  const float* bias[kMaxInst];
+  void* out[kMaxInst];
+  const void* mask[kMaxInst];       // ReLU mask source for dgrad epilogues
+  float scale[kMaxInst];
   int M, N, K, N16;          // GEMM shape; N16 = n-tiles per k-step of the packed B
   int ldo;                   // output row stride (elements)
   int IH, IW, OH, OW, pad_t, pad_l;
@@ -82,6 +87,8 @@ struct HeadArgs {
   float* zero_ptr; int zero_n;   // grad range zeroed in-kernel (conv wgrads accumulate atomically)
   int has_actor;                 // infer mode: run the fused actor step on the Q tile
   ActorArgs actor;
+  const void* act_h;             // training mode + fused acting: the actors' hidden layer [E][HH]
+  int act_E;                     //   (an extra workgroup runs the acting step), 0 = off
   int atoms;                     // C51 head (rainbow.hip): atoms per action, support [vmin, vmax]
   float vmin, vmax;
   int64_t* prof;                 // optional s_memtime phase stamps of block 0 (profiling)
@@ -99,11 +106,12 @@ struct NoisyJob {
 // Fused per-sample Nature trunk (trunk.hip): conv1 -> conv2 -> conv3 in one launch.
 struct TrunkArgs {
   const uint8_t* frames;           // frame ring [F][84*84] (slot path)
-  const int32_t* slots[3];         // [B][4] frame slots per instance (or nullptr -> states)
-  const uint8_t* states[3];        // [B][84][84][4] NHWC stacks per instance (materialised path)
-  const void* w1[3]; const void* w2[3]; const void* w3[3];   // packed bf16 fragments
-  const float* b1[3]; const float* b2[3]; const float* b3[3];
-  __bf16* x1[3]; __bf16* x2[3]; __bf16* x3[3];               // activations out ([B][...] NHWC)
+  const int32_t* slots[kMaxInst];  // [B][4] frame slots per instance (or nullptr -> states)
+  const uint8_t* states[kMaxInst]; // [B][84][84][4] NHWC stacks per instance (materialised path)
+  const void* w1[kMaxInst]; const void* w2[kMaxInst]; const void* w3[kMaxInst];   // packed bf16 fragments
+  const float* b1[kMaxInst]; const float* b2[kMaxInst]; const float* b3[kMaxInst];
+  __bf16* x1[kMaxInst]; __bf16* x2[kMaxInst]; __bf16* x3[kMaxInst];   // activations out ([B][...] NHWC)
+  int M[kMaxInst];                 // valid samples per instance (the fused actor's E < B)
   float scale;                     // input scale folded into conv1
   int64_t* prof;                   // optional [ninst][B][8] s_memtime phase stamps (profiling)
 };
@@ -111,12 +119,13 @@ struct TrunkArgs {
 // Reference `cnn` (SAME convs + 2x2 max-pools), per-sample fused kernels (cnn.hip).
 struct CnnFwdArgs {
   const uint8_t* frames;
-  const int32_t* slots[3];
-  const uint8_t* states[3];
-  const void* w1[3]; const void* w2[3]; const void* w3[3];   // packed bf16 fwd fragments
-  const float* b1[3]; const float* b2[3]; const float* b3[3];
+  const int32_t* slots[kMaxInst];
+  const uint8_t* states[kMaxInst];
+  const void* w1[kMaxInst]; const void* w2[kMaxInst]; const void* w3[kMaxInst];   // packed bf16 fwd fragments
+  const float* b1[kMaxInst]; const float* b2[kMaxInst]; const float* b3[kMaxInst];
   __bf16* a1; __bf16* p1; __bf16* a2; __bf16* p2; __bf16* a3;  // instance 0, for the backward
-  __bf16* x3[3];                                               // [B][256] pooled fc inputs
+  __bf16* x3[kMaxInst];                                        // [B][256] pooled fc inputs
+  int M[kMaxInst];                                             // valid samples per instance
   float scale;
 };
 

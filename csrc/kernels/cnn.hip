@@ -50,6 +50,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   __bf16* a3 = xin + OFF_A3;
   float* red = reinterpret_cast<float*>(xin + OFF_RED);
   const int b = blockIdx.x, inst = blockIdx.y;
+  if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, kg = 8 * (lane >> 4), cq = 4 * (lane >> 4);
   const bool keep = inst == 0 && a.a1 != nullptr;

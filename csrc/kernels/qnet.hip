@@ -441,9 +441,12 @@ __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
 // Q tiles come from MFMA over packed head fragments (16 rows x 16 actions per
 // wave task); the TD loss, dQ and the head backward (dW, db, dH masked by
 // ReLU(H) > 0) follow in the same workgroup.
-__global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float hsm[];
-  const int B = a.B, A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
+// head_body: one workgroup's share (blk of nblk) of the head. B / h0 / infer / actor /
+// q_out / zeroing are parameters so the fused-acting block can run the acting path
+// on the actors' hidden layer inside the learner's launch.
+DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h0, const bool infer,
+                       const bool has_actor, float* q_out, const bool do_zero, const int blk, const int nblk) {
+  const int A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
   float* q = hsm;                           // [3][B][A]
   float* vv = q + 3 * B * A;                // [3][B] dueling value stream
   float* dq = vv + 3 * B;                   // [B][A]  dL/dQ (dueling: dL/dA)
@@ -451,49 +454,51 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
   float* red = dv + B;                      // [32]
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
-  const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  const int ninst = infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  auto hptr = [&](int inst) { return inst == 0 && h0 != nullptr ? h0 : a.h[inst]; };
   // ---- 0. zero the gradient range the conv wgrads accumulate into (nothing in
   //         this kernel touches it; saves a separate fill launch)
-  if (a.zero_ptr != nullptr) {
+  if (do_zero && a.zero_ptr != nullptr) {
     float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
-    for (int t = blockIdx.x * nth + tid; t < a.zero_n / 4; t += gridDim.x * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = blk * nth + tid; t < a.zero_n / 4; t += nblk * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // ---- 1. Q tiles on MFMA: task = (instance, 16-row tile)
-  const int mtiles = (B + 15) / 16, K32 = HID / 32;
-  for (int task = wave; task < ninst * mtiles; task += nwave) {
-    const int inst = task / mtiles, mt = task - inst * mtiles;
+  // ---- 1. Q tiles on MFMA: task = (instance, 16-row tile, n-tile); the dueling value
+  // stream is one extra n-tile, so every tile's loads run on their own wave
+  const int mtiles = (B + 15) / 16, K32 = HID / 32, ntl = a.N16 + (a.dueling ? 1 : 0);
+  for (int task = wave; task < ninst * mtiles * ntl; task += nwave) {
+    const int nt = task % ntl, im = task / ntl;
+    const int inst = im / mtiles, mt = im - inst * mtiles;
     const int b_row = mt * 16 + (lane & 15);
     const bool rok = b_row < B;
-    const __bf16* hrow = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)(rok ? b_row : 0) * HH;
+    const __bf16* hrow = reinterpret_cast<const __bf16*>(hptr(inst)) + (int64_t)(rok ? b_row : 0) * HH;
     const __bf16* ha = a.dueling ? hrow + HID : hrow;
     const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
     const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
     const int kg = 8 * (lane >> 4);
-    for (int nt = 0; nt < a.N16; ++nt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accv = {0.f, 0.f, 0.f, 0.f};
-      for (int ks = 0; ks < K32; ks += 4) {
-        bfx8 af[4], bf[4], avf[4], bvf[4];
+    {
+      const bool val = nt == a.N16;
+      const __bf16* src = val ? hrow : ha;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < K32; ks += 8) {          // 8 k-steps of loads in flight per batch
+        bfx8 af[8], bf[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          af[u] = rok ? *reinterpret_cast<const bfx8*>(ha + (ks + u) * 32 + kg) : zero8();
-          bf[u] = pw[((ks + u) * a.N16 + nt) * 64 + lane];
-          if (a.dueling && nt == 0) {
-            avf[u] = rok ? *reinterpret_cast<const bfx8*>(hrow + (ks + u) * 32 + kg) : zero8();
-            bvf[u] = pv[(ks + u) * 64 + lane];
-          }
+        for (int u = 0; u < 8; ++u) {
+          const bool kok = ks + u < K32;
+          af[u] = rok && kok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : zero8();
+          bf[u] = !kok ? zero8() : val ? pv[(ks + u) * 64 + lane] : pw[((ks + u) * a.N16 + nt) * 64 + lane];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc = mfma16(af[u], bf[u], acc);
-          if (a.dueling && nt == 0) accv = mfma16(avf[u], bvf[u], accv);
-        }
+        for (int u = 0; u < 8; ++u) acc = mfma16(af[u], bf[u], acc);
       }
       const int act = nt * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = mt * 16 + 4 * (lane >> 4) + r;
-        if (b < B && act < A) q[(inst * B + b) * A + act] = acc[r] + a.b[inst][act];
-        if (a.dueling && nt == 0 && (lane & 15) == 0 && b < B) vv[inst * B + b] = accv[r] + a.bv[inst][0];
+        if (val) {
+          if ((lane & 15) == 0 && b < B) vv[inst * B + b] = acc[r] + a.bv[inst][0];
+        } else if (b < B && act < A) {
+          q[(inst * B + b) * A + act] = acc[r] + a.b[inst][act];
+        }
       }
     }
   }
@@ -508,10 +513,10 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
     }
     __syncthreads();
   }
-  if (a.infer) {                            // acting: Q of instance 0 only
-    if (a.q_out != nullptr)
-      for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
-    if (a.has_actor) actor_step_block(a.actor, q, reinterpret_cast<int*>(red + 32));
+  if (infer) {                              // acting: Q of instance 0 only
+    if (q_out != nullptr)
+      for (int t = tid; t < B * A; t += nth) q_out[t] = q[t];
+    if (has_actor) actor_step_block(a.actor, q, reinterpret_cast<int*>(red + 32));
     return;
   }
   // ---- 2. TD loss (one thread per sample)
@@ -544,16 +549,16 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
       dv[b] = gsc;
       for (int i = 0; i < A; ++i) dq[b * A + i] -= gsc / (float)A;
     }
-    if (blockIdx.x == 0) a.prio[b] = fabsf(d);
+    if (blk == 0) a.prio[b] = fabsf(d);
   }
   {
     const float s = wave_sum(contrib);
     if (lane == 0) red[wave] = s;
   }
-  if (a.q_out != nullptr && blockIdx.x == 0)
-    for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
+  if (q_out != nullptr && blk == 0)
+    for (int t = tid; t < B * A; t += nth) q_out[t] = q[t];
   __syncthreads();
-  if (tid == 0 && blockIdx.x == 0) {
+  if (tid == 0 && blk == 0) {
     float s = 0.f;
     for (int i = 0; i < nwave; ++i) s += red[i];
     a.loss[0] = s / (float)B;
@@ -561,9 +566,9 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
   // ---- 3. head backward (online instance 0 only), partitioned over the grid's
   // blocks (phases 1-2 above are recomputed by every block: cheap MFMA work);
   // k fastest across threads -> coalesced H reads
-  const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
-  const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
-  const __bf16* ha0 = a.dueling ? h0 + HID : h0;
+  const int gt = blk * nth + tid, gn = nblk * nth;
+  const __bf16* hb0 = reinterpret_cast<const __bf16*>(a.h[0]);
+  const __bf16* ha0 = a.dueling ? hb0 + HID : hb0;
   const float* W0 = a.w[0];
   __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
   for (int t = gt; t < HID * A; t += gn) {              // dW[k][i] = sum_b Ha[b][k] dA[b][i]
@@ -580,7 +585,7 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
   if (a.dueling) {
     for (int k = gt; k < HID; k += gn) {
       float s = 0.f;
-      for (int b = 0; b < B; ++b) s += (float)h0[(int64_t)b * HH + k] * dv[b];
+      for (int b = 0; b < B; ++b) s += (float)hb0[(int64_t)b * HH + k] * dv[b];
       a.dwv[k] = s;
     }
     if (gt == 0) {
@@ -599,9 +604,21 @@ __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
       const int kk = a.dueling ? k - HID : k;
       for (int i = 0; i < A; ++i) s += dq[b * A + i] * W0[(int64_t)kk * A + i];
     }
-    const float hval = (float)h0[t];
+    const float hval = (float)hb0[t];
     dh[t] = (__bf16)(hval > 0.f ? s : 0.f);
   }
+}
+
+__global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  // fused acting: the LAST workgroup runs the acting step on the actors' hidden layer
+  // (online weights = instance 0), the others the learner's loss + head backward
+  if (a.act_E > 0 && blockIdx.x == gridDim.x - 1) {
+    head_body(a, hsm, a.act_E, a.act_h, true, true, nullptr, false, 0, 1);
+    return;
+  }
+  head_body(a, hsm, a.B, nullptr, a.infer != 0, a.has_actor != 0, a.q_out, true, blockIdx.x,
+            gridDim.x - (a.act_E > 0 ? 1 : 0));
 }
 
 }  // namespace dqn
@@ -725,7 +742,8 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32 + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
-  // training: 8 blocks share the backward; acting (infer): one block
-  hipLaunchKernelGGL(head_loss_kernel, dim3(a.infer ? 1 : 8), dim3(1024), lds, st, a);
+  const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32 + (a.has_actor || a.act_E > 0 ? a.actor.E : 0)) *
+                     sizeof(float);
+  // training: 8 blocks share the backward (+1 fused acting block); acting (infer): one block
+  hipLaunchKernelGGL(head_loss_kernel, dim3(a.infer ? 1 : 8 + (a.act_E > 0 ? 1 : 0)), dim3(1024), lds, st, a);
 }

@@ -40,6 +40,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   float* red = reinterpret_cast<float*>(xin + 6144);   // conv3 k-half partials, after act2 (R2 * L2 = 5832)
   static_assert(R2 * L2 <= 6144 && 6144 * 2 + 4 * 4 * 1024 <= HW * 8, "act2 + partials fit xin");
   const int b = blockIdx.x, inst = blockIdx.y;
+  if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = lane & 15, kg = 8 * (lane >> 4);
   int64_t* prof = a.prof != nullptr && tid == 0 ? a.prof + ((int64_t)inst * gridDim.x + b) * 16 : nullptr;

@@ -30,7 +30,7 @@ dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_
                         const std::vector<int64_t>& mask, const std::vector<double>& scale,
                         const std::vector<int64_t>& d) {
   TORCH_CHECK(d.size() == 11 || d.size() == 13, "dims: M, N, K, N16, ldo, IH, IW, OH, OW, pad_t, pad_l[, frames, hw]");
-  TORCH_CHECK(in.size() >= 1 && in.size() <= 3, "1..3 instances");
+  TORCH_CHECK(in.size() >= 1 && in.size() <= (size_t)dqn::kMaxInst, "1..4 instances");
   dqn::ConvArgs a{};
   for (size_t i = 0; i < in.size(); ++i) {
     a.in[i] = P<const void*>(in[i]);
@@ -70,7 +70,7 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
                         const std::vector<int64_t>& w, const std::vector<int64_t>& b, const std::vector<int64_t>& wv,
                         const std::vector<int64_t>& bv, const std::vector<int64_t>& io, const std::vector<int64_t>& pw,
                         const std::vector<int64_t>& pwv, const std::vector<int64_t>& zero,
-                        const std::vector<int64_t>& actor, const std::vector<double>& actor_f) {
+                        const std::vector<int64_t>& actor, const std::vector<double>& actor_f, int64_t act_h = 0) {
   // ints: B, A, HID, dueling, huber, infer
   // io: act, rew, done, gam, wts, loss, prio, q_out, dw, db, dwv, dbv, dh
   TORCH_CHECK(ints.size() == 6 && io.size() == 13, "head args");
@@ -96,7 +96,7 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
   }
   if (!actor.empty()) {
     // actor = 15 pointers (ActorArgs order, q unused) + E, A, K, HW, C, F ; actor_f = gamma, p_done
-    TORCH_CHECK(actor.size() == 21 && actor_f.size() == 2 && a.infer, "fused actor args");
+    TORCH_CHECK(actor.size() == 21 && actor_f.size() == 2, "fused actor args");
     dqn::ActorArgs& x = a.actor;
     x.q = nullptr; x.frames = P<uint8_t*>(actor[1]); x.stacks = P<int32_t*>(actor[2]);
     x.cursor = P<int64_t*>(actor[3]); x.size_dev = P<int32_t*>(actor[4]); x.state_idx = P<int32_t*>(actor[5]);
@@ -105,9 +105,16 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
     x.rng = P<int64_t*>(actor[12]); x.ticket = P<int32_t*>(actor[13]); x.frames_done = P<int64_t*>(actor[14]);
     x.E = (int)actor[15]; x.A = (int)actor[16]; x.K = (int)actor[17]; x.HW = (int)actor[18]; x.C = (int)actor[19];
     x.F = (int)actor[20]; x.gamma = (float)actor_f[0]; x.p_done = (float)actor_f[1];
-    TORCH_CHECK(x.E == a.B && x.A == a.A, "actor env batch must be the inference batch");
+    TORCH_CHECK(x.A == a.A, "actor action count");
     TORCH_CHECK(x.F >= 2 * x.C + x.K, "frame ring must hold 2C + k frames");
-    a.has_actor = 1;
+    if (a.infer) {                 // acting launch: the batch IS the env batch
+      TORCH_CHECK(x.E == a.B, "actor env batch must be the inference batch");
+      a.has_actor = 1;
+    } else {                       // learner launch + one fused acting workgroup
+      TORCH_CHECK(act_h != 0 && x.E >= 1 && x.E <= a.B, "fused acting needs the actors' hidden layer, E <= B");
+      a.act_h = P<const void*>(act_h);
+      a.act_E = x.E;
+    }
   }
   a.act = P<const int32_t*>(io[0]); a.rew = P<const float*>(io[1]); a.done = P<const float*>(io[2]);
   a.gam = P<const float*>(io[3]); a.wts = P<const float*>(io[4]);
@@ -137,23 +144,29 @@ void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vec
   TORCH_CHECK(launch_wgrad_group(G, cur_stream()) == 0, "unknown wgrad kind in group");
 }
 
-// ptrs: slots[3], states[3], w1[3], w2[3], w3[3], b1[3], b2[3], b3[3], x3[3], a1, p1, a2, p2, a3
-void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale) {
-  TORCH_CHECK(ptrs.size() == 32 && ninst >= 1 && ninst <= 3 && B >= 1, "cnn_fwd args");
+// ptrs (4 per group): slots, states, w1, w2, w3, b1, b2, b3, x3, then a1, p1, a2, p2, a3; M as in trunk
+void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale,
+             std::vector<int64_t> M) {
+  constexpr int I = dqn::kMaxInst;
+  TORCH_CHECK(ptrs.size() == 9 * I + 5 && ninst >= 1 && ninst <= I && B >= 1 && M.size() <= (size_t)I, "cnn_fwd args");
   dqn::CnnFwdArgs a{};
   a.frames = P<const uint8_t*>(frames);
-  for (int i = 0; i < 3; ++i) {
-    a.slots[i] = P<const int32_t*>(ptrs[i]); a.states[i] = P<const uint8_t*>(ptrs[3 + i]);
-    a.w1[i] = P<const void*>(ptrs[6 + i]); a.w2[i] = P<const void*>(ptrs[9 + i]); a.w3[i] = P<const void*>(ptrs[12 + i]);
-    a.b1[i] = P<const float*>(ptrs[15 + i]); a.b2[i] = P<const float*>(ptrs[18 + i]); a.b3[i] = P<const float*>(ptrs[21 + i]);
-    a.x3[i] = P<__bf16*>(ptrs[24 + i]);
+  for (int i = 0; i < I; ++i) {
+    a.slots[i] = P<const int32_t*>(ptrs[0 * I + i]); a.states[i] = P<const uint8_t*>(ptrs[1 * I + i]);
+    a.w1[i] = P<const void*>(ptrs[2 * I + i]); a.w2[i] = P<const void*>(ptrs[3 * I + i]);
+    a.w3[i] = P<const void*>(ptrs[4 * I + i]);
+    a.b1[i] = P<const float*>(ptrs[5 * I + i]); a.b2[i] = P<const float*>(ptrs[6 * I + i]);
+    a.b3[i] = P<const float*>(ptrs[7 * I + i]);
+    a.x3[i] = P<__bf16*>(ptrs[8 * I + i]);
+    a.M[i] = i < (int)M.size() ? (int)M[i] : 0;
+    TORCH_CHECK(a.M[i] >= 0 && a.M[i] <= B, "cnn_fwd: per-instance sample count");
     if (i < ninst) {
       TORCH_CHECK((a.slots[i] != nullptr && a.frames != nullptr) || a.states[i] != nullptr, "cnn_fwd input");
       TORCH_CHECK(a.w1[i] && a.w2[i] && a.w3[i] && a.b1[i] && a.b2[i] && a.b3[i] && a.x3[i], "cnn_fwd weights/out");
     }
   }
-  a.a1 = P<__bf16*>(ptrs[27]); a.p1 = P<__bf16*>(ptrs[28]); a.a2 = P<__bf16*>(ptrs[29]);
-  a.p2 = P<__bf16*>(ptrs[30]); a.a3 = P<__bf16*>(ptrs[31]);
+  a.a1 = P<__bf16*>(ptrs[9 * I + 0]); a.p1 = P<__bf16*>(ptrs[9 * I + 1]); a.a2 = P<__bf16*>(ptrs[9 * I + 2]);
+  a.p2 = P<__bf16*>(ptrs[9 * I + 3]); a.a3 = P<__bf16*>(ptrs[9 * I + 4]);
   TORCH_CHECK(a.a1 == nullptr || (a.p1 && a.a2 && a.p2 && a.a3), "cnn_fwd: keep all activations or none");
   a.scale = (float)scale;
   launch_cnn_fwd(a, (int)B, (int)ninst, cur_stream());
@@ -173,9 +186,9 @@ void cnn_bwd(std::vector<int64_t> ptrs, int64_t B) {
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
                std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
                std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
-               std::vector<int64_t> actor, std::vector<double> actor_f) {
+               std::vector<int64_t> actor, std::vector<double> actor_f, int64_t act_h) {
   TORCH_CHECK(flts.size() == 1, "flts = [huber delta]");
-  dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f);
+  dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h);
   a.delta = (float)flts[0];
   launch_head_loss(a, cur_stream());
 }
@@ -211,17 +224,24 @@ void noisy_grad(int64_t grad, int64_t noise, int64_t jobs, int64_t njobs, int64_
                     (int)max_elems, cur_stream());
 }
 
-// ptrs per instance (3 entries each, 0 = absent): slots, states, w1, w2, w3, b1, b2, b3, x1, x2, x3
-void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale, int64_t prof) {
-  TORCH_CHECK(ptrs.size() == 33 && ninst >= 1 && ninst <= 3 && B >= 1, "trunk args");
+// ptrs per instance (4 entries each, 0 = absent): slots, states, w1, w2, w3, b1, b2, b3, x1, x2, x3;
+// M: valid samples per instance (empty = all B)
+void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale, int64_t prof,
+           std::vector<int64_t> M) {
+  constexpr int I = dqn::kMaxInst;
+  TORCH_CHECK(ptrs.size() == 11 * I && ninst >= 1 && ninst <= I && B >= 1 && M.size() <= (size_t)I, "trunk args");
   dqn::TrunkArgs a{};
   a.frames = P<const uint8_t*>(frames);
-  for (int i = 0; i < 3; ++i) {
-    a.slots[i] = P<const int32_t*>(ptrs[0 + i]);
-    a.states[i] = P<const uint8_t*>(ptrs[3 + i]);
-    a.w1[i] = P<const void*>(ptrs[6 + i]); a.w2[i] = P<const void*>(ptrs[9 + i]); a.w3[i] = P<const void*>(ptrs[12 + i]);
-    a.b1[i] = P<const float*>(ptrs[15 + i]); a.b2[i] = P<const float*>(ptrs[18 + i]); a.b3[i] = P<const float*>(ptrs[21 + i]);
-    a.x1[i] = P<__bf16*>(ptrs[24 + i]); a.x2[i] = P<__bf16*>(ptrs[27 + i]); a.x3[i] = P<__bf16*>(ptrs[30 + i]);
+  for (int i = 0; i < I; ++i) {
+    a.slots[i] = P<const int32_t*>(ptrs[0 * I + i]);
+    a.states[i] = P<const uint8_t*>(ptrs[1 * I + i]);
+    a.w1[i] = P<const void*>(ptrs[2 * I + i]); a.w2[i] = P<const void*>(ptrs[3 * I + i]);
+    a.w3[i] = P<const void*>(ptrs[4 * I + i]);
+    a.b1[i] = P<const float*>(ptrs[5 * I + i]); a.b2[i] = P<const float*>(ptrs[6 * I + i]);
+    a.b3[i] = P<const float*>(ptrs[7 * I + i]);
+    a.x1[i] = P<__bf16*>(ptrs[8 * I + i]); a.x2[i] = P<__bf16*>(ptrs[9 * I + i]); a.x3[i] = P<__bf16*>(ptrs[10 * I + i]);
+    a.M[i] = i < (int)M.size() ? (int)M[i] : 0;
+    TORCH_CHECK(a.M[i] >= 0 && a.M[i] <= B, "trunk: per-instance sample count");
     if (i < ninst) {
       TORCH_CHECK((a.slots[i] != nullptr && a.frames != nullptr) || a.states[i] != nullptr, "trunk input");
       TORCH_CHECK(a.w1[i] && a.w2[i] && a.w3[i] && a.b1[i] && a.b2[i] && a.b3[i] && a.x3[i], "trunk weights/out");
@@ -236,14 +256,19 @@ void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, 
 
 void register_net_ops(pybind11::module_& m) {
   m.def("qnet_trunk", &trunk, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
-        pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("prof") = 0);
+        pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("prof") = 0,
+        pybind11::arg("M") = std::vector<int64_t>{});
   m.def("qnet_pack", &pack, pybind11::arg("src"), pybind11::arg("dst"), pybind11::arg("jobs"), pybind11::arg("njobs"),
         pybind11::arg("max_threads"), pybind11::arg("dst2") = 0, pybind11::arg("step") = 0, pybind11::arg("freq") = 1);
   m.def("qnet_igemm", &igemm);
   m.def("qnet_wgrad", &wgrad);
-  m.def("qnet_head_loss", &head_loss);
+  m.def("qnet_head_loss", &head_loss, pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
+        pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"), pybind11::arg("io"),
+        pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),
+        pybind11::arg("actor_f"), pybind11::arg("act_h") = 0);
   m.def("qnet_wgrad_group", &wgrad_group);
-  m.def("qnet_cnn_fwd", &cnn_fwd);
+  m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
+        pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{});
   m.def("qnet_cnn_bwd", &cnn_bwd);
   m.def("qnet_c51_head", &c51_head, pybind11::arg("ints"), pybind11::arg("dist"), pybind11::arg("flts"),
         pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),

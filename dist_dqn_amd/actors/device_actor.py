@@ -52,19 +52,35 @@ class DeviceActor:
         self._graph = None
         self._warm = 0
 
+    def _actor_args(self):
+        r = self.replay
+        ptrs = [0] + [t.data_ptr() for t in (r.frames, self.stacks, r.cursor, r.size_dev, r.state_idx,
+                                               r.next_idx, r.actions, r.rewards, r.dones, r.gammas, self.eps,
+                                               self.rng, self.ticket, self.frames_done)]
+        ints = [self.E, self.net.arch.num_actions, r.k, r.frames.shape[1] * r.frames.shape[2], r.capacity,
+                r.num_frames]
+        return ptrs, ints, [self.gamma, self.p_done]
+
+    def can_fuse(self, batch_size: int) -> bool:
+        """One acting step per learner step that the learner's launches can carry."""
+        ex = self.net.executor
+        return (self.steps == 1 and self.E <= min(64, batch_size) and getattr(ex, 'consumes_slots', False)
+                and hasattr(ex, 'supports_fused_acting') and ex.supports_fused_acting()
+                and not self.replay.prioritized)
+
+    def fused_args(self) -> dict:
+        """Arguments of the fused acting step (executor.loss_and_grad(acting=...))."""
+        ptrs, ints, f = self._actor_args()
+        return {'stacks': self.stacks, 'ptrs': ptrs, 'ints': ints, 'f': f}
+
     def _one(self):
         r = self.replay
         ex = self.net.executor
         if getattr(ex, 'consumes_slots', False) and self.E <= 64:
-            # 5 launches: conv1 reads the frame ring through the actors' stacks; the
+            # 3 launches: fused trunk reads the frame ring through the actors' stacks; the
             # eps-greedy / env step / replay append run inside the head kernel
-            ptrs = [0] + [t.data_ptr() for t in (r.frames, self.stacks, r.cursor, r.size_dev, r.state_idx,
-                                                   r.next_idx, r.actions, r.rewards, r.dones, r.gammas, self.eps,
-                                                   self.rng, self.ticket, self.frames_done)]
-            ints = [self.E, self.net.arch.num_actions, r.k, r.frames.shape[1] * r.frames.shape[2], r.capacity,
-                    r.num_frames]
-            ex.act_fused(self.net.online.flat, r.frames, self.stacks, ptrs, ints, [self.gamma, self.p_done],
-                         noise=self.net.noise)
+            ptrs, ints, f = self._actor_args()
+            ex.act_fused(self.net.online.flat, r.frames, self.stacks, ptrs, ints, f, noise=self.net.noise)
             return
         self.ext.stack_states(r.frames, self.stacks, self.states)
         q = self.net.q_values(self.states).float().contiguous()

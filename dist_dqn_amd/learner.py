@@ -35,7 +35,7 @@ log = logging.getLogger(__name__)
 
 class Learner:
     def __init__(self, network: Network, replay, config, ctx: Optional[DistContext] = None,
-                 use_graph: Optional[bool] = None, ps_client=None):
+                 use_graph: Optional[bool] = None, ps_client=None, actor=None):
         self.net = network
         self.replay = replay
         self.config = config
@@ -60,6 +60,9 @@ class Learner:
         # --async_ps worker: gradients go to the rank-0 parameter server, which answers with
         # its current parameters (parallel/async_ps.py); no local optimizer step
         self.ps = ps_client
+        # fused acting: a DeviceActor whose acting step runs inside this learner's launches
+        # (one more trunk/fc instance + one head workgroup); its own step() is then not used
+        self.actor = actor if (actor is not None and actor.can_fuse(self.B)) else None
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -84,7 +87,11 @@ class Learner:
             if per:
                 batch['weights'] = self.weights
         self.net.reset_noise()
-        loss, prio = self.net.compute_grads(batch)
+        if self.actor is not None:
+            assert 'frames' in batch, 'fused acting needs the slot-batch sampler'
+            loss, prio = self.net.compute_grads(batch, acting=self.actor.fused_args())
+        else:
+            loss, prio = self.net.compute_grads(batch)
         # keep references (static buffers under graph capture) instead of copies
         self.loss = loss.view(1)
         self.prio = prio.view(-1)

@@ -102,9 +102,13 @@ class Network:
             self.noise_target.normal_(generator=generator)
 
     # ------------------------------------------------------------- training
-    def compute_grads(self, batch: Dict[str, torch.Tensor]):
-        loss, prio = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
-                                                 self.noise, self.noise_target)
+    def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None):
+        if acting is not None:     # fused acting (HIP executor): the actors' step rides along
+            loss, prio = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
+                                                     self.noise, self.noise_target, acting=acting)
+        else:
+            loss, prio = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
+                                                     self.noise, self.noise_target)
         self.last_loss = loss
         return loss, prio
 

@@ -295,8 +295,8 @@ class HipExecutor:
         ws = {
             'x1': torch.zeros(3, B * h1 * w1 * c1.cout, **bf),
             'x2': torch.zeros(3, B * h2 * w2 * c2.cout, **bf),
-            'x3': torch.zeros(3, B * h3 * w3 * c3.cout, **bf),
-            'h': torch.zeros(3, B * self.HH, **bf),
+            'x3': torch.zeros(4, B * h3 * w3 * c3.cout, **bf),     # 4th row: fused-acting instance
+            'h': torch.zeros(4, B * self.HH, **bf),
             'dh': torch.zeros(B * self.HH, **bf),
             'dz3': torch.zeros(B * self.FLAT, **bf),
             'dz2': torch.zeros(B * h2 * w2 * c2.cout, **bf),
@@ -310,8 +310,9 @@ class HipExecutor:
         return ws
 
     # ------------------------------------------------------------ forward
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True):
-        """conv1..fc for `ninst` instances -> ws['h'].
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=()):
+        """conv1..fc for `ninst` instances -> ws['h'] (M: valid rows per instance, e.g. the
+        fused actor instance's E < B).
 
         xs: uint8 NHWC [B, 84, 84, 4] inputs, or (frames given) int32 [B, 4] slot
         tables into the frame ring ``frames`` [F, 84, 84] (fused gather)."""
@@ -323,7 +324,7 @@ class HipExecutor:
         rows = lambda t, i: t[i].data_ptr()
         if self.fused_trunk:
             # ONE launch for conv1..conv3: a workgroup per (sample, instance), activations in LDS
-            pad = lambda v: list(v) + [0] * (3 - len(v))
+            pad = lambda v: list(v) + [0] * (4 - len(v))
             slots = [x.data_ptr() for x in xs] if frames is not None else []
             states = [] if frames is not None else [x.data_ptr() for x in xs]
             ptrs = (pad(slots) + pad(states) + pad(pk('conv1/fwd')) + pad(pk('conv2/fwd')) + pad(pk('conv3/fwd'))
@@ -332,7 +333,8 @@ class HipExecutor:
                     + pad([rows(ws['x1'], 0)] if keep_acts else []) + pad([rows(ws['x2'], 0)] if keep_acts else [])
                     + pad([rows(ws['x3'], i) for i in range(ninst)]))
             prof = self.trunk_prof.data_ptr() if self.trunk_prof is not None else 0
-            ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale, prof)
+            ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale, prof,
+                           list(M))
             self._fc_fwd(packs, ws, B, ninst)
             return
         d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
@@ -406,16 +408,17 @@ class HipExecutor:
             self._ws[key] = ws
         return ws
 
-    def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f):
+    def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h=0):
         """Output layer + loss (+ backward) launch: scalar head or the C51 head."""
         if self.dist:
+            assert act_h == 0, 'fused acting is not wired into the C51 head'
             self._c51_B = ints[0]
             lg, vl = self._c51_logits(hs, b, bv, pw, pwv)
             prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
             self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
                                    wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl)
         else:
-            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f)
+            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h)
 
     def q_values(self, flat: torch.Tensor, x: torch.Tensor, noise=None) -> torch.Tensor:
         """Q [B, A] (C51: expected value of the return distribution)."""
@@ -458,8 +461,17 @@ class HipExecutor:
         return pw, pwv
 
     # ----------------------------------------------------------- training
+    def supports_fused_acting(self) -> bool:
+        return not self.dist and not self.two_stream
+
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
-                      grad_out: torch.Tensor, noise=None, noise_target=None):
+                      grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None):
+        """acting (fused acting, slot batches only): {'stacks': [E, 4] int32 frame slots of the
+        device actors' states, 'ptrs', 'ints', 'f': the actor-step arguments of act_fused}. The
+        actors' states ride along as one more trunk / fc instance with the online weights, and
+        one extra workgroup of the head launch runs the eps-greedy / env / replay-append step:
+        acting costs no launches of its own. (The learner's minibatch is drawn before this
+        step's transitions land: a one-step lag vs acting first.)"""
         ext, lay = self.ext, self.layout
         frames = batch.get('frames')
         if frames is not None:             # slot batch: conv1 reads the replay frame ring directly
@@ -481,6 +493,10 @@ class HipExecutor:
         xs = [s, ns, ns][:ninst]
         packs = [po, pt, po][:ninst]
         flats = [eo, et, eo][:ninst]
+        if acting is not None:
+            assert frames is not None and self.supports_fused_acting(), 'fused acting needs a slot batch'
+            E = acting['stacks'].shape[0]
+            assert acting['stacks'].dtype == torch.int32 and acting['stacks'].is_contiguous() and E <= B
         # conv weight/bias grads are accumulated with atomics across M-chunks: the head
         # kernel zeroes that range in-kernel; fc grads are plain stores while B <= 32
         conv_lo = lay.offsets[self.arch.convs[0].name + '/w']
@@ -500,7 +516,11 @@ class HipExecutor:
             with torch.cuda.stream(side):
                 grad_out.zero_()
             ev_zero = self._event('zero', side)
-        self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames)
+        if acting is None:
+            self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames)
+        else:
+            self._fwd_trunk(xs + [acting['stacks']], packs + [po], flats + [eo], ws, B, ninst + 1, frames=frames,
+                            M=[B] * ninst + [E])
         if not zero_in_head:
             main.wait_event(ev_zero)
         zero = [grad_out.data_ptr() + 4 * conv_lo, conv_hi - conv_lo] if zero_in_head else []
@@ -523,7 +543,10 @@ class HipExecutor:
                    [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
                     wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
                     ws['q'].data_ptr() if not self.dist else 0, dw, db, dwv, dbv, ws['dh'].data_ptr()],
-                   *self._head_packs(packs), zero, [], [])
+                   *self._head_packs(packs), zero,
+                   [] if acting is None else list(acting['ptrs']) + list(acting['ints']),
+                   [] if acting is None else list(acting['f']),
+                   act_h=0 if acting is None else ws['h'][ninst].data_ptr())
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
@@ -616,8 +639,8 @@ class HipCnnExecutor(HipExecutor):
         bf = dict(dtype=torch.bfloat16, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         ws = {
-            'x3': torch.zeros(3, B * self.FLAT, **bf),
-            'h': torch.zeros(3, B * self.HH, **bf),
+            'x3': torch.zeros(4, B * self.FLAT, **bf),
+            'h': torch.zeros(4, B * self.HH, **bf),
             'a1': torch.zeros(B * 441 * 32, **bf), 'p1': torch.zeros(B * 121 * 32, **bf),
             'a2': torch.zeros(B * 36 * 64, **bf), 'p2': torch.zeros(B * 9 * 64, **bf),
             'a3': torch.zeros(B * 9 * 64, **bf),
@@ -630,9 +653,9 @@ class HipCnnExecutor(HipExecutor):
         self._ws[key] = ws
         return ws
 
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True):
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=()):
         lay = self.layout
-        pad = lambda v: list(v) + [0] * (3 - len(v))
+        pad = lambda v: list(v) + [0] * (4 - len(v))
         pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
         bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
         slots = [x.data_ptr() for x in xs] if frames is not None else []
@@ -641,7 +664,8 @@ class HipCnnExecutor(HipExecutor):
         ptrs = (pad(slots) + pad(states) + pad(pk('conv1/fwd')) + pad(pk('conv2/fwd')) + pad(pk('conv3/fwd'))
                 + pad(bias('conv1/b')) + pad(bias('conv2/b')) + pad(bias('conv3/b'))
                 + pad([ws['x3'][i].data_ptr() for i in range(ninst)]) + keep)
-        self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale)
+        self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale,
+                              list(M))
         self._fc_fwd(packs, ws, B, ninst)
 
     def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev):

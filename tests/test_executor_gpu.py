@@ -205,3 +205,39 @@ def test_cnn_learner_graph_equals_eager():
         torch.cuda.synchronize()
         outs.append(net.online.flat.clone())
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('network', ['nature', 'cnn'])
+def test_fused_acting_matches_separate_actor(network):
+    """The device actors' step inside the learner launches (extra trunk/fc instance + one
+    head workgroup) writes the same transitions / frames / eps as the stand-alone act_fused
+    path with the same weights and RNG."""
+    from dist_dqn_amd.actors.device_actor import DeviceActor
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    outs = []
+    for fused in (False, True):
+        cfg = preset(network if network == 'nature' else 'atari', 'Pong-v0',
+                     '--seed=4 --backend=hip --replay_memory_capacity=65536')
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        rep = DeviceReplay(65536, (84, 84), 4, device=DEV, seed=5)
+        rep.fill_synthetic(65536, 6, seed=5)
+        actor = DeviceActor(net, rep, cfg, num_envs=4, steps_per_call=1, seed=11, use_graph=False)
+        assert actor.can_fuse(cfg.minibatch_size)
+        ln = Learner(net, rep, cfg, use_graph=False, actor=actor if fused else None)
+        assert (ln.actor is not None) == fused
+        for _ in range(3):
+            if not fused:
+                actor.step()
+            ln.step()
+        torch.cuda.synchronize()
+        cur = rep.cursor.clone()
+        t0 = int(cur[0]) - 12
+        outs.append(dict(cursor=cur, actions=rep.actions[t0:t0 + 12].clone(), rewards=rep.rewards[t0:t0 + 12].clone(),
+                         eps=actor.eps.clone(), frames_done=actor.frames_done.clone(), stacks=actor.stacks.clone(),
+                         frame=rep.frames[int(actor.stacks[0, -1])].clone()))
+    a, b = outs
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
