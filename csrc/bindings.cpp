@@ -127,6 +127,35 @@ void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tens
                         (int)target_freq, cur_stream());
 }
 
+// optimizer step fused with the executor's weight packing (optim.hip optim_pack_kernel)
+void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s0, torch::Tensor s1,
+                torch::Tensor beta_pow, torch::Tensor ticket, double lr, double reg, int64_t reg_end,
+                double grad_scale, torch::Tensor step, std::vector<double> hp, torch::Tensor jobs,
+                torch::Tensor packed, c10::optional<torch::Tensor> target, c10::optional<torch::Tensor> target_packed,
+                int64_t target_freq) {
+  CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
+  CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
+  CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, torch::kBFloat16);
+  TORCH_CHECK(grad.numel() == w.numel() && hp.size() == 9, "optim_pack args");
+  TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
+  float* tgt = nullptr;
+  void* tgtp = nullptr;
+  if (target.has_value() && target->defined()) {
+    CHECK_T((*target), torch::kFloat32);
+    TORCH_CHECK(target->numel() == w.numel() && target_packed.has_value() && target_packed->defined() &&
+                target_packed->numel() == packed.numel() && target_freq >= 1, "optim_pack: target sync args");
+    tgt = ptr<float>(*target);
+    tgtp = target_packed->data_ptr();
+  }
+  float h[9];
+  for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
+  launch_optim_pack((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1), ptr<float>(beta_pow),
+                    ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
+                    (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
+                    tgtp, (int)target_freq, cur_stream());
+}
+
 void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tensor step, int64_t freq,
                    bool use_step, std::vector<torch::Tensor> extra) {
   CHECK_T(dst, torch::kFloat32); CHECK_T(src, torch::kFloat32);
@@ -266,6 +295,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("has_step"), pybind11::arg("hp"), pybind11::arg("target") = pybind11::none(),
         pybind11::arg("target_freq") = 1);
   m.def("target_update", &target_update);
+  m.def("optim_pack", &optim_pack);
+  m.attr("UPD_JOB_INTS") = upd_job_ints();
   m.def("td_loss_scalar", &td_loss_scalar);
   m.def("td_loss_c51", &td_loss_c51);
   m.def("preprocess_batch", &preprocess_batch);

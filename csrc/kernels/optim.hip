@@ -109,6 +109,187 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
   }
 }
 
+
+// ------------------------------------------------------------- update + pack
+// The optimizer step fused with the executor's weight packing: a workgroup owns
+// a 32 (k) x 64 (n) tile of a weight matrix (TF layout [K][N]), updates it in
+// registers (8 consecutive n per thread), writes fp32 weights + slots back, and
+// emits the tile's bf16 MFMA fragments straight away:
+//   * forward fragments ([K/32][N/16][64][8]: 8 consecutive k per lane) through
+//     one LDS transpose of the tile;
+//   * dgrad fragments (dense transpose, or conv (tap, co) x ci) directly from the
+//     thread's registers: their 8 consecutive K' ARE 8 consecutive n of one row.
+// Elementwise items (biases, ...) carry an optional fp32 copy into the packed
+// buffer (the concatenated fc bias). Same ticket as optim_kernel; the hard target
+// sync writes the target's fp32 master and packed fragments under the predicate.
+typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+
+struct UpdJob {
+  int kind;                      // 0 = tile, 1 = elementwise chunk
+  int src_off, K, N, k0, n0;     // tile: tensor offset / shape / origin; elem: offset, count (K)
+  int fwd_off, fwd_N16, fwd_nt_off, fwd_ks_off;   // forward fragments (elem: fp32 copy offset or -1)
+  int dg_mode, dg_off, dg_N16, dg_nt_off, dg_ks_off, dg_cin;   // dgrad: 0 none, 1 conv, 2 dense
+};
+
+template <int OP>
+DQN_DEV void upd8(float* w, const float* g, float* a, float* b, int k0flat, int reg_end, const OptHP& h,
+                  float lr_t, bool* ok) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (!ok[j]) continue;
+    float gg = g[j] * h.grad_scale;
+    if (k0flat + j < reg_end) gg += h.reg * w[j];
+    update_one<OP>(w[j], gg, a[j], b[j], h, lr_t);
+  }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(256)
+optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
+                  float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
+                  const UpdJob* __restrict__ jobs, int njobs, __bf16* __restrict__ packed, float* __restrict__ tgt,
+                  __bf16* __restrict__ tgt_packed, int tfreq) {
+  __shared__ __attribute__((aligned(16))) __bf16 tile[32 * 72];
+  float lr_t = h.lr;
+  if constexpr (OP == 3) {
+    const float b1p = beta_pow[0], b2p = beta_pow[1];
+    lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  }
+  const bool sync = tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6;
+  const int t = threadIdx.x;
+  for (int ji = blockIdx.x; ji < njobs; ji += gridDim.x) {
+    const UpdJob jb = jobs[ji];
+    float w[8], g[8], a[8], b[8];
+    bool ok[8];
+    if (jb.kind == 1) {                                   // elementwise chunk of up to 2048
+      const int base = jb.src_off + t * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ok[j] = t * 8 + j < jb.K;
+        const int i = base + j;
+        w[j] = ok[j] ? W[i] : 0.f; g[j] = ok[j] ? G[i] : 0.f;
+        a[j] = (OP != 0 && ok[j]) ? S0[i] : 0.f; b[j] = (TWO && ok[j]) ? S1[i] : 0.f;
+      }
+      upd8<OP>(w, g, a, b, base, h.reg_end, h, lr_t, ok);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!ok[j]) continue;
+        const int i = base + j;
+        W[i] = w[j];
+        if constexpr (OP != 0) S0[i] = a[j];
+        if constexpr (TWO) S1[i] = b[j];
+        if (sync) tgt[i] = w[j];
+        if (jb.fwd_off >= 0) {                            // fp32 copy inside the packed buffer
+          reinterpret_cast<float*>(packed + jb.fwd_off)[t * 8 + j] = w[j];
+          if (sync) reinterpret_cast<float*>(tgt_packed + jb.fwd_off)[t * 8 + j] = w[j];
+        }
+      }
+      continue;
+    }
+    // ---- tile: row r, 8 columns c8..c8+7
+    const int r = t >> 3, c8 = (t & 7) * 8;
+    const int k = jb.k0 + r, n = jb.n0 + c8;
+    const int64_t e0 = (int64_t)jb.src_off + (int64_t)k * jb.N + n;
+    const bool rowok = k < jb.K;
+    const bool vec = rowok && n + 8 <= jb.N && (jb.N % 4) == 0;
+    if (vec) {
+      const float4* W4 = reinterpret_cast<const float4*>(W + e0);
+      const float4* G4 = reinterpret_cast<const float4*>(G + e0);
+      const float4 w0 = W4[0], w1 = W4[1], g0 = G4[0], g1 = G4[1];
+      w[0] = w0.x; w[1] = w0.y; w[2] = w0.z; w[3] = w0.w; w[4] = w1.x; w[5] = w1.y; w[6] = w1.z; w[7] = w1.w;
+      g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
+      if constexpr (OP != 0) {
+        const float4 a0 = reinterpret_cast<const float4*>(S0 + e0)[0], a1 = reinterpret_cast<const float4*>(S0 + e0)[1];
+        a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+      }
+      if constexpr (TWO) {
+        const float4 b0 = reinterpret_cast<const float4*>(S1 + e0)[0], b1 = reinterpret_cast<const float4*>(S1 + e0)[1];
+        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ok[j] = true;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ok[j] = rowok && n + j < jb.N;
+        const int64_t i = e0 + j;
+        w[j] = ok[j] ? W[i] : 0.f; g[j] = ok[j] ? G[i] : 0.f;
+        a[j] = (OP != 0 && ok[j]) ? S0[i] : 0.f; b[j] = (TWO && ok[j]) ? S1[i] : 0.f;
+      }
+    }
+    upd8<OP>(w, g, a, b, (int)e0, h.reg_end, h, lr_t, ok);
+    if (vec) {
+      float4* W4 = reinterpret_cast<float4*>(W + e0);
+      W4[0] = make_float4(w[0], w[1], w[2], w[3]); W4[1] = make_float4(w[4], w[5], w[6], w[7]);
+      if (sync) {
+        float4* T4 = reinterpret_cast<float4*>(tgt + e0);
+        T4[0] = W4[0]; T4[1] = W4[1];
+      }
+      if constexpr (OP != 0) {
+        float4* A4 = reinterpret_cast<float4*>(S0 + e0);
+        A4[0] = make_float4(a[0], a[1], a[2], a[3]); A4[1] = make_float4(a[4], a[5], a[6], a[7]);
+      }
+      if constexpr (TWO) {
+        float4* B4 = reinterpret_cast<float4*>(S1 + e0);
+        B4[0] = make_float4(b[0], b[1], b[2], b[3]); B4[1] = make_float4(b[4], b[5], b[6], b[7]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!ok[j]) continue;
+        const int64_t i = e0 + j;
+        W[i] = w[j];
+        if constexpr (OP != 0) S0[i] = a[j];
+        if constexpr (TWO) S1[i] = b[j];
+        if (sync) tgt[i] = w[j];
+      }
+    }
+    bfx8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)(ok[j] ? w[j] : 0.f);
+    // dgrad fragments straight from the registers
+    if (jb.dg_mode != 0 && rowok) {
+      int kp, np;                                        // K' of the first of the 8 values, N'
+      if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
+      else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
+      const int lane = ((kp & 31) >> 3) * 16 + (np & 15);
+      const int64_t o = jb.dg_off + ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8;
+      if (n < jb.N) {
+        *reinterpret_cast<bfx8*>(packed + o) = v;
+        if (sync) *reinterpret_cast<bfx8*>(tgt_packed + o) = v;
+      }
+    }
+    // forward fragments through an LDS transpose of the bf16 tile
+    *reinterpret_cast<bfx8*>(tile + r * 72 + c8) = v;
+    __syncthreads();
+    {
+      const int nt = t >> 6, l = t & 63, nl = nt * 16 + (l & 15), kk = 8 * (l >> 4);
+      if (jb.n0 + nt * 16 < jb.N) {
+        bfx8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = tile[(kk + j) * 72 + nl];
+        const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
+                                                  ((jb.n0 >> 4) + nt)) * 64 + l) * 8;
+        *reinterpret_cast<bfx8*>(packed + o) = f;
+        if (sync) *reinterpret_cast<bfx8*>(tgt_packed + o) = f;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == (int)gridDim.x - 1) {
+      if (step) step[0] += 1;
+      if constexpr (OP == 3) {
+        beta_pow[0] *= h.b1;
+        beta_pow[1] *= h.b2;
+      }
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // target <- tau * online + (1 - tau) * target, optionally only when step % freq == 0.
 __global__ void __launch_bounds__(256)
 target_update_kernel(float* __restrict__ dst, const float* __restrict__ src, float tau,
@@ -172,6 +353,31 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
     default: break;
   }
 }
+
+void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
+                       int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
+                       const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
+                       hipStream_t st) {
+  OptHP h;
+  h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
+  h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
+  h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
+  const int grid = njobs < 256 ? njobs : 256;    // ticket arrivals <= 256 (see grid_for_ticket)
+  const UpdJob* J = reinterpret_cast<const UpdJob*>(jobs);
+  __bf16* P = reinterpret_cast<__bf16*>(packed);
+  __bf16* TP = reinterpret_cast<__bf16*>(tgt_packed);
+  const int tf = tfreq < 1 ? 1 : tfreq;
+#define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(256), 0, st, w, g, s0, s1, beta_pow, step, \
+                                  ticket, h, J, njobs, P, tgt, TP, tf)
+  switch (op) {
+    case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
+    case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break;
+    default: break;
+  }
+#undef OPK
+}
+
+int upd_job_ints() { return (int)(sizeof(UpdJob) / sizeof(int)); }
 
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
                           float* dst2, const float* src2, int n2, hipStream_t st) {

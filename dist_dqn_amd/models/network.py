@@ -122,6 +122,11 @@ class Network:
         ex = self.executor
         fuse = (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
                 and hasattr(ex, 'packed'))
+        if fuse and not getattr(ex, 'noisy', False) and hasattr(ex, 'update_and_pack'):
+            # optimizer + repack + hard target sync: one launch
+            ex.update_and_pack(self.optimizer, self.online.flat, self.grad, grad_scale, self.global_step,
+                               target=self.target.flat, target_freq=int(target_freq))
+            return True
         if fuse:
             self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,
                                 target=self.target.flat, target_freq=int(target_freq))

@@ -144,6 +144,65 @@ class HipExecutor:
         self._jobs_dev: Dict[torch.device, torch.Tensor] = {}
         self._max_threads = max(j.threads() for j in jobs)
         self._plan_noisy()
+        self._plan_update()
+
+    def _plan_update(self):
+        """Work list of the fused optimizer+pack kernel (optim.hip optim_pack_kernel): 32x64
+        tiles of every packed weight tensor (forward fragments + its dgrad fragments), then
+        2048-element chunks of everything else (with the fc bias fp32 copy)."""
+        lay = self.layout
+        fwd, dg, copy = {}, {}, {}
+        for j in self.jobs:
+            if j.mode == 0:
+                fwd[j.src_off] = j
+            elif j.mode in (1, 2):
+                dg[j.src_off] = j
+            else:
+                copy[j.src_off] = j
+        items = []
+        for src, f in sorted(fwd.items()):
+            d = dg.get(src)
+            for k0 in range(0, f.K, 32):
+                for n0 in range(0, f.N, 64):
+                    items.append([0, src, f.K, f.N, k0, n0, f.dst_off, f.dst_N16, f.nt_off, f.ks_off,
+                                  d.mode if d else 0, d.dst_off if d else 0, d.dst_N16 if d else 0,
+                                  d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0])
+        for name in lay.names:
+            off, n = lay.offsets[name], lay.numel(name)
+            if off in fwd:
+                continue
+            c = copy.get(off)
+            for s0 in range(0, n, 2048):
+                cnt = min(2048, n - s0)
+                items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + 2 * s0) if c else -1] + [0] * 9)
+        self.upd_items = items
+        self._upd_dev: Dict[torch.device, torch.Tensor] = {}
+
+    def update_and_pack(self, opt, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float,
+                        global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1):
+        """Optimizer step + repack in ONE launch (+ the hard target sync under the device
+        predicate when ``target`` is given). Returns False if the layout can't use it."""
+        from ..optim import OPT_IDS
+        dev = flat.device
+        jobs = self._upd_dev.get(dev)
+        if jobs is None:
+            ints = [v for it in self.upd_items for v in it]
+            assert len(ints) == len(self.upd_items) * self.ext.UPD_JOB_INTS
+            jobs = torch.tensor(ints, dtype=torch.int32, device=dev)
+            self._upd_dev[dev] = jobs
+        hp = opt.hp
+        s0 = opt.slots[0] if len(opt.slots) > 0 else flat
+        s1 = opt.slots[1] if len(opt.slots) > 1 else flat
+        if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev:
+            opt.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        p = self.packed(flat)
+        pt = self.packed(target) if target is not None else None
+        self.ext.optim_pack(OPT_IDS[opt.name], flat, grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr),
+                            float(opt.reg_param), int(opt.layout.reg_end), float(grad_scale), global_step,
+                            [float(hp['momentum']), float(hp['rho']), float(hp['rms_mom']), float(hp['rms_eps']),
+                             float(hp['b1']), float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']),
+                             float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq))
+        return True
 
     def _plan_noisy(self):
         """Mix jobs (rainbow.hip NoisyJob): every mu tensor -> the effective buffer;

@@ -241,3 +241,37 @@ def test_fused_acting_matches_separate_actor(network):
     a, b = outs
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize('extra', ['--optimizer=rmsprop', '--optimizer=adam --dueling', 'cnn:--optimizer=momentum'])
+def test_fused_update_and_pack_equals_optimizer_plus_repack(extra):
+    """optim_pack_kernel (update + forward/dgrad fragments + fp32 bias copy in one launch)
+    == the plain optimizer kernel followed by the pack kernel, bit for bit."""
+    net, _, batch = _setup(extra + ' --reg_param=0.001')
+    ex, opt = net.executor, net.optimizer
+    g = torch.Generator(device=DEV).manual_seed(9)
+    grad = torch.randn(net.online.flat.shape, device=DEV, generator=g) * 1e-2
+    states = []
+    for fused in (False, True):
+        flat = net.online.flat.clone()
+        slots = [s.clone() for s in opt.slots]
+        bp = opt.beta_powers.clone()
+        step = torch.zeros(1, dtype=torch.int64, device=DEV)
+        o_slots, o_bp = opt.slots, opt.beta_powers
+        opt.slots, opt.beta_powers = slots, bp
+        try:
+            for _ in range(2):
+                if fused:
+                    ex.update_and_pack(opt, flat, grad, 0.5, step)
+                else:
+                    opt.step(flat, grad, 0.5, step)
+                    ex.repack(flat)
+        finally:
+            opt.slots, opt.beta_powers = o_slots, o_bp
+        torch.cuda.synchronize()
+        states.append((flat, [s.clone() for s in slots], bp, step, ex.packed(flat).clone()))
+    (f0, s0, b0, st0, p0), (f1, s1, b1, st1, p1) = states
+    assert torch.equal(f0, f1) and torch.equal(b0, b1) and torch.equal(st0, st1)
+    for a, b in zip(s0, s1):
+        assert torch.equal(a, b)
+    assert torch.equal(p0.view(torch.int16), p1.view(torch.int16))
