@@ -21,8 +21,19 @@ struct OptHP {
   int reg_end;
 };
 
+// Contraction is pinned off in the update math so every kernel that inlines it
+// (optim_kernel's float4 loop, optim_pack_kernel's tiles) rounds identically:
+// with fp-contract=fast the backend fuses differently per call site.
+DQN_DEV float opt_grad(float g, float w, bool reg, const OptHP& h) {
+#pragma clang fp contract(off)
+  float x = g * h.grad_scale;
+  if (reg) x += h.reg * w;
+  return x;
+}
+
 template <int OP>
 DQN_DEV void update_one(float& w, float g, float& s0, float& s1, const OptHP& h, float lr_t) {
+#pragma clang fp contract(off)
   if constexpr (OP == 0) {            // sgd
     w -= h.lr * g;
   } else if constexpr (OP == 1) {     // momentum (non-Nesterov)
@@ -81,9 +92,7 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
     float aa[4] = {a.x, a.y, a.z, a.w}, bb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float g = gg[j] * h.grad_scale;
-      if (reg) g += h.reg * ww[j];
-      update_one<OP>(ww[j], g, aa[j], bb[j], h, lr_t);
+      update_one<OP>(ww[j], opt_grad(gg[j], ww[j], reg, h), aa[j], bb[j], h, lr_t);
     }
     const float4 nw = make_float4(ww[0], ww[1], ww[2], ww[3]);
     W[i] = nw;
@@ -137,9 +146,7 @@ DQN_DEV void upd8(float* w, const float* g, float* a, float* b, int k0flat, int 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (!ok[j]) continue;
-    float gg = g[j] * h.grad_scale;
-    if (k0flat + j < reg_end) gg += h.reg * w[j];
-    update_one<OP>(w[j], gg, a[j], b[j], h, lr_t);
+    update_one<OP>(w[j], opt_grad(g[j], w[j], k0flat + j < reg_end, h), a[j], b[j], h, lr_t);
   }
 }
 

@@ -40,9 +40,17 @@ def _torch_flags():
     return inc, libdirs, defs
 
 
-def _newer(src, obj, headers):
+def _newer(src, obj, headers, cmd=None):
     if not os.path.exists(obj):
         return True
+    if cmd is not None:                   # a flag change rebuilds too
+        stamp = obj + '.cmd'
+        line = ' '.join(cmd)
+        old = open(stamp).read() if os.path.exists(stamp) else ''
+        if old != line:
+            with open(stamp, 'w') as f:
+                f.write(line)
+            return True
     t = os.path.getmtime(obj)
     return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
 
@@ -60,21 +68,21 @@ def build(verbose=False, jobs=None):
         obj = os.path.join(BUILD, os.path.basename(src) + '.o')
         objs.append(obj)
         cmd = [HIPCC, '-c', src, '-o', obj, '-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH,
-               '-ffp-contract=fast', '-I' + os.path.join(ROOT, 'csrc'), '-D__HIP_PLATFORM_AMD__=1']
-        if _newer(src, obj, headers):
+               '-ffp-contract=fast-honor-pragmas', '-I' + os.path.join(ROOT, 'csrc'), '-D__HIP_PLATFORM_AMD__=1']
+        if _newer(src, obj, headers, cmd):
             cmds.append(cmd)
     for src in host:
         obj = os.path.join(BUILD, 'host_' + os.path.basename(src) + '.o')
         objs.append(obj)
         cmd = ['g++', '-c', src, '-o', obj, '-O3', '-std=c++17', '-fPIC', '-Wall']
-        if _newer(src, obj, headers):
+        if _newer(src, obj, headers, cmd):
             cmds.append(cmd)
     for src in binds:
         obj = os.path.join(BUILD, 'bind_' + os.path.basename(src) + '.o')
         objs.append(obj)
         cmd = [HIPCC, '-c', src, '-o', obj, '-O2', '-std=c++17', '-fPIC', '-I' + os.path.join(ROOT, 'csrc')] + \
               ['-I' + i for i in inc] + defs
-        if _newer(src, obj, headers):
+        if _newer(src, obj, headers, cmd):
             cmds.append(cmd)
 
     def run(cmd):

@@ -251,6 +251,13 @@ def test_fused_update_and_pack_equals_optimizer_plus_repack(extra):
     ex, opt = net.executor, net.optimizer
     g = torch.Generator(device=DEV).manual_seed(9)
     grad = torch.randn(net.online.flat.shape, device=DEV, generator=g) * 1e-2
+    # the fused path updates only named tensors (the alignment padding between them
+    # carries no gradient and no consumer): compare on the named regions
+    lay = net.layout
+    named = torch.zeros_like(grad, dtype=torch.bool)
+    for n in lay.names:
+        named[lay.offsets[n]:lay.offsets[n] + lay.numel(n)] = True
+    grad[~named] = 0.0
     states = []
     for fused in (False, True):
         flat = net.online.flat.clone()
@@ -271,7 +278,8 @@ def test_fused_update_and_pack_equals_optimizer_plus_repack(extra):
         torch.cuda.synchronize()
         states.append((flat, [s.clone() for s in slots], bp, step, ex.packed(flat).clone()))
     (f0, s0, b0, st0, p0), (f1, s1, b1, st1, p1) = states
-    assert torch.equal(f0, f1) and torch.equal(b0, b1) and torch.equal(st0, st1)
+    assert torch.equal(f0, f1), float((f0 - f1).abs().max())
+    assert torch.equal(b0, b1) and torch.equal(st0, st1)
     for a, b in zip(s0, s1):
-        assert torch.equal(a, b)
+        assert torch.equal(a[named], b[named]), float((a - b)[named].abs().max())
     assert torch.equal(p0.view(torch.int16), p1.view(torch.int16))
