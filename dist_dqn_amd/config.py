@@ -138,6 +138,8 @@ def build_parser() -> argparse.ArgumentParser:
       help='wire dtype of the gradient all-reduce (bf16 halves the bytes; optimizer stays fp32)')
     a('--grad_bucket_mb', default=64.0, type=float,
       help='all-reduce bucket size; the default keeps the whole flat gradient in ONE collective')
+    a('--overlap_allreduce', default=1, type=int,
+      help='DP: all-reduce the dense-layer gradients while the conv backward runs (two collectives)')
     a('--hip_graph', default=1, type=int, help='Capture the learner step in a HIP graph')
     a('--checkpoint_secs', default=600, type=int)
     a('--max_to_keep', default=5, type=int)
@@ -216,6 +218,7 @@ class Config:
     allreduce: str = 'rccl'
     allreduce_dtype: str = 'fp32'
     grad_bucket_mb: float = 64.0
+    overlap_allreduce: int = 1
     hip_graph: int = 1
     checkpoint_secs: int = 600
     max_to_keep: int = 5

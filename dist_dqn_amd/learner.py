@@ -63,6 +63,11 @@ class Learner:
         # fused acting: a DeviceActor whose acting step runs inside this learner's launches
         # (one more trunk/fc instance + one head workgroup); its own step() is then not used
         self.actor = actor if (actor is not None and actor.can_fuse(self.B)) else None
+        # data parallelism: all-reduce the dense-layer gradients (fc: ~95% of Nature-CNN's
+        # bytes) while the conv backward runs, then the conv gradients (config.overlap_allreduce)
+        self._tail = None
+        self._split = bool(self.ctx.enabled and ps_client is None and getattr(config, 'overlap_allreduce', True))
+        self._dense_hi = network.dense_range()[1] if self._split else 0
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -87,11 +92,14 @@ class Learner:
             if per:
                 batch['weights'] = self.weights
         self.net.reset_noise()
+        acting = None
         if self.actor is not None:
             assert 'frames' in batch, 'fused acting needs the slot-batch sampler'
-            loss, prio = self.net.compute_grads(batch, acting=self.actor.fused_args())
+            acting = self.actor.fused_args()
+        if self._split:
+            loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True)
         else:
-            loss, prio = self.net.compute_grads(batch)
+            loss, prio = self.net.compute_grads(batch, acting=acting)
         # keep references (static buffers under graph capture) instead of copies
         self.loss = loss.view(1)
         self.prio = prio.view(-1)
@@ -112,12 +120,34 @@ class Learner:
         elif not fused:
             self.net.hard_target_update(self.net.global_step, cfg.target_update_freq)
 
+    def _run_tail(self):
+        if self._tail is not None:
+            self._tail()
+
+    def _overlapped_allreduce(self, tail_runner):
+        """dense-range all-reduce || conv backward (tail_runner), then the remaining range."""
+        total = self.net.grad.numel()
+        if self._tail is None or self._dense_hi <= 0:
+            tail_runner()
+            self.reducer.allreduce()
+            return
+        with trace('allreduce.dense'):
+            h1 = self.reducer.allreduce_range_async(0, self._dense_hi)
+        tail_runner()
+        with trace('allreduce.rest'):
+            h2 = self.reducer.allreduce_range_async(self._dense_hi, total)
+        self.reducer.wait_all([h1, h2])
+
     def _eager_step(self):
         self._sample_and_grad()
         if self.ps is not None:
+            self._run_tail()
             self._ps_exchange()
             return
-        self.reducer.allreduce()
+        if self._split:
+            self._overlapped_allreduce(self._run_tail)
+        else:
+            self.reducer.allreduce()
         self._apply()
 
     def _ps_exchange(self):
@@ -144,9 +174,14 @@ class Learner:
             elif self.ctx.enabled:
                 with torch.cuda.graph(g_pre, stream=s):
                     self._sample_and_grad()
+                g_tail = None
+                if self._split and self._tail is not None:
+                    g_tail = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_tail, stream=s):
+                        self._tail()
                 with torch.cuda.graph(g_post, stream=s):
                     self._apply()
-                self._graphs = (g_pre, g_post)
+                self._graphs = (g_pre, g_post, g_tail)
             else:
                 with torch.cuda.graph(g_pre, stream=s):
                     self._sample_and_grad()
@@ -174,8 +209,12 @@ class Learner:
             if self.ps is not None:
                 self._ps_exchange()
             elif len(self._graphs) > 1:
-                with trace('allreduce'):
-                    self.reducer.allreduce()
+                g_tail = self._graphs[2]
+                if g_tail is not None:
+                    self._overlapped_allreduce(g_tail.replay)
+                else:
+                    with trace('allreduce'):
+                        self.reducer.allreduce()
                 self._graphs[1].replay()
         self.train_steps += 1
         return self.loss

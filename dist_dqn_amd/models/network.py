@@ -102,15 +102,35 @@ class Network:
             self.noise_target.normal_(generator=generator)
 
     # ------------------------------------------------------------- training
-    def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None):
+    def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False):
+        """Loss + gradient into ``self.grad``. ``split=True`` returns ``(loss, prio, tail)``: when
+        ``tail`` is not None only the dense-layer gradients (``dense_range()``) are final and
+        ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad)."""
+        kw = {}
         if acting is not None:     # fused acting (HIP executor): the actors' step rides along
-            loss, prio = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
-                                                     self.noise, self.noise_target, acting=acting)
-        else:
-            loss, prio = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
-                                                     self.noise, self.noise_target)
+            kw['acting'] = acting
+        can_split = split and hasattr(self.executor, 'supports_fused_acting')
+        if can_split:
+            kw['split'] = True
+        out = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
+                                          self.noise, self.noise_target, **kw)
+        loss, prio = out[0], out[1]
+        tail = out[2] if can_split else None
         self.last_loss = loss
-        return loss, prio
+        return (loss, prio, tail) if split else (loss, prio)
+
+    def dense_range(self):
+        """[0, X): the longest prefix of the flat buffer holding only dense-layer parameters
+        (the L2-regularised dense weights come first, `models/params.py`). Its gradient is final
+        before the conv backward runs, so data parallelism reduces it first."""
+        lay = self.layout
+        dense = {n for n in lay.names if not any(n.startswith(c.name + '/') for c in self.arch.convs)}
+        end = 0
+        for n in sorted(lay.names, key=lambda n: lay.offsets[n]):
+            if n not in dense:
+                break
+            end = lay.offsets[n] + lay.numel(n)
+        return 0, end
 
     def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None) -> bool:
         """Optimizer step (global_step += 1 inside it) + executor repack.

@@ -524,13 +524,20 @@ class HipExecutor:
         return not self.dist and not self.two_stream
 
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
-                      grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None):
+                      grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
+                      split: bool = False):
         """acting (fused acting, slot batches only): {'stacks': [E, 4] int32 frame slots of the
         device actors' states, 'ptrs', 'ints', 'f': the actor-step arguments of act_fused}. The
         actors' states ride along as one more trunk / fc instance with the online weights, and
         one extra workgroup of the head launch runs the eps-greedy / env / replay-append step:
         acting costs no launches of its own. (The learner's minibatch is drawn before this
-        step's transitions land: a one-step lag vs acting first.)"""
+        step's transitions land: a one-step lag vs acting first.)
+
+        split (data parallelism): return ``(loss, prio, tail)`` where this call has launched
+        everything up to the dense-layer weight gradients (the dense range of the flat gradient,
+        ~95% of Nature-CNN's bytes, is final when it returns) and ``tail()`` launches the conv
+        backward. The learner starts the all-reduce of the dense range between the two, so it
+        overlaps the conv backward. ``tail`` is None when this network has no split point."""
         ext, lay = self.ext, self.layout
         frames = batch.get('frames')
         if frames is not None:             # slot batch: conv1 reads the replay frame ring directly
@@ -616,7 +623,8 @@ class HipExecutor:
         else:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
         if self.arch.network == 'cnn':
-            return self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev)
+            out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev)
+            return out + (None,) if split else out
         x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         mc_fc = (B + 31) // 32 * 32
         K1, K2, K3 = c1.k * c1.k * c1.cin, c2.k * c2.k * c2.cin, c3.k * c3.k * c3.cin
@@ -629,27 +637,42 @@ class HipExecutor:
         if self.grouped_wgrad and not self.two_stream and B <= 32:
             # dgrad chain: dz3 = (dh W_fc^T)*(x3>0) -> dz2 -> dz1, then ONE grouped launch for
             # the four weight gradients (conv1 first: the longest member)
-            ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()],
-                           [x3], [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
-            ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [], [ws['dz2'].data_ptr()],
-                           [x2], [1.0], [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2,
-                                         h3, w3, 0, 0])
-            ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [], [ws['dz1'].data_ptr()],
-                           [x1], [1.0], [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1,
-                                         h2, w2, 0, 0])
-            ext.qnet_wgrad_group(
-                [[kind1, s.data_ptr(), ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout,
-                  c1.cout],
-                 [_KIND['C3'], x2, ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout],
-                 [_KIND['C2'], x1, ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout, c2.cout],
-                 [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]],
-                [d1, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
-                 [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]],
-                [self.input_scale, 1.0, 1.0, 1.0])
-            if self.noisy and noise is not None:
-                ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
-                                    len(self.noisy_jobs), self._noisy_max)
-            return ws['loss'], ws['prio']
+            members = [[kind1, s.data_ptr(), ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0,
+                        c1.cout, c1.cout],
+                       [_KIND['C3'], x2, ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout,
+                        c3.cout],
+                       [_KIND['C2'], x1, ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout,
+                        c2.cout],
+                       [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]]
+            dims = [d1, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
+                    [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]]
+            scales = [self.input_scale, 1.0, 1.0, 1.0]
+            noisy = self.noisy and noise is not None
+            if split and not noisy:
+                # dense weight gradients now (they need only dh and x3): the dense range is final
+                ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
+                members, dims, scales = members[:3], dims[:3], scales[:3]
+
+            def tail():
+                ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [],
+                               [ws['dz3'].data_ptr()], [x3], [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
+                ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [],
+                               [ws['dz2'].data_ptr()], [x2], [1.0],
+                               [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3,
+                                0, 0])
+                ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [],
+                               [ws['dz1'].data_ptr()], [x1], [1.0],
+                               [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
+                                0, 0])
+                ext.qnet_wgrad_group(members, dims, scales)
+                if noisy:
+                    ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
+                                        len(self.noisy_jobs), self._noisy_max)
+
+            if split and not noisy:
+                return ws['loss'], ws['prio'], tail
+            tail()
+            return (ws['loss'], ws['prio'], None) if split else (ws['loss'], ws['prio'])
         side.wait_event(self._event('head', main))
         with torch.cuda.stream(side):
             # fc wgrad: dW[F][HH] = x3^T dh, db = sum dh
@@ -681,7 +704,7 @@ class HipExecutor:
             ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                 len(self.noisy_jobs), self._noisy_max)
         main.wait_stream(side)
-        return ws['loss'], ws['prio']
+        return (ws['loss'], ws['prio'], None) if split else (ws['loss'], ws['prio'])
 
 
 class HipCnnExecutor(HipExecutor):

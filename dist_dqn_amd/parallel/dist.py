@@ -81,10 +81,13 @@ def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600) ->
     backend = 'none'
     if world > 1:
         backend = 'nccl' if use_gpu else 'gloo'
+        # DQN_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks on ONE
+        # device (RCCL refuses two ranks per GPU; gloo stages CUDA tensors through the host)
+        backend = os.environ.get('DQN_DIST_BACKEND', backend)
         if not dist.is_initialized():
             kw = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
-            if use_gpu:
+            if use_gpu and backend == 'nccl':
                 kw['device_id'] = dev
             dist.init_process_group(**kw)
     return DistContext(rank, world, local_rank, dev, backend)

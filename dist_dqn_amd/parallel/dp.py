@@ -58,6 +58,28 @@ class GradAllReducer:
         for lo, hi in self.buckets:
             dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM)
 
+    def allreduce_range_async(self, lo: int, hi: int):
+        """Start the sum of flat[lo:hi] (whole range, one collective); returns a handle for
+        ``wait_all``. RCCL runs it on its own stream, ordered after the work already queued on the
+        current stream, so the kernels queued next overlap it."""
+        if not self.ctx.enabled or hi <= lo:
+            return None
+        if self.wire is not None:
+            w = self.wire[lo:hi]
+            w.copy_(self.flat[lo:hi])
+            return (dist.all_reduce(w, op=dist.ReduceOp.SUM, async_op=True), lo, hi)
+        return (dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True), lo, hi)
+
+    def wait_all(self, handles):
+        """Make the current stream wait for the started range all-reduces (no host sync)."""
+        for h in handles:
+            if h is None:
+                continue
+            work, lo, hi = h
+            work.wait()
+            if self.wire is not None:
+                self.flat[lo:hi].copy_(self.wire[lo:hi])
+
     def allreduce_async(self, lo: int, hi: int):
         """Issue the sum of flat[lo:hi] on the comm stream (overlap with remaining backward)."""
         if not self.ctx.enabled:
