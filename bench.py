@@ -9,7 +9,8 @@ Per GPU (weak scaling): minibatch 32 from an HBM replay of synthetic 84x84x4
 uint8 frames, random-init Nature-CNN (VALID convs 32/64/64, FC512, A=6),
 RMSProp (TF semantics), MSE TD loss, target copy every 10k steps — one full
 SGD step per timed step (sample, gather, online+target forward, loss,
-backward, gradient all-reduce over RCCL when N > 1, optimizer, target
+backward, gradient all-reduce when N > 1 (peer-to-peer xGMI kernel inside the step's
+HIP graph, or RCCL, whichever the start-up probe measured faster), optimizer, target
 predicate). The device actor runs inside each timed step and writes its
 frames into the same replay: ``--actor_envs`` envs x ``update_freq // envs``
 batched eps-greedy steps = update_freq (4) env frames per SGD step, the
@@ -120,7 +121,9 @@ def main():
                        'hip_graph': bool(args.graph), 'actor_envs': args.actor_envs,
                        'acting': 'fused into the learner launches' if fused else 'separate launches',
                        'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
-                       'num_actions': args.actions, 'extra': args.extra, 'final_loss': loss},
+                       'num_actions': args.actions, 'extra': args.extra, 'final_loss': loss,
+                       'allreduce': learner.reducer.mode if ctx.enabled else None,
+                       'allreduce_probe_us': learner.reducer.timings or None},
         }
         print(json.dumps(out), flush=True)
     if ctx.enabled:

@@ -1,6 +1,7 @@
 // Python bindings of dist_dqn_amd._C: validates every operand on the host
 // (device, dtype, contiguity, shapes the kernels assume) and launches on the
 // current HIP stream, so the ops are captured correctly into HIP graphs.
+#include <cstring>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -281,11 +282,75 @@ int64_t ring_pop(torch::Tensor buf, torch::Tensor out, int64_t max_n) {
 }
 int64_t ring_size(torch::Tensor buf) { return dqn_ring_size(ptr<uint8_t>(buf)); }
 
+// ---------------------------------------------------------------- xGMI all-reduce
+// Fine-grained (uncached) device memory: peers read/write it over xGMI with no stale
+// cache lines (csrc/kernels/xgmi_ar.hip). Zeroed on allocation.
+int64_t xgmi_alloc(int64_t nbytes) {
+  TORCH_CHECK(nbytes > 0, "xgmi_alloc: size");
+  void* p = nullptr;
+  TORCH_CHECK(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocUncached) == hipSuccess,
+              "hipExtMallocWithFlags(uncached) failed");
+  TORCH_CHECK(hipMemset(p, 0, (size_t)nbytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess,
+              "xgmi_alloc: memset");
+  return reinterpret_cast<int64_t>(p);
+}
+void xgmi_free(int64_t p) { if (p) (void)hipFree(reinterpret_cast<void*>(p)); }
+torch::Tensor xgmi_ipc_handle(int64_t p) {
+  hipIpcMemHandle_t h;
+  TORCH_CHECK(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(p)) == hipSuccess, "hipIpcGetMemHandle failed");
+  auto out = torch::empty({(int64_t)sizeof(h)}, torch::kUInt8);
+  std::memcpy(out.data_ptr(), &h, sizeof(h));
+  return out;
+}
+int64_t xgmi_ipc_open(torch::Tensor handle) {
+  hipIpcMemHandle_t h;
+  TORCH_CHECK(!handle.is_cuda() && handle.numel() == (int64_t)sizeof(h) && handle.scalar_type() == torch::kUInt8,
+              "ipc handle: uint8 CPU tensor of the handle size");
+  std::memcpy(&h, handle.data_ptr(), sizeof(h));
+  void* p = nullptr;
+  TORCH_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess, "hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+void xgmi_ipc_close(int64_t p) { if (p) (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); }
+
+// grad: fp32 GPU slice to reduce in place; data/sig: one pointer per rank (mine included)
+void xgmi_allreduce(torch::Tensor grad, std::vector<int64_t> data, std::vector<int64_t> sig, int64_t seq,
+                    int64_t err, int64_t cap, int64_t rank, int64_t world, bool bf16, int64_t blocks) {
+  CHECK_T(grad, torch::kFloat32);
+  TORCH_CHECK(world >= 1 && world <= dqn::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi: rank/world");
+  TORCH_CHECK((int64_t)data.size() == world && (int64_t)sig.size() == world && seq && err, "xgmi: pointers");
+  TORCH_CHECK(grad.numel() % (4 * world) == 0 && grad.numel() <= cap, "xgmi: n % (4 world) and capacity");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(grad.data_ptr()) & 15) == 0, "xgmi: 16-byte aligned gradient");
+  TORCH_CHECK(blocks >= 1 && blocks <= dqn::kXgmiMaxBlocks, "xgmi: blocks");
+  dqn::XgmiArgs a{};
+  for (int i = 0; i < world; ++i) {
+    TORCH_CHECK(data[i] && sig[i], "xgmi: null peer pointer");
+    a.data[i] = reinterpret_cast<void*>(data[i]);
+    a.sig[i] = reinterpret_cast<uint32_t*>(sig[i]);
+  }
+  a.seq = reinterpret_cast<uint32_t*>(seq);
+  a.err = reinterpret_cast<int*>(err);
+  a.grad = ptr<float>(grad);
+  a.n = grad.numel();
+  a.cap = cap;
+  a.rank = (int)rank; a.world = (int)world; a.bf16 = bf16 ? 1 : 0;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
+  TORCH_CHECK(launch_xgmi_allreduce(a, (int)blocks, cur_stream()) == 0, "xgmi: launch arguments");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dist_dqn_amd native extension (gfx950 HIP kernels + C++ host runtime)";
   m.def("replay_sample_uniform", &replay_sample_uniform);
+  m.def("xgmi_alloc", &xgmi_alloc);
+  m.def("xgmi_free", &xgmi_free);
+  m.def("xgmi_ipc_handle", &xgmi_ipc_handle);
+  m.def("xgmi_ipc_open", &xgmi_ipc_open);
+  m.def("xgmi_ipc_close", &xgmi_ipc_close);
+  m.def("xgmi_allreduce", &xgmi_allreduce);
+  m.attr("XGMI_MAX_BLOCKS") = dqn::kXgmiMaxBlocks;
+  m.attr("XGMI_SIG_WORDS") = dqn::kXgmiMaxRanks * dqn::kXgmiMaxBlocks;
   m.def("replay_gather_frames", &replay_gather_frames);
   m.def("sumtree_set", &sumtree_set);
   m.def("sumtree_sample", &sumtree_sample);

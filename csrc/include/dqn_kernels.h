@@ -51,3 +51,20 @@ void launch_actor_step(const float* q, uint8_t* frames, int32_t* stacks, int64_t
                        int A, int K, int HW, int C, int F, float gamma, float p_done, hipStream_t st);
 void launch_stack_states(const uint8_t* frames, const int32_t* stacks, uint8_t* out, int E, int HW, int K,
                          hipStream_t st);
+
+// Peer-to-peer (xGMI) two-shot all-reduce, csrc/kernels/xgmi_ar.hip.
+namespace dqn {
+constexpr int kXgmiMaxRanks = 16;
+constexpr int kXgmiMaxBlocks = 256;
+struct XgmiArgs {
+  void* data[kXgmiMaxRanks];       // every rank's staging buffer (2 parities x cap elements), peer-mapped
+  uint32_t* sig[kXgmiMaxRanks];    // every rank's signal words [kXgmiMaxRanks][kXgmiMaxBlocks], peer-mapped
+  uint32_t* seq;                   // this rank's per-block call counters [kXgmiMaxBlocks]
+  int* err;                        // set to 1 by a block whose wait timed out
+  float* grad;                     // local gradient (in: my addend, out: the sum)
+  long n;                          // elements to reduce (n % (4 * world) == 0)
+  long cap;                        // staging capacity per parity, elements
+  int rank, world, bf16;
+};
+}  // namespace dqn
+int launch_xgmi_allreduce(const dqn::XgmiArgs& a, int blocks, hipStream_t st);

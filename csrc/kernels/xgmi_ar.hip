@@ -1,0 +1,192 @@
+// Peer-to-peer gradient all-reduce over xGMI (reference message M3, the per-step
+// gradient push of the async PS, /root/reference/src/network.py:198-202, here a
+// synchronous sum across data-parallel ranks).
+//
+// Every rank owns one fine-grained (uncached) HBM region, IPC-mapped into every
+// peer: [signal words][staging, 2 parities]. One launch does a two-shot all-reduce
+// entirely with direct loads over the point-to-point xGMI mesh:
+//   A  copy (fp32 or bf16) my gradient into my staging buffer, signal "A done"
+//   B  reduce-scatter: my 1/W slice = sum over ranks of their staging slice, written
+//      back to my gradient and to my staging slice, signal "B done"
+//   C  all-gather: every other slice is read from its owner's staging buffer
+// so each link carries 2*S/W bytes (S = message bytes) instead of a ring's 2(W-1)
+// latency hops, and the kernel is an ordinary launch: it is captured in the learner's
+// HIP graph with no host involvement.
+//
+// Synchronisation is per block: block b of every rank handles the same chunk of every
+// slice, so block b only waits for block b of its peers (no grid barrier, no
+// co-residency requirement beyond "each rank eventually runs block b"). Flags are
+// monotonically increasing per-block sequence numbers (2k+1 after A, 2k+2 after B of
+// call k), written with system-scope release stores into the PEER's signal words and
+// polled with system-scope acquire loads. Staging alternates parity per call, so a
+// slow peer still reading call k's staging never sees call k+1's writes (a rank can
+// only reach call k+2 after every peer passed A of call k+1).
+// Every spin has a wall-clock bound (s_memrealtime, 100 MHz): on expiry the block sets
+// the error word and returns instead of hanging the GPU; the host checks the word.
+#include "common.h"
+#include "../include/dqn_kernels.h"
+
+namespace dqn {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr uint64_t kTimeoutTicks = 1000000000ull;   // 10 s at 100 MHz
+
+DQN_DEV uint32_t load_acq(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+DQN_DEV void store_rel(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// publish this block's writes, then raise flag `val` for block b in every peer's signal words
+DQN_DEV void signal_all(const XgmiArgs& a, int b, uint32_t val) {
+  __threadfence_system();
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < a.world) store_rel(a.sig[t] + a.rank * kXgmiMaxBlocks + b, val);
+}
+
+// wait until every peer raised flag >= val for block b; false on timeout
+DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val) {
+  const int t = threadIdx.x;
+  __shared__ int timed_out;
+  if (t == 0) timed_out = 0;
+  __syncthreads();
+  if (t < a.world) {
+    const uint32_t* f = a.sig[a.rank] + t * kXgmiMaxBlocks + b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(load_acq(f) - val) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+        atomicExch(a.err, 1);
+        timed_out = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // system-scope acquire for every thread
+  return timed_out == 0;
+}
+
+struct F4 { float x, y, z, w; };
+
+template <bool BF16>
+DQN_DEV void put4(void* stage, long v, F4 f) {
+  if constexpr (BF16) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(f.x) | ((uint32_t)f2bf(f.y) << 16);
+    u.y = (uint32_t)f2bf(f.z) | ((uint32_t)f2bf(f.w) << 16);
+    reinterpret_cast<uint2*>(stage)[v] = u;
+  } else {
+    reinterpret_cast<float4*>(stage)[v] = make_float4(f.x, f.y, f.z, f.w);
+  }
+}
+
+template <bool BF16>
+DQN_DEV F4 get4(const void* stage, long v) {
+  if constexpr (BF16) {
+    const uint2 u = reinterpret_cast<const uint2*>(stage)[v];
+    return F4{bf2f((uint16_t)(u.x & 0xffff)), bf2f((uint16_t)(u.x >> 16)), bf2f((uint16_t)(u.y & 0xffff)),
+              bf2f((uint16_t)(u.y >> 16))};
+  } else {
+    const float4 q = reinterpret_cast<const float4*>(stage)[v];
+    return F4{q.x, q.y, q.z, q.w};
+  }
+}
+
+template <bool BF16>
+DQN_DEV F4 round_wire(F4 f) {           // the value every rank ends with: wire precision
+  if constexpr (BF16) {
+    return F4{bf2f(f2bf(f.x)), bf2f(f2bf(f.y)), bf2f(f2bf(f.z)), bf2f(f2bf(f.w))};
+  } else {
+    return f;
+  }
+}
+
+// WC: compile-time world size (0: runtime) so the per-peer loads of phases B/C are
+// unrolled and all in flight at once (remote xGMI loads are ~1 us round trips)
+template <bool BF16, int WC>
+__global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
+  const int b = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  const int W = WC ? WC : a.world, r = a.rank;
+  const uint32_t k = a.seq[b];                       // calls completed by this block
+  const int par = (int)(k & 1u);
+  const long esz = BF16 ? 2 : 4;
+  auto stage = [&](int q) -> char* { return reinterpret_cast<char*>(a.data[q]) + (long)par * a.cap * esz; };
+  float4* grad = reinterpret_cast<float4*>(a.grad);
+  const long nv = a.n / 4;                           // float4 vectors (host: n % (4 W) == 0)
+  const long sv = nv / W;                            // vectors per slice
+  // block b's share of every slice: [lo, hi) in slice-local vector units
+  const long per = (sv + G - 1) / G;
+  const long lo = per * b < sv ? per * b : sv;
+  const long hi = per * (b + 1) < sv ? per * (b + 1) : sv;
+
+  // ---- A: my gradient -> my staging (all slices, block b's chunk of each)
+  char* mine = stage(r);
+  for (int s = 0; s < W; ++s) {
+    for (long v = lo + t; v < hi; v += kThreads) {
+      const long i = (long)s * sv + v;
+      const float4 g = grad[i];
+      put4<BF16>(mine, i, F4{g.x, g.y, g.z, g.w});
+    }
+  }
+  signal_all(a, b, 2u * k + 1u);
+  if (!wait_all(a, b, 2u * k + 1u)) return;
+
+  // ---- B: reduce my slice over all ranks' staging (fixed rank order: identical sums everywhere)
+  for (long v = lo + t; v < hi; v += kThreads) {
+    const long i = (long)r * sv + v;
+    F4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < (WC ? WC : kXgmiMaxRanks); ++q) {
+      if (!WC && q >= W) break;
+      const F4 x = get4<BF16>(stage(q), i);
+      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    }
+    acc = round_wire<BF16>(acc);
+    put4<BF16>(mine, i, acc);
+    grad[i] = make_float4(acc.x, acc.y, acc.z, acc.w);
+  }
+  signal_all(a, b, 2u * k + 2u);
+  if (!wait_all(a, b, 2u * k + 2u)) return;
+
+  // ---- C: gather the other slices from their owners
+  for (long v = lo + t; v < hi; v += kThreads) {
+#pragma unroll
+    for (int d = 1; d < (WC ? WC : kXgmiMaxRanks); ++d) {
+      if (!WC && d >= W) break;
+      const int q = (r + d) % W;                      // stagger peers across links
+      const long i = (long)q * sv + v;
+      const F4 x = get4<BF16>(stage(q), i);
+      grad[i] = make_float4(x.x, x.y, x.z, x.w);
+    }
+  }
+  if (t == 0) a.seq[b] = k + 1u;
+}
+
+}  // namespace
+
+}  // namespace dqn
+
+int launch_xgmi_allreduce(const dqn::XgmiArgs& a, int blocks, hipStream_t st) {
+  if (blocks < 1 || blocks > dqn::kXgmiMaxBlocks || a.world < 1 || a.world > dqn::kXgmiMaxRanks) return 1;
+  if (a.n % (4L * a.world) != 0 || a.n > a.cap) return 2;
+#define XGMI_LAUNCH(WC)                                                                                   \
+  do {                                                                                                    \
+    if (a.bf16)                                                                                           \
+      hipLaunchKernelGGL((dqn::xgmi_allreduce_kernel<true, WC>), dim3(blocks), dim3(dqn::kThreads), 0, st, a); \
+    else                                                                                                  \
+      hipLaunchKernelGGL((dqn::xgmi_allreduce_kernel<false, WC>), dim3(blocks), dim3(dqn::kThreads), 0, st, a); \
+  } while (0)
+  switch (a.world) {
+    case 2: XGMI_LAUNCH(2); break;
+    case 4: XGMI_LAUNCH(4); break;
+    case 8: XGMI_LAUNCH(8); break;
+    default: XGMI_LAUNCH(0); break;
+  }
+#undef XGMI_LAUNCH
+  return 0;
+}

@@ -133,7 +133,9 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_eps_base', default=0.4, type=float, help='Ape-X per-actor epsilon base')
     a('--apex_eps_alpha', default=7.0, type=float, help='Ape-X per-actor epsilon exponent spread')
     a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
-    a('--allreduce', default='rccl', choices=['rccl'], help='gradient all-reduce transport (RCCL over xGMI)')
+    a('--allreduce', default='auto', choices=['auto', 'rccl', 'xgmi'],
+      help='gradient all-reduce transport: RCCL, the peer-to-peer xGMI kernel (in-graph), or auto '
+           '(self-test + time both at start-up, keep the faster)')
     a('--allreduce_dtype', default='fp32', choices=['fp32', 'bf16'],
       help='wire dtype of the gradient all-reduce (bf16 halves the bytes; optimizer stays fp32)')
     a('--grad_bucket_mb', default=64.0, type=float,
@@ -215,7 +217,7 @@ class Config:
     apex_eps_base: float = 0.4
     apex_eps_alpha: float = 7.0
     apex_ring: int = 1024
-    allreduce: str = 'rccl'
+    allreduce: str = 'auto'
     allreduce_dtype: str = 'fp32'
     grad_bucket_mb: float = 64.0
     overlap_allreduce: int = 1

@@ -68,6 +68,7 @@ class Learner:
         self._tail = None
         self._split = bool(self.ctx.enabled and ps_client is None and getattr(config, 'overlap_allreduce', True))
         self._dense_hi = network.dense_range()[1] if self._split else 0
+        self._ar_stream = None
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -138,13 +139,35 @@ class Learner:
             h2 = self.reducer.allreduce_range_async(self._dense_hi, total)
         self.reducer.wait_all([h1, h2])
 
+    def _kernel_allreduce(self):
+        """xgmi transport: both all-reduces are kernel launches (graph-capturable). The dense
+        range runs on a side stream (channel 0) concurrently with the conv backward; the conv
+        range follows on the main stream (channel 1)."""
+        total = self.net.grad.numel()
+        if self._tail is None or self._dense_hi <= 0:
+            self._run_tail()
+            self.reducer.allreduce_range(0, total, channel=0)
+            return
+        main = torch.cuda.current_stream(self.device)
+        if self._ar_stream is None:
+            self._ar_stream = torch.cuda.Stream(device=self.device)
+        side = self._ar_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.reducer.allreduce_range(0, self._dense_hi, channel=0)
+        self._tail()
+        self.reducer.allreduce_range(self._dense_hi, total, channel=1)
+        main.wait_stream(side)
+
     def _eager_step(self):
         self._sample_and_grad()
         if self.ps is not None:
             self._run_tail()
             self._ps_exchange()
             return
-        if self._split:
+        if self.reducer.in_graph:
+            self._kernel_allreduce()
+        elif self._split:
             self._overlapped_allreduce(self._run_tail)
         else:
             self.reducer.allreduce()
@@ -170,6 +193,12 @@ class Learner:
             if self.ps is not None:          # post-exchange work is host-driven (eager)
                 with torch.cuda.graph(g_pre, stream=s):
                     self._sample_and_grad()
+                self._graphs = (g_pre,)
+            elif self.ctx.enabled and self.reducer.in_graph:
+                with torch.cuda.graph(g_pre, stream=s):      # the whole DP step: ONE graph
+                    self._sample_and_grad()
+                    self._kernel_allreduce()
+                    self._apply()
                 self._graphs = (g_pre,)
             elif self.ctx.enabled:
                 with torch.cuda.graph(g_pre, stream=s):

@@ -125,11 +125,11 @@ class Network:
         before the conv backward runs, so data parallelism reduces it first."""
         lay = self.layout
         dense = {n for n in lay.names if not any(n.startswith(c.name + '/') for c in self.arch.convs)}
-        end = 0
+        end = lay.total
         for n in sorted(lay.names, key=lambda n: lay.offsets[n]):
             if n not in dense:
+                end = lay.offsets[n]        # 64-element aligned: whole collective vectors
                 break
-            end = lay.offsets[n] + lay.numel(n)
         return 0, end
 
     def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None) -> bool:

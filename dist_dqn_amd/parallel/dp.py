@@ -1,6 +1,5 @@
-"""Synchronous data parallelism over RCCL (replaces the reference's
-parameter server, `/root/reference/src/network.py:184-202` and
-`/root/reference/src/main.py:105-121`).
+"""Synchronous data parallelism (replaces the reference's parameter server,
+`/root/reference/src/network.py:184-202` and `/root/reference/src/main.py:105-121`).
 
 Every rank holds the online AND target parameters in HBM. Per SGD step the
 flat gradient buffer is summed across ranks and every rank applies the same
@@ -8,14 +7,24 @@ fused optimizer update with ``grad_scale = 1/world`` folded into the kernel,
 so parameters stay bit-identical without any parameter traffic (reference
 messages M1/M2/M4/M6 disappear; only M3 = one gradient all-reduce remains).
 
+Transports (``--allreduce``):
+  * ``rccl``  — ``torch.distributed`` all_reduce (RCCL over xGMI; gloo on the CPU),
+    issued between HIP-graph segments.
+  * ``xgmi``  — the peer-to-peer kernel of `parallel/xgmi.py` (IPC-mapped peer
+    buffers, two-shot over the point-to-point links); a plain launch, so the whole
+    step including both all-reduces stays ONE captured HIP graph.
+  * ``auto``  (default) — on GPUs, set up ``xgmi``, self-test it, time both on the
+    real gradient size and keep the faster (decided on rank 0, same on every rank);
+    RCCL whenever xgmi cannot be set up or fails its self-test.
+
 Gradient message sizing for xGMI: the reference `cnn` is
-0.58 MB fp32, Nature-CNN 6.7 MB. Messages this small are latency-bound on the
-7-link point-to-point mesh, so the default bucket holds the WHOLE flat
-gradient: one RCCL collective per SGD step. ``--allreduce_dtype=bf16`` sends
-bf16 on the wire (one cast kernel each way, fp32 master gradient kept).
+0.58 MB fp32, Nature-CNN 6.7 MB (95% of it the FC layer). ``--allreduce_dtype=bf16``
+sends bf16 on the wire (fp32 master gradient kept; every rank ends with the same
+bf16-rounded sum).
 """
 from __future__ import annotations
 
+import logging
 from typing import List, Optional, Tuple
 
 import torch
@@ -23,31 +32,93 @@ import torch.distributed as dist
 
 from .dist import DistContext
 
+log = logging.getLogger(__name__)
+
 
 class GradAllReducer:
     def __init__(self, ctx: DistContext, flat_grad: torch.Tensor, bucket_mb: float = 64.0,
-                 mode: str = 'rccl', wire_dtype: str = 'fp32'):
+                 mode: str = 'auto', wire_dtype: str = 'fp32'):
         self.ctx = ctx
         self.flat = flat_grad
-        self.mode = mode
         n = flat_grad.numel()
         per = max(1, int(bucket_mb * 1024 * 1024 / flat_grad.element_size()))
         per = (per + 63) // 64 * 64
         self.buckets: List[Tuple[int, int]] = [(o, min(n, o + per)) for o in range(0, n, per)]
         self.comm_stream = (torch.cuda.Stream(device=flat_grad.device)
                             if flat_grad.is_cuda and ctx.enabled else None)
-        assert mode == 'rccl', mode
+        assert mode in ('rccl', 'xgmi', 'auto'), mode
+        self.requested = mode
+        self.wire_dtype = wire_dtype
         self.wire = None
         if wire_dtype == 'bf16' and ctx.enabled:
             self.wire = torch.zeros(n, dtype=torch.bfloat16, device=flat_grad.device)
+        self.xgmi = None
+        self.timings = {}
+        if ctx.enabled and flat_grad.is_cuda and mode in ('xgmi', 'auto'):
+            self.xgmi = self._setup_xgmi(mode)
+        self.mode = 'xgmi' if self.xgmi is not None else 'rccl'
+
+    # ------------------------------------------------------------ transport choice
+    def _setup_xgmi(self, mode: str):
+        from .xgmi import XgmiAllReduce
+        n = self.flat.numel()
+        try:
+            x = XgmiAllReduce(self.ctx, n, self.wire_dtype)
+        except Exception as e:  # noqa: BLE001
+            if mode == 'xgmi':
+                raise
+            log.warning('xgmi all-reduce unavailable (%s); using RCCL', e)
+            return None
+        if not x.self_test(n):
+            x.close()
+            if mode == 'xgmi':
+                raise RuntimeError('xgmi all-reduce failed its self-test')
+            log.warning('xgmi all-reduce failed its self-test; using RCCL')
+            return None
+        if mode == 'auto':
+            t_x = self._time(lambda t: x.allreduce(t, 0))
+            t_r = self._time(lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM))
+            self.timings = {'xgmi_us': t_x, 'rccl_us': t_r}
+            if self.ctx.is_chief:
+                log.info('gradient all-reduce (%d elems): xgmi %.1f us, rccl %.1f us', n, t_x, t_r)
+            if t_x > t_r:
+                x.close()
+                return None
+        return x
+
+    def _time(self, fn, iters: int = 20) -> float:
+        """Mean us per call over ``iters`` (after 3 warm-up calls), max over ranks."""
+        t = torch.zeros_like(self.flat)
+        for _ in range(3):
+            fn(t)
+        self.ctx.barrier()
+        torch.cuda.synchronize(self.flat.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn(t)
+        e1.record()
+        torch.cuda.synchronize(self.flat.device)
+        us = torch.tensor([1000.0 * e0.elapsed_time(e1) / iters], dtype=torch.float64, device=self.flat.device)
+        dist.all_reduce(us, op=dist.ReduceOp.MAX)
+        return float(us)
+
+    @property
+    def in_graph(self) -> bool:
+        """True when the all-reduce is a plain kernel launch (capturable in the step graph)."""
+        return self.xgmi is not None
 
     @property
     def scale(self) -> float:
         return 1.0 / self.ctx.world_size
 
+    # --------------------------------------------------------------- collectives
     def allreduce(self):
         """Blocking (stream-ordered) sum of the whole flat gradient."""
         if not self.ctx.enabled:
+            return
+        if self.xgmi is not None:
+            self.xgmi.allreduce(self.flat, 0)
             return
         if self.wire is not None:
             self.wire.copy_(self.flat)
@@ -57,6 +128,13 @@ class GradAllReducer:
             return
         for lo, hi in self.buckets:
             dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM)
+
+    def allreduce_range(self, lo: int, hi: int, channel: int = 0):
+        """xgmi: sum of flat[lo:hi] on the current stream (graph-capturable); channels 0/1
+        may run concurrently on different streams."""
+        assert self.xgmi is not None
+        if hi > lo:
+            self.xgmi.allreduce(self.flat[lo:hi], channel)
 
     def allreduce_range_async(self, lo: int, hi: int):
         """Start the sum of flat[lo:hi] (whole range, one collective); returns a handle for
@@ -80,22 +158,15 @@ class GradAllReducer:
             if self.wire is not None:
                 self.flat[lo:hi].copy_(self.wire[lo:hi])
 
-    def allreduce_async(self, lo: int, hi: int):
-        """Issue the sum of flat[lo:hi] on the comm stream (overlap with remaining backward)."""
-        if not self.ctx.enabled:
-            return None
-        if self.comm_stream is None:
-            dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM)
-            return None
-        cur = torch.cuda.current_stream(self.flat.device)
-        self.comm_stream.wait_stream(cur)
-        with torch.cuda.stream(self.comm_stream):
-            dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM)
-        return self.comm_stream
+    def check(self):
+        """Raise if the xgmi transport reported a timed-out peer wait (host sync)."""
+        if self.xgmi is not None and not self.xgmi.check():
+            raise RuntimeError('xgmi all-reduce: a peer wait timed out (rank %d)' % self.ctx.rank)
 
-    def wait(self):
-        if self.comm_stream is not None:
-            torch.cuda.current_stream(self.flat.device).wait_stream(self.comm_stream)
+    def close(self):
+        if self.xgmi is not None:
+            self.xgmi.close()
+            self.xgmi = None
 
 
 def broadcast_flat(ctx: DistContext, flat: torch.Tensor, src: int = 0):

@@ -24,12 +24,87 @@ def _free_port():
     return p
 
 
+def _run_ranks(target, args, world=2, timeout=100):
+    ctx = mp.get_context('spawn')
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + tuple(args) + (errq,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=timeout)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not alive, 'rank(s) hung'
+    assert not errs, '\n'.join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _setup(rank, world, port):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK='0', DQN_DIST_BACKEND='gloo')
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _worker_xgmi(rank, world, port, wire, errq):
+    try:
+        _setup(rank, world, port)
+        from dist_dqn_amd.parallel import init_distributed
+        from dist_dqn_amd.parallel.xgmi import XgmiAllReduce
+        ctx = init_distributed(None, device='cuda')
+        cap = 1 << 20
+        x = XgmiAllReduce(ctx, cap, wire)
+        assert x.self_test(cap)
+        g = torch.Generator(device='cuda').manual_seed(1234)
+        for n in (8 * world, 4096 + 8 * world, cap):
+            for call in range(3):                          # both staging parities, then again
+                parts = [torch.randn(n, generator=g, device='cuda') for _ in range(world)]
+                t = parts[rank].clone()
+                x.allreduce(t, channel=call % 2)
+                torch.cuda.synchronize()
+                if wire == 'bf16':
+                    ref = sum(p.bfloat16().float() for p in parts).bfloat16().float()
+                else:
+                    ref = parts[0].clone()
+                    for p in parts[1:]:
+                        ref += p                            # same rank order as the kernel
+                assert torch.equal(t, ref), (n, call, (t - ref).abs().max())
+        # both channels concurrently on two streams (the learner's dense || conv schedule)
+        a = torch.full((cap,), float(rank + 1), device='cuda')
+        b = torch.full((4096,), float(10 * (rank + 1)), device='cuda')
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            x.allreduce(a, channel=0)
+        x.allreduce(b, channel=1)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        s = world * (world + 1) / 2
+        assert bool((a == s).all()) and bool((b == 10 * s).all())
+        assert x.check()
+        x.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 - report to the parent
+        import traceback
+        errq.put('rank %d: %s\n%s' % (rank, e, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize('wire', ['fp32', 'bf16'])
+def test_xgmi_allreduce_two_ranks_one_gpu(wire):
+    """The peer-to-peer kernel (IPC-mapped fine-grained buffers) against exact sums."""
+    _run_ranks(_worker_xgmi, (wire,))
+
+
 def _worker(rank, world, port, network, extra, errq):
     try:
-        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                          LOCAL_RANK='0', DQN_DIST_BACKEND='gloo')
-        import sys
-        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        _setup(rank, world, port)
         from dist_dqn_amd.config import preset
         from dist_dqn_amd.learner import Learner
         from dist_dqn_amd.models.network import Network
@@ -56,7 +131,12 @@ def _worker(rank, world, port, network, extra, errq):
             assert torch.isfinite(ln.loss).all()
             assert check_replicas_equal(ctx, net.online.flat), 'replicas diverged (overlap=%d)' % overlap
             assert int(net.global_step) == 6
-            if overlap and network == 'nature':
+            xgmi = '--allreduce=xgmi' in extra
+            assert ln.reducer.mode == ('xgmi' if xgmi else 'rccl')
+            if xgmi:
+                assert len(ln._graphs) == 1, 'xgmi DP step should be one graph'
+                ln.reducer.check()
+            elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
             outs[overlap] = net.online.flat.clone()
         # same data, same init: the overlapped schedule reduces the same sums (conv wgrads
@@ -70,23 +150,14 @@ def _worker(rank, world, port, network, extra, errq):
         raise
 
 
-@pytest.mark.parametrize('network,extra', [('nature', ''), ('nature', '--dueling --double_dqn --loss=huber'),
-                                           ('atari', ''), ('nature', '--allreduce_dtype=bf16')])
+@pytest.mark.parametrize('network,extra', [('nature', '--allreduce=rccl'),
+                                           ('nature', '--allreduce=rccl --dueling --double_dqn --loss=huber'),
+                                           ('atari', '--allreduce=rccl'),
+                                           ('nature', '--allreduce=rccl --allreduce_dtype=bf16'),
+                                           ('nature', '--allreduce=xgmi'),
+                                           ('nature', '--allreduce=xgmi --dueling --double_dqn --loss=huber'),
+                                           ('atari', '--allreduce=xgmi'),
+                                           ('nature', '--allreduce=xgmi --allreduce_dtype=bf16')])
 def test_dp_learner_two_ranks_one_gpu(network, extra):
-    ctx = mp.get_context('spawn')
-    errq = ctx.SimpleQueue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, network, extra, errq)) for r in range(2)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=100)
-    alive = [p for p in procs if p.is_alive()]
-    for p in alive:
-        p.kill()
-    errs = []
-    while not errq.empty():
-        errs.append(errq.get())
-    assert not alive, 'rank(s) hung'
-    assert not errs, '\n'.join(errs)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    """(--allreduce=rccl means the process group's collective: gloo in this rehearsal.)"""
+    _run_ranks(_worker, (network, extra))
