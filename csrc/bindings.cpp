@@ -22,6 +22,8 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUD
 
 template <typename T>
 T* ptr(const torch::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <class T>
+T P(int64_t v) { return reinterpret_cast<T>(static_cast<intptr_t>(v)); }
 
 // [] or [state_idx, next_idx, actions, rewards, dones, gammas, a_out, r_out, d_out, g_out, st_slots, nx_slots]
 SampleOut sample_out(const std::vector<torch::Tensor>& v, int64_t B) {
@@ -338,11 +340,50 @@ void xgmi_allreduce(torch::Tensor grad, std::vector<int64_t> data, std::vector<i
   TORCH_CHECK(launch_xgmi_allreduce(a, (int)blocks, cur_stream()) == 0, "xgmi: launch arguments");
 }
 
+// ---------------------------------------------------------------- fused MLP
+// ints: [L, A, P, Hs, Ds, sw, B, double, huber, fin x4, fout x4, act x4, w_off x4, b_off x4]
+// ptrs: [w_on, w_tg, x, xn, act, rew, done, gam, wts, loss, prio, grad, q_out] (0 = unused)
+void mlp(int64_t train, std::vector<int64_t> ints, std::vector<int64_t> ptrs, std::vector<double> flts,
+         torch::Tensor like) {
+  constexpr int NL = dqn::kMlpMaxLayers;
+  TORCH_CHECK(ints.size() == 9 + 5 * NL && ptrs.size() == 13 && flts.size() == 2, "mlp: argument counts");
+  CHECK_DEV(like);
+  dqn::MlpArgs a{};
+  a.L = (int)ints[0]; a.A = (int)ints[1]; a.P = (int)ints[2]; a.Hs = (int)ints[3]; a.Ds = (int)ints[4];
+  a.sw = (int)ints[5]; a.B = (int)ints[6]; a.double_dqn = (int)ints[7]; a.huber = (int)ints[8];
+  for (int l = 0; l < NL; ++l) {
+    a.fin[l] = (int)ints[9 + l]; a.fout[l] = (int)ints[9 + NL + l]; a.act[l] = (int)ints[9 + 2 * NL + l];
+    a.w_off[l] = (int)ints[9 + 3 * NL + l]; a.b_off[l] = (int)ints[9 + 4 * NL + l];
+  }
+  a.w_on = P<const float*>(ptrs[0]); a.w_tg = P<const float*>(ptrs[1]);
+  a.x = P<const float*>(ptrs[2]); a.xn = P<const float*>(ptrs[3]); a.act_idx = P<const int32_t*>(ptrs[4]);
+  a.rew = P<const float*>(ptrs[5]); a.done = P<const float*>(ptrs[6]); a.gam = P<const float*>(ptrs[7]);
+  a.wts = P<const float*>(ptrs[8]); a.loss = P<float*>(ptrs[9]); a.prio = P<float*>(ptrs[10]);
+  a.grad = P<float*>(ptrs[11]); a.q_out = P<float*>(ptrs[12]);
+  a.delta = (float)flts[0]; a.in_scale = (float)flts[1];
+  if (train) {
+    TORCH_CHECK(a.w_on && a.w_tg && a.x && a.xn && a.act_idx && a.rew && a.done && a.gam && a.loss && a.prio &&
+                a.grad, "mlp train: null operand");
+  } else {
+    TORCH_CHECK(a.w_on && a.x && a.q_out, "mlp forward: null operand");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(like.device());
+  const int rc = launch_mlp(a, (int)train, cur_stream());
+  TORCH_CHECK(rc == 0, "mlp: unsupported shape (code ", rc, ")");
+}
+int64_t mlp_lds_bytes(std::vector<int64_t> ints) {
+  dqn::MlpArgs a{};
+  a.P = (int)ints[0]; a.Hs = (int)ints[1]; a.Ds = (int)ints[2];
+  return (int64_t)mlp_train_lds_bytes(a);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dist_dqn_amd native extension (gfx950 HIP kernels + C++ host runtime)";
   m.def("replay_sample_uniform", &replay_sample_uniform);
+  m.def("mlp", &mlp);
+  m.def("mlp_lds_bytes", &mlp_lds_bytes);
   m.def("xgmi_alloc", &xgmi_alloc);
   m.def("xgmi_free", &xgmi_free);
   m.def("xgmi_ipc_handle", &xgmi_ipc_handle);

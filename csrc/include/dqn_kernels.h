@@ -68,3 +68,27 @@ struct XgmiArgs {
 };
 }  // namespace dqn
 int launch_xgmi_allreduce(const dqn::XgmiArgs& a, int blocks, hipStream_t st);
+
+// Fused MLP Q-network (reference SimpleNetwork), csrc/kernels/mlp.hip.
+namespace dqn {
+constexpr int kMlpMaxLayers = 4;
+constexpr int kMlpMaxWidth = 64;
+constexpr int kMlpThreads = 128;
+struct MlpArgs {
+  const float* w_on;               // online flat parameters (TF layouts: dense W [in, out])
+  const float* w_tg;               // target flat parameters
+  int L, A, P;                     // layers, actions, flat length
+  int Hs, Ds, sw;                  // LDS row strides (activations, deltas) and max layer width
+  int fin[kMlpMaxLayers], fout[kMlpMaxLayers], act[kMlpMaxLayers];   // act: 0 none, 1 tanh, 2 relu
+  int w_off[kMlpMaxLayers], b_off[kMlpMaxLayers];
+  const float* x;                  // states [B, fin0]
+  const float* xn;                 // next states [B, fin0]
+  const int32_t* act_idx;
+  const float* rew; const float* done; const float* gam; const float* wts;   // wts may be null
+  float* loss; float* prio; float* grad; float* q_out;
+  int B, double_dqn, huber;
+  float delta, in_scale;
+};
+}  // namespace dqn
+size_t mlp_train_lds_bytes(const dqn::MlpArgs& a);
+int launch_mlp(const dqn::MlpArgs& a, int train, hipStream_t st);

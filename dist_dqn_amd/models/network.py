@@ -44,7 +44,14 @@ def make_executor(arch: ArchSpec, layout, config, device: torch.device):
     backend = getattr(config, 'backend', 'auto')
     kw = dict(input_scale=config.input_scale, loss=config.loss, huber_delta=config.huber_delta,
               double_dqn=config.double_dqn)
-    if device.type == 'cuda' and backend in ('auto', 'hip'):
+    if device.type == 'cuda' and backend in ('auto', 'hip') and not arch.is_conv:
+        # MLP nets (the reference SimpleNetwork): one fused fp32 kernel per SGD step
+        from ..ops.mlp_executor import HipMlpExecutor, supports_mlp
+        if supports_mlp(arch):
+            return HipMlpExecutor(arch, layout, **kw)
+        if backend == 'hip':
+            raise RuntimeError('HIP MLP executor does not support %s' % (arch,))
+    if device.type == 'cuda' and backend in ('auto', 'hip') and arch.is_conv:
         from ..ops.executor import make_hip_executor, supports
         if supports(arch):
             return make_hip_executor(arch, layout, dtype=config.dtype, **kw)
