@@ -135,12 +135,14 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 torch::Tensor beta_pow, torch::Tensor ticket, double lr, double reg, int64_t reg_end,
                 double grad_scale, torch::Tensor step, std::vector<double> hp, torch::Tensor jobs,
                 torch::Tensor packed, c10::optional<torch::Tensor> target, c10::optional<torch::Tensor> target_packed,
-                int64_t target_freq) {
+                int64_t target_freq, int64_t max_grid) {
   CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
   CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
   CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, torch::kBFloat16);
   TORCH_CHECK(grad.numel() == w.numel() && hp.size() == 9, "optim_pack args");
   TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
+  TORCH_CHECK(max_grid <= 256 || ticket.numel() >= 17 * 32, "optim_pack: wide grid needs the 17x32-word ticket");
+  TORCH_CHECK(max_grid >= 1 && max_grid <= 65535, "optim_pack: max_grid");
   float* tgt = nullptr;
   void* tgtp = nullptr;
   if (target.has_value() && target->defined()) {
@@ -156,7 +158,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   launch_optim_pack((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1), ptr<float>(beta_pow),
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
-                    tgtp, (int)target_freq, cur_stream());
+                    tgtp, (int)target_freq, (int)max_grid, cur_stream());
 }
 
 void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tensor step, int64_t freq,

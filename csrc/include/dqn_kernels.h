@@ -31,7 +31,7 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
                            float grad_scale, int n, float* tgt, int tfreq, hipStream_t st);
 void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
-                       const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
+                       const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        hipStream_t st);
 int upd_job_ints();
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,

@@ -7,6 +7,15 @@
 
 #define DQN_DEV __device__ __forceinline__
 
+// Device-side bounds checks of the debug build (DQN_DEBUG=1 python setup.py build_ext):
+// a failing check traps the kernel with file:line; compiled out of the release build.
+#ifdef DQN_DEBUG
+#include <cassert>
+#define DQN_ASSERT(c) assert(c)
+#else
+#define DQN_ASSERT(c) ((void)0)
+#endif
+
 namespace dqn {
 
 constexpr int kWave = 64;

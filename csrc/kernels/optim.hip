@@ -133,6 +133,8 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 // sync writes the target's fp32 master and packed fragments under the predicate.
 typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
 
+constexpr int kTicketSubs = 16, kTicketStride = 32;    // hierarchical ticket: int32 words
+
 struct UpdJob {
   int kind;                      // 0 = tile, 1 = elementwise chunk
   int src_off, K, N, k0, n0;     // tile: tensor offset / shape / origin; elem: offset, count (K)
@@ -155,7 +157,7 @@ __global__ void __launch_bounds__(256)
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, __bf16* __restrict__ packed, float* __restrict__ tgt,
-                  __bf16* __restrict__ tgt_packed, int tfreq) {
+                  __bf16* __restrict__ tgt_packed, int tfreq, int hier) {
   __shared__ __attribute__((aligned(16))) __bf16 tile[32 * 72];
   float lr_t = h.lr;
   if constexpr (OP == 3) {
@@ -285,8 +287,24 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == (int)gridDim.x - 1) {
+    bool last;
+    if (hier) {
+      // two-level arrival ticket (one block per job: ~1k arrivals): blocks count into one
+      // of 16 sub-tickets on their own 128-byte lines; each sub-ticket's last arriver
+      // counts into the top ticket, whose last arriver is the grid's last block
+      const int j = blockIdx.x & (kTicketSubs - 1);
+      const int members = ((int)gridDim.x - j + kTicketSubs - 1) / kTicketSubs;
+      int32_t* sub = ticket + kTicketStride * (1 + j);
+      last = false;
+      if (__hip_atomic_fetch_add(sub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+        __hip_atomic_store(sub, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int nsub = (int)gridDim.x < kTicketSubs ? (int)gridDim.x : kTicketSubs;
+        last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1;
+      }
+    } else {
+      last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    }
+    if (last) {
       if (step) step[0] += 1;
       if constexpr (OP == 3) {
         beta_pow[0] *= h.b1;
@@ -364,18 +382,22 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
 void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
-                       hipStream_t st) {
+                       int max_grid, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
-  const int grid = njobs < 256 ? njobs : 256;    // ticket arrivals <= 256 (see grid_for_ticket)
+  // max_grid <= 256: grid-stride over the jobs with a flat ticket (<= 256 arrivals);
+  // larger: one block per job (up to max_grid) with the two-level ticket
+  const int cap = max_grid > 256 ? max_grid : 256;
+  const int grid = njobs < cap ? njobs : cap;
+  const int hier = grid > 256 ? 1 : 0;
   const UpdJob* J = reinterpret_cast<const UpdJob*>(jobs);
   __bf16* P = reinterpret_cast<__bf16*>(packed);
   __bf16* TP = reinterpret_cast<__bf16*>(tgt_packed);
   const int tf = tfreq < 1 ? 1 : tfreq;
 #define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(256), 0, st, w, g, s0, s1, beta_pow, step, \
-                                  ticket, h, J, njobs, P, tgt, TP, tf)
+                                  ticket, h, J, njobs, P, tgt, TP, tf, hier)
   switch (op) {
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
     case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break;

@@ -89,6 +89,7 @@ sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ 
     if (i < B) v = cand[i];
   }
   if (i < B) {
+    DQN_ASSERT(v >= 0 && (uint32_t)v < n);
     out[i] = v;
     write_sample_outputs(so, i, v);
   }
@@ -119,6 +120,8 @@ __global__ void gather_frames_kernel(const uint8_t* __restrict__ frames, const i
 #pragma unroll
   for (int c = 0; c < K; ++c) slots[c] = state_idx[(int64_t)tr * K + c];
   slots[K] = next_idx[tr];
+#pragma unroll
+  for (int c = 0; c <= K; ++c) DQN_ASSERT(slots[c] >= 0);
   uint32_t px[K + 1];
 #pragma unroll
   for (int c = 0; c <= K; ++c)

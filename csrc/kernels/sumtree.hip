@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(1024) sumtree_sample_kernel(const float* __res
     }
     const int n = max(size_p[0], 1);
     int leaf = min(node - P, n - 1);
+    DQN_ASSERT(leaf >= 0 && node >= P && node < 2 * P);
     idx_out[i] = leaf;
     const float beta = beta_p[0];
     const float p = sum[P + leaf] / total;

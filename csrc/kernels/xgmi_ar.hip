@@ -123,6 +123,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
   const long per = (sv + G - 1) / G;
   const long lo = per * b < sv ? per * b : sv;
   const long hi = per * (b + 1) < sv ? per * (b + 1) : sv;
+  DQN_ASSERT(a.n % (4L * W) == 0 && a.n <= a.cap && b < kXgmiMaxBlocks);
 
   // ---- A: my gradient -> my staging (all slices, block b's chunk of each)
   char* mine = stage(r);

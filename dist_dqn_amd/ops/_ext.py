@@ -17,7 +17,9 @@ def load(required: bool = False):
     global _ext, _err
     if _ext is None and _err is None:
         try:
-            _ext = importlib.import_module('dist_dqn_amd._C')
+            # DQN_DEBUG_EXT=1: the bounds-checked debug build (DQN_DEBUG=1 python setup.py build_ext)
+            name = '_C_debug' if os.environ.get('DQN_DEBUG_EXT', '0') == '1' else '_C'
+            _ext = importlib.import_module('dist_dqn_amd.' + name)
         except Exception as e:  # pragma: no cover - depends on build
             _err = e
     if _ext is None and required:

@@ -91,6 +91,10 @@ class HipExecutor:
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
+        # fused optimizer+pack grid: <= 256 = grid-stride with a flat ticket; larger = one block
+        # per 32x64 tile with the two-level ticket (DQN_OPT_GRID overrides, for A/B runs)
+        import os
+        self.opt_max_grid = int(os.environ.get('DQN_OPT_GRID', '2048'))
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self.head_prof = None       # int64 [16] C51 head phase stamps (scripts/probe_c51.py)
         self._events = {}
@@ -193,15 +197,15 @@ class HipExecutor:
         hp = opt.hp
         s0 = opt.slots[0] if len(opt.slots) > 0 else flat
         s1 = opt.slots[1] if len(opt.slots) > 1 else flat
-        if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev:
-            opt.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev or opt.ticket.numel() < 17 * 32:
+            opt.ticket = torch.zeros(17 * 32, dtype=torch.int32, device=dev)   # 1 + 16 sub-tickets, 128 B apart
         p = self.packed(flat)
         pt = self.packed(target) if target is not None else None
         self.ext.optim_pack(OPT_IDS[opt.name], flat, grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr),
                             float(opt.reg_param), int(opt.layout.reg_end), float(grad_scale), global_step,
                             [float(hp['momentum']), float(hp['rho']), float(hp['rms_mom']), float(hp['rms_eps']),
                              float(hp['b1']), float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']),
-                             float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq))
+                             float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq), self.opt_max_grid)
         return True
 
     def _plan_noisy(self):

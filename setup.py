@@ -21,8 +21,12 @@ import sysconfig
 ROOT = os.path.dirname(os.path.abspath(__file__))
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 HIPCC = os.path.join(os.environ.get('ROCM_PATH', '/opt/rocm'), 'bin', 'hipcc')
-BUILD = os.path.join(ROOT, 'build', 'obj')
-OUT = os.path.join(ROOT, 'dist_dqn_amd', '_C' + sysconfig.get_config_var('EXT_SUFFIX'))
+# DQN_DEBUG=1: bounds-checked debug variant (-O1 -g, device DQN_ASSERTs live) built next to
+# the release module as dist_dqn_amd/_C_debug*.so; selected at import by DQN_DEBUG_EXT=1
+DEBUG = os.environ.get('DQN_DEBUG', '0') == '1'
+MOD = '_C_debug' if DEBUG else '_C'
+BUILD = os.path.join(ROOT, 'build', 'obj_debug' if DEBUG else 'obj')
+OUT = os.path.join(ROOT, 'dist_dqn_amd', MOD + sysconfig.get_config_var('EXT_SUFFIX'))
 HOST_OUT = os.path.join(ROOT, 'dist_dqn_amd', 'libdqn_host.so')   # torch-free host runtime (ctypes)
 
 
@@ -36,7 +40,7 @@ def _torch_flags():
         else ce.library_paths(cuda=True)
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     defs = ['-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1', '-DTORCH_API_INCLUDE_EXTENSION_H',
-            '-DTORCH_EXTENSION_NAME=_C', '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi]
+            '-DTORCH_EXTENSION_NAME=%s' % MOD, '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi]
     return inc, libdirs, defs
 
 
@@ -67,8 +71,9 @@ def build(verbose=False, jobs=None):
     for src in kern:
         obj = os.path.join(BUILD, os.path.basename(src) + '.o')
         objs.append(obj)
-        cmd = [HIPCC, '-c', src, '-o', obj, '-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH,
-               '-ffp-contract=fast-honor-pragmas', '-I' + os.path.join(ROOT, 'csrc'), '-D__HIP_PLATFORM_AMD__=1']
+        cmd = [HIPCC, '-c', src, '-o', obj, '-O1' if DEBUG else '-O3', '-std=c++17', '-fPIC',
+               '--offload-arch=' + ARCH, '-ffp-contract=fast-honor-pragmas', '-I' + os.path.join(ROOT, 'csrc'),
+               '-D__HIP_PLATFORM_AMD__=1'] + (['-g', '-DDQN_DEBUG=1'] if DEBUG else [])
         if _newer(src, obj, headers, cmd):
             cmds.append(cmd)
     for src in host:
@@ -98,7 +103,7 @@ def build(verbose=False, jobs=None):
         for f in cf.as_completed([ex.submit(run, c) for c in cmds]):
             f.result()
     host_objs = [o for o in objs if os.path.basename(o).startswith('host_')]
-    if cmds or not os.path.exists(HOST_OUT):
+    if not DEBUG and (cmds or not os.path.exists(HOST_OUT)):
         run(['g++', '-shared', '-fPIC', '-o', HOST_OUT] + host_objs + ['-lpthread'])
     if cmds or not os.path.exists(OUT):
         link = [HIPCC, '-shared', '-fPIC', '-o', OUT] + objs + ['-L' + d for d in libdirs] + \
