@@ -41,7 +41,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--network', default='nature')
     ap.add_argument('--batch', type=int, default=32)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--backend', default='auto', choices=['auto', 'hip', 'torch'])
     ap.add_argument('--replay', type=int, default=200000)
     ap.add_argument('--actions', type=int, default=6)

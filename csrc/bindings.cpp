@@ -7,6 +7,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include "include/dqn_act.h"
 #include "include/dqn_host.h"
 #include "include/dqn_kernels.h"
 #include "include/dqn_nets.h"
@@ -138,7 +139,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 int64_t target_freq, int64_t max_grid) {
   CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
   CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
-  CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, torch::kBFloat16);
+  CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
   TORCH_CHECK(grad.numel() == w.numel() && hp.size() == 9, "optim_pack args");
   TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
   TORCH_CHECK(max_grid <= 256 || ticket.numel() >= 17 * 32, "optim_pack: wide grid needs the 17x32-word ticket");

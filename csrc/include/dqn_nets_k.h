@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "dqn_act.h"
 
 namespace dqn {
 
@@ -110,7 +111,7 @@ struct TrunkArgs {
   const uint8_t* states[kMaxInst]; // [B][84][84][4] NHWC stacks per instance (materialised path)
   const void* w1[kMaxInst]; const void* w2[kMaxInst]; const void* w3[kMaxInst];   // packed bf16 fragments
   const float* b1[kMaxInst]; const float* b2[kMaxInst]; const float* b3[kMaxInst];
-  __bf16* x1[kMaxInst]; __bf16* x2[kMaxInst]; __bf16* x3[kMaxInst];   // activations out ([B][...] NHWC)
+  act_t* x1[kMaxInst]; act_t* x2[kMaxInst]; act_t* x3[kMaxInst];   // activations out ([B][...] NHWC)
   int M[kMaxInst];                 // valid samples per instance (the fused actor's E < B)
   float scale;                     // input scale folded into conv1
   int64_t* prof;                   // optional [ninst][B][8] s_memtime phase stamps (profiling)
@@ -123,17 +124,17 @@ struct CnnFwdArgs {
   const uint8_t* states[kMaxInst];
   const void* w1[kMaxInst]; const void* w2[kMaxInst]; const void* w3[kMaxInst];   // packed bf16 fwd fragments
   const float* b1[kMaxInst]; const float* b2[kMaxInst]; const float* b3[kMaxInst];
-  __bf16* a1; __bf16* p1; __bf16* a2; __bf16* p2; __bf16* a3;  // instance 0, for the backward
-  __bf16* x3[kMaxInst];                                        // [B][256] pooled fc inputs
+  act_t* a1; act_t* p1; act_t* a2; act_t* p2; act_t* a3;  // instance 0, for the backward
+  act_t* x3[kMaxInst];                                        // [B][256] pooled fc inputs
   int M[kMaxInst];                                             // valid samples per instance
   float scale;
 };
 
 struct CnnBwdArgs {
-  const __bf16* dp3;                          // [B][256] d(pool3 out), masked by its ReLU
-  const __bf16* a1; const __bf16* a2; const __bf16* a3;   // post-ReLU pre-pool activations
+  const act_t* dp3;                          // [B][256] d(pool3 out), masked by its ReLU
+  const act_t* a1; const act_t* a2; const act_t* a3;   // post-ReLU pre-pool activations
   const void* w3d; const void* w2d;           // packed conv3 / conv2 dgrad fragments
-  __bf16* dz1; __bf16* dz2; __bf16* dz3;      // d(conv pre-activation) for the wgrads
+  act_t* dz1; act_t* dz2; act_t* dz3;      // d(conv pre-activation) for the wgrads
 };
 
 // Grouped weight-gradient launch (qnet.hip): up to 4 independent layers.

@@ -42,12 +42,12 @@ DQN_DEV bfx8 max8(bfx8 a, const bfx8& b) {
 
 __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   using namespace cnn;
-  __shared__ __attribute__((aligned(16))) __bf16 xin[XW * XW * 4];
-  __shared__ __attribute__((aligned(16))) __bf16 a1[R1 * L1];
-  __bf16* p1p = xin + OFF_P1;
-  __bf16* a2 = xin + OFF_A2;
-  __bf16* p2p = xin + OFF_P2;
-  __bf16* a3 = xin + OFF_A3;
+  __shared__ __attribute__((aligned(16))) act_t xin[XW * XW * 4];
+  __shared__ __attribute__((aligned(16))) act_t a1[R1 * L1];
+  act_t* p1p = xin + OFF_P1;
+  act_t* a2 = xin + OFF_A2;
+  act_t* p2p = xin + OFF_P2;
+  act_t* a3 = xin + OFF_A3;
   float* red = reinterpret_cast<float*>(xin + OFF_RED);
   const int b = blockIdx.x, inst = blockIdx.y;
   if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     const int t = tid + 512 * j;
     if (t >= NT) continue;
     const int y = (4 * t) / IH, x = 4 * t - y * IH;          // 4 consecutive pixels of one row
-    __bf16* dst = xin + ((y + XP) * XW + x + XP) * 4;
+    act_t* dst = xin + ((y + XP) * XW + x + XP) * 4;
     if (slot_path) {
       planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], dst);
     } else {
@@ -123,12 +123,12 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   {
     const float scale = a.scale;
     const int kw = kg >> 2;
-    __bf16* ga1 = keep ? a.a1 + (int64_t)b * R1 * N1 : nullptr;
+    act_t* ga1 = keep ? a.a1 + (int64_t)b * R1 * N1 : nullptr;
     for (int mt = wave; mt < (R1 + 15) / 16; mt += 8) {
       const int p = mt * 16 + l16;
       const bool ok = p < R1;
       const int oy = ok ? p / O1 : 0, ox = ok ? p - oy * O1 : 0;
-      const __bf16* base = xin + ((oy * 4) * XW + ox * 4 + kw) * 4;
+      const act_t* base = xin + ((oy * 4) * XW + ox * 4 + kw) * 4;
       bfx8 fa[K1 / 32];
 #pragma unroll
       for (int ks = 0; ks < K1 / 32; ++ks) fa[ks] = ok ? *reinterpret_cast<const bfx8*>(base + ks * XW * 4) : tz8();
@@ -181,12 +181,12 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
 
   // ---- conv2 (4x4/2 SAME) -> a2: wave = n-tile (wave & 3), m-tiles {wave>>2, +2}
   {
-    __bf16* ga2 = keep ? a.a2 + (int64_t)b * R2 * N2 : nullptr;
+    act_t* ga2 = keep ? a.a2 + (int64_t)b * R2 * N2 : nullptr;
     for (int mt = hi; mt < (R2 + 15) / 16; mt += 2) {
       const int p = mt * 16 + l16;
       const bool ok = p < R2;
       const int oy = ok ? p / O2 : 0, ox = ok ? p - oy * O2 : 0;
-      const __bf16* base = p1p + ((oy * 2) * P1W + ox * 2) * LP1 + kg;
+      const act_t* base = p1p + ((oy * 2) * P1W + ox * 2) * LP1 + kg;
       bfx8 fa[K2 / 32];
 #pragma unroll
       for (int ks = 0; ks < K2 / 32; ++ks)                 // k = (kh*4 + kw)*32 + ci
@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   // ---- pool2 (6 -> 3) -> padded p2
   for (int t = tid; t < Q2 * Q2 * 8; t += 512) {
     const int pix = t >> 3, c8 = (t & 7) * 8, py = pix / Q2, px = pix - py * Q2;
-    const __bf16* r0 = a2 + ((2 * py) * O2 + 2 * px) * L2 + c8;
+    const act_t* r0 = a2 + ((2 * py) * O2 + 2 * px) * L2 + c8;
     bfx8 m = max8(*reinterpret_cast<const bfx8*>(r0), *reinterpret_cast<const bfx8*>(r0 + L2));
     m = max8(m, *reinterpret_cast<const bfx8*>(r0 + O2 * L2));
     m = max8(m, *reinterpret_cast<const bfx8*>(r0 + O2 * L2 + L2));
@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     const int p = l16;
     const bool ok = p < R3;
     const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
-    const __bf16* base = p2p + (oy * P2W + ox) * LP2 + kg;
+    const act_t* base = p2p + (oy * P2W + ox) * LP2 + kg;
     bfx8 fa[K3 / 64];
 #pragma unroll
     for (int j = 0; j < K3 / 64; ++j) {                    // k = (kh*3 + kw)*64 + ci
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
 // ======================================================================= backward
 // position (y, x) of a pre-pool map is the argmax of its 2x2/2 window (first max in
 // row-major order over the valid cells) for channel c?
-DQN_DEV bool is_argmax(const __bf16* act, int OW, int OH, int L, int y, int x, int c) {
+DQN_DEV bool is_argmax(const act_t* act, int OW, int OH, int L, int y, int x, int c) {
   const int y0 = y & ~1, x0 = x & ~1;
   float best = -INFINITY;
   int by = y0, bx = x0;
@@ -291,20 +291,20 @@ DQN_DEV bool is_argmax(const __bf16* act, int OW, int OH, int L, int y, int x, i
 
 __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   using namespace cnn;
-  __shared__ __attribute__((aligned(16))) __bf16 a1s[R1 * N1];
-  __shared__ __attribute__((aligned(16))) __bf16 a2s[R2 * N2];
-  __shared__ __attribute__((aligned(16))) __bf16 a3s[R3 * N3];
-  __shared__ __attribute__((aligned(16))) __bf16 dz3s[R3 * L3];
-  __shared__ __attribute__((aligned(16))) __bf16 dz2s[R2 * L2];
+  __shared__ __attribute__((aligned(16))) act_t a1s[R1 * N1];
+  __shared__ __attribute__((aligned(16))) act_t a2s[R2 * N2];
+  __shared__ __attribute__((aligned(16))) act_t a3s[R3 * N3];
+  __shared__ __attribute__((aligned(16))) act_t dz3s[R3 * L3];
+  __shared__ __attribute__((aligned(16))) act_t dz2s[R2 * L2];
   __shared__ __attribute__((aligned(16))) float dp3s[Q3 * Q3 * N3];
   __shared__ __attribute__((aligned(16))) float dp2[Q2 * Q2 * N2];
   __shared__ __attribute__((aligned(16))) float dp1[Q1 * Q1 * N1];
   __shared__ __attribute__((aligned(16))) float red[4 * 256];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, kg = 8 * (lane >> 4);
-  const __bf16* ga1 = a.a1 + (int64_t)b * R1 * N1;
-  const __bf16* ga2 = a.a2 + (int64_t)b * R2 * N2;
-  const __bf16* ga3 = a.a3 + (int64_t)b * R3 * N3;
+  const act_t* ga1 = a.a1 + (int64_t)b * R1 * N1;
+  const act_t* ga2 = a.a2 + (int64_t)b * R2 * N2;
+  const act_t* ga3 = a.a3 + (int64_t)b * R3 * N3;
   for (int t = tid; t < R1 * N1 / 8; t += 512)
     reinterpret_cast<bfx8*>(a1s)[t] = reinterpret_cast<const bfx8*>(ga1)[t];
   for (int t = tid; t < R2 * N2 / 8; t += 512)
@@ -319,8 +319,8 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
     const float av = (float)a3s[p * N3 + c];
     float d = 0.f;
     if (av > 0.f && is_argmax(a3s, O3, O3, N3, y, x, c)) d = dp3s[((y >> 1) * Q3 + (x >> 1)) * N3 + c];
-    dz3s[p * L3 + c] = (__bf16)d;
-    a.dz3[(int64_t)b * R3 * N3 + t] = (__bf16)d;
+    dz3s[p * L3 + c] = (act_t)d;
+    a.dz3[(int64_t)b * R3 * N3 + t] = (act_t)d;
   }
   __syncthreads();
 
@@ -358,8 +358,8 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
     const float av = (float)a2s[p * N2 + c];
     float d = 0.f;
     if (av > 0.f && is_argmax(a2s, O2, O2, N2, y, x, c)) d = dp2[((y >> 1) * Q2 + (x >> 1)) * N2 + c];
-    dz2s[p * L2 + c] = (__bf16)d;
-    a.dz2[(int64_t)b * R2 * N2 + t] = (__bf16)d;
+    dz2s[p * L2 + c] = (act_t)d;
+    a.dz2[(int64_t)b * R2 * N2 + t] = (act_t)d;
   }
   __syncthreads();
 
@@ -395,13 +395,13 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   __syncthreads();
 
   // ---- pool1 backward + mask -> dz1 (global only: the conv1 wgrad input)
-  __bf16* gdz1 = a.dz1 + (int64_t)b * R1 * N1;
+  act_t* gdz1 = a.dz1 + (int64_t)b * R1 * N1;
   for (int t = tid; t < R1 * N1; t += 512) {
     const int p = t / N1, c = t - p * N1, y = p / O1, x = p - y * O1;
     const float av = (float)a1s[p * N1 + c];
     float d = 0.f;
     if (av > 0.f && is_argmax(a1s, O1, O1, N1, y, x, c)) d = dp1[((y >> 1) * Q1 + (x >> 1)) * N1 + c];
-    gdz1[t] = (__bf16)d;
+    gdz1[t] = (act_t)d;
   }
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include "../include/dqn_act.h"
 
 #define DQN_DEV __device__ __forceinline__
 

@@ -7,12 +7,12 @@
 
 namespace dqn {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+typedef __attribute__((ext_vector_type(8))) act_t bfx8;
 
 DQN_DEV bfx8 tz8() {
   bfx8 z;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  for (int j = 0; j < 8; ++j) z[j] = (act_t)0.f;
   return z;
 }
 
@@ -20,24 +20,24 @@ DQN_DEV f32x4 f4(const float4& v) { return f32x4{v.x, v.y, v.z, v.w}; }
 
 // ReLU + 4 floats -> 4 packed bf16 (8 bytes)
 DQN_DEV uint2 pack4(const f32x4& v) {
-  const __bf16 a = (__bf16)fmaxf(v[0], 0.f), b = (__bf16)fmaxf(v[1], 0.f);
-  const __bf16 c = (__bf16)fmaxf(v[2], 0.f), d = (__bf16)fmaxf(v[3], 0.f);
+  const act_t a = (act_t)fmaxf(v[0], 0.f), b = (act_t)fmaxf(v[1], 0.f);
+  const act_t c = (act_t)fmaxf(v[2], 0.f), d = (act_t)fmaxf(v[3], 0.f);
   return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16),
                     (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16));
 }
 
 DQN_DEV f32x4 tmfma(const bfx8& a, const bfx8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  return DQN_MFMA16_BUILTIN(a, b, c, 0, 0, 0);
 }
 
 // 4 pixels x 4 channels (one uint32 per channel plane, or one uint4 NHWC word
 // group) -> 4 NHWC bf16 pixels (32 B) in LDS.
 DQN_DEV uint32_t bfpair(uint32_t a, uint32_t b) {   // two integers 0..255 -> packed bf16 (exact)
-  const __bf16 x = (__bf16)(float)a, y = (__bf16)(float)b;
+  const act_t x = (act_t)(float)a, y = (act_t)(float)b;
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
-DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, __bf16* dst) {
+DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, act_t* dst) {
   uint32_t o[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -131,7 +131,7 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 // Elementwise items (biases, ...) carry an optional fp32 copy into the packed
 // buffer (the concatenated fc bias). Same ticket as optim_kernel; the hard target
 // sync writes the target's fp32 master and packed fragments under the predicate.
-typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+typedef __attribute__((ext_vector_type(8))) act_t bfx8;
 
 constexpr int kTicketSubs = 16, kTicketStride = 32;    // hierarchical ticket: int32 words
 
@@ -156,9 +156,9 @@ template <int OP>
 __global__ void __launch_bounds__(256)
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
-                  const UpdJob* __restrict__ jobs, int njobs, __bf16* __restrict__ packed, float* __restrict__ tgt,
-                  __bf16* __restrict__ tgt_packed, int tfreq, int hier) {
-  __shared__ __attribute__((aligned(16))) __bf16 tile[32 * 72];
+                  const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
+                  act_t* __restrict__ tgt_packed, int tfreq, int hier) {
+  __shared__ __attribute__((aligned(16))) act_t tile[32 * 72];
   float lr_t = h.lr;
   if constexpr (OP == 3) {
     const float b1p = beta_pow[0], b2p = beta_pow[1];
@@ -256,7 +256,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     bfx8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (__bf16)(ok[j] ? w[j] : 0.f);
+    for (int j = 0; j < 8; ++j) v[j] = (act_t)(ok[j] ? w[j] : 0.f);
     // dgrad fragments straight from the registers
     if (jb.dg_mode != 0 && rowok) {
       int kp, np;                                        // K' of the first of the 8 values, N'
@@ -393,8 +393,8 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   const int grid = njobs < cap ? njobs : cap;
   const int hier = grid > 256 ? 1 : 0;
   const UpdJob* J = reinterpret_cast<const UpdJob*>(jobs);
-  __bf16* P = reinterpret_cast<__bf16*>(packed);
-  __bf16* TP = reinterpret_cast<__bf16*>(tgt_packed);
+  act_t* P = reinterpret_cast<act_t*>(packed);
+  act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
   const int tf = tfreq < 1 ? 1 : tfreq;
 #define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(256), 0, st, w, g, s0, s1, beta_pow, step, \
                                   ticket, h, J, njobs, P, tgt, TP, tf, hier)

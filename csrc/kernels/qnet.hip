@@ -23,12 +23,12 @@
 
 namespace dqn {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+typedef __attribute__((ext_vector_type(8))) act_t bfx8;
 
 DQN_DEV bfx8 zero8() {
   bfx8 z;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  for (int j = 0; j < 8; ++j) z[j] = (act_t)0.f;
   return z;
 }
 
@@ -36,21 +36,21 @@ DQN_DEV bfx8 u8x8_to_bf(uint32_t lo, uint32_t hi) {
   bfx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    r[j] = (__bf16)(float)((lo >> (8 * j)) & 0xffu);
-    r[4 + j] = (__bf16)(float)((hi >> (8 * j)) & 0xffu);
+    r[j] = (act_t)(float)((lo >> (8 * j)) & 0xffu);
+    r[4 + j] = (act_t)(float)((hi >> (8 * j)) & 0xffu);
   }
   return r;
 }
 
 DQN_DEV f32x4 mfma16(const bfx8& a, const bfx8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  return DQN_MFMA16_BUILTIN(a, b, c, 0, 0, 0);
 }
 
 // ============================================================== weight packing
 // dst2 (optional): the target network's packed copy, written too when step % freq == 0
 // (the fused hard target sync: online was just copied to the target's fp32 master).
-__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src, __bf16* __restrict__ dst,
-                                                   const PackJob* __restrict__ jobs, __bf16* __restrict__ dst2,
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src, act_t* __restrict__ dst,
+                                                   const PackJob* __restrict__ jobs, act_t* __restrict__ dst2,
                                                    const int64_t* __restrict__ step, int freq) {
   const PackJob jb = jobs[blockIdx.y];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src
         x = src[jb.src_off + (int64_t)n * jb.p0 + k];
       }
     }
-    v[j] = (__bf16)x;
+    v[j] = (act_t)x;
   }
   const int64_t o = jb.dst_off + ((int64_t)((jb.ks_off + ks) * jb.dst_N16 + jb.nt_off + nt) * 64 + l) * 8;
   *reinterpret_cast<bfx8*>(dst + o) = v;
@@ -166,14 +166,14 @@ struct FrameLoader {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const uint32_t v = *reinterpret_cast<const uint16_t*>(fb[c] + off);   // pixels ix, ix+1 of frame c
-        r[c] = (__bf16)(float)(v & 0xffu);
-        r[4 + c] = (__bf16)(float)(v >> 8);
+        r[c] = (act_t)(float)(v & 0xffu);
+        r[4 + c] = (act_t)(float)(v >> 8);
       }
     } else {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if (in0) r[c] = (__bf16)(float)fb[c][off];
-        if (in1) r[4 + c] = (__bf16)(float)fb[c][off + 1];
+        if (in0) r[c] = (act_t)(float)fb[c][off];
+        if (in1) r[4 + c] = (act_t)(float)fb[c][off + 1];
       }
     }
     return r;
@@ -184,7 +184,7 @@ struct FrameLoader {
 // A[m][k] = dZ[b][oy][ox][co] where iy + pad_t - kh = S*oy (else 0).
 template <int COUT, int KH, int KW, int S>
 struct DgradLoader {
-  const __bf16* base;
+  const act_t* base;
   int OH, OW, ty, tx;
   bool ok;
   DQN_DEV DgradLoader() {}
@@ -196,7 +196,7 @@ struct DgradLoader {
     OH = a.OH; OW = a.OW;
     ty = iy + a.pad_t;
     tx = ix + a.pad_l;
-    base = reinterpret_cast<const __bf16*>(a.in[inst]) + (int64_t)b * OH * OW * COUT;
+    base = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)b * OH * OW * COUT;
   }
   DQN_DEV bfx8 frag(int k0) const {
     if (!ok) return zero8();
@@ -210,14 +210,14 @@ struct DgradLoader {
 };
 
 struct DenseLoader {
-  const __bf16* row;
+  const act_t* row;
   bool ok;
   DQN_DEV DenseLoader() {}
   DQN_DEV DenseLoader(const ConvArgs& a, int inst, int m) {
     ok = m < a.M;
     // row stride: a.IW when given (a K-wide slice of wider rows, e.g. one half of the
     // dueling [value | advantage] hidden layer), else K
-    row = reinterpret_cast<const __bf16*>(a.in[inst]) + (int64_t)(ok ? m : 0) * (a.IW > 0 ? a.IW : a.K);
+    row = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)(ok ? m : 0) * (a.IW > 0 ? a.IW : a.K);
   }
   DQN_DEV bfx8 frag(int k0) const {
     if (!ok) return zero8();
@@ -316,12 +316,12 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
         const int64_t o = (int64_t)m * a.ldo + n;
         if constexpr (EPI == 0) {
           v = fmaxf(v * scale + bv, 0.f);
-          reinterpret_cast<__bf16*>(a.out[inst])[o] = (__bf16)v;
+          reinterpret_cast<act_t*>(a.out[inst])[o] = (act_t)v;
         } else if constexpr (EPI == 1) {
           reinterpret_cast<float*>(a.out[inst])[o] = v * scale + bv;
         } else {
-          const float mk = (float)reinterpret_cast<const __bf16*>(a.mask[inst])[o];
-          reinterpret_cast<__bf16*>(a.out[inst])[o] = (__bf16)(mk > 0.f ? v : 0.f);
+          const float mk = (float)reinterpret_cast<const act_t*>(a.mask[inst])[o];
+          reinterpret_cast<act_t*>(a.out[inst])[o] = (act_t)(mk > 0.f ? v : 0.f);
         }
       }
     }
@@ -339,28 +339,28 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 template <int MC, int KB, int NB>
 struct WgradTile {
   static constexpr int LR = MC + 8;
-  static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(__bf16);
+  static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(act_t);
 };
 
 // Body shared by the per-layer launch and the grouped launch (one block = one
 // (M-chunk, K-range, N-range) tile; LDS passed in so a grouped kernel can carve
 // every member's staging from one buffer).
 template <class LD, int MC, int KB, int NB>
-DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, __bf16* lds) {
+DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, act_t* lds) {
   constexpr int LR = MC + 8;
   constexpr int TPR = 256 / MC;                  // threads per staged row
   constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
   constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
   static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0, "tiling");
-  __bf16* At = lds;
-  __bf16* Zt = lds + KB * LR;
+  act_t* At = lds;
+  act_t* Zt = lds + KB * LR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
   {
     const int r = threadIdx.x % MC, p = threadIdx.x / MC;
     const int m = m_lo + r;
     const bool mok = m < a.M;
-    const __bf16* dz = reinterpret_cast<const __bf16*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
+    const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
     LD ld(a, 0, m);
     bfx8 va[GA], vz[GZ];
 #pragma unroll
@@ -391,12 +391,13 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
   if (g.db != nullptr && by == 0) {
     for (int n = threadIdx.x; n < NB; n += 256) {
       float s = 0.f;
-      const __bf16* zr = Zt + n * LR;
+      const act_t* zr = Zt + n * LR;
 #pragma unroll 8
       for (int r = 0; r < MC; ++r) s += (float)zr[r];
       const int nn = n_lo + n;
       if (nn < g.N) {
         float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        s *= kInvLossScale;
         if (atomic) atomicAdd(pdb, s); else *pdb = s;
       }
     }
@@ -421,7 +422,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
       if (k < a.K && n < g.N) {
         float* p = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
                                 : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
-        const float v = acc[r] * g.scale;
+        const float v = acc[r] * (g.scale * kInvLossScale);
         if (atomic) atomicAdd(p, v); else *p = v;
       }
     }
@@ -430,7 +431,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
 
 template <class LD, int MC, int KB, int NB>
 __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[WgradTile<MC, KB, NB>::lds_bytes / sizeof(__bf16)];
+  __shared__ __attribute__((aligned(16))) act_t lds[WgradTile<MC, KB, NB>::lds_bytes / sizeof(act_t)];
   wgrad_block<LD, MC, KB, NB>(a, g, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
@@ -470,14 +471,14 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
     const int inst = im / mtiles, mt = im - inst * mtiles;
     const int b_row = mt * 16 + (lane & 15);
     const bool rok = b_row < B;
-    const __bf16* hrow = reinterpret_cast<const __bf16*>(hptr(inst)) + (int64_t)(rok ? b_row : 0) * HH;
-    const __bf16* ha = a.dueling ? hrow + HID : hrow;
+    const act_t* hrow = reinterpret_cast<const act_t*>(hptr(inst)) + (int64_t)(rok ? b_row : 0) * HH;
+    const act_t* ha = a.dueling ? hrow + HID : hrow;
     const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
     const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
     const int kg = 8 * (lane >> 4);
     {
       const bool val = nt == a.N16;
-      const __bf16* src = val ? hrow : ha;
+      const act_t* src = val ? hrow : ha;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       for (int ks = 0; ks < K32; ks += 8) {          // 8 k-steps of loads in flight per batch
         bfx8 af[8], bf[8];
@@ -567,10 +568,10 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
   // blocks (phases 1-2 above are recomputed by every block: cheap MFMA work);
   // k fastest across threads -> coalesced H reads
   const int gt = blk * nth + tid, gn = nblk * nth;
-  const __bf16* hb0 = reinterpret_cast<const __bf16*>(a.h[0]);
-  const __bf16* ha0 = a.dueling ? hb0 + HID : hb0;
+  const act_t* hb0 = reinterpret_cast<const act_t*>(a.h[0]);
+  const act_t* ha0 = a.dueling ? hb0 + HID : hb0;
   const float* W0 = a.w[0];
-  __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
+  act_t* dh = reinterpret_cast<act_t*>(a.dh);
   for (int t = gt; t < HID * A; t += gn) {              // dW[k][i] = sum_b Ha[b][k] dA[b][i]
     const int i = t / HID, k = t - i * HID;
     float s = 0.f;
@@ -605,7 +606,7 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
       for (int i = 0; i < A; ++i) s += dq[b * A + i] * W0[(int64_t)kk * A + i];
     }
     const float hval = (float)hb0[t];
-    dh[t] = (__bf16)(hval > 0.f ? s : 0.f);
+    dh[t] = (act_t)(hval > 0.f ? s * kLossScale : 0.f);   // scaled: see dqn_act.h
   }
 }
 
@@ -629,8 +630,8 @@ using namespace dqn;
 void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs, int max_threads, void* dst2,
                  const int64_t* step, int freq, hipStream_t st) {
   dim3 grid((max_threads + 255) / 256, njobs);
-  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, src, reinterpret_cast<__bf16*>(dst), jobs_dev,
-                     reinterpret_cast<__bf16*>(dst2), step, freq < 1 ? 1 : freq);
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, src, reinterpret_cast<act_t*>(dst), jobs_dev,
+                     reinterpret_cast<act_t*>(dst2), step, freq < 1 ? 1 : freq);
 }
 
 #define IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, U)                                                \
@@ -641,8 +642,8 @@ void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs
 #define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI) IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, 4)
 
 using NatC1 = ConvLoader<uint8_t, 4, 8, 8, 4>;
-using NatC2 = ConvLoader<__bf16, 32, 4, 4, 2>;
-using NatC3 = ConvLoader<__bf16, 64, 3, 3, 1>;
+using NatC2 = ConvLoader<act_t, 32, 4, 4, 2>;
+using NatC3 = ConvLoader<act_t, 64, 3, 3, 1>;
 using NatD3 = DgradLoader<64, 3, 3, 1>;
 using NatD2 = DgradLoader<64, 4, 4, 2>;
 using NatF1 = FrameLoader<8, 8, 4>;
@@ -690,13 +691,13 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
 // longest member first; each block runs its member's wgrad_block.
 namespace dqn {
 template <class LD, int MC, int KB, int NB>
-DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, int gy, __bf16* lds) {
+DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, int gy, act_t* lds) {
   const int bx = b % gx, r = b / gx, by = r % gy, bz = r / gy;
   wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
 }
 
 __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
-  extern __shared__ __attribute__((aligned(16))) __bf16 glds[];
+  extern __shared__ __attribute__((aligned(16))) act_t glds[];
   int b = blockIdx.x, i = 0;
   while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
   switch (G.kind[i]) {
@@ -718,7 +719,7 @@ static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
     case L_DENSE_FWD_RELU: MC = 32; KB = 64; NB = 128; break;
     default: return false;
   }
-  lds = (size_t)(KB + NB) * (MC + 8) * sizeof(__bf16);
+  lds = (size_t)(KB + NB) * (MC + 8) * sizeof(act_t);
   return true;
 }
 

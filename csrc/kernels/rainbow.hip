@@ -24,12 +24,12 @@
 
 namespace dqn {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bfx8;
+typedef __attribute__((ext_vector_type(8))) act_t bfx8;
 
 DQN_DEV bfx8 rz8() {
   bfx8 z;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  for (int j = 0; j < 8; ++j) z[j] = (act_t)0.f;
   return z;
 }
 
@@ -50,8 +50,8 @@ DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int l
     const int nt = val ? t2 - N16 : t2;
     const int b_row = mt * 16 + (lane & 15);
     const bool rok = b_row < B;
-    const __bf16* hrow = reinterpret_cast<const __bf16*>(a.h[inst]) + (int64_t)(rok ? b_row : 0) * HH;
-    const __bf16* src = (a.dueling && !val) ? hrow + HID : hrow;  // [value | advantage] halves of h
+    const act_t* hrow = reinterpret_cast<const act_t*>(a.h[inst]) + (int64_t)(rok ? b_row : 0) * HH;
+    const act_t* src = (a.dueling && !val) ? hrow + HID : hrow;  // [value | advantage] halves of h
     const bfx8* W = val ? pv : pw;
     const int n16 = val ? N16v : N16;
     const int col0 = nt * 16 + (lane & 15);
@@ -66,7 +66,7 @@ DQN_DEV void c51_logits(const HeadArgs& a, int inst, float* lg, float* vl, int l
         bf[u] = kok ? W[((ks + u) * n16 + nt) * 64 + lane] : rz8();
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bf[u], acc, 0, 0, 0);
+      for (int u = 0; u < 8; ++u) acc = DQN_MFMA16_BUILTIN(af[u], bf[u], acc, 0, 0, 0);
     }
     const int col = nt * 16 + (lane & 15);
     const float bias = bias_pre;
@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   __syncthreads();
   const int gw = blockIdx.x * nwave + wave, GW = gridDim.x * nwave;
   const int kg = 8 * (lane >> 4), l16 = lane & 15;
-  const __bf16* h0 = reinterpret_cast<const __bf16*>(a.h[0]);
+  const act_t* h0 = reinterpret_cast<const act_t*>(a.h[0]);
   const int KB = (B + 31) / 32;                 // k-steps over the batch
   // (a) dW[k][j] = sum_b h[b][k] dOut[b][j]  (+ dWv with g): M = HID rows, N = outputs
   {
@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
       const int mt = task % MT, t2 = task / MT;
       const bool val = t2 >= NT;
       const int nt = val ? t2 - NT : t2, ncol = val ? NA : NO;
-      const __bf16* hsrc = (a.dueling && !val) ? h0 + HID : h0;   // advantage half / value half
+      const act_t* hsrc = (a.dueling && !val) ? h0 + HID : h0;   // advantage half / value half
       const float* bsrc = val ? lp : dout;
       const int k = mt * 16 + l16, j = nt * 16 + l16;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -282,22 +282,22 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int b = kb * 32 + kg + u;
-          af[u] = b < B ? hsrc[(int64_t)b * HH + k] : (__bf16)0.f;
-          bf[u] = (__bf16)(b < B && j < ncol ? bsrc[b * ncol + j] : 0.f);
+          af[u] = b < B ? hsrc[(int64_t)b * HH + k] : (act_t)0.f;
+          bf[u] = (act_t)(b < B && j < ncol ? bsrc[b * ncol + j] * kLossScale : 0.f);
         }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
+        acc = DQN_MFMA16_BUILTIN(af, bf, acc, 0, 0, 0);
       }
       if (j < ncol) {
         float* dst = val ? a.dwv : a.dw;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(int64_t)(mt * 16 + 4 * (lane >> 4) + r) * ncol + j] = acc[r];
+        for (int r = 0; r < 4; ++r) dst[(int64_t)(mt * 16 + 4 * (lane >> 4) + r) * ncol + j] = acc[r] * kInvLossScale;
       }
     }
   }
   C51_MARK(6);
   // (b) dH[b][k] = (sum_j dOut[b][j] W[k][j]) * (h > 0); value half: sum_n g[b][n] Wv[k][n]
   {
-    __bf16* dh = reinterpret_cast<__bf16*>(a.dh);
+    act_t* dh = reinterpret_cast<act_t*>(a.dh);
     const int MT = (B + 15) / 16, NT = HH / 16;
     for (int task = gw; task < MT * NT; task += GW) {
       const int mt = task % MT, nt = task / MT;
@@ -314,17 +314,17 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int jj = ks * 32 + kg + u;
-          af[u] = (__bf16)(b < B && jj < KD ? asrc[b * KD + jj] : 0.f);
-          bf[u] = (__bf16)(jj < KD ? Wrow[jj] : 0.f);
+          af[u] = (act_t)(b < B && jj < KD ? asrc[b * KD + jj] * kLossScale : 0.f);   // dH leaves scaled
+          bf[u] = (act_t)(jj < KD ? Wrow[jj] : 0.f);
         }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
+        acc = DQN_MFMA16_BUILTIN(af, bf, acc, 0, 0, 0);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int bb = mt * 16 + 4 * (lane >> 4) + r;
         if (bb < B) {
           const int64_t o = (int64_t)bb * HH + kcol0 + l16;
-          dh[o] = (__bf16)((float)h0[o] > 0.f ? acc[r] : 0.f);
+          dh[o] = (act_t)((float)h0[o] > 0.f ? acc[r] : 0.f);
         }
       }
     }

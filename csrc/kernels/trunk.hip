@@ -34,9 +34,9 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   using namespace trunk;
   // xin: the sample as bf16 NHWC [84*84][4] (converted once); dead after conv1, so
   // act2 and the conv2/conv3 K-split partials live in the same bytes afterwards.
-  __shared__ __attribute__((aligned(16))) __bf16 xin[HW * 4];
-  __shared__ __attribute__((aligned(16))) __bf16 act1[R1 * L1];
-  __bf16* act2 = xin;
+  __shared__ __attribute__((aligned(16))) act_t xin[HW * 4];
+  __shared__ __attribute__((aligned(16))) act_t act1[R1 * L1];
+  act_t* act2 = xin;
   float* red = reinterpret_cast<float*>(xin + 6144);   // conv3 k-half partials, after act2 (R2 * L2 = 5832)
   static_assert(R2 * L2 <= 6144 && 6144 * 2 + 4 * 4 * 1024 <= HW * 8, "act2 + partials fit xin");
   const int b = blockIdx.x, inst = blockIdx.y;
@@ -128,10 +128,10 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   {
     const float scale = a.scale;
     const int kw = kg >> 2;                               // 0, 2, 4, 6: pixel pair of this lane
-    __bf16* x1 = a.x1[inst] != nullptr ? a.x1[inst] + (int64_t)b * R1 * N1 : nullptr;
+    act_t* x1 = a.x1[inst] != nullptr ? a.x1[inst] + (int64_t)b * R1 * N1 : nullptr;
     auto load1 = [&](bfx8* f, int mt) {
       const int p = mt * 16 + row, oy = p / O1, ox = p - oy * O1;
-      const __bf16* base = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
+      const act_t* base = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
 #pragma unroll
       for (int ks = 0; ks < K1 / 32; ++ks) f[ks] = *reinterpret_cast<const bfx8*>(base + ks * IW * 4);
     };
@@ -167,12 +167,12 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   // ---------------------------------------------------------------- conv2 -> act2 (+x2)
   {
     constexpr int KS = K2 / 32;                           // 16 k-steps
-    __bf16* x2 = a.x2[inst] != nullptr ? a.x2[inst] + (int64_t)b * R2 * N2 : nullptr;
+    act_t* x2 = a.x2[inst] != nullptr ? a.x2[inst] + (int64_t)b * R2 * N2 : nullptr;
     auto load2 = [&](bfx8* f, int mt) {
       const int p = mt * 16 + row;
       const bool ok = p < R2;
       const int oy = ok ? p / O2 : 0, ox = ok ? p - oy * O2 : 0;
-      const __bf16* base = act1 + ((oy * 2) * O1 + ox * 2) * L1 + kg;
+      const act_t* base = act1 + ((oy * 2) * O1 + ox * 2) * L1 + kg;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {                   // k = (kh*4 + kw)*32 + ci, tap = ks
         const int kh = ks >> 2, kw = ks & 3;
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       const int p = mt * 16 + row;
       const bool ok = p < R3;
       const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
-      const __bf16* base = act2 + (oy * O2 + ox) * L2 + kg;
+      const act_t* base = act2 + (oy * O2 + ox) * L2 + kg;
 #pragma unroll
       for (int j = 0; j < KJ; ++j) {                      // k = (kh*3 + kw)*64 + ci
         const int ks = hi * KJ + j, tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     __syncthreads();
     TRUNK_MARK(9);
     if (hi == 0) {
-      __bf16* x3 = a.x3[inst] + (int64_t)b * R3 * N3;
+      act_t* x3 = a.x3[inst] + (int64_t)b * R3 * N3;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const f32x4 v = unpark(red, nq * MT + mt, lane, acc[mt]);

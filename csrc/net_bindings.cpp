@@ -157,7 +157,7 @@ void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst
     a.w3[i] = P<const void*>(ptrs[4 * I + i]);
     a.b1[i] = P<const float*>(ptrs[5 * I + i]); a.b2[i] = P<const float*>(ptrs[6 * I + i]);
     a.b3[i] = P<const float*>(ptrs[7 * I + i]);
-    a.x3[i] = P<__bf16*>(ptrs[8 * I + i]);
+    a.x3[i] = P<act_t*>(ptrs[8 * I + i]);
     a.M[i] = i < (int)M.size() ? (int)M[i] : 0;
     TORCH_CHECK(a.M[i] >= 0 && a.M[i] <= B, "cnn_fwd: per-instance sample count");
     if (i < ninst) {
@@ -165,8 +165,8 @@ void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst
       TORCH_CHECK(a.w1[i] && a.w2[i] && a.w3[i] && a.b1[i] && a.b2[i] && a.b3[i] && a.x3[i], "cnn_fwd weights/out");
     }
   }
-  a.a1 = P<__bf16*>(ptrs[9 * I + 0]); a.p1 = P<__bf16*>(ptrs[9 * I + 1]); a.a2 = P<__bf16*>(ptrs[9 * I + 2]);
-  a.p2 = P<__bf16*>(ptrs[9 * I + 3]); a.a3 = P<__bf16*>(ptrs[9 * I + 4]);
+  a.a1 = P<act_t*>(ptrs[9 * I + 0]); a.p1 = P<act_t*>(ptrs[9 * I + 1]); a.a2 = P<act_t*>(ptrs[9 * I + 2]);
+  a.p2 = P<act_t*>(ptrs[9 * I + 3]); a.a3 = P<act_t*>(ptrs[9 * I + 4]);
   TORCH_CHECK(a.a1 == nullptr || (a.p1 && a.a2 && a.p2 && a.a3), "cnn_fwd: keep all activations or none");
   a.scale = (float)scale;
   launch_cnn_fwd(a, (int)B, (int)ninst, cur_stream());
@@ -177,9 +177,9 @@ void cnn_bwd(std::vector<int64_t> ptrs, int64_t B) {
   TORCH_CHECK(ptrs.size() == 9 && B >= 1, "cnn_bwd args");
   for (auto p : ptrs) TORCH_CHECK(p != 0, "cnn_bwd: null pointer");
   dqn::CnnBwdArgs a{};
-  a.dp3 = P<const __bf16*>(ptrs[0]); a.a1 = P<const __bf16*>(ptrs[1]); a.a2 = P<const __bf16*>(ptrs[2]);
-  a.a3 = P<const __bf16*>(ptrs[3]); a.w3d = P<const void*>(ptrs[4]); a.w2d = P<const void*>(ptrs[5]);
-  a.dz1 = P<__bf16*>(ptrs[6]); a.dz2 = P<__bf16*>(ptrs[7]); a.dz3 = P<__bf16*>(ptrs[8]);
+  a.dp3 = P<const act_t*>(ptrs[0]); a.a1 = P<const act_t*>(ptrs[1]); a.a2 = P<const act_t*>(ptrs[2]);
+  a.a3 = P<const act_t*>(ptrs[3]); a.w3d = P<const void*>(ptrs[4]); a.w2d = P<const void*>(ptrs[5]);
+  a.dz1 = P<act_t*>(ptrs[6]); a.dz2 = P<act_t*>(ptrs[7]); a.dz3 = P<act_t*>(ptrs[8]);
   launch_cnn_bwd(a, (int)B, cur_stream());
 }
 
@@ -239,7 +239,7 @@ void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, 
     a.w3[i] = P<const void*>(ptrs[4 * I + i]);
     a.b1[i] = P<const float*>(ptrs[5 * I + i]); a.b2[i] = P<const float*>(ptrs[6 * I + i]);
     a.b3[i] = P<const float*>(ptrs[7 * I + i]);
-    a.x1[i] = P<__bf16*>(ptrs[8 * I + i]); a.x2[i] = P<__bf16*>(ptrs[9 * I + i]); a.x3[i] = P<__bf16*>(ptrs[10 * I + i]);
+    a.x1[i] = P<act_t*>(ptrs[8 * I + i]); a.x2[i] = P<act_t*>(ptrs[9 * I + i]); a.x3[i] = P<act_t*>(ptrs[10 * I + i]);
     a.M[i] = i < (int)M.size() ? (int)M[i] : 0;
     TORCH_CHECK(a.M[i] >= 0 && a.M[i] <= B, "trunk: per-instance sample count");
     if (i < ninst) {

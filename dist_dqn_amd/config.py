@@ -105,7 +105,9 @@ def build_parser() -> argparse.ArgumentParser:
     a('--device', default='auto', choices=['auto', 'cpu', 'cuda'])
     a('--backend', default='auto', choices=['auto', 'hip', 'torch'],
       help='Learner executor: hand-written HIP kernels or the torch oracle')
-    a('--dtype', default='fp32', choices=['fp32', 'bf16'], help='Compute dtype')
+    a('--dtype', default='fp32', choices=['fp32', 'bf16', 'fp16'],
+      help='Compute dtype of the MFMA network kernels (fp32 master weights always; the HIP executor '
+           'computes in bf16 unless fp16 is asked for)')
     a('--input_scale', default=1.0, type=float,
       help='Multiplier on raw uint8 pixels (reference: 1.0, i.e. no /255)')
     a('--loss', default='mse', choices=['mse', 'huber'])

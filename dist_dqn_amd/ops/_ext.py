@@ -9,24 +9,28 @@ from __future__ import annotations
 import importlib
 import os
 
-_ext = None
-_err = None
+_mods = {}
+_errs = {}
 
 
-def load(required: bool = False):
-    global _ext, _err
-    if _ext is None and _err is None:
+def load(required: bool = False, variant: str = ''):
+    """The native module: '' -> _C (bf16 network kernels), 'f16' -> _C_f16 (fp16 network
+    kernels, csrc/include/dqn_act.h). DQN_DEBUG_EXT=1 swaps in the bounds-checked debug
+    build (_C_debug, bf16) for the default variant."""
+    name = '_C_f16' if variant == 'f16' else '_C'
+    if name == '_C' and os.environ.get('DQN_DEBUG_EXT', '0') == '1':
+        name = '_C_debug'
+    if name not in _mods and name not in _errs:
         try:
-            # DQN_DEBUG_EXT=1: the bounds-checked debug build (DQN_DEBUG=1 python setup.py build_ext)
-            name = '_C_debug' if os.environ.get('DQN_DEBUG_EXT', '0') == '1' else '_C'
-            _ext = importlib.import_module('dist_dqn_amd.' + name)
+            _mods[name] = importlib.import_module('dist_dqn_amd.' + name)
         except Exception as e:  # pragma: no cover - depends on build
-            _err = e
-    if _ext is None and required:
+            _errs[name] = e
+    mod = _mods.get(name)
+    if mod is None and required:
         raise RuntimeError(
-            'dist_dqn_amd native extension is not built/importable (%r). Run '
-            '`python setup.py build_ext --inplace` (PYTORCH_ROCM_ARCH=gfx950).' % (_err,))
-    return _ext
+            'dist_dqn_amd native extension %s is not built/importable (%r). Run '
+            '`python setup.py build_ext --inplace` (PYTORCH_ROCM_ARCH=gfx950).' % (name, _errs.get(name)))
+    return mod
 
 
 def available() -> bool:

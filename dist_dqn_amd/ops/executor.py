@@ -68,7 +68,12 @@ class HipExecutor:
     def __init__(self, arch, layout, dtype: str = 'bf16', input_scale: float = 1.0, loss: str = 'mse',
                  huber_delta: float = 1.0, double_dqn: bool = False):
         assert supports(arch), 'HIP executor: unsupported architecture'
-        self.ext = _ext.load(required=True)
+        # fp16 (--dtype=fp16): the same kernels built with -DDQN_F16 (fp16 MFMA, static loss
+        # scale inside the kernels); everything else (bf16 default, fp32 master state) is shared
+        self.fp16 = dtype == 'fp16'
+        self.compute_dtype = 'fp16' if self.fp16 else 'bf16'
+        self.act_dtype = torch.float16 if self.fp16 else torch.bfloat16
+        self.ext = _ext.load(required=True, variant='f16' if self.fp16 else '')
         self.arch, self.layout = arch, layout
         self.input_scale = float(input_scale)
         self.huber = loss == 'huber'
@@ -272,7 +277,7 @@ class HipExecutor:
     def _packed_for(self, key: int, like: torch.Tensor) -> torch.Tensor:
         p = self._packed.get(key)
         if p is None:
-            p = torch.zeros(self.packed_elems, dtype=torch.bfloat16, device=like.device)
+            p = torch.zeros(self.packed_elems, dtype=self.act_dtype, device=like.device)
             self._packed[key] = p
         return p
 
@@ -289,7 +294,7 @@ class HipExecutor:
         key = flat.data_ptr()
         p = self._packed.get(key)
         if p is None:
-            p = torch.zeros(self.packed_elems, dtype=torch.bfloat16, device=flat.device)
+            p = torch.zeros(self.packed_elems, dtype=self.act_dtype, device=flat.device)
             self._packed[key] = p
             self.repack(flat)
         return p
@@ -350,7 +355,7 @@ class HipExecutor:
         ws = self._ws.get(key)
         if ws is not None:
             return ws
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=self.act_dtype, device=dev)
         c1, c2, c3 = self.arch.convs
         h1, w1 = c1.out_hw
         h2, w2 = c2.out_hw
@@ -722,7 +727,7 @@ class HipCnnExecutor(HipExecutor):
         ws = self._ws.get(key)
         if ws is not None:
             return ws
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=self.act_dtype, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         ws = {
             'x3': torch.zeros(4, B * self.FLAT, **bf),

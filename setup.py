@@ -1,4 +1,4 @@
-"""Build the in-tree native extension ``dist_dqn_amd/_C<EXT_SUFFIX>`` for gfx950.
+"""Build the in-tree native extensions for gfx950.
 
     python setup.py build_ext --inplace        (or: python setup.py)
 
@@ -7,9 +7,13 @@ A direct hipcc build (no hipify pass, no CUDA compatibility layer):
   * csrc/host/*.cpp      -> g++ (C++ host runtime: preprocessing, SPSC rings, CRC32C)
   * csrc/*bindings.cpp   -> hipcc host compile with the torch headers
   * link                 -> hipcc -shared with libtorch / libamdhip64
-  * csrc/host/*.cpp also -> dist_dqn_amd/libdqn_host.so (no torch/HIP: loaded by
-                            CPU actor processes through ctypes)
-Objects go to build/ and are rebuilt when the source or any csrc header is newer.
+Variants (same sources, one module each):
+  * dist_dqn_amd/_C*.so       bf16 MFMA network kernels (default executor)
+  * dist_dqn_amd/_C_f16*.so   -DDQN_F16: fp16 MFMA network kernels (--dtype=fp16; csrc/include/dqn_act.h)
+  * dist_dqn_amd/_C_debug*.so only with DQN_DEBUG=1: -O1 -g, device DQN_ASSERTs (DQN_DEBUG_EXT=1 selects it)
+  * dist_dqn_amd/libdqn_host.so  csrc/host/*.cpp without torch/HIP (CPU actor processes, ctypes)
+Objects go to build/<variant>/ and are rebuilt when the source, any csrc header or the
+compile command changes.
 """
 import concurrent.futures as cf
 import glob
@@ -21,16 +25,17 @@ import sysconfig
 ROOT = os.path.dirname(os.path.abspath(__file__))
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 HIPCC = os.path.join(os.environ.get('ROCM_PATH', '/opt/rocm'), 'bin', 'hipcc')
-# DQN_DEBUG=1: bounds-checked debug variant (-O1 -g, device DQN_ASSERTs live) built next to
-# the release module as dist_dqn_amd/_C_debug*.so; selected at import by DQN_DEBUG_EXT=1
-DEBUG = os.environ.get('DQN_DEBUG', '0') == '1'
-MOD = '_C_debug' if DEBUG else '_C'
-BUILD = os.path.join(ROOT, 'build', 'obj_debug' if DEBUG else 'obj')
-OUT = os.path.join(ROOT, 'dist_dqn_amd', MOD + sysconfig.get_config_var('EXT_SUFFIX'))
+SUFFIX = sysconfig.get_config_var('EXT_SUFFIX')
 HOST_OUT = os.path.join(ROOT, 'dist_dqn_amd', 'libdqn_host.so')   # torch-free host runtime (ctypes)
+# (module name, object dir, extra kernel flags)
+VARIANTS = {
+    'release': ('_C', 'obj', ['-O3']),
+    'f16': ('_C_f16', 'obj_f16', ['-O3', '-DDQN_F16=1']),
+    'debug': ('_C_debug', 'obj_debug', ['-O1', '-g', '-DDQN_DEBUG=1']),
+}
 
 
-def _torch_flags():
+def _torch_flags(mod):
     import torch
     from torch.utils import cpp_extension as ce
     inc = ce.include_paths(device_type='cuda') if 'device_type' in ce.include_paths.__code__.co_varnames \
@@ -40,7 +45,7 @@ def _torch_flags():
         else ce.library_paths(cuda=True)
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     defs = ['-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1', '-DTORCH_API_INCLUDE_EXTENSION_H',
-            '-DTORCH_EXTENSION_NAME=%s' % MOD, '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi]
+            '-DTORCH_EXTENSION_NAME=%s' % mod, '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi]
     return inc, libdirs, defs
 
 
@@ -59,36 +64,56 @@ def _newer(src, obj, headers, cmd=None):
     return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
 
 
-def build(verbose=False, jobs=None):
-    inc, libdirs, defs = _torch_flags()
-    os.makedirs(BUILD, exist_ok=True)
+def _plan(variant):
+    mod, sub, kflags = VARIANTS[variant]
+    inc, libdirs, defs = _torch_flags(mod)
+    build = os.path.join(ROOT, 'build', sub)
+    os.makedirs(build, exist_ok=True)
     headers = glob.glob(os.path.join(ROOT, 'csrc', '**', '*.h'), recursive=True)
     kern = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'kernels', '*.hip')))
-    host = sorted(glob.glob(os.path.join(ROOT, 'csrc', 'host', '*.cpp')))
     binds = sorted(glob.glob(os.path.join(ROOT, 'csrc', '*.cpp')))
-    cmds = []
-    objs = []
+    cmds, objs = [], []
+    vdefs = [f for f in kflags if f.startswith('-D')]
     for src in kern:
-        obj = os.path.join(BUILD, os.path.basename(src) + '.o')
+        obj = os.path.join(build, os.path.basename(src) + '.o')
         objs.append(obj)
-        cmd = [HIPCC, '-c', src, '-o', obj, '-O1' if DEBUG else '-O3', '-std=c++17', '-fPIC',
-               '--offload-arch=' + ARCH, '-ffp-contract=fast-honor-pragmas', '-I' + os.path.join(ROOT, 'csrc'),
-               '-D__HIP_PLATFORM_AMD__=1'] + (['-g', '-DDQN_DEBUG=1'] if DEBUG else [])
+        cmd = [HIPCC, '-c', src, '-o', obj] + kflags + ['-std=c++17', '-fPIC', '--offload-arch=' + ARCH,
+                                                       '-ffp-contract=fast-honor-pragmas',
+                                                       '-I' + os.path.join(ROOT, 'csrc'), '-D__HIP_PLATFORM_AMD__=1']
         if _newer(src, obj, headers, cmd):
             cmds.append(cmd)
-    for src in host:
-        obj = os.path.join(BUILD, 'host_' + os.path.basename(src) + '.o')
+    for src in binds:
+        obj = os.path.join(build, 'bind_' + os.path.basename(src) + '.o')
+        objs.append(obj)
+        cmd = [HIPCC, '-c', src, '-o', obj, '-O2', '-std=c++17', '-fPIC', '-I' + os.path.join(ROOT, 'csrc')] + \
+              ['-I' + i for i in inc] + defs + vdefs
+        if _newer(src, obj, headers, cmd):
+            cmds.append(cmd)
+    out = os.path.join(ROOT, 'dist_dqn_amd', mod + SUFFIX)
+    # -Bsymbolic: each variant's launchers bind to its own kernels when several are loaded
+    link = [HIPCC, '-shared', '-fPIC', '-Wl,-Bsymbolic', '-o', out] + objs + ['-L' + d for d in libdirs] + \
+           ['-Wl,-rpath,' + d for d in libdirs] + \
+           ['-lc10', '-ltorch', '-ltorch_cpu', '-ltorch_python', '-lamdhip64', '-lc10_hip', '-ltorch_hip']
+    return cmds, link, out
+
+
+def _plan_host():
+    build = os.path.join(ROOT, 'build', 'host')
+    os.makedirs(build, exist_ok=True)
+    headers = glob.glob(os.path.join(ROOT, 'csrc', '**', '*.h'), recursive=True)
+    cmds, objs = [], []
+    for src in sorted(glob.glob(os.path.join(ROOT, 'csrc', 'host', '*.cpp'))):
+        obj = os.path.join(build, os.path.basename(src) + '.o')
         objs.append(obj)
         cmd = ['g++', '-c', src, '-o', obj, '-O3', '-std=c++17', '-fPIC', '-Wall']
         if _newer(src, obj, headers, cmd):
             cmds.append(cmd)
-    for src in binds:
-        obj = os.path.join(BUILD, 'bind_' + os.path.basename(src) + '.o')
-        objs.append(obj)
-        cmd = [HIPCC, '-c', src, '-o', obj, '-O2', '-std=c++17', '-fPIC', '-I' + os.path.join(ROOT, 'csrc')] + \
-              ['-I' + i for i in inc] + defs
-        if _newer(src, obj, headers, cmd):
-            cmds.append(cmd)
+    return cmds, ['g++', '-shared', '-fPIC', '-o', HOST_OUT] + objs + ['-lpthread'], objs
+
+
+def build(verbose=False, jobs=None, variants=None):
+    if variants is None:
+        variants = ['debug'] if os.environ.get('DQN_DEBUG', '0') == '1' else ['release', 'f16']
 
     def run(cmd):
         if verbose:
@@ -98,21 +123,26 @@ def build(verbose=False, jobs=None):
             raise RuntimeError('compile failed: %s\n%s%s' % (' '.join(cmd), r.stdout, r.stderr))
         return cmd[2] if len(cmd) > 2 else ''
 
+    hcmds, hlink, host_objs = _plan_host()
+    plans = [_plan(v) for v in variants]
+    # the host runtime's objects are linked into every extension module too
+    plans = [(c, l[:l.index('-o') + 2] + host_objs + l[l.index('-o') + 2:], o) for c, l, o in plans]
+    allc = hcmds + [c for p in plans for c in p[0]]
     jobs = jobs or int(os.environ.get('MAX_JOBS', min(16, os.cpu_count() or 4)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        for f in cf.as_completed([ex.submit(run, c) for c in cmds]):
+        for f in cf.as_completed([ex.submit(run, c) for c in allc]):
             f.result()
-    host_objs = [o for o in objs if os.path.basename(o).startswith('host_')]
-    if not DEBUG and (cmds or not os.path.exists(HOST_OUT)):
-        run(['g++', '-shared', '-fPIC', '-o', HOST_OUT] + host_objs + ['-lpthread'])
-    if cmds or not os.path.exists(OUT):
-        link = [HIPCC, '-shared', '-fPIC', '-o', OUT] + objs + ['-L' + d for d in libdirs] + \
-               ['-Wl,-rpath,' + d for d in libdirs] + \
-               ['-lc10', '-ltorch', '-ltorch_cpu', '-ltorch_python', '-lamdhip64', '-lc10_hip', '-ltorch_hip']
-        run(link)
-    return OUT
+    if hcmds or not os.path.exists(HOST_OUT):
+        run(hlink)
+    outs = []
+    for cmds, link, out in plans:
+        if cmds or hcmds or not os.path.exists(out):
+            run(link)
+        outs.append(out)
+    return outs
 
 
 if __name__ == '__main__':
     args = [a for a in sys.argv[1:] if a not in ('build_ext', '--inplace')]
-    print(build(verbose='-v' in args))
+    for o in build(verbose='-v' in args):
+        print(o)

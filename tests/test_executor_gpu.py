@@ -17,6 +17,9 @@ def _setup(extra='', B=32, seed=0):
     cfg = preset(kind, 'Pong-v0', '--seed=%d --backend=hip %s' % (seed, extra))
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     assert net.executor.name == 'hip'
+    assert net.executor.compute_dtype == ('fp16' if '--dtype=fp16' in extra else 'bf16')
+    if '--dtype=fp16' in extra:
+        assert net.executor.ext.__name__.endswith('_C_f16')
     g = torch.Generator(device=DEV).manual_seed(seed)
     # larger-than-init weights so every layer carries signal
     net.online.flat.normal_(0.0, 0.03, generator=g)
@@ -45,8 +48,11 @@ def _rel(a, b):
 RAINBOW = '--distributional --noisy --dueling --double_dqn'
 
 
+F16 = ' --dtype=fp16'
+
+
 @pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', '--distributional', '--noisy --dueling',
-                                   RAINBOW, 'cnn:', 'cnn:--dueling'])
+                                   RAINBOW, 'cnn:', 'cnn:--dueling', F16, RAINBOW + F16, 'cnn:' + F16])
 def test_q_values_match_oracle(extra):
     net, oracle, batch = _setup(extra)
     q = net.q_values(batch['states'])
@@ -59,7 +65,11 @@ def test_q_values_match_oracle(extra):
                                              ('--distributional', 32, False), ('--noisy', 32, False),
                                              (RAINBOW, 32, True), (RAINBOW, 13, False),
                                              ('cnn:', 32, False), ('cnn:--dueling --double_dqn --loss=huber', 32, True),
-                                             ('cnn:', 7, False), ('cnn:--double_dqn', 64, False)])
+                                             ('cnn:', 7, False), ('cnn:--double_dqn', 64, False),
+                                             # fp16 MFMA build (_C_f16, static loss scale)
+                                             (F16, 32, False), ('--dueling --double_dqn --loss=huber' + F16, 32, True),
+                                             ('--double_dqn' + F16, 64, False), (RAINBOW + F16, 32, True),
+                                             ('cnn:' + F16, 32, False)])
 def test_loss_and_grad_match_oracle(extra, B, weighted):
     net, oracle, batch = _setup(extra, B)
     if weighted:
@@ -87,7 +97,8 @@ def test_loss_and_grad_match_oracle(extra, B, weighted):
         assert cos > 0.99 and abs(ratio - 1.0) < tol, (name, cos, ratio)
 
 
-def test_learner_step_graph_equals_eager():
+@pytest.mark.parametrize('dtype', ['bf16', 'fp16'])
+def test_learner_step_graph_equals_eager(dtype):
     """HIP-graph replay of the full SGD step == the same step run eagerly."""
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.learner import Learner
@@ -95,7 +106,7 @@ def test_learner_step_graph_equals_eager():
     from dist_dqn_amd.replay import DeviceReplay
     outs = []
     for graph in (False, True):
-        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096')
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 --dtype=%s' % dtype)
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
         rep.fill_synthetic(4096, 6, seed=5)
