@@ -32,6 +32,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "learner SGD steps/sec + env frames/sec, Atari Nature-CNN DQN at 1/2/4/8 MI355X"
+VARIANTS = {
+    'dqn': '',
+    'dd': '--dueling --double_dqn --loss=huber',
+    'rainbow': '--dueling --double_dqn --distributional --noisy --prioritized_replay --optimizer=adam --lr=0.0000625',
+}
 
 
 def main():
@@ -49,6 +54,9 @@ def main():
     ap.add_argument('--update_freq', type=int, default=4)
     ap.add_argument('--graph', type=int, default=1)
     ap.add_argument('--extra', default='', help='extra config flags, e.g. "--dueling --double_dqn"')
+    ap.add_argument('--variant', default='dqn', choices=sorted(VARIANTS),
+                    help='algorithm variant (BASELINE.json configs): dqn = Nature DQN, dd = Double+Dueling+Huber, '
+                         'rainbow = C51 + noisy nets + dueling + double + PER + Adam')
     ap.add_argument('--fuse_acting', type=int, default=1,
                     help='run the device actors\' step inside the learner step\'s launches when possible')
     args = ap.parse_args()
@@ -63,7 +71,7 @@ def main():
     cfg = preset('nature' if args.network == 'nature' else 'atari', 'Pong-v0',
                  '--minibatch_size=%d --dtype=%s --backend=%s --hip_graph=%d --replay_memory_capacity=%d '
                  '--update_freq=%d --seed=0 %s' % (args.batch, args.dtype, args.backend, args.graph, args.replay,
-                                                    args.update_freq, args.extra))
+                                                    args.update_freq, VARIANTS[args.variant] + ' ' + args.extra))
     if args.network not in ('nature', 'cnn'):
         cfg = cfg.replace(network=args.network)
     ctx = init_distributed(cfg, device='cuda')
@@ -121,7 +129,8 @@ def main():
                        'hip_graph': bool(args.graph), 'actor_envs': args.actor_envs,
                        'acting': 'fused into the learner launches' if fused else 'separate launches',
                        'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
-                       'num_actions': args.actions, 'extra': args.extra, 'final_loss': loss,
+                       'num_actions': args.actions, 'variant': args.variant, 'extra': args.extra,
+                       'final_loss': loss,
                        'allreduce': learner.reducer.mode if ctx.enabled else None,
                        'allreduce_probe_us': learner.reducer.timings or None},
         }

@@ -17,8 +17,9 @@ run_bench() {   # name, args...
   tail -1 $OUT/bench_$name.log
 }
 run_bench nature --steps 400 --warmup 40
-run_bench dd --steps 400 --warmup 40 --extra="--dueling --double_dqn --loss=huber"
-run_bench rainbow --steps 300 --warmup 30 --extra="--dueling --double_dqn --distributional --noisy --prioritized_replay --optimizer=adam --lr=0.0000625"
+run_bench dd --steps 400 --warmup 40 --variant dd
+run_bench rainbow --steps 300 --warmup 30 --variant rainbow
+run_bench rainbow16 --steps 300 --warmup 30 --variant rainbow --dtype fp16
 run_bench cnn --steps 300 --warmup 30 --network cnn
 if [ "${APEX:-1}" == "1" ]; then
   timeout -k 10 200 python scripts/bench_apex.py --actors 16 --seconds 45 > $OUT/apex.log 2>&1; stop_on $? apex
