@@ -92,16 +92,23 @@ void sumtree_set(torch::Tensor sum, torch::Tensor mn, torch::Tensor maxp, torch:
 }
 
 void sumtree_sample(torch::Tensor sum, torch::Tensor mn, torch::Tensor rng, torch::Tensor size, torch::Tensor beta,
-                    torch::Tensor idx_out, torch::Tensor w_out, int64_t P, std::vector<torch::Tensor> so) {
+                    torch::Tensor idx_out, torch::Tensor w_out, int64_t P, std::vector<torch::Tensor> so,
+                    double beta0, double beta_steps) {
+  // beta: float32 [1] = the IS exponent itself, or int64 [1] = the device global_step of the
+  // annealing schedule beta = min(1, beta0 + (1 - beta0) * step / beta_steps)
   CHECK_T(sum, torch::kFloat32); CHECK_T(mn, torch::kFloat32); CHECK_T(rng, torch::kInt64);
-  CHECK_T(size, torch::kInt32); CHECK_T(beta, torch::kFloat32); CHECK_T(idx_out, torch::kInt32);
-  CHECK_T(w_out, torch::kFloat32);
+  CHECK_T(size, torch::kInt32); CHECK_T(idx_out, torch::kInt32); CHECK_T(w_out, torch::kFloat32);
+  CHECK_DEV(beta); CHECK_CONTIG(beta);
+  const bool sched = beta.scalar_type() == torch::kInt64;
+  TORCH_CHECK(sched || beta.scalar_type() == torch::kFloat32, "beta: float32 value or int64 step");
+  TORCH_CHECK(!sched || beta_steps >= 1.0, "beta schedule steps must be >= 1");
   TORCH_CHECK(idx_out.numel() <= 1024 && w_out.numel() == idx_out.numel(), "PER batch must be <= 1024");
   TORCH_CHECK(sum.numel() == 2 * P, "tree size must be 2P");
   c10::hip::HIPGuardMasqueradingAsCUDA g(sum.device());
-  launch_sumtree_sample(ptr<float>(sum), ptr<float>(mn), ptr<int64_t>(rng), ptr<int32_t>(size), ptr<float>(beta),
-                        ptr<int32_t>(idx_out), ptr<float>(w_out), (int)idx_out.numel(), (int)P,
-                        sample_out(so, idx_out.numel()), cur_stream());
+  launch_sumtree_sample(ptr<float>(sum), ptr<float>(mn), ptr<int64_t>(rng), ptr<int32_t>(size),
+                        sched ? nullptr : ptr<float>(beta), ptr<int32_t>(idx_out), ptr<float>(w_out),
+                        (int)idx_out.numel(), (int)P, sample_out(so, idx_out.numel()),
+                        sched ? ptr<int64_t>(beta) : nullptr, (float)beta0, (float)beta_steps, cur_stream());
 }
 
 void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s0, torch::Tensor s1,
@@ -136,7 +143,12 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 torch::Tensor beta_pow, torch::Tensor ticket, double lr, double reg, int64_t reg_end,
                 double grad_scale, torch::Tensor step, std::vector<double> hp, torch::Tensor jobs,
                 torch::Tensor packed, c10::optional<torch::Tensor> target, c10::optional<torch::Tensor> target_packed,
-                int64_t target_freq, int64_t max_grid) {
+                int64_t target_freq, int64_t max_grid, c10::optional<torch::Tensor> noise,
+                c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
+                c10::optional<torch::Tensor> noise_dst) {
+  // grad_noise: derive the sigma gradients from the mu gradients under that noise sample;
+  // noise_dst: the last block copies `noise` there (next sample becomes the current one)
+  // op -1: no optimizer update, only the (noisy) mix + pack of w (noise / eff given)
   CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
   CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
   CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
@@ -144,14 +156,44 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
   TORCH_CHECK(max_grid <= 256 || ticket.numel() >= 17 * 32, "optim_pack: wide grid needs the 17x32-word ticket");
   TORCH_CHECK(max_grid >= 1 && max_grid <= 65535, "optim_pack: max_grid");
+  TORCH_CHECK(op >= -1 && op <= 6, "optim_pack: op");
   float* tgt = nullptr;
   void* tgtp = nullptr;
   if (target.has_value() && target->defined()) {
     CHECK_T((*target), torch::kFloat32);
-    TORCH_CHECK(target->numel() == w.numel() && target_packed.has_value() && target_packed->defined() &&
-                target_packed->numel() == packed.numel() && target_freq >= 1, "optim_pack: target sync args");
+    TORCH_CHECK(target->numel() == w.numel() && target_freq >= 1, "optim_pack: target sync args");
     tgt = ptr<float>(*target);
-    tgtp = target_packed->data_ptr();
+    if (target_packed.has_value() && target_packed->defined()) {   // noisy nets: fp32 target only
+      TORCH_CHECK(target_packed->numel() == packed.numel(), "optim_pack: target packed size");
+      tgtp = target_packed->data_ptr();
+    }
+  }
+  const float* nz = nullptr;
+  float* ef = nullptr;
+  if (noise.has_value() && noise->defined()) {
+    CHECK_T((*noise), torch::kFloat32);
+    nz = ptr<float>(*noise);
+  }
+  if (eff.has_value() && eff->defined()) {
+    CHECK_T((*eff), torch::kFloat32);
+    TORCH_CHECK(eff->numel() == w.numel(), "optim_pack: eff size");
+    ef = ptr<float>(*eff);
+  }
+  TORCH_CHECK(op >= 0 || tgt == nullptr, "optim_pack: mix-only call with a target");
+  const float* gnz = nullptr;
+  float* ndst = nullptr;
+  int nn = 0;
+  if (grad_noise.has_value() && grad_noise->defined()) {
+    CHECK_T((*grad_noise), torch::kFloat32);
+    TORCH_CHECK(nz != nullptr && grad_noise->numel() == noise->numel(), "optim_pack: grad_noise size");
+    gnz = ptr<float>(*grad_noise);
+  }
+  if (noise_dst.has_value() && noise_dst->defined()) {
+    CHECK_T((*noise_dst), torch::kFloat32);
+    TORCH_CHECK(op >= 0 && nz != nullptr && noise_dst->numel() == noise->numel() &&
+                noise_dst->data_ptr() != noise->data_ptr(), "optim_pack: noise_dst");
+    ndst = ptr<float>(*noise_dst);
+    nn = (int)noise_dst->numel();
   }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
@@ -159,7 +201,20 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   launch_optim_pack((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1), ptr<float>(beta_pow),
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
-                    tgtp, (int)target_freq, (int)max_grid, cur_stream());
+                    tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, cur_stream());
+}
+
+void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {
+  CHECK_T(out0, torch::kFloat32); CHECK_T(rng, torch::kInt64);
+  TORCH_CHECK(rng.numel() >= 2, "noise rng state is [seed, counter]");
+  float* o1 = nullptr;
+  if (out1.has_value() && out1->defined()) {
+    CHECK_T((*out1), torch::kFloat32);
+    TORCH_CHECK(out1->numel() == out0.numel(), "noise_normal: out1 size");
+    o1 = ptr<float>(*out1);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out0.device());
+  launch_noise_normal(ptr<float>(out0), o1, (int)out0.numel(), ptr<int64_t>(rng), cur_stream());
 }
 
 void target_update(torch::Tensor dst, torch::Tensor src, double tau, torch::Tensor step, int64_t freq,
@@ -405,6 +460,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("target_freq") = 1);
   m.def("target_update", &target_update);
   m.def("optim_pack", &optim_pack);
+  m.def("noise_normal", &noise_normal);
   m.attr("UPD_JOB_INTS") = upd_job_ints();
   m.def("td_loss_scalar", &td_loss_scalar);
   m.def("td_loss_c51", &td_loss_c51);

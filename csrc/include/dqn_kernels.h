@@ -25,14 +25,17 @@ void launch_sumtree_set(float* sum, float* mn, float* maxp, const int32_t* idx, 
                         float eps, int use_max, int n, int P, hipStream_t st);
 void launch_sumtree_sample(const float* sum, const float* mn, int64_t* rng, const int32_t* size,
                            const float* beta, int32_t* idx_out, float* w_out, int B, int P, const SampleOut& so,
-                           hipStream_t st);
+                           const int64_t* sched_step, float beta0, float beta_steps, hipStream_t st);
 void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
                            int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
                            float grad_scale, int n, float* tgt, int tfreq, hipStream_t st);
 void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
+                       const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        hipStream_t st);
+// standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
+void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
                           float* dst2, const float* src2, int n2, hipStream_t st);

@@ -55,6 +55,36 @@ DQN_DEV float wave_max(float v) {
   return v;
 }
 
+// Reductions over the 16 lanes of one DPP row (lanes 16r..16r+15), result in every lane:
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror. VALU-only
+// (no LDS crossbar, unlike __shfl_xor); all 16 lanes of the row must be active.
+template <int CTRL>
+DQN_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+DQN_DEV float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+DQN_DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return v;
+}
+
+// Whole-wave sum: DPP row sums, then the 4 row totals via readlane (uniform result).
+DQN_DEV float wave_sum_dpp(float v) {
+  v = row16_sum(v);
+  const int iv = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(iv, 0)) + __int_as_float(__builtin_amdgcn_readlane(iv, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(iv, 32)) + __int_as_float(__builtin_amdgcn_readlane(iv, 48)));
+}
+
 // -------------------------------------------------------------------- bf16
 DQN_DEV uint16_t f2bf(float f) {  // round-to-nearest-even (NaN kept by the cast path)
   __hip_bfloat16 b = __float2bfloat16(f);

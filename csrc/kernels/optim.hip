@@ -120,159 +120,194 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 
 
 // ------------------------------------------------------------- update + pack
-// The optimizer step fused with the executor's weight packing: a workgroup owns
-// a 32 (k) x 64 (n) tile of a weight matrix (TF layout [K][N]), updates it in
-// registers (8 consecutive n per thread), writes fp32 weights + slots back, and
-// emits the tile's bf16 MFMA fragments straight away:
+// The optimizer step fused with the executor's weight packing: a 512-thread workgroup
+// owns a 32 (k) x 64 (n) tile of a weight matrix (TF layout [K][N]), each thread 4
+// consecutive n of one row (one float4 per operand: few VGPRs, high occupancy). It
+// updates the tile in registers, writes fp32 weights + slots back, and emits the tile's
+// bf16 MFMA fragments straight away:
 //   * forward fragments ([K/32][N/16][64][8]: 8 consecutive k per lane) through
 //     one LDS transpose of the tile;
 //   * dgrad fragments (dense transpose, or conv (tap, co) x ci) directly from the
-//     thread's registers: their 8 consecutive K' ARE 8 consecutive n of one row.
+//     thread's registers: its 4 consecutive K' ARE 4 consecutive n of one row (half
+//     of one lane's 8-value slot).
 // Elementwise items (biases, ...) carry an optional fp32 copy into the packed
 // buffer (the concatenated fc bias). Same ticket as optim_kernel; the hard target
 // sync writes the target's fp32 master and packed fragments under the predicate.
 typedef __attribute__((ext_vector_type(8))) act_t bfx8;
+typedef __attribute__((ext_vector_type(4))) act_t bfx4;
 
 constexpr int kTicketSubs = 16, kTicketStride = 32;    // hierarchical ticket: int32 words
+constexpr int kPackThreads = 512;
 
 struct UpdJob {
   int kind;                      // 0 = tile, 1 = elementwise chunk
   int src_off, K, N, k0, n0;     // tile: tensor offset / shape / origin; elem: offset, count (K)
   int fwd_off, fwd_N16, fwd_nt_off, fwd_ks_off;   // forward fragments (elem: fp32 copy offset or -1)
   int dg_mode, dg_off, dg_N16, dg_nt_off, dg_ks_off, dg_cin;   // dgrad: 0 none, 1 conv, 2 dense
+  // noisy nets (factorised Gaussian): the sigma tensor is updated in the same thread as mu
+  // and the packed / eff values are mu + sigma * f(noise[ein + k]) f(noise[eout + n])
+  // (ein < 0: f = 1, biases; elem chunks: eout already offset to the chunk start)
+  int sig_off, ein_off, eout_off;
+  int eff;                       // 1: also store the effective fp32 value at eff[src index]
 };
 
-template <int OP>
-DQN_DEV void upd8(float* w, const float* g, float* a, float* b, int k0flat, int reg_end, const OptHP& h,
-                  float lr_t, bool* ok) {
+DQN_DEV float fnz(float x) { return copysignf(sqrtf(fabsf(x)), x); }
+
+// 4 consecutive floats: one float4 when `vec` (16-byte aligned, all in range), else per-element
+DQN_DEV void load4(const float* p, bool vec, const bool* ok, float* v) {
+  if (vec) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 4; ++j) v[j] = ok[j] ? p[j] : 0.f;
+  }
+}
+DQN_DEV void store4(float* p, bool vec, const bool* ok, const float* v) {
+  if (vec) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (ok[j]) p[j] = v[j];
+  }
+}
+
+template <int OP>
+DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, int reg_end, const OptHP& h,
+                  float lr_t, const bool* ok) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
     if (!ok[j]) continue;
     update_one<OP>(w[j], opt_grad(g[j], w[j], k0flat + j < reg_end, h), a[j], b[j], h, lr_t);
   }
 }
 
 template <int OP>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kPackThreads)
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
-                  act_t* __restrict__ tgt_packed, int tfreq, int hier) {
+                  act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
+                  float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
+                  int noise_n) {
+  // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
+  // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
+  // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
+  // noise on every DP rank makes that exact for the all-reduced sum), instead of being read.
+  // noise_dst: the grid's last block copies noise[0, noise_n) there (next sample -> current).
+  constexpr bool UPD = OP >= 0;
   __shared__ __attribute__((aligned(16))) act_t tile[32 * 72];
   float lr_t = h.lr;
   if constexpr (OP == 3) {
     const float b1p = beta_pow[0], b2p = beta_pow[1];
     lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   }
-  const bool sync = tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  const bool sync = UPD && tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  const bool psync = sync && tgt_packed != nullptr;
   constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6;
+  constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
   for (int ji = blockIdx.x; ji < njobs; ji += gridDim.x) {
     const UpdJob jb = jobs[ji];
-    float w[8], g[8], a[8], b[8];
-    bool ok[8];
-    if (jb.kind == 1) {                                   // elementwise chunk of up to 2048
-      const int base = jb.src_off + t * 8;
+    const bool elem = jb.kind == 1;
+    const bool noisy = jb.sig_off >= 0;
+    bool ok[4];
+    int k, n;                      // row (tile) and column / element index within the tensor
+    bool rowok, vec;
+    int64_t e0;
+    if (elem) {                    // chunk of up to 2048 elements: 4 per thread
+      k = 0;
+      n = 4 * t;
+      rowok = true;
+      e0 = (int64_t)jb.src_off + n;
+      vec = n + 4 <= jb.K;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ok[j] = t * 8 + j < jb.K;
-        const int i = base + j;
-        w[j] = ok[j] ? W[i] : 0.f; g[j] = ok[j] ? G[i] : 0.f;
-        a[j] = (OP != 0 && ok[j]) ? S0[i] : 0.f; b[j] = (TWO && ok[j]) ? S1[i] : 0.f;
+      for (int j = 0; j < 4; ++j) ok[j] = n + j < jb.K;
+    } else {                       // tile: row r, columns c4..c4+3
+      const int r = t >> 4, c4 = (t & 15) * 4;
+      k = jb.k0 + r;
+      n = jb.n0 + c4;
+      rowok = k < jb.K;
+      e0 = (int64_t)jb.src_off + (int64_t)k * jb.N + n;
+      vec = rowok && n + 4 <= jb.N && (jb.N % 4) == 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ok[j] = rowok && n + j < jb.N;
+    }
+    const int64_t s0i = noisy ? (elem ? (int64_t)jb.sig_off + n : (int64_t)jb.sig_off + (int64_t)k * jb.N + n) : e0;
+    // every load (mu and, for noisy layers, sigma) is issued before any math
+    float w[4], g[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], e[4];
+    load4(W + e0, vec, ok, w);
+    if constexpr (UPD) load4(G + e0, vec, ok, g);
+    if constexpr (ONE) load4(S0 + e0, vec, ok, a);
+    if constexpr (TWO) load4(S1 + e0, vec, ok, b);
+    if (noisy) {
+      load4(W + s0i, vec, ok, ws);
+      if constexpr (UPD) {
+        if (gnoise == nullptr) load4(G + s0i, vec, ok, gs);
+        if constexpr (ONE) load4(S0 + s0i, vec, ok, as);
+        if constexpr (TWO) load4(S1 + s0i, vec, ok, bs);
       }
-      upd8<OP>(w, g, a, b, base, h.reg_end, h, lr_t, ok);
+    }
+    if constexpr (UPD) {
+      if (noisy && gnoise != nullptr) {                   // dL/dsigma from the mu-slot gradient
+        const float gin = (!elem && jb.ein_off >= 0 && rowok) ? fnz(gnoise[jb.ein_off + k]) : 1.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (!ok[j]) continue;
-        const int i = base + j;
-        W[i] = w[j];
-        if constexpr (OP != 0) S0[i] = a[j];
-        if constexpr (TWO) S1[i] = b[j];
-        if (sync) tgt[i] = w[j];
-        if (jb.fwd_off >= 0) {                            // fp32 copy inside the packed buffer
-          reinterpret_cast<float*>(packed + jb.fwd_off)[t * 8 + j] = w[j];
-          if (sync) reinterpret_cast<float*>(tgt_packed + jb.fwd_off)[t * 8 + j] = w[j];
+        for (int j = 0; j < 4; ++j) gs[j] = ok[j] ? g[j] * gin * fnz(gnoise[jb.eout_off + n + j]) : 0.f;
+      }
+      upd4<OP>(w, g, a, b, e0, h.reg_end, h, lr_t, ok);
+      store4(W + e0, vec, ok, w);
+      if constexpr (ONE) store4(S0 + e0, vec, ok, a);
+      if constexpr (TWO) store4(S1 + e0, vec, ok, b);
+      if (sync) store4(tgt + e0, vec, ok, w);
+      if (noisy) {
+        upd4<OP>(ws, gs, as, bs, s0i, h.reg_end, h, lr_t, ok);
+        store4(W + s0i, vec, ok, ws);
+        if constexpr (ONE) store4(S0 + s0i, vec, ok, as);
+        if constexpr (TWO) store4(S1 + s0i, vec, ok, bs);
+        if (sync) store4(tgt + s0i, vec, ok, ws);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = w[j];
+    if (noisy) {
+      const float fin = (!elem && jb.ein_off >= 0 && rowok) ? fnz(noise[jb.ein_off + k]) : 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ok[j]) e[j] = w[j] + ws[j] * fin * fnz(noise[jb.eout_off + n + j]);
+    }
+    if (jb.eff) store4(eff + e0, vec, ok, e);
+    if (elem) {
+      if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
+        float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
+        float* tf = psync ? reinterpret_cast<float*>(tgt_packed + jb.fwd_off) + n : nullptr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!ok[j]) continue;
+          pf[j] = e[j];
+          if (tf) tf[j] = e[j];
         }
       }
-      continue;
+      continue;                    // uniform per block: no barrier below is skipped unevenly
     }
-    // ---- tile: row r, 8 columns c8..c8+7
-    const int r = t >> 3, c8 = (t & 7) * 8;
-    const int k = jb.k0 + r, n = jb.n0 + c8;
-    const int64_t e0 = (int64_t)jb.src_off + (int64_t)k * jb.N + n;
-    const bool rowok = k < jb.K;
-    const bool vec = rowok && n + 8 <= jb.N && (jb.N % 4) == 0;
-    if (vec) {
-      const float4* W4 = reinterpret_cast<const float4*>(W + e0);
-      const float4* G4 = reinterpret_cast<const float4*>(G + e0);
-      const float4 w0 = W4[0], w1 = W4[1], g0 = G4[0], g1 = G4[1];
-      w[0] = w0.x; w[1] = w0.y; w[2] = w0.z; w[3] = w0.w; w[4] = w1.x; w[5] = w1.y; w[6] = w1.z; w[7] = w1.w;
-      g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
-      if constexpr (OP != 0) {
-        const float4 a0 = reinterpret_cast<const float4*>(S0 + e0)[0], a1 = reinterpret_cast<const float4*>(S0 + e0)[1];
-        a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
-      }
-      if constexpr (TWO) {
-        const float4 b0 = reinterpret_cast<const float4*>(S1 + e0)[0], b1 = reinterpret_cast<const float4*>(S1 + e0)[1];
-        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
-      }
+    bfx4 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ok[j] = true;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ok[j] = rowok && n + j < jb.N;
-        const int64_t i = e0 + j;
-        w[j] = ok[j] ? W[i] : 0.f; g[j] = ok[j] ? G[i] : 0.f;
-        a[j] = (OP != 0 && ok[j]) ? S0[i] : 0.f; b[j] = (TWO && ok[j]) ? S1[i] : 0.f;
-      }
-    }
-    upd8<OP>(w, g, a, b, (int)e0, h.reg_end, h, lr_t, ok);
-    if (vec) {
-      float4* W4 = reinterpret_cast<float4*>(W + e0);
-      W4[0] = make_float4(w[0], w[1], w[2], w[3]); W4[1] = make_float4(w[4], w[5], w[6], w[7]);
-      if (sync) {
-        float4* T4 = reinterpret_cast<float4*>(tgt + e0);
-        T4[0] = W4[0]; T4[1] = W4[1];
-      }
-      if constexpr (OP != 0) {
-        float4* A4 = reinterpret_cast<float4*>(S0 + e0);
-        A4[0] = make_float4(a[0], a[1], a[2], a[3]); A4[1] = make_float4(a[4], a[5], a[6], a[7]);
-      }
-      if constexpr (TWO) {
-        float4* B4 = reinterpret_cast<float4*>(S1 + e0);
-        B4[0] = make_float4(b[0], b[1], b[2], b[3]); B4[1] = make_float4(b[4], b[5], b[6], b[7]);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (!ok[j]) continue;
-        const int64_t i = e0 + j;
-        W[i] = w[j];
-        if constexpr (OP != 0) S0[i] = a[j];
-        if constexpr (TWO) S1[i] = b[j];
-        if (sync) tgt[i] = w[j];
-      }
-    }
-    bfx8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (act_t)(ok[j] ? w[j] : 0.f);
-    // dgrad fragments straight from the registers
-    if (jb.dg_mode != 0 && rowok) {
-      int kp, np;                                        // K' of the first of the 8 values, N'
+    for (int j = 0; j < 4; ++j) v[j] = (act_t)(ok[j] ? e[j] : 0.f);
+    // dgrad fragments straight from the registers: 4 consecutive K' of one lane's slot
+    if (jb.dg_mode != 0 && rowok && n < jb.N) {
+      int kp, np;                                        // K' of the first of the 4 values, N'
       if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
       else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
       const int lane = ((kp & 31) >> 3) * 16 + (np & 15);
-      const int64_t o = jb.dg_off + ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8;
-      if (n < jb.N) {
-        *reinterpret_cast<bfx8*>(packed + o) = v;
-        if (sync) *reinterpret_cast<bfx8*>(tgt_packed + o) = v;
-      }
+      const int64_t o = jb.dg_off + ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8
+                        + (kp & 7);
+      *reinterpret_cast<bfx4*>(packed + o) = v;
+      if (psync) *reinterpret_cast<bfx4*>(tgt_packed + o) = v;
     }
     // forward fragments through an LDS transpose of the bf16 tile
-    *reinterpret_cast<bfx8*>(tile + r * 72 + c8) = v;
+    *reinterpret_cast<bfx4*>(tile + (t >> 4) * 72 + (t & 15) * 4) = v;
     __syncthreads();
-    {
+    if (t < 256) {
       const int nt = t >> 6, l = t & 63, nl = nt * 16 + (l & 15), kk = 8 * (l >> 4);
       if (jb.n0 + nt * 16 < jb.N) {
         bfx8 f;
@@ -281,11 +316,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
                                                   ((jb.n0 >> 4) + nt)) * 64 + l) * 8;
         *reinterpret_cast<bfx8*>(packed + o) = f;
-        if (sync) *reinterpret_cast<bfx8*>(tgt_packed + o) = f;
+        if (psync) *reinterpret_cast<bfx8*>(tgt_packed + o) = f;
       }
     }
     __syncthreads();
   }
+  if (!UPD) return;
+  __shared__ int s_last;
   if (threadIdx.x == 0) {
     bool last;
     if (hier) {
@@ -312,6 +349,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
       __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    s_last = last ? 1 : 0;
+  }
+  if (noise_dst != nullptr) {
+    // every other block consumed gnoise before its ticket add: the last block may overwrite it
+    __syncthreads();
+    if (s_last)
+      for (int i = threadIdx.x; i < noise_n; i += blockDim.x) noise_dst[i] = noise[i];
   }
 }
 
@@ -382,7 +426,8 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
 void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
-                       int max_grid, hipStream_t st) {
+                       int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
+                       int noise_n, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
@@ -396,9 +441,10 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   act_t* P = reinterpret_cast<act_t*>(packed);
   act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
   const int tf = tfreq < 1 ? 1 : tfreq;
-#define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(256), 0, st, w, g, s0, s1, beta_pow, step, \
-                                  ticket, h, J, njobs, P, tgt, TP, tf, hier)
+#define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
+                                  ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n)
   switch (op) {
+    case -1: OPK(-1); break;
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
     case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break;
     default: break;

@@ -95,12 +95,16 @@ DQN_DEV void c51_load_logits(const HeadArgs& a, int inst, float* lg, float* vl, 
   }
 }
 
-// dueling combine per atom, then in-place softmax of every (b, a) row, ONE LANE PER
-// ROW (51-atom rows at an odd LDS stride: conflict-free, no cross-lane reductions).
-// If logp != nullptr the log-probabilities of each sample's TAKEN action row are
-// kept there ([B][NA]).
-DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* logp, int tid, int nth, int lane,
-                         int wave, int nwave) {
+DQN_DEV float c51_z(const HeadArgs& a, int n) {
+  return a.vmin + (a.vmax - a.vmin) * (float)n / (float)(a.atoms - 1);
+}
+
+// dueling combine per atom, then in-place softmax of every (b, a) row: SIXTEEN LANES PER
+// ROW (one DPP row; atom n = l16 + 16 i, i < 4, so atoms <= 64), max / sum reductions on
+// DPP row ops (no LDS crossbar). If logp != nullptr the log-probabilities of each
+// sample's TAKEN action row are kept there ([B][NA]); if q != nullptr the expected value
+// q[b][i] = sum_n p_n z_n is written too (action selection / acting).
+DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* logp, float* q, int tid, int nth) {
   const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
   if (a.dueling) {
     for (int t = tid; t < B * NA; t += nth) {
@@ -113,30 +117,46 @@ DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* l
     }
     __syncthreads();
   }
-  for (int row = tid; row < B * A; row += nth) {
+  const int l16 = tid & 15;
+  for (int row = tid >> 4; row < B * A; row += nth >> 4) {     // uniform per 16-lane group
     const int b = row / A, i = row - b * A;
     float* r = lg + b * NO + i * NA;
-    float* lq = (logp != nullptr && i == a.act[b]) ? logp + b * NA : nullptr;
+    float x[4];
     float mx = -INFINITY;
-    for (int n = 0; n < NA; ++n) mx = fmaxf(mx, r[n]);
-    float s = 0.f;
-    for (int n = 0; n < NA; ++n) {
-      const float x = r[n] - mx, e = __expf(x);
-      s += e;
-      r[n] = e;
-      if (lq) lq[n] = x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = l16 + 16 * u;
+      x[u] = n < NA ? r[n] : -INFINITY;
+      mx = fmaxf(mx, x[u]);
     }
-    const float inv = 1.f / s, ls = __logf(s);
-    for (int n = 0; n < NA; ++n) {
-      r[n] *= inv;
-      if (lq) lq[n] -= ls;
+    mx = row16_max(mx);
+    float e[4], s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      e[u] = l16 + 16 * u < NA ? __expf(x[u] - mx) : 0.f;
+      s += e[u];
+    }
+    s = row16_sum(s);
+    const float inv = 1.f / s;
+    float qs = 0.f;
+    const bool keep = logp != nullptr && i == a.act[b];
+    const float ls = keep ? __logf(s) : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = l16 + 16 * u;
+      if (n < NA) {
+        const float p = e[u] * inv;
+        r[n] = p;
+        qs += p * c51_z(a, n);
+        if (keep) logp[b * NA + n] = x[u] - mx - ls;
+      }
+    }
+    if (q != nullptr) {
+      qs = row16_sum(qs);
+      if (l16 == 0) q[row] = qs;
     }
   }
   __syncthreads();
-}
-
-DQN_DEV float c51_z(const HeadArgs& a, int n) {
-  return a.vmin + (a.vmax - a.vmin) * (float)n / (float)(a.atoms - 1);
 }
 
 __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
@@ -164,20 +184,10 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     if (a.lgi[inst] != nullptr) c51_load_logits(a, inst, lg, vl, tid, nth);
     else c51_logits(a, inst, lg, vl, lane, wave, nwave);
   };
-  auto expected_q = [&]() {             // q[b][i] = sum_n p z_n  (one lane per row)
-    for (int row = tid; row < B * A; row += nth) {
-      const float* r = lg + row * NA;
-      float s = 0.f;
-      for (int n = 0; n < NA; ++n) s += r[n] * c51_z(a, n);
-      q[row] = s;
-    }
-    __syncthreads();
-  };
   if (a.infer) {
     logits(0);
     __syncthreads();
-    c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
-    expected_q();
+    c51_softmax(a, lg, vl, nullptr, q, tid, nth);
     if (a.q_out != nullptr)
       for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
     if (a.has_actor) actor_step_block(a.actor, q, sdone);
@@ -188,8 +198,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   logits(sel);
   __syncthreads();
   C51_MARK(1);
-  c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
-  expected_q();
+  c51_softmax(a, lg, vl, nullptr, q, tid, nth);
   C51_MARK(2);
   for (int b = tid; b < B; b += nth) {
     int best = 0;
@@ -203,7 +212,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   if (sel != 1) {
     logits(1);
     __syncthreads();
-    c51_softmax(a, lg, vl, nullptr, tid, nth, lane, wave, nwave);
+    c51_softmax(a, lg, vl, nullptr, nullptr, tid, nth);
   }
   for (int t = tid; t < B * NA; t += nth) mt[t] = 0.f;
   __syncthreads();
@@ -227,10 +236,10 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   __syncthreads();                      // projection reads of lg done, its atomics complete
   logits(0);
   __syncthreads();
-  c51_softmax(a, lg, vl, lp, tid, nth, lane, wave, nwave);
+  c51_softmax(a, lg, vl, lp, nullptr, tid, nth);
   float contrib = 0.f;
   for (int b = wave; b < B; b += nwave) {
-    const float ce = -wave_sum(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
+    const float ce = -wave_sum_dpp(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
     const float w = a.wts != nullptr ? a.wts[b] : 1.f;
     if (lane < NA) {   // d(mean w*CE)/d logit of the taken action = w/B (p - m); reuse lp for it
       const float p = lg[b * NO + a.act[b] * NA + lane];
@@ -242,7 +251,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     }
   }
   {
-    const float s = wave_sum(contrib);
+    const float s = wave_sum_dpp(contrib);
     if (lane == 0) red[wave] = s;
   }
   __syncthreads();
@@ -350,6 +359,38 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
 // ------------------------------------------------------------------ noisy nets
 DQN_DEV float fnoise(float x) { return copysignf(sqrtf(fabsf(x)), x); }
 
+// Standard normals for the factorised noise: Box-Muller over Philox4x32-10 keyed by the run
+// seed rng[0] at counter rng[1] (4 normals per Philox call) -> out0[0, n) then out1[0, n).
+// Same seed on every DP rank -> the same noise everywhere (the fused optimizer derives the
+// sigma gradients from the all-reduced mu gradients with it). ONE block: the counter bump
+// after the barrier is ordered after every lane's read; graph-capturable (no host state).
+__global__ void __launch_bounds__(1024) noise_normal_kernel(float* __restrict__ out0, float* __restrict__ out1,
+                                                            int n, int64_t* __restrict__ rng) {
+  const uint64_t seed = (uint64_t)rng[0], ctr = (uint64_t)rng[1];
+  const int total = out1 != nullptr ? 2 * n : n;
+  for (int q = threadIdx.x; 4 * q < total; q += blockDim.x) {
+    const u32x4 r = philox(seed ^ 0x2545f4914f6cdd1dull, ctr, (uint32_t)q, 0x6e6f6973u);
+    const uint32_t u[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float u1 = ((float)(u[2 * h] >> 8) + 1.f) * (1.0f / 16777216.0f);   // (0, 1]
+      const float u2 = (float)(u[2 * h + 1] >> 8) * (1.0f / 16777216.0f);       // [0, 1)
+      const float rad = sqrtf(-2.f * __logf(u1));
+      float sn, cs;
+      __sincosf(6.283185307179586f * u2, &sn, &cs);
+      const float z[2] = {rad * cs, rad * sn};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = 4 * q + 2 * h + j;
+        if (i < n) out0[i] = z[j];
+        else if (i < total) out1[i - n] = z[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) rng[1] = (int64_t)(ctr + 1);
+}
+
 __global__ void __launch_bounds__(256) noisy_mix_kernel(const float* __restrict__ flat, float* __restrict__ eff,
                                                         const float* __restrict__ noise,
                                                         const NoisyJob* __restrict__ jobs) {
@@ -388,7 +429,9 @@ size_t c51_head_lds_bytes(const HeadArgs& a) {
 }
 
 void launch_c51_head(const HeadArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(c51_head_kernel, dim3(a.infer ? 1 : 8), dim3(1024), c51_head_lds_bytes(a), st, a);
+  // training: phases 1-3 run redundantly in every block (L2-hot inputs); the output-layer
+  // backward tiles spread over all 32 x 16 waves
+  hipLaunchKernelGGL(c51_head_kernel, dim3(a.infer ? 1 : 32), dim3(1024), c51_head_lds_bytes(a), st, a);
 }
 
 void launch_noisy_mix(const float* flat, float* eff, const float* noise, const NoisyJob* jobs, int njobs,
@@ -396,6 +439,10 @@ void launch_noisy_mix(const float* flat, float* eff, const float* noise, const N
   int g = (max_elems + 255) / 256;
   g = g < 1 ? 1 : (g > 512 ? 512 : g);
   hipLaunchKernelGGL(noisy_mix_kernel, dim3(g, njobs), dim3(256), 0, st, flat, eff, noise, jobs);
+}
+
+void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st) {
+  hipLaunchKernelGGL(noise_normal_kernel, dim3(1), dim3(1024), 0, st, out0, out1, n, rng);
 }
 
 void launch_noisy_grad(float* grad, const float* noise, const NoisyJob* jobs, int njobs, int max_elems,

@@ -76,9 +76,8 @@ class Learner:
         per = getattr(r, 'prioritized', False)
         beta = None
         if per:
-            beta = torch.clamp(self.config.per_beta0 + (1.0 - self.config.per_beta0)
-                               * self.net.global_step.float() / max(1, self.config.per_beta_steps),
-                               max=1.0)
+            # annealed in the sampling kernel from the device global_step
+            beta = (self.net.global_step, self.config.per_beta0, self.config.per_beta_steps)
         if (getattr(self.net.executor, 'consumes_slots', False) and getattr(r, 'frame_mode', False)
                 and self.device.type == 'cuda'):
             # one launch: indices + scalars + frame-slot tables; conv1 reads the ring
@@ -92,24 +91,30 @@ class Learner:
             batch = r.gather(self.idx)
             if per:
                 batch['weights'] = self.weights
-        self.net.reset_noise()
+        self.net.begin_step_noise()
         acting = None
         if self.actor is not None:
             assert 'frames' in batch, 'fused acting needs the slot-batch sampler'
             acting = self.actor.fused_args()
+        # noisy nets: the fused optimizer derives dL/dsigma itself (not for async-PS pushes)
+        sg = not (self.ps is None and self.net.fuses_sigma_grads(self._target_freq()))
         if self._split:
-            loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True)
+            loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True, sigma_grads=sg)
         else:
-            loss, prio = self.net.compute_grads(batch, acting=acting)
+            loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg)
         # keep references (static buffers under graph capture) instead of copies
         self.loss = loss.view(1)
         self.prio = prio.view(-1)
+
+    def _target_freq(self):
+        """target_freq argument of apply_grads: the hard sync rides in the optimizer launch."""
+        return self.config.target_update_freq if self.tau >= 1.0 else None
 
     def _apply(self):
         cfg = self.config
         hard = self.tau >= 1.0
         # hard target sync folded into the optimizer + repack launches when the backend can
-        fused = self.net.apply_grads(self.reducer.scale, target_freq=cfg.target_update_freq if hard else None)
+        fused = self.net.apply_grads(self.reducer.scale, target_freq=self._target_freq())
         if getattr(self.replay, 'prioritized', False):
             self.replay.update_priorities(self.idx, self.prio, cfg.per_eps)
         # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).

@@ -80,6 +80,20 @@ class Network:
         self.noise = torch.zeros(nz, device=self.device) if nz else None
         self.noise_target = torch.zeros(nz, device=self.device) if nz else None
         self.last_loss = torch.zeros(1, device=self.device)
+        # noisy nets on the HIP executor: the online weights' packed / effective buffers are
+        # kept mixed under self.noise. Samples come from a device Philox stream seeded by the
+        # run seed (identical on every DP rank); after each update the fused optimizer derives
+        # the sigma gradients from the mu gradients under self.noise, mixes in the next sample
+        # (drawn with the next target sample, one launch) and makes it current — so the
+        # learner and the device actors launch no mix for the online net.
+        self._premixed = bool(nz) and hasattr(self.executor, 'premix')
+        if self._premixed:
+            self.noise_next = torch.zeros_like(self.noise)
+            seed = int(config.seed) if getattr(config, 'seed', None) is not None else 0
+            self.noise_rng = torch.tensor([(seed * 0x9E3779B1 + 0x6E6F) & 0x7fffffffffff, 0], dtype=torch.int64,
+                                          device=self.device)
+            self.executor.draw_noise(self.noise, self.noise_target, self.noise_rng)
+            self.executor.premix(self.online.flat, self.noise)
 
     # -------------------------------------------------------------- factory
     @staticmethod
@@ -104,16 +118,38 @@ class Network:
         return self.executor.q_values(self.target.flat, self._to_dev(x), self.noise_target)
 
     def reset_noise(self, generator=None):
-        if self.noise is not None:
+        """Fresh online and target noise samples now (torch RNG when a generator is given)."""
+        if self.noise is None:
+            return
+        if self._premixed and generator is None:
+            self.executor.draw_noise(self.noise, self.noise_target, self.noise_rng)
+        else:
             self.noise.normal_(generator=generator)
             self.noise_target.normal_(generator=generator)
+        if self._premixed:
+            self.executor.premix(self.online.flat, self.noise)
+
+    def begin_step_noise(self):
+        """Noise for one learner step. Premixed executors: nothing to do (both samples were
+        drawn by the previous ``apply_grads``); otherwise fresh online and target samples."""
+        if self.noise is not None and not self._premixed:
+            self.reset_noise()
+
+    def fuses_sigma_grads(self, target_freq: Optional[int]) -> bool:
+        """True when ``apply_grads(.., target_freq)`` runs the fused noisy optimizer, which
+        derives dL/dsigma itself (so ``compute_grads(sigma_grads=False)`` may skip it)."""
+        return (self._premixed and target_freq is not None and self.online.flat.is_cuda
+                and self.optimizer.backend != 'torch')
 
     # ------------------------------------------------------------- training
-    def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False):
+    def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False,
+                      sigma_grads: bool = True):
         """Loss + gradient into ``self.grad``. ``split=True`` returns ``(loss, prio, tail)``: when
         ``tail`` is not None only the dense-layer gradients (``dense_range()``) are final and
         ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad)."""
         kw = {}
+        if self._premixed and not sigma_grads:
+            kw['sigma_grads'] = False
         if acting is not None:     # fused acting (HIP executor): the actors' step rides along
             kw['acting'] = acting
         can_split = split and hasattr(self.executor, 'supports_fused_acting')
@@ -149,10 +185,17 @@ class Network:
         ex = self.executor
         fuse = (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
                 and hasattr(ex, 'packed'))
-        if fuse and not getattr(ex, 'noisy', False) and hasattr(ex, 'update_and_pack'):
-            # optimizer + repack + hard target sync: one launch
+        if fuse and hasattr(ex, 'update_and_pack') and (self._premixed or not getattr(ex, 'noisy', False)):
+            # optimizer + repack + hard target sync: one launch (noisy nets: + the mix of the
+            # next online noise sample, drawn here)
+            kw = {}
+            if self._premixed:
+                # next online sample (+ the next step's target sample); the optimizer derives
+                # dL/dsigma under the current one, mixes the next one in and makes it current
+                self.executor.draw_noise(self.noise_next, self.noise_target, self.noise_rng)
+                kw.update(noise=self.noise_next, grad_noise=self.noise, noise_dst=self.noise)
             ex.update_and_pack(self.optimizer, self.online.flat, self.grad, grad_scale, self.global_step,
-                               target=self.target.flat, target_freq=int(target_freq))
+                               target=self.target.flat, target_freq=int(target_freq), **kw)
             return True
         if fuse:
             self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,

@@ -158,7 +158,12 @@ class HipExecutor:
     def _plan_update(self):
         """Work list of the fused optimizer+pack kernel (optim.hip optim_pack_kernel): 32x64
         tiles of every packed weight tensor (forward fragments + its dgrad fragments), then
-        2048-element chunks of everything else (with the fc bias fp32 copy)."""
+        2048-element chunks of everything else (with the fc bias fp32 copy).
+
+        Noisy nets: each noisy mu tile / chunk also carries its sigma tensor (updated in the
+        same thread; sigma tensors get no items of their own) and the noise offsets, so the
+        packed fragments (and the fp32 ``eff`` values of everything read in fp32: all but the
+        big fc weights) are mu + sigma * f(eps_in) f(eps_out) under the bound noise sample."""
         lay = self.layout
         fwd, dg, copy = {}, {}, {}
         for j in self.jobs:
@@ -168,49 +173,124 @@ class HipExecutor:
                 dg[j.src_off] = j
             else:
                 copy[j.src_off] = j
+        nz, sig = {}, set()
+        if self.noisy:
+            noff = 0
+            for d in self.arch.dense_layers():
+                if d.noisy:
+                    nz[lay.offsets[d.name + '/w']] = (lay.offsets[d.name + '/w_sigma'], noff, noff + d.fin)
+                    nz[lay.offsets[d.name + '/b']] = (lay.offsets[d.name + '/b_sigma'], -1, noff + d.fin)
+                    sig |= {lay.offsets[d.name + '/w_sigma'], lay.offsets[d.name + '/b_sigma']}
+                    noff += d.fin + d.fout
+        fc_w = {lay.offsets[n + '/w'] for n in ('fcl', 'value/fcl', 'advantage/fcl') if n + '/w' in lay.offsets}
         items = []
         for src, f in sorted(fwd.items()):
             d = dg.get(src)
+            so, ei, eo = nz.get(src, (-1, -1, -1))
+            eff = int(self.noisy and src not in fc_w)
             for k0 in range(0, f.K, 32):
                 for n0 in range(0, f.N, 64):
                     items.append([0, src, f.K, f.N, k0, n0, f.dst_off, f.dst_N16, f.nt_off, f.ks_off,
                                   d.mode if d else 0, d.dst_off if d else 0, d.dst_N16 if d else 0,
-                                  d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0])
+                                  d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0, so, ei, eo, eff])
         for name in lay.names:
             off, n = lay.offsets[name], lay.numel(name)
-            if off in fwd:
+            if off in fwd or off in sig:
                 continue
             c = copy.get(off)
+            so, _, eo = nz.get(off, (-1, -1, -1))
             for s0 in range(0, n, 2048):
                 cnt = min(2048, n - s0)
-                items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + 2 * s0) if c else -1] + [0] * 9)
+                items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + 2 * s0) if c else -1] + [0] * 9
+                             + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy)])
         self.upd_items = items
         self._upd_dev: Dict[torch.device, torch.Tensor] = {}
+        self._bound: Dict[int, torch.Tensor] = {}   # flat ptr -> noise its packed/eff buffers reflect
+        self._dummies: Dict[torch.device, tuple] = {}
 
-    def update_and_pack(self, opt, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float,
-                        global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1):
-        """Optimizer step + repack in ONE launch (+ the hard target sync under the device
-        predicate when ``target`` is given). Returns False if the layout can't use it."""
-        from ..optim import OPT_IDS
-        dev = flat.device
+    def _upd_jobs(self, dev):
         jobs = self._upd_dev.get(dev)
         if jobs is None:
             ints = [v for it in self.upd_items for v in it]
             assert len(ints) == len(self.upd_items) * self.ext.UPD_JOB_INTS
             jobs = torch.tensor(ints, dtype=torch.int32, device=dev)
             self._upd_dev[dev] = jobs
+        return jobs
+
+    def _eff_for(self, key: int, like: torch.Tensor) -> torch.Tensor:
+        eff = self._eff.get(key)
+        if eff is None:
+            eff = torch.zeros_like(like)
+            self._eff[key] = eff
+        return eff
+
+    def _mix_pack(self, flat: torch.Tensor, noise: Optional[torch.Tensor], eff: torch.Tensor, p: torch.Tensor):
+        """Noisy nets: ONE launch (optim_pack_kernel<-1>, no update) writing the packed fragments
+        and the fp32 effective values of ``flat`` under ``noise`` (None: zero noise, eff = mu)."""
+        dev = flat.device
+        d = self._dummies.get(dev)
+        if d is None:
+            from ..models.torch_net import noise_size
+            d = (torch.zeros(2, dtype=torch.float32, device=dev), torch.zeros(17 * 32, dtype=torch.int32, device=dev),
+                 torch.zeros(1, dtype=torch.int64, device=dev),
+                 torch.zeros(noise_size(self.arch), dtype=torch.float32, device=dev))
+            self._dummies[dev] = d
+        if noise is None:
+            noise = d[3]
+        assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
+        self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
+                            self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None)
+
+    def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
+        """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
+        self.ext.noise_normal(out0, out1, rng)
+
+    def premix(self, flat: torch.Tensor, noise: torch.Tensor):
+        """Bind ``noise`` to ``flat``: its packed / eff buffers now hold the effective weights
+        under that sample, and stay so (the noisy fused optimizer re-mixes after each update),
+        so consumers using that same noise tensor (learner online instance, device actors,
+        q_values) launch no mix of their own."""
+        assert self.noisy
+        k = flat.data_ptr()
+        self._mix_pack(flat, noise, self._eff_for(k, flat), self._packed_for(k, flat))
+        self._bound[k] = noise
+
+    def update_and_pack(self, opt, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float,
+                        global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1,
+                        noise: Optional[torch.Tensor] = None, grad_noise: Optional[torch.Tensor] = None,
+                        noise_dst: Optional[torch.Tensor] = None):
+        """Optimizer step + repack in ONE launch (+ the hard target sync under the device
+        predicate when ``target`` is given). Noisy nets: ``noise`` (the next sample for this
+        flat) is mixed in and bound (see ``premix``); the target's packed copy is not written
+        (the target is re-mixed under its own noise every step). ``grad_noise``: derive the
+        sigma gradients from the mu-slot gradients under that sample (the one the forward
+        used) instead of reading them; ``noise_dst``: the kernel's last block copies ``noise``
+        there, and ``noise_dst`` becomes the bound noise. Returns True."""
+        from ..optim import OPT_IDS
+        dev = flat.device
+        jobs = self._upd_jobs(dev)
         hp = opt.hp
         s0 = opt.slots[0] if len(opt.slots) > 0 else flat
         s1 = opt.slots[1] if len(opt.slots) > 1 else flat
         if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev or opt.ticket.numel() < 17 * 32:
             opt.ticket = torch.zeros(17 * 32, dtype=torch.int32, device=dev)   # 1 + 16 sub-tickets, 128 B apart
-        p = self.packed(flat)
-        pt = self.packed(target) if target is not None else None
+        eff = None
+        if self.noisy:
+            assert noise is not None and noise.dtype == torch.float32
+            k = flat.data_ptr()
+            p, eff = self._packed_for(k, flat), self._eff_for(k, flat)
+            pt = None
+        else:
+            p = self.packed(flat)
+            pt = self.packed(target) if target is not None else None
         self.ext.optim_pack(OPT_IDS[opt.name], flat, grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr),
                             float(opt.reg_param), int(opt.layout.reg_end), float(grad_scale), global_step,
                             [float(hp['momentum']), float(hp['rho']), float(hp['rms_mom']), float(hp['rms_eps']),
                              float(hp['b1']), float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']),
-                             float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq), self.opt_max_grid)
+                             float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq), self.opt_max_grid,
+                            noise, eff, grad_noise, noise_dst)
+        if self.noisy:
+            self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
         return True
 
     def _plan_noisy(self):
@@ -257,21 +337,19 @@ class HipExecutor:
     def effective(self, flat: torch.Tensor, noise: Optional[torch.Tensor], key: Optional[int] = None
                   ) -> torch.Tensor:
         """Noisy nets: eff = mu + sigma*f(e_in)f(e_out) for the noisy layers (mu elsewhere),
-        then packed into ``flat``'s fragment buffer. Returns the effective fp32 buffer the
-        kernels read biases / head weights from. No-op (returns flat) without noisy layers."""
+        packed into ``flat``'s fragment buffer (or ``key``'s) in one launch. Returns the
+        effective fp32 buffer the kernels read biases / head weights from. No launch when
+        ``noise`` is bound to ``flat`` (``premix``); no-op (returns flat) without noisy layers."""
         if not self.noisy:
             return flat
         k = flat.data_ptr() if key is None else key
-        eff = self._eff.get(k)
-        if eff is None:
-            eff = torch.zeros_like(flat)
-            self._eff[k] = eff
-        jobs = self._noisy_jobs_on(flat.device)
-        self.ext.qnet_noisy_mix(flat.data_ptr(), eff.data_ptr(), noise.data_ptr() if noise is not None else 0,
-                                jobs.data_ptr(), len(self.noisy_jobs), self._noisy_max)
-        p = self.packed(flat) if key is None else self._packed_for(key, flat)
-        self.ext.qnet_pack(eff.data_ptr(), p.data_ptr(), self._jobs_on(flat.device).data_ptr(), len(self.jobs),
-                           self._max_threads)
+        if key is None and noise is not None and self._bound.get(k) is noise:
+            return self._eff[k]
+        if key is None:
+            self._bound.pop(k, None)
+        eff = self._eff_for(k, flat)
+        p = self._packed_for(k, flat)
+        self._mix_pack(flat, noise, eff, p)
         return eff
 
     def _packed_for(self, key: int, like: torch.Tensor) -> torch.Tensor:
@@ -305,6 +383,10 @@ class HipExecutor:
 
         target/step/freq: also write the fragments into ``target``'s packed copy when
         step % freq == 0 (device predicate; the fused hard target sync)."""
+        bound = self._bound.get(flat.data_ptr()) if self.noisy else None
+        if bound is not None:                    # noisy: keep the bound noise sample mixed in
+            self.premix(flat, bound)
+            return
         p = self._packed.get(flat.data_ptr())
         if p is None:
             self.packed(flat)
@@ -534,8 +616,11 @@ class HipExecutor:
 
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
-                      split: bool = False):
-        """acting (fused acting, slot batches only): {'stacks': [E, 4] int32 frame slots of the
+                      split: bool = False, sigma_grads: bool = True):
+        """sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
+        optimizer derives dL/dsigma from the mu-slot gradient and the noise itself.
+
+        acting (fused acting, slot batches only): {'stacks': [E, 4] int32 frame slots of the
         device actors' states, 'ptrs', 'ints', 'f': the actor-step arguments of act_fused}. The
         actors' states ride along as one more trunk / fc instance with the online weights, and
         one extra workgroup of the head launch runs the eps-greedy / env / replay-append step:
@@ -548,6 +633,7 @@ class HipExecutor:
         backward. The learner starts the all-reduce of the dense range between the two, so it
         overlaps the conv backward. ``tail`` is None when this network has no split point."""
         ext, lay = self.ext, self.layout
+        gnoise = noise if sigma_grads else None      # noise of the dL/dsigma split (None: skip it)
         frames = batch.get('frames')
         if frames is not None:             # slot batch: conv1 reads the replay frame ring directly
             s, ns = batch['state_slots'], batch['next_slots']
@@ -632,7 +718,7 @@ class HipExecutor:
         else:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
         if self.arch.network == 'cnn':
-            out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev)
+            out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, gnoise, dev)
             return out + (None,) if split else out
         x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         mc_fc = (B + 31) // 32 * 32
@@ -656,7 +742,7 @@ class HipExecutor:
             dims = [d1, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
                     [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]]
             scales = [self.input_scale, 1.0, 1.0, 1.0]
-            noisy = self.noisy and noise is not None
+            noisy = self.noisy and gnoise is not None
             if split and not noisy:
                 # dense weight gradients now (they need only dh and x3): the dense range is final
                 ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
@@ -675,7 +761,7 @@ class HipExecutor:
                                 0, 0])
                 ext.qnet_wgrad_group(members, dims, scales)
                 if noisy:
-                    ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
+                    ext.qnet_noisy_grad(grad_out.data_ptr(), gnoise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                         len(self.noisy_jobs), self._noisy_max)
 
             if split and not noisy:
@@ -709,8 +795,8 @@ class HipExecutor:
         # conv1: wgrad only (input scale folded in); last kernel of the step, on main
         ext.qnet_wgrad(kind1, s.data_ptr(), d1, ws['dz1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0,
                        c1.cout, c1.cout, 128, 256, 32, self.input_scale, True)
-        if self.noisy and noise is not None:       # dL/dsigma from dL/dW_eff (in the mu slots)
-            ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
+        if self.noisy and gnoise is not None:      # dL/dsigma from dL/dW_eff (in the mu slots)
+            ext.qnet_noisy_grad(grad_out.data_ptr(), gnoise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                 len(self.noisy_jobs), self._noisy_max)
         main.wait_stream(side)
         return (ws['loss'], ws['prio'], None) if split else (ws['loss'], ws['prio'])

@@ -104,11 +104,25 @@ def sumtree_set(tree, idx: torch.Tensor, td_abs: Optional[torch.Tensor], alpha: 
 
 
 def sumtree_sample(tree, rng_state, size_dev, beta, idx_out, w_out, sample_out: Optional[list] = None):
-    """Stratified proportional sample + importance weights (max-normalised)."""
+    """Stratified proportional sample + importance weights (max-normalised).
+
+    beta: the IS exponent as a float tensor [1], or a ``(global_step, beta0, steps)`` schedule
+    (int64 device step): the kernel anneals beta = min(1, beta0 + (1 - beta0) step / steps)
+    itself, so a graph-captured learner step needs no host math or extra launches for it."""
     ext = _hip(tree.sum)
+    sched = isinstance(beta, tuple)
     if ext is not None:
-        ext.sumtree_sample(tree.sum, tree.min, rng_state, size_dev, beta, idx_out, w_out, tree.P, sample_out or [])
+        if sched:
+            step, b0, steps = beta
+            ext.sumtree_sample(tree.sum, tree.min, rng_state, size_dev, step, idx_out, w_out, tree.P,
+                               sample_out or [], float(b0), float(max(1, steps)))
+        else:
+            ext.sumtree_sample(tree.sum, tree.min, rng_state, size_dev, beta, idx_out, w_out, tree.P,
+                               sample_out or [], 0.0, 1.0)
         return
+    if sched:
+        step, b0, steps = beta
+        beta = torch.clamp(b0 + (1.0 - b0) * step.float() / max(1, steps), max=1.0)
     B, P = idx_out.numel(), tree.P
     g = _cpu_gen(rng_state)
     total = tree.sum[1]

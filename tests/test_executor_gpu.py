@@ -294,3 +294,106 @@ def test_fused_update_and_pack_equals_optimizer_plus_repack(extra):
     for a, b in zip(s0, s1):
         assert torch.equal(a[named], b[named]), float((a - b)[named].abs().max())
     assert torch.equal(p0.view(torch.int16), p1.view(torch.int16))
+
+
+def _noisy_eff_ref(net, flat, noise):
+    """Torch fp32 effective weights: mu + sigma * f(eps_in) f(eps_out) per noisy dense layer."""
+    lay, eff = net.layout, flat.clone()
+    f = lambda x: x.sign() * x.abs().sqrt()
+    noff = 0
+    for d in net.arch.dense_layers():
+        if not d.noisy:
+            continue
+        ei, eo = f(noise[noff:noff + d.fin]), f(noise[noff + d.fin:noff + d.fin + d.fout])
+        v = lambda n: flat[lay.offsets[n]:lay.offsets[n] + lay.numel(n)]
+        ow, ob = lay.offsets[d.name + '/w'], lay.offsets[d.name + '/b']
+        eff[ow:ow + d.fin * d.fout] = v(d.name + '/w') + (v(d.name + '/w_sigma').view(d.fin, d.fout)
+                                                          * torch.outer(ei, eo)).view(-1)
+        eff[ob:ob + d.fout] = v(d.name + '/b') + v(d.name + '/b_sigma') * eo
+        noff += d.fin + d.fout
+    return eff
+
+
+@pytest.mark.parametrize('extra', [RAINBOW, '--noisy --dueling'])
+def test_noisy_fused_update_mixes_next_noise(extra):
+    """Noisy nets: apply_grads = ONE launch doing the optimizer step on mu AND sigma plus the
+    mix + pack under the next online noise sample. The update equals the plain optimizer
+    kernel bit for bit; the fp32 effective weights match torch; Q-values of the premixed
+    online net match the fp32 oracle under the new noise."""
+    net, oracle, batch = _setup(extra + ' --reg_param=0.001')
+    ex, opt = net.executor, net.optimizer
+    g = torch.Generator(device=DEV).manual_seed(9)
+    grad = torch.randn(net.online.flat.shape, device=DEV, generator=g) * 1e-2
+    lay = net.layout
+    named = torch.zeros_like(grad, dtype=torch.bool)
+    for n in lay.names:
+        named[lay.offsets[n]:lay.offsets[n] + lay.numel(n)] = True
+    grad[~named] = 0.0
+    ref = net.online.flat.clone()
+    slots = [s.clone() for s in opt.slots]
+    bp, step = opt.beta_powers.clone(), net.global_step.clone()
+    old_noise = net.noise.clone()
+    # the fused kernel derives dL/dsigma = dL/dW_eff * f(e_in) f(e_out) under the current noise
+    grad_ref = grad.clone()
+    f = lambda x: x.sign() * x.abs().sqrt()
+    sig, noff = torch.zeros_like(named), 0
+    for d in net.arch.dense_layers():
+        if not d.noisy:
+            continue
+        ei, eo = f(old_noise[noff:noff + d.fin]), f(old_noise[noff + d.fin:noff + d.fin + d.fout])
+        for kind, fac in (('w', torch.outer(ei, eo).view(-1)), ('b', eo)):
+            o, os_ = lay.offsets[d.name + '/' + kind], lay.offsets[d.name + '/' + kind + '_sigma']
+            k = lay.numel(d.name + '/' + kind)
+            grad_ref[os_:os_ + k] = grad[o:o + k] * fac
+            sig[os_:os_ + k] = True
+        noff += d.fin + d.fout
+    net.grad.copy_(grad)
+    assert net.apply_grads(0.5, target_freq=1000)
+    o_slots, o_bp = opt.slots, opt.beta_powers
+    opt.slots, opt.beta_powers = slots, bp
+    try:
+        opt.step(ref, grad_ref, 0.5, step)
+    finally:
+        opt.slots, opt.beta_powers = o_slots, o_bp
+    torch.cuda.synchronize()
+    assert not torch.equal(old_noise, net.noise), 'apply_grads draws the next online noise'
+    mu = named & ~sig
+    assert torch.equal(net.online.flat[mu], ref[mu]), float((net.online.flat - ref)[mu].abs().max())
+    torch.testing.assert_close(net.online.flat[sig], ref[sig], rtol=1e-5, atol=1e-7)
+    for a, b in zip(opt.slots, slots):
+        assert torch.equal(a[mu], b[mu])
+        torch.testing.assert_close(a[sig], b[sig], rtol=1e-4, atol=1e-9)
+    eff = ex._eff[net.online.flat.data_ptr()]
+    eff_ref = _noisy_eff_ref(net, ref, net.noise)
+    fc = {lay.offsets[n + '/w'] for n in ('fcl', 'value/fcl', 'advantage/fcl') if n + '/w' in lay.offsets}
+    for n in lay.names:
+        o, k = lay.offsets[n], lay.numel(n)
+        if o in fc or lay.kinds[n] in ('w_sigma', 'b_sigma'):
+            continue                   # fc weights are consumed packed only; sigma has no eff
+        torch.testing.assert_close(eff[o:o + k], eff_ref[o:o + k], rtol=1e-5, atol=1e-6, msg=n)
+    q = net.q_values(batch['states'])
+    q_ref = oracle.q_values(net.online.flat, batch['states'], net.noise)
+    assert _rel(q, q_ref) < 2e-2
+
+
+def test_rainbow_learner_keeps_online_premixed():
+    """Graph-replayed Rainbow learner steps (target noise drawn per step, online noise drawn
+    inside the fused optimizer): the online net's packed weights always reflect net.noise."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.executor import TorchExecutor
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 ' + RAINBOW)
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+    rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
+    rep.fill_synthetic(4096, 6, seed=5)
+    ln = Learner(net, rep, cfg, use_graph=True)
+    for _ in range(6):
+        ln.step()
+    torch.cuda.synchronize()
+    assert int(net.global_step) == 6 and bool(torch.isfinite(net.online.flat).all())
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+                           huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
+    x = torch.randint(0, 256, (16, 84, 84, 4), dtype=torch.uint8, device=DEV)
+    assert _rel(net.q_values(x), oracle.q_values(net.online.flat, x, net.noise)) < 2e-2

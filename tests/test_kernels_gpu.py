@@ -85,6 +85,32 @@ def test_sumtree_set_and_sample():
     assert np.corrcoef(counts, expected)[0, 1] > 0.9
 
 
+@pytest.mark.parametrize('B', [32, 64, 100])
+def test_sumtree_update_duplicates_matches_cpu(B):
+    """Batch updates with duplicate indices (B <= 64: the one-wave sorted climb; B > 64: the
+    level-synchronous kernel) == the sequential CPU tree: last batch position wins a leaf,
+    every ancestor exact, the min-tree and the running max too."""
+    from dist_dqn_amd.replay.sumtree import DeviceSumTree
+    C = 200_000                                     # 18 levels
+    t_cpu, t_gpu = DeviceSumTree(C, 'cpu'), DeviceSumTree(C, DEV)
+    t_cpu.set_max_priority(torch.arange(C, dtype=torch.int32))
+    t_gpu.set_max_priority(torch.arange(C, dtype=torch.int32, device=DEV))
+    g = torch.Generator().manual_seed(1)
+    for it in range(8):
+        upd = torch.randint(0, C, (B,), dtype=torch.int32, generator=g)
+        upd[1::7] = upd[0]                          # duplicates, incl. adjacent leaves / shared paths
+        upd[3] = (upd[2] ^ 1) if it % 2 else upd[3]
+        td = torch.rand(B, generator=g) * 3
+        if B > 64:                                  # concurrent duplicate writes: keep values equal
+            td[1::7] = td[0]
+        t_cpu.update(upd, td, 0.6, 1e-6)
+        t_gpu.update(upd.to(DEV), td.to(DEV), 0.6, 1e-6)
+    torch.testing.assert_close(t_gpu.sum.cpu(), t_cpu.sum, rtol=1e-6, atol=1e-6)
+    # (leaf values are powf on the GPU vs torch.pow on the CPU: 1-ulp differences)
+    torch.testing.assert_close(t_gpu.min.cpu(), t_cpu.min, rtol=1e-6, atol=0)
+    torch.testing.assert_close(t_gpu.max_p.cpu(), t_cpu.max_p)
+
+
 @pytest.mark.parametrize('name', ['sgd', 'momentum', 'rmsprop', 'adam', 'adagrad', 'adadelta', 'ftrl'])
 def test_fused_optimizer_matches_oracle(name):
     from dist_dqn_amd.models import ParamStore, build_arch
