@@ -306,6 +306,7 @@ void actor_step(torch::Tensor q, torch::Tensor frames, torch::Tensor stacks, tor
   const int E = (int)q.size(0), A = (int)q.size(1), K = (int)stacks.size(1);
   const int F = (int)frames.size(0), HW = (int)(frames.size(1) * frames.size(2)), C = (int)state_idx.size(0);
   TORCH_CHECK(stacks.size(0) == E && state_idx.size(1) == K, "stack shapes");
+  TORCH_CHECK(K >= 1 && K <= 4, "actor: frames_per_state must be 1..4");
   TORCH_CHECK(cursor.numel() == 3 && eps.numel() == 3 && rng.numel() == 2, "state vectors");
   TORCH_CHECK(F >= 2 * C + K, "frame ring must hold 2C + k frames");
   TORCH_CHECK(E >= 1 && E <= C, "env count");

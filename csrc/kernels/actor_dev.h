@@ -19,7 +19,8 @@ DQN_DEV void write_random_frame(uint8_t* dst, int HW, uint64_t seed, uint64_t ct
 
 // Env e's decision + replay append (one thread). Returns done; frame slots via refs.
 DQN_DEV int actor_env_step(const ActorArgs& a, const float* qe, int e, int64_t t0, int64_t f0, float eps0,
-                           float eps_min, float decay, uint64_t seed, uint64_t ctr, int& fslot, int& rslot) {
+                           float eps_min, float decay, uint64_t seed, uint64_t ctr, int& fslot, int& rslot,
+                           const int32_t* st_pre = nullptr) {
   fslot = (int)((f0 + 2 * e) % a.F);
   rslot = (int)((f0 + 2 * e + 1) % a.F);
   // reference: eps decays BEFORE each roll (dqn_agent.py:162-174); env e rolls the (e+1)-th time
@@ -36,10 +37,13 @@ DQN_DEV int actor_env_step(const ActorArgs& a, const float* qe, int e, int64_t t
   }
   const float u = u01(r.z);
   const float reward = u < 0.01f ? 1.f : (u < 0.02f ? -1.f : 0.f);
-  const int done = u01(r.w) < a.p_done ? 1 : 0;
+  const int done = u01(r.w) < a.p_done ? 1 : 0;          // == actor_done(a, seed, ctr, e)
   const int t = (int)((t0 + e) % a.C);
   int32_t* st = a.stacks + (int64_t)e * a.K;
-  for (int c = 0; c < a.K; ++c) a.state_idx[(int64_t)t * a.K + c] = st[c];
+  DQN_ASSERT(a.K >= 1 && a.K <= 4);
+  int32_t cur[4];                                        // K <= 4 (frames_per_state, host-checked)
+  for (int c = 0; c < a.K; ++c) cur[c] = st_pre != nullptr ? st_pre[c] : st[c];
+  for (int c = 0; c < a.K; ++c) a.state_idx[(int64_t)t * a.K + c] = cur[c];
   a.next_idx[t] = fslot;
   a.actions[t] = act;
   a.rewards[t] = reward;
@@ -48,7 +52,7 @@ DQN_DEV int actor_env_step(const ActorArgs& a, const float* qe, int e, int64_t t
   if (done) {
     for (int c = 0; c < a.K; ++c) st[c] = rslot;     // new episode: reset frame duplicated k times
   } else {
-    for (int c = 0; c + 1 < a.K; ++c) st[c] = st[c + 1];
+    for (int c = 0; c + 1 < a.K; ++c) st[c] = cur[c + 1];
     st[a.K - 1] = fslot;
   }
   return done;
@@ -68,25 +72,68 @@ DQN_DEV void actor_advance(const ActorArgs& a, int64_t t0, int64_t f0, int64_t s
   a.frames_done[0] += a.E;
 }
 
-// Whole actor step for all E envs inside ONE workgroup; q = [E][A] (LDS or global).
-DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, int* s_done /* LDS [E] */) {
+DQN_DEV void actor_advance(const ActorArgs& a, int64_t t0, int64_t f0, int64_t size0, float eps0, float eps_min,
+                           float decay, uint64_t ctr, int64_t frames_done0) {
+  float eps = eps0;
+  for (int i = 0; i < a.E && eps > eps_min; ++i) eps -= decay;
+  a.eps[0] = eps;
+  a.cursor[0] = (t0 + a.E) % a.C;
+  a.cursor[1] = (f0 + 2 * a.E) % a.F;
+  const int64_t ns = size0 + a.E < a.C ? size0 + a.E : a.C;
+  a.cursor[2] = ns;
+  a.size_dev[0] = (int32_t)ns;
+  a.rng[1] = (int64_t)(ctr + 1);
+  a.frames_done[0] = frames_done0 + a.E;
+}
+
+// The actor's step state (cursor, eps schedule, rng): loaded up front so a caller can
+// issue these loads before unrelated work (the fused head's Q tiles) and hide them.
+struct ActorPre {
+  int64_t t0, f0, size0, frames_done;
+  float eps0, eps_min, decay;
+  uint64_t seed, ctr;
+  int32_t st[4];                 // this thread's env stack (thread e < E), K <= 4
+};
+
+DQN_DEV ActorPre actor_prefetch(const ActorArgs& a) {
+  ActorPre p;
+  p.t0 = a.cursor[0]; p.f0 = a.cursor[1]; p.size0 = a.cursor[2];
+  p.eps0 = a.eps[0]; p.eps_min = a.eps[1]; p.decay = a.eps[2];
+  p.seed = (uint64_t)a.rng[0]; p.ctr = (uint64_t)a.rng[1];
+  p.frames_done = threadIdx.x == 0 ? a.frames_done[0] : 0;
+  const int e = threadIdx.x;
+  for (int c = 0; c < 4; ++c) p.st[c] = (e < a.E && c < a.K) ? a.stacks[(int64_t)e * a.K + c] : 0;
+  return p;
+}
+
+// env e's episode end this step: the same draw actor_env_step makes (any thread can ask)
+DQN_DEV bool actor_done(const ActorArgs& a, uint64_t seed, uint64_t ctr, int e) {
+  const u32x4 r = philox(seed ^ 0xA5A5A5A5ull, ctr, (uint32_t)e, 1u);
+  return u01(r.w) < a.p_done;
+}
+
+// Whole actor step for all E envs inside ONE workgroup; q = [E][A] (LDS or global, visible
+// to every thread on entry). No barrier inside: every thread re-derives the envs' episode
+// ends from the rng instead of waiting on the deciding threads, so the replay / frame
+// stores are never waited for (a __syncthreads would drain them, ~us per barrier).
+DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, int* /*s_done*/, const ActorPre& p) {
   const int tid = threadIdx.x, nth = blockDim.x;
-  const int64_t t0 = a.cursor[0], f0 = a.cursor[1], size0 = a.cursor[2];
-  const float eps0 = a.eps[0], eps_min = a.eps[1], decay = a.eps[2];
-  const uint64_t seed = (uint64_t)a.rng[0], ctr = (uint64_t)a.rng[1];
-  __syncthreads();
   for (int e = tid; e < a.E; e += nth) {
     int fs, rs;
-    s_done[e] = actor_env_step(a, q + e * a.A, e, t0, f0, eps0, eps_min, decay, seed, ctr, fs, rs);
+    actor_env_step(a, q + e * a.A, e, p.t0, p.f0, p.eps0, p.eps_min, p.decay, p.seed, p.ctr, fs, rs,
+                   e == tid ? p.st : nullptr);
   }
-  __syncthreads();
   for (int e = 0; e < a.E; ++e) {
-    const int fslot = (int)((f0 + 2 * e) % a.F), rslot = (int)((f0 + 2 * e + 1) % a.F);
-    write_random_frame(a.frames + (int64_t)fslot * a.HW, a.HW, seed, ctr, 0x100u + 2u * e, tid, nth);
-    if (s_done[e]) write_random_frame(a.frames + (int64_t)rslot * a.HW, a.HW, seed, ctr, 0x101u + 2u * e, tid, nth);
+    const int fslot = (int)((p.f0 + 2 * e) % a.F), rslot = (int)((p.f0 + 2 * e + 1) % a.F);
+    write_random_frame(a.frames + (int64_t)fslot * a.HW, a.HW, p.seed, p.ctr, 0x100u + 2u * e, tid, nth);
+    if (actor_done(a, p.seed, p.ctr, e))
+      write_random_frame(a.frames + (int64_t)rslot * a.HW, a.HW, p.seed, p.ctr, 0x101u + 2u * e, tid, nth);
   }
-  __syncthreads();
-  if (tid == 0) actor_advance(a, t0, f0, size0, eps0, eps_min, decay, ctr);
+  if (tid == 0) actor_advance(a, p.t0, p.f0, p.size0, p.eps0, p.eps_min, p.decay, p.ctr, p.frames_done);
+}
+
+DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, int* s_done) {
+  actor_step_block(a, q, s_done, actor_prefetch(a));
 }
 
 }  // namespace dqn

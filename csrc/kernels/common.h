@@ -7,6 +7,7 @@
 #include "../include/dqn_act.h"
 
 #define DQN_DEV __device__ __forceinline__
+#define DQN_DEV_HOST_INLINE __host__ __device__ inline
 
 // Device-side bounds checks of the debug build (DQN_DEBUG=1 python setup.py build_ext):
 // a failing check traps the kernel with file:line; compiled out of the release build.

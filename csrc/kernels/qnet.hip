@@ -445,28 +445,57 @@ __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
 // head_body: one workgroup's share (blk of nblk) of the head. B / h0 / infer / actor /
 // q_out / zeroing are parameters so the fused-acting block can run the acting path
 // on the actors' hidden layer inside the learner's launch.
+constexpr int kHeadPartFloats = 16 * 64 * 4;
+constexpr int kHeadActorScratch = 64;          // actor LDS scratch after red[32] (E <= 64)
+constexpr int kHeadMaxA = 32;                  // output biases staged in LDS up to this many actions
 DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h0, const bool infer,
                        const bool has_actor, float* q_out, const bool do_zero, const int blk, const int nblk) {
   const int A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
-  float* q = hsm;                           // [3][B][A]
+  float* part_lds = hsm;                    // [16 waves][64][4] split-K partial Q tiles
+  float* q = hsm + kHeadPartFloats;         // [3][B][A]
   float* vv = q + 3 * B * A;                // [3][B] dueling value stream
   float* dq = vv + 3 * B;                   // [B][A]  dL/dQ (dueling: dL/dA)
   float* dv = dq + B * A;                   // [B]     dueling: dL/dV
-  float* red = dv + B;                      // [32]
+  float* red = dv + B;                      // [32] (+ actor scratch)
+  float* bl = red + 32 + kHeadActorScratch; // [3][A] output bias, [3] value bias (A <= kHeadMaxA)
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
   const int ninst = infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
   auto hptr = [&](int inst) { return inst == 0 && h0 != nullptr ? h0 : a.h[inst]; };
-  // ---- 0. zero the gradient range the conv wgrads accumulate into (nothing in
-  //         this kernel touches it; saves a separate fill launch)
-  if (do_zero && a.zero_ptr != nullptr) {
-    float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
-    for (int t = blk * nth + tid; t < a.zero_n / 4; t += nblk * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // phase stamps (scripts/probe_head.py): learner block 0 -> prof[0..7], acting block -> prof[16..19]
+  int64_t* prof = (a.prof != nullptr && tid == 0 && blk == 0) ? a.prof + (infer && has_actor ? 16 : 0) : nullptr;
+#define HEAD_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
+  HEAD_MARK(0);
+  ActorPre apre{};
+  if (infer && has_actor) apre = actor_prefetch(a.actor);   // loads overlap the Q tiles
+  float tr = 0.f, tg = 0.f, td = 0.f, tw = 1.f;              // this thread's sample (TD loss)
+  int ta = 0;
+  if (!infer && tid < B) {
+    tr = a.rew[tid]; tg = a.gam[tid]; td = a.done[tid]; ta = a.act[tid];
+    if (a.wts != nullptr) tw = a.wts[tid];
   }
+  // Small operands of the later phases are loaded NOW, so their latency hides under the
+  // Q-tile loads: the TD-loss inputs (registers) and the output biases (LDS). (The dW / dH
+  // operands are NOT: their ~50 loads per thread would queue ahead of the Q-tile loads.)
+  const bool bias_lds = A <= kHeadMaxA;
+  if (bias_lds) {
+    for (int t = tid; t < ninst * A; t += nth) bl[t] = a.b[t / A][t % A];
+    if (a.dueling && tid < ninst) bl[3 * kHeadMaxA + tid] = a.bv[tid][0];
+  }
+  const int gt = blk * nth + tid, gn = nblk * nth;
+  const act_t* hb0 = reinterpret_cast<const act_t*>(a.h[0]);
+  const act_t* ha0 = a.dueling ? hb0 + HID : hb0;
+  const float* W0 = a.w[0];
   // ---- 1. Q tiles on MFMA: task = (instance, 16-row tile, n-tile); the dueling value
-  // stream is one extra n-tile, so every tile's loads run on their own wave
+  // stream is one extra n-tile. The K loop of every task is split over kspl waves (all
+  // waves busy, one batch of loads in flight per wave); partial tiles meet in LDS.
   const int mtiles = (B + 15) / 16, K32 = HID / 32, ntl = a.N16 + (a.dueling ? 1 : 0);
-  for (int task = wave; task < ninst * mtiles * ntl; task += nwave) {
+  const int ntask = ninst * mtiles * ntl;
+  int kspl = nwave / ntask;
+  kspl = kspl < 1 ? 1 : (kspl > K32 ? K32 : kspl);
+  const int kps = (K32 + kspl - 1) / kspl;                 // k-steps per wave part
+  for (int wt = wave; wt < ntask * kspl; wt += nwave) {
+    const int task = wt / kspl, part = wt - task * kspl;
     const int nt = task % ntl, im = task / ntl;
     const int inst = im / mtiles, mt = im - inst * mtiles;
     const int b_row = mt * 16 + (lane & 15);
@@ -476,34 +505,62 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
     const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
     const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
     const int kg = 8 * (lane >> 4);
-    {
-      const bool val = nt == a.N16;
-      const act_t* src = val ? hrow : ha;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int ks = 0; ks < K32; ks += 8) {          // 8 k-steps of loads in flight per batch
-        bfx8 af[8], bf[8];
+    const bool val = nt == a.N16;
+    const act_t* src = val ? hrow : ha;
+    const int k_lo = part * kps, k_hi = min(K32, k_lo + kps);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = k_lo; ks < k_hi; ks += 4) {            // 4 k-steps of loads in flight per batch
+      bfx8 af[4], bf[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const bool kok = ks + u < K32;
-          af[u] = rok && kok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : zero8();
-          bf[u] = !kok ? zero8() : val ? pv[(ks + u) * 64 + lane] : pw[((ks + u) * a.N16 + nt) * 64 + lane];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = mfma16(af[u], bf[u], acc);
+      for (int u = 0; u < 4; ++u) {
+        const bool kok = ks + u < k_hi;
+        af[u] = rok && kok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : zero8();
+        bf[u] = !kok ? zero8() : val ? pv[(ks + u) * 64 + lane] : pw[((ks + u) * a.N16 + nt) * 64 + lane];
       }
-      const int act = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = mfma16(af[u], bf[u], acc);
+    }
+    if (kspl > 1) {
+      *reinterpret_cast<f32x4*>(part_lds + (wt * 64 + lane) * 4) = acc;
+      continue;
+    }
+    const int act = nt * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = mt * 16 + 4 * (lane >> 4) + r;
+      if (val) {
+        if ((lane & 15) == 0 && b < B) vv[inst * B + b] = acc[r] + a.bv[inst][0];
+      } else if (b < B && act < A) {
+        q[(inst * B + b) * A + act] = acc[r] + a.b[inst][act];
+      }
+    }
+  }
+  if (kspl > 1) {                                          // (the bias LDS is written before this barrier)                                          // sum the parts of every task
+    __syncthreads();
+    for (int t = tid; t < ntask * 64; t += nth) {
+      const int task = t >> 6, ln = t & 63;
+      const int nt = task % ntl, im = task / ntl;
+      const int inst = im / mtiles, mt = im - inst * mtiles;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < kspl; ++p) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(part_lds + ((task * kspl + p) * 64 + ln) * 4);
+        acc += v;
+      }
+      const bool val = nt == a.N16;
+      const int act = nt * 16 + (ln & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = mt * 16 + 4 * (lane >> 4) + r;
+        const int b = mt * 16 + 4 * (ln >> 4) + r;
         if (val) {
-          if ((lane & 15) == 0 && b < B) vv[inst * B + b] = acc[r] + a.bv[inst][0];
+          if ((ln & 15) == 0 && b < B) vv[inst * B + b] = acc[r] + (bias_lds ? bl[3 * kHeadMaxA + inst] : a.bv[inst][0]);
         } else if (b < B && act < A) {
-          q[(inst * B + b) * A + act] = acc[r] + a.b[inst][act];
+          q[(inst * B + b) * A + act] = acc[r] + (bias_lds ? bl[inst * A + act] : a.b[inst][act]);
         }
       }
     }
   }
   __syncthreads();
+  HEAD_MARK(1);
   if (a.dueling) {
     for (int t = tid; t < ninst * B; t += nth) {
       float mean = 0.f;
@@ -517,7 +574,9 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
   if (infer) {                              // acting: Q of instance 0 only
     if (q_out != nullptr)
       for (int t = tid; t < B * A; t += nth) q_out[t] = q[t];
-    if (has_actor) actor_step_block(a.actor, q, reinterpret_cast<int*>(red + 32));
+    HEAD_MARK(2);
+    if (has_actor) actor_step_block(a.actor, q, reinterpret_cast<int*>(red + 32), apre);
+    HEAD_MARK(3);
     return;
   }
   // ---- 2. TD loss (one thread per sample)
@@ -529,10 +588,10 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
     float bvv = sel[0];
     for (int i = 1; i < A; ++i) if (sel[i] > bvv) { bvv = sel[i]; best = i; }
     const float nxt = q[(B + b) * A + best];
-    const float y = a.rew[b] + a.gam[b] * (1.f - a.done[b]) * nxt;
-    const int at = a.act[b];
+    const float y = tr + tg * (1.f - td) * nxt;
+    const int at = ta;
     const float d = q[b * A + at] - y;
-    const float w = a.wts != nullptr ? a.wts[b] : 1.f;
+    const float w = tw;
     float per, dper;
     if (a.huber) {
       const float ad = fabsf(d);
@@ -564,13 +623,10 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
     for (int i = 0; i < nwave; ++i) s += red[i];
     a.loss[0] = s / (float)B;
   }
+  HEAD_MARK(2);
   // ---- 3. head backward (online instance 0 only), partitioned over the grid's
   // blocks (phases 1-2 above are recomputed by every block: cheap MFMA work);
   // k fastest across threads -> coalesced H reads
-  const int gt = blk * nth + tid, gn = nblk * nth;
-  const act_t* hb0 = reinterpret_cast<const act_t*>(a.h[0]);
-  const act_t* ha0 = a.dueling ? hb0 + HID : hb0;
-  const float* W0 = a.w[0];
   act_t* dh = reinterpret_cast<act_t*>(a.dh);
   for (int t = gt; t < HID * A; t += gn) {              // dW[k][i] = sum_b Ha[b][k] dA[b][i]
     const int i = t / HID, k = t - i * HID;
@@ -595,19 +651,30 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
       a.dbv[0] = s;
     }
   }
+  HEAD_MARK(3);
   // dH[b][k] = (sum_i dA[b][i] W[k][i]) * (H > 0);   dueling value half: dV[b] * wv[k]
+  const float* Wd = W0;                                 // output W [HID][A]
+  const float* wvd = a.wv[0];
   for (int t = gt; t < B * HH; t += gn) {
     const int b = t / HH, k = t - b * HH;
     float s = 0.f;
     if (a.dueling && k < HID) {
-      s = dv[b] * a.wv[0][k];
+      s = dv[b] * wvd[k];
     } else {
       const int kk = a.dueling ? k - HID : k;
-      for (int i = 0; i < A; ++i) s += dq[b * A + i] * W0[(int64_t)kk * A + i];
+      for (int i = 0; i < A; ++i) s += dq[b * A + i] * Wd[kk * A + i];
     }
     const float hval = (float)hb0[t];
     dh[t] = (act_t)(hval > 0.f ? s * kLossScale : 0.f);   // scaled: see dqn_act.h
   }
+  // ---- 4. zero the gradient range the conv wgrads accumulate into (nothing in this
+  //         kernel touches it; saves a fill launch). Last, so no barrier waits on it.
+  if (do_zero && a.zero_ptr != nullptr) {
+    float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
+    for (int t = blk * nth + tid; t < a.zero_n / 4; t += nblk * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  HEAD_MARK(4);
+#undef HEAD_MARK
 }
 
 __global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
@@ -743,8 +810,14 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(4 * a.B * a.A + 4 * a.B + 32 + (a.has_actor || a.act_E > 0 ? a.actor.E : 0)) *
-                     sizeof(float);
+  const size_t lds = (size_t)(kHeadPartFloats + 4 * a.B * a.A + 4 * a.B + 32 + kHeadActorScratch +
+                              4 * kHeadMaxA) * sizeof(float);
+  static size_t lds_set = 64 * 1024;          // dynamic LDS above 64 KB must be opted into
+  if (lds > lds_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_loss_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    lds_set = lds;
+  }
   // training: 8 blocks share the backward (+1 fused acting block); acting (infer): one block
   hipLaunchKernelGGL(head_loss_kernel, dim3(a.infer ? 1 : 8 + (a.act_E > 0 ? 1 : 0)), dim3(1024), lds, st, a);
 }

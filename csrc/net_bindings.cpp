@@ -107,6 +107,7 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
     x.F = (int)actor[20]; x.gamma = (float)actor_f[0]; x.p_done = (float)actor_f[1];
     TORCH_CHECK(x.A == a.A, "actor action count");
     TORCH_CHECK(x.F >= 2 * x.C + x.K, "frame ring must hold 2C + k frames");
+    TORCH_CHECK(x.K >= 1 && x.K <= 4 && x.E >= 1 && x.E <= 64, "fused actor: 1 <= K <= 4, 1 <= E <= 64");
     if (a.infer) {                 // acting launch: the batch IS the env batch
       TORCH_CHECK(x.E == a.B, "actor env batch must be the inference batch");
       a.has_actor = 1;
@@ -186,9 +187,10 @@ void cnn_bwd(std::vector<int64_t> ptrs, int64_t B) {
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
                std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
                std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
-               std::vector<int64_t> actor, std::vector<double> actor_f, int64_t act_h) {
+               std::vector<int64_t> actor, std::vector<double> actor_f, int64_t act_h, int64_t prof) {
   TORCH_CHECK(flts.size() == 1, "flts = [huber delta]");
   dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h);
+  a.prof = P<int64_t*>(prof);
   a.delta = (float)flts[0];
   launch_head_loss(a, cur_stream());
 }
@@ -265,7 +267,7 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_head_loss", &head_loss, pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"), pybind11::arg("io"),
         pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),
-        pybind11::arg("actor_f"), pybind11::arg("act_h") = 0);
+        pybind11::arg("actor_f"), pybind11::arg("act_h") = 0, pybind11::arg("prof") = 0);
   m.def("qnet_wgrad_group", &wgrad_group);
   m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
         pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{});

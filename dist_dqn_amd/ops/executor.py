@@ -101,7 +101,7 @@ class HipExecutor:
         import os
         self.opt_max_grid = int(os.environ.get('DQN_OPT_GRID', '2048'))
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
-        self.head_prof = None       # int64 [16] C51 head phase stamps (scripts/probe_c51.py)
+        self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_c51.py, probe_head.py)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -568,7 +568,9 @@ class HipExecutor:
             self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
                                    wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl)
         else:
-            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h)
+            prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
+            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h,
+                                    prof)
 
     def q_values(self, flat: torch.Tensor, x: torch.Tensor, noise=None) -> torch.Tensor:
         """Q [B, A] (C51: expected value of the return distribution)."""
