@@ -102,6 +102,9 @@ def test_xgmi_allreduce_two_ranks_one_gpu(wire):
     _run_ranks(_worker_xgmi, (wire,))
 
 
+RAINBOW_DP = '--distributional --noisy --dueling --double_dqn --optimizer=adam --lr=0.0000625'
+
+
 def _worker(rank, world, port, network, extra, errq):
     try:
         _setup(rank, world, port)
@@ -157,7 +160,12 @@ def _worker(rank, world, port, network, extra, errq):
                                            ('nature', '--allreduce=xgmi'),
                                            ('nature', '--allreduce=xgmi --dueling --double_dqn --loss=huber'),
                                            ('atari', '--allreduce=xgmi'),
-                                           ('nature', '--allreduce=xgmi --allreduce_dtype=bf16')])
+                                           ('nature', '--allreduce=xgmi --allreduce_dtype=bf16'),
+                                           # Rainbow minus PER: noisy sigma gradients are derived in the
+                                           # optimizer from the all-reduced mu gradients under the
+                                           # rank-shared noise stream, so replicas stay bit-identical
+                                           ('nature', '--allreduce=rccl ' + RAINBOW_DP),
+                                           ('nature', '--allreduce=xgmi ' + RAINBOW_DP)])
 def test_dp_learner_two_ranks_one_gpu(network, extra):
     """(--allreduce=rccl means the process group's collective: gloo in this rehearsal.)"""
     _run_ranks(_worker, (network, extra))
