@@ -112,6 +112,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t)
     loss = float(learner.loss)
+    xgmi_ok = learner.reducer.xgmi.check() if learner.reducer.xgmi is not None else True
     if ctx.rank == 0:
         sps = args.steps * ctx.world_size / el
         frames = (args.actor_envs * max(1, args.update_freq // args.actor_envs)) * args.steps * ctx.world_size / el
@@ -125,14 +126,16 @@ def main():
             'config': {'model': 'nature-cnn' if args.network == 'nature' else args.network,
                        'global_batch': args.batch * ctx.world_size, 'seq_len': None,
                        'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
-                       'frames_per_state': 4, 'optimizer': 'rmsprop(tf)', 'executor': net.executor.name,
+                       'frames_per_state': 4, 'optimizer': cfg.optimizer + '(tf)', 'executor': net.executor.name,
                        'hip_graph': bool(args.graph), 'actor_envs': args.actor_envs,
                        'acting': 'fused into the learner launches' if fused else 'separate launches',
                        'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
                        'num_actions': args.actions, 'variant': args.variant, 'extra': args.extra,
                        'final_loss': loss,
                        'allreduce': learner.reducer.mode if ctx.enabled else None,
-                       'allreduce_probe_us': learner.reducer.timings or None},
+                       'allreduce_probe_us': learner.reducer.timings or None,
+                       'allreduce_peer_timeouts': not xgmi_ok,
+                       'sampling': learner._sample_mode()},
         }
         print(json.dumps(out), flush=True)
     if ctx.enabled:

@@ -11,6 +11,7 @@
 #include "include/dqn_host.h"
 #include "include/dqn_kernels.h"
 #include "include/dqn_nets.h"
+#include "include/dqn_nets_k.h"
 
 namespace {
 
@@ -145,7 +146,9 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 torch::Tensor packed, c10::optional<torch::Tensor> target, c10::optional<torch::Tensor> target_packed,
                 int64_t target_freq, int64_t max_grid, c10::optional<torch::Tensor> noise,
                 c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
-                c10::optional<torch::Tensor> noise_dst) {
+                c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample) {
+  // sample: [] or 16 pointers (TrunkSample order) + B: an extra block draws the next step's
+  // uniform minibatch (frame-stacked replay, k = 4)
   // grad_noise: derive the sigma gradients from the mu gradients under that noise sample;
   // noise_dst: the last block copies `noise` there (next sample becomes the current one)
   // op -1: no optimizer update, only the (noisy) mix + pack of w (noise / eff given)
@@ -195,13 +198,29 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
     ndst = ptr<float>(*noise_dst);
     nn = (int)noise_dst->numel();
   }
+  dqn::TrunkSample smp{};
+  if (!sample.empty()) {
+    TORCH_CHECK(op >= 0 && sample.size() == 17, "optim_pack sample: 16 pointers + B (update calls only)");
+    for (int i = 0; i < 16; ++i) TORCH_CHECK(sample[i] != 0, "optim_pack sample: null pointer");
+    smp.size = P<const int32_t*>(sample[0]); smp.rng = P<int64_t*>(sample[1]); smp.ticket = P<int32_t*>(sample[2]);
+    smp.state_idx = P<const int32_t*>(sample[3]); smp.next_idx = P<const int32_t*>(sample[4]);
+    smp.actions = P<const int32_t*>(sample[5]); smp.rewards = P<const float*>(sample[6]);
+    smp.dones = P<const float*>(sample[7]); smp.gammas = P<const float*>(sample[8]);
+    smp.idx_out = P<int32_t*>(sample[9]); smp.a_out = P<int32_t*>(sample[10]); smp.r_out = P<float*>(sample[11]);
+    smp.d_out = P<float*>(sample[12]); smp.g_out = P<float*>(sample[13]);
+    smp.st_slots = P<int32_t*>(sample[14]); smp.nx_slots = P<int32_t*>(sample[15]);
+    smp.B = (int)sample[16];
+    smp.ninst = 0;
+    TORCH_CHECK(smp.B >= 1 && smp.B <= 512, "optim_pack sample: 1 <= B <= 512 (one lane per sample)");
+  }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
   launch_optim_pack((int)op, ptr<float>(w), ptr<float>(grad), ptr<float>(s0), ptr<float>(s1), ptr<float>(beta_pow),
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
-                    tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, cur_stream());
+                    tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
+                    cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {

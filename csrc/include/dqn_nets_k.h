@@ -105,6 +105,19 @@ struct NoisyJob {
 };
 
 // Fused per-sample Nature trunk (trunk.hip): conv1 -> conv2 -> conv3 in one launch.
+// Fused uniform sampling inside the trunk launch (size == nullptr: off). Every sampled
+// workgroup re-derives the batch (sample_dev.h), takes its own transition's frame slots,
+// instance 0 writes the per-sample outputs the head / wgrad read, and the last workgroup
+// to arrive (ticket) advances the rng counter.
+struct TrunkSample {
+  const int32_t* size; int64_t* rng; int32_t* ticket;
+  const int32_t* state_idx; const int32_t* next_idx;            // replay [C][4], [C]
+  const int32_t* actions; const float* rewards; const float* dones; const float* gammas;
+  int32_t* idx_out; int32_t* a_out; float* r_out; float* d_out; float* g_out;
+  int32_t* st_slots; int32_t* nx_slots;                          // [B][4]
+  int B, ninst;                    // samples drawn; leading instances that use them
+};
+
 struct TrunkArgs {
   const uint8_t* frames;           // frame ring [F][84*84] (slot path)
   const int32_t* slots[kMaxInst];  // [B][4] frame slots per instance (or nullptr -> states)
@@ -115,6 +128,7 @@ struct TrunkArgs {
   int M[kMaxInst];                 // valid samples per instance (the fused actor's E < B)
   float scale;                     // input scale folded into conv1
   int64_t* prof;                   // optional [ninst][B][8] s_memtime phase stamps (profiling)
+  TrunkSample smp;                 // fused sampling (smp.size == nullptr: use `slots`)
 };
 
 // Reference `cnn` (SAME convs + 2x2 max-pools), per-sample fused kernels (cnn.hip).

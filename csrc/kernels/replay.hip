@@ -9,6 +9,8 @@
 #include "common.h"
 #include "../include/dqn_kernels.h"
 
+#include "sample_dev.h"
+
 namespace dqn {
 
 DQN_DEV void write_sample_outputs(const SampleOut& so, int i, int tr) {
@@ -29,65 +31,12 @@ DQN_DEV void write_sample_outputs(const SampleOut& so, int i, int tr) {
 __global__ void __launch_bounds__(1024)
 sample_uniform_kernel(const int32_t* __restrict__ size_p, int64_t* __restrict__ rng,
                       int32_t* __restrict__ out, int B, SampleOut so) {
-  __shared__ int32_t cand[1024];
-  __shared__ int any_dup;
+  __shared__ SampleLds sl;
   const int i = threadIdx.x;
   const uint32_t n = (uint32_t)max(size_p[0], 1);
   const uint64_t seed = (uint64_t)rng[0];
   const uint64_t ctr = (uint64_t)rng[1];
-  uint32_t attempt = 0;
-  auto draw = [&]() -> int32_t {
-    u32x4 r = philox(seed, ctr, (uint32_t)i, attempt++);
-    return (int32_t)(((uint64_t)r.x * n) >> 32);
-  };
-  int32_t v = (i < B) ? draw() : -1;
-  const bool distinct_possible = n >= (uint32_t)B;
-  for (int round = 0; round < 64; ++round) {
-    if (i < 1024) cand[i] = v;
-    if (i == 0) any_dup = 0;
-    __syncthreads();
-    bool dup = false;
-    if (i < B && distinct_possible) {
-      for (int j = 0; j < i; ++j) dup |= (cand[j] == v);
-    }
-    if (dup) any_dup = 1;
-    __syncthreads();
-    if (!any_dup) break;
-    if (dup) v = draw();
-    __syncthreads();
-  }
-  // Rejection stalls when B is close to n (coupon collector): resolve what is
-  // left serially with an LDS bitmap (only reachable for small n).
-  __shared__ uint32_t used[2048];                  // 65536 bits
-  __shared__ int fix_needed;
-  if (i == 0) fix_needed = 0;
-  if (i < 1024) cand[i] = v;
-  __syncthreads();
-  bool dup = false;
-  if (i < B && distinct_possible) {
-    for (int j = 0; j < i; ++j) dup |= (cand[j] == v);
-    if (dup) fix_needed = 1;
-  }
-  __syncthreads();
-  if (fix_needed && n <= 65536u) {
-    for (int w = i; w < 2048; w += blockDim.x) used[w] = 0;
-    __syncthreads();
-    if (i < B && !dup) atomicOr(&used[v >> 5], 1u << (v & 31));
-    __syncthreads();
-    if (i == 0) {
-      for (int j = 0; j < B; ++j) {
-        bool dj = false;
-        for (int q = 0; q < j; ++q) dj |= (cand[q] == cand[j]);
-        if (!dj) continue;
-        uint32_t c = (uint32_t)cand[j];
-        while (used[c >> 5] & (1u << (c & 31))) c = (c + 1) % n;
-        used[c >> 5] |= 1u << (c & 31);
-        cand[j] = (int32_t)c;
-      }
-    }
-    __syncthreads();
-    if (i < B) v = cand[i];
-  }
+  const int32_t v = draw_distinct(seed, ctr, n, B, sl);
   if (i < B) {
     DQN_ASSERT(v >= 0 && (uint32_t)v < n);
     out[i] = v;

@@ -18,6 +18,7 @@
 // Everything is v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
 #include "common.h"
 #include "fused_util.h"
+#include "sample_dev.h"
 #include "../include/dqn_nets_k.h"
 
 namespace dqn {
@@ -39,6 +40,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   act_t* act2 = xin;
   float* red = reinterpret_cast<float*>(xin + 6144);   // conv3 k-half partials, after act2 (R2 * L2 = 5832)
   static_assert(R2 * L2 <= 6144 && 6144 * 2 + 4 * 4 * 1024 <= HW * 8, "act2 + partials fit xin");
+  static_assert(sizeof(SampleLds) <= HW * 8, "sampler scratch fits xin");
   const int b = blockIdx.x, inst = blockIdx.y;
   if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -47,13 +49,40 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
 #define TRUNK_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
   TRUNK_MARK(0);
 
+  // ---------------------------------------------------------------- fused sampling
+  // (the sampler launch folded in: xin is dead until the frames land, so it holds the
+  // sampler's LDS scratch; every sampled workgroup draws the same batch)
+  const bool sampled = a.smp.size != nullptr && inst < a.smp.ninst;
+  int4 sl_s = make_int4(0, 0, 0, 0);
+  if (sampled) {
+    SampleLds& sls = *reinterpret_cast<SampleLds*>(xin);
+    const uint32_t n = (uint32_t)max(a.smp.size[0], 1);
+    const uint64_t seed = (uint64_t)a.smp.rng[0], ctr = (uint64_t)a.smp.rng[1];
+    draw_distinct(seed, ctr, n, a.smp.B, sls);
+    const int32_t tr = sls.cand[b];
+    __syncthreads();                                    // every lane has its index before xin is reused
+    DQN_ASSERT(tr >= 0 && (uint32_t)tr < n);
+    const int4 st = reinterpret_cast<const int4*>(a.smp.state_idx)[tr];
+    const int32_t nx = a.smp.next_idx[tr];
+    sl_s = inst == 0 ? st : make_int4(st.y, st.z, st.w, nx);
+    if (tid == 0) {
+      if (inst == 0) write_sample_slots(a.smp, b, tr, st, nx);
+      // relaxed ticket (as optim.hip): every workgroup read the counter before its add
+      const int t = __hip_atomic_fetch_add(a.smp.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == a.smp.B * a.smp.ninst - 1) {
+        a.smp.rng[1] = (int64_t)(ctr + 1);
+        __hip_atomic_store(a.smp.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+
   // ---------------------------------------------------------------- input loads (first)
   // 1764 tasks of 4 pixels; a thread owns tasks tid + 512 j (j < 4)
   constexpr int NT = HW / 4;
   uint32_t in[4][4];
-  const bool slot_path = a.slots[inst] != nullptr;
+  const bool slot_path = sampled || a.slots[inst] != nullptr;
   if (slot_path) {
-    const int4 sl = reinterpret_cast<const int4*>(a.slots[inst])[b];
+    const int4 sl = sampled ? sl_s : reinterpret_cast<const int4*>(a.slots[inst])[b];
     const uint32_t* f0 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW);
     const uint32_t* f1 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW);
     const uint32_t* f2 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.z * HW);

@@ -229,7 +229,7 @@ void noisy_grad(int64_t grad, int64_t noise, int64_t jobs, int64_t njobs, int64_
 // ptrs per instance (4 entries each, 0 = absent): slots, states, w1, w2, w3, b1, b2, b3, x1, x2, x3;
 // M: valid samples per instance (empty = all B)
 void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale, int64_t prof,
-           std::vector<int64_t> M) {
+           std::vector<int64_t> M, std::vector<int64_t> sample) {
   constexpr int I = dqn::kMaxInst;
   TORCH_CHECK(ptrs.size() == 11 * I && ninst >= 1 && ninst <= I && B >= 1 && M.size() <= (size_t)I, "trunk args");
   dqn::TrunkArgs a{};
@@ -251,6 +251,25 @@ void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, 
   }
   a.scale = (float)scale;
   a.prof = P<int64_t*>(prof);
+  // sample: [] or 16 pointers (TrunkSample order) + ninst_sampled; the replay must be
+  // frame-stacked with k = 4 (int4 slot rows)
+  if (!sample.empty()) {
+    TORCH_CHECK(sample.size() == 17, "trunk sample: 16 pointers + sampled instances");
+    for (int i = 0; i < 16; ++i) TORCH_CHECK(sample[i] != 0, "trunk sample: null pointer");
+    dqn::TrunkSample& s = a.smp;
+    s.size = P<const int32_t*>(sample[0]); s.rng = P<int64_t*>(sample[1]); s.ticket = P<int32_t*>(sample[2]);
+    s.state_idx = P<const int32_t*>(sample[3]); s.next_idx = P<const int32_t*>(sample[4]);
+    s.actions = P<const int32_t*>(sample[5]); s.rewards = P<const float*>(sample[6]);
+    s.dones = P<const float*>(sample[7]); s.gammas = P<const float*>(sample[8]);
+    s.idx_out = P<int32_t*>(sample[9]); s.a_out = P<int32_t*>(sample[10]); s.r_out = P<float*>(sample[11]);
+    s.d_out = P<float*>(sample[12]); s.g_out = P<float*>(sample[13]);
+    s.st_slots = P<int32_t*>(sample[14]); s.nx_slots = P<int32_t*>(sample[15]);
+    s.B = (int)B;
+    s.ninst = (int)sample[16];
+    TORCH_CHECK(B >= 1 && B <= 512 && s.ninst >= 1 && s.ninst <= ninst && a.frames != nullptr,
+                "trunk sample: 1 <= B <= 512 (one lane per sample), sampled instances <= ninst");
+    for (int i = 0; i < s.ninst; ++i) TORCH_CHECK(a.M[i] == 0 || a.M[i] == B, "sampled instances use all B");
+  }
   launch_trunk_fwd(a, (int)B, (int)ninst, cur_stream());
 }
 
@@ -259,7 +278,7 @@ void trunk(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, 
 void register_net_ops(pybind11::module_& m) {
   m.def("qnet_trunk", &trunk, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
         pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("prof") = 0,
-        pybind11::arg("M") = std::vector<int64_t>{});
+        pybind11::arg("M") = std::vector<int64_t>{}, pybind11::arg("sample") = std::vector<int64_t>{});
   m.def("qnet_pack", &pack, pybind11::arg("src"), pybind11::arg("dst"), pybind11::arg("jobs"), pybind11::arg("njobs"),
         pybind11::arg("max_threads"), pybind11::arg("dst2") = 0, pybind11::arg("step") = 0, pybind11::arg("freq") = 1);
   m.def("qnet_igemm", &igemm);

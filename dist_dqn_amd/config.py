@@ -145,6 +145,9 @@ def build_parser() -> argparse.ArgumentParser:
     a('--overlap_allreduce', default=1, type=int,
       help='DP: all-reduce the dense-layer gradients while the conv backward runs (two collectives)')
     a('--hip_graph', default=1, type=int, help='Capture the learner step in a HIP graph')
+    a('--fuse_sampling', default=2, type=int, choices=[0, 1, 2],
+      help='Uniform GPU replay: 0 = sampler launch per step, 1 = the Nature trunk draws the minibatch, '
+           '2 = the previous step\'s optimizer launch draws it (one extra block, off the critical path)')
     a('--checkpoint_secs', default=600, type=int)
     a('--max_to_keep', default=5, type=int)
     a('--save_agent_state', action='store_true', help='Checkpoint epsilon/step sidecar')
@@ -224,6 +227,7 @@ class Config:
     grad_bucket_mb: float = 64.0
     overlap_allreduce: int = 1
     hip_graph: int = 1
+    fuse_sampling: int = 2
     checkpoint_secs: int = 600
     max_to_keep: int = 5
     save_agent_state: bool = False

@@ -69,6 +69,7 @@ class Learner:
         self._split = bool(self.ctx.enabled and ps_client is None and getattr(config, 'overlap_allreduce', True))
         self._dense_hi = network.dense_range()[1] if self._split else 0
         self._ar_stream = None
+        self._presampled = False    # this step's minibatch was drawn by the last optimizer launch
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -80,8 +81,15 @@ class Learner:
             beta = (self.net.global_step, self.config.per_beta0, self.config.per_beta_steps)
         if (getattr(self.net.executor, 'consumes_slots', False) and getattr(r, 'frame_mode', False)
                 and self.device.type == 'cuda'):
-            # one launch: indices + scalars + frame-slot tables; conv1 reads the ring
-            batch = r.sample_slots(self.B, beta)
+            # one launch: indices + scalars + frame-slot tables; conv1 reads the ring. Uniform
+            # replay: usually no launch at all — the previous step's optimizer launch drew this
+            # batch ('opt'), or the Nature trunk draws it ('trunk')
+            mode = self._sample_mode()
+            if mode == 'opt' and self._presampled:
+                batch = r.sample_slots(self.B, beta, defer=True)
+                batch.pop('sample_spec', None)
+            else:
+                batch = r.sample_slots(self.B, beta, defer=mode == 'trunk')
             self.idx = batch['idx']
         else:
             if per:
@@ -106,6 +114,19 @@ class Learner:
         self.loss = loss.view(1)
         self.prio = prio.view(-1)
 
+    def _sample_mode(self) -> str:
+        """Where the uniform minibatch is drawn: 'opt' (an extra block of the previous step's
+        optimizer launch), 'trunk' (the Nature trunk launch) or 'launch' (a sampler launch)."""
+        r = self.replay
+        fs = int(getattr(self.config, 'fuse_sampling', 2))
+        if getattr(r, 'prioritized', False) or not getattr(r, 'can_defer_sampling', lambda: False)():
+            return 'launch'
+        if fs >= 2 and self.ps is None and self.net.fuses_update(self._target_freq()):
+            return 'opt'
+        if fs >= 1 and getattr(self.net.executor, 'fused_sampling', False):
+            return 'trunk'
+        return 'launch'
+
     def _target_freq(self):
         """target_freq argument of apply_grads: the hard sync rides in the optimizer launch."""
         return self.config.target_update_freq if self.tau >= 1.0 else None
@@ -114,7 +135,12 @@ class Learner:
         cfg = self.config
         hard = self.tau >= 1.0
         # hard target sync folded into the optimizer + repack launches when the backend can
-        fused = self.net.apply_grads(self.reducer.scale, target_freq=self._target_freq())
+        # (and, 'opt' sampling, the NEXT step's minibatch drawn by one extra block of it)
+        nxt = None
+        if self._sample_mode() == 'opt':
+            nxt = (self.replay.sample_slots(self.B, None, defer=True)['sample_spec'], self.B)
+        fused = self.net.apply_grads(self.reducer.scale, target_freq=self._target_freq(), next_sample=nxt)
+        self._presampled = nxt is not None and fused
         if getattr(self.replay, 'prioritized', False):
             self.replay.update_priorities(self.idx, self.prio, cfg.per_eps)
         # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).

@@ -135,6 +135,13 @@ class Network:
         if self.noise is not None and not self._premixed:
             self.reset_noise()
 
+    def fuses_update(self, target_freq: Optional[int]) -> bool:
+        """True when ``apply_grads(.., target_freq)`` is ONE optimizer+pack launch (which can
+        also draw the next uniform minibatch, ``next_sample``)."""
+        ex = self.executor
+        return (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
+                and hasattr(ex, 'update_and_pack') and (self._premixed or not getattr(ex, 'noisy', False)))
+
     def fuses_sigma_grads(self, target_freq: Optional[int]) -> bool:
         """True when ``apply_grads(.., target_freq)`` runs the fused noisy optimizer, which
         derives dL/dsigma itself (so ``compute_grads(sigma_grads=False)`` may skip it)."""
@@ -175,13 +182,14 @@ class Network:
                 break
         return 0, end
 
-    def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None) -> bool:
+    def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None, next_sample=None) -> bool:
         """Optimizer step (global_step += 1 inside it) + executor repack.
 
         target_freq: also do the hard target sync (target <- online when the new
         global_step % target_freq == 0, device predicate) inside those same two
         launches. Returns True when it was fused that way; otherwise the caller
-        still owes the target update (``hard_target_update``)."""
+        still owes the target update (``hard_target_update``). next_sample: ``(spec, B)`` — the
+        fused launch also draws the next uniform minibatch (only honoured when it returns True)."""
         ex = self.executor
         fuse = (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
                 and hasattr(ex, 'packed'))
@@ -195,8 +203,9 @@ class Network:
                 self.executor.draw_noise(self.noise_next, self.noise_target, self.noise_rng)
                 kw.update(noise=self.noise_next, grad_noise=self.noise, noise_dst=self.noise)
             ex.update_and_pack(self.optimizer, self.online.flat, self.grad, grad_scale, self.global_step,
-                               target=self.target.flat, target_freq=int(target_freq), **kw)
+                               target=self.target.flat, target_freq=int(target_freq), next_sample=next_sample, **kw)
             return True
+        assert next_sample is None or not fuse, 'next_sample needs the fused optimizer+pack launch'
         if fuse:
             self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,
                                 target=self.target.flat, target_freq=int(target_freq))

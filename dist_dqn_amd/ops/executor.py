@@ -239,7 +239,7 @@ class HipExecutor:
             noise = d[3]
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
-                            self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None)
+                            self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [])
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
@@ -258,14 +258,16 @@ class HipExecutor:
     def update_and_pack(self, opt, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float,
                         global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1,
                         noise: Optional[torch.Tensor] = None, grad_noise: Optional[torch.Tensor] = None,
-                        noise_dst: Optional[torch.Tensor] = None):
+                        noise_dst: Optional[torch.Tensor] = None, next_sample=None):
         """Optimizer step + repack in ONE launch (+ the hard target sync under the device
         predicate when ``target`` is given). Noisy nets: ``noise`` (the next sample for this
         flat) is mixed in and bound (see ``premix``); the target's packed copy is not written
         (the target is re-mixed under its own noise every step). ``grad_noise``: derive the
         sigma gradients from the mu-slot gradients under that sample (the one the forward
         used) instead of reading them; ``noise_dst``: the kernel's last block copies ``noise``
-        there, and ``noise_dst`` becomes the bound noise. Returns True."""
+        there, and ``noise_dst`` becomes the bound noise. ``next_sample``: ``(spec, B)`` of
+        ``DeviceReplay.sample_slots(defer=True)`` — one extra block of this launch draws the
+        next step's uniform minibatch. Returns True."""
         from ..optim import OPT_IDS
         dev = flat.device
         jobs = self._upd_jobs(dev)
@@ -288,7 +290,8 @@ class HipExecutor:
                             [float(hp['momentum']), float(hp['rho']), float(hp['rms_mom']), float(hp['rms_eps']),
                              float(hp['b1']), float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']),
                              float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq), self.opt_max_grid,
-                            noise, eff, grad_noise, noise_dst)
+                            noise, eff, grad_noise, noise_dst,
+                            list(next_sample[0]) + [int(next_sample[1])] if next_sample is not None else [])
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
         return True
@@ -460,9 +463,15 @@ class HipExecutor:
         return ws
 
     # ------------------------------------------------------------ forward
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=()):
+    @property
+    def fused_sampling(self) -> bool:
+        """The fused trunk can draw the uniform minibatch itself (replay.sample_slots(defer))."""
+        return self.fused_trunk
+
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=(), sample=None):
         """conv1..fc for `ninst` instances -> ws['h'] (M: valid rows per instance, e.g. the
-        fused actor instance's E < B).
+        fused actor instance's E < B). sample: (spec pointers, sampled instances) — the
+        trunk draws the uniform batch itself (the slot tables of those instances are outputs).
 
         xs: uint8 NHWC [B, 84, 84, 4] inputs, or (frames given) int32 [B, 4] slot
         tables into the frame ring ``frames`` [F, 84, 84] (fused gather)."""
@@ -483,8 +492,9 @@ class HipExecutor:
                     + pad([rows(ws['x1'], 0)] if keep_acts else []) + pad([rows(ws['x2'], 0)] if keep_acts else [])
                     + pad([rows(ws['x3'], i) for i in range(ninst)]))
             prof = self.trunk_prof.data_ptr() if self.trunk_prof is not None else 0
+            smp = list(sample[0]) + [int(sample[1])] if sample is not None else []
             ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale, prof,
-                           list(M))
+                           list(M), smp)
             self._fc_fwd(packs, ws, B, ninst)
             return
         d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
@@ -679,11 +689,15 @@ class HipExecutor:
             with torch.cuda.stream(side):
                 grad_out.zero_()
             ev_zero = self._event('zero', side)
+        spec = batch.get('sample_spec')
+        if spec is not None:
+            assert self.fused_trunk and frames is not None, 'deferred sampling needs the fused trunk'
+        sample = (spec, ninst) if spec is not None else None
         if acting is None:
-            self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames)
+            self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames, sample=sample)
         else:
             self._fwd_trunk(xs + [acting['stacks']], packs + [po], flats + [eo], ws, B, ninst + 1, frames=frames,
-                            M=[B] * ninst + [E])
+                            M=[B] * ninst + [E], sample=sample)
         if not zero_in_head:
             main.wait_event(ev_zero)
         zero = [grad_out.data_ptr() + 4 * conv_lo, conv_hi - conv_lo] if zero_in_head else []
@@ -810,6 +824,8 @@ class HipCnnExecutor(HipExecutor):
     backward (pool argmax routing + conv dgrads) kernels from csrc/kernels/cnn.hip,
     plus the shared fc / head / grouped-wgrad / optimizer / pack kernels."""
 
+    fused_sampling = False          # cnn.hip's forward reads sampler-made slot tables
+
     def _workspace(self, B: int, dev) -> dict:
         key = (B, dev.index if dev.index is not None else 0)
         ws = self._ws.get(key)
@@ -832,7 +848,8 @@ class HipCnnExecutor(HipExecutor):
         self._ws[key] = ws
         return ws
 
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=()):
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=(), sample=None):
+        assert sample is None, 'the cnn forward reads sampler-made slot tables'
         lay = self.layout
         pad = lambda v: list(v) + [0] * (4 - len(v))
         pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]

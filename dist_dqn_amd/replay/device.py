@@ -304,10 +304,15 @@ class DeviceReplay:
         self.tree.sample(self.rng_state, self.size_dev, beta, idx_out, w_out)
         return idx_out, w_out
 
-    def sample_slots(self, batch_size: int, beta: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    def sample_slots(self, batch_size: int, beta: Optional[torch.Tensor] = None,
+                     defer: bool = False) -> Dict[str, torch.Tensor]:
         """GPU fast path: ONE sampling launch returns indices, per-sample scalars and the
         frame-slot tables of s and s' ([B, k] int32) — executors that read the frame ring
-        directly (the HIP executor's conv1) never materialise the uint8 stacks."""
+        directly (the HIP executor's conv1) never materialise the uint8 stacks.
+
+        defer=True (uniform, k = 4): NO launch; the returned buffers are filled by the
+        consumer's first kernel instead (the Nature trunk draws the batch itself, see
+        csrc/kernels/sample_dev.h): ``out['sample_spec']`` holds the pointers it needs."""
         assert self.frame_mode and self.device.type == 'cuda'
         B = batch_size
         if not hasattr(self, '_slot_bufs'):
@@ -322,6 +327,16 @@ class DeviceReplay:
                    'dones': torch.zeros(B, **f32), 'gammas': torch.zeros(B, **f32),
                    'state_slots': torch.zeros(B, self.k, **i32), 'next_slots': torch.zeros(B, self.k, **i32)}
             self._slot_bufs[B] = buf
+        if defer and self.can_defer_sampling():
+            if getattr(self, '_sample_ticket', None) is None:
+                self._sample_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+            out = {k: buf[k] for k in ('idx', 'actions', 'rewards', 'dones', 'gammas', 'state_slots', 'next_slots')}
+            out['frames'] = self.frames
+            out['sample_spec'] = [t.data_ptr() for t in (
+                self.size_dev, self.rng_state, self._sample_ticket, self.state_idx, self.next_idx, self.actions,
+                self.rewards, self.dones, self.gammas, buf['idx'], buf['actions'], buf['rewards'], buf['dones'],
+                buf['gammas'], buf['state_slots'], buf['next_slots'])]
+            return out
         so = [self.state_idx, self.next_idx, self.actions, self.rewards, self.dones, self.gammas,
               buf['actions'], buf['rewards'], buf['dones'], buf['gammas'], buf['state_slots'], buf['next_slots']]
         if self.prioritized:
@@ -334,6 +349,10 @@ class DeviceReplay:
         if self.prioritized:
             out['weights'] = buf['weights']
         return out
+
+    def can_defer_sampling(self) -> bool:
+        """Uniform frame-stacked (k = 4) GPU replay: a consumer kernel may draw the batch."""
+        return self.frame_mode and self.device.type == 'cuda' and not self.prioritized and self.k == 4
 
     def update_priorities(self, idx: torch.Tensor, td_abs: torch.Tensor, eps: float = 1e-6):
         self.tree.update(idx, td_abs, self.alpha, eps)

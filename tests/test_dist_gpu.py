@@ -132,6 +132,8 @@ def _worker(rank, world, port, network, extra, errq):
                 ln.step()
             torch.cuda.synchronize()
             assert torch.isfinite(ln.loss).all()
+            if ln.reducer.xgmi is not None:
+                ln.reducer.check()                          # a timed-out peer wait raises here
             assert check_replicas_equal(ctx, net.online.flat), 'replicas diverged (overlap=%d)' % overlap
             assert int(net.global_step) == 6
             xgmi = '--allreduce=xgmi' in extra
