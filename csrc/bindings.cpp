@@ -146,7 +146,11 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 torch::Tensor packed, c10::optional<torch::Tensor> target, c10::optional<torch::Tensor> target_packed,
                 int64_t target_freq, int64_t max_grid, c10::optional<torch::Tensor> noise,
                 c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
-                c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample) {
+                c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
+                std::vector<double> per_f) {
+  // per_p: [] or [sum, min, max_p, P, levels, upd_idx, upd_td, rng, size, step, idx_out, w_out,
+  //   state_idx, next_idx, actions, rewards, dones, gammas, a_out, r_out, d_out, g_out, st_slots,
+  //   nx_slots, B] ; per_f: [alpha, eps, beta0, beta_steps] — prioritized variant of `sample`
   // sample: [] or 16 pointers (TrunkSample order) + B: an extra block draws the next step's
   // uniform minibatch (frame-stacked replay, k = 4)
   // grad_noise: derive the sigma gradients from the mu gradients under that noise sample;
@@ -213,6 +217,28 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
     smp.ninst = 0;
     TORCH_CHECK(smp.B >= 1 && smp.B <= 512, "optim_pack sample: 1 <= B <= 512 (one lane per sample)");
   }
+  PerStep per{};
+  if (!per_p.empty()) {
+    TORCH_CHECK(op >= 0 && sample.empty() && per_p.size() == 25 && per_f.size() == 4,
+                "optim_pack per: 25 ints + 4 floats (update calls only, not with a uniform sample)");
+    for (int i : {0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23})
+      TORCH_CHECK(per_p[i] != 0, "optim_pack per: null pointer ", i);
+    per.sum = P<float*>(per_p[0]); per.mn = P<float*>(per_p[1]); per.maxp = P<float*>(per_p[2]);
+    per.P = (int)per_p[3]; per.levels = (int)per_p[4];
+    per.upd_idx = P<const int32_t*>(per_p[5]); per.upd_td = P<const float*>(per_p[6]);
+    per.rng = P<int64_t*>(per_p[7]); per.size = P<const int32_t*>(per_p[8]); per.step = P<const int64_t*>(per_p[9]);
+    per.idx_out = P<int32_t*>(per_p[10]); per.w_out = P<float*>(per_p[11]);
+    per.so = SampleOut{P<const int32_t*>(per_p[12]), P<const int32_t*>(per_p[13]), 4, P<const int32_t*>(per_p[14]),
+                       P<const float*>(per_p[15]), P<const float*>(per_p[16]), P<const float*>(per_p[17]),
+                       P<int32_t*>(per_p[18]), P<float*>(per_p[19]), P<float*>(per_p[20]), P<float*>(per_p[21]),
+                       P<int32_t*>(per_p[22]), P<int32_t*>(per_p[23])};
+    per.B = (int)per_p[24];
+    per.alpha = (float)per_f[0]; per.eps = (float)per_f[1]; per.beta0 = (float)per_f[2];
+    per.beta_steps = (float)per_f[3];
+    TORCH_CHECK(per.B >= 1 && per.B <= 64 && per.P >= 2 && (per.P & (per.P - 1)) == 0 &&
+                (1 << per.levels) == per.P && per.levels <= 30 && per.beta_steps >= 1.f,
+                "optim_pack per: 1 <= B <= 64 (one-wave tree update), P = 2^levels, beta_steps >= 1");
+  }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
@@ -220,7 +246,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
-                    cur_stream());
+                    per_p.empty() ? nullptr : &per, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {

@@ -14,6 +14,15 @@ struct SampleOut {
   int32_t* a_out; float* r_out; float* d_out; float* g_out;
   int32_t* st_slots; int32_t* nx_slots;
 };
+// Prioritized replay inside the optimizer launch's extra block (optim.hip): update the
+// priorities of this step's batch, then draw the next step's prioritized sample.
+struct PerStep {
+  float* sum; float* mn; float* maxp; int P, levels;
+  const int32_t* upd_idx; const float* upd_td; float alpha, eps;   // this step's batch / |TD|
+  int64_t* rng; const int32_t* size; const int64_t* step;          // next sample: rng, replay size, global_step
+  float beta0, beta_steps;
+  int32_t* idx_out; float* w_out; SampleOut so; int B;
+};
 void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, const SampleOut& so,
                                   hipStream_t st);
 struct GatherScalars {   // optional per-sample scalar gather (a_out == nullptr: skip)
@@ -35,7 +44,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
-                       const dqn::TrunkSample* smp, hipStream_t st);
+                       const dqn::TrunkSample* smp, const PerStep* per, hipStream_t st);
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
 void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();

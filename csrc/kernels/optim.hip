@@ -12,6 +12,7 @@
 // ticket), together with global_step, so no extra launch is needed.
 #include "common.h"
 #include "sample_dev.h"
+#include "sumtree_dev.h"
 #include "../include/dqn_kernels.h"
 
 namespace dqn {
@@ -191,13 +192,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
                   act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
-                  int noise_n, TrunkSample smp) {
+                  int noise_n, TrunkSample smp, PerStep per) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
   // noise on every DP rank makes that exact for the all-reduced sum), instead of being read.
   // noise_dst: the grid's last block copies noise[0, noise_n) there (next sample -> current).
-  // smp.size != nullptr: the grid's extra LAST block draws the NEXT step's uniform minibatch
+  // smp.size != nullptr: the grid's extra block (block 0) draws the NEXT step's uniform minibatch
   // (sample_dev.h) while the others update: the replay is quiet during this launch, and
   // the sampler leaves the next step's critical path.
   constexpr bool UPD = OP >= 0;
@@ -205,8 +206,12 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   __shared__ __attribute__((aligned(16))) unsigned char smem[sizeof(SampleLds) > kTileBytes ? sizeof(SampleLds)
                                                                                            : kTileBytes];
   act_t* tile = reinterpret_cast<act_t*>(smem);
-  const bool sampler = smp.size != nullptr && blockIdx.x == gridDim.x - 1;
-  const int nwork = (int)gridDim.x - (smp.size != nullptr ? 1 : 0);
+  static_assert(sizeof(SumtreeLds) <= sizeof(smem), "sum-tree scratch fits");
+  const bool extra = smp.size != nullptr || per.sum != nullptr;   // the grid has a sampler block
+  // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
+  const bool sampler = extra && blockIdx.x == 0;
+  const int nwork = (int)gridDim.x - (extra ? 1 : 0);
+  const int wid = (int)blockIdx.x - (extra ? 1 : 0);      // work index of an update block
   float lr_t = h.lr;
   if constexpr (OP == 3) {
     const float b1p = beta_pow[0], b2p = beta_pow[1];
@@ -217,7 +222,23 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6;
   constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
-  if (sampler) {
+  if (sampler && per.sum != nullptr) {
+    // prioritized: this step's priorities into the tree (one wave), then the next step's
+    // stratified sample from the updated tree (beta of the NEXT global_step)
+    const int64_t step0 = per.step[0];                  // read before this block's ticket add
+    const uint64_t seed = (uint64_t)per.rng[0], ctr = (uint64_t)per.rng[1];
+    SumtreeLds& L = *reinterpret_cast<SumtreeLds*>(smem);
+    sumtree_update_wave(per.sum, per.mn, per.maxp, per.upd_idx, per.upd_td, per.alpha, per.eps, 0, per.B, per.P,
+                        per.levels, L);
+    __syncthreads();                                    // tree writes visible to every lane of the block
+    if ((int)threadIdx.x < per.B) {
+      const float beta = fminf(1.f, per.beta0 + (1.f - per.beta0) * (float)(step0 + 1) / per.beta_steps);
+      per_sample_lane(per.sum, per.mn, seed, ctr, per.size[0], threadIdx.x, per.B, per.P, beta, per.idx_out,
+                      per.w_out, per.so);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) per.rng[1] = (int64_t)(ctr + 1);
+  } else if (sampler) {
     SampleLds& sls = *reinterpret_cast<SampleLds*>(smem);
     const uint32_t n = (uint32_t)max(smp.size[0], 1);
     const uint64_t seed = (uint64_t)smp.rng[0], ctr = (uint64_t)smp.rng[1];
@@ -228,7 +249,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     if (threadIdx.x == 0) smp.rng[1] = (int64_t)(ctr + 1);   // every lane read it before the barriers
   }
-  for (int ji = sampler ? njobs : (int)blockIdx.x; ji < njobs; ji += nwork) {
+  for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) {
     const UpdJob jb = jobs[ji];
     const bool elem = jb.kind == 1;
     const bool noisy = jb.sig_off >= 0;
@@ -447,7 +468,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
-                       int noise_n, const TrunkSample* smp, hipStream_t st) {
+                       int noise_n, const TrunkSample* smp, const PerStep* per, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
@@ -456,14 +477,15 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   // larger: one block per job (up to max_grid) with the two-level ticket
   const int cap = max_grid > 256 ? max_grid : 256;
   const TrunkSample sm = smp != nullptr ? *smp : TrunkSample{};
-  const int grid = (njobs < cap ? njobs : cap) + (sm.size != nullptr ? 1 : 0);   // + the sampler block
+  const PerStep pe = per != nullptr ? *per : PerStep{};
+  const int grid = (njobs < cap ? njobs : cap) + (sm.size != nullptr || pe.sum != nullptr ? 1 : 0);   // + sampler
   const int hier = grid > 256 ? 1 : 0;
   const UpdJob* J = reinterpret_cast<const UpdJob*>(jobs);
   act_t* P = reinterpret_cast<act_t*>(packed);
   act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
   const int tf = tfreq < 1 ? 1 : tfreq;
 #define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
-                                  ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm)
+                                  ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe)
   switch (op) {
     case -1: OPK(-1); break;
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;

@@ -86,8 +86,7 @@ class Learner:
             # batch ('opt'), or the Nature trunk draws it ('trunk')
             mode = self._sample_mode()
             if mode == 'opt' and self._presampled:
-                batch = r.sample_slots(self.B, beta, defer=True)
-                batch.pop('sample_spec', None)
+                batch = r.slot_batch(self.B)
             else:
                 batch = r.sample_slots(self.B, beta, defer=mode == 'trunk')
             self.idx = batch['idx']
@@ -119,10 +118,12 @@ class Learner:
         optimizer launch), 'trunk' (the Nature trunk launch) or 'launch' (a sampler launch)."""
         r = self.replay
         fs = int(getattr(self.config, 'fuse_sampling', 2))
+        if (fs >= 2 and self.ps is None and getattr(r, 'can_fuse_sampling', lambda B: False)(self.B)
+                and getattr(self.net.executor, 'consumes_slots', False)
+                and self.net.fuses_update(self._target_freq())):
+            return 'opt'            # (prioritized too: priority update + sample in that block)
         if getattr(r, 'prioritized', False) or not getattr(r, 'can_defer_sampling', lambda: False)():
             return 'launch'
-        if fs >= 2 and self.ps is None and self.net.fuses_update(self._target_freq()):
-            return 'opt'
         if fs >= 1 and getattr(self.net.executor, 'fused_sampling', False):
             return 'trunk'
         return 'launch'
@@ -137,11 +138,14 @@ class Learner:
         # hard target sync folded into the optimizer + repack launches when the backend can
         # (and, 'opt' sampling, the NEXT step's minibatch drawn by one extra block of it)
         nxt = None
+        per = getattr(self.replay, 'prioritized', False)
         if self._sample_mode() == 'opt':
-            nxt = (self.replay.sample_slots(self.B, None, defer=True)['sample_spec'], self.B)
+            nxt = self.replay.next_sample_spec(
+                self.B, per=(self.idx, self.prio, self.net.global_step, cfg.per_eps, cfg.per_beta0,
+                             cfg.per_beta_steps) if per else None)
         fused = self.net.apply_grads(self.reducer.scale, target_freq=self._target_freq(), next_sample=nxt)
         self._presampled = nxt is not None and fused
-        if getattr(self.replay, 'prioritized', False):
+        if per and not self._presampled:
             self.replay.update_priorities(self.idx, self.prio, cfg.per_eps)
         # hard copy when global_step % target_update_freq == 0 (device predicate, no sync).
         # Under sync DP every rank's online params are bit-identical, so the local

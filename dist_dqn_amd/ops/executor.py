@@ -239,7 +239,8 @@ class HipExecutor:
             noise = d[3]
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
-                            self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [])
+                            self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [], [],
+                            [])
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
@@ -265,9 +266,10 @@ class HipExecutor:
         (the target is re-mixed under its own noise every step). ``grad_noise``: derive the
         sigma gradients from the mu-slot gradients under that sample (the one the forward
         used) instead of reading them; ``noise_dst``: the kernel's last block copies ``noise``
-        there, and ``noise_dst`` becomes the bound noise. ``next_sample``: ``(spec, B)`` of
-        ``DeviceReplay.sample_slots(defer=True)`` — one extra block of this launch draws the
-        next step's uniform minibatch. Returns True."""
+        there, and ``noise_dst`` becomes the bound noise. ``next_sample``: a
+        ``DeviceReplay.next_sample_spec`` dict — one extra block of this launch draws the next
+        step's minibatch (uniform, or prioritized after writing this step's priorities).
+        Returns True."""
         from ..optim import OPT_IDS
         dev = flat.device
         jobs = self._upd_jobs(dev)
@@ -291,7 +293,10 @@ class HipExecutor:
                              float(hp['b1']), float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']),
                              float(hp['ad_eps'])], jobs, p, target, pt, int(target_freq), self.opt_max_grid,
                             noise, eff, grad_noise, noise_dst,
-                            list(next_sample[0]) + [int(next_sample[1])] if next_sample is not None else [])
+                            (list(next_sample['spec']) + [int(next_sample['B'])]
+                             if next_sample is not None and next_sample['kind'] == 'uniform' else []),
+                            (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
+                            (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []))
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
         return True

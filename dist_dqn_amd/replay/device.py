@@ -315,18 +315,7 @@ class DeviceReplay:
         csrc/kernels/sample_dev.h): ``out['sample_spec']`` holds the pointers it needs."""
         assert self.frame_mode and self.device.type == 'cuda'
         B = batch_size
-        if not hasattr(self, '_slot_bufs'):
-            self._slot_bufs = {}
-        buf = self._slot_bufs.get(B)
-        if buf is None:
-            dev = self.device
-            i32 = dict(dtype=torch.int32, device=dev)
-            f32 = dict(dtype=torch.float32, device=dev)
-            buf = {'idx': torch.zeros(B, **i32), 'weights': torch.ones(B, **f32),
-                   'actions': torch.zeros(B, **i32), 'rewards': torch.zeros(B, **f32),
-                   'dones': torch.zeros(B, **f32), 'gammas': torch.zeros(B, **f32),
-                   'state_slots': torch.zeros(B, self.k, **i32), 'next_slots': torch.zeros(B, self.k, **i32)}
-            self._slot_bufs[B] = buf
+        buf = self._slot_buffers(B)
         if defer and self.can_defer_sampling():
             if getattr(self, '_sample_ticket', None) is None:
                 self._sample_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -349,6 +338,60 @@ class DeviceReplay:
         if self.prioritized:
             out['weights'] = buf['weights']
         return out
+
+    def _slot_buffers(self, B: int) -> dict:
+        if not hasattr(self, '_slot_bufs'):
+            self._slot_bufs = {}
+        buf = self._slot_bufs.get(B)
+        if buf is None:
+            dev = self.device
+            i32 = dict(dtype=torch.int32, device=dev)
+            f32 = dict(dtype=torch.float32, device=dev)
+            buf = {'idx': torch.zeros(B, **i32), 'weights': torch.ones(B, **f32),
+                   'actions': torch.zeros(B, **i32), 'rewards': torch.zeros(B, **f32),
+                   'dones': torch.zeros(B, **f32), 'gammas': torch.zeros(B, **f32),
+                   'state_slots': torch.zeros(B, self.k, **i32), 'next_slots': torch.zeros(B, self.k, **i32)}
+            self._slot_bufs[B] = buf
+        return buf
+
+    def slot_batch(self, B: int) -> Dict[str, torch.Tensor]:
+        """The minibatch buffers as they are (no launch): a batch some earlier kernel drew
+        (the optimizer launch's sampler block, see ``next_sample_spec``)."""
+        buf = self._slot_buffers(B)
+        out = {k: buf[k] for k in ('idx', 'actions', 'rewards', 'dones', 'gammas', 'state_slots', 'next_slots')}
+        out['frames'] = self.frames
+        if self.prioritized:
+            out['weights'] = buf['weights']
+        return out
+
+    def can_fuse_sampling(self, B: int) -> bool:
+        """The next minibatch can be drawn by an extra block of the optimizer launch."""
+        ok = self.frame_mode and self.device.type == 'cuda' and self.k == 4 and 1 <= B <= 512
+        return ok and (not self.prioritized or B <= 64)
+
+    def next_sample_spec(self, B: int, per=None) -> dict:
+        """Arguments of the optimizer launch's sampler block (csrc/kernels/optim.hip): it draws
+        the NEXT minibatch into ``slot_batch(B)``'s buffers. per (prioritized replay):
+        (upd_idx, upd_td, global_step, per_eps, beta0, beta_steps) — the block first writes
+        this step's priorities |td| of upd_idx into the sum-tree, then samples from it."""
+        buf = self._slot_buffers(B)
+        if not self.prioritized:
+            if getattr(self, '_sample_ticket', None) is None:
+                self._sample_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+            return {'kind': 'uniform', 'B': B, 'spec': [t.data_ptr() for t in (
+                self.size_dev, self.rng_state, self._sample_ticket, self.state_idx, self.next_idx, self.actions,
+                self.rewards, self.dones, self.gammas, buf['idx'], buf['actions'], buf['rewards'], buf['dones'],
+                buf['gammas'], buf['state_slots'], buf['next_slots'])]}
+        upd_idx, upd_td, step, eps, beta0, beta_steps = per
+        t = self.tree
+        levels = t.P.bit_length() - 1
+        ptr = lambda x: x.data_ptr()
+        p = [ptr(t.sum), ptr(t.min), ptr(t.max_p), t.P, levels, ptr(upd_idx), ptr(upd_td), ptr(self.rng_state),
+             ptr(self.size_dev), ptr(step), ptr(buf['idx']), ptr(buf['weights']), ptr(self.state_idx),
+             ptr(self.next_idx), ptr(self.actions), ptr(self.rewards), ptr(self.dones), ptr(self.gammas),
+             ptr(buf['actions']), ptr(buf['rewards']), ptr(buf['dones']), ptr(buf['gammas']),
+             ptr(buf['state_slots']), ptr(buf['next_slots']), B]
+        return {'kind': 'per', 'p': p, 'f': [float(self.alpha), float(eps), float(beta0), float(max(1, beta_steps))]}
 
     def can_defer_sampling(self) -> bool:
         """Uniform frame-stacked (k = 4) GPU replay: a consumer kernel may draw the batch."""

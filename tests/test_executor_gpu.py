@@ -431,3 +431,42 @@ def test_fused_sampling_equals_sampler_launch(extra, acting):
     assert torch.equal(s0, s1) and torch.equal(s0, s2)
     torch.testing.assert_close(f0, f1, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(f0, f2, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('extra', ['--prioritized_replay --double_dqn --dueling',
+                                   '--prioritized_replay ' + RAINBOW + ' --optimizer=adam'])
+def test_per_fused_in_optimizer_equals_separate_launches(extra):
+    """Prioritized replay with --fuse_sampling=2: the optimizer launch's extra block writes
+    this step's priorities into the sum-tree (one wave) and draws the next prioritized batch
+    == the separate sumtree_set / sumtree_sample launches (same tree, same IS weights, same
+    parameters)."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    outs = []
+    for fuse in (0, 2):
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 '
+                     '--fuse_sampling=%d %s' % (fuse, extra))
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)
+        rep.fill_synthetic(4096, 6, seed=5)
+        ln = Learner(net, rep, cfg, use_graph=True)
+        assert ln._sample_mode() == ('opt' if fuse == 2 else 'launch')
+        for _ in range(6):
+            ln.step()
+        torch.cuda.synchronize()
+        if fuse == 0:      # the fused run has already drawn step 7's batch: draw it here too
+            rep.sample_slots(32, (net.global_step, cfg.per_beta0, cfg.per_beta_steps))
+        else:
+            assert ln._presampled
+        torch.cuda.synchronize()
+        b = rep.slot_batch(32)
+        outs.append((net.online.flat.clone(), rep.tree.sum.clone(), rep.tree.min.clone(), rep.rng_state.clone(),
+                     b['idx'].clone(), b['weights'].clone()))
+    (f0, s0, m0, r0, i0, w0), (f1, s1, m1, r1, i1, w1) = outs
+    assert torch.equal(r0, r1) and torch.equal(i0, i1)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(w1, w0, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(f1, f0, rtol=1e-4, atol=1e-6)
