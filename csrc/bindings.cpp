@@ -147,7 +147,9 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 int64_t target_freq, int64_t max_grid, c10::optional<torch::Tensor> noise,
                 c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
-                std::vector<double> per_f) {
+                std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
+                c10::optional<torch::Tensor> tpk) {
+  // tnoise / teff / tpk (noisy nets): mix + pack the target under tnoise in the same launch
   // per_p: [] or [sum, min, max_p, P, levels, upd_idx, upd_td, rng, size, step, idx_out, w_out,
   //   state_idx, next_idx, actions, rewards, dones, gammas, a_out, r_out, d_out, g_out, st_slots,
   //   nx_slots, B] ; per_f: [alpha, eps, beta0, beta_steps] — prioritized variant of `sample`
@@ -239,6 +241,22 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 (1 << per.levels) == per.P && per.levels <= 30 && per.beta_steps >= 1.f,
                 "optim_pack per: 1 <= B <= 64 (one-wave tree update), P = 2^levels, beta_steps >= 1");
   }
+  const float* tnz = nullptr;
+  float* tef = nullptr;
+  void* tpkp = nullptr;
+  if (tnoise.has_value() && tnoise->defined()) {
+    CHECK_T((*tnoise), torch::kFloat32);
+    TORCH_CHECK(op >= 0 && tgt != nullptr && nz != nullptr && tnoise->numel() == noise->numel() &&
+                teff.has_value() && teff->defined() && tpk.has_value() && tpk->defined(),
+                "optim_pack: target mix needs target, noise, teff, tpk");
+    CHECK_T((*teff), torch::kFloat32);
+    CHECK_T((*tpk), DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
+    TORCH_CHECK(teff->numel() == w.numel() && tpk->numel() == packed.numel() && tpk->data_ptr() != packed.data_ptr(),
+                "optim_pack: teff / tpk sizes");
+    tnz = ptr<float>(*tnoise);
+    tef = ptr<float>(*teff);
+    tpkp = tpk->data_ptr();
+  }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
@@ -246,7 +264,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
-                    per_p.empty() ? nullptr : &per, cur_stream());
+                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {

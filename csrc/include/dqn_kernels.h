@@ -44,7 +44,8 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
-                       const dqn::TrunkSample* smp, const PerStep* per, hipStream_t st);
+                       const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
+                       hipStream_t st);
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
 void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();

@@ -185,14 +185,15 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
   }
 }
 
-template <int OP>
+template <int OP, bool TMIX>
 __global__ void __launch_bounds__(kPackThreads)
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
                   act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
-                  int noise_n, TrunkSample smp, PerStep per) {
+                  int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
+                  float* __restrict__ teff, act_t* __restrict__ tpk) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
@@ -201,7 +202,11 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // smp.size != nullptr: the grid's extra block (block 0) draws the NEXT step's uniform minibatch
   // (sample_dev.h) while the others update: the replay is quiet during this launch, and
   // the sampler leaves the next step's critical path.
+  // tnoise (noisy nets, update calls): also mix + pack the TARGET under its next noise
+  // sample into teff / tpk (the target's eff / packed buffers): no separate target mix launch.
   constexpr bool UPD = OP >= 0;
+  // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
+  const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
   constexpr size_t kTileBytes = 32 * 72 * sizeof(act_t);
   __shared__ __attribute__((aligned(16))) unsigned char smem[sizeof(SampleLds) > kTileBytes ? sizeof(SampleLds)
                                                                                            : kTileBytes];
@@ -317,50 +322,79 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       for (int j = 0; j < 4; ++j)
         if (ok[j]) e[j] = w[j] + ws[j] * fin * fnz(noise[jb.eout_off + n + j]);
     }
+    // noisy nets, tmix: the TARGET's next effective weights under tnoise ride along (its
+    // fp32 mu / sigma, or this update's values when the hard sync copied them just now)
+    float te[4];
+    if (tmix) {
+      float tw[4], tws[4];
+      if (sync) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { tw[j] = w[j]; tws[j] = noisy ? ws[j] : 0.f; }
+      } else {
+        load4(tgt + e0, vec, ok, tw);
+        if (noisy) load4(tgt + s0i, vec, ok, tws);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) te[j] = tw[j];
+      if (noisy) {
+        const float fin = (!elem && jb.ein_off >= 0 && rowok) ? fnz(tnoise[jb.ein_off + k]) : 1.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (ok[j]) te[j] = tw[j] + tws[j] * fin * fnz(tnoise[jb.eout_off + n + j]);
+      }
+      if (jb.eff) store4(teff + e0, vec, ok, te);
+    }
     if (jb.eff) store4(eff + e0, vec, ok, e);
     if (elem) {
       if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
         float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
         float* tf = psync ? reinterpret_cast<float*>(tgt_packed + jb.fwd_off) + n : nullptr;
+        float* mf = tmix ? reinterpret_cast<float*>(tpk + jb.fwd_off) + n : nullptr;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (!ok[j]) continue;
           pf[j] = e[j];
           if (tf) tf[j] = e[j];
+          if (mf) mf[j] = te[j];
         }
       }
       continue;                    // uniform per block: no barrier below is skipped unevenly
     }
-    bfx4 v;
+    // bf16 fragments of this tile into dst (+ dst2): dgrad straight from the registers (4
+    // consecutive K' of one lane's slot), forward through an LDS transpose of the tile
+    auto emit = [&](const float* ev, act_t* dst, act_t* dst2) {
+      bfx4 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (act_t)(ok[j] ? e[j] : 0.f);
-    // dgrad fragments straight from the registers: 4 consecutive K' of one lane's slot
-    if (jb.dg_mode != 0 && rowok && n < jb.N) {
-      int kp, np;                                        // K' of the first of the 4 values, N'
-      if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
-      else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
-      const int lane = ((kp & 31) >> 3) * 16 + (np & 15);
-      const int64_t o = jb.dg_off + ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8
-                        + (kp & 7);
-      *reinterpret_cast<bfx4*>(packed + o) = v;
-      if (psync) *reinterpret_cast<bfx4*>(tgt_packed + o) = v;
-    }
-    // forward fragments through an LDS transpose of the bf16 tile
-    *reinterpret_cast<bfx4*>(tile + (t >> 4) * 72 + (t & 15) * 4) = v;
-    __syncthreads();
-    if (t < 256) {
-      const int nt = t >> 6, l = t & 63, nl = nt * 16 + (l & 15), kk = 8 * (l >> 4);
-      if (jb.n0 + nt * 16 < jb.N) {
-        bfx8 f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = tile[(kk + j) * 72 + nl];
-        const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
-                                                  ((jb.n0 >> 4) + nt)) * 64 + l) * 8;
-        *reinterpret_cast<bfx8*>(packed + o) = f;
-        if (psync) *reinterpret_cast<bfx8*>(tgt_packed + o) = f;
+      for (int j = 0; j < 4; ++j) v[j] = (act_t)(ok[j] ? ev[j] : 0.f);
+      if (jb.dg_mode != 0 && rowok && n < jb.N) {
+        int kp, np;                                        // K' of the first of the 4 values, N'
+        if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
+        else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
+        const int lane = ((kp & 31) >> 3) * 16 + (np & 15);
+        const int64_t o = jb.dg_off +
+                          ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8 +
+                          (kp & 7);
+        *reinterpret_cast<bfx4*>(dst + o) = v;
+        if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = v;
       }
-    }
-    __syncthreads();
+      *reinterpret_cast<bfx4*>(tile + (t >> 4) * 72 + (t & 15) * 4) = v;
+      __syncthreads();
+      if (t < 256) {
+        const int nt = t >> 6, l = t & 63, nl = nt * 16 + (l & 15), kk = 8 * (l >> 4);
+        if (jb.n0 + nt * 16 < jb.N) {
+          bfx8 f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = tile[(kk + j) * 72 + nl];
+          const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
+                                                    ((jb.n0 >> 4) + nt)) * 64 + l) * 8;
+          *reinterpret_cast<bfx8*>(dst + o) = f;
+          if (dst2) *reinterpret_cast<bfx8*>(dst2 + o) = f;
+        }
+      }
+      __syncthreads();
+    };
+    emit(e, packed, psync ? tgt_packed : nullptr);
+    if (tmix) emit(te, tpk, nullptr);
   }
   if (!UPD) return;
   __shared__ int s_last;
@@ -468,7 +502,8 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
-                       int noise_n, const TrunkSample* smp, const PerStep* per, hipStream_t st) {
+                       int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
+                       void* tpk, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
@@ -484,8 +519,14 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   act_t* P = reinterpret_cast<act_t*>(packed);
   act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
   const int tf = tfreq < 1 ? 1 : tfreq;
-#define OPK(N) hipLaunchKernelGGL(optim_pack_kernel<N>, dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
-                                  ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe)
+#define OPK(N) do { if (tnoise != nullptr) \
+    hipLaunchKernelGGL((optim_pack_kernel<N, true>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
+                       ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe, tnoise, \
+                       teff, reinterpret_cast<act_t*>(tpk)); \
+  else \
+    hipLaunchKernelGGL((optim_pack_kernel<N, false>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
+                       ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe, tnoise, \
+                       teff, reinterpret_cast<act_t*>(tpk)); } while (0)
   switch (op) {
     case -1: OPK(-1); break;
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;

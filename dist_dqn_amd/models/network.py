@@ -94,6 +94,7 @@ class Network:
                                           device=self.device)
             self.executor.draw_noise(self.noise, self.noise_target, self.noise_rng)
             self.executor.premix(self.online.flat, self.noise)
+            self.executor.premix(self.target.flat, self.noise_target)
 
     # -------------------------------------------------------------- factory
     @staticmethod
@@ -128,6 +129,7 @@ class Network:
             self.noise_target.normal_(generator=generator)
         if self._premixed:
             self.executor.premix(self.online.flat, self.noise)
+            self.executor.premix(self.target.flat, self.noise_target)
 
     def begin_step_noise(self):
         """Noise for one learner step. Premixed executors: nothing to do (both samples were
@@ -201,7 +203,8 @@ class Network:
                 # next online sample (+ the next step's target sample); the optimizer derives
                 # dL/dsigma under the current one, mixes the next one in and makes it current
                 self.executor.draw_noise(self.noise_next, self.noise_target, self.noise_rng)
-                kw.update(noise=self.noise_next, grad_noise=self.noise, noise_dst=self.noise)
+                kw.update(noise=self.noise_next, grad_noise=self.noise, noise_dst=self.noise,
+                          target_noise=self.noise_target)
             ex.update_and_pack(self.optimizer, self.online.flat, self.grad, grad_scale, self.global_step,
                                target=self.target.flat, target_freq=int(target_freq), next_sample=next_sample, **kw)
             return True
@@ -230,6 +233,8 @@ class Network:
             pt, po = ex.packed(self.target.flat), ex.packed(self.online.flat)
             kernels.target_update(self.target.flat, self.online.flat, 1.0, step, freq,
                                   extra=(pt.view(torch.float32), po.view(torch.float32)))
+            if self._premixed:              # noisy: the target's fragments follow its own noise
+                ex.premix(self.target.flat, self.noise_target)
         else:
             kernels.target_update(self.target.flat, self.online.flat, 1.0, step, freq)
 

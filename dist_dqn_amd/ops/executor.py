@@ -240,7 +240,7 @@ class HipExecutor:
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
                             self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [], [],
-                            [])
+                            [], None, None, None)
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
@@ -259,7 +259,8 @@ class HipExecutor:
     def update_and_pack(self, opt, flat: torch.Tensor, grad: torch.Tensor, grad_scale: float,
                         global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1,
                         noise: Optional[torch.Tensor] = None, grad_noise: Optional[torch.Tensor] = None,
-                        noise_dst: Optional[torch.Tensor] = None, next_sample=None):
+                        noise_dst: Optional[torch.Tensor] = None, next_sample=None,
+                        target_noise: Optional[torch.Tensor] = None):
         """Optimizer step + repack in ONE launch (+ the hard target sync under the device
         predicate when ``target`` is given). Noisy nets: ``noise`` (the next sample for this
         flat) is mixed in and bound (see ``premix``); the target's packed copy is not written
@@ -269,7 +270,8 @@ class HipExecutor:
         there, and ``noise_dst`` becomes the bound noise. ``next_sample``: a
         ``DeviceReplay.next_sample_spec`` dict — one extra block of this launch draws the next
         step's minibatch (uniform, or prioritized after writing this step's priorities).
-        Returns True."""
+        ``target_noise`` (noisy nets): the target is mixed + packed under it in the same launch
+        and bound to it (no target mix launch next step). Returns True."""
         from ..optim import OPT_IDS
         dev = flat.device
         jobs = self._upd_jobs(dev)
@@ -278,12 +280,16 @@ class HipExecutor:
         s1 = opt.slots[1] if len(opt.slots) > 1 else flat
         if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev or opt.ticket.numel() < 17 * 32:
             opt.ticket = torch.zeros(17 * 32, dtype=torch.int32, device=dev)   # 1 + 16 sub-tickets, 128 B apart
-        eff = None
+        eff = teff = tpk = None
         if self.noisy:
             assert noise is not None and noise.dtype == torch.float32
             k = flat.data_ptr()
             p, eff = self._packed_for(k, flat), self._eff_for(k, flat)
             pt = None
+            if target_noise is not None:
+                assert target is not None and target_noise.dtype == torch.float32
+                tk = target.data_ptr()
+                tpk, teff = self._packed_for(tk, target), self._eff_for(tk, target)
         else:
             p = self.packed(flat)
             pt = self.packed(target) if target is not None else None
@@ -296,9 +302,12 @@ class HipExecutor:
                             (list(next_sample['spec']) + [int(next_sample['B'])]
                              if next_sample is not None and next_sample['kind'] == 'uniform' else []),
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
-                            (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []))
+                            (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
+                            target_noise, teff, tpk)
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
+            if target_noise is not None:
+                self._bound[target.data_ptr()] = target_noise
         return True
 
     def _plan_noisy(self):
@@ -414,6 +423,10 @@ class HipExecutor:
                     step: Optional[torch.Tensor] = None, freq: int = 1):
         """Refresh the target's packed copy after a target update of the fp32 master."""
         from . import kernels
+        bound = self._bound.get(target.data_ptr()) if self.noisy else None
+        if bound is not None:               # noisy: re-mix the (possibly) new target under its noise
+            self.premix(target, bound)
+            return
         pt = self.packed(target)
         if tau >= 1.0:
             po = self.packed(online)
