@@ -70,6 +70,9 @@ struct ActorArgs {
   int64_t* frames_done;    // [1] env-frame counter
   int E, A, K, HW, C, F;
   float gamma, p_done;
+  // prioritized replay (tsum != nullptr): new transitions enter the sum-tree with the max priority
+  float* tsum; float* tmin; float* tmaxp;
+  int tP, tlevels;
 };
 
 struct HeadArgs {

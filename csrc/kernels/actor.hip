@@ -33,14 +33,22 @@ __global__ void __launch_bounds__(256) actor_step_kernel(ActorArgs a) {
   if (s_done)
     write_random_frame(a.frames + (int64_t)rslot * a.HW, a.HW, seed, ctr, 0x101u + 2u * e, threadIdx.x, blockDim.x);
   __syncthreads();
+  __shared__ int s_last;
   if (threadIdx.x == 0) {
     // relaxed ticket: the last block only writes the cursor/eps/rng words that
     // every block read at its start (see optim.hip for the same pattern)
     const int tk = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == (int)gridDim.x - 1) {
+    s_last = tk == (int)gridDim.x - 1 ? 1 : 0;
+    if (s_last) {
       actor_advance(a, t0, f0, size0, eps0, eps_min, decay, ctr);
       __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  if (a.tsum != nullptr) {           // PER: the last block inserts the E new transitions at max priority
+    __shared__ SumtreeLds L;
+    __syncthreads();
+    if (s_last) sumtree_update_wave(a.tsum, a.tmin, a.tmaxp, nullptr, nullptr, 0.f, 0.f, 1, a.E, a.tP, a.tlevels, L,
+                                    (int)(t0 % a.C), a.C);
   }
 }
 

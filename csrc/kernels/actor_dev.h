@@ -3,6 +3,7 @@
 // (qnet.hip: Q tile -> eps-greedy -> env step -> replay append in ONE launch).
 #pragma once
 #include "common.h"
+#include "sumtree_dev.h"
 #include "../include/dqn_nets_k.h"
 
 namespace dqn {
@@ -116,7 +117,8 @@ DQN_DEV bool actor_done(const ActorArgs& a, uint64_t seed, uint64_t ctr, int e) 
 // to every thread on entry). No barrier inside: every thread re-derives the envs' episode
 // ends from the rng instead of waiting on the deciding threads, so the replay / frame
 // stores are never waited for (a __syncthreads would drain them, ~us per barrier).
-DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, int* /*s_done*/, const ActorPre& p) {
+DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, void* lds_scratch, const ActorPre& p) {
+  // lds_scratch: >= sizeof(SumtreeLds) bytes of dead LDS (prioritized replay's tree insert)
   const int tid = threadIdx.x, nth = blockDim.x;
   for (int e = tid; e < a.E; e += nth) {
     int fs, rs;
@@ -130,10 +132,13 @@ DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, int* /*s_done*
       write_random_frame(a.frames + (int64_t)rslot * a.HW, a.HW, p.seed, p.ctr, 0x101u + 2u * e, tid, nth);
   }
   if (tid == 0) actor_advance(a, p.t0, p.f0, p.size0, p.eps0, p.eps_min, p.decay, p.ctr, p.frames_done);
+  if (a.tsum != nullptr)           // PER: the E new transitions enter with the running max priority
+    sumtree_update_wave(a.tsum, a.tmin, a.tmaxp, nullptr, nullptr, 0.f, 0.f, 1, a.E, a.tP, a.tlevels,
+                        *reinterpret_cast<SumtreeLds*>(lds_scratch), (int)(p.t0 % a.C), a.C);
 }
 
-DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, int* s_done) {
-  actor_step_block(a, q, s_done, actor_prefetch(a));
+DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, void* lds_scratch) {
+  actor_step_block(a, q, lds_scratch, actor_prefetch(a));
 }
 
 }  // namespace dqn

@@ -575,7 +575,7 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
     if (q_out != nullptr)
       for (int t = tid; t < B * A; t += nth) q_out[t] = q[t];
     HEAD_MARK(2);
-    if (has_actor) actor_step_block(a.actor, q, reinterpret_cast<int*>(red + 32), apre);
+    if (has_actor) actor_step_block(a.actor, q, part_lds, apre);      // (split-K partials are dead)
     HEAD_MARK(3);
     return;
   }

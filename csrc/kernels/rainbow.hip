@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     c51_softmax(a, lg, vl, nullptr, q, tid, nth);
     if (a.q_out != nullptr)
       for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
-    if (a.has_actor) actor_step_block(a.actor, q, sdone);
+    if (a.has_actor) actor_step_block(a.actor, q, lg);       // (the probabilities are dead after q)
     return;
   }
   // ---- 1. action choice on s' (Double DQN: online net, else the target net)
@@ -425,7 +425,9 @@ using namespace dqn;
 
 size_t c51_head_lds_bytes(const HeadArgs& a) {
   const int B = a.B, NA = a.atoms, NO = a.A * NA;
-  return (size_t)(B * NO + 4 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
+  const size_t n = (size_t)(B * NO + 4 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
+  // the fused actor's PER tree insert reuses the (dead) probabilities at the start of LDS
+  return a.has_actor && a.actor.tsum != nullptr && n < sizeof(SumtreeLds) ? sizeof(SumtreeLds) : n;
 }
 
 void launch_c51_head(const HeadArgs& a, hipStream_t st) {

@@ -24,7 +24,9 @@ struct SumtreeLds {                 // LDS scratch of the one-wave update
 // pure ALU + shuffles; stores are fire-and-forget. Every thread of the block must call it.
 DQN_DEV void sumtree_update_wave(float* __restrict__ sum, float* __restrict__ mn, float* __restrict__ maxp,
                                  const int32_t* __restrict__ idx, const float* __restrict__ td, float alpha,
-                                 float eps, int use_max, int n, int P, int levels, SumtreeLds& L) {
+                                 float eps, int use_max, int n, int P, int levels, SumtreeLds& L, int first = 0,
+                                 int cap = 1) {
+  // idx == nullptr: the n consecutive ring slots (first + lane) % cap
   const int lane = threadIdx.x;
   const bool w0 = threadIdx.x < 64;
   const bool valid = lane < n;
@@ -37,7 +39,8 @@ DQN_DEV void sumtree_update_wave(float* __restrict__ sum, float* __restrict__ mn
       if (lane == 0) maxp[0] = fmaxf(mp, m);
     }
     // unique keys (the lane breaks ties); padding lanes sort last with leaf field 0xffffffff
-    L.keys[lane] = ((uint64_t)(valid ? (uint32_t)idx[lane] : 0xffffffffu) << 6) | (uint64_t)lane;
+    const uint32_t li = idx != nullptr ? (uint32_t)idx[lane] : (uint32_t)((first + lane) % cap);
+    L.keys[lane] = ((uint64_t)(valid ? li : 0xffffffffu) << 6) | (uint64_t)lane;
   }
   __syncthreads();
   if (w0) {

@@ -95,8 +95,9 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
     a.zero_ptr = P<float*>(zero[0]); a.zero_n = (int)zero[1];
   }
   if (!actor.empty()) {
-    // actor = 15 pointers (ActorArgs order, q unused) + E, A, K, HW, C, F ; actor_f = gamma, p_done
-    TORCH_CHECK(actor.size() == 21 && actor_f.size() == 2, "fused actor args");
+    // actor = 15 pointers (ActorArgs order, q unused) + E, A, K, HW, C, F
+    //         [+ PER tree: sum, min, max_p, P, levels] ; actor_f = gamma, p_done
+    TORCH_CHECK((actor.size() == 21 || actor.size() == 26) && actor_f.size() == 2, "fused actor args");
     dqn::ActorArgs& x = a.actor;
     x.q = nullptr; x.frames = P<uint8_t*>(actor[1]); x.stacks = P<int32_t*>(actor[2]);
     x.cursor = P<int64_t*>(actor[3]); x.size_dev = P<int32_t*>(actor[4]); x.state_idx = P<int32_t*>(actor[5]);
@@ -105,6 +106,12 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
     x.rng = P<int64_t*>(actor[12]); x.ticket = P<int32_t*>(actor[13]); x.frames_done = P<int64_t*>(actor[14]);
     x.E = (int)actor[15]; x.A = (int)actor[16]; x.K = (int)actor[17]; x.HW = (int)actor[18]; x.C = (int)actor[19];
     x.F = (int)actor[20]; x.gamma = (float)actor_f[0]; x.p_done = (float)actor_f[1];
+    if (actor.size() == 26) {
+      x.tsum = P<float*>(actor[21]); x.tmin = P<float*>(actor[22]); x.tmaxp = P<float*>(actor[23]);
+      x.tP = (int)actor[24]; x.tlevels = (int)actor[25];
+      TORCH_CHECK(x.tsum && x.tmin && x.tmaxp && x.tP >= x.C && (1 << x.tlevels) == x.tP && x.tlevels <= 30,
+                  "actor PER tree: P = 2^levels >= capacity");
+    }
     TORCH_CHECK(x.A == a.A, "actor action count");
     TORCH_CHECK(x.F >= 2 * x.C + x.K, "frame ring must hold 2C + k frames");
     TORCH_CHECK(x.K >= 1 && x.K <= 4 && x.E >= 1 && x.E <= 64, "fused actor: 1 <= K <= 4, 1 <= E <= 64");

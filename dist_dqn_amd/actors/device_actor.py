@@ -59,14 +59,16 @@ class DeviceActor:
                                                self.rng, self.ticket, self.frames_done)]
         ints = [self.E, self.net.arch.num_actions, r.k, r.frames.shape[1] * r.frames.shape[2], r.capacity,
                 r.num_frames]
+        if r.prioritized:              # new transitions enter the sum-tree at the running max priority
+            t = r.tree
+            ints += [t.sum.data_ptr(), t.min.data_ptr(), t.max_p.data_ptr(), t.P, t.P.bit_length() - 1]
         return ptrs, ints, [self.gamma, self.p_done]
 
     def can_fuse(self, batch_size: int) -> bool:
         """One acting step per learner step that the learner's launches can carry."""
         ex = self.net.executor
         return (self.steps == 1 and self.E <= min(64, batch_size) and getattr(ex, 'consumes_slots', False)
-                and hasattr(ex, 'supports_fused_acting') and ex.supports_fused_acting()
-                and not self.replay.prioritized)
+                and hasattr(ex, 'supports_fused_acting') and ex.supports_fused_acting())
 
     def fused_args(self) -> dict:
         """Arguments of the fused acting step (executor.loss_and_grad(acting=...))."""

@@ -470,3 +470,39 @@ def test_per_fused_in_optimizer_equals_separate_launches(extra):
     torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(w1, w0, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(f1, f0, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('network,extra', [('nature', ''), ('nature', RAINBOW)])
+def test_device_actor_inserts_max_priority(network, extra):
+    """PER + device actors: each acting step's new transitions enter the sum-tree at the
+    running max priority (one-wave insert inside the acting launch), and every ancestor
+    stays the exact sum / min of its children."""
+    from dist_dqn_amd.actors.device_actor import DeviceActor
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    cfg = preset(network, 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 --prioritized_replay '
+                 + extra)
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+    rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)
+    rep.fill_synthetic(4096, 6, seed=5)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    idx = torch.randint(0, 4096, (64,), dtype=torch.int32, device=DEV, generator=g)
+    rep.update_priorities(idx, torch.rand(64, device=DEV, generator=g) * 5.0, 1e-6)   # raises max_p
+    actor = DeviceActor(net, rep, cfg, num_envs=4, steps_per_call=1, seed=1000)
+    for _ in range(3):
+        t0 = int(rep.cursor[0])
+        actor.step()
+        torch.cuda.synchronize()
+        P, mp = rep.tree.P, float(rep.tree.max_p)
+        for e in range(4):
+            leaf = (t0 + e) % 4096
+            assert float(rep.tree.sum[P + leaf]) == mp and float(rep.tree.min[P + leaf]) == mp
+    s, m = rep.tree.sum.cpu(), rep.tree.min.cpu()
+    lvl = s[P:2 * P].clone()
+    mn = m[P:2 * P].clone()
+    while lvl.numel() > 1:
+        lvl = lvl.view(-1, 2).sum(1)
+        mn = mn.view(-1, 2).min(1).values
+    torch.testing.assert_close(s[1], lvl[0], rtol=1e-5, atol=1e-3)
+    assert float(m[1]) == float(mn[0])
