@@ -98,6 +98,8 @@ struct HeadArgs {
   int64_t* prof;                 // optional s_memtime phase stamps of block 0 (profiling)
   const float* lgi[3];           // C51: precomputed logits [B][A*atoms] per instance (igemm, many CUs)
   const float* vli[3];           // C51 dueling: precomputed value logits [B][atoms]
+  const float* act_lgi;          // C51 + fused acting: the actors' logits [E][A*atoms] (+ act_vli [E][atoms])
+  const float* act_vli;
 };
 
 // One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =

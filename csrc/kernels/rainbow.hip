@@ -104,8 +104,9 @@ DQN_DEV float c51_z(const HeadArgs& a, int n) {
 // DPP row ops (no LDS crossbar). If logp != nullptr the log-probabilities of each
 // sample's TAKEN action row are kept there ([B][NA]); if q != nullptr the expected value
 // q[b][i] = sum_n p_n z_n is written too (action selection / acting).
-DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* logp, float* q, int tid, int nth) {
-  const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
+DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* logp, float* q, int tid, int nth,
+                         int B) {
+  const int A = a.A, NA = a.atoms, NO = A * NA;
   if (a.dueling) {
     for (int t = tid; t < B * NA; t += nth) {
       const int b = t / NA, n = t - b * NA;
@@ -159,8 +160,31 @@ DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* l
   __syncthreads();
 }
 
+// Fused acting (training launch, last block): the actors' E logits rows -> softmax ->
+// expected Q -> eps-greedy / env step / replay append (+ PER insert), all in this block's LDS.
+DQN_DEV void c51_act_block(const HeadArgs& a, float* sm) {
+  const int E = a.act_E, NA = a.atoms, NO = a.A * NA;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const ActorPre apre = actor_prefetch(a.actor);           // loads overlap the logits copy
+  float* lg = sm;                                          // [E][NO]
+  float* vl = lg + E * NO;                                 // [E][NA]
+  float* q = vl + E * NA;                                  // [E][A]
+  for (int t = tid; t < E * NO; t += nth) lg[t] = a.act_lgi[t];
+  if (a.dueling)
+    for (int t = tid; t < E * NA; t += nth) vl[t] = a.act_vli[t];
+  __syncthreads();
+  c51_softmax(a, lg, vl, nullptr, q, tid, nth, E);
+  actor_step_block(a.actor, q, lg, apre);                  // (the probabilities are dead after q)
+}
+
 __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (a.act_E > 0 && !a.infer && blockIdx.x == gridDim.x - 1) {
+    c51_act_block(a, sm);
+    return;
+  }
+  // (the learner's blocks: all but the fused acting block)
+  const int nblk = (int)gridDim.x - (a.act_E > 0 && !a.infer ? 1 : 0);
   const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
   float* lg = sm;                       // [B][NO] logits -> probabilities
   float* vl = lg + B * NO;              // [B][NA] dueling value logits
@@ -178,7 +202,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   C51_MARK(0);
   if (a.zero_ptr != nullptr) {
     float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
-    for (int t = blockIdx.x * nth + tid; t < a.zero_n / 4; t += gridDim.x * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = blockIdx.x * nth + tid; t < a.zero_n / 4; t += nblk * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   auto logits = [&](int inst) {          // precomputed (igemm) or in-block MFMA logits
     if (a.lgi[inst] != nullptr) c51_load_logits(a, inst, lg, vl, tid, nth);
@@ -187,7 +211,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   if (a.infer) {
     logits(0);
     __syncthreads();
-    c51_softmax(a, lg, vl, nullptr, q, tid, nth);
+    c51_softmax(a, lg, vl, nullptr, q, tid, nth, B);
     if (a.q_out != nullptr)
       for (int t = tid; t < B * A; t += nth) a.q_out[t] = q[t];
     if (a.has_actor) actor_step_block(a.actor, q, lg);       // (the probabilities are dead after q)
@@ -198,7 +222,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   logits(sel);
   __syncthreads();
   C51_MARK(1);
-  c51_softmax(a, lg, vl, nullptr, q, tid, nth);
+  c51_softmax(a, lg, vl, nullptr, q, tid, nth, B);
   C51_MARK(2);
   for (int b = tid; b < B; b += nth) {
     int best = 0;
@@ -212,7 +236,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   if (sel != 1) {
     logits(1);
     __syncthreads();
-    c51_softmax(a, lg, vl, nullptr, nullptr, tid, nth);
+    c51_softmax(a, lg, vl, nullptr, nullptr, tid, nth, B);
   }
   for (int t = tid; t < B * NA; t += nth) mt[t] = 0.f;
   __syncthreads();
@@ -236,7 +260,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   __syncthreads();                      // projection reads of lg done, its atomics complete
   logits(0);
   __syncthreads();
-  c51_softmax(a, lg, vl, lp, nullptr, tid, nth);
+  c51_softmax(a, lg, vl, lp, nullptr, tid, nth, B);
   float contrib = 0.f;
   for (int b = wave; b < B; b += nwave) {
     const float ce = -wave_sum_dpp(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
@@ -271,7 +295,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     dout[t] = lp[b * NA + n] * ((i == a.act[b] ? 1.f : 0.f) - inva);
   }
   __syncthreads();
-  const int gw = blockIdx.x * nwave + wave, GW = gridDim.x * nwave;
+  const int gw = blockIdx.x * nwave + wave, GW = nblk * nwave;
   const int kg = 8 * (lane >> 4), l16 = lane & 15;
   const act_t* h0 = reinterpret_cast<const act_t*>(a.h[0]);
   const int KB = (B + 31) / 32;                 // k-steps over the batch
@@ -340,7 +364,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   }
   C51_MARK(7);
   // (c) bias gradients
-  const int gt = blockIdx.x * nth + tid, gn = gridDim.x * nth;
+  const int gt = blockIdx.x * nth + tid, gn = nblk * nth;
   for (int j = gt; j < NO; j += gn) {
     float s = 0.f;
     for (int b = 0; b < B; ++b) s += dout[b * NO + j];
@@ -427,13 +451,14 @@ size_t c51_head_lds_bytes(const HeadArgs& a) {
   const int B = a.B, NA = a.atoms, NO = a.A * NA;
   const size_t n = (size_t)(B * NO + 4 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
   // the fused actor's PER tree insert reuses the (dead) probabilities at the start of LDS
-  return a.has_actor && a.actor.tsum != nullptr && n < sizeof(SumtreeLds) ? sizeof(SumtreeLds) : n;
+  return (a.has_actor || a.act_E > 0) && a.actor.tsum != nullptr && n < sizeof(SumtreeLds) ? sizeof(SumtreeLds) : n;
 }
 
 void launch_c51_head(const HeadArgs& a, hipStream_t st) {
   // training: phases 1-3 run redundantly in every block (L2-hot inputs); the output-layer
   // backward tiles spread over all 32 x 16 waves
-  hipLaunchKernelGGL(c51_head_kernel, dim3(a.infer ? 1 : 32), dim3(1024), c51_head_lds_bytes(a), st, a);
+  hipLaunchKernelGGL(c51_head_kernel, dim3(a.infer ? 1 : 32 + (a.act_E > 0 ? 1 : 0)), dim3(1024),
+                     c51_head_lds_bytes(a), st, a);
 }
 
 void launch_noisy_mix(const float* flat, float* eff, const float* noise, const NoisyJob* jobs, int njobs,

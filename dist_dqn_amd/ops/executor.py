@@ -581,20 +581,25 @@ class HipExecutor:
         ws = self._ws.get(key)
         if ws is None:
             dev = self._c51_dev
-            ws = {'lg': torch.zeros(3, B * self.NO, dtype=torch.float32, device=dev),
-                  'vl': torch.zeros(3, B * self.atoms, dtype=torch.float32, device=dev)}
+            ws = {'lg': torch.zeros(4, B * self.NO, dtype=torch.float32, device=dev),
+                  'vl': torch.zeros(4, B * self.atoms, dtype=torch.float32, device=dev)}
             self._ws[key] = ws
         return ws
 
     def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h=0):
         """Output layer + loss (+ backward) launch: scalar head or the C51 head."""
         if self.dist:
-            assert act_h == 0, 'fused acting is not wired into the C51 head'
             self._c51_B = ints[0]
-            lg, vl = self._c51_logits(hs, b, bv, pw, pwv)
+            if act_h:
+                # fused acting: the actors' logits ride in the same igemm launch as one more
+                # instance (online weights), the acting step in one more C51-head workgroup
+                lg, vl = self._c51_logits(list(hs) + [act_h], list(b) + [b[0]], list(bv) + bv[:1],
+                                          list(pw) + [pw[0]], list(pwv) + pwv[:1])
+            else:
+                lg, vl = self._c51_logits(hs, b, bv, pw, pwv)
             prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
             self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
-                                   wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl)
+                                   wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl, act_h)
         else:
             prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
             self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h,
@@ -642,7 +647,7 @@ class HipExecutor:
 
     # ----------------------------------------------------------- training
     def supports_fused_acting(self) -> bool:
-        return not self.dist and not self.two_stream
+        return not self.two_stream
 
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,

@@ -218,8 +218,9 @@ def test_cnn_learner_graph_equals_eager():
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize('network', ['nature', 'cnn'])
-def test_fused_acting_matches_separate_actor(network):
+@pytest.mark.parametrize('network,extra', [('nature', ''), ('cnn', ''), ('nature', '--distributional --dueling'),
+                                           ('nature', RAINBOW), ('nature', RAINBOW + ' --prioritized_replay')])
+def test_fused_acting_matches_separate_actor(network, extra):
     """The device actors' step inside the learner launches (extra trunk/fc instance + one
     head workgroup) writes the same transitions / frames / eps as the stand-alone act_fused
     path with the same weights and RNG."""
@@ -231,9 +232,9 @@ def test_fused_acting_matches_separate_actor(network):
     outs = []
     for fused in (False, True):
         cfg = preset(network if network == 'nature' else 'atari', 'Pong-v0',
-                     '--seed=4 --backend=hip --replay_memory_capacity=65536')
+                     '--seed=4 --backend=hip --replay_memory_capacity=65536 ' + extra)
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
-        rep = DeviceReplay(65536, (84, 84), 4, device=DEV, seed=5)
+        rep = DeviceReplay(65536, (84, 84), 4, device=DEV, seed=5, prioritized=cfg.prioritized_replay)
         rep.fill_synthetic(65536, 6, seed=5)
         actor = DeviceActor(net, rep, cfg, num_envs=4, steps_per_call=1, seed=11, use_graph=False)
         assert actor.can_fuse(cfg.minibatch_size)
