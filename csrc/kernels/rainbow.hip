@@ -160,6 +160,68 @@ DQN_DEV void c51_softmax(const HeadArgs& a, float* lg, const float* vl, float* l
   __syncthreads();
 }
 
+DQN_DEV void c51_rows_softmax(const HeadArgs& a, float* pc, float* logp, int tid, int nth);
+
+// Only ONE action row per sample matters for the target (a*) and online (taken action)
+// distributions: combine (dueling: v + adv_i - mean_j adv_j) straight from the precomputed
+// global logits into a compact [B][NA] LDS buffer and softmax those B rows (16 lanes per
+// row) instead of staging and normalising all B*A rows. logp (optional): log-probabilities.
+DQN_DEV void c51_rows(const HeadArgs& a, int inst, const int32_t* rows, float* pc, float* logp, int tid, int nth) {
+  const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
+  const float* src = a.lgi[inst];
+  for (int t = tid; t < B * NA; t += nth) {
+    const int b = t / NA, n = t - b * NA;
+    const float* col = src + b * NO + n;
+    float x = col[rows[b] * NA];
+    if (a.dueling) {
+      float mean = 0.f;
+      for (int i = 0; i < A; ++i) mean += col[i * NA];
+      mean /= (float)A;
+      const float v = a.vli[inst][b * NA + n] - mean;
+      x += v;
+    }
+    pc[t] = x;
+  }
+  __syncthreads();
+  c51_rows_softmax(a, pc, logp, tid, nth);
+}
+
+// in-place softmax of the B compact rows pc[b][0..NA) (16 lanes per row)
+DQN_DEV void c51_rows_softmax(const HeadArgs& a, float* pc, float* logp, int tid, int nth) {
+  const int B = a.B, NA = a.atoms;
+  const int l16 = tid & 15;
+  for (int b = tid >> 4; b < B; b += nth >> 4) {               // uniform per 16-lane group
+    float* r = pc + b * NA;
+    float x[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = l16 + 16 * u;
+      x[u] = n < NA ? r[n] : -INFINITY;
+      mx = fmaxf(mx, x[u]);
+    }
+    mx = row16_max(mx);
+    float e[4], s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      e[u] = l16 + 16 * u < NA ? __expf(x[u] - mx) : 0.f;
+      s += e[u];
+    }
+    s = row16_sum(s);
+    const float inv = 1.f / s;
+    const float ls = logp != nullptr ? __logf(s) : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = l16 + 16 * u;
+      if (n < NA) {
+        r[n] = e[u] * inv;
+        if (logp != nullptr) logp[b * NA + n] = x[u] - mx - ls;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Fused acting (training launch, last block): the actors' E logits rows -> softmax ->
 // expected Q -> eps-greedy / env step / replay append (+ PER insert), all in this block's LDS.
 DQN_DEV void c51_act_block(const HeadArgs& a, float* sm) {
@@ -194,6 +256,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   float* red = q + B * A;               // [32]
   int* astar = reinterpret_cast<int*>(red + 32);   // [B]
   int* sdone = astar + B;               // [E] fused actor scratch
+  float* pc = reinterpret_cast<float*>(sdone + (a.has_actor ? a.actor.E : 0));   // [B][NA] one row per sample
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
   const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
@@ -233,10 +296,16 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   __syncthreads();
   C51_MARK(3);
   // ---- 2. target distribution of a* projected onto the support
-  if (sel != 1) {
+  // pc[b] = target distribution of a*[b]
+  if (sel == 1) {
+    for (int t = tid; t < B * NA; t += nth) pc[t] = lg[(t / NA) * NO + astar[t / NA] * NA + t % NA];
+  } else if (a.lgi[1] != nullptr) {
+    c51_rows(a, 1, astar, pc, nullptr, tid, nth);
+  } else {
     logits(1);
     __syncthreads();
     c51_softmax(a, lg, vl, nullptr, nullptr, tid, nth, B);
+    for (int t = tid; t < B * NA; t += nth) pc[t] = lg[(t / NA) * NO + astar[t / NA] * NA + t % NA];
   }
   for (int t = tid; t < B * NA; t += nth) mt[t] = 0.f;
   __syncthreads();
@@ -244,7 +313,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     const float dz = (a.vmax - a.vmin) / (float)(NA - 1);
     for (int b = wave; b < B; b += nwave) {
       if (lane < NA) {
-        const float p = lg[b * NO + astar[b] * NA + lane];
+        const float p = pc[b * NA + lane];
         float tz = a.rew[b] + a.gam[b] * (1.f - a.done[b]) * c51_z(a, lane);
         tz = fminf(fmaxf(tz, a.vmin), a.vmax);
         const float bj = (tz - a.vmin) / dz;
@@ -257,16 +326,23 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   }
   C51_MARK(4);
   // ---- 3. online distribution of (s, a): cross-entropy, d logits
-  __syncthreads();                      // projection reads of lg done, its atomics complete
-  logits(0);
-  __syncthreads();
-  c51_softmax(a, lg, vl, lp, nullptr, tid, nth, B);
+  __syncthreads();                      // projection reads of pc done, its atomics complete
+  // pc[b] = online distribution of the taken action, lp its log
+  if (a.lgi[0] != nullptr) {
+    c51_rows(a, 0, a.act, pc, lp, tid, nth);
+  } else {
+    logits(0);
+    __syncthreads();
+    c51_softmax(a, lg, vl, lp, nullptr, tid, nth, B);
+    for (int t = tid; t < B * NA; t += nth) pc[t] = lg[(t / NA) * NO + a.act[t / NA] * NA + t % NA];
+    __syncthreads();
+  }
   float contrib = 0.f;
   for (int b = wave; b < B; b += nwave) {
     const float ce = -wave_sum_dpp(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
     const float w = a.wts != nullptr ? a.wts[b] : 1.f;
     if (lane < NA) {   // d(mean w*CE)/d logit of the taken action = w/B (p - m); reuse lp for it
-      const float p = lg[b * NO + a.act[b] * NA + lane];
+      const float p = pc[b * NA + lane];
       lp[b * NA + lane] = w / (float)B * (p - mt[b * NA + lane]);
     }
     if (lane == 0) {
@@ -449,7 +525,7 @@ using namespace dqn;
 
 size_t c51_head_lds_bytes(const HeadArgs& a) {
   const int B = a.B, NA = a.atoms, NO = a.A * NA;
-  const size_t n = (size_t)(B * NO + 4 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
+  const size_t n = (size_t)(B * NO + 5 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
   // the fused actor's PER tree insert reuses the (dead) probabilities at the start of LDS
   return (a.has_actor || a.act_E > 0) && a.actor.tsum != nullptr && n < sizeof(SumtreeLds) ? sizeof(SumtreeLds) : n;
 }
