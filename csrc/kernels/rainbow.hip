@@ -166,9 +166,9 @@ DQN_DEV void c51_rows_softmax(const HeadArgs& a, float* pc, float* logp, int tid
 // distributions: combine (dueling: v + adv_i - mean_j adv_j) straight from the precomputed
 // global logits into a compact [B][NA] LDS buffer and softmax those B rows (16 lanes per
 // row) instead of staging and normalising all B*A rows. logp (optional): log-probabilities.
-DQN_DEV void c51_rows(const HeadArgs& a, int inst, const int32_t* rows, float* pc, float* logp, int tid, int nth) {
+DQN_DEV void c51_rows(const HeadArgs& a, const float* src, const float* vsrc, const int32_t* rows, float* pc,
+                      float* logp, int tid, int nth) {
   const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
-  const float* src = a.lgi[inst];
   for (int t = tid; t < B * NA; t += nth) {
     const int b = t / NA, n = t - b * NA;
     const float* col = src + b * NO + n;
@@ -177,7 +177,7 @@ DQN_DEV void c51_rows(const HeadArgs& a, int inst, const int32_t* rows, float* p
       float mean = 0.f;
       for (int i = 0; i < A; ++i) mean += col[i * NA];
       mean /= (float)A;
-      const float v = a.vli[inst][b * NA + n] - mean;
+      const float v = vsrc[b * NA + n] - mean;
       x += v;
     }
     pc[t] = x;
@@ -222,6 +222,84 @@ DQN_DEV void c51_rows_softmax(const HeadArgs& a, float* pc, float* logp, int tid
   __syncthreads();
 }
 
+// LDS plan of the training head (floats). Base: lg [B][NO], vl / mt / lp [B][NA],
+// q [B][A], red [32], astar [B], actor scratch [E], pc [B][NA]. Staged (when it fits one CU's 160 KB): the
+// target and online logits [B][NO] + [B][NA] each, and act / rew / gam / done / wts [B].
+DQN_DEV_HOST_INLINE size_t c51_base_floats(const HeadArgs& a) {
+  const size_t B = a.B, NA = a.atoms, NO = (size_t)a.A * NA;
+  return B * NO + 4 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0);
+}
+DQN_DEV_HOST_INLINE size_t c51_stage_floats(const HeadArgs& a) {
+  return 2 * ((size_t)a.B * a.A * a.atoms + (size_t)a.B * a.atoms) + 5 * (size_t)a.B;
+}
+DQN_DEV_HOST_INLINE bool c51_staged(const HeadArgs& a) {
+  const bool dbl = a.h[2] != nullptr;
+  return !a.infer && a.lgi[0] != nullptr && a.lgi[1] != nullptr && (!dbl || a.lgi[2] != nullptr) &&
+         (c51_base_floats(a) + c51_stage_floats(a)) * sizeof(float) <= 160 * 1024;
+}
+
+// Every input phases 1-3 read, in ONE batch of global loads per thread instead of one
+// dependent round trip per phase: the selection instance's logits into lg / vl, the target
+// (Double DQN) and online logits into lgT / vlT / lgO / vlO, and the per-sample scalars into
+// sc = [act | rew | gam | done | wts]. Fixed-size register batches from fixed base pointers
+// (no pointer tables: those land in scratch); elements beyond a batch take a plain loop.
+constexpr int kStageLg = 10, kStageV = 2;   // per-thread batch: B*NO <= 10 * 1024, B*NA <= 2 * 1024
+template <int U>
+DQN_DEV void stage_ld(const float* src, int n, int tid, int nth, float (&r)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = tid + u * nth;
+    r[u] = src[t < n ? t : 0];                  // (t >= n: re-reads element 0, discarded)
+  }
+}
+template <int U>
+DQN_DEV void stage_st(float* dst, const float* src, int n, int tid, int nth, const float (&r)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = tid + u * nth;
+    if (t < n) dst[t] = r[u];
+  }
+  for (int t = tid + U * nth; t < n; t += nth) dst[t] = src[t];
+}
+DQN_DEV void c51_stage(const HeadArgs& a, int ninst, float* lg, float* vl, float* lgT, float* vlT, float* lgO,
+                       float* vlO, float* sc, int tid, int nth) {
+  const int B = a.B, NA = a.atoms, NO = a.A * NA, NV = a.dueling ? B * NA : 0;
+  const int sel = ninst == 3 ? 2 : 1;
+  const bool dbl = ninst == 3;
+  const float* any = a.lgi[0];                // valid base for empty segments
+  const float* l0 = a.lgi[sel];
+  const float* l1 = dbl ? a.lgi[1] : any;
+  const float* l2 = a.lgi[0];
+  const float* v0 = NV ? a.vli[sel] : any;
+  const float* v1 = NV && dbl ? a.vli[1] : any;
+  const float* v2 = NV ? a.vli[0] : any;
+  const int n1 = dbl ? B * NO : 0, nv1 = dbl ? NV : 0;
+  float r0[kStageLg], r1[kStageLg], r2[kStageLg], q0[kStageV], q1[kStageV], q2[kStageV];
+  stage_ld(l0, B * NO, tid, nth, r0);
+  stage_ld(l1, n1, tid, nth, r1);
+  stage_ld(l2, B * NO, tid, nth, r2);
+  stage_ld(v0, NV, tid, nth, q0);
+  stage_ld(v1, nv1, tid, nth, q1);
+  stage_ld(v2, NV, tid, nth, q2);
+  const int sg = tid / B, sb = tid - sg * B;   // scalars: thread tid < 4B loads one
+  const float* sp = sg == 0 ? reinterpret_cast<const float*>(a.act) : sg == 1 ? a.rew : sg == 2 ? a.gam : a.done;
+  const float sv = sp[tid < 4 * B ? sb : 0];
+  const float wv = a.wts != nullptr ? a.wts[tid < B ? tid : 0] : 1.f;
+  stage_st(lg, l0, B * NO, tid, nth, r0);
+  stage_st(lgT, l1, n1, tid, nth, r1);
+  stage_st(lgO, l2, B * NO, tid, nth, r2);
+  stage_st(vl, v0, NV, tid, nth, q0);
+  stage_st(vlT, v1, nv1, tid, nth, q1);
+  stage_st(vlO, v2, NV, tid, nth, q2);
+  if (tid < 4 * B) sc[tid] = sv;             // (act bits copied as raw 32-bit words)
+  if (tid < B) sc[4 * B + tid] = wv;
+  for (int t = tid + nth; t < 5 * B; t += nth) {   // B > nth / 4: the rest of the scalars
+    const int g = t / B, b = t - g * B;
+    sc[t] = g == 0 ? __int_as_float(a.act[b]) : g == 1 ? a.rew[b] : g == 2 ? a.gam[b] : g == 3 ? a.done[b]
+          : (a.wts != nullptr ? a.wts[b] : 1.f);
+  }
+}
+
 // Fused acting (training launch, last block): the actors' E logits rows -> softmax ->
 // expected Q -> eps-greedy / env step / replay append (+ PER insert), all in this block's LDS.
 DQN_DEV void c51_act_block(const HeadArgs& a, float* sm) {
@@ -257,6 +335,13 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   int* astar = reinterpret_cast<int*>(red + 32);   // [B]
   int* sdone = astar + B;               // [E] fused actor scratch
   float* pc = reinterpret_cast<float*>(sdone + (a.has_actor ? a.actor.E : 0));   // [B][NA] one row per sample
+  const bool staged = c51_staged(a);
+  float* lgT = pc + B * NA;
+  float* vlT = lgT + B * NO;
+  float* lgO = vlT + B * NA;
+  float* vlO = lgO + B * NO;
+  float* sc = vlO + B * NA;             // [act | rew | gam | done | wts] x B
+  const int32_t* sact = staged ? reinterpret_cast<const int32_t*>(sc) : a.act;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
   const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
@@ -282,7 +367,8 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   }
   // ---- 1. action choice on s' (Double DQN: online net, else the target net)
   const int sel = ninst == 3 ? 2 : 1;
-  logits(sel);
+  if (staged) c51_stage(a, ninst, lg, vl, lgT, vlT, lgO, vlO, sc, tid, nth);
+  else logits(sel);
   __syncthreads();
   C51_MARK(1);
   c51_softmax(a, lg, vl, nullptr, q, tid, nth, B);
@@ -300,7 +386,8 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   if (sel == 1) {
     for (int t = tid; t < B * NA; t += nth) pc[t] = lg[(t / NA) * NO + astar[t / NA] * NA + t % NA];
   } else if (a.lgi[1] != nullptr) {
-    c51_rows(a, 1, astar, pc, nullptr, tid, nth);
+    if (staged) c51_rows(a, lgT, vlT, astar, pc, nullptr, tid, nth);
+    else c51_rows(a, a.lgi[1], a.vli[1], astar, pc, nullptr, tid, nth);
   } else {
     logits(1);
     __syncthreads();
@@ -314,7 +401,9 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     for (int b = wave; b < B; b += nwave) {
       if (lane < NA) {
         const float p = pc[b * NA + lane];
-        float tz = a.rew[b] + a.gam[b] * (1.f - a.done[b]) * c51_z(a, lane);
+        const float rw = staged ? sc[B + b] : a.rew[b], gm = staged ? sc[2 * B + b] : a.gam[b];
+        const float dn = staged ? sc[3 * B + b] : a.done[b];
+        float tz = rw + gm * (1.f - dn) * c51_z(a, lane);
         tz = fminf(fmaxf(tz, a.vmin), a.vmax);
         const float bj = (tz - a.vmin) / dz;
         const float lo = floorf(bj), hi = ceilf(bj);
@@ -329,7 +418,8 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   __syncthreads();                      // projection reads of pc done, its atomics complete
   // pc[b] = online distribution of the taken action, lp its log
   if (a.lgi[0] != nullptr) {
-    c51_rows(a, 0, a.act, pc, lp, tid, nth);
+    if (staged) c51_rows(a, lgO, vlO, sact, pc, lp, tid, nth);
+    else c51_rows(a, a.lgi[0], a.vli[0], a.act, pc, lp, tid, nth);
   } else {
     logits(0);
     __syncthreads();
@@ -340,7 +430,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   float contrib = 0.f;
   for (int b = wave; b < B; b += nwave) {
     const float ce = -wave_sum_dpp(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
-    const float w = a.wts != nullptr ? a.wts[b] : 1.f;
+    const float w = staged ? sc[4 * B + b] : (a.wts != nullptr ? a.wts[b] : 1.f);
     if (lane < NA) {   // d(mean w*CE)/d logit of the taken action = w/B (p - m); reuse lp for it
       const float p = pc[b * NA + lane];
       lp[b * NA + lane] = w / (float)B * (p - mt[b * NA + lane]);
@@ -368,7 +458,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   float* dout = lg;
   for (int t = tid; t < B * NO; t += nth) {
     const int b = t / NO, j = t - b * NO, i = j / NA, n = j - i * NA;
-    dout[t] = lp[b * NA + n] * ((i == a.act[b] ? 1.f : 0.f) - inva);
+    dout[t] = lp[b * NA + n] * ((i == sact[b] ? 1.f : 0.f) - inva);
   }
   __syncthreads();
   const int gw = blockIdx.x * nwave + wave, GW = nblk * nwave;
@@ -524,8 +614,7 @@ __global__ void __launch_bounds__(256) noisy_grad_kernel(float* __restrict__ gra
 using namespace dqn;
 
 size_t c51_head_lds_bytes(const HeadArgs& a) {
-  const int B = a.B, NA = a.atoms, NO = a.A * NA;
-  const size_t n = (size_t)(B * NO + 5 * B * NA + B * a.A + 32 + B + (a.has_actor ? a.actor.E : 0)) * sizeof(float);
+  const size_t n = (c51_base_floats(a) + (c51_staged(a) ? c51_stage_floats(a) : 0)) * sizeof(float);
   // the fused actor's PER tree insert reuses the (dead) probabilities at the start of LDS
   return (a.has_actor || a.act_E > 0) && a.actor.tsum != nullptr && n < sizeof(SumtreeLds) ? sizeof(SumtreeLds) : n;
 }
