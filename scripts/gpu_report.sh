@@ -13,6 +13,7 @@ run_bench() {   # name, args
   echo "$1: $(python -c "import json; d=json.loads(open('$OUT/bench_$1.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['dtype'])")"
 }
 rm -f $OUT/benches.jsonl
+run_bench default ""
 run_bench dqn "--steps 1000 --warmup 100"
 run_bench dqn_fp16 "--steps 1000 --warmup 100 --dtype fp16"
 run_bench dqn_sep "--steps 1000 --warmup 100 --fuse_acting 0"
