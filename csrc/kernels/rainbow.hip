@@ -416,6 +416,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
   C51_MARK(4);
   // ---- 3. online distribution of (s, a): cross-entropy, d logits
   __syncthreads();                      // projection reads of pc done, its atomics complete
+  C51_MARK(14);
   // pc[b] = online distribution of the taken action, lp its log
   if (a.lgi[0] != nullptr) {
     if (staged) c51_rows(a, lgO, vlO, sact, pc, lp, tid, nth);
@@ -427,6 +428,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     for (int t = tid; t < B * NA; t += nth) pc[t] = lg[(t / NA) * NO + a.act[t / NA] * NA + t % NA];
     __syncthreads();
   }
+  C51_MARK(15);
   float contrib = 0.f;
   for (int b = wave; b < B; b += nwave) {
     const float ce = -wave_sum_dpp(lane < NA ? mt[b * NA + lane] * lp[b * NA + lane] : 0.f);
@@ -444,6 +446,7 @@ __global__ void __launch_bounds__(1024) c51_head_kernel(HeadArgs a) {
     const float s = wave_sum_dpp(contrib);
     if (lane == 0) red[wave] = s;
   }
+  C51_MARK(16);
   __syncthreads();
   if (tid == 0 && blockIdx.x == 0) {
     float s = 0.f;

@@ -27,3 +27,6 @@ names = ['logits(sel)', 'softmax+Q(sel)', 'argmax', 'target logits+softmax+proj'
 print('C51 head block-0 cycles: total %.0f | ' % sum(d) + ' | '.join('%s %.0f' % kv for kv in zip(names, d)))
 tt = ex.head_prof[10:14].double()
 print('wave-0 logits tasks (cycles):', (tt[1:] - tt[:-1]).tolist(), 'from kernel start to first task:', float(tt[0] - t[0]))
+t3 = ex.head_prof[[4, 14, 15, 16, 5]].double()
+print('online phase split (cycles): wait projection %.0f | rows+softmax %.0f | CE %.0f | reduce+loss %.0f'
+      % tuple((t3[1:] - t3[:-1]).tolist()))
