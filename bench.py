@@ -48,7 +48,7 @@ def main():
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--backend', default='auto', choices=['auto', 'hip', 'torch'])
-    ap.add_argument('--replay', type=int, default=200000)
+    ap.add_argument('--replay', type=int, default=1000000, help='replay capacity (the Atari preset: 1M transitions)')
     ap.add_argument('--actions', type=int, default=6)
     ap.add_argument('--actor_envs', type=int, default=4)
     ap.add_argument('--update_freq', type=int, default=4)
@@ -65,7 +65,7 @@ def main():
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.learner import Learner
     from dist_dqn_amd.models.network import Network
-    from dist_dqn_amd.parallel import broadcast_flat, init_distributed
+    from dist_dqn_amd.parallel import broadcast_state, check_state_equal, init_distributed
     from dist_dqn_amd.replay import DeviceReplay
 
     cfg = preset('nature' if args.network == 'nature' else 'atari', 'Pong-v0',
@@ -78,8 +78,9 @@ def main():
     dev = ctx.device
     assert dev.type == 'cuda', 'bench.py needs a GPU'
     net = Network.create_network(cfg, (84, 84, 4), args.actions, num_replicas=ctx.world_size, device=dev)
-    broadcast_flat(ctx, net.online.flat)
     net.target.copy_from(net.online)
+    net.refresh_packed()
+    broadcast_state(ctx, net)          # every replica tensor from rank 0 (params, target, slots, noise)
     replay = DeviceReplay(cfg.replay_memory_capacity, (84, 84), 4, device=dev,
                           prioritized=cfg.prioritized_replay, seed=ctx.rank)
     replay.fill_synthetic(cfg.replay_memory_capacity, args.actions, seed=ctx.rank)
@@ -101,6 +102,7 @@ def main():
         step()
     ctx.barrier()
     torch.cuda.synchronize(dev)
+    frames0 = actor.env_frames() if actor is not None else 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -111,17 +113,25 @@ def main():
     if ctx.enabled:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t)
+    # env frames the device actors actually stepped in the timed region (device counter), summed
+    frames = torch.tensor([(actor.env_frames() - frames0) if actor is not None else 0], dtype=torch.float64,
+                          device=dev)
+    if ctx.enabled:
+        dist.all_reduce(frames)
+    frames = float(frames)
     loss = float(learner.loss)
     xgmi_ok = learner.reducer.xgmi.check() if learner.reducer.xgmi is not None else True
+    # (outside the timed region) every replica tensor must still be bit-identical to rank 0's
+    eq = check_state_equal(ctx, net)
+    replicas_equal = all(eq.values())
     if ctx.rank == 0:
         sps = args.steps * ctx.world_size / el
-        frames = (args.actor_envs * max(1, args.update_freq // args.actor_envs)) * args.steps * ctx.world_size / el
         out = {
             'metric': METRIC, 'value': round(sps, 2), 'unit': 'SGD steps/s (all GPUs)',
             'n_gpus': ctx.world_size, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(1000.0 * el / args.steps, 4), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': getattr(net.executor, 'compute_dtype', 'fp32'), 'data': 'synthetic (random uint8 84x84 frames, random init)',
-            'env_frames_per_sec': round(frames, 1),
+            'env_frames_per_sec': round(frames / el, 1),
             'samples_per_sec': round(sps * args.batch, 1),
             'config': {'model': 'nature-cnn' if args.network == 'nature' else args.network,
                        'global_batch': args.batch * ctx.world_size, 'seq_len': None,
@@ -135,11 +145,18 @@ def main():
                        'allreduce': learner.reducer.mode if ctx.enabled else None,
                        'allreduce_probe_us': learner.reducer.timings or None,
                        'allreduce_peer_timeouts': not xgmi_ok,
+                       'world_size': ctx.world_size, 'dist_backend': ctx.backend,
+                       'replicas_equal': replicas_equal,
+                       'replicas_diverged': sorted(k for k, v in eq.items() if not v),
                        'sampling': learner._sample_mode()},
         }
         print(json.dumps(out), flush=True)
     if ctx.enabled:
         dist.destroy_process_group()
+    if not replicas_equal or not xgmi_ok:
+        print('bench: replicas diverged (%s) or an xgmi peer wait timed out (%s)'
+              % (sorted(k for k, v in eq.items() if not v), not xgmi_ok), file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == '__main__':

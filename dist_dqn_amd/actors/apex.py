@@ -366,6 +366,16 @@ class ApexTrainer:
         self._thread.start()
         t0 = last = time.time()
         steps_at_last = frames_at_last = 0
+        # sync-DP Ape-X: every learner step is a collective, so local reasons to stop (time
+        # budget, dead actors) become stop requests the ranks agree on (supervisor.py)
+        coordinated = bool(getattr(supervisor, 'coordinated', False))
+
+        def want_stop(reason):
+            if not coordinated:
+                return True
+            supervisor.request_stop(reason)
+            return False
+
         try:
             while True:
                 with trace('apex.drain'):
@@ -375,6 +385,8 @@ class ApexTrainer:
                     if self._snap is not None and self.learner.train_steps % self.sync_freq == 0:
                         with self._lock:
                             self._refresh_snapshot()
+                    if supervisor is not None:
+                        supervisor.on_train_step(self.learner.train_steps)
                 else:
                     time.sleep(0.001)
                 now = time.time()
@@ -394,15 +406,16 @@ class ApexTrainer:
                     last, steps_at_last, frames_at_last = now, self.learner.train_steps, self.pool.frames
                 if max_train_steps and self.learner.train_steps >= max_train_steps:
                     break
-                if max_seconds and now - t0 >= max_seconds:
+                if max_seconds and now - t0 >= max_seconds and want_stop('Ape-X time budget'):
                     break
                 if supervisor is not None and supervisor.should_stop():
                     log.warning('Received signal to stop. Exiting Ape-X loop.')
                     break
                 if self.pool.alive() == 0 and self.pool.procs:
-                    log.warning('all actors exited')
                     self.pool.drain(self.replay)
-                    break
+                    if self.replay.size() < start or want_stop('all actors exited'):
+                        log.warning('all actors exited')
+                        break
         finally:
             self._stop.set()
             self._thread.join(5.0)

@@ -68,6 +68,7 @@ class DQNAgent:
             self.summary_writer = summary_writer
         self.metrics = metrics
         self.monitor = monitor
+        self._supervisor = None
         self.sgd_meter = RateMeter()
         self.frame_meter = RateMeter()
         self.frame_buffer = FrameBuffer(config.frames_per_state, self._get_frame_resizer(env, config))
@@ -78,7 +79,20 @@ class DQNAgent:
 
     # ------------------------------------------------------------ train loop
     def train(self, num_episodes, max_steps_per_episode, supervisor=None):
-        for episode in range(num_episodes):
+        """Reference `train` (`dqn_agent.py:52-70`): episodes until ``num_episodes`` or the
+        supervisor says stop. The supervisor also sees every train step (periodic checkpoint,
+        heartbeat, fault injection, stop agreement). Under synchronous data parallelism
+        (``supervisor.coordinated``) a rank that runs out of episodes keeps training until
+        the ranks agree to stop, and leaves mid-episode at the agreed step, so every rank
+        takes the same number of collective SGD steps."""
+        self._supervisor = supervisor
+        coordinated = bool(getattr(supervisor, 'coordinated', False))
+        episode = 0
+        while True:
+            if episode >= num_episodes:
+                if not coordinated:
+                    break
+                supervisor.request_stop('num_episodes reached')
             reward, steps = self.train_episode(max_steps_per_episode)
             self.stats.log_episode(reward, steps)
             mean_reward = self.stats.last_100_mean_reward()
@@ -93,10 +107,11 @@ class DQNAgent:
                                    sgd_steps_per_sec=self.sgd_meter.rate(),
                                    env_frames_per_sec=self.frame_meter.rate(),
                                    replay_size=self.replay_memory.size())
+            episode += 1
             if supervisor and supervisor.should_stop():
                 log.warning('Received signal to stop. Exiting train loop.')
                 break
-            if self.config.max_train_steps and self.training_steps >= self.config.max_train_steps:
+            if self._train_budget_done():
                 break
 
     def _begin_episode(self):
@@ -150,10 +165,26 @@ class DQNAgent:
             state = next_state
             if steps % self.config.update_freq == 0:
                 self._train_minibatch(self.config.minibatch_size)
+                if self._leave_episode():
+                    break
         return total_reward, steps
+
+    def _train_budget_done(self) -> bool:
+        m = self.config.max_train_steps
+        return bool(m) and self.training_steps >= m
+
+    def _leave_episode(self) -> bool:
+        """Leave mid-episode when the train-step budget is spent (every DP rank spends it at the
+        same step) or when the coordinated stop was agreed at this step."""
+        sv = self._supervisor
+        if self._train_budget_done():
+            return True
+        return sv is not None and getattr(sv, 'coordinated', False) and sv.should_stop()
 
     # ---------------------------------------------------------- learner step
     def _train_minibatch(self, minibatch_size):
+        if self._train_budget_done():
+            return
         # device replay: staged (not yet flushed) transitions count, the flush below ships them
         avail = self.replay_memory.size() + (self.replay_memory.staged() if self._device_replay else 0)
         if avail < minibatch_size:
@@ -178,6 +209,11 @@ class DQNAgent:
                 self.network.update_target(self.config.target_update_tau)
             else:
                 self._update_target_network()
+        sv = self._supervisor
+        if sv is not None:
+            if getattr(self.session, 'stop_requested', False):    # e.g. the async PS said stop
+                sv.request_stop('parameter server stopped')
+            sv.on_train_step(self.training_steps)
 
     # ---------------------------------------------------------------- acting
     def _pick_action(self, state):
@@ -248,3 +284,11 @@ class DQNAgent:
 
     def agent_state(self):
         return {'random_action_prob': self.random_action_prob, 'training_steps': self.training_steps}
+
+    def load_agent_state(self, state: Optional[dict]):
+        """Apply an ``--save_agent_state`` sidecar (opt-in; the reference restarts epsilon and
+        the local step count)."""
+        if not state:
+            return
+        self.random_action_prob = float(state.get('random_action_prob', self.random_action_prob))
+        self.training_steps = int(state.get('training_steps', self.training_steps))

@@ -28,7 +28,7 @@ def run_worker(config: Config):
     from .agent import DQNAgent
     from .learner import Learner
     from .models.network import Network
-    from .parallel import broadcast_flat, init_distributed
+    from .parallel import broadcast_state, init_distributed
     from .replay import DeviceReplay, ReplayMemory
     from .supervisor import RunSupervisor
     from .utils.metrics import EpisodeMonitor, JsonlWriter
@@ -43,10 +43,17 @@ def run_worker(config: Config):
     log.info('rank %d/%d device=%s executor=%s params=%d', ctx.rank, ctx.world_size, ctx.device,
              network.executor.name, network.arch.num_params())
 
+    if ctx.enabled and not (config.sync or config.async_ps):
+        # reference semantics: no --sync means asynchronous PS training (network.py:186-202)
+        log.warning('world size %d without --sync or --async_ps: running synchronous data parallelism '
+                    '(the reference default is asynchronous parameter-server training; pass --async_ps '
+                    'for that, or --sync to silence this warning)', ctx.world_size)
+    coordinated = ctx.enabled and not config.async_ps
     sv = RunSupervisor(is_chief=ctx.is_chief, logdir=config.logdir, network=network, rank=ctx.rank,
                        world_size=ctx.world_size, save_secs=config.checkpoint_secs,
-                       max_to_keep=config.max_to_keep)
-    sv.prepare(broadcast_fn=lambda: broadcast_flat(ctx, network.online.flat))
+                       max_to_keep=config.max_to_keep, ctx=ctx, coordinated=coordinated,
+                       stop_sync_steps=config.stop_sync_steps)
+    sv.prepare(broadcast_fn=lambda: broadcast_state(ctx, network))
 
     if config.async_ps and ctx.enabled and ctx.rank == 0:
         return _run_parameter_server(config, ctx, network, sv)
@@ -63,24 +70,46 @@ def run_worker(config: Config):
         if config.async_ps and ctx.enabled:
             from .parallel.async_ps import AsyncPSClient
             ps = AsyncPSClient(ctx, network.online.flat)
-            ps.pull(network.online.flat, network.global_step)      # start from the PS parameters
-            network._repack()
+            # start from the PS parameters (and the PS-owned target under --disable_target_replication)
+            ps.pull(network.online.flat, network.global_step,
+                    target=network.target.flat if config.disable_target_replication else None)
+            network.refresh_packed()
         session = Learner(network, replay, config, ctx, ps_client=ps)
     else:
         replay = ReplayMemory(config.replay_memory_capacity, rng=random.Random(seed + 7919 * (ctx.rank + 1)))
         session = None
     monitor = EpisodeMonitor(config.monitor_path, ctx.rank) if config.monitor else None
     metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))
+    metrics.write(kind='start', rank=ctx.rank, world_size=ctx.world_size, restored_from=sv.restored_from,
+                  global_step=int(network.global_step), executor=network.executor.name)
     with sv.managed():
         agent = DQNAgent(env, network, session, replay, config, enable_summary=ctx.is_chief,
                          metrics=metrics, monitor=monitor)
-        sv.ckpt.agent_state_fn = agent.agent_state if config.save_agent_state else None
+        if config.save_agent_state:
+            sv.ckpt.agent_state_fn = agent.agent_state
+            agent.load_agent_state(sv.agent_state)
         try:
             agent.train(config.num_episodes, config.max_steps_per_episode, sv)
         finally:
             if session is not None and session.ps is not None:
                 session.ps.close()
+        if coordinated and config.replica_check:
+            _replica_check(ctx, network, metrics, agent.training_steps)
     return agent
+
+
+def _replica_check(ctx, network, metrics, steps: int):
+    """End of a sync-DP run: every replica tensor (online, target, optimizer slots, beta
+    powers, global_step, noise stream) must be bit-identical to rank 0's."""
+    from .parallel import check_state_equal
+    eq = check_state_equal(ctx, network)
+    ok = all(eq.values())
+    metrics.write(kind='replica_check', equal=ok, tensors=eq, global_step=int(network.global_step),
+                  training_steps=steps, world_size=ctx.world_size)
+    if not ok:
+        raise RuntimeError('replicas diverged on rank %d: %s' % (ctx.rank, {k: v for k, v in eq.items() if not v}))
+    log.info('replica check: %d tensors bit-identical across %d ranks at global_step %d', len(eq),
+             ctx.world_size, int(network.global_step))
 
 
 def _run_parameter_server(config: Config, ctx, network, sv):
@@ -90,7 +119,7 @@ def _run_parameter_server(config: Config, ctx, network, sv):
     server = AsyncPSServer(ctx, network)
     log.info('async PS on rank 0 serving %d workers', len(server.workers))
     with sv.managed():
-        server.serve()
+        server.serve(supervisor=sv)
     log.info('async PS done: %d updates %s', server.updates, server.per_worker)
     return server
 

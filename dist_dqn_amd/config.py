@@ -148,11 +148,18 @@ def build_parser() -> argparse.ArgumentParser:
     a('--fuse_sampling', default=2, type=int, choices=[0, 1, 2],
       help='Uniform GPU replay: 0 = sampler launch per step, 1 = the Nature trunk draws the minibatch, '
            '2 = the previous step\'s optimizer launch draws it (one extra block, off the critical path)')
-    a('--checkpoint_secs', default=600, type=int)
+    a('--checkpoint_secs', default=600, type=float,
+      help='chief: seconds between periodic checkpoints (reference Supervisor: 600; <= 0 disables)')
     a('--max_to_keep', default=5, type=int)
     a('--save_agent_state', action='store_true', help='Checkpoint epsilon/step sidecar')
     a('--async_ps', action='store_true', help='Emulate async parameter-server updates')
     a('--max_train_steps', default=0, type=int, help='Stop after N learner steps (0 = no limit)')
+    a('--allreduce_check_steps', default=1000, type=int,
+      help='xgmi transport: read its peer-timeout error word every N learner steps (host sync)')
+    a('--stop_sync_steps', default=10, type=int,
+      help='sync DP: ranks agree on a pending stop request every N train steps (CPU control plane)')
+    a('--replica_check', default=1, type=int,
+      help='sync DP: verify at the end of the run that every replica tensor is bit-identical')
     return p
 
 
@@ -228,11 +235,14 @@ class Config:
     overlap_allreduce: int = 1
     hip_graph: int = 1
     fuse_sampling: int = 2
-    checkpoint_secs: int = 600
+    checkpoint_secs: float = 600
     max_to_keep: int = 5
     save_agent_state: bool = False
     async_ps: bool = False
     max_train_steps: int = 0
+    allreduce_check_steps: int = 1000
+    stop_sync_steps: int = 10
+    replica_check: int = 1
 
     def replace(self, **kw) -> 'Config':
         return dataclasses.replace(self, **kw)

@@ -12,5 +12,5 @@ gym/ALE are not available, so:
 """
 from .spaces import Box, Discrete, EnvSpec  # noqa: F401
 from .cartpole import CartPoleEnv  # noqa: F401
-from .synthetic import SyntheticAtariEnv, ATARI_ACTIONS  # noqa: F401
+from .synthetic import BlockBanditEnv, SyntheticAtariEnv, ATARI_ACTIONS  # noqa: F401
 from .registry import make, is_atari  # noqa: F401

@@ -70,3 +70,51 @@ class SyntheticAtariEnv:
 
     def close(self):
         pass
+
+
+class BlockBanditEnv:
+    """A LEARNABLE Atari-shaped environment (for end-to-end learning checks of the image
+    learners; `SyntheticAtariEnv` rewards are pure noise). Each frame is a dark screen with
+    one bright block in one of ``num_actions`` vertical bands; the reward is 1 when the action
+    names the block's band of the CURRENT frame, else 0, and the next frame's band is drawn at
+    random. Episodes last ``episode_len`` steps (terminal), so the best return is
+    ``episode_len`` and a uniformly random policy scores ``episode_len / num_actions``.
+    Solving it needs the Q-network to read the newest frame of the stack through the conv
+    trunk — what the reference's Atari learner has to do (`/root/reference/src/dqn_agent.py:72-106`)."""
+    SCREEN = (210, 160, 3)
+
+    def __init__(self, env_id: str = 'SyntheticBlock-v0', seed: Optional[int] = None,
+                 episode_len: int = 8, num_actions: int = 4):
+        self.spec = EnvSpec(env_id, episode_len)
+        self.action_space = Discrete(num_actions, random.Random(seed))
+        self.observation_space = Box(0, 255, self.SCREEN, np.uint8)
+        self._rng = np.random.default_rng(seed)
+        self.episode_len = episode_len
+        self._t = 0
+        self._band = 0
+
+    def seed(self, seed=None):
+        self._rng = np.random.default_rng(seed)
+        self.action_space.seed(seed)
+
+    def _frame(self):
+        f = np.full(self.SCREEN, 16, dtype=np.uint8)
+        w = self.SCREEN[1] // self.action_space.n
+        x0 = self._band * w + w // 4
+        f[60:150, x0:x0 + w // 2, :] = 240
+        return f
+
+    def reset(self):
+        self._t = 0
+        self._band = int(self._rng.integers(0, self.action_space.n))
+        return self._frame()
+
+    def step(self, action):
+        assert self.action_space.contains(action)
+        reward = 1.0 if int(action) == self._band else 0.0
+        self._t += 1
+        self._band = int(self._rng.integers(0, self.action_space.n))
+        return self._frame(), reward, self._t >= self.episode_len, {}
+
+    def close(self):
+        pass

@@ -70,6 +70,12 @@ class Learner:
         self._dense_hi = network.dense_range()[1] if self._split else 0
         self._ar_stream = None
         self._presampled = False    # this step's minibatch was drawn by the last optimizer launch
+        # sync DP + --disable_target_replication: rank 0's target is broadcast after each hard
+        # sync; the host mirrors the device global_step to know when (one read, here)
+        self._own_target = bool(self.ctx.enabled and ps_client is None and self.tau >= 1.0
+                                and getattr(config, 'disable_target_replication', False))
+        self._host_step = int(network.global_step) if self._own_target else 0
+        self._xgmi_check_every = max(1, int(getattr(config, 'allreduce_check_steps', 1000)))
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -208,16 +214,44 @@ class Learner:
             self.reducer.allreduce()
         self._apply()
 
+    @property
+    def stop_requested(self) -> bool:
+        """The async parameter server answered STOP (no more pushes are accepted)."""
+        return self.ps is not None and self.ps.stopped
+
     def _ps_exchange(self):
         """Async-PS worker: push grads, pull the PS parameters, repack; target cadence on
-        the LOCAL train-step count (reference `dqn_agent.py:143,215-222`)."""
+        the LOCAL train-step count (reference `dqn_agent.py:143,215-222`). With
+        --disable_target_replication the sync is a request to the PS, which owns the target
+        and ships it back when it changed."""
+        own = bool(self.config.disable_target_replication)
+        due = self.tau >= 1.0 and (self.train_steps + 1) % max(1, self.config.target_update_freq) == 0
         with trace('ps.exchange'):
-            self.ps.exchange(self.net.grad, self.net.online.flat, self.net.global_step)
+            ok = self.ps.exchange(self.net.grad, self.net.online.flat, self.net.global_step,
+                                  sync_target=own and due, target=self.net.target.flat if own else None)
+        if not ok:
+            return
         self.net._repack()
         if self.tau < 1.0:
             self.update_target_now(self.tau)
-        elif (self.train_steps + 1) % max(1, self.config.target_update_freq) == 0:
+        elif own:
+            if self.ps.target_updated and hasattr(self.net.executor, 'repack'):
+                self.net.executor.repack(self.net.target.flat)
+        elif due:
             self.update_target_now()
+
+    def _broadcast_owned_target(self):
+        """Sync DP + --disable_target_replication: rank 0 owns the target (reference: target
+        variables on the PS, `network.py:226-231`); after each hard sync its copy is broadcast
+        and every rank's packed target fragments are rebuilt from it."""
+        self._host_step += 1
+        f = max(1, int(self.config.target_update_freq))
+        if self._own_target and self._host_step % f == 0:
+            with trace('target.broadcast'):
+                import torch.distributed as dist
+                dist.broadcast(self.net.target.flat, src=0)
+                if hasattr(self.net.executor, 'repack'):
+                    self.net.executor.repack(self.net.target.flat)
 
     # ------------------------------------------------------------ graph
     def _capture(self):
@@ -280,7 +314,14 @@ class Learner:
                     with trace('allreduce'):
                         self.reducer.allreduce()
                 self._graphs[1].replay()
+        if self._own_target:
+            self._broadcast_owned_target()
         self.train_steps += 1
+        if self.reducer.xgmi is not None and self.train_steps % self._xgmi_check_every == 0:
+            # the in-graph xgmi kernel reports a timed-out peer wait through an error word (its
+            # gradient is then only partly reduced): read it off the hot path, fail loudly so the
+            # supervisor stops the run and the chief keeps its last consistent checkpoint
+            self.reducer.check()
         return self.loss
 
     def update_target_now(self, tau: float = 1.0):

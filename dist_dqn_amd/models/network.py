@@ -13,12 +13,16 @@ buffers:
   target_update_ops           -> update_target()    (one D2D copy / Polyak kernel)
   global_step                 -> global_step (device int64, advanced by the optimizer)
 
-Target parameters are always replicated per rank (reference default,
-`network.py:216-225`); `--disable_target_replication` makes rank 0 the owner
-and broadcasts it at update time (`parallel/dp.py`).
+Target parameters are replicated per rank (reference default,
+`network.py:216-225`). With `--disable_target_replication` (reference
+`network.py:226-231`: target on the PS) rank 0 owns the target: under sync DP
+the learner broadcasts rank 0's target after every target sync (`Learner`),
+under `--async_ps` the parameter server holds it and workers pull it when it
+changes (`parallel/async_ps.py`), and checkpoints carry ``target/*``.
 """
 from __future__ import annotations
 
+import logging
 from typing import Dict, Optional
 
 import torch
@@ -29,6 +33,8 @@ from . import torch_net
 from .arch import ArchSpec, arch_from_config
 from .executor import TorchExecutor
 from .params import ParamStore
+
+log = logging.getLogger(__name__)
 
 
 def resolve_device(config) -> torch.device:
@@ -54,9 +60,16 @@ def make_executor(arch: ArchSpec, layout, config, device: torch.device):
     if device.type == 'cuda' and backend in ('auto', 'hip') and arch.is_conv:
         from ..ops.executor import make_hip_executor, supports
         if supports(arch):
+            if config.dtype == 'fp32':
+                log.warning('--dtype=fp32 on the HIP conv executor: the MFMA network kernels compute in '
+                            'bf16 (fp32 accumulation, fp32 master weights, gradients and optimizer state); '
+                            'pass --dtype=bf16 to silence this, or --backend=torch for fp32 compute')
             return make_hip_executor(arch, layout, dtype=config.dtype, **kw)
         if backend == 'hip':
             raise RuntimeError('HIP executor does not support %s' % (arch,))
+        log.warning('HIP conv executor does not support this architecture (network=%s input=%s atoms=%s); '
+                    'falling back to the torch (MIOpen) executor, which is several times slower',
+                    arch.network, tuple(arch.input_shape), getattr(arch, 'atoms', None))
     return TorchExecutor(arch, layout, **kw)
 
 
@@ -225,6 +238,13 @@ class Network:
         if hasattr(self.executor, 'repack'):
             self.executor.repack(self.online.flat)
 
+    def refresh_packed(self):
+        """Rebuild the executor's packed copies of online AND target from their fp32 masters
+        (after a broadcast or restore; noisy nets re-mix under their bound noise samples)."""
+        if hasattr(self.executor, 'repack'):
+            self.executor.repack(self.online.flat)
+            self.executor.repack(self.target.flat)
+
     def hard_target_update(self, step: Optional[torch.Tensor] = None, freq: int = 1):
         """target <- online when step % freq == 0 (device predicate); fp32 master and the
         executor's packed copy move in ONE launch."""
@@ -275,6 +295,4 @@ class Network:
         tsd = {k[len('target/'):]: v for k, v in sd.items() if k.startswith('target/')}
         if tsd:
             self.target.load_state_dict(tsd)
-        self._repack()
-        if hasattr(self.executor, 'repack'):
-            self.executor.repack(self.target.flat)
+        self.refresh_packed()

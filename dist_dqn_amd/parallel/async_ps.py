@@ -13,9 +13,22 @@ gradient push IN ARRIVAL ORDER with the fused optimizer kernel, then answers
 that worker with the fresh parameters and global step. Workers (ranks >= 1)
 never wait for each other, so a push is applied to parameters other workers
 have moved since that worker's pull: the same staleness as the reference.
-Transport is torch.distributed point-to-point (RCCL send/recv over xGMI on
-the GPU, gloo on the CPU): one ``[n + 1]`` fp32 message each way per step,
-the extra slot carrying a header (push: +1 / goodbye: -1; reply: global step).
+
+Transport: torch.distributed point-to-point (RCCL send/recv over xGMI on the GPU,
+gloo on the CPU), one fp32 message each way per step: ``[n params (padded to even)]``
+followed by a 2 x int64 header viewed in place (kind, value), so ``global_step`` travels
+exactly (int64, not an fp32 that stops counting at 2^24).
+
+  worker -> PS kinds: PUSH, PUSH_SYNC_TARGET (apply, then target <- online on the PS),
+                      BYE (worker leaves)
+  PS -> worker kinds: PARAMS, PARAMS_TARGET (a second message with the PS-owned target
+                      follows), STOP (the PS is stopping: no more pushes)
+
+``--disable_target_replication`` (reference `network.py:226-231`: the target variables
+live on the PS): the PS owns the only target. A worker asks for the target sync at its own
+cadence with PUSH_SYNC_TARGET (the reference's workers run the assign ops against the PS
+target the same way, `dqn_agent.py:215-222`), and receives the PS target whenever it changed
+since that worker last saw it. Without the flag each worker keeps its own replicated target.
 """
 from __future__ import annotations
 
@@ -30,42 +43,81 @@ from .dist import DistContext
 
 log = logging.getLogger(__name__)
 
-PUSH, BYE = 1.0, -1.0
+PUSH, PUSH_SYNC_TARGET, BYE = 1, 2, -1
+PARAMS, PARAMS_TARGET, STOP = 0, 3, 4
+
+
+class _Msg:
+    """fp32 payload + int64 (kind, value) header in one contiguous buffer."""
+
+    def __init__(self, n: int, device):
+        self.n = n
+        self.pad = n + (n & 1)                  # 8-byte aligned header
+        self.buf = torch.zeros(self.pad + 4, dtype=torch.float32, device=device)
+        self.body = self.buf[:n]
+        self.hdr = self.buf[self.pad:].view(torch.int64)
+
+    def header(self):
+        k, v = self.hdr.tolist()
+        return int(k), int(v)
 
 
 class AsyncPSServer:
-    """Rank 0. ``net`` supplies the master parameters, gradient buffer and optimizer."""
+    """Rank 0. ``net`` supplies the master parameters, gradient buffer, optimizer and (with
+    ``own_target``) the PS-owned target."""
 
-    def __init__(self, ctx: DistContext, network):
+    def __init__(self, ctx: DistContext, network, own_target: Optional[bool] = None):
         assert ctx.enabled and ctx.rank == 0 and ctx.world_size >= 2, 'the PS is rank 0 of a world >= 2'
         self.ctx, self.net = ctx, network
         self.n = network.online.flat.numel()
         dev = network.online.flat.device
+        if own_target is None:
+            own_target = bool(getattr(network.config, 'disable_target_replication', False))
+        self.own_target = own_target
         self.workers = list(range(1, ctx.world_size))
-        self._in: Dict[int, torch.Tensor] = {w: torch.zeros(self.n + 1, device=dev) for w in self.workers}
-        self._out: Dict[int, torch.Tensor] = {w: torch.zeros(self.n + 1, device=dev) for w in self.workers}
+        self._in: Dict[int, _Msg] = {w: _Msg(self.n, dev) for w in self.workers}
+        self._out: Dict[int, _Msg] = {w: _Msg(self.n, dev) for w in self.workers}
+        self._tout: Dict[int, torch.Tensor] = ({w: torch.zeros(self.n, device=dev) for w in self.workers}
+                                               if own_target else {})
         self._recv: Dict[int, object] = {}
-        self._send: Dict[int, object] = {}
+        self._send: Dict[int, list] = {}
         # gloo completes a p2p receive only inside wait(), so there the server takes the
         # next push with ONE any-source receive; RCCL has no any-source receive, so there
         # it polls one posted irecv per worker (event queries)
         self._any_source = ctx.backend == 'gloo'
-        self._any = torch.zeros(self.n + 1, device=dev) if self._any_source else None
+        self._any = _Msg(self.n, dev) if self._any_source else None
         self.updates = 0
         self.per_worker = {w: 0 for w in self.workers}
+        self.target_version = 0
+        self.target_syncs = 0
+        self._seen_version = {w: -1 for w in self.workers}
+        self.stopped_workers = 0
 
-    def _reply(self, w: int):
-        if self._send.get(w) is not None:
-            self._send[w].wait()              # the previous snapshot for w has left
+    def _reply(self, w: int, kind: int = PARAMS):
+        for h in self._send.get(w) or []:
+            h.wait()                          # the previous snapshot for w has left
         out = self._out[w]
-        out[:self.n].copy_(self.net.online.flat)
-        out[self.n:].copy_(self.net.global_step.to(out.dtype).view(1))
-        self._send[w] = dist.isend(out, dst=w)
+        send_target = kind == PARAMS and self.own_target and self._seen_version[w] != self.target_version
+        if send_target:
+            kind = PARAMS_TARGET
+        out.body.copy_(self.net.online.flat)
+        out.hdr[0] = kind
+        out.hdr[1:2].copy_(self.net.global_step.view(1))
+        hs = [dist.isend(out.buf, dst=w)]
+        if send_target:
+            self._tout[w].copy_(self.net.target.flat)
+            hs.append(dist.isend(self._tout[w], dst=w))
+            self._seen_version[w] = self.target_version
+        self._send[w] = hs
+
+    def _post(self, w: int):
+        if not self._any_source:
+            self._recv[w] = dist.irecv(self._in[w].buf, src=w)
 
     def _next_push(self, active, idle_sleep: float):
         """(worker, message) of the next push to arrive."""
         if self._any_source:
-            w = dist.recv(self._any)
+            w = dist.recv(self._any.buf)
             return w, self._any
         while True:
             for w in sorted(active):
@@ -75,29 +127,40 @@ class AsyncPSServer:
                     return w, self._in[w]
             time.sleep(idle_sleep)
 
-    def serve(self, max_updates: int = 0, idle_sleep: float = 1e-4) -> int:
-        """Apply pushes until every worker said goodbye (or max_updates)."""
+    def serve(self, max_updates: int = 0, idle_sleep: float = 1e-4, supervisor=None) -> int:
+        """Apply pushes until every worker said goodbye (or max_updates). When ``supervisor``
+        asks to stop, every worker's next push is answered with STOP instead of applied."""
         for w in self.workers:                # initial pull: every worker starts from the PS params
             self._reply(w)
-            if not self._any_source:
-                self._recv[w] = dist.irecv(self._in[w], src=w)
+            self._post(w)
         active = set(self.workers)
         while active and not (max_updates and self.updates >= max_updates):
             w, msg = self._next_push(active, idle_sleep)
-            if float(msg[self.n]) == BYE:
+            kind, _ = msg.header()
+            if kind == BYE:
                 active.discard(w)
                 continue
+            if supervisor is not None and supervisor.should_stop():
+                self._reply(w, STOP)          # no further receive is posted for w
+                active.discard(w)
+                self.stopped_workers += 1
+                continue
             # arrival-order apply: grad -> fused optimizer (global_step += 1 inside)
-            self.net.grad.copy_(msg[:self.n])
+            self.net.grad.copy_(msg.body)
             self.net.apply_grads(1.0)
+            if kind == PUSH_SYNC_TARGET and self.own_target:
+                self.net.update_target(1.0)
+                self.target_version += 1
+                self.target_syncs += 1
             self.updates += 1
             self.per_worker[w] += 1
             self._reply(w)
-            if not self._any_source:
-                self._recv[w] = dist.irecv(self._in[w], src=w)
+            self._post(w)
+            if supervisor is not None:
+                supervisor.on_train_step(self.updates)
         for w in self.workers:
-            if self._send.get(w) is not None:
-                self._send[w].wait()
+            for h in self._send.get(w) or []:
+                h.wait()
         return self.updates
 
 
@@ -108,23 +171,44 @@ class AsyncPSClient:
         assert ctx.enabled and ctx.rank >= 1
         self.ctx = ctx
         self.n = flat.numel()
-        self._out = torch.zeros(self.n + 1, device=flat.device)
-        self._in = torch.zeros(self.n + 1, device=flat.device)
+        self._out = _Msg(self.n, flat.device)
+        self._in = _Msg(self.n, flat.device)
         self.pushes = 0
+        self.stopped = False           # the PS answered STOP: push nothing more
+        self.target_updated = False    # the last pull also brought the PS-owned target
 
-    def pull(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
-        dist.recv(self._in, src=0)
-        flat.copy_(self._in[:self.n])
+    def pull(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None,
+             target: Optional[torch.Tensor] = None):
+        dist.recv(self._in.buf, src=0)
+        kind, _ = self._in.header()
+        if kind == STOP:
+            self.stopped = True
+            return
+        flat.copy_(self._in.body)
         if global_step is not None:
-            global_step.copy_(self._in[self.n:].to(global_step.dtype).view_as(global_step))
+            global_step.copy_(self._in.hdr[1:2].view_as(global_step))
+        self.target_updated = False
+        if kind == PARAMS_TARGET:
+            if target is None:
+                target = torch.empty_like(flat)       # keep the p2p sequence intact
+            dist.recv(target, src=0)
+            self.target_updated = True
 
-    def exchange(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
-        self._out[:self.n].copy_(grad)
-        self._out[self.n] = PUSH
-        dist.send(self._out, dst=0)
+    def exchange(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None,
+                 sync_target: bool = False, target: Optional[torch.Tensor] = None) -> bool:
+        """Push ``grad``, pull the parameters; False once the PS has said STOP."""
+        if self.stopped:
+            return False
+        self._out.body.copy_(grad)
+        self._out.hdr[0] = PUSH_SYNC_TARGET if sync_target else PUSH
+        self._out.hdr[1] = self.pushes
+        dist.send(self._out.buf, dst=0)
         self.pushes += 1
-        self.pull(flat, global_step)
+        self.pull(flat, global_step, target)
+        return not self.stopped
 
     def close(self):
-        self._out[self.n] = BYE
-        dist.send(self._out, dst=0)
+        if self.stopped:
+            return                     # the PS already dropped this worker
+        self._out.hdr[0] = BYE
+        dist.send(self._out.buf, dst=0)

@@ -30,10 +30,30 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device('cpu')
     backend: str = 'none'
+    # control plane: a gloo group over the same ranks (the default group itself when that is
+    # gloo). Stop agreement, restored-path/sidecar broadcast and replica fingerprints go here,
+    # as CPU tensors, so they never queue behind (or synchronise with) the GPU stream.
+    ctrl_group: object = None
 
     @property
     def is_chief(self) -> bool:
         return self.rank == 0
+
+    def ctrl_allreduce_max(self, value: int) -> int:
+        """max over ranks of a host integer (control plane; no GPU involvement)."""
+        if not self.enabled:
+            return int(value)
+        t = torch.tensor([int(value)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl_group)
+        return int(t)
+
+    def ctrl_broadcast_object(self, obj, src: int = 0):
+        """rank ``src``'s picklable ``obj`` on every rank (control plane)."""
+        if not self.enabled:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.ctrl_group)
+        return box[0]
 
     @property
     def enabled(self) -> bool:
@@ -90,7 +110,10 @@ def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600) ->
             if use_gpu and backend == 'nccl':
                 kw['device_id'] = dev
             dist.init_process_group(**kw)
-    return DistContext(rank, world, local_rank, dev, backend)
+    ctrl = None
+    if world > 1 and backend != 'gloo':
+        ctrl = dist.new_group(backend='gloo', timeout=datetime.timedelta(seconds=timeout_s))
+    return DistContext(rank, world, local_rank, dev, backend, ctrl)
 
 
 def shutdown(ctx: Optional[DistContext] = None):

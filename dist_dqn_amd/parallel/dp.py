@@ -75,16 +75,43 @@ class GradAllReducer:
                 raise RuntimeError('xgmi all-reduce failed its self-test')
             log.warning('xgmi all-reduce failed its self-test; using RCCL')
             return None
+        agree = self._cross_check(x)
+        if not agree:
+            x.close()
+            if mode == 'xgmi':
+                raise RuntimeError('xgmi all-reduce disagrees with RCCL on the gradient buffer')
+            log.warning('xgmi all-reduce disagrees with RCCL on the gradient buffer; using RCCL')
+            return None
         if mode == 'auto':
             t_x = self._time(lambda t: x.allreduce(t, 0))
             t_r = self._time(lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM))
-            self.timings = {'xgmi_us': t_x, 'rccl_us': t_r}
+            self.timings.update(xgmi_us=t_x, rccl_us=t_r)
             if self.ctx.is_chief:
                 log.info('gradient all-reduce (%d elems): xgmi %.1f us, rccl %.1f us', n, t_x, t_r)
             if t_x > t_r:
                 x.close()
                 return None
         return x
+
+    def _cross_check(self, x) -> bool:
+        """Start-up consistency check on the real gradient size: the xgmi sum of random
+        gradients must match RCCL's (to summation-order rounding: fp32 1e-5 relative, bf16 wire
+        2e-2) and be bit-identical on every rank (the replicas' invariant). Agreed on all ranks."""
+        n = self.flat.numel()
+        g = torch.Generator(device=self.flat.device).manual_seed(1234 + self.ctx.rank)
+        t = torch.randn(n, generator=g, device=self.flat.device)
+        a, b = t.clone(), t.clone()
+        x.allreduce(a, 0)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        ref = a.clone()
+        dist.broadcast(ref, src=0)
+        rel = float(((a - b).abs().max() / b.abs().max().clamp_min(1e-30)))
+        tol = 2e-2 if self.wire_dtype == 'bf16' else 1e-5
+        ok = torch.tensor([1 if (rel <= tol and torch.equal(ref, a) and x.check()) else 0], dtype=torch.int32,
+                          device=self.flat.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        self.timings['xgmi_vs_rccl_max_rel'] = rel
+        return bool(int(ok))
 
     def _time(self, fn, iters: int = 20) -> float:
         """Mean us per call over ``iters`` (after 3 warm-up calls), max over ranks."""
@@ -170,9 +197,50 @@ class GradAllReducer:
 
 
 def broadcast_flat(ctx: DistContext, flat: torch.Tensor, src: int = 0):
-    """Reference M8/M6: chief's initialised (or restored) parameters to every rank."""
+    """One flat buffer from ``src`` to every rank."""
     if ctx.enabled:
         dist.broadcast(flat, src=src)
+
+
+def state_tensors(net) -> List[Tuple[str, torch.Tensor]]:
+    """Every device tensor that must be identical on all sync-DP replicas: online and target
+    parameters, every optimizer slot, Adam's beta powers, the device global_step and, for
+    noisy nets, the current noise samples and the device Philox state that draws the next."""
+    out = [('online', net.online.flat), ('target', net.target.flat), ('global_step', net.global_step)]
+    out += [('slot/%s' % n, s) for n, s in zip(net.optimizer.slot_names(), net.optimizer.slots)]
+    out.append(('beta_powers', net.optimizer.beta_powers))
+    for name in ('noise', 'noise_target', 'noise_rng'):
+        t = getattr(net, name, None)
+        if t is not None:
+            out.append((name, t))
+    return out
+
+
+def broadcast_state(ctx: DistContext, net, src: int = 0):
+    """Reference M8 (Supervisor init / restore, `/root/reference/src/main.py:136-143,155`): the
+    chief's initialised or restored state reaches every rank — parameters, target, optimizer
+    slots, beta powers, global_step and the noise stream — and every rank then rebuilds its
+    packed MFMA fragments (noisy nets: re-mixed under the broadcast noise)."""
+    if not ctx.enabled:
+        return
+    for _, t in state_tensors(net):
+        dist.broadcast(t, src=src)
+    net.refresh_packed()
+
+
+def check_state_equal(ctx: DistContext, net) -> dict:
+    """{tensor name: bit-equal to rank 0 on every rank} over `state_tensors` (host sync)."""
+    out = {}
+    for name, t in state_tensors(net):
+        if not ctx.enabled:
+            out[name] = True
+            continue
+        ref = t.clone()
+        dist.broadcast(ref, src=0)
+        same = torch.tensor([1 if torch.equal(ref, t) else 0], dtype=torch.int32, device=t.device)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        out[name] = bool(int(same))
+    return out
 
 
 def check_replicas_equal(ctx: DistContext, flat: torch.Tensor) -> bool:

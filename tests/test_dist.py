@@ -186,3 +186,107 @@ def _worker_bf16_wire(rank, world, port, tmpdir):
 
 def test_allreduce_bf16_wire(tmp_path):
     mp.spawn(_worker_bf16_wire, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def _worker_broadcast_state(rank, world, port, tmpdir):
+    """Chief-only restore, then broadcast_state: every replica tensor equal on every rank."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import broadcast_state, check_state_equal, init_distributed
+    cfg = parse_args(['--device=cpu', '--seed=%d' % (10 + rank), '--optimizer=adam', '--network=cnn'])
+    ctx = init_distributed(cfg, device='cpu')
+    net = Network.create_network(cfg, (84, 84, 4), 6)
+    if rank == 0:                      # the chief "restored" a trained state
+        net.global_step.fill_(123456789)
+        net.optimizer.slots[1].fill_(0.5)
+        net.optimizer.beta_powers.fill_(0.25)
+        net.target.flat.mul_(2.0)
+    assert not all(check_state_equal(ctx, net).values())
+    broadcast_state(ctx, net)
+    eq = check_state_equal(ctx, net)
+    assert all(eq.values()), eq
+    assert int(net.global_step) == 123456789 and float(net.optimizer.beta_powers[0]) == 0.25
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_state_world2(tmp_path):
+    mp.spawn(_worker_broadcast_state, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def _worker_async_owned_target(rank, world, port, tmpdir):
+    """--disable_target_replication under --async_ps: the PS owns the target, a worker's sync
+    request copies PS online -> PS target, and the new target reaches the workers; the int64
+    header carries a global_step beyond fp32's exact range."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import broadcast_flat, init_distributed
+    from dist_dqn_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
+    cfg = parse_args(['--device=cpu', '--seed=7', '--optimizer=sgd', '--lr=1.0', '--reg_param=0',
+                      '--disable_target_replication'])
+    ctx = init_distributed(cfg, device='cpu')
+    net = Network.create_network(cfg, (4,), 2)
+    broadcast_flat(ctx, net.online.flat)
+    big = (1 << 24) + 1                 # not representable in fp32
+    if rank == 0:
+        net.global_step.fill_(big)
+        net.target.flat.fill_(3.0)
+        srv = AsyncPSServer(ctx, net)
+        assert srv.own_target
+        srv.serve()
+        assert srv.target_syncs == 1
+        torch.testing.assert_close(net.target.flat, net.online.flat + 1.0)   # synced before push 2
+    else:
+        cli = AsyncPSClient(ctx, net.online.flat)
+        cli.pull(net.online.flat, net.global_step, target=net.target.flat)
+        assert int(net.global_step) == big and cli.target_updated
+        assert bool((net.target.flat == 3.0).all())                     # the PS-owned target arrived
+        ones = torch.ones_like(net.online.flat)
+        cli.exchange(ones, net.online.flat, net.global_step, sync_target=True, target=net.target.flat)
+        assert cli.target_updated and torch.equal(net.target.flat, net.online.flat)
+        assert int(net.global_step) == big + 1
+        cli.exchange(ones, net.online.flat, net.global_step, target=net.target.flat)
+        assert not cli.target_updated and int(net.global_step) == big + 2
+        cli.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_ps_owned_target_and_int64_step(tmp_path):
+    mp.spawn(_worker_async_owned_target, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def _worker_sync_owned_target(rank, world, port, tmpdir):
+    """Sync DP + --disable_target_replication: rank 0's target is broadcast after each sync."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from dist_dqn_amd.config import parse_args
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel import broadcast_state, check_state_equal, init_distributed
+    from dist_dqn_amd.replay import DeviceReplay
+    cfg = parse_args(['--device=cpu', '--seed=5', '--network=cnn', '--optimizer=rmsprop', '--minibatch_size=4',
+                      '--target_update_freq=2', '--replay_memory_capacity=64', '--disable_target_replication'])
+    ctx = init_distributed(cfg, device='cpu')
+    net = Network.create_network(cfg, (84, 84, 4), 6)
+    broadcast_state(ctx, net)
+    rep = DeviceReplay(64, (84, 84), 4, device='cpu', seed=rank)
+    rep.fill_synthetic(64, 6, seed=rank, episode_len=16)
+    ln = Learner(net, rep, cfg, ctx)
+    assert ln._own_target
+    for _ in range(4):
+        ln.step()
+        if rank == 1:                   # a stray local target write is overwritten by rank 0's copy
+            net.target.flat.add_(1.0)
+    eq = check_state_equal(ctx, net)
+    assert eq['online'] and eq['global_step'] and not eq['target']     # step 4 was a sync, then rank 1 wrote
+    ln.step()
+    ln.step()                           # step 6 syncs + broadcasts again
+    assert all(check_state_equal(ctx, net).values())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sync_dp_owned_target_broadcast(tmp_path):
+    mp.spawn(_worker_sync_owned_target, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)

@@ -111,19 +111,20 @@ def _worker(rank, world, port, network, extra, errq):
         from dist_dqn_amd.config import preset
         from dist_dqn_amd.learner import Learner
         from dist_dqn_amd.models.network import Network
-        from dist_dqn_amd.parallel import broadcast_flat, check_replicas_equal, init_distributed
+        from dist_dqn_amd.parallel import broadcast_state, check_state_equal, init_distributed
         from dist_dqn_amd.replay import DeviceReplay
         outs = {}
         ctx = None
         for overlap in (1, 0):
-            cfg = preset(network, 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=2048 '
-                         '--overlap_allreduce=%d %s' % (overlap, extra))
+            # a different init seed per rank: broadcast_state must carry EVERYTHING (params, target,
+            # slots, noise stream) and every rank must rebuild its packed / premixed fragments
+            cfg = preset(network, 'Pong-v0', '--seed=%d --backend=hip --replay_memory_capacity=2048 '
+                         '--overlap_allreduce=%d %s' % (3 + rank, overlap, extra))
             if ctx is None:
                 ctx = init_distributed(cfg, device='cuda')
                 assert ctx.world_size == world and ctx.backend == 'gloo' and ctx.device.index == 0
             net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
-            broadcast_flat(ctx, net.online.flat)
-            net.target.copy_from(net.online)
+            broadcast_state(ctx, net)
             rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
             rep.fill_synthetic(2048, 6, seed=rank)          # different data per rank
             ln = Learner(net, rep, cfg, ctx)
@@ -134,7 +135,8 @@ def _worker(rank, world, port, network, extra, errq):
             assert torch.isfinite(ln.loss).all()
             if ln.reducer.xgmi is not None:
                 ln.reducer.check()                          # a timed-out peer wait raises here
-            assert check_replicas_equal(ctx, net.online.flat), 'replicas diverged (overlap=%d)' % overlap
+            eq = check_state_equal(ctx, net)
+            assert all(eq.values()), 'replicas diverged (overlap=%d): %s' % (overlap, eq)
             assert int(net.global_step) == 6
             xgmi = '--allreduce=xgmi' in extra
             assert ln.reducer.mode == ('xgmi' if xgmi else 'rccl')
@@ -171,3 +173,23 @@ def _worker(rank, world, port, network, extra, errq):
 def test_dp_learner_two_ranks_one_gpu(network, extra):
     """(--allreduce=rccl means the process group's collective: gloo in this rehearsal.)"""
     _run_ranks(_worker, (network, extra))
+
+
+def test_bench_two_ranks_replicas_equal(tmp_path):
+    """bench.py under torchrun (2 ranks on one GPU over gloo): the JSON line reports the
+    end-of-run replica check, the world size and the transport."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DQN_DIST_BACKEND='gloo', OMP_NUM_THREADS='4')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(root, 'bench.py'),
+           '--gpus', '2', '--steps', '20', '--warmup', '5', '--replay', '20000', '--actor_envs', '0']
+    out = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith('{')][-1]
+    d = json.loads(line)
+    assert d['n_gpus'] == 2 and d['config']['world_size'] == 2
+    assert d['config']['replicas_equal'] is True and d['config']['replicas_diverged'] == []
+    assert d['config']['dist_backend'] == 'gloo'
