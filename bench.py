@@ -102,7 +102,7 @@ def main():
         step()
     ctx.barrier()
     torch.cuda.synchronize(dev)
-    frames0 = actor.env_frames() if actor is not None else 0
+    frames0 = actor.env_frames if actor is not None else 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -114,7 +114,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t)
     # env frames the device actors actually stepped in the timed region (device counter), summed
-    frames = torch.tensor([(actor.env_frames() - frames0) if actor is not None else 0], dtype=torch.float64,
+    frames = torch.tensor([(actor.env_frames - frames0) if actor is not None else 0], dtype=torch.float64,
                           device=dev)
     if ctx.enabled:
         dist.all_reduce(frames)

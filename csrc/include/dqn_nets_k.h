@@ -38,6 +38,12 @@ struct ConvArgs {
   int IH, IW, OH, OW, pad_t, pad_l;
   const void* frames;        // frame ring [F][H*W] u8 for the frame-slot conv1 loader
   int frame_hw;
+  // optional side duties of the launch (null = off): zero [zero_ptr, +zero_n) (a gradient range
+  // the conv weight gradients later accumulate into with atomics), and (block 0) loss_out[0] =
+  // loss_mul * sum of loss_parts[0..nparts) (the scalar head's per-tile loss partials)
+  float* zero_ptr; int zero_n;
+  const float* loss_parts; int nparts;
+  float* loss_out; float loss_mul;
 };
 
 struct WgradArgs {
@@ -100,6 +106,11 @@ struct HeadArgs {
   const float* vli[3];           // C51 dueling: precomputed value logits [B][atoms]
   const float* act_lgi;          // C51 + fused acting: the actors' logits [E][A*atoms] (+ act_vli [E][atoms])
   const float* act_vli;
+  // scalar heads (head_loss_kernel): per-16-sample-tile loss partials (summed by the fc dgrad
+  // launch) and dL/dQ as act_t [B][64] (plain / advantage in columns 0..31, value in 32), the dZ
+  // operand of the output layer's grouped weight-gradient members; dH goes to dh
+  float* loss_parts;
+  void* dq16;
 };
 
 // One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =
@@ -157,11 +168,12 @@ struct CnnBwdArgs {
 };
 
 // Grouped weight-gradient launch (qnet.hip): up to 4 independent layers.
+constexpr int kMaxWgradMembers = 6;
 struct WgradGroup {
-  ConvArgs a[4];
-  WgradArgs g[4];
-  int kind[4];
-  int nblk[4], gx[4], gy[4];     // filled by the launcher
+  ConvArgs a[kMaxWgradMembers];
+  WgradArgs g[kMaxWgradMembers];
+  int kind[kMaxWgradMembers];
+  int nblk[kMaxWgradMembers], gx[kMaxWgradMembers], gy[kMaxWgradMembers];     // filled by the launcher
   int n;
 };
 
@@ -170,6 +182,7 @@ enum LayerKind {
   L_DENSE_FWD_RELU = 4, L_DENSE_FWD_F32 = 5, L_DENSE_DGRAD = 6,
   L_NAT_CONV3_DGRAD = 7, L_NAT_CONV2_DGRAD = 8,
   L_NAT_CONV1_FRAMES = 9,   // conv1 reading the frame ring through a [B][4] slot table
+  L_HEAD_WGRAD = 11,        // output layer weight gradient (grouped wgrad member: N <= 32)
 };
 
 }  // namespace dqn

@@ -17,6 +17,8 @@
 //                      bias gradient fused, fp32 atomics only across M-chunks;
 //   * head_loss_kernel output layer + dueling combine + TD loss + dQ + head backward
 //                      (dW, db, dH masked by ReLU) in ONE workgroup.
+#include <stdio.h>
+#include <stdlib.h>
 #include "common.h"
 #include "actor_dev.h"
 #include "../include/dqn_nets_k.h"
@@ -253,6 +255,24 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   for (int i = 0; i < MT; ++i) ld[i] = LD(a, inst, m_base + i * 16 + (lane & 15));
   const int kg = 8 * (lane >> 4);
   const int ks_lo = (K32 * wk) / KSPLIT, ks_hi = (K32 * (wk + 1)) / KSPLIT;
+  // EPI 2: the ReLU-mask operand of the epilogue is loaded NOW (clamped indices, no branch
+  // per load) so its latency hides under the k-loop instead of serialising the epilogue
+  float mk[EPI == 2 ? MT : 1][EPI == 2 ? NT : 1][4];
+  if constexpr (EPI == 2) {
+    if (wk == 0) {
+      const act_t* __restrict__ msrc = reinterpret_cast<const act_t*>(a.mask[inst]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = min((nt_base + j) * 16 + (lane & 15), a.N - 1);
+            const int m = min(m_base + i * 16 + 4 * (lane >> 4) + r, a.M - 1);
+            mk[i][j][r] = (float)msrc[(int64_t)m * a.ldo + n];
+          }
+    }
+  }
   // U k-steps per batch: all A/B fragment loads of the batch are issued before
   // its MFMAs, so U x (MT + NT) global loads are in flight per wave (the loop
   // is latency-bound at these sizes, not MFMA-bound). A partial last batch is
@@ -298,6 +318,19 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += red[(((slot + s) * MT + i) * NT + j) * 256 + r * 64 + lane];
   }
+  // side duties of the launch (ConvArgs aux): zero a gradient range (the conv weight gradients
+  // accumulate into it with atomics later in the step) and sum the head's per-tile loss partials
+  if (a.zero_ptr != nullptr) {
+    const int nblk = gridDim.x * gridDim.y * gridDim.z;
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
+    for (int t = blk * 64 + lane; t < a.zero_n / 4; t += nblk * 64) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (a.loss_parts != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+    const float v = lane < a.nparts ? a.loss_parts[lane] : 0.f;
+    const float sl = wave_sum(v);
+    if (lane == 0) a.loss_out[0] = sl * a.loss_mul;
+  }
   // epilogue: C/D layout col = lane & 15, row = 4*(lane >> 4) + r
   const float scale = a.scale[inst];
   const float* __restrict__ bias = a.bias[inst];
@@ -320,8 +353,7 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
         } else if constexpr (EPI == 1) {
           reinterpret_cast<float*>(a.out[inst])[o] = v * scale + bv;
         } else {
-          const float mk = (float)reinterpret_cast<const act_t*>(a.mask[inst])[o];
-          reinterpret_cast<act_t*>(a.out[inst])[o] = (act_t)(mk > 0.f ? v : 0.f);
+          reinterpret_cast<act_t*>(a.out[inst])[o] = (act_t)(mk[i][j][r] > 0.f ? v : 0.f);
         }
       }
     }
@@ -436,162 +468,216 @@ __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
 }
 
 // =========================================================== fused head + loss
-// Instances of the last hidden layer H (bf16): h[0] = online(s), h[1] = target(s'),
-// h[2] = online(s') (Double DQN). Plain: Q = H W + b. Dueling: H = [Hv | Ha],
-// Q = (Hv wv + bv) + (Ha Wa + ba) - mean_a(Ha Wa + ba).
-// Q tiles come from MFMA over packed head fragments (16 rows x 16 actions per
-// wave task); the TD loss, dQ and the head backward (dW, db, dH masked by
-// ReLU(H) > 0) follow in the same workgroup.
-// head_body: one workgroup's share (blk of nblk) of the head. B / h0 / infer / actor /
-// q_out / zeroing are parameters so the fused-acting block can run the acting path
-// on the actors' hidden layer inside the learner's launch.
-constexpr int kHeadPartFloats = 16 * 64 * 4;
-constexpr int kHeadActorScratch = 64;          // actor LDS scratch after red[32] (E <= 64)
-constexpr int kHeadMaxA = 32;                  // output biases staged in LDS up to this many actions
-DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h0, const bool infer,
-                       const bool has_actor, float* q_out, const bool do_zero, const int blk, const int nblk) {
-  const int A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID;
-  float* part_lds = hsm;                    // [16 waves][64][4] split-K partial Q tiles
-  float* q = hsm + kHeadPartFloats;         // [3][B][A]
-  float* vv = q + 3 * B * A;                // [3][B] dueling value stream
-  float* dq = vv + 3 * B;                   // [B][A]  dL/dQ (dueling: dL/dA)
-  float* dv = dq + B * A;                   // [B]     dueling: dL/dV
-  float* red = dv + B;                      // [32] (+ actor scratch)
-  float* bl = red + 32 + kHeadActorScratch; // [3][A] output bias, [3] value bias (A <= kHeadMaxA)
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int lane = tid & 63, wave = tid >> 6, nwave = nth >> 6;
-  const int ninst = infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
-  auto hptr = [&](int inst) { return inst == 0 && h0 != nullptr ? h0 : a.h[inst]; };
-  // phase stamps (scripts/probe_head.py): learner block 0 -> prof[0..7], acting block -> prof[16..19]
-  int64_t* prof = (a.prof != nullptr && tid == 0 && blk == 0) ? a.prof + (infer && has_actor ? 16 : 0) : nullptr;
-#define HEAD_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
-  HEAD_MARK(0);
-  ActorPre apre{};
-  if (infer && has_actor) apre = actor_prefetch(a.actor);   // loads overlap the Q tiles
-  float tr = 0.f, tg = 0.f, td = 0.f, tw = 1.f;              // this thread's sample (TD loss)
-  int ta = 0;
-  if (!infer && tid < B) {
-    tr = a.rew[tid]; tg = a.gam[tid]; td = a.done[tid]; ta = a.act[tid];
-    if (a.wts != nullptr) tw = a.wts[tid];
-  }
-  // Small operands of the later phases are loaded NOW, so their latency hides under the
-  // Q-tile loads: the TD-loss inputs (registers) and the output biases (LDS). (The dW / dH
-  // operands are NOT: their ~50 loads per thread would queue ahead of the Q-tile loads.)
-  const bool bias_lds = A <= kHeadMaxA;
-  if (bias_lds) {
-    for (int t = tid; t < ninst * A; t += nth) bl[t] = a.b[t / A][t % A];
-    if (a.dueling && tid < ninst) bl[3 * kHeadMaxA + tid] = a.bv[tid][0];
-  }
-  const int gt = blk * nth + tid, gn = nblk * nth;
-  const act_t* hb0 = reinterpret_cast<const act_t*>(a.h[0]);
-  const act_t* ha0 = a.dueling ? hb0 + HID : hb0;
-  const float* W0 = a.w[0];
-  // ---- 1. Q tiles on MFMA: task = (instance, 16-row tile, n-tile); the dueling value
-  // stream is one extra n-tile. The K loop of every task is split over kspl waves (all
-  // waves busy, one batch of loads in flight per wave); partial tiles meet in LDS.
-  const int mtiles = (B + 15) / 16, K32 = HID / 32, ntl = a.N16 + (a.dueling ? 1 : 0);
-  const int ntask = ninst * mtiles * ntl;
-  int kspl = nwave / ntask;
-  kspl = kspl < 1 ? 1 : (kspl > K32 ? K32 : kspl);
-  const int kps = (K32 + kspl - 1) / kspl;                 // k-steps per wave part
-  for (int wt = wave; wt < ntask * kspl; wt += nwave) {
-    const int task = wt / kspl, part = wt - task * kspl;
-    const int nt = task % ntl, im = task / ntl;
-    const int inst = im / mtiles, mt = im - inst * mtiles;
-    const int b_row = mt * 16 + (lane & 15);
-    const bool rok = b_row < B;
-    const act_t* hrow = reinterpret_cast<const act_t*>(hptr(inst)) + (int64_t)(rok ? b_row : 0) * HH;
-    const act_t* ha = a.dueling ? hrow + HID : hrow;
-    const bfx8* pw = reinterpret_cast<const bfx8*>(a.pw[inst]);
-    const bfx8* pv = reinterpret_cast<const bfx8*>(a.pwv[inst]);
-    const int kg = 8 * (lane >> 4);
-    const bool val = nt == a.N16;
-    const act_t* src = val ? hrow : ha;
-    const int k_lo = part * kps, k_hi = min(K32, k_lo + kps);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = k_lo; ks < k_hi; ks += 4) {            // 4 k-steps of loads in flight per batch
-      bfx8 af[4], bf[4];
+// Scalar heads (plain or dueling; MSE or Huber TD loss): output layer + TD loss + dL/dQ.
+// Parallel over samples: each LEARNER block owns a 16-sample tile, computes its rows of Q
+// for every instance (online(s), target(s'), online(s') for Double DQN) on MFMA with the
+// K loop split over 8 waves (every load of the block issued in ONE batch: h fragments,
+// packed output-layer fragments, TD inputs, biases), then the TD loss, |TD| priorities,
+// dL/dQ (published as dqv [B][A + 1] = dQ | dV for the fused fc dgrad, which carries the
+// head backward) and its loss partial (summed by the fc dgrad launch). Fused acting: one
+// ACTING block per env computes that env's 16-row Q tile with the online weights, then the
+// env's eps-greedy decision, synthetic frame and replay append; the last acting block to
+// arrive (ticket) advances the cursors / eps / rng (and inserts into the PER tree).
+// INFER blocks (q_values) write their rows of Q.
+constexpr int kHeadRows = 16, kHeadWaves = 8, kHeadThreads = 64 * kHeadWaves;
+constexpr int kHeadKPW = 2;                     // k-steps per wave: HID <= 32 * kHeadWaves * kHeadKPW = 512
+constexpr int kHeadMaxNt = 3;                   // n-tiles: A <= 32 (2) + the dueling value tile
+constexpr int kHeadMaxW = 512 * 33;             // output layer staged for dH: HID * A (+ HID) floats
+struct HeadSmem {
+  float part[kHeadWaves][3][kHeadMaxNt][256];  // per-wave split-K partial tiles
+  float q[3][kHeadRows][32];                   // Q rows of the block's tile
+  float v[3][kHeadRows];                       // dueling value stream
+  float dq[kHeadRows][33];                     // dL/dQ rows (| dV)
+  float w[kHeadMaxW];                          // online output layer: W [HID][A] then w_v [HID]
+  float red[kHeadWaves];
+  SumtreeLds st;                               // acting: PER insert scratch
+  int flag;
+};
+
+// Q[inst][r][*] (+ V) of rows r0..r0+15 for ninst instances into S.q / S.v. Instance i reads
+// hidden layer hs[i] and packed weights pw[wi[i]] / pwv[wi[i]]; biases b[wi[i]], bv[wi[i]].
+DQN_DEV void head_q_tile(const HeadArgs& a, HeadSmem& S, const void* h0, const void* h1, const void* h2,
+                         int w0, int w1, int w2, const int ninst, const int r0, const int nrows,
+                         bfx8 (*h0f)[2] = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int A = a.A, HID = a.HID, HH = a.dueling ? 2 * HID : HID, K32 = HID / 32;
+  const int ntl = a.N16 + (a.dueling ? 1 : 0);
+  const int kg = 8 * (lane >> 4);
+  const int row = min(r0 + (lane & 15), r0 + nrows - 1);          // clamped: no branch per load
+  const int ks0 = wave * kHeadKPW;
+  // one batch: every A / B fragment of this wave (<= 3 inst x 2 k-steps x (2 A + 3 B))
+  bfx8 af[3][kHeadKPW][2], bf[3][kHeadKPW][kHeadMaxNt];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool kok = ks + u < k_hi;
-        af[u] = rok && kok ? *reinterpret_cast<const bfx8*>(src + (ks + u) * 32 + kg) : zero8();
-        bf[u] = !kok ? zero8() : val ? pv[(ks + u) * 64 + lane] : pw[((ks + u) * a.N16 + nt) * 64 + lane];
-      }
+  for (int i = 0; i < 3; ++i) {
+    const int ii = i < ninst ? i : 0;
+    const act_t* hr = reinterpret_cast<const act_t*>(ii == 0 ? h0 : ii == 1 ? h1 : h2) + (int64_t)row * HH;
+    const int wi = ii == 0 ? w0 : ii == 1 ? w1 : w2;
+    const bfx8* pw = reinterpret_cast<const bfx8*>(wi == 0 ? a.pw[0] : wi == 1 ? a.pw[1] : a.pw[2]);
+    const bfx8* pv = reinterpret_cast<const bfx8*>(wi == 0 ? a.pwv[0] : wi == 1 ? a.pwv[1] : a.pwv[2]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = mfma16(af[u], bf[u], acc);
-    }
-    if (kspl > 1) {
-      *reinterpret_cast<f32x4*>(part_lds + (wt * 64 + lane) * 4) = acc;
-      continue;
-    }
-    const int act = nt * 16 + (lane & 15);
+    for (int u = 0; u < kHeadKPW; ++u) {
+      const int ks = min(ks0 + u, K32 - 1);
+      af[i][u][0] = *reinterpret_cast<const bfx8*>(hr + (a.dueling ? HID : 0) + ks * 32 + kg);   // plain / adv
+      af[i][u][1] = a.dueling ? *reinterpret_cast<const bfx8*>(hr + ks * 32 + kg) : zero8();     // value
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = mt * 16 + 4 * (lane >> 4) + r;
-      if (val) {
-        if ((lane & 15) == 0 && b < B) vv[inst * B + b] = acc[r] + a.bv[inst][0];
-      } else if (b < B && act < A) {
-        q[(inst * B + b) * A + act] = acc[r] + a.b[inst][act];
+      for (int t = 0; t < kHeadMaxNt; ++t) {
+        const bool isv = a.dueling && t == a.N16;
+        const int tt = min(t, a.N16 - 1);
+        bf[i][u][t] = t >= ntl ? zero8() : isv ? pv[ks * 64 + lane] : pw[(ks * a.N16 + tt) * 64 + lane];
       }
     }
   }
-  if (kspl > 1) {                                          // (the bias LDS is written before this barrier)                                          // sum the parts of every task
-    __syncthreads();
-    for (int t = tid; t < ntask * 64; t += nth) {
-      const int task = t >> 6, ln = t & 63;
-      const int nt = task % ntl, im = task / ntl;
-      const int inst = im / mtiles, mt = im - inst * mtiles;
+  if (h0f != nullptr) {                        // instance 0's h fragments (the learner's dH mask)
+#pragma unroll
+    for (int u = 0; u < kHeadKPW; ++u) { h0f[u][0] = af[0][u][0]; h0f[u][1] = af[0][u][1]; }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= ninst) break;
+#pragma unroll
+    for (int t = 0; t < kHeadMaxNt; ++t) {
+      if (t >= ntl) break;
+      const bool isv = a.dueling && t == a.N16;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int p = 0; p < kspl; ++p) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(part_lds + ((task * kspl + p) * 64 + ln) * 4);
-        acc += v;
-      }
-      const bool val = nt == a.N16;
-      const int act = nt * 16 + (ln & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = mt * 16 + 4 * (ln >> 4) + r;
-        if (val) {
-          if ((ln & 15) == 0 && b < B) vv[inst * B + b] = acc[r] + (bias_lds ? bl[3 * kHeadMaxA + inst] : a.bv[inst][0]);
-        } else if (b < B && act < A) {
-          q[(inst * B + b) * A + act] = acc[r] + (bias_lds ? bl[inst * A + act] : a.b[inst][act]);
-        }
-      }
+      for (int u = 0; u < kHeadKPW; ++u)
+        if (ks0 + u < K32) acc = mfma16(af[i][u][isv ? 1 : 0], bf[i][u][t], acc);
+      *reinterpret_cast<f32x4*>(&S.part[wave][i][t][lane * 4]) = acc;
     }
   }
   __syncthreads();
-  HEAD_MARK(1);
+  // sum the 8 waves' partial tiles; C/D layout: col = lane & 15, row = 4 * (lane >> 4) + r
+  for (int e = tid; e < ninst * ntl * 256; e += kHeadThreads) {
+    const int i = e / (ntl * 256), rem = e - i * ntl * 256, t = rem >> 8, x = rem & 255;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < kHeadWaves; ++w) sum += S.part[w][i][t][x];
+    const int ln = x >> 2, r = 4 * (ln >> 4) + (x & 3), col = ln & 15;
+    const int wi = i == 0 ? w0 : i == 1 ? w1 : w2;
+    if (a.dueling && t == a.N16) {
+      if (col == 0) S.v[i][r] = sum + (wi == 0 ? a.bv[0] : wi == 1 ? a.bv[1] : a.bv[2])[0];
+    } else {
+      const int c = t * 16 + col;
+      if (c < A) S.q[i][r][c] = sum + (wi == 0 ? a.b[0] : wi == 1 ? a.b[1] : a.b[2])[c];
+    }
+  }
+  __syncthreads();
   if (a.dueling) {
-    for (int t = tid; t < ninst * B; t += nth) {
+    for (int e = tid; e < ninst * kHeadRows; e += kHeadThreads) {
+      const int i = e / kHeadRows, r = e - i * kHeadRows;
       float mean = 0.f;
-      for (int i = 0; i < A; ++i) mean += q[t * A + i];
+      for (int c = 0; c < A; ++c) mean += S.q[i][r][c];
       mean /= (float)A;
-      const float v = vv[t];
-      for (int i = 0; i < A; ++i) q[t * A + i] += v - mean;
+      for (int c = 0; c < A; ++c) S.q[i][r][c] += S.v[i][r] - mean;
     }
     __syncthreads();
   }
-  if (infer) {                              // acting: Q of instance 0 only
-    if (q_out != nullptr)
-      for (int t = tid; t < B * A; t += nth) q_out[t] = q[t];
+}
+
+// AT = the action count at compile time (the common Atari counts; 0 = runtime): the per-action
+// loops (argmax, dH inner products, dQ rows) unroll, so their LDS reads are issued together
+template <int AT>
+__global__ void __launch_bounds__(kHeadThreads) head_loss_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char head_smem[];
+  HeadSmem& S = *reinterpret_cast<HeadSmem*>(head_smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int A = AT > 0 ? AT : a.A, A1 = A + 1;
+  const int nlearn = a.infer ? 0 : (a.B + kHeadRows - 1) / kHeadRows;
+  const bool acting = a.infer ? a.has_actor != 0 : (a.act_E > 0 && (int)blockIdx.x >= nlearn);
+  int64_t* prof = (a.prof != nullptr && tid == 0 && (blockIdx.x == 0 || (acting && (int)blockIdx.x == nlearn)))
+                      ? a.prof + (acting ? 16 : 0) : nullptr;
+#define HEAD_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
+  HEAD_MARK(0);
+  if (acting) {
+    // ---- one env per block: its 16-row Q tile (online weights), then that env's step
+    const int e = (int)blockIdx.x - nlearn;
+    const ActorArgs& x = a.actor;
+    const int E = x.E;
+    const ActorPre pre = actor_prefetch(x);                      // overlaps the Q loads
+    int32_t st_e[4] = {0, 0, 0, 0};                              // env e's frame stack (thread 0)
+    if (tid == 0)
+      for (int c = 0; c < 4; ++c) st_e[c] = x.stacks[(int64_t)e * x.K + min(c, x.K - 1)];
+    const int r0 = (e / kHeadRows) * kHeadRows;
+    const void* hh = a.infer ? a.h[0] : a.act_h;
+    head_q_tile(a, S, hh, hh, hh, 0, 0, 0, 1, r0, min(kHeadRows, E - r0));
+    HEAD_MARK(1);
+    const float* qe = &S.q[0][e - r0][0];
+    if (a.infer && a.q_out != nullptr && tid < A) a.q_out[(int64_t)e * A + tid] = qe[tid];
+    if (tid == 0) {
+      int fs, rs;
+      S.flag = actor_env_step(x, qe, e, pre.t0, pre.f0, pre.eps0, pre.eps_min, pre.decay, pre.seed, pre.ctr, fs, rs,
+                              st_e);
+    }
+    __syncthreads();
+    const int fslot = (int)((pre.f0 + 2 * e) % x.F), rslot = (int)((pre.f0 + 2 * e + 1) % x.F);
+    write_random_frame(x.frames + (int64_t)fslot * x.HW, x.HW, pre.seed, pre.ctr, 0x100u + 2u * e, tid, kHeadThreads);
+    if (S.flag)
+      write_random_frame(x.frames + (int64_t)rslot * x.HW, x.HW, pre.seed, pre.ctr, 0x101u + 2u * e, tid, kHeadThreads);
     HEAD_MARK(2);
-    if (has_actor) actor_step_block(a.actor, q, part_lds, apre);      // (split-K partials are dead)
+    // the LAST acting block to arrive advances the actor state (every block read it at its start)
+    __syncthreads();
+    if (tid == 0) {
+      const int tk = __hip_atomic_fetch_add(x.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      S.flag = tk == E - 1 ? 1 : 0;
+      if (S.flag) {
+        actor_advance(x, pre.t0, pre.f0, pre.size0, pre.eps0, pre.eps_min, pre.decay, pre.ctr);
+        __hip_atomic_store(x.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (x.tsum != nullptr) {          // PER: the last block inserts the E new transitions at max priority
+      __syncthreads();
+      if (S.flag) sumtree_update_wave(x.tsum, x.tmin, x.tmaxp, nullptr, nullptr, 0.f, 0.f, 1, E, x.tP, x.tlevels, S.st,
+                                      (int)(pre.t0 % x.C), x.C);
+    }
     HEAD_MARK(3);
     return;
   }
-  // ---- 2. TD loss (one thread per sample)
+  const int r0 = (int)blockIdx.x * kHeadRows, nrows = min(kHeadRows, a.B - r0);
+  if (a.infer) {                                               // q_values: rows of Q
+    head_q_tile(a, S, a.h[0], a.h[0], a.h[0], 0, 0, 0, 1, r0, nrows);
+    if (a.q_out != nullptr)
+      for (int t = tid; t < nrows * A; t += kHeadThreads) a.q_out[(int64_t)r0 * A + t] = S.q[0][t / A][t % A];
+    return;
+  }
+  // ---- learner tile: TD inputs and the online output layer (for dH) first: their loads join
+  //      the Q tile's batch (clamped indices: unconditional loads)
+  const int ninst = a.h[2] != nullptr ? 3 : 2;
+  const int HID = a.HID, HH = a.dueling ? 2 * HID : HID;
+  float tr = 0.f, tg = 0.f, td = 0.f, tw = 1.f;
+  int ta = 0;
+  if (tid < nrows) {
+    const int b = r0 + tid;
+    tr = a.rew[b]; tg = a.gam[b]; td = a.done[b]; ta = a.act[b];
+    if (a.wts != nullptr) tw = a.wts[b];
+  }
+  const int nw = HID * A, nwt = nw + (a.dueling ? HID : 0);
+  // (clamped indices, unconditional loads: a predicated load per iteration compiles to a branch
+  //  + wait each; AT known: just enough iterations for HID <= 512)
+  constexpr int kWIt = AT > 0 ? (512 * (AT + 1) + kHeadThreads - 1) / kHeadThreads : kHeadMaxW / kHeadThreads;
+  float wr[kWIt];
+#pragma unroll
+  for (int i = 0; i < kWIt; ++i) {
+    const int t = min(tid + kHeadThreads * i, nwt - 1);
+    wr[i] = t < nw ? a.w[0][t] : a.wv[0][t - nw];
+  }
+  bfx8 h0f[kHeadKPW][2];
+  head_q_tile(a, S, a.h[0], a.h[1], a.h[2], 0, 1, 2, ninst, r0, nrows, h0f);
+#pragma unroll
+  for (int i = 0; i < kWIt; ++i)
+    if (tid + kHeadThreads * i < nwt) S.w[tid + kHeadThreads * i] = wr[i];
+  HEAD_MARK(1);
   float contrib = 0.f;
-  if (tid < B) {
-    const int b = tid;
-    const float* sel = q + ((ninst == 3 ? 2 : 1) * B + b) * A;
+  if (tid < nrows) {
+    const int b = r0 + tid;
+    const float* sel = &S.q[ninst == 3 ? 2 : 1][tid][0];
     int best = 0;
     float bvv = sel[0];
-    for (int i = 1; i < A; ++i) if (sel[i] > bvv) { bvv = sel[i]; best = i; }
-    const float nxt = q[(B + b) * A + best];
+#pragma unroll
+    for (int i = 1; i < (AT > 0 ? AT : 32); ++i)
+      if ((AT > 0 || i < A) && sel[i] > bvv) { bvv = sel[i]; best = i; }
+    const float nxt = S.q[1][tid][best];
     const float y = tr + tg * (1.f - td) * nxt;
-    const int at = ta;
-    const float d = q[b * A + at] - y;
-    const float w = tw;
+    const float d = S.q[0][tid][ta] - y;
     float per, dper;
     if (a.huber) {
       const float ad = fabsf(d);
@@ -601,92 +687,67 @@ DQN_DEV void head_body(const HeadArgs& a, float* hsm, const int B, const void* h
       per = d * d;
       dper = 2.f * d;
     }
-    contrib = w * per;
-    const float gsc = w * dper / (float)B;
-    for (int i = 0; i < A; ++i) dq[b * A + i] = (i == at) ? gsc : 0.f;
-    if (a.dueling) {
-      // Q_i = V + A_i - mean(A): dV = sum_i dQ_i, dA_i = dQ_i - mean(dQ)
-      dv[b] = gsc;
-      for (int i = 0; i < A; ++i) dq[b * A + i] -= gsc / (float)A;
-    }
-    if (blk == 0) a.prio[b] = fabsf(d);
+    contrib = tw * per;
+    const float gsc = tw * dper / (float)a.B;
+    // Q_i = V + A_i - mean(A): dV = sum_i dQ_i, dA_i = dQ_i - mean(dQ)
+    const float sub = a.dueling ? gsc / (float)A : 0.f;
+#pragma unroll
+    for (int i = 0; i < (AT > 0 ? AT : 32); ++i)
+      if (AT > 0 || i < A) S.dq[tid][i] = ((i == ta) ? gsc : 0.f) - sub;
+    S.dq[tid][A] = a.dueling ? gsc : 0.f;
+    a.prio[b] = fabsf(d);
   }
-  {
-    const float s = wave_sum(contrib);
-    if (lane == 0) red[wave] = s;
+  if (wave == 0) {
+    const float sum = wave_sum(contrib);
+    if (lane == 0) a.loss_parts[blockIdx.x] = sum;           // summed by the fc dgrad launch
   }
-  if (q_out != nullptr && blk == 0)
-    for (int t = tid; t < B * A; t += nth) q_out[t] = q[t];
   __syncthreads();
-  if (tid == 0 && blk == 0) {
-    float s = 0.f;
-    for (int i = 0; i < nwave; ++i) s += red[i];
-    a.loss[0] = s / (float)B;
+  // dQ (| dV) as act_t [B][64] (plain / adv in columns 0..31, value in 32; zero padding): the dZ
+  // operand of the output layer's weight-gradient members of the grouped wgrad launch (+ Q rows)
+  for (int t = tid; t < nrows * 64; t += kHeadThreads) {
+    const int r = t >> 6, c = t & 63;
+    const float g = c < A ? S.dq[r][c] : (c == 32 && a.dueling ? S.dq[r][A] : 0.f);
+    reinterpret_cast<act_t*>(a.dq16)[(int64_t)(r0 + r) * 64 + c] = (act_t)(g * kLossScale);
   }
+  if (a.q_out != nullptr)
+    for (int t = tid; t < nrows * A; t += kHeadThreads) a.q_out[(int64_t)r0 * A + t] = S.q[0][t / A][t % A];
   HEAD_MARK(2);
-  // ---- 3. head backward (online instance 0 only), partitioned over the grid's
-  // blocks (phases 1-2 above are recomputed by every block: cheap MFMA work);
-  // k fastest across threads -> coalesced H reads
-  act_t* dh = reinterpret_cast<act_t*>(a.dh);
-  for (int t = gt; t < HID * A; t += gn) {              // dW[k][i] = sum_b Ha[b][k] dA[b][i]
-    const int i = t / HID, k = t - i * HID;
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += (float)ha0[(int64_t)b * HH + k] * dq[b * A + i];
-    a.dw[k * A + i] = s;
-  }
-  for (int i = gt; i < A; i += gn) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dq[b * A + i];
-    a.db[i] = s;
-  }
-  if (a.dueling) {
-    for (int k = gt; k < HID; k += gn) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += (float)hb0[(int64_t)b * HH + k] * dv[b];
-      a.dwv[k] = s;
-    }
-    if (gt == 0) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += dv[b];
-      a.dbv[0] = s;
+  // ---- dH[row][k] = (sum_i dQ[row][i] W[k][i]) * (h > 0) (dueling: value units dV wv[k]), from
+  //      the online h fragments this wave already holds: row lane & 15, units ks * 32 + kg + j
+  {
+    const int rr = lane & 15, row = r0 + rr;
+    const int kg = 8 * (lane >> 4);
+    act_t* dh = reinterpret_cast<act_t*>(a.dh);
+    const float* g = S.dq[rr];
+#pragma unroll
+    for (int u = 0; u < kHeadKPW; ++u) {
+      const int ks = wave * kHeadKPW + u;
+      if (ks >= HID / 32) break;
+      const int k0 = ks * 32 + kg;
+      bfx8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float* w = S.w + (k0 + j) * A;
+        float sj = 0.f;
+        if constexpr (AT > 0) {
+#pragma unroll
+          for (int i = 0; i < AT; ++i) sj += g[i] * w[i];
+        } else {
+          for (int i = 0; i < A; ++i) sj += g[i] * w[i];
+        }
+        o[j] = (act_t)((float)h0f[u][0][j] > 0.f ? sj * kLossScale : 0.f);     // scaled: see dqn_act.h
+      }
+      if (row < a.B) *reinterpret_cast<bfx8*>(dh + (int64_t)row * HH + (a.dueling ? HID : 0) + k0) = o;
+      if (a.dueling) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          o[j] = (act_t)((float)h0f[u][1][j] > 0.f ? g[A] * S.w[nw + k0 + j] * kLossScale : 0.f);
+        if (row < a.B) *reinterpret_cast<bfx8*>(dh + (int64_t)row * HH + k0) = o;
+      }
     }
   }
   HEAD_MARK(3);
-  // dH[b][k] = (sum_i dA[b][i] W[k][i]) * (H > 0);   dueling value half: dV[b] * wv[k]
-  const float* Wd = W0;                                 // output W [HID][A]
-  const float* wvd = a.wv[0];
-  for (int t = gt; t < B * HH; t += gn) {
-    const int b = t / HH, k = t - b * HH;
-    float s = 0.f;
-    if (a.dueling && k < HID) {
-      s = dv[b] * wvd[k];
-    } else {
-      const int kk = a.dueling ? k - HID : k;
-      for (int i = 0; i < A; ++i) s += dq[b * A + i] * Wd[kk * A + i];
-    }
-    const float hval = (float)hb0[t];
-    dh[t] = (act_t)(hval > 0.f ? s * kLossScale : 0.f);   // scaled: see dqn_act.h
-  }
-  // ---- 4. zero the gradient range the conv wgrads accumulate into (nothing in this
-  //         kernel touches it; saves a fill launch). Last, so no barrier waits on it.
-  if (do_zero && a.zero_ptr != nullptr) {
-    float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
-    for (int t = blk * nth + tid; t < a.zero_n / 4; t += nblk * nth) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  HEAD_MARK(4);
 #undef HEAD_MARK
-}
-
-__global__ void __launch_bounds__(1024) head_loss_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float hsm[];
-  // fused acting: the LAST workgroup runs the acting step on the actors' hidden layer
-  // (online weights = instance 0), the others the learner's loss + head backward
-  if (a.act_E > 0 && blockIdx.x == gridDim.x - 1) {
-    head_body(a, hsm, a.act_E, a.act_h, true, true, nullptr, false, 0, 1);
-    return;
-  }
-  head_body(a, hsm, a.B, nullptr, a.infer != 0, a.has_actor != 0, a.q_out, true, blockIdx.x,
-            gridDim.x - (a.act_E > 0 ? 1 : 0));
 }
 
 }  // namespace dqn
@@ -715,20 +776,49 @@ using NatD3 = DgradLoader<64, 3, 3, 1>;
 using NatD2 = DgradLoader<64, 4, 4, 2>;
 using NatF1 = FrameLoader<8, 8, 4>;
 
+// Tile-variant sweep (DQN_TILES="kind:variant,..." read once): A/B measurements of the
+// latency-bound layer GEMMs without a rebuild; variant 0 = the default tiles below.
+static int tile_variant(int kind) {
+  static int v[16] = {-1};
+  if (v[0] == -1) {
+    for (int i = 0; i < 16; ++i) v[i] = 0;
+    if (const char* s = getenv("DQN_TILES")) {
+      int k, x, n = 0;
+      while (sscanf(s, "%d:%d%n", &k, &x, &n) == 2) {
+        if (k > 0 && k < 16) v[k] = x;
+        s += n;
+        if (*s == ',') ++s;
+      }
+    }
+  }
+  return kind > 0 && kind < 16 ? v[kind] : 0;
+}
+
 // layer kinds: see dqn_nets_k.h.  Tiles: (MT, NT, WM, WN, KSPLIT, EPI)
 int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
+  switch (tile_variant(kind) * 100 + kind) {
+    // ---- sweep variants (DQN_TILES; r2 sweep: profiles/r2_tile_sweep.md): the previous defaults
+    case 100 + L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 0, 13); return 0;   // 32-row blocks
+    case 200 + L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 4, 0, 13); return 0;   // 16 x 32, split-K 4
+    case 100 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 2, 2, 2, 8); return 0;
+    case 200 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 4, 2, 4); return 0;
+    case 100 + L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 4, 2, 1, 2, 2, 9); return 0;
+    case 100 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 1, 1, 4, 2, 8); return 0;         // 16 rows, split-K 4
+    default: break;
+  }
   switch (kind) {
     // ---- forward, fused bias + ReLU, bf16 NHWC out
     case L_NAT_CONV1_FWD: IGEMM_LAUNCH(NatC1, 1, 2, 4, 1, 1, 0); return 0;       // K 256: 8 k-steps
     case L_NAT_CONV1_FRAMES: IGEMM_LAUNCH(NatF1, 1, 2, 4, 1, 1, 0); return 0;
     case L_NAT_CONV2_FWD: IGEMM_LAUNCH(NatC2, 1, 4, 2, 1, 2, 0); return 0;       // K 512: split-K 2
     case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 4, 2, 1, 2, 0); return 0;       // K 576: split-K 2
-    // K 3136 = 98 k-steps, split-K 8: one 13-step load batch per wave
-    case L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 0, 13); return 0;
+    // K 3136 = 98 k-steps, split-K 8: one 13-step load batch per wave; 16-row blocks so the
+    // B=32 step spreads over 2x the CUs (each block's L2->CU bytes are the bound, not MFMA)
+    case L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 8, 0, 13); return 0;
     case L_DENSE_FWD_F32: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 1, 13); return 0;
     // ---- backward data, ReLU mask of the layer input
-    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 2, 2, 2, 8); return 0;   // K 512-1024
-    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 4, 2, 1, 2, 2, 9); return 0;     // 18 k-steps
+    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 2, 2, 8); return 0;   // K 512-1024
+    case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 2, 1, 2, 2, 2, 9); return 0;     // 18 k-steps, 16 x 64 blocks
     case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;     // 32 k-steps
     default: return -1;
   }
@@ -749,6 +839,7 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
     case L_NAT_CONV2_FWD: WGRAD_LAUNCH(NatC2, 128, 128, 64); return 0;   // 21 x 4 blocks
     case L_NAT_CONV3_FWD: WGRAD_LAUNCH(NatC3, 128, 192, 64); return 0;   // 13 x 3 blocks
     case L_DENSE_FWD_RELU: WGRAD_LAUNCH(DenseLoader, 32, 64, 128); return 0;
+    case L_HEAD_WGRAD: WGRAD_LAUNCH(DenseLoader, 32, 64, 64); return 0;
     default: return -1;
   }
 }
@@ -768,11 +859,17 @@ __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
   int b = blockIdx.x, i = 0;
   while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
   switch (G.kind[i]) {
-    case L_NAT_CONV1_FWD: group_member<NatC1, 128, 256, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV1_FRAMES: group_member<NatF1, 128, 256, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV2_FWD: group_member<NatC2, 128, 128, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV3_FWD: group_member<NatC3, 128, 192, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    // 256-row M-chunks, K split over blocks: 2-4x fewer fp32 atomic partials than 128-row chunks
+    case L_NAT_CONV1_FWD: group_member<NatC1, 256, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV1_FRAMES: group_member<NatF1, 256, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV2_FWD: group_member<NatC2, 256, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV3_FWD: group_member<NatC3, 256, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     case L_DENSE_FWD_RELU: group_member<DenseLoader, 32, 64, 128>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_HEAD_WGRAD: group_member<DenseLoader, 32, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    // sweep variants (kind + 100 * variant, DQN_TILES): the r1 128-row tiles
+    case 100 + L_NAT_CONV1_FRAMES: group_member<NatF1, 128, 256, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case 100 + L_NAT_CONV2_FWD: group_member<NatC2, 128, 128, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case 100 + L_NAT_CONV3_FWD: group_member<NatC3, 128, 192, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     default: break;
   }
 }
@@ -780,10 +877,14 @@ __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
 
 static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
   switch (kind) {
-    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = 128; KB = 256; NB = 32; break;
-    case L_NAT_CONV2_FWD: MC = 128; KB = 128; NB = 64; break;
-    case L_NAT_CONV3_FWD: MC = 128; KB = 192; NB = 64; break;
+    case 100 + L_NAT_CONV1_FRAMES: MC = 128; KB = 256; NB = 32; break;
+    case 100 + L_NAT_CONV2_FWD: MC = 128; KB = 128; NB = 64; break;
+    case 100 + L_NAT_CONV3_FWD: MC = 128; KB = 192; NB = 64; break;
+    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = 256; KB = 64; NB = 32; break;
+    case L_NAT_CONV2_FWD: MC = 256; KB = 64; NB = 64; break;
+    case L_NAT_CONV3_FWD: MC = 256; KB = 64; NB = 64; break;
     case L_DENSE_FWD_RELU: MC = 32; KB = 64; NB = 128; break;
+    case L_HEAD_WGRAD: MC = 32; KB = 64; NB = 64; break;
     default: return false;
   }
   lds = (size_t)(KB + NB) * (MC + 8) * sizeof(act_t);
@@ -794,9 +895,14 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   int total = 0;
   size_t lds = 0;
   for (int i = 0; i < G.n; ++i) {
+    // DQN_TILES wgrad slots: 13 = conv1 (frame loader), 14 = conv2, 15 = conv3
+    const int slot = G.kind[i] == L_NAT_CONV1_FRAMES ? 13 : G.kind[i] == L_NAT_CONV2_FWD ? 14
+                   : G.kind[i] == L_NAT_CONV3_FWD ? 15 : 0;
+    if (slot) G.kind[i] += 100 * tile_variant(slot);
     int MC, KB, NB;
     size_t l;
     if (!wgrad_tiles(G.kind[i], MC, KB, NB, l)) return -1;
+    if (l > 160 * 1024) return -2;
     G.gx[i] = (G.a[i].M + MC - 1) / MC;
     G.gy[i] = (G.a[i].K + KB - 1) / KB;
     const int gz = (G.g[i].N + NB - 1) / NB;
@@ -810,14 +916,30 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(kHeadPartFloats + 4 * a.B * a.A + 4 * a.B + 32 + kHeadActorScratch +
-                              4 * kHeadMaxA) * sizeof(float);
-  static size_t lds_set = 64 * 1024;          // dynamic LDS above 64 KB must be opted into
-  if (lds > lds_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_loss_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    lds_set = lds;
+  static bool lds_set = false;                // dynamic LDS above 64 KB must be opted into
+  if (!lds_set) {
+    const void* fns[] = {reinterpret_cast<const void*>(head_loss_kernel<0>), reinterpret_cast<const void*>(head_loss_kernel<2>),
+                         reinterpret_cast<const void*>(head_loss_kernel<3>), reinterpret_cast<const void*>(head_loss_kernel<4>),
+                         reinterpret_cast<const void*>(head_loss_kernel<6>), reinterpret_cast<const void*>(head_loss_kernel<9>),
+                         reinterpret_cast<const void*>(head_loss_kernel<18>)};
+    for (const void* f : fns)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(HeadSmem));
+    lds_set = true;
   }
-  // training: 8 blocks share the backward (+1 fused acting block); acting (infer): one block
-  hipLaunchKernelGGL(head_loss_kernel, dim3(a.infer ? 1 : 8 + (a.act_E > 0 ? 1 : 0)), dim3(1024), lds, st, a);
+  const int tiles = (a.B + kHeadRows - 1) / kHeadRows;
+  int grid;
+  if (a.infer) grid = a.has_actor ? a.actor.E : tiles;        // acting launch: one block per env
+  else grid = tiles + (a.act_E > 0 ? a.act_E : 0);            // learner tiles (+ fused acting blocks)
+#define HEAD(AT) hipLaunchKernelGGL(head_loss_kernel<AT>, dim3(grid), dim3(kHeadThreads), sizeof(HeadSmem), st, a)
+  switch (a.A) {                   // the Atari action counts (and CartPole's 2) at compile time
+    case 2: HEAD(2); break;
+    case 3: HEAD(3); break;
+    case 4: HEAD(4); break;
+    case 6: HEAD(6); break;
+    case 9: HEAD(9); break;
+    case 18: HEAD(18); break;
+    default: HEAD(0); break;
+  }
+#undef HEAD
 }
+

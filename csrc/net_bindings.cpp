@@ -46,9 +46,20 @@ dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_
   return a;
 }
 
+// aux = [] or [zero_ptr (16 B aligned), zero_n (% 4 == 0), loss_parts, nparts (<= 64), loss_out]
+// with aux_f = [loss_mul]: the launch's side duties (ConvArgs)
 void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_t> bias,
-           std::vector<int64_t> out, std::vector<int64_t> mask, std::vector<double> scale, std::vector<int64_t> dims) {
+           std::vector<int64_t> out, std::vector<int64_t> mask, std::vector<double> scale, std::vector<int64_t> dims,
+           std::vector<int64_t> aux, std::vector<double> aux_f) {
   dqn::ConvArgs a = conv_args(in, w, bias, out, mask, scale, dims);
+  if (!aux.empty()) {
+    TORCH_CHECK(aux.size() == 5 && aux_f.size() == 1 && aux[0] % 16 == 0 && aux[1] % 4 == 0 && aux[3] <= 64,
+                "igemm aux = [zero_ptr, zero_n, loss_parts, nparts, loss_out], [loss_mul]");
+    a.zero_ptr = P<float*>(aux[0]); a.zero_n = (int)aux[1];
+    a.loss_parts = P<const float*>(aux[2]); a.nparts = (int)aux[3]; a.loss_out = P<float*>(aux[4]);
+    a.loss_mul = (float)aux_f[0];
+    TORCH_CHECK(a.loss_parts == nullptr || a.loss_out != nullptr, "igemm aux: loss output");
+  }
   TORCH_CHECK(launch_igemm((int)kind, a, (int)in.size(), cur_stream()) == 0, "unknown igemm kind ", kind);
 }
 
@@ -135,8 +146,8 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
 // members: per layer [kind, in, dz, ldz, dw, db, dw2, db2, nsplit, N] + dims (11 or 13) + scale
 void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vector<int64_t>> dims,
                  std::vector<double> scales) {
-  TORCH_CHECK(members.size() >= 1 && members.size() <= 4 && dims.size() == members.size() &&
-              scales.size() == members.size(), "1..4 group members");
+  TORCH_CHECK(members.size() >= 1 && members.size() <= (size_t)dqn::kMaxWgradMembers &&
+              dims.size() == members.size() && scales.size() == members.size(), "1..6 group members");
   dqn::WgradGroup G{};
   G.n = (int)members.size();
   for (int i = 0; i < G.n; ++i) {
@@ -191,14 +202,28 @@ void cnn_bwd(std::vector<int64_t> ptrs, int64_t B) {
   launch_cnn_bwd(a, (int)B, cur_stream());
 }
 
+// Scalar head. qp = [loss_parts, dq16]: per-16-sample-tile loss partials (training; summed by
+// the fc dgrad launch's aux duty) and dQ as act_t [B][64] (the output layer's wgrad dZ); dH goes
+// to io[12]. h = the learner instances' hidden layers (online(s), target(s')[, online(s')]) or,
+// infer, the one instance; pw / pwv = their packed output-layer fragments.
 void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h, std::vector<int64_t> w,
                std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv, std::vector<int64_t> io,
-               std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
+               std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> qp,
                std::vector<int64_t> actor, std::vector<double> actor_f, int64_t act_h, int64_t prof) {
   TORCH_CHECK(flts.size() == 1, "flts = [huber delta]");
-  dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h);
+  TORCH_CHECK(qp.size() == 2, "qp = [loss_parts, dq16]");
+  dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, {}, actor, actor_f, act_h);
   a.prof = P<int64_t*>(prof);
   a.delta = (float)flts[0];
+  a.loss_parts = P<float*>(qp[0]);
+  a.dq16 = P<void*>(qp[1]);
+  const int ninst = a.infer ? 1 : (a.h[2] != nullptr ? 3 : 2);
+  for (int i = 0; i < ninst; ++i) TORCH_CHECK(a.h[i] && a.pw[i] && a.b[i] && (!a.dueling || (a.pwv[i] && a.bv[i])),
+                                              "head: instance ", i, " pointers");
+  TORCH_CHECK(a.infer || (a.dq16 && a.loss_parts && a.dh && a.w[0] && (!a.dueling || a.wv[0]) && a.B <= 1024),
+              "head: training outputs / online output layer");
+  TORCH_CHECK(a.HID <= 512 && a.A <= 32, "scalar head: hidden width <= 512, A <= 32");
+  TORCH_CHECK(!a.has_actor || a.actor.E <= 64, "head: acting E <= 64");
   launch_head_loss(a, cur_stream());
 }
 
@@ -295,11 +320,13 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("M") = std::vector<int64_t>{}, pybind11::arg("sample") = std::vector<int64_t>{});
   m.def("qnet_pack", &pack, pybind11::arg("src"), pybind11::arg("dst"), pybind11::arg("jobs"), pybind11::arg("njobs"),
         pybind11::arg("max_threads"), pybind11::arg("dst2") = 0, pybind11::arg("step") = 0, pybind11::arg("freq") = 1);
-  m.def("qnet_igemm", &igemm);
+  m.def("qnet_igemm", &igemm, pybind11::arg("kind"), pybind11::arg("inp"), pybind11::arg("w"), pybind11::arg("bias"),
+        pybind11::arg("out"), pybind11::arg("mask"), pybind11::arg("scale"), pybind11::arg("dims"),
+        pybind11::arg("aux") = std::vector<int64_t>{}, pybind11::arg("aux_f") = std::vector<double>{});
   m.def("qnet_wgrad", &wgrad);
   m.def("qnet_head_loss", &head_loss, pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"), pybind11::arg("io"),
-        pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),
+        pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("qp"), pybind11::arg("actor"),
         pybind11::arg("actor_f"), pybind11::arg("act_h") = 0, pybind11::arg("prof") = 0);
   m.def("qnet_wgrad_group", &wgrad_group);
   m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),

@@ -26,7 +26,7 @@ import torch
 
 from . import _ext
 
-_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9)
+_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9, HW=11)
 
 
 def supports(arch) -> bool:
@@ -477,8 +477,17 @@ class HipExecutor:
             'q': torch.zeros(B * self.A, dtype=torch.float32, device=dev),
             'ones': torch.ones(B, dtype=torch.float32, device=dev),
         }
+        ws.update(self._head_ws(B, dev))
         self._ws[key] = ws
         return ws
+
+    def _head_ws(self, B, dev) -> dict:
+        """Scalar heads: per-16-sample-tile loss partials (summed by the fc dgrad launch) and the
+        head's dQ as act_t [B][64] (the output layer's weight-gradient dZ)."""
+        if self.dist:
+            return {}
+        f32 = dict(dtype=torch.float32, device=dev)
+        return {'loss_parts': torch.zeros(64, **f32), 'dq16': torch.zeros(B * 64, dtype=self.act_dtype, device=dev)}
 
     # ------------------------------------------------------------ forward
     @property
@@ -513,7 +522,7 @@ class HipExecutor:
             smp = list(sample[0]) + [int(sample[1])] if sample is not None else []
             ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale, prof,
                            list(M), smp)
-            self._fc_fwd(packs, ws, B, ninst)
+            self._fc_fwd(packs, flats, ws, B, ninst)
             return
         d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
         kind1 = _KIND['C1']
@@ -528,9 +537,9 @@ class HipExecutor:
         ext.qnet_igemm(_KIND['C3'], [rows(ws['x2'], i) for i in range(ninst)], pk('conv3/fwd'), bias('conv3/b'),
                        [rows(ws['x3'], i) for i in range(ninst)], [], [1.0] * ninst,
                        [B * h3 * w3, c3.cout, c3.k * c3.k * c3.cin, c3.cout // 16, c3.cout, h2, w2, h3, w3, 0, 0])
-        self._fc_fwd(packs, ws, B, ninst)
+        self._fc_fwd(packs, flats, ws, B, ninst)
 
-    def _fc_fwd(self, packs, ws, B, ninst):
+    def _fc_fwd(self, packs, flats, ws, B, ninst):
         fcb = [p.data_ptr() + 2 * self.poff['fc/bias'] for p in packs]
         self.ext.qnet_igemm(_KIND['DFWD'], [ws['x3'][i].data_ptr() for i in range(ninst)],
                             [p.data_ptr() + 2 * self.poff['fc/fwd'] for p in packs], fcb,
@@ -586,7 +595,7 @@ class HipExecutor:
             self._ws[key] = ws
         return ws
 
-    def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h=0):
+    def _head(self, ints, hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h=0, ws=None):
         """Output layer + loss (+ backward) launch: scalar head or the C51 head."""
         if self.dist:
             self._c51_B = ints[0]
@@ -602,8 +611,8 @@ class HipExecutor:
                                    wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl, act_h)
         else:
             prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
-            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h,
-                                    prof)
+            self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv,
+                                    [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()], actor, actor_f, act_h, prof)
 
     def q_values(self, flat: torch.Tensor, x: torch.Tensor, noise=None) -> torch.Tensor:
         """Q [B, A] (C51: expected value of the return distribution)."""
@@ -619,7 +628,7 @@ class HipExecutor:
         pw, pwv = self._head_packs([p])
         self._c51_dev = x.device
         self._head([B, self.A, self.HID, int(self.dueling), 0, 1], [ws['h'][0].data_ptr()],
-                   w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv, [], [], [])
+                   w, b, wv, bv, [0] * 7 + [q.data_ptr()] + [0] * 5, pw, pwv, [], [], [], ws=ws)
         return q
 
     def act_fused(self, flat: torch.Tensor, frames: torch.Tensor, stacks: torch.Tensor, actor_ptrs, actor_ints,
@@ -638,12 +647,42 @@ class HipExecutor:
         self._c51_dev = frames.device
         self._head([E, self.A, self.HID, int(self.dueling), 0, 1], [ws['h'][0].data_ptr()],
                    w, b, wv, bv, [0] * 7 + [q_out.data_ptr() if q_out is not None else 0] + [0] * 5,
-                   pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f))
+                   pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f), ws=ws)
 
     def _head_packs(self, packs):
         pw = [p.data_ptr() + 2 * self.poff['head/w'] for p in packs]
         pwv = [p.data_ptr() + 2 * self.poff['head/v'] for p in packs] if self.dueling else []
         return pw, pwv
+
+    def _fc_dgrad(self, ws, B, po, zero=()):
+        """dz3 = (dH W_fc^T) * (x3 > 0) on the igemm kernel. Scalar heads: the launch also zeroes
+        the conv weight-gradient range and sums the head's per-tile loss partials (side duties;
+        the head kernel wrote dH); C51: the head did both itself."""
+        F, HH = self.FLAT, self.HH
+        pk = po.data_ptr() + 2 * self.poff['fc/dgrad']
+        x3, dz3 = ws['x3'][0].data_ptr(), ws['dz3'].data_ptr()
+        aux, aux_f = [], []
+        if not self.dist:
+            zp, zn = (zero[0], zero[1]) if zero else (0, 0)
+            aux = [zp, zn, ws['loss_parts'].data_ptr(), (B + 15) // 16, ws['loss'].data_ptr()]
+            aux_f = [1.0 / B]
+        self.ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pk], [], [dz3], [x3], [1.0],
+                            [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0], aux, aux_f)
+
+    def _head_wgrad_members(self, ws, B, h0, hgrads):
+        """Grouped-wgrad members of the scalar output layer: dW = h^T dQ (dueling: advantage
+        stream over h's second half, value stream over its first half) from the head's dq16."""
+        if self.dist:
+            return [], []
+        dw, db, dwv, dbv = hgrads
+        H, HH, A = self.HID, self.HH, self.A
+        dq = ws['dq16'].data_ptr()
+        esz = ws['dq16'].element_size()
+        if not self.dueling:
+            return ([[_KIND['HW'], h0, dq, 64, dw, db, 0, 0, A, A]], [[B, A, H, 0, 0, 0, HH, 0, 0, 0, 0]])
+        return ([[_KIND['HW'], h0 + esz * H, dq, 64, dw, db, 0, 0, A, A],
+                 [_KIND['HW'], h0, dq + esz * 32, 64, dwv, dbv, 0, 0, 1, 1]],
+                [[B, A, H, 0, 0, 0, HH, 0, 0, 0, 0], [B, 1, H, 0, 0, 0, HH, 0, 0, 0, 0]])
 
     # ----------------------------------------------------------- training
     def supports_fused_acting(self) -> bool:
@@ -743,10 +782,10 @@ class HipExecutor:
                    [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
                     wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
                     ws['q'].data_ptr() if not self.dist else 0, dw, db, dwv, dbv, ws['dh'].data_ptr()],
-                   *self._head_packs(packs), zero,
+                   *self._head_packs(packs), zero if self.dist else [],     # (scalar: zeroed in fc dgrad)
                    [] if acting is None else list(acting['ptrs']) + list(acting['ints']),
                    [] if acting is None else list(acting['f']),
-                   act_h=0 if acting is None else ws['h'][ninst].data_ptr())
+                   act_h=0 if acting is None else ws['h'][ninst].data_ptr(), ws=ws)
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
@@ -756,8 +795,12 @@ class HipExecutor:
             fw, fb, fw2, fb2 = g('value/fcl/w'), g('value/fcl/b'), g('advantage/fcl/w'), g('advantage/fcl/b')
         else:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
+        # fc dgrad (+ the scalar head's backward: dH, dW_out, db_out from the head's dQ)
+        hmembers, hdims = self._head_wgrad_members(ws, B, ws['h'][0].data_ptr(), (dw, db, dwv, dbv))
+        fc_dgrad = lambda: self._fc_dgrad(ws, B, po, zero)
         if self.arch.network == 'cnn':
-            out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, gnoise, dev)
+            out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, gnoise, dev, fc_dgrad,
+                                     hmembers, hdims)
             return out + (None,) if split else out
         x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         mc_fc = (B + 31) // 32 * 32
@@ -777,19 +820,18 @@ class HipExecutor:
                         c3.cout],
                        [_KIND['C2'], x1, ws['dz2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0, c2.cout,
                         c2.cout],
-                       [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]]
+                       [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]] + hmembers
             dims = [d1, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
-                    [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]]
-            scales = [self.input_scale, 1.0, 1.0, 1.0]
+                    [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]] + hdims
+            scales = [self.input_scale] + [1.0] * (len(members) - 1)
             noisy = self.noisy and gnoise is not None
+            fc_dgrad()
             if split and not noisy:
-                # dense weight gradients now (they need only dh and x3): the dense range is final
+                # dense weight gradients now (they need only dh, dQ and x3 / h): the dense range is final
                 ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
                 members, dims, scales = members[:3], dims[:3], scales[:3]
 
             def tail():
-                ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [],
-                               [ws['dz3'].data_ptr()], [x3], [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
                 ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [],
                                [ws['dz2'].data_ptr()], [x2], [1.0],
                                [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3,
@@ -807,15 +849,15 @@ class HipExecutor:
                 return ws['loss'], ws['prio'], tail
             tail()
             return (ws['loss'], ws['prio'], None) if split else (ws['loss'], ws['prio'])
-        side.wait_event(self._event('head', main))
+        # fc dgrad: dz3 = (dh W^T) * (x3 > 0) (scalar heads: dh itself is built in this launch)
+        fc_dgrad()
+        side.wait_event(self._event('dz3', main))
         with torch.cuda.stream(side):
             # fc wgrad: dW[F][HH] = x3^T dh, db = sum dh
             ext.qnet_wgrad(_KIND['DFWD'], x3, [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0], ws['dh'].data_ptr(), HH,
                            fw, fb, fw2, fb2, H, HH, mc_fc, 64, 128, 1.0, False)
-        # fc dgrad: dz3 = (dh W^T) * (x3 > 0)
-        ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()], [x3],
-                       [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
-        side.wait_event(self._event('dz3', main))
+            for m, d in zip(hmembers, hdims):           # output layer (B > 32: atomics on the zeroed grad)
+                ext.qnet_wgrad(m[0], m[1], d, m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9], 32, 64, 64, 1.0, True)
         with torch.cuda.stream(side):
             ext.qnet_wgrad(_KIND['C3'], x2, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
                            ws['dz3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0, c3.cout, c3.cout,
@@ -868,6 +910,7 @@ class HipCnnExecutor(HipExecutor):
             'loss': torch.zeros(1, **f32), 'prio': torch.zeros(B, **f32), 'q': torch.zeros(B * self.A, **f32),
             'ones': torch.ones(B, **f32),
         }
+        ws.update(self._head_ws(B, dev))
         self._ws[key] = ws
         return ws
 
@@ -885,16 +928,16 @@ class HipCnnExecutor(HipExecutor):
                 + pad([ws['x3'][i].data_ptr() for i in range(ninst)]) + keep)
         self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale,
                               list(M))
-        self._fc_fwd(packs, ws, B, ninst)
+        self._fc_fwd(packs, flats, ws, B, ninst)
 
-    def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev):
+    def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev, fc_dgrad,
+                      hmembers=(), hdims=()):
         ext = self.ext
         F, HH, H = self.FLAT, self.HH, self.HID
         pko = lambda key: po.data_ptr() + 2 * self.poff[key]
         x3 = ws['x3'][0].data_ptr()
         # dp3 = (dh W_fc^T) * (pooled conv3 output > 0)
-        ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pko('fc/dgrad')], [], [ws['dz3'].data_ptr()], [x3],
-                       [1.0], [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0])
+        fc_dgrad()
         # pool / ReLU / conv dgrad chain per sample -> d(conv pre-activations)
         ext.qnet_cnn_bwd([ws['dz3'].data_ptr(), ws['a1'].data_ptr(), ws['a2'].data_ptr(), ws['a3'].data_ptr(),
                           pko('conv3/dgrad'), pko('conv2/dgrad'), ws['dc1'].data_ptr(), ws['dc2'].data_ptr(),
@@ -914,10 +957,11 @@ class HipCnnExecutor(HipExecutor):
               c3.cout, c3.cout],
              [_KIND['C2'], ws['p1'].data_ptr(), ws['dc2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0,
               c2.cout, c2.cout],
-             [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]],
+             [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]] + list(hmembers),
             [d1, [B * 9, c3.cout, c3.k * c3.k * c3.cin, 0, 0, 3, 3, 3, 3, t3, l3],
-             [B * 36, c2.cout, c2.k * c2.k * c2.cin, 0, 0, 11, 11, 6, 6, t2, l2], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]],
-            [self.input_scale, 1.0, 1.0, 1.0])
+             [B * 36, c2.cout, c2.k * c2.k * c2.cin, 0, 0, 11, 11, 6, 6, t2, l2],
+             [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]] + list(hdims),
+            [self.input_scale] + [1.0] * (3 + len(hmembers)))
         if self.noisy and noise is not None:
             ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                 len(self.noisy_jobs), self._noisy_max)

@@ -1,10 +1,11 @@
 """Phase timing (s_memtime) of the scalar head kernel in the flagship configuration
 (Nature-CNN, fused acting): learner block 0 and the fused acting block."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, '.')
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dist_dqn_amd.actors.device_actor import DeviceActor  # noqa: E402
 from dist_dqn_amd.config import preset  # noqa: E402
 from dist_dqn_amd.learner import Learner  # noqa: E402
@@ -27,8 +28,9 @@ for _ in range(30):
 torch.cuda.synchronize()
 t = net.executor.head_prof.double().tolist()
 d = lambda i, j: t[j] - t[i]
-print('learner block 0 (cycles): Q tiles %.0f | dueling+TD loss %.0f | dW/db %.0f | dH %.0f | total %.0f'
-      % (d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(0, 4)))
+print('learner block 0 (cycles): Q tile %.0f | TD loss + dQ %.0f | dH %.0f | total %.0f'
+      % (d(0, 1), d(1, 2), d(2, 3), d(0, 3)))
 if t[16]:
-    print('acting block (cycles): Q tiles %.0f | to actor %.0f | actor step %.0f | total %.0f'
+    print('acting block (cycles): Q tile %.0f | decision + frames %.0f | advance %.0f | total %.0f'
           % (d(16, 17), d(17, 18), d(18, 19), d(16, 19)))
+

@@ -1,6 +1,11 @@
 """Phase timing of the fused trunk kernel (s_memtime stamps written by thread 0
 of every workgroup): input staging, conv1, conv2, conv3 in shader-clock cycles."""
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from dist_dqn_amd.config import preset
 from dist_dqn_amd.models.network import Network

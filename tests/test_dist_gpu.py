@@ -185,7 +185,7 @@ def test_bench_two_ranks_replicas_equal(tmp_path):
     env = dict(os.environ, DQN_DIST_BACKEND='gloo', OMP_NUM_THREADS='4')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(root, 'bench.py'),
-           '--gpus', '2', '--steps', '20', '--warmup', '5', '--replay', '20000', '--actor_envs', '0']
+           '--gpus', '2', '--steps', '20', '--warmup', '5', '--replay', '20000']
     out = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith('{')][-1]
