@@ -165,7 +165,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
   TORCH_CHECK(max_grid <= 256 || ticket.numel() >= 17 * 32, "optim_pack: wide grid needs the 17x32-word ticket");
   TORCH_CHECK(max_grid >= 1 && max_grid <= 65535, "optim_pack: max_grid");
-  TORCH_CHECK(op >= -1 && op <= 6, "optim_pack: op");
+  TORCH_CHECK(op >= -1 && op <= 7, "optim_pack: op (7 = rmsprop without momentum)");
   float* tgt = nullptr;
   void* tgtp = nullptr;
   if (target.has_value() && target->defined()) {

@@ -45,6 +45,10 @@ DQN_DEV void update_one(float& w, float g, float& s0, float& s1, const OptHP& h,
     s0 = h.rho * s0 + (1.f - h.rho) * g * g;
     s1 = h.rms_mom * s1 + h.lr * g / sqrtf(s0 + h.rms_eps);
     w -= s1;
+  } else if constexpr (OP == 7) {     // rmsprop with momentum 0 (the TF / reference default):
+    s0 = h.rho * s0 + (1.f - h.rho) * g * g;   // mom = 0 * mom + u == u exactly, so mom is
+    s1 = h.lr * g / sqrtf(s0 + h.rms_eps);     // written (checkpoint slot) but never read
+    w -= s1;
   } else if constexpr (OP == 3) {     // adam (TF epsilon-hat form)
     s0 = h.b1 * s0 + (1.f - h.b1) * g;
     s1 = h.b2 * s1 + (1.f - h.b2) * g * g;
@@ -88,7 +92,7 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
     float4 wv = W[i], gv = G[i];
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
     if constexpr (OP != 0) a = S0[i];
-    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6) b = S1[i];
+    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6) b = S1[i];      // (OP 7: mom never read)
     const bool reg = (i * 4) < h.reg_end;       // reg_end is a multiple of 64
     float ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
     float aa[4] = {a.x, a.y, a.z, a.w}, bb[4] = {b.x, b.y, b.z, b.w};
@@ -100,7 +104,7 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
     W[i] = nw;
     if (sync) T[i] = nw;
     if constexpr (OP != 0) S0[i] = make_float4(aa[0], aa[1], aa[2], aa[3]);
-    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6) S1[i] = make_float4(bb[0], bb[1], bb[2], bb[3]);
+    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7) S1[i] = make_float4(bb[0], bb[1], bb[2], bb[3]);
   }
   // last block advances global_step and (Adam) the beta powers. Every block
   // read beta_pow above, before its ticket add, so the update cannot race.
@@ -224,7 +228,8 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   }
   const bool sync = UPD && tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
   const bool psync = sync && tgt_packed != nullptr;
-  constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6;
+  constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7;   // second slot written
+  constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
   constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
   if (sampler && per.sum != nullptr) {
@@ -286,13 +291,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     load4(W + e0, vec, ok, w);
     if constexpr (UPD) load4(G + e0, vec, ok, g);
     if constexpr (ONE) load4(S0 + e0, vec, ok, a);
-    if constexpr (TWO) load4(S1 + e0, vec, ok, b);
+    if constexpr (TWO_LD) load4(S1 + e0, vec, ok, b);
     if (noisy) {
       load4(W + s0i, vec, ok, ws);
       if constexpr (UPD) {
         if (gnoise == nullptr) load4(G + s0i, vec, ok, gs);
         if constexpr (ONE) load4(S0 + s0i, vec, ok, as);
-        if constexpr (TWO) load4(S1 + s0i, vec, ok, bs);
+        if constexpr (TWO_LD) load4(S1 + s0i, vec, ok, bs);
       }
     }
     if constexpr (UPD) {
@@ -494,6 +499,7 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
     case 4: hipLaunchKernelGGL(optim_kernel<4>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
     case 5: hipLaunchKernelGGL(optim_kernel<5>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
     case 6: hipLaunchKernelGGL(optim_kernel<6>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
+    case 7: hipLaunchKernelGGL(optim_kernel<7>, grid, block, 0, st, w, g, s0, s1, beta_pow, step, ticket, h, n4, tgt, tfreq < 1 ? 1 : tfreq); break;
     default: break;
   }
 }
@@ -530,7 +536,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   switch (op) {
     case -1: OPK(-1); break;
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
-    case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break;
+    case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break; case 7: OPK(7); break;
     default: break;
   }
 #undef OPK

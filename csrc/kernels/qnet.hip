@@ -866,10 +866,6 @@ __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
     case L_NAT_CONV3_FWD: group_member<NatC3, 256, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     case L_DENSE_FWD_RELU: group_member<DenseLoader, 32, 64, 128>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     case L_HEAD_WGRAD: group_member<DenseLoader, 32, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    // sweep variants (kind + 100 * variant, DQN_TILES): the r1 128-row tiles
-    case 100 + L_NAT_CONV1_FRAMES: group_member<NatF1, 128, 256, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case 100 + L_NAT_CONV2_FWD: group_member<NatC2, 128, 128, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case 100 + L_NAT_CONV3_FWD: group_member<NatC3, 128, 192, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     default: break;
   }
 }
@@ -877,9 +873,6 @@ __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
 
 static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
   switch (kind) {
-    case 100 + L_NAT_CONV1_FRAMES: MC = 128; KB = 256; NB = 32; break;
-    case 100 + L_NAT_CONV2_FWD: MC = 128; KB = 128; NB = 64; break;
-    case 100 + L_NAT_CONV3_FWD: MC = 128; KB = 192; NB = 64; break;
     case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = 256; KB = 64; NB = 32; break;
     case L_NAT_CONV2_FWD: MC = 256; KB = 64; NB = 64; break;
     case L_NAT_CONV3_FWD: MC = 256; KB = 64; NB = 64; break;
@@ -895,10 +888,6 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   int total = 0;
   size_t lds = 0;
   for (int i = 0; i < G.n; ++i) {
-    // DQN_TILES wgrad slots: 13 = conv1 (frame loader), 14 = conv2, 15 = conv3
-    const int slot = G.kind[i] == L_NAT_CONV1_FRAMES ? 13 : G.kind[i] == L_NAT_CONV2_FWD ? 14
-                   : G.kind[i] == L_NAT_CONV3_FWD ? 15 : 0;
-    if (slot) G.kind[i] += 100 * tile_variant(slot);
     int MC, KB, NB;
     size_t l;
     if (!wgrad_tiles(G.kind[i], MC, KB, NB, l)) return -1;

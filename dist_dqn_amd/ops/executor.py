@@ -272,7 +272,7 @@ class HipExecutor:
         step's minibatch (uniform, or prioritized after writing this step's priorities).
         ``target_noise`` (noisy nets): the target is mixed + packed under it in the same launch
         and bound to it (no target mix launch next step). Returns True."""
-        from ..optim import OPT_IDS
+        from ..optim import kernel_op
         dev = flat.device
         jobs = self._upd_jobs(dev)
         hp = opt.hp
@@ -293,7 +293,7 @@ class HipExecutor:
         else:
             p = self.packed(flat)
             pt = self.packed(target) if target is not None else None
-        self.ext.optim_pack(OPT_IDS[opt.name], flat, grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr),
+        self.ext.optim_pack(kernel_op(opt), flat, grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr),
                             float(opt.reg_param), int(opt.layout.reg_end), float(grad_scale), global_step,
                             [float(hp['momentum']), float(hp['rho']), float(hp['rms_mom']), float(hp['rms_eps']),
                              float(hp['b1']), float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']),

@@ -148,13 +148,13 @@ def optimizer_step(opt, param: torch.Tensor, grad: torch.Tensor, grad_scale: flo
                    global_step: Optional[torch.Tensor] = None, target: Optional[torch.Tensor] = None,
                    target_freq: int = 1):
     ext = _ext.load(required=True)
-    from ..optim import OPT_IDS
+    from ..optim import kernel_op
     hp = opt.hp
     s0 = opt.slots[0] if len(opt.slots) > 0 else param
     s1 = opt.slots[1] if len(opt.slots) > 1 else param
     if getattr(opt, 'ticket', None) is None or opt.ticket.device != param.device:
         opt.ticket = torch.zeros(1, dtype=torch.int32, device=param.device)
-    ext.optimizer_step(OPT_IDS[opt.name], param, grad, s0, s1, opt.beta_powers, opt.ticket,
+    ext.optimizer_step(kernel_op(opt), param, grad, s0, s1, opt.beta_powers, opt.ticket,
                        float(opt.lr), float(opt.reg_param), int(opt.layout.reg_end),
                        float(grad_scale), global_step if global_step is not None else opt.beta_powers,
                        global_step is not None, [float(hp['momentum']), float(hp['rho']),

@@ -24,6 +24,15 @@ import torch
 from .models.params import FlatLayout
 
 OPT_IDS = {'sgd': 0, 'momentum': 1, 'rmsprop': 2, 'adam': 3, 'adagrad': 4, 'adadelta': 5, 'ftrl': 6}
+RMSPROP_NO_MOMENTUM = 7    # kernel variant: rmsprop with momentum 0 never reads the mom slot
+
+
+def kernel_op(opt) -> int:
+    """Kernel op id of an optimizer (RMSProp at the TF default momentum 0 skips its mom read:
+    bit-identical update, one fp32 slot less of HBM traffic per step)."""
+    if opt.name == 'rmsprop' and float(opt.hp['rms_mom']) == 0.0:
+        return RMSPROP_NO_MOMENTUM
+    return OPT_IDS[opt.name]
 
 # (slot suffixes in TF checkpoint naming, initial value)
 _SLOTS = {
