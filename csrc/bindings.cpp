@@ -148,7 +148,9 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
                 std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
-                c10::optional<torch::Tensor> tpk) {
+                c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng) {
+  // noise_rng (noisy nets): [seed, counter] of the noise stream whose next samples an earlier
+  // launch of this step drew (the fc dgrad's noise duty); the last block advances the counter
   // tnoise / teff / tpk (noisy nets): mix + pack the target under tnoise in the same launch
   // per_p: [] or [sum, min, max_p, P, levels, upd_idx, upd_td, rng, size, step, idx_out, w_out,
   //   state_idx, next_idx, actions, rewards, dones, gammas, a_out, r_out, d_out, g_out, st_slots,
@@ -257,6 +259,12 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
     tef = ptr<float>(*teff);
     tpkp = tpk->data_ptr();
   }
+  int64_t* nrng = nullptr;
+  if (noise_rng.has_value() && noise_rng->defined()) {
+    CHECK_T((*noise_rng), torch::kInt64);
+    TORCH_CHECK(op >= 0 && noise_rng->numel() >= 2, "optim_pack: noise_rng = [seed, counter] (update calls)");
+    nrng = ptr<int64_t>(*noise_rng);
+  }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
@@ -264,7 +272,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
-                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, cur_stream());
+                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {

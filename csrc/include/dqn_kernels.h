@@ -45,7 +45,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
-                       hipStream_t st);
+                       int64_t* noise_rng, hipStream_t st);
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
 void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();

@@ -44,6 +44,11 @@ struct ConvArgs {
   float* zero_ptr; int zero_n;
   const float* loss_parts; int nparts;
   float* loss_out; float loss_mul;
+  // noisy nets: draw the next noise samples (noise_normals4 at the stream's current counter,
+  // spread over the launch's blocks) into nz_out0[0, nz_n) | nz_out1[0, nz_n); the counter is
+  // advanced later by the fused optimizer's last block (every block of this launch read it)
+  float* nz_out0; float* nz_out1; int nz_n;
+  const int64_t* nz_rng;
 };
 
 struct WgradArgs {
@@ -108,7 +113,10 @@ struct HeadArgs {
   const float* act_vli;
   // scalar heads (head_loss_kernel): per-16-sample-tile loss partials (summed by the fc dgrad
   // launch) and dL/dQ as act_t [B][64] (plain / advantage in columns 0..31, value in 32), the dZ
-  // operand of the output layer's grouped weight-gradient members; dH goes to dh
+  // operand of the output layer's grouped weight-gradient members; dH goes to dh.
+  // C51 (c51_train_kernel): per-block loss partials and dL/dlogits as act_t [B][KD] (plain /
+  // advantage at [0, NO), value at [VO, VO + atoms), VO = NO rounded up to 32), the A operand
+  // of the dH igemm and the dZ of the output layer's weight-gradient members
   float* loss_parts;
   void* dq16;
 };
@@ -198,6 +206,7 @@ void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
 void launch_trunk_fwd(const dqn::TrunkArgs& a, int B, int ninst, hipStream_t st);
 void launch_c51_head(const dqn::HeadArgs& a, hipStream_t st);
 size_t c51_head_lds_bytes(const dqn::HeadArgs& a);
+int c51_train_blocks(const dqn::HeadArgs& a);     // learner blocks = loss partials of the training head
 void launch_noisy_mix(const float* flat, float* eff, const float* noise, const dqn::NoisyJob* jobs, int njobs,
                       int max_elems, hipStream_t st);
 void launch_noisy_grad(float* grad, const float* noise, const dqn::NoisyJob* jobs, int njobs, int max_elems,

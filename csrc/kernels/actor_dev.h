@@ -141,4 +141,40 @@ DQN_DEV void actor_step_block(const ActorArgs& a, const float* q, void* lds_scra
   actor_step_block(a, q, lds_scratch, actor_prefetch(a));
 }
 
+// Fused acting with ONE ENV PER WORKGROUP (the head kernels' acting blocks), in two parts so
+// the caller can put its Q computation in between:
+//   actor_env_frames  env e's new frame (+ reset frame): they depend only on the rng state,
+//                     never on Q, so every thread writes them while the Q loads are in flight;
+//   actor_env_finish  thread 0 decides + appends from qe (env e's Q row, visible to thread 0),
+//                     and the LAST block to arrive (ticket) advances the actor state (every
+//                     block read it at its start) and, PER, inserts the E new transitions.
+// flag / st: block LDS scratch.
+DQN_DEV void actor_env_frames(const ActorArgs& x, int e, const ActorPre& pre) {
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int fslot = (int)((pre.f0 + 2 * e) % x.F), rslot = (int)((pre.f0 + 2 * e + 1) % x.F);
+  write_random_frame(x.frames + (int64_t)fslot * x.HW, x.HW, pre.seed, pre.ctr, 0x100u + 2u * e, tid, nth);
+  if (actor_done(x, pre.seed, pre.ctr, e))
+    write_random_frame(x.frames + (int64_t)rslot * x.HW, x.HW, pre.seed, pre.ctr, 0x101u + 2u * e, tid, nth);
+}
+
+DQN_DEV void actor_env_finish(const ActorArgs& x, const float* qe, int e, const ActorPre& pre, const int32_t* st_e,
+                              int* flag, SumtreeLds& st) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int fs, rs;
+    actor_env_step(x, qe, e, pre.t0, pre.f0, pre.eps0, pre.eps_min, pre.decay, pre.seed, pre.ctr, fs, rs, st_e);
+    const int tk = __hip_atomic_fetch_add(x.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = tk == x.E - 1 ? 1 : 0;
+    if (*flag) {
+      actor_advance(x, pre.t0, pre.f0, pre.size0, pre.eps0, pre.eps_min, pre.decay, pre.ctr);
+      __hip_atomic_store(x.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (x.tsum != nullptr) {          // PER: the last block inserts the E new transitions at max priority
+    __syncthreads();
+    if (*flag) sumtree_update_wave(x.tsum, x.tmin, x.tmaxp, nullptr, nullptr, 0.f, 0.f, 1, x.E, x.tP, x.tlevels, st,
+                                   (int)(pre.t0 % x.C), x.C);
+  }
+}
+
 }  // namespace dqn

@@ -44,6 +44,30 @@ DQN_DEV float u01(uint32_t x) {  // [0, 1)
   return (float)(x >> 8) * (1.0f / 16777216.0f);
 }
 
+// Standard normals of the noisy-net stream: Box-Muller over Philox4x32-10 keyed by `seed`
+// at counter `ctr`; call index q yields elements 4q .. 4q+3 of [out0[0, n) | out1[0, n)].
+// (noise_normal_kernel and the fc dgrad launch's noise duty draw the same values.)
+DQN_DEV void noise_normals4(float* out0, float* out1, int n, uint64_t seed, uint64_t ctr, int q) {
+  const int total = out1 != nullptr ? 2 * n : n;
+  const u32x4 r = philox(seed ^ 0x2545f4914f6cdd1dull, ctr, (uint32_t)q, 0x6e6f6973u);
+  const uint32_t u[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float u1 = ((float)(u[2 * h] >> 8) + 1.f) * (1.0f / 16777216.0f);   // (0, 1]
+    const float u2 = (float)(u[2 * h + 1] >> 8) * (1.0f / 16777216.0f);       // [0, 1)
+    const float rad = sqrtf(-2.f * __logf(u1));
+    float sn, cs;
+    __sincosf(6.283185307179586f * u2, &sn, &cs);
+    const float z[2] = {rad * cs, rad * sn};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = 4 * q + 2 * h + j;
+      if (i < n) out0[i] = z[j];
+      else if (i < total) out1[i - n] = z[j];
+    }
+  }
+}
+
 // ----------------------------------------------------------------- reductions
 DQN_DEV float wave_sum(float v) {
 #pragma unroll
@@ -84,6 +108,13 @@ DQN_DEV float wave_sum_dpp(float v) {
   const int iv = __float_as_int(v);
   return (__int_as_float(__builtin_amdgcn_readlane(iv, 0)) + __int_as_float(__builtin_amdgcn_readlane(iv, 16))) +
          (__int_as_float(__builtin_amdgcn_readlane(iv, 32)) + __int_as_float(__builtin_amdgcn_readlane(iv, 48)));
+}
+
+DQN_DEV float wave_max_dpp(float v) {
+  v = row16_max(v);
+  const int iv = __float_as_int(v);
+  return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(iv, 0)), __int_as_float(__builtin_amdgcn_readlane(iv, 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(iv, 32)), __int_as_float(__builtin_amdgcn_readlane(iv, 48))));
 }
 
 // -------------------------------------------------------------------- bf16

@@ -10,6 +10,7 @@
 // then the TF update rule. Adam's beta powers (TF non-slot variables) are
 // read by every block and advanced by the LAST block to finish (arrival
 // ticket), together with global_step, so no extra launch is needed.
+#include <type_traits>
 #include "common.h"
 #include "sample_dev.h"
 #include "sumtree_dev.h"
@@ -159,26 +160,6 @@ struct UpdJob {
 
 DQN_DEV float fnz(float x) { return copysignf(sqrtf(fabsf(x)), x); }
 
-// 4 consecutive floats: one float4 when `vec` (16-byte aligned, all in range), else per-element
-DQN_DEV void load4(const float* p, bool vec, const bool* ok, float* v) {
-  if (vec) {
-    const float4 x = *reinterpret_cast<const float4*>(p);
-    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = ok[j] ? p[j] : 0.f;
-  }
-}
-DQN_DEV void store4(float* p, bool vec, const bool* ok, const float* v) {
-  if (vec) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (ok[j]) p[j] = v[j];
-  }
-}
-
 template <int OP>
 DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, int reg_end, const OptHP& h,
                   float lr_t, const bool* ok) {
@@ -197,7 +178,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                   act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
                   int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
-                  float* __restrict__ teff, act_t* __restrict__ tpk) {
+                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
@@ -259,20 +240,24 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     if (threadIdx.x == 0) smp.rng[1] = (int64_t)(ctr + 1);   // every lane read it before the barriers
   }
-  for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) {
-    const UpdJob jb = jobs[ji];
+  // One job item = a 32x64 tile (or a 2048-element chunk) updated by 4 consecutive elements per
+  // thread. The body is instantiated per (AL = 16-byte aligned float4 rows, NZ = noisy) so that
+  // every global load of the item (mu / sigma / grad / slots / target / noise factors) is an
+  // UNCONDITIONAL load issued in one batch: out-of-range threads read the job's first element
+  // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
+  // vmcnt wait between loads and serialise the item on memory latency.)
+  auto item = [&](const UpdJob& jb, auto al_c, auto nz_c) {
+    constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value;
     const bool elem = jb.kind == 1;
-    const bool noisy = jb.sig_off >= 0;
     bool ok[4];
     int k, n;                      // row (tile) and column / element index within the tensor
-    bool rowok, vec;
+    bool rowok;
     int64_t e0;
     if (elem) {                    // chunk of up to 2048 elements: 4 per thread
       k = 0;
       n = 4 * t;
       rowok = true;
       e0 = (int64_t)jb.src_off + n;
-      vec = n + 4 <= jb.K;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ok[j] = n + j < jb.K;
     } else {                       // tile: row r, columns c4..c4+3
@@ -281,75 +266,106 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       n = jb.n0 + c4;
       rowok = k < jb.K;
       e0 = (int64_t)jb.src_off + (int64_t)k * jb.N + n;
-      vec = rowok && n + 4 <= jb.N && (jb.N % 4) == 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ok[j] = rowok && n + j < jb.N;
     }
-    const int64_t s0i = noisy ? (elem ? (int64_t)jb.sig_off + n : (int64_t)jb.sig_off + (int64_t)k * jb.N + n) : e0;
-    // every load (mu and, for noisy layers, sigma) is issued before any math
-    float w[4], g[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], e[4];
-    load4(W + e0, vec, ok, w);
-    if constexpr (UPD) load4(G + e0, vec, ok, g);
-    if constexpr (ONE) load4(S0 + e0, vec, ok, a);
-    if constexpr (TWO_LD) load4(S1 + e0, vec, ok, b);
-    if (noisy) {
-      load4(W + s0i, vec, ok, ws);
-      if constexpr (UPD) {
-        if (gnoise == nullptr) load4(G + s0i, vec, ok, gs);
-        if constexpr (ONE) load4(S0 + s0i, vec, ok, as);
-        if constexpr (TWO_LD) load4(S1 + s0i, vec, ok, bs);
-      }
-    }
-    if constexpr (UPD) {
-      if (noisy && gnoise != nullptr) {                   // dL/dsigma from the mu-slot gradient
-        const float gin = (!elem && jb.ein_off >= 0 && rowok) ? fnz(gnoise[jb.ein_off + k]) : 1.f;
+    const int64_t d0 = e0 - jb.src_off;                  // offset within the tensor
+    // clamped element indices: AL -> all 4 in range or none (one float4), else per element
+    int64_t ix[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) gs[j] = ok[j] ? g[j] * gin * fnz(gnoise[jb.eout_off + n + j]) : 0.f;
-      }
-      upd4<OP>(w, g, a, b, e0, h.reg_end, h, lr_t, ok);
-      store4(W + e0, vec, ok, w);
-      if constexpr (ONE) store4(S0 + e0, vec, ok, a);
-      if constexpr (TWO) store4(S1 + e0, vec, ok, b);
-      if (sync) store4(tgt + e0, vec, ok, w);
-      if (noisy) {
-        upd4<OP>(ws, gs, as, bs, s0i, h.reg_end, h, lr_t, ok);
-        store4(W + s0i, vec, ok, ws);
-        if constexpr (ONE) store4(S0 + s0i, vec, ok, as);
-        if constexpr (TWO) store4(S1 + s0i, vec, ok, bs);
-        if (sync) store4(tgt + s0i, vec, ok, ws);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) e[j] = w[j];
-    if (noisy) {
-      const float fin = (!elem && jb.ein_off >= 0 && rowok) ? fnz(noise[jb.ein_off + k]) : 1.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (ok[j]) e[j] = w[j] + ws[j] * fin * fnz(noise[jb.eout_off + n + j]);
-    }
-    // noisy nets, tmix: the TARGET's next effective weights under tnoise ride along (its
-    // fp32 mu / sigma, or this update's values when the hard sync copied them just now)
-    float te[4];
-    if (tmix) {
-      float tw[4], tws[4];
-      if (sync) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { tw[j] = w[j]; tws[j] = noisy ? ws[j] : 0.f; }
+    for (int j = 0; j < 4; ++j) ix[j] = (AL ? ok[0] : ok[j]) ? d0 + j : 0;
+    auto ld = [&](const float* base, int64_t off, float* v) {
+      if constexpr (AL) {
+        const float4 x = *reinterpret_cast<const float4*>(base + off + ix[0]);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
       } else {
-        load4(tgt + e0, vec, ok, tw);
-        if (noisy) load4(tgt + s0i, vec, ok, tws);
-      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) te[j] = tw[j];
-      if (noisy) {
-        const float fin = (!elem && jb.ein_off >= 0 && rowok) ? fnz(tnoise[jb.ein_off + k]) : 1.f;
+        for (int j = 0; j < 4; ++j) v[j] = base[off + ix[j]];
+      }
+    };
+    auto st = [&](float* base, int64_t off, const float* v) {
+      if constexpr (AL) {
+        if (ok[0]) *reinterpret_cast<float4*>(base + off + d0) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (ok[j]) te[j] = tw[j] + tws[j] * fin * fnz(tnoise[jb.eout_off + n + j]);
+          if (ok[j]) base[off + d0 + j] = v[j];
       }
-      if (jb.eff) store4(teff + e0, vec, ok, te);
+    };
+    const int64_t mo = jb.src_off, so = NZ ? jb.sig_off : jb.src_off;
+    // ---- every load of the item, issued before any math
+    float w[4], g[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], tw[4], tws[4], e[4], te[4];
+    ld(W, mo, w);
+    if constexpr (UPD) ld(G, mo, g);
+    if constexpr (ONE) ld(S0, mo, a);
+    if constexpr (TWO_LD) ld(S1, mo, b);
+    if constexpr (NZ) {
+      ld(W, so, ws);
+      if constexpr (UPD) {
+        ld(G, so, gs);                                    // (replaced below when derived from gnoise)
+        if constexpr (ONE) ld(S0, so, as);
+        if constexpr (TWO_LD) ld(S1, so, bs);
+      }
     }
-    if (jb.eff) store4(eff + e0, vec, ok, e);
+    if (tmix) {                                           // (sync steps use this update's values)
+      ld(tgt, mo, tw);
+      if constexpr (NZ) ld(tgt, so, tws);
+    }
+    // factorised-noise factors: f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
+    float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
+    float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};
+    if constexpr (NZ) {
+      const bool hin = !elem && jb.ein_off >= 0;
+      const int ki = jb.ein_off + (hin && rowok ? k : 0);            // clamped: always in range
+      const float* gn = gnoise != nullptr ? gnoise : noise;
+      const float* tn = tmix ? tnoise : noise;
+      const float ni = noise[hin ? ki : 0], gi = gn[hin ? ki : 0], ti = tn[hin ? ki : 0];
+      float no[4], go[4], to[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int oi = jb.eout_off + (ok[j] ? n + j : 0);
+        no[j] = noise[oi]; go[j] = gn[oi]; to[j] = tn[oi];
+      }
+      if (hin) { nin = fnz(ni); gin = fnz(gi); tin = fnz(ti); }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); tout[j] = fnz(to[j]); }
+    }
+    // ---- update
+    if constexpr (UPD) {
+      if (NZ && gnoise != nullptr) {                      // dL/dsigma from the mu-slot gradient
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gs[j] = ok[j] ? g[j] * gin * gout[j] : 0.f;
+      }
+      upd4<OP>(w, g, a, b, e0, h.reg_end, h, lr_t, ok);
+      st(W, mo, w);
+      if constexpr (ONE) st(S0, mo, a);
+      if constexpr (TWO) st(S1, mo, b);
+      if (sync) st(tgt, mo, w);
+      if constexpr (NZ) {
+        upd4<OP>(ws, gs, as, bs, so + d0, h.reg_end, h, lr_t, ok);
+        st(W, so, ws);
+        if constexpr (ONE) st(S0, so, as);
+        if constexpr (TWO) st(S1, so, bs);
+        if (sync) st(tgt, so, ws);
+      }
+    }
+    // ---- effective values (noisy: mu + sigma f(eps_in) f(eps_out)) of this net and, tmix,
+    //      of the TARGET under its own next noise sample
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      e[j] = w[j];
+      if constexpr (NZ) e[j] = w[j] + ws[j] * nin * nout[j];
+    }
+    if (tmix) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float mu = sync ? w[j] : tw[j];
+        te[j] = mu;
+        if constexpr (NZ) te[j] = mu + (sync ? ws[j] : tws[j]) * tin * tout[j];
+      }
+      if (jb.eff) st(teff, mo, te);
+    }
+    if (jb.eff) st(eff, mo, e);
     if (elem) {
       if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
         float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
@@ -363,7 +379,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
           if (mf) mf[j] = te[j];
         }
       }
-      continue;                    // uniform per block: no barrier below is skipped unevenly
+      return;                      // uniform per block: no barrier below is skipped unevenly
     }
     // bf16 fragments of this tile into dst (+ dst2): dgrad straight from the registers (4
     // consecutive K' of one lane's slot), forward through an LDS transpose of the tile
@@ -400,6 +416,19 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     };
     emit(e, packed, psync ? tgt_packed : nullptr);
     if (tmix) emit(te, tpk, nullptr);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) {
+    const UpdJob jb = jobs[ji];
+    const bool nz = jb.sig_off >= 0;
+    // float4 rows: 16-byte aligned tensor (and sigma) offsets and a row / chunk length % 4 == 0
+    const bool al = ((jb.src_off | (nz ? jb.sig_off : 0)) & 3) == 0 && ((jb.kind == 1 ? jb.K : jb.N) & 3) == 0;
+    if (al) {
+      if (nz) item(jb, T_{}, T_{}); else item(jb, T_{}, F_{});
+    } else {
+      if (nz) item(jb, F_{}, T_{}); else item(jb, F_{}, F_{});
+    }
   }
   if (!UPD) return;
   __shared__ int s_last;
@@ -427,6 +456,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         beta_pow[0] *= h.b1;
         beta_pow[1] *= h.b2;
       }
+      if (noise_rng != nullptr) noise_rng[1] += 1;      // (the drawing launch completed before this one)
       __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     s_last = last ? 1 : 0;
@@ -509,7 +539,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
                        int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
-                       void* tpk, hipStream_t st) {
+                       void* tpk, int64_t* noise_rng, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
@@ -528,11 +558,11 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
 #define OPK(N) do { if (tnoise != nullptr) \
     hipLaunchKernelGGL((optim_pack_kernel<N, true>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
                        ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe, tnoise, \
-                       teff, reinterpret_cast<act_t*>(tpk)); \
+                       teff, reinterpret_cast<act_t*>(tpk), noise_rng); \
   else \
     hipLaunchKernelGGL((optim_pack_kernel<N, false>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
                        ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe, tnoise, \
-                       teff, reinterpret_cast<act_t*>(tpk)); } while (0)
+                       teff, reinterpret_cast<act_t*>(tpk), noise_rng); } while (0)
   switch (op) {
     case -1: OPK(-1); break;
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;

@@ -295,6 +295,15 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[u][i], bf[u][j], acc[i][j]);
   }
+  // noise duty (every thread of the block, before the split-K waves retire)
+  if (a.nz_out0 != nullptr) {
+    const int nblk = gridDim.x * gridDim.y * gridDim.z;
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int nq = ((a.nz_out1 != nullptr ? 2 : 1) * a.nz_n + 3) / 4;
+    const int nt = blockDim.x, tq = (int)threadIdx.x;
+    const uint64_t seed = (uint64_t)a.nz_rng[0], ctr = (uint64_t)a.nz_rng[1];
+    for (int q = blk * nt + tq; q < nq; q += nblk * nt) noise_normals4(a.nz_out0, a.nz_out1, a.nz_n, seed, ctr, q);
+  }
   if constexpr (KSPLIT > 1) {
     // waves wk > 0 hand partial tiles to wk == 0 through LDS
     const int slot = ((wm * WN + wn) * (KSPLIT - 1));
@@ -597,38 +606,17 @@ __global__ void __launch_bounds__(kHeadThreads) head_loss_kernel(HeadArgs a) {
     int32_t st_e[4] = {0, 0, 0, 0};                              // env e's frame stack (thread 0)
     if (tid == 0)
       for (int c = 0; c < 4; ++c) st_e[c] = x.stacks[(int64_t)e * x.K + min(c, x.K - 1)];
+    // env e's frames first (rng-only), then its Q row, then decision / append / advance
+    actor_env_frames(x, e, pre);
     const int r0 = (e / kHeadRows) * kHeadRows;
     const void* hh = a.infer ? a.h[0] : a.act_h;
     head_q_tile(a, S, hh, hh, hh, 0, 0, 0, 1, r0, min(kHeadRows, E - r0));
     HEAD_MARK(1);
     const float* qe = &S.q[0][e - r0][0];
     if (a.infer && a.q_out != nullptr && tid < A) a.q_out[(int64_t)e * A + tid] = qe[tid];
-    if (tid == 0) {
-      int fs, rs;
-      S.flag = actor_env_step(x, qe, e, pre.t0, pre.f0, pre.eps0, pre.eps_min, pre.decay, pre.seed, pre.ctr, fs, rs,
-                              st_e);
-    }
     __syncthreads();
-    const int fslot = (int)((pre.f0 + 2 * e) % x.F), rslot = (int)((pre.f0 + 2 * e + 1) % x.F);
-    write_random_frame(x.frames + (int64_t)fslot * x.HW, x.HW, pre.seed, pre.ctr, 0x100u + 2u * e, tid, kHeadThreads);
-    if (S.flag)
-      write_random_frame(x.frames + (int64_t)rslot * x.HW, x.HW, pre.seed, pre.ctr, 0x101u + 2u * e, tid, kHeadThreads);
     HEAD_MARK(2);
-    // the LAST acting block to arrive advances the actor state (every block read it at its start)
-    __syncthreads();
-    if (tid == 0) {
-      const int tk = __hip_atomic_fetch_add(x.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      S.flag = tk == E - 1 ? 1 : 0;
-      if (S.flag) {
-        actor_advance(x, pre.t0, pre.f0, pre.size0, pre.eps0, pre.eps_min, pre.decay, pre.ctr);
-        __hip_atomic_store(x.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (x.tsum != nullptr) {          // PER: the last block inserts the E new transitions at max priority
-      __syncthreads();
-      if (S.flag) sumtree_update_wave(x.tsum, x.tmin, x.tmaxp, nullptr, nullptr, 0.f, 0.f, 1, E, x.tP, x.tlevels, S.st,
-                                      (int)(pre.t0 % x.C), x.C);
-    }
+    actor_env_finish(x, qe, e, pre, st_e, &S.flag, S.st);
     HEAD_MARK(3);
     return;
   }

@@ -53,8 +53,15 @@ void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::v
            std::vector<int64_t> aux, std::vector<double> aux_f) {
   dqn::ConvArgs a = conv_args(in, w, bias, out, mask, scale, dims);
   if (!aux.empty()) {
-    TORCH_CHECK(aux.size() == 5 && aux_f.size() == 1 && aux[0] % 16 == 0 && aux[1] % 4 == 0 && aux[3] <= 64,
-                "igemm aux = [zero_ptr, zero_n, loss_parts, nparts, loss_out], [loss_mul]");
+    // + optional noise duty [out0, out1, n, rng]: the next noisy-net samples at the stream's counter
+    TORCH_CHECK((aux.size() == 5 || aux.size() == 9) && aux_f.size() == 1 && aux[0] % 16 == 0 && aux[1] % 4 == 0 &&
+                aux[3] <= 64, "igemm aux = [zero_ptr, zero_n, loss_parts, nparts, loss_out(, nz_out0, nz_out1, "
+                "nz_n, nz_rng)], [loss_mul]");
+    if (aux.size() == 9) {
+      TORCH_CHECK(aux[5] != 0 && aux[7] >= 1 && aux[8] != 0, "igemm noise duty: out0, n, rng");
+      a.nz_out0 = P<float*>(aux[5]); a.nz_out1 = P<float*>(aux[6]); a.nz_n = (int)aux[7];
+      a.nz_rng = P<const int64_t*>(aux[8]);
+    }
     a.zero_ptr = P<float*>(aux[0]); a.zero_n = (int)aux[1];
     a.loss_parts = P<const float*>(aux[2]); a.nparts = (int)aux[3]; a.loss_out = P<float*>(aux[4]);
     a.loss_mul = (float)aux_f[0];
@@ -232,14 +239,20 @@ void c51_head(std::vector<int64_t> ints, std::vector<int64_t> dist, std::vector<
               std::vector<int64_t> w, std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv,
               std::vector<int64_t> io, std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
               std::vector<int64_t> actor, std::vector<double> actor_f, int64_t prof, std::vector<int64_t> lg,
-              std::vector<int64_t> vl, int64_t act_h) {
-  // training + actor: fused acting; lg / vl then carry one more entry, the actors' logits
+              std::vector<int64_t> vl, int64_t act_h, std::vector<int64_t> qp) {
+  // training + actor: fused acting; lg / vl then carry one more entry, the actors' logits.
+  // qp (training): [loss_parts (>= c51_train_blocks floats), dout16 act_t [B][KD]]
   TORCH_CHECK(dist.size() == 1 && flts.size() == 2, "c51 args");
   dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h);
   a.atoms = (int)dist[0]; a.vmin = (float)flts[0]; a.vmax = (float)flts[1];
   TORCH_CHECK(a.atoms >= 2 && a.atoms <= 64, "C51: 2..64 atoms (one wave64 lane per atom)");
   TORCH_CHECK(a.vmax > a.vmin, "C51 support");
   TORCH_CHECK(c51_head_lds_bytes(a) <= 160 * 1024, "C51 head: batch too large for one workgroup's LDS");
+  if (!a.infer) {
+    TORCH_CHECK(qp.size() == 2 && qp[0] != 0 && qp[1] != 0 && io[6] != 0, "C51 training: loss partials, dout16, prio");
+    a.loss_parts = P<float*>(qp[0]);
+    a.dq16 = P<void*>(qp[1]);
+  }
   a.prof = P<int64_t*>(prof);
   if (a.act_E > 0) {
     TORCH_CHECK(!lg.empty() && (!a.dueling || vl.size() == lg.size()), "c51 fused acting: the actors' logits");
@@ -250,7 +263,8 @@ void c51_head(std::vector<int64_t> ints, std::vector<int64_t> dist, std::vector<
   TORCH_CHECK(lg.size() <= 3 && vl.size() <= 3, "c51: up to 3 precomputed logit buffers");
   for (size_t i = 0; i < lg.size(); ++i) a.lgi[i] = P<const float*>(lg[i]);
   for (size_t i = 0; i < vl.size(); ++i) a.vli[i] = P<const float*>(vl[i]);
-  TORCH_CHECK(lg.empty() || !a.dueling || vl.size() == lg.size(), "c51: dueling needs value logits too");
+  TORCH_CHECK(!a.dueling || vl.size() == lg.size(), "c51: dueling needs value logits too");
+  TORCH_CHECK(a.infer ? lg.size() >= 1 : (lg.size() == 2 || lg.size() == 3), "c51: logits of every instance");
   launch_c51_head(a, cur_stream());
 }
 
@@ -336,7 +350,8 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),
         pybind11::arg("io"), pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),
         pybind11::arg("actor_f"), pybind11::arg("prof") = 0, pybind11::arg("lg") = std::vector<int64_t>{},
-        pybind11::arg("vl") = std::vector<int64_t>{}, pybind11::arg("act_h") = 0);
+        pybind11::arg("vl") = std::vector<int64_t>{}, pybind11::arg("act_h") = 0,
+        pybind11::arg("qp") = std::vector<int64_t>{});
   m.def("qnet_noisy_mix", &noisy_mix);
   m.def("qnet_noisy_grad", &noisy_grad);
   m.attr("NOISY_JOB_INTS") = (int)(sizeof(dqn::NoisyJob) / sizeof(int));

@@ -171,7 +171,11 @@ class Network:
         ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad)."""
         kw = {}
         if self._premixed and not sigma_grads:
+            # the fused noisy optimizer follows: it derives dL/dsigma itself, and the next samples
+            # are drawn by a launch of this backward (no noise launch of their own)
             kw['sigma_grads'] = False
+            kw['draw_noise'] = (self.noise_next, self.noise_target, self.noise_rng)
+            self._noise_drawn = True
         if acting is not None:     # fused acting (HIP executor): the actors' step rides along
             kw['acting'] = acting
         can_split = split and hasattr(self.executor, 'supports_fused_acting')
@@ -214,8 +218,14 @@ class Network:
             kw = {}
             if self._premixed:
                 # next online sample (+ the next step's target sample); the optimizer derives
-                # dL/dsigma under the current one, mixes the next one in and makes it current
-                self.executor.draw_noise(self.noise_next, self.noise_target, self.noise_rng)
+                # dL/dsigma under the current one, mixes the next one in and makes it current.
+                # The samples were drawn during compute_grads (its fc dgrad launch) when it knew
+                # this fused update follows; the optimizer then advances the stream's counter.
+                if getattr(self, '_noise_drawn', False):
+                    kw['noise_rng'] = self.noise_rng
+                    self._noise_drawn = False
+                else:
+                    self.executor.draw_noise(self.noise_next, self.noise_target, self.noise_rng)
                 kw.update(noise=self.noise_next, grad_noise=self.noise, noise_dst=self.noise,
                           target_noise=self.noise_target)
             ex.update_and_pack(self.optimizer, self.online.flat, self.grad, grad_scale, self.global_step,

@@ -90,6 +90,9 @@ class HipExecutor:
         self.HID = fc.fout
         self.HH = 2 * self.HID if self.dueling else self.HID
         self.FLAT = arch.flat_features
+        # C51 dL/dlogits rows (dout16 [B][KD]): logits at [0, NO), dueling value at [VO, VO + atoms)
+        self.c51_VO = (self.NO + 31) // 32 * 32
+        self.c51_KD = self.c51_VO + ((self.atoms + 31) // 32 * 32 if self.dueling else 0)
         self._plan_packing()
         self._packed: Dict[int, torch.Tensor] = {}
         self._ws: Dict[Tuple[int, int], dict] = {}
@@ -101,7 +104,7 @@ class HipExecutor:
         import os
         self.opt_max_grid = int(os.environ.get('DQN_OPT_GRID', '2048'))
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
-        self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_c51.py, probe_head.py)
+        self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_head.py)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -142,6 +145,15 @@ class HipExecutor:
         add('head/w', H, self.NO, [dict(src_off=lay.offsets[hw], K=H, N=self.NO, mode=0)])
         if self.dueling:
             add('head/v', H, self.atoms, [dict(src_off=lay.offsets['value/output/w'], K=H, N=self.atoms, mode=0)])
+        if self.dist:
+            # C51: dgrad fragments of the output layer(s) for the dH igemm, K' = [logits | value]:
+            # dH = dout16 [B][KD] . (plain / advantage W^T into h's advantage half, Wv^T into the value half)
+            dg = [dict(src_off=lay.offsets[hw], K=self.NO, N=H, nt_off=H // 16 if self.dueling else 0, mode=2,
+                       p0=self.NO)]
+            if self.dueling:
+                dg.append(dict(src_off=lay.offsets['value/output/w'], K=self.atoms, N=H, ks_off=self.c51_VO // 32,
+                               mode=2, p0=self.atoms))
+            add('head/dgrad', self.c51_KD, self.HH, dg)
         # concatenated fc bias (fp32, 2 bf16 slots per float)
         self.poff['fc/bias'] = off
         for n, o in fcs:
@@ -240,7 +252,7 @@ class HipExecutor:
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
                             self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [], [],
-                            [], None, None, None)
+                            [], None, None, None, None)
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
@@ -260,7 +272,7 @@ class HipExecutor:
                         global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1,
                         noise: Optional[torch.Tensor] = None, grad_noise: Optional[torch.Tensor] = None,
                         noise_dst: Optional[torch.Tensor] = None, next_sample=None,
-                        target_noise: Optional[torch.Tensor] = None):
+                        target_noise: Optional[torch.Tensor] = None, noise_rng: Optional[torch.Tensor] = None):
         """Optimizer step + repack in ONE launch (+ the hard target sync under the device
         predicate when ``target`` is given). Noisy nets: ``noise`` (the next sample for this
         flat) is mixed in and bound (see ``premix``); the target's packed copy is not written
@@ -271,7 +283,9 @@ class HipExecutor:
         ``DeviceReplay.next_sample_spec`` dict — one extra block of this launch draws the next
         step's minibatch (uniform, or prioritized after writing this step's priorities).
         ``target_noise`` (noisy nets): the target is mixed + packed under it in the same launch
-        and bound to it (no target mix launch next step). Returns True."""
+        and bound to it (no target mix launch next step). ``noise_rng``: the stream whose next
+        samples ``loss_and_grad(draw_noise=...)`` drew this step; the last block advances its
+        counter. Returns True."""
         from ..optim import kernel_op
         dev = flat.device
         jobs = self._upd_jobs(dev)
@@ -303,7 +317,7 @@ class HipExecutor:
                              if next_sample is not None and next_sample['kind'] == 'uniform' else []),
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
-                            target_noise, teff, tpk)
+                            target_noise, teff, tpk, noise_rng)
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:
@@ -482,12 +496,17 @@ class HipExecutor:
         return ws
 
     def _head_ws(self, B, dev) -> dict:
-        """Scalar heads: per-16-sample-tile loss partials (summed by the fc dgrad launch) and the
-        head's dQ as act_t [B][64] (the output layer's weight-gradient dZ)."""
-        if self.dist:
-            return {}
+        """Per-block loss partials of the head launch (summed by the fc dgrad launch) and the
+        head's dZ rows as act_t: scalar heads dQ [B][64]; C51 dL/dlogits [B][KD] (the dH igemm's
+        A operand; its pad columns stay zero from here on)."""
         f32 = dict(dtype=torch.float32, device=dev)
-        return {'loss_parts': torch.zeros(64, **f32), 'dq16': torch.zeros(B * 64, dtype=self.act_dtype, device=dev)}
+        width = self.c51_KD if self.dist else 64
+        return {'loss_parts': torch.zeros(64, **f32), 'dq16': torch.zeros(B * width, dtype=self.act_dtype, device=dev)}
+
+    def _loss_parts(self, B):
+        """Loss partials the head launch writes: one per 16-sample tile (scalar) or per C51
+        learner block (8 samples each, at most 64 blocks)."""
+        return min((B + 7) // 8, 64) if self.dist else (B + 15) // 16
 
     # ------------------------------------------------------------ forward
     @property
@@ -606,9 +625,10 @@ class HipExecutor:
                                           list(pw) + [pw[0]], list(pwv) + pwv[:1])
             else:
                 lg, vl = self._c51_logits(hs, b, bv, pw, pwv)
-            prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
+            qp = [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()] if not ints[5] else []
+            prof = self.head_prof.data_ptr() if self.head_prof is not None and not ints[5] else 0
             self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
-                                   wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl, act_h)
+                                   wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl, act_h, qp)
         else:
             prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
             self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv,
@@ -654,35 +674,44 @@ class HipExecutor:
         pwv = [p.data_ptr() + 2 * self.poff['head/v'] for p in packs] if self.dueling else []
         return pw, pwv
 
-    def _fc_dgrad(self, ws, B, po, zero=()):
-        """dz3 = (dH W_fc^T) * (x3 > 0) on the igemm kernel. Scalar heads: the launch also zeroes
-        the conv weight-gradient range and sums the head's per-tile loss partials (side duties;
-        the head kernel wrote dH); C51: the head did both itself."""
+    def _fc_dgrad(self, ws, B, po, zero=(), draw_noise=None):
+        """dz3 = (dH W_fc^T) * (x3 > 0) on the igemm kernel; the launch also zeroes the conv
+        weight-gradient range and sums the head's loss partials (side duties). Scalar heads: the
+        head kernel wrote dH; C51: dH = (dout16 [W | Wv]^T) * (h > 0) is one more igemm launch
+        before it, over the head's dL/dlogits rows. draw_noise = (out0, out1, rng): the launch
+        also draws the next noisy-net samples (see ``loss_and_grad``)."""
         F, HH = self.FLAT, self.HH
+        h0, dh = ws['h'][0].data_ptr(), ws['dh'].data_ptr()
+        if self.dist:
+            self.ext.qnet_igemm(_KIND['DDGRAD'], [ws['dq16'].data_ptr()],
+                                [po.data_ptr() + 2 * self.poff['head/dgrad']], [], [dh], [h0], [1.0],
+                                [B, HH, self.c51_KD, HH // 16, HH, 0, 0, 0, 0, 0, 0])
         pk = po.data_ptr() + 2 * self.poff['fc/dgrad']
         x3, dz3 = ws['x3'][0].data_ptr(), ws['dz3'].data_ptr()
-        aux, aux_f = [], []
-        if not self.dist:
-            zp, zn = (zero[0], zero[1]) if zero else (0, 0)
-            aux = [zp, zn, ws['loss_parts'].data_ptr(), (B + 15) // 16, ws['loss'].data_ptr()]
-            aux_f = [1.0 / B]
-        self.ext.qnet_igemm(_KIND['DDGRAD'], [ws['dh'].data_ptr()], [pk], [], [dz3], [x3], [1.0],
-                            [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0], aux, aux_f)
+        zp, zn = (zero[0], zero[1]) if zero else (0, 0)
+        aux = [zp, zn, ws['loss_parts'].data_ptr(), self._loss_parts(B), ws['loss'].data_ptr()]
+        if draw_noise is not None:
+            o0, o1, rng = draw_noise
+            assert o0.dtype == torch.float32 and (o1 is None or o1.numel() == o0.numel()) and rng.dtype == torch.int64
+            aux += [o0.data_ptr(), o1.data_ptr() if o1 is not None else 0, o0.numel(), rng.data_ptr()]
+        self.ext.qnet_igemm(_KIND['DDGRAD'], [dh], [pk], [], [dz3], [x3], [1.0],
+                            [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0], aux, [1.0 / B])
 
     def _head_wgrad_members(self, ws, B, h0, hgrads):
-        """Grouped-wgrad members of the scalar output layer: dW = h^T dQ (dueling: advantage
-        stream over h's second half, value stream over its first half) from the head's dq16."""
-        if self.dist:
-            return [], []
+        """Grouped-wgrad members of the output layer: dW = h^T dZ (dueling: advantage stream over
+        h's second half, value stream over its first half) from the head's dZ rows (dq16):
+        scalar heads dQ (ld 64, value dQ in column 32), C51 dL/dlogits (ld KD, value at VO)."""
         dw, db, dwv, dbv = hgrads
-        H, HH, A = self.HID, self.HH, self.A
+        H, HH = self.HID, self.HH
+        N, NV = (self.NO, self.atoms) if self.dist else (self.A, 1)
+        ld, vo = (self.c51_KD, self.c51_VO) if self.dist else (64, 32)
         dq = ws['dq16'].data_ptr()
         esz = ws['dq16'].element_size()
         if not self.dueling:
-            return ([[_KIND['HW'], h0, dq, 64, dw, db, 0, 0, A, A]], [[B, A, H, 0, 0, 0, HH, 0, 0, 0, 0]])
-        return ([[_KIND['HW'], h0 + esz * H, dq, 64, dw, db, 0, 0, A, A],
-                 [_KIND['HW'], h0, dq + esz * 32, 64, dwv, dbv, 0, 0, 1, 1]],
-                [[B, A, H, 0, 0, 0, HH, 0, 0, 0, 0], [B, 1, H, 0, 0, 0, HH, 0, 0, 0, 0]])
+            return ([[_KIND['HW'], h0, dq, ld, dw, db, 0, 0, N, N]], [[B, N, H, 0, 0, 0, HH, 0, 0, 0, 0]])
+        return ([[_KIND['HW'], h0 + esz * H, dq, ld, dw, db, 0, 0, N, N],
+                 [_KIND['HW'], h0, dq + esz * vo, ld, dwv, dbv, 0, 0, NV, NV]],
+                [[B, N, H, 0, 0, 0, HH, 0, 0, 0, 0], [B, NV, H, 0, 0, 0, HH, 0, 0, 0, 0]])
 
     # ----------------------------------------------------------- training
     def supports_fused_acting(self) -> bool:
@@ -690,9 +719,13 @@ class HipExecutor:
 
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
-                      split: bool = False, sigma_grads: bool = True):
+                      split: bool = False, sigma_grads: bool = True, draw_noise=None):
         """sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
         optimizer derives dL/dsigma from the mu-slot gradient and the noise itself.
+
+        draw_noise = (out0, out1, rng) (noisy nets, fused optimizer to follow): the fc dgrad launch
+        also draws the next noise samples from the device stream ``rng`` into out0 / out1 (no
+        launch of its own); ``update_and_pack(noise_rng=rng)`` then advances the stream.
 
         acting (fused acting, slot batches only): {'stacks': [E, 4] int32 frame slots of the
         device actors' states, 'ptrs', 'ints', 'f': the actor-step arguments of act_fused}. The
@@ -782,7 +815,7 @@ class HipExecutor:
                    [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
                     wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
                     ws['q'].data_ptr() if not self.dist else 0, dw, db, dwv, dbv, ws['dh'].data_ptr()],
-                   *self._head_packs(packs), zero if self.dist else [],     # (scalar: zeroed in fc dgrad)
+                   *self._head_packs(packs), [],              # (the conv grad range is zeroed by the fc dgrad)
                    [] if acting is None else list(acting['ptrs']) + list(acting['ints']),
                    [] if acting is None else list(acting['f']),
                    act_h=0 if acting is None else ws['h'][ninst].data_ptr(), ws=ws)
@@ -797,7 +830,7 @@ class HipExecutor:
             fw, fb, fw2, fb2 = g('fcl/w'), g('fcl/b'), 0, 0
         # fc dgrad (+ the scalar head's backward: dH, dW_out, db_out from the head's dQ)
         hmembers, hdims = self._head_wgrad_members(ws, B, ws['h'][0].data_ptr(), (dw, db, dwv, dbv))
-        fc_dgrad = lambda: self._fc_dgrad(ws, B, po, zero)
+        fc_dgrad = lambda: self._fc_dgrad(ws, B, po, zero, draw_noise)
         if self.arch.network == 'cnn':
             out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, gnoise, dev, fc_dgrad,
                                      hmembers, hdims)

@@ -1,5 +1,6 @@
-"""Phase timing (s_memtime) of the scalar head kernel in the flagship configuration
-(Nature-CNN, fused acting): learner block 0 and the fused acting block."""
+"""Phase timing (s_memtime) of the head kernel with fused acting: learner block 0 and the
+fused acting block. Scalar head by default; pass e.g. `--distributional --noisy --dueling
+--double_dqn --optimizer=adam` for the C51 training head."""
 import os
 import sys
 
@@ -28,9 +29,17 @@ for _ in range(30):
 torch.cuda.synchronize()
 t = net.executor.head_prof.double().tolist()
 d = lambda i, j: t[j] - t[i]
-print('learner block 0 (cycles): Q tile %.0f | TD loss + dQ %.0f | dH %.0f | total %.0f'
-      % (d(0, 1), d(1, 2), d(2, 3), d(0, 3)))
-if t[16]:
-    print('acting block (cycles): Q tile %.0f | decision + frames %.0f | advance %.0f | total %.0f'
-          % (d(16, 17), d(17, 18), d(18, 19), d(16, 19)))
+if net.arch.distributional:
+    print('C51 learner block 0 wave 0 (cycles): loads + selection %.0f | target softmax %.0f | projection %.0f | '
+          'CE + dlogits %.0f | block reduce %.0f | total %.0f'
+          % (d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5), d(0, 5)))
+    if t[16]:
+        print('C51 acting block, env 0 (cycles): prefetch + frames %.0f | Q row %.0f | decision + advance %.0f | total %.0f'
+              % (d(16, 17), d(17, 18), d(18, 19), d(16, 19)))
+else:
+    print('learner block 0 (cycles): Q tile %.0f | TD loss + dQ %.0f | dH %.0f | total %.0f'
+          % (d(0, 1), d(1, 2), d(2, 3), d(0, 3)))
+    if t[16]:
+        print('acting block, env 0 (cycles): frames + Q tile %.0f | barrier %.0f | decision + advance %.0f | total %.0f'
+              % (d(16, 17), d(17, 18), d(18, 19), d(16, 19)))
 

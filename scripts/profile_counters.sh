@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 REPO=$(pwd)
-OUT=$REPO/gpurun_out/pmc
+OUT=$REPO/gpurun_out/${PMC_OUT:-pmc}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 ARGS=${BENCH_ARGS:-"--steps 60 --warmup 10"}

@@ -125,6 +125,7 @@ def _worker(rank, world, port, network, extra, errq):
                 assert ctx.world_size == world and ctx.backend == 'gloo' and ctx.device.index == 0
             net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
             broadcast_state(ctx, net)
+            init = net.online.flat.clone()
             rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
             rep.fill_synthetic(2048, 6, seed=rank)          # different data per rank
             ln = Learner(net, rep, cfg, ctx)
@@ -146,9 +147,22 @@ def _worker(rank, world, port, network, extra, errq):
             elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
             outs[overlap] = net.online.flat.clone()
-        # same data, same init: the overlapped schedule reduces the same sums (conv wgrads
-        # use fp32 atomics, so the last bits are order-dependent)
-        torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-6)
+        # same data, same init: the overlapped schedule reduces the same sums. The conv weight
+        # gradients accumulate M-chunk partials with fp32 atomics, so their last bits depend on
+        # arrival order. SGD / RMSProp keep such differences at rounding level; Adam turns a
+        # near-zero gradient into a ~lr * sign(g) step, and the flipped elements then perturb
+        # every later gradient, so there the two runs' parameter updates must agree in direction
+        # and size per tensor instead of elementwise.
+        if cfg.optimizer == 'adam':
+            lay = net.layout
+            for name in lay.names:
+                o, n = lay.offsets[name], lay.numel(name)
+                d1, d0 = outs[1][o:o + n] - init[o:o + n], outs[0][o:o + n] - init[o:o + n]
+                cos = float(torch.nn.functional.cosine_similarity(d1, d0, dim=0))
+                ratio = float(d1.norm() / (d0.norm() + 1e-30))
+                assert cos > 0.99 and abs(ratio - 1) < 0.02, (name, cos, ratio)
+        else:
+            torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-6)
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # noqa: BLE001 - report to the parent
