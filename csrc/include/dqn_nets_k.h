@@ -107,10 +107,9 @@ struct HeadArgs {
   int atoms;                     // C51 head (rainbow.hip): atoms per action, support [vmin, vmax]
   float vmin, vmax;
   int64_t* prof;                 // optional s_memtime phase stamps of block 0 (profiling)
-  const float* lgi[3];           // C51: precomputed logits [B][A*atoms] per instance (igemm, many CUs)
-  const float* vli[3];           // C51 dueling: precomputed value logits [B][atoms]
-  const float* act_lgi;          // C51 + fused acting: the actors' logits [E][A*atoms] (+ act_vli [E][atoms])
-  const float* act_vli;
+  const float* lgi[3];           // C51: precomputed logits rows [B][KD] per instance (one igemm over the
+                                 // combined output layer: logits | pad | dueling value logits at VO)
+  const float* act_lgi;          // C51 + fused acting: the actors' logits rows [E][KD]
   // scalar heads (head_loss_kernel): per-16-sample-tile loss partials (summed by the fc dgrad
   // launch) and dL/dQ as act_t [B][64] (plain / advantage in columns 0..31, value in 32), the dZ
   // operand of the output layer's grouped weight-gradient members; dH goes to dh.

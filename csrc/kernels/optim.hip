@@ -246,8 +246,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // UNCONDITIONAL load issued in one batch: out-of-range threads read the job's first element
   // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
   // vmcnt wait between loads and serialise the item on memory latency.)
-  auto item = [&](const UpdJob& jb, auto al_c, auto nz_c) {
-    constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value;
+  auto item = [&](const UpdJob& jb, auto al_c, auto nz_c, auto dg_c) {
+    // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read
+    constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value, DG = decltype(dg_c)::value;
     const bool elem = jb.kind == 1;
     bool ok[4];
     int k, n;                      // row (tile) and column / element index within the tensor
@@ -302,7 +303,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     if constexpr (NZ) {
       ld(W, so, ws);
       if constexpr (UPD) {
-        ld(G, so, gs);                                    // (replaced below when derived from gnoise)
+        if constexpr (!DG) ld(G, so, gs);
         if constexpr (ONE) ld(S0, so, as);
         if constexpr (TWO_LD) ld(S1, so, bs);
       }
@@ -317,14 +318,14 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     if constexpr (NZ) {
       const bool hin = !elem && jb.ein_off >= 0;
       const int ki = jb.ein_off + (hin && rowok ? k : 0);            // clamped: always in range
-      const float* gn = gnoise != nullptr ? gnoise : noise;
+      const float* gn = DG ? gnoise : noise;             // (DG: the sample the forward used)
       const float* tn = tmix ? tnoise : noise;
-      const float ni = noise[hin ? ki : 0], gi = gn[hin ? ki : 0], ti = tn[hin ? ki : 0];
+      const float ni = noise[hin ? ki : 0], gi = DG ? gn[hin ? ki : 0] : 1.f, ti = tn[hin ? ki : 0];
       float no[4], go[4], to[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int oi = jb.eout_off + (ok[j] ? n + j : 0);
-        no[j] = noise[oi]; go[j] = gn[oi]; to[j] = tn[oi];
+        no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f; to[j] = tn[oi];
       }
       if (hin) { nin = fnz(ni); gin = fnz(gi); tin = fnz(ti); }
 #pragma unroll
@@ -332,7 +333,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     // ---- update
     if constexpr (UPD) {
-      if (NZ && gnoise != nullptr) {                      // dL/dsigma from the mu-slot gradient
+      if constexpr (NZ && DG) {                           // dL/dsigma from the mu-slot gradient
 #pragma unroll
         for (int j = 0; j < 4; ++j) gs[j] = ok[j] ? g[j] * gin * gout[j] : 0.f;
       }
@@ -383,11 +384,11 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     // bf16 fragments of this tile into dst (+ dst2): dgrad straight from the registers (4
     // consecutive K' of one lane's slot), forward through an LDS transpose of the tile
-    auto emit = [&](const float* ev, act_t* dst, act_t* dst2) {
+    auto emit = [&](const float* ev, act_t* dst, act_t* dst2, bool dgrad) {
       bfx4 v;
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = (act_t)(ok[j] ? ev[j] : 0.f);
-      if (jb.dg_mode != 0 && rowok && n < jb.N) {
+      if (dgrad && jb.dg_mode != 0 && rowok && n < jb.N) {
         int kp, np;                                        // K' of the first of the 4 values, N'
         if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
         else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
@@ -414,8 +415,8 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
       __syncthreads();
     };
-    emit(e, packed, psync ? tgt_packed : nullptr);
-    if (tmix) emit(te, tpk, nullptr);
+    emit(e, packed, psync ? tgt_packed : nullptr, true);
+    if (tmix) emit(te, tpk, nullptr, false);              // (the target runs forward only)
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -424,10 +425,12 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     const bool nz = jb.sig_off >= 0;
     // float4 rows: 16-byte aligned tensor (and sigma) offsets and a row / chunk length % 4 == 0
     const bool al = ((jb.src_off | (nz ? jb.sig_off : 0)) & 3) == 0 && ((jb.kind == 1 ? jb.K : jb.N) & 3) == 0;
-    if (al) {
-      if (nz) item(jb, T_{}, T_{}); else item(jb, T_{}, F_{});
+    if (!nz) {
+      if (al) item(jb, T_{}, F_{}, F_{}); else item(jb, F_{}, F_{}, F_{});
+    } else if (gnoise != nullptr) {
+      if (al) item(jb, T_{}, T_{}, T_{}); else item(jb, F_{}, T_{}, T_{});
     } else {
-      if (nz) item(jb, F_{}, T_{}); else item(jb, F_{}, F_{});
+      if (al) item(jb, T_{}, T_{}, F_{}); else item(jb, F_{}, T_{}, F_{});
     }
   }
   if (!UPD) return;

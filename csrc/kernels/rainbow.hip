@@ -32,15 +32,21 @@ DQN_DEV bfx8 rz8() {
   return z;
 }
 
+// Row layout of the precomputed logits (one igemm over the combined output layer): KD floats
+// per row = [plain / advantage logits (NO) | pad | dueling value logits (atoms) at VO | pad],
+// VO = NO rounded up to 32 (the same columns as the dL/dlogits rows of dout16).
+DQN_DEV_HOST_INLINE int c51_vo(const HeadArgs& a) { return (a.A * a.atoms + 31) / 32 * 32; }
+DQN_DEV_HOST_INLINE int c51_kd(const HeadArgs& a) {
+  return c51_vo(a) + (a.dueling ? (a.atoms + 31) / 32 * 32 : 0);
+}
+
 // logits of one instance from the precomputed igemm outputs (global fp32) into LDS
 DQN_DEV void c51_load_logits(const HeadArgs& a, int inst, float* lg, float* vl, int tid, int nth, int B) {
-  const int NA = a.atoms, NO = a.A * NA;
+  const int NA = a.atoms, NO = a.A * NA, KD = c51_kd(a), VO = c51_vo(a);
   const float* src = a.lgi[inst];
-  for (int t = tid; t < B * NO; t += nth) lg[t] = src[t];
-  if (a.dueling) {
-    const float* sv = a.vli[inst];
-    for (int t = tid; t < B * NA; t += nth) vl[t] = sv[t];
-  }
+  for (int t = tid; t < B * NO; t += nth) lg[t] = src[(t / NO) * KD + t % NO];
+  if (a.dueling)
+    for (int t = tid; t < B * NA; t += nth) vl[t] = src[(t / NA) * KD + VO + t % NA];
 }
 
 DQN_DEV float c51_z(const HeadArgs& a, int n) {
@@ -157,9 +163,10 @@ DQN_DEV void c51_act_env_block(const HeadArgs& a, int e, SumtreeLds& st) {
   const int ln = on ? lane : 0;
   float xr[AM], v = 0.f;
   if (wave == 0) {                                   // the Q row's loads first ...
+    const float* row = a.act_lgi + (int64_t)e * c51_kd(a);
 #pragma unroll
-    for (int i = 0; i < AM; ++i) xr[i] = a.act_lgi[(int64_t)e * NO + min(i, A - 1) * NA + ln];
-    v = a.dueling ? a.act_vli[(int64_t)e * NA + ln] : 0.f;
+    for (int i = 0; i < AM; ++i) xr[i] = row[min(i, A - 1) * NA + ln];
+    v = a.dueling ? row[c51_vo(a) + ln] : 0.f;
   }
   actor_env_frames(x, e, pre);                       // ... the frames under their latency
   if (prof) prof[17] = (int64_t)__builtin_amdgcn_s_memtime();
@@ -200,7 +207,7 @@ __global__ void __launch_bounds__(kC51Threads) c51_train_kernel(HeadArgs a) {
     return;
   }
   const int B = a.B, A = a.A, NA = a.atoms, NO = A * NA;
-  const int VO = (NO + 31) / 32 * 32, KD = a.dueling ? VO + (NA + 31) / 32 * 32 : VO;
+  const int VO = c51_vo(a), KD = c51_kd(a);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool on = lane < NA;
   const int ln = on ? lane : 0;                 // clamped: loads of idle lanes stay in bounds
@@ -208,9 +215,7 @@ __global__ void __launch_bounds__(kC51Threads) c51_train_kernel(HeadArgs a) {
   const float* lsel = a.lgi[dbl ? 2 : 1];       // action choice on s'
   const float* ltgt = a.lgi[1];                 // target distribution (same buffer without Double DQN)
   const float* lon = a.lgi[0];
-  const float* vsel = a.dueling ? a.vli[dbl ? 2 : 1] : lsel;
-  const float* vtgt = a.dueling ? a.vli[1] : ltgt;
-  const float* von = a.dueling ? a.vli[0] : lon;
+
   const float dz = (a.vmax - a.vmin) / (float)(NA - 1);
   const float z = c51_z(a, ln);
   const float inva = a.dueling ? 1.f / (float)A : 0.f;
@@ -223,7 +228,7 @@ __global__ void __launch_bounds__(kC51Threads) c51_train_kernel(HeadArgs a) {
   float contrib = 0.f;
   for (int b = blockIdx.x * kC51Waves + wave; b < B; b += nlearn * kC51Waves) {
     float xs[AM], xt[AM], xo[AM];
-    const int64_t r0 = (int64_t)b * NO + ln;
+    const int64_t r0 = (int64_t)b * KD + ln;
 #pragma unroll
     for (int i = 0; i < AM; ++i) {
       const int ii = i < A ? i : 0;
@@ -231,8 +236,8 @@ __global__ void __launch_bounds__(kC51Threads) c51_train_kernel(HeadArgs a) {
       xt[i] = ltgt[r0 + ii * NA];
       xo[i] = lon[r0 + ii * NA];
     }
-    const int64_t v0 = a.dueling ? (int64_t)b * NA + ln : r0;
-    float vs = vsel[v0], vt = vtgt[v0], vo = von[v0];
+    const int64_t v0 = (int64_t)b * KD + (a.dueling ? VO : 0) + ln;   // (no dueling: an ignored in-row load)
+    float vs = lsel[v0], vt = ltgt[v0], vo = lon[v0];
     const int act = a.act[b];
     const float rw = a.rew[b], gm = a.gam[b] * (1.f - a.done[b]);
     const float w = a.wts != nullptr ? a.wts[b] : 1.f;

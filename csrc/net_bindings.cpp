@@ -234,13 +234,14 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
   launch_head_loss(a, cur_stream());
 }
 
-// C51 head: ints as head_loss; dist = [atoms]; flts = [v_min, v_max]
+// C51 head: ints as head_loss; dist = [atoms]; flts = [v_min, v_max]; lg = the instances' logits
+// rows (one igemm over the combined output layer: KD floats per row, rainbow.hip c51_kd)
 void c51_head(std::vector<int64_t> ints, std::vector<int64_t> dist, std::vector<double> flts, std::vector<int64_t> h,
               std::vector<int64_t> w, std::vector<int64_t> b, std::vector<int64_t> wv, std::vector<int64_t> bv,
               std::vector<int64_t> io, std::vector<int64_t> pw, std::vector<int64_t> pwv, std::vector<int64_t> zero,
               std::vector<int64_t> actor, std::vector<double> actor_f, int64_t prof, std::vector<int64_t> lg,
-              std::vector<int64_t> vl, int64_t act_h, std::vector<int64_t> qp) {
-  // training + actor: fused acting; lg / vl then carry one more entry, the actors' logits.
+              int64_t act_h, std::vector<int64_t> qp) {
+  // training + actor: fused acting; lg then carries one more entry, the actors' logits.
   // qp (training): [loss_parts (>= c51_train_blocks floats), dout16 act_t [B][KD]]
   TORCH_CHECK(dist.size() == 1 && flts.size() == 2, "c51 args");
   dqn::HeadArgs a = head_args(ints, h, w, b, wv, bv, io, pw, pwv, zero, actor, actor_f, act_h);
@@ -255,16 +256,12 @@ void c51_head(std::vector<int64_t> ints, std::vector<int64_t> dist, std::vector<
   }
   a.prof = P<int64_t*>(prof);
   if (a.act_E > 0) {
-    TORCH_CHECK(!lg.empty() && (!a.dueling || vl.size() == lg.size()), "c51 fused acting: the actors' logits");
+    TORCH_CHECK(!lg.empty(), "c51 fused acting: the actors' logits");
     a.act_lgi = P<const float*>(lg.back());
     lg.pop_back();
-    if (a.dueling) { a.act_vli = P<const float*>(vl.back()); vl.pop_back(); }
   }
-  TORCH_CHECK(lg.size() <= 3 && vl.size() <= 3, "c51: up to 3 precomputed logit buffers");
+  TORCH_CHECK(a.infer ? lg.size() == 1 : (lg.size() == 2 || lg.size() == 3), "c51: logits of every instance");
   for (size_t i = 0; i < lg.size(); ++i) a.lgi[i] = P<const float*>(lg[i]);
-  for (size_t i = 0; i < vl.size(); ++i) a.vli[i] = P<const float*>(vl[i]);
-  TORCH_CHECK(!a.dueling || vl.size() == lg.size(), "c51: dueling needs value logits too");
-  TORCH_CHECK(a.infer ? lg.size() >= 1 : (lg.size() == 2 || lg.size() == 3), "c51: logits of every instance");
   launch_c51_head(a, cur_stream());
 }
 
@@ -350,8 +347,7 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),
         pybind11::arg("io"), pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),
         pybind11::arg("actor_f"), pybind11::arg("prof") = 0, pybind11::arg("lg") = std::vector<int64_t>{},
-        pybind11::arg("vl") = std::vector<int64_t>{}, pybind11::arg("act_h") = 0,
-        pybind11::arg("qp") = std::vector<int64_t>{});
+        pybind11::arg("act_h") = 0, pybind11::arg("qp") = std::vector<int64_t>{});
   m.def("qnet_noisy_mix", &noisy_mix);
   m.def("qnet_noisy_grad", &noisy_grad);
   m.attr("NOISY_JOB_INTS") = (int)(sizeof(dqn::NoisyJob) / sizeof(int));

@@ -140,12 +140,23 @@ class HipExecutor:
                                     for n, o in fcs])
         add('fc/dgrad', self.HH, F, [dict(src_off=lay.offsets[n + '/w'], K=H, N=F, ks_off=o // 32, mode=2, p0=H)
                                       for n, o in fcs])
-        # head (output layer) fragments for the MFMA Q tiles of the head kernel
         hw = 'advantage/output/w' if self.dueling else 'output/w'
-        add('head/w', H, self.NO, [dict(src_off=lay.offsets[hw], K=H, N=self.NO, mode=0)])
-        if self.dueling:
-            add('head/v', H, self.atoms, [dict(src_off=lay.offsets['value/output/w'], K=H, N=self.atoms, mode=0)])
-        if self.dist:
+        hb = 'advantage/output/b' if self.dueling else 'output/b'
+        if not self.dist:
+            # scalar head: output-layer fragments for the head kernel's MFMA Q tiles
+            add('head/w', H, self.NO, [dict(src_off=lay.offsets[hw], K=H, N=self.NO, mode=0)])
+            if self.dueling:
+                add('head/v', H, self.atoms, [dict(src_off=lay.offsets['value/output/w'], K=H, N=self.atoms,
+                                                   mode=0)])
+        else:
+            # C51: the output layer as ONE combined GEMM over the whole hidden row [value | advantage]:
+            # Wc [HH][KD] = [[0, Wv at column VO], [W_adv, 0]] (block diagonal), so every instance's
+            # logits AND value logits come from one igemm launch (rows of KD = dout16's columns)
+            wc = [dict(src_off=lay.offsets[hw], K=H, N=self.NO, ks_off=(H // 32) if self.dueling else 0, mode=0)]
+            if self.dueling:
+                wc.append(dict(src_off=lay.offsets['value/output/w'], K=H, N=self.atoms, nt_off=self.c51_VO // 16,
+                               mode=0))
+            add('head/wc', self.HH, self.c51_KD, wc)
             # C51: dgrad fragments of the output layer(s) for the dH igemm, K' = [logits | value]:
             # dH = dout16 [B][KD] . (plain / advantage W^T into h's advantage half, Wv^T into the value half)
             dg = [dict(src_off=lay.offsets[hw], K=self.NO, N=H, nt_off=H // 16 if self.dueling else 0, mode=2,
@@ -160,6 +171,15 @@ class HipExecutor:
             jobs.append(_Job(src_off=lay.offsets[n + '/b'], K=H, dst_off=off + 2 * o, mode=3))
         off += 2 * self.HH
         off = (off + 255) // 256 * 256
+        if self.dist:
+            # C51: the combined output layer's bias row (fp32): logits bias | pad | value bias at VO
+            self.poff['head/bias'] = off
+            jobs.append(_Job(src_off=lay.offsets[hb], K=self.NO, dst_off=off, mode=3))
+            if self.dueling:
+                jobs.append(_Job(src_off=lay.offsets['value/output/b'], K=self.atoms, dst_off=off + 2 * self.c51_VO,
+                                 mode=3))
+            off += 2 * self.c51_KD
+            off = (off + 255) // 256 * 256
         self.packed_elems = off
         self.jobs = jobs
         self._jobs_dev: Dict[torch.device, torch.Tensor] = {}
@@ -586,31 +606,23 @@ class HipExecutor:
     def forward(self, flat, x, noise=None):
         return self.q_values(flat, x, noise)
 
-    def _c51_logits(self, hs, b, bv, pw, pwv):
-        """C51 logits of every instance as fp32 [B][A*atoms] (+ value [B][atoms]) on the
-        igemm kernel: spread over many CUs instead of re-streaming the 313 KB output
-        layer through one CU per head workgroup."""
-        B = self._c51_B
+    def _c51_logits(self, hs, pwc, pbias):
+        """C51 logits of every instance as fp32 rows [B][KD] (logits | pad | dueling value logits
+        at VO) from ONE igemm launch over the combined output layer (``head/wc``): spread over
+        many CUs instead of re-streaming the output layer through one CU per head workgroup."""
+        B, KD = self._c51_B, self.c51_KD
         n = len(hs)
-        ws = self._c51_ws(B, n)
+        ws = self._c51_ws(B)
         lg = [ws['lg'][i].data_ptr() for i in range(n)]
-        hsrc = [h + 2 * self.HID for h in hs] if self.dueling else list(hs)      # advantage half of [value | adv]
-        self.ext.qnet_igemm(_KIND['DF32'], hsrc, pw, b, lg, [], [1.0] * n,
-                            [B, self.NO, self.HID, (self.NO + 15) // 16, self.NO, 0, self.HH, 0, 0, 0, 0])
-        vl = []
-        if self.dueling:
-            vl = [ws['vl'][i].data_ptr() for i in range(n)]
-            self.ext.qnet_igemm(_KIND['DF32'], list(hs), pwv, bv, vl, [], [1.0] * n,
-                                [B, self.atoms, self.HID, (self.atoms + 15) // 16, self.atoms, 0, self.HH, 0, 0, 0, 0])
-        return lg, vl
+        self.ext.qnet_igemm(_KIND['DF32'], list(hs), pwc, pbias, lg, [], [1.0] * n,
+                            [B, KD, self.HH, KD // 16, KD, 0, self.HH, 0, 0, 0, 0])
+        return lg
 
-    def _c51_ws(self, B, n):
+    def _c51_ws(self, B):
         key = ('c51', B)
         ws = self._ws.get(key)
         if ws is None:
-            dev = self._c51_dev
-            ws = {'lg': torch.zeros(4, B * self.NO, dtype=torch.float32, device=dev),
-                  'vl': torch.zeros(4, B * self.atoms, dtype=torch.float32, device=dev)}
+            ws = {'lg': torch.zeros(4, B * self.c51_KD, dtype=torch.float32, device=self._c51_dev)}
             self._ws[key] = ws
         return ws
 
@@ -618,17 +630,17 @@ class HipExecutor:
         """Output layer + loss (+ backward) launch: scalar head or the C51 head."""
         if self.dist:
             self._c51_B = ints[0]
+            # (pw, pwv = the combined output layer's fragments and bias rows, see _head_packs)
             if act_h:
                 # fused acting: the actors' logits ride in the same igemm launch as one more
-                # instance (online weights), the acting step in one more C51-head workgroup
-                lg, vl = self._c51_logits(list(hs) + [act_h], list(b) + [b[0]], list(bv) + bv[:1],
-                                          list(pw) + [pw[0]], list(pwv) + pwv[:1])
+                # instance (online weights), the acting step in more C51-head workgroups
+                lg = self._c51_logits(list(hs) + [act_h], list(pw) + [pw[0]], list(pwv) + [pwv[0]])
             else:
-                lg, vl = self._c51_logits(hs, b, bv, pw, pwv)
+                lg = self._c51_logits(hs, pw, pwv)
             qp = [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()] if not ints[5] else []
             prof = self.head_prof.data_ptr() if self.head_prof is not None and not ints[5] else 0
             self.ext.qnet_c51_head(ints, [self.atoms], [float(self.arch.v_min), float(self.arch.v_max)], hs, w, b,
-                                   wv, bv, io, pw, pwv, zero, actor, actor_f, prof, lg, vl, act_h, qp)
+                                   wv, bv, io, [], [], zero, actor, actor_f, prof, lg, act_h, qp)
         else:
             prof = self.head_prof.data_ptr() if self.head_prof is not None else 0
             self.ext.qnet_head_loss(ints, [self.delta], hs, w, b, wv, bv, io, pw, pwv,
@@ -670,6 +682,11 @@ class HipExecutor:
                    pw, pwv, [], list(actor_ptrs) + list(actor_ints), list(actor_f), ws=ws)
 
     def _head_packs(self, packs):
+        """Scalar heads: the output layer's fragments (plain / advantage, dueling value); C51: the
+        combined output layer's fragments and its fp32 bias row."""
+        if self.dist:
+            return ([p.data_ptr() + 2 * self.poff['head/wc'] for p in packs],
+                    [p.data_ptr() + 2 * self.poff['head/bias'] for p in packs])
         pw = [p.data_ptr() + 2 * self.poff['head/w'] for p in packs]
         pwv = [p.data_ptr() + 2 * self.poff['head/v'] for p in packs] if self.dueling else []
         return pw, pwv
