@@ -55,3 +55,16 @@ int64_t dqn_ring_size(uint8_t* buf) {
   return (int64_t)(__atomic_load_n(u64(buf, kHead), __ATOMIC_ACQUIRE) -
                    __atomic_load_n(u64(buf, kTail), __ATOMIC_ACQUIRE));
 }
+
+const uint8_t* dqn_ring_peek(uint8_t* buf, uint64_t* tail, uint64_t* avail, uint64_t* cap, uint64_t* rec_bytes) {
+  *cap = *u64(buf, kCap);
+  *rec_bytes = *u64(buf, kRec);
+  *tail = __atomic_load_n(u64(buf, kTail), __ATOMIC_RELAXED);
+  *avail = __atomic_load_n(u64(buf, kHead), __ATOMIC_ACQUIRE) - *tail;
+  return buf + kData;
+}
+
+void dqn_ring_release(uint8_t* buf, uint64_t n) {
+  const uint64_t tail = __atomic_load_n(u64(buf, kTail), __ATOMIC_RELAXED);
+  __atomic_store_n(u64(buf, kTail), tail + n, __ATOMIC_RELEASE);
+}

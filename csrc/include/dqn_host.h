@@ -23,3 +23,21 @@ int64_t dqn_mbox_collect(uint8_t* region, int64_t n, int64_t state_bytes, uint8_
                          uint64_t* out_seq, int64_t max_batch);
 void dqn_mbox_respond(uint8_t* region, int64_t state_bytes, const int32_t* ids, const uint64_t* seq,
                       const int32_t* actions, int64_t m);
+
+// In-place consumption of a ring (apex_ingest.cpp): records [tail, tail + avail) are read where
+// they lie, then released with dqn_ring_release.
+const uint8_t* dqn_ring_peek(uint8_t* buf, uint64_t* tail, uint64_t* avail, uint64_t* cap, uint64_t* rec_bytes);
+void dqn_ring_release(uint8_t* buf, uint64_t n);
+
+// Ape-X ingest (apex_ingest.cpp): one actor's ring straight into the replay's pinned staging.
+struct DqnIngestStage {
+  uint8_t* frames; int64_t frames_cap; int64_t nf;      // frame staging [frames_cap][HW], fill count
+  int32_t* sidx; int32_t* nidx; int32_t* act; float* rew; float* done; float* gam;
+  int64_t trans_cap; int64_t nt;                         // transition staging columns, fill count
+  int64_t f_next; int64_t num_frames;                    // replay frame-slot cursor / ring size
+};
+struct DqnIngestOut {
+  int64_t consumed, frames, episodes, n_returns, stage_full;
+};
+void dqn_apex_ingest(uint8_t* ring, int64_t max_n, int32_t* actor_state, int k, int nstep, double gamma,
+                     int64_t frame_bytes, DqnIngestStage* st, float* returns, int64_t returns_cap, DqnIngestOut* out);

@@ -28,6 +28,7 @@ import logging
 import multiprocessing as mp
 import os
 import random
+import sys
 import time
 import uuid
 from collections import deque
@@ -210,6 +211,8 @@ class ApexActorPool:
         self.episodes = 0
         self.returns: deque = deque(maxlen=100)
         self.served = 0                      # greedy actions answered
+        # native drain's staging ship cadence (0: flush on every drain; ApexTrainer batches)
+        self.flush_min, self.flush_max_delay = 0, 0.0
         self._closed = False
 
     # -------------------------------------------------------------- life
@@ -248,6 +251,13 @@ class ApexActorPool:
         self.stop()
 
     # ----------------------------------------------------------- serving
+    def pin_states(self, torch):
+        """Collect mailbox states straight into page-locked memory (a GPU learner's H2D copy
+        source, no staging copy or per-batch pinning); returns that torch tensor [n, bytes]."""
+        t = torch.zeros((self.n, self.state_bytes), dtype=torch.uint8, pin_memory=True)
+        self._states = t.numpy()
+        return t
+
     def serve(self, q_fn: Callable[[np.ndarray], np.ndarray], max_batch: Optional[int] = None) -> int:
         """Answer every pending mailbox with ONE batched forward. q_fn maps a uint8/f32
         state batch [m, ...] to actions [m] (int). Returns m."""
@@ -267,7 +277,14 @@ class ApexActorPool:
 
     # ------------------------------------------------------------ ingest
     def drain(self, replay, max_per_actor: Optional[int] = None) -> int:
-        """Move every actor's pending transitions into the replay's staging (then flush)."""
+        """Move every actor's pending transitions into the replay's staging (then flush).
+        Image envs with a frame-stacked HBM replay: ONE native call per actor
+        (DeviceReplay.ingest_ring -> csrc/host/apex_ingest.cpp) reads the ring in place and
+        writes frames, slot stacks and n-step transitions straight into the pinned staging;
+        otherwise (vector observations) the per-record path below."""
+        if self.frame_hw is not None and hasattr(replay, 'ingest_ring') and replay.frame_mode \
+                and not replay.device_writer:
+            return self._drain_native(replay, max_per_actor)
         total = 0
         hsz = HEADER.itemsize
         cap = min(self.ring_capacity, max_per_actor or self.ring_capacity)
@@ -302,6 +319,29 @@ class ApexActorPool:
         return total
 
 
+    def _drain_native(self, replay, max_per_actor: Optional[int]) -> int:
+        """Staging is shipped (H2D copies + PER insert) once ``flush_min`` transitions are
+        staged or ``flush_max_delay`` seconds passed, not per drain: a flush orders the copy
+        stream after the queued learner steps, so flushing every loop iteration would hold the
+        host to the GPU and the learner to the drain cadence."""
+        if getattr(self, '_astate', None) is None:
+            words = replay.ingest_state_size(self.k, self.n_step)
+            self._astate = np.zeros((self.n, words), dtype=np.int32)
+            base = self.rings.ctypes.data
+            self._ring_addrs = np.array([base + i * self.ring_stride for i in range(self.n)], dtype=np.int64)
+            self._last_flush = time.time()
+        total, frames, eps, rets = replay.ingest_rings(self.lib, self._ring_addrs, self._astate, self.n_step,
+                                                       self.gamma, -1 if max_per_actor is None else int(max_per_actor))
+        self.frames += frames
+        self.episodes += eps
+        self.returns.extend(rets)
+        now = time.time()
+        if replay.staged() and (replay.staged() >= self.flush_min or now - self._last_flush >= self.flush_max_delay):
+            replay.flush()
+            self._last_flush = now
+        return total
+
+
 class ApexTrainer:
     """One learner rank of Ape-X: actor pool + inference thread + replay ingest + learner.
 
@@ -325,10 +365,28 @@ class ApexTrainer:
         if self.sync_freq > 0:
             self._snap = network.online.flat.clone()
             self._refresh_snapshot()
+        # inference I/O: states collected into pinned memory, one async H2D copy into a
+        # persistent device buffer, actions back through a pinned buffer (one event wait)
+        self._pin_in = self._dev_in = self._pin_out = None
+        if self.device.type == 'cuda':
+            self._pin_in = pool.pin_states(torch)
+            self._dev_in = torch.zeros(self._pin_in.shape, dtype=torch.uint8, device=self.device)
+            self._pin_out = torch.zeros(pool.n, dtype=torch.int32, pin_memory=True)
+            self._gout = torch.zeros(pool.n, dtype=torch.int32, device=self.device)
+            self._done = torch.cuda.Event()
+        self._graphs = {}                   # batch size -> captured inference graph
+        self._graphs_off = not bool(getattr(config, 'apex_infer_graphs', True))
         self._stop = threading.Event()
         self._lock = threading.Lock()       # one forward at a time vs the snapshot refresh
         self._thread = threading.Thread(target=self._serve_loop, name='apex-inference', daemon=True)
+        pool.flush_min, pool.flush_max_delay = 256, 0.005     # ship staging in batches (see _drain_native)
+        self.drain_every_s = 0.001          # ring drain cadence of the learner loop
+        self.max_inflight = 16              # queued learner steps before the loop waits on the GPU
+        self.gil_switch_s = 0.0005          # GIL hand-over interval while running
         self.serve_calls = 0
+        self.learn_t0 = None                # wall time / env frames when the learner took its first step
+        self.learn_frames0 = 0
+        self.loop_time = {'drain': 0.0, 'step': 0.0, 'iters': 0}   # main-loop wall split (bench)
 
     def _refresh_snapshot(self):
         with self.torch.no_grad():
@@ -336,17 +394,60 @@ class ApexTrainer:
             if hasattr(self.net.executor, 'repack'):
                 self.net.executor.repack(self._snap)
 
+    def _act_on(self, x):
+        """Greedy actions of a device state batch with the live (or snapshot) online weights."""
+        if self._snap is not None:
+            q = self.net.executor.q_values(self._snap, x.contiguous())
+        else:
+            q = self.net.q_values(x)
+        return q.argmax(1).to(self.torch.int32)
+
+    def _infer_graph(self, m: int, shape, f32: bool):
+        """HIP graph of the whole inference for batch size m (device state buffer -> actions
+        buffer): one replay call instead of the executor's per-launch Python work, which the
+        inference thread would otherwise spend holding the GIL the learner loop needs."""
+        torch = self.torch
+        g = self._graphs.get(m)
+        if g is not None or self._graphs_off:
+            return g
+        d = self._dev_in[:m]
+        x = d.view(torch.float32).view(shape) if f32 else d.view(shape)
+        try:
+            self._gout[:m].copy_(self._act_on(x))              # warm-up: workspaces, packed buffers
+            torch.cuda.current_stream().synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s), torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+                self._gout[:m].copy_(self._act_on(x))
+            torch.cuda.current_stream().wait_stream(s)
+            self._graphs[m] = g
+        except Exception as e:  # noqa: BLE001 - fall back to eager inference, once
+            log.warning('Ape-X inference graphs disabled (%s); serving eagerly', e)
+            self._graphs_off = True
+            g = None
+        return g
+
     def _q_actions(self, batch: np.ndarray) -> np.ndarray:
         torch = self.torch
-        x = torch.from_numpy(batch)
-        if self.device.type == 'cuda':
-            x = x.pin_memory().to(self.device, non_blocking=True)
+        m = batch.shape[0]
         with self._lock, torch.no_grad():
-            if self._snap is not None:
-                q = self.net.executor.q_values(self._snap, x.contiguous())
+            if self._pin_in is None:
+                return self._act_on(torch.from_numpy(batch)).numpy()
+            # batch is a view of the pinned collect buffer: one async H2D copy
+            self._dev_in[:m].copy_(self._pin_in[:m], non_blocking=True)
+            f32 = batch.dtype == np.float32
+            g = self._infer_graph(m, batch.shape, f32)
+            if g is not None:
+                g.replay()
             else:
-                q = self.net.q_values(x)
-            return q.argmax(1).to(torch.int32).cpu().numpy()
+                d = self._dev_in[:m]
+                self._gout[:m].copy_(self._act_on(d.view(torch.float32).view(batch.shape) if f32
+                                                  else d.view(batch.shape)))
+            self._pin_out[:m].copy_(self._gout[:m], non_blocking=True)
+            self._done.record()
+            self._done.synchronize()         # (the actors wait for these actions)
+            return self._pin_out[:m].numpy()
 
     def _serve_loop(self):
         from ..utils.trace import trace
@@ -376,12 +477,37 @@ class ApexTrainer:
             supervisor.request_stop(reason)
             return False
 
+        # The learner thread and the inference thread share the GIL: drain on a time cadence
+        # (the native ingest handles any backlog in one call) instead of per SGD step, bound the
+        # queued graph launches with events (waiting on one releases the GIL), and hand the GIL
+        # over at a finer interval so greedy requests are not parked behind learner launches.
+        torch = self.torch
+        cuda = self.device.type == 'cuda'
+        inflight = deque()
+        switch = sys.getswitchinterval()
+        sys.setswitchinterval(self.gil_switch_s)
+        last_drain = 0.0
         try:
             while True:
-                with trace('apex.drain'):
-                    self.pool.drain(self.replay)
+                ta = time.perf_counter()
+                if ta - last_drain >= self.drain_every_s or self.replay.size() < start:
+                    with trace('apex.drain'):
+                        self.pool.drain(self.replay)
+                    last_drain = ta
+                tb = time.perf_counter()
+                self.loop_time['drain'] += tb - ta
+                self.loop_time['iters'] += 1
                 if self.replay.size() >= start:
+                    if self.learn_t0 is None:
+                        self.learn_t0, self.learn_frames0 = time.time(), self.pool.frames
+                    if cuda and len(inflight) >= self.max_inflight:
+                        inflight.popleft().synchronize()
                     self.learner.step()
+                    if cuda:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                        inflight.append(ev)
+                    self.loop_time['step'] += time.perf_counter() - tb
                     if self._snap is not None and self.learner.train_steps % self.sync_freq == 0:
                         with self._lock:
                             self._refresh_snapshot()
@@ -413,10 +539,12 @@ class ApexTrainer:
                     break
                 if self.pool.alive() == 0 and self.pool.procs:
                     self.pool.drain(self.replay)
+                    self.replay.flush()
                     if self.replay.size() < start or want_stop('all actors exited'):
                         log.warning('all actors exited')
                         break
         finally:
+            sys.setswitchinterval(switch)
             self._stop.set()
             self._thread.join(5.0)
             self.pool.stop()

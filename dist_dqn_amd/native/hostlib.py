@@ -44,6 +44,9 @@ class HostLib:
             'dqnh_mbox_respond': (None, [vp, i64, vp, vp, vp, i64]),
             'dqnh_preprocess': (None, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int]),
             'dqnh_crc32c': (C.c_uint32, [vp, sz]),
+            'dqnh_apex_ingest': (None, [vp, i64, vp, C.c_int, C.c_int, C.c_double, i64, vp, vp, i64, vp]),
+            'dqnh_apex_ingest_many': (None, [i64, vp, vp, i64, i64, i64, C.c_int, C.c_int, C.c_double, i64, vp, vp,
+                                             i64, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -101,6 +104,26 @@ class HostLib:
             out = np.empty((H, W), dtype=np.uint8)
         self.L.dqnh_preprocess(_ptr(rgb), rgb.shape[0], rgb.shape[1], _ptr(out), H, W)
         return out
+
+    # ------------------------------------------------------------- Ape-X
+    def apex_ingest(self, ring, max_n: int, actor_state: np.ndarray, k: int, nstep: int, gamma: float,
+                    frame_bytes: int, stage: np.ndarray, returns: np.ndarray, out: np.ndarray):
+        """One actor ring -> replay staging (csrc/host/apex_ingest.cpp). stage: int64[13] in
+        DqnIngestStage order (updated in place); out: int64[5] = consumed, frames, episodes,
+        returns written, stage full."""
+        assert actor_state.dtype == np.int32 and stage.dtype == np.int64 and out.dtype == np.int64
+        assert returns.dtype == np.float32
+        self.L.dqnh_apex_ingest(_ptr(ring), max_n, _ptr(actor_state), k, nstep, gamma, frame_bytes, _ptr(stage),
+                                _ptr(returns), returns.size, _ptr(out))
+
+    def apex_ingest_many(self, rings: np.ndarray, states: np.ndarray, first: int, max_n: int, k: int, nstep: int,
+                         gamma: float, frame_bytes: int, stage: np.ndarray, returns: np.ndarray, out: np.ndarray):
+        """apex_ingest over every ring (int64 addresses) from actor ``first`` on, in one call;
+        out: int64[6] = consumed, frames, episodes, returns written, stage full, resume actor."""
+        assert rings.dtype == np.int64 and states.dtype == np.int32 and states.ndim == 2
+        assert states.shape[0] == rings.size and out.size >= 6
+        self.L.dqnh_apex_ingest_many(rings.size, _ptr(rings), _ptr(states), states.shape[1], first, max_n, k, nstep,
+                                     gamma, frame_bytes, _ptr(stage), _ptr(returns), returns.size, _ptr(out))
 
     def crc32c(self, data: bytes) -> int:
         b = np.frombuffer(data, dtype=np.uint8)

@@ -228,6 +228,74 @@ class DeviceReplay:
     def write_frame(self, frame) -> int:
         return self._alloc_frame(frame)
 
+    @staticmethod
+    def ingest_state_size(k: int, nstep: int) -> int:
+        """int32 words of one actor's native ingest state (stack + n-step window)."""
+        return k + 1 + nstep * (k + 2)
+
+    def ingest_rings(self, lib, rings: np.ndarray, states: np.ndarray, nstep: int, gamma: float, max_n: int = -1):
+        """``ingest_ring`` over many actors' rings (int64 addresses, one state row each) in one
+        native call per staging set. Returns (consumed, frames, episodes, returns)."""
+        assert self.frame_mode and not self.device_writer, 'native ingest: frame-stacked host-fed replay'
+        H, W = self.obs_shape
+        if getattr(self, '_ingm', None) is None:
+            self._ingm = (np.zeros(13, dtype=np.int64), np.zeros(6, dtype=np.int64), np.zeros(1024, dtype=np.float32))
+        arg, out, rbuf = self._ingm
+        consumed = frames = episodes = 0
+        rets: List[float] = []
+        first = 0
+        while True:
+            st = self._stage
+            arg[:] = [st.frames.ctypes.data, st.frames.shape[0], st.nf, st.sidx.ctypes.data, st.nidx.ctypes.data,
+                      st.act.ctypes.data, st.rew.ctypes.data, st.done.ctypes.data, st.gam.ctypes.data,
+                      st.act.shape[0], st.nt, self._f_next, self.num_frames]
+            lib.apex_ingest_many(rings, states, first, max_n, self.k, nstep, gamma, H * W, arg, rbuf, out)
+            st.nf, st.nt, self._f_next = int(arg[2]), int(arg[10]), int(arg[11])
+            consumed += int(out[0])
+            frames += int(out[1])
+            episodes += int(out[2])
+            rets.extend(rbuf[:int(out[3])].tolist())
+            if st.nt >= self._stage_size:
+                self.flush()
+            if not out[4]:
+                break
+            first = int(out[5])
+            self.flush()                    # staging full: ship it, resume with that actor
+        return consumed, frames, episodes, rets
+
+    def ingest_ring(self, lib, ring, actor_state: np.ndarray, nstep: int, gamma: float, max_n: int = -1):
+        """Ape-X: move one actor's pending ring records straight into the pinned staging with the
+        native ingest (csrc/host/apex_ingest.cpp: frames, slot stacks and the n-step fold, the
+        same transitions begin_episode / add_step(_nstep) would stage), flushing whenever the
+        staging fills. ``actor_state``: that actor's int32 ingest state (``ingest_state_size``).
+        Returns (records consumed, env frames, episodes ended, their returns (the first 256 per
+        native call))."""
+        assert self.frame_mode and not self.device_writer, 'native ingest: frame-stacked host-fed replay'
+        H, W = self.obs_shape
+        if getattr(self, '_ing', None) is None:
+            self._ing = (np.zeros(13, dtype=np.int64), np.zeros(5, dtype=np.int64), np.zeros(256, dtype=np.float32))
+        arg, out, rbuf = self._ing
+        consumed = frames = episodes = 0
+        rets: List[float] = []
+        while max_n < 0 or consumed < max_n:
+            st = self._stage
+            arg[:] = [st.frames.ctypes.data, st.frames.shape[0], st.nf, st.sidx.ctypes.data, st.nidx.ctypes.data,
+                      st.act.ctypes.data, st.rew.ctypes.data, st.done.ctypes.data, st.gam.ctypes.data,
+                      st.act.shape[0], st.nt, self._f_next, self.num_frames]
+            lib.apex_ingest(ring, -1 if max_n < 0 else max_n - consumed, actor_state, self.k, nstep, gamma, H * W,
+                            arg, rbuf, out)
+            st.nf, st.nt, self._f_next = int(arg[2]), int(arg[10]), int(arg[11])
+            consumed += int(out[0])
+            frames += int(out[1])
+            episodes += int(out[2])
+            rets.extend(rbuf[:int(out[3])].tolist())
+            if st.nt >= self._stage_size:
+                self.flush()
+            if not out[4]:
+                break
+            self.flush()                    # staging full: ship it and continue with the next set
+        return consumed, frames, episodes, rets
+
     def flush(self):
         """Copy staged frames/transitions into the device ring (contiguous, wrap-split)
         as async H2D copies on the side stream, then switch staging sets."""

@@ -44,13 +44,19 @@ def main():
     tr = ApexTrainer(net, rep, ln, pool, cfg)
     t0 = time.time()
     tr.run(max_seconds=args.seconds, log_every=10.0)
-    wall = time.time() - t0
+    t1 = time.time()
+    wall = t1 - t0
+    lw = t1 - tr.learn_t0 if tr.learn_t0 is not None else 0.0      # steady state: learner running
     print(json.dumps({
         'metric': 'Ape-X env frames/sec + learner SGD steps/sec (1 rank)', 'actors': cfg.num_actors,
         'seconds': round(wall, 1), 'env_frames': pool.frames, 'env_frames_per_sec': round(pool.frames / wall, 1),
         'sgd_steps': ln.train_steps, 'sgd_steps_per_sec': round(ln.train_steps / wall, 1),
+        'learning_seconds': round(lw, 1),
+        'learner_sgd_steps_per_sec': round(ln.train_steps / lw, 1) if lw > 0 else None,
+        'learner_env_frames_per_sec': round((pool.frames - tr.learn_frames0) / lw, 1) if lw > 0 else None,
         'greedy_actions_served': pool.served, 'serve_calls': tr.serve_calls,
         'mean_serve_batch': round(pool.served / max(1, tr.serve_calls), 2), 'executor': net.executor.name,
+        'main_loop_s': {k: round(v, 2) for k, v in tr.loop_time.items()},
         'config': 'apex preset: double+dueling, PER, n_step=3, nature-cnn', 'dtype': net.executor.compute_dtype,
         'device': str(dev)}))
 

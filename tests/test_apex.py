@@ -103,6 +103,70 @@ def test_pool_serves_and_drains_image_actors():
     assert sum(follow) >= 240 - 2 * 4        # all but the last step of each (cut) episode
 
 
+@pytest.mark.parametrize('nstep,many', [(1, False), (3, False), (3, True)])
+def test_native_ingest_matches_python_path(nstep, many):
+    """csrc/host/apex_ingest.cpp (one call per actor ring, staging flushes included) stages
+    exactly the transitions of DeviceReplay.begin_episode / add_step(_nstep) per record."""
+    from dist_dqn_amd.replay import DeviceReplay
+    from dist_dqn_amd.replay.nstep import NStepAccumulator
+    L = load()
+    H = W = 84
+    k, gamma = 4, 0.9
+    rb = HEADER.itemsize + H * W
+    cap = 512
+    ring = np.zeros(L.ring_bytes(cap, rb), dtype=np.uint8)
+    L.ring_init(ring, cap, rb)
+    rng = np.random.default_rng(0)
+    recs = np.zeros((300, rb), dtype=np.uint8)
+    hdr = recs[:, :HEADER.itemsize].view(HEADER).reshape(-1)
+    recs[:, HEADER.itemsize:] = rng.integers(0, 256, (300, H * W), dtype=np.uint8)
+    ep_left = 0
+    for i in range(300):
+        if ep_left == 0:
+            hdr[i] = (0, 0, 0, 0, 0.0, 0.0)                 # reset record
+            ep_left = int(rng.integers(3, 15))
+            continue
+        ep_left -= 1
+        done = int(ep_left == 0 and rng.random() < 0.7)
+        ep_left = 0 if done else ep_left
+        hdr[i] = (1, done, 0, int(rng.integers(0, 6)), float(rng.normal()), 5.0 if done else np.nan)
+    # the Python path
+    ref = DeviceReplay(2000, (H, W), k, device='cpu', stage_size=64)
+    acc = NStepAccumulator(nstep, gamma)
+    for i in range(300):
+        h, obs = hdr[i], recs[i, HEADER.itemsize:].reshape(H, W)
+        if h['kind'] == 0:
+            ref.begin_episode(obs.copy())
+            acc.reset()
+        elif nstep > 1:
+            ref.add_step_nstep(acc, int(h['action']), float(h['reward']), obs.copy(), bool(h['done']))
+        else:
+            ref.add_step(int(h['action']), float(h['reward']), obs.copy(), bool(h['done']), gamma_n=gamma)
+    ref.flush()
+    # the native path, in two ring fills (state carried across calls), small staging sets
+    nat = DeviceReplay(2000, (H, W), k, device='cpu', stage_size=64)
+    state = np.zeros(nat.ingest_state_size(k, nstep), dtype=np.int32)
+    got = [0, 0, 0]
+    for lo, hi in ((0, 170), (170, 300)):
+        assert L.ring_push(ring, recs[lo:hi], hi - lo) == hi - lo
+        if many:                                            # the all-actors call (one ring here)
+            m, frames, eps, rets = nat.ingest_rings(L, np.array([ring.ctypes.data], dtype=np.int64), state[None],
+                                                    nstep, gamma)
+        else:
+            m, frames, eps, rets = nat.ingest_ring(L, ring, state, nstep, gamma)
+        got = [got[0] + m, got[1] + frames, got[2] + eps]
+        assert all(r == 5.0 for r in rets)
+    nat.flush()
+    assert got[0] == 300 and got[1] == int((hdr['kind'] == 1).sum()) and got[2] == int(hdr['done'].sum())
+    assert nat.size() == ref.size() > 0
+    n = ref.size()
+    for name in ('state_idx', 'next_idx', 'actions', 'rewards', 'dones', 'gammas'):
+        np.testing.assert_array_equal(getattr(nat, name).numpy()[:n], getattr(ref, name).numpy()[:n], err_msg=name)
+    nf = ref._f_next
+    assert nat._f_next == nf
+    np.testing.assert_array_equal(nat.frames.numpy()[:nf], ref.frames.numpy()[:nf])
+
+
 def test_apex_cartpole_end_to_end(tmp_path):
     from dist_dqn_amd.cli import run_worker
     cfg = parse_args(['--env=CartPole-v0', '--network=simple', '--optimizer=adam', '--lr=0.001',
