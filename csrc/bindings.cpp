@@ -162,7 +162,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   // op -1: no optimizer update, only the (noisy) mix + pack of w (noise / eff given)
   CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
   CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
-  CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
+  CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, DQN_ACT_F32 ? torch::kFloat32 : DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
   TORCH_CHECK(grad.numel() == w.numel() && hp.size() == 9, "optim_pack args");
   TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
   TORCH_CHECK(max_grid <= 256 || ticket.numel() >= 17 * 32, "optim_pack: wide grid needs the 17x32-word ticket");
@@ -252,7 +252,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 teff.has_value() && teff->defined() && tpk.has_value() && tpk->defined(),
                 "optim_pack: target mix needs target, noise, teff, tpk");
     CHECK_T((*teff), torch::kFloat32);
-    CHECK_T((*tpk), DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
+    CHECK_T((*tpk), DQN_ACT_F32 ? torch::kFloat32 : DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
     TORCH_CHECK(teff->numel() == w.numel() && tpk->numel() == packed.numel() && tpk->data_ptr() != packed.data_ptr(),
                 "optim_pack: teff / tpk sizes");
     tnz = ptr<float>(*tnoise);

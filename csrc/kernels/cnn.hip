@@ -28,10 +28,11 @@ constexpr int O2 = 6, R2 = O2 * O2, N2 = 64, K2 = 512, L2 = N2 + 8;
 constexpr int Q2 = 3, P2W = Q2 + 2, LP2 = N2 + 8;                  // conv3 SAME pad 1
 constexpr int O3 = 3, R3 = O3 * O3, N3 = 64, K3 = 576, L3 = N3 + 8;
 constexpr int Q3 = 2;                                               // pool3 (SAME, pad bottom/right 1)
-// LDS carve-up of the (dead after conv1) padded-input region, in bf16 elements
+// LDS carve-up of the (dead after conv1) padded-input region, in act_t elements
 constexpr int OFF_P1 = 0, OFF_A2 = OFF_P1 + P1W * P1W * LP1, OFF_P2 = OFF_A2 + R2 * L2,
               OFF_A3 = OFF_P2 + P2W * P2W * LP2, OFF_RED = OFF_A3 + R3 * L3;
-static_assert((OFF_RED * 2) % 16 == 0 && OFF_RED + 2048 <= XW * XW * 4, "fwd LDS carve-up");
+static_assert((OFF_RED * sizeof(act_t)) % 16 == 0 &&
+              OFF_RED * sizeof(act_t) + 4096 <= XW * XW * 4 * sizeof(in_t), "fwd LDS carve-up");
 }  // namespace cnn
 
 DQN_DEV bfx8 max8(bfx8 a, const bfx8& b) {
@@ -42,13 +43,14 @@ DQN_DEV bfx8 max8(bfx8 a, const bfx8& b) {
 
 __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   using namespace cnn;
-  __shared__ __attribute__((aligned(16))) act_t xin[XW * XW * 4];
+  __shared__ __attribute__((aligned(16))) in_t xin[XW * XW * 4];
   __shared__ __attribute__((aligned(16))) act_t a1[R1 * L1];
-  act_t* p1p = xin + OFF_P1;
-  act_t* a2 = xin + OFF_A2;
-  act_t* p2p = xin + OFF_P2;
-  act_t* a3 = xin + OFF_A3;
-  float* red = reinterpret_cast<float*>(xin + OFF_RED);
+  act_t* const xa = reinterpret_cast<act_t*>(xin);
+  act_t* p1p = xa + OFF_P1;
+  act_t* a2 = xa + OFF_A2;
+  act_t* p2p = xa + OFF_P2;
+  act_t* a3 = xa + OFF_A3;
+  float* red = reinterpret_cast<float*>(xa + OFF_RED);
   const int b = blockIdx.x, inst = blockIdx.y;
   if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -105,7 +107,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     const int t = tid + 512 * j;
     if (t >= NT) continue;
     const int y = (4 * t) / IH, x = 4 * t - y * IH;          // 4 consecutive pixels of one row
-    act_t* dst = xin + ((y + XP) * XW + x + XP) * 4;
+    in_t* dst = xin + ((y + XP) * XW + x + XP) * 4;
     if (slot_path) {
       planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], dst);
     } else {
@@ -128,10 +130,10 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
       const int p = mt * 16 + l16;
       const bool ok = p < R1;
       const int oy = ok ? p / O1 : 0, ox = ok ? p - oy * O1 : 0;
-      const act_t* base = xin + ((oy * 4) * XW + ox * 4 + kw) * 4;
+      const in_t* base = xin + ((oy * 4) * XW + ox * 4 + kw) * 4;
       bfx8 fa[K1 / 32];
 #pragma unroll
-      for (int ks = 0; ks < K1 / 32; ++ks) fa[ks] = ok ? *reinterpret_cast<const bfx8*>(base + ks * XW * 4) : tz8();
+      for (int ks = 0; ks < K1 / 32; ++ks) fa[ks] = ok ? ld_in8(base + ks * XW * 4) : tz8();
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
       for (int ks = 0; ks < K1 / 32; ++ks) {
@@ -139,12 +141,12 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
         c1 = tmfma(w1r[1][ks], fa[ks], c1);
       }
       if (ok) {
-        const uint2 v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
-        *reinterpret_cast<uint2*>(a1 + p * L1 + cq) = v0;
-        *reinterpret_cast<uint2*>(a1 + p * L1 + 16 + cq) = v1;
+        const pk4_t v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
+        *reinterpret_cast<pk4_t*>(a1 + p * L1 + cq) = v0;
+        *reinterpret_cast<pk4_t*>(a1 + p * L1 + 16 + cq) = v1;
         if (ga1 != nullptr) {
-          *reinterpret_cast<uint2*>(ga1 + p * N1 + cq) = v0;
-          *reinterpret_cast<uint2*>(ga1 + p * N1 + 16 + cq) = v1;
+          *reinterpret_cast<pk4_t*>(ga1 + p * N1 + cq) = v0;
+          *reinterpret_cast<pk4_t*>(ga1 + p * N1 + 16 + cq) = v1;
         }
       }
     }
@@ -195,9 +197,9 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
 #pragma unroll
       for (int ks = 0; ks < K2 / 32; ++ks) c = tmfma(w2r[ks], fa[ks], c);
       if (ok) {
-        const uint2 v = pack4(c + f4(bias2));
-        *reinterpret_cast<uint2*>(a2 + p * L2 + nq * 16 + cq) = v;
-        if (ga2 != nullptr) *reinterpret_cast<uint2*>(ga2 + p * N2 + nq * 16 + cq) = v;
+        const pk4_t v = pack4(c + f4(bias2));
+        *reinterpret_cast<pk4_t*>(a2 + p * L2 + nq * 16 + cq) = v;
+        if (ga2 != nullptr) *reinterpret_cast<pk4_t*>(ga2 + p * N2 + nq * 16 + cq) = v;
       }
     }
   }
@@ -248,9 +250,9 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     if (hi == 0) {
       c = unpark(red, nq, lane, c);
       if (ok) {
-        const uint2 v = pack4(c + f4(bias3));
-        *reinterpret_cast<uint2*>(a3 + p * L3 + nq * 16 + cq) = v;
-        if (keep) *reinterpret_cast<uint2*>(a.a3 + (int64_t)b * R3 * N3 + p * N3 + nq * 16 + cq) = v;
+        const pk4_t v = pack4(c + f4(bias3));
+        *reinterpret_cast<pk4_t*>(a3 + p * L3 + nq * 16 + cq) = v;
+        if (keep) *reinterpret_cast<pk4_t*>(a.a3 + (int64_t)b * R3 * N3 + p * N3 + nq * 16 + cq) = v;
       }
     }
   }

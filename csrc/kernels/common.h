@@ -128,6 +128,17 @@ DQN_DEV float bf2f(uint16_t h) {
 
 using bf16x8 = __attribute__((ext_vector_type(8))) short;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+#if DQN_ACT_F32
+// fp32 build: one 32-deep k-step of the 16-bit builds' fragment layout as 8 16x16x4 fp32
+// MFMAs (lane group g supplies k = 8g + j to the j-th; see dqn_act.h)
+typedef __attribute__((ext_vector_type(8))) float f32x8_frag;
+DQN_DEV f32x4 mfma_f32_k32(const f32x8_frag& a, const f32x8_frag& b, f32x4 c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], c, 0, 0, 0);
+  return c;
+}
+#endif
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 }  // namespace dqn

@@ -18,12 +18,34 @@ DQN_DEV bfx8 tz8() {
 
 DQN_DEV f32x4 f4(const float4& v) { return f32x4{v.x, v.y, v.z, v.w}; }
 
-// ReLU + 4 floats -> 4 packed bf16 (8 bytes)
-DQN_DEV uint2 pack4(const f32x4& v) {
+// ReLU + 4 floats -> 4 packed act_t (8 bytes; 16 in the fp32 build): pk4_t
+#if DQN_ACT_F32
+typedef float4 pk4_t;
+DQN_DEV pk4_t pack4(const f32x4& v) {
+  return make_float4(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+}
+#else
+typedef uint2 pk4_t;
+DQN_DEV pk4_t pack4(const f32x4& v) {
   const act_t a = (act_t)fmaxf(v[0], 0.f), b = (act_t)fmaxf(v[1], 0.f);
   const act_t c = (act_t)fmaxf(v[2], 0.f), d = (act_t)fmaxf(v[3], 0.f);
   return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16),
                     (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16));
+}
+#endif
+
+// 8 consecutive input-image elements (in_t, LDS) as an MFMA fragment
+DQN_DEV bfx8 ld_in8(const in_t* p) {
+#if DQN_ACT_F32
+  typedef __attribute__((ext_vector_type(8))) in_t in8;
+  const in8 v = *reinterpret_cast<const in8*>(p);
+  bfx8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (float)v[j];
+  return r;
+#else
+  return *reinterpret_cast<const bfx8*>(p);
+#endif
 }
 
 DQN_DEV f32x4 tmfma(const bfx8& a, const bfx8& b, const f32x4& c) {
@@ -32,12 +54,12 @@ DQN_DEV f32x4 tmfma(const bfx8& a, const bfx8& b, const f32x4& c) {
 
 // 4 pixels x 4 channels (one uint32 per channel plane, or one uint4 NHWC word
 // group) -> 4 NHWC bf16 pixels (32 B) in LDS.
-DQN_DEV uint32_t bfpair(uint32_t a, uint32_t b) {   // two integers 0..255 -> packed bf16 (exact)
-  const act_t x = (act_t)(float)a, y = (act_t)(float)b;
+DQN_DEV uint32_t bfpair(uint32_t a, uint32_t b) {   // two integers 0..255 -> packed in_t (exact)
+  const in_t x = (in_t)(float)a, y = (in_t)(float)b;
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
-DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, act_t* dst) {
+DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, in_t* dst) {
   uint32_t o[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -750,10 +750,12 @@ void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs
                      reinterpret_cast<act_t*>(dst2), step, freq < 1 ? 1 : freq);
 }
 
+// fp32 build: fragments take twice the VGPRs, so each load batch holds half the k-steps
+constexpr int kLoadBatch(int u) { return DQN_ACT_F32 ? (u + 1) / 2 : u; }
 #define IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, U)                                                \
   do {                                                                                                  \
     dim3 grid((a.M + WM * MT * 16 - 1) / (WM * MT * 16), (a.N + WN * NT * 16 - 1) / (WN * NT * 16), ninst); \
-    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI, U>), grid, dim3(64 * WM * WN * KS), 0, st, a); \
+    hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI, kLoadBatch(U)>), grid, dim3(64 * WM * WN * KS), 0, st, a); \
   } while (0)
 #define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI) IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, 4)
 

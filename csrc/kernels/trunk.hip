@@ -35,12 +35,13 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   using namespace trunk;
   // xin: the sample as bf16 NHWC [84*84][4] (converted once); dead after conv1, so
   // act2 and the conv2/conv3 K-split partials live in the same bytes afterwards.
-  __shared__ __attribute__((aligned(16))) act_t xin[HW * 4];
+  __shared__ __attribute__((aligned(16))) in_t xin[HW * 4];
   __shared__ __attribute__((aligned(16))) act_t act1[R1 * L1];
-  act_t* act2 = xin;
-  float* red = reinterpret_cast<float*>(xin + 6144);   // conv3 k-half partials, after act2 (R2 * L2 = 5832)
-  static_assert(R2 * L2 <= 6144 && 6144 * 2 + 4 * 4 * 1024 <= HW * 8, "act2 + partials fit xin");
-  static_assert(sizeof(SampleLds) <= HW * 8, "sampler scratch fits xin");
+  act_t* act2 = reinterpret_cast<act_t*>(xin);
+  constexpr size_t kRedOff = (R2 * L2 * sizeof(act_t) + 255) / 256 * 256;   // conv3 k-half partials after act2
+  float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(xin) + kRedOff);
+  static_assert(kRedOff + 4 * 4 * 1024 <= sizeof(xin), "act2 + partials fit xin");
+  static_assert(sizeof(SampleLds) <= sizeof(xin), "sampler scratch fits xin");
   const int b = blockIdx.x, inst = blockIdx.y;
   if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -160,9 +161,9 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     act_t* x1 = a.x1[inst] != nullptr ? a.x1[inst] + (int64_t)b * R1 * N1 : nullptr;
     auto load1 = [&](bfx8* f, int mt) {
       const int p = mt * 16 + row, oy = p / O1, ox = p - oy * O1;
-      const act_t* base = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
+      const in_t* base = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
 #pragma unroll
-      for (int ks = 0; ks < K1 / 32; ++ks) f[ks] = *reinterpret_cast<const bfx8*>(base + ks * IW * 4);
+      for (int ks = 0; ks < K1 / 32; ++ks) f[ks] = ld_in8(base + ks * IW * 4);
     };
     constexpr int MT = R1 / 16, ITER = (MT + 7) / 8;      // 25 m-tiles (no tail) over 8 waves
 #pragma unroll
@@ -178,12 +179,12 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
         c1 = tmfma(w1r[1][ks], fa[ks], c1);
       }
       const int p = mt * 16 + row;
-      const uint2 v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
-      *reinterpret_cast<uint2*>(act1 + p * L1 + cq) = v0;
-      *reinterpret_cast<uint2*>(act1 + p * L1 + 16 + cq) = v1;
+      const pk4_t v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
+      *reinterpret_cast<pk4_t*>(act1 + p * L1 + cq) = v0;
+      *reinterpret_cast<pk4_t*>(act1 + p * L1 + 16 + cq) = v1;
       if (x1 != nullptr) {   // conv2 wgrad input + ReLU mask of the backward
-        *reinterpret_cast<uint2*>(x1 + p * N1 + cq) = v0;
-        *reinterpret_cast<uint2*>(x1 + p * N1 + 16 + cq) = v1;
+        *reinterpret_cast<pk4_t*>(x1 + p * N1 + cq) = v0;
+        *reinterpret_cast<pk4_t*>(x1 + p * N1 + 16 + cq) = v1;
       }
     }
   }
@@ -218,9 +219,9 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int ks = 0; ks < KS; ++ks) c = tmfma(w2r[ks], fa[ks], c);
       const int p = mt * 16 + row;
       if (p < R2) {
-        const uint2 v = pack4(c + f4(bias2));
-        *reinterpret_cast<uint2*>(act2 + p * L2 + nq * 16 + cq) = v;
-        if (x2 != nullptr) *reinterpret_cast<uint2*>(x2 + p * N2 + nq * 16 + cq) = v;
+        const pk4_t v = pack4(c + f4(bias2));
+        *reinterpret_cast<pk4_t*>(act2 + p * L2 + nq * 16 + cq) = v;
+        if (x2 != nullptr) *reinterpret_cast<pk4_t*>(x2 + p * N2 + nq * 16 + cq) = v;
       }
     }
   }
@@ -267,7 +268,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int mt = 0; mt < MT; ++mt) {
         const f32x4 v = unpark(red, nq * MT + mt, lane, acc[mt]);
         const int p = mt * 16 + row;
-        if (p < R3) *reinterpret_cast<uint2*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
+        if (p < R3) *reinterpret_cast<pk4_t*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
       }
     }
   }

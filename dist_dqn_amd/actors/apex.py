@@ -362,6 +362,7 @@ class ApexTrainer:
         self.device = network.device
         self.sync_freq = int(config.actor_param_sync_freq)
         self._snap = None
+        self._synced = 0                    # snapshot refreshes done (every sync_freq learner steps)
         if self.sync_freq > 0:
             self._snap = network.online.flat.clone()
             self._refresh_snapshot()
@@ -373,6 +374,8 @@ class ApexTrainer:
             self._dev_in = torch.zeros(self._pin_in.shape, dtype=torch.uint8, device=self.device)
             self._pin_out = torch.zeros(pool.n, dtype=torch.int32, pin_memory=True)
             self._gout = torch.zeros(pool.n, dtype=torch.int32, device=self.device)
+            lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, 'priority_range') else (0, -1)
+            self._istream = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
             self._done = torch.cuda.Event()
         self._graphs = {}                   # batch size -> captured inference graph
         self._graphs_off = not bool(getattr(config, 'apex_infer_graphs', True))
@@ -381,8 +384,10 @@ class ApexTrainer:
         self._thread = threading.Thread(target=self._serve_loop, name='apex-inference', daemon=True)
         pool.flush_min, pool.flush_max_delay = 256, 0.005     # ship staging in batches (see _drain_native)
         self.drain_every_s = 0.001          # ring drain cadence of the learner loop
-        self.max_inflight = 16              # queued learner steps before the loop waits on the GPU
+        self.graph_steps = max(1, int(getattr(config, 'apex_graph_steps', 4)))   # SGD steps per host call
+        self.max_inflight = max(2, 16 // self.graph_steps)   # queued launches before the loop waits
         self.gil_switch_s = 0.0005          # GIL hand-over interval while running
+        self.serve_gap_s = float(getattr(config, 'apex_serve_gap_us', 100)) * 1e-6
         self.serve_calls = 0
         self.learn_t0 = None                # wall time / env frames when the learner took its first step
         self.learn_frames0 = 0
@@ -413,14 +418,15 @@ class ApexTrainer:
         d = self._dev_in[:m]
         x = d.view(torch.float32).view(shape) if f32 else d.view(shape)
         try:
-            self._gout[:m].copy_(self._act_on(x))              # warm-up: workspaces, packed buffers
-            torch.cuda.current_stream().synchronize()
+            with torch.cuda.stream(self._istream):
+                self._gout[:m].copy_(self._act_on(x))          # warm-up: workspaces, packed buffers
+            self._istream.synchronize()
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream())
+            s.wait_stream(self._istream)
             with torch.cuda.stream(s), torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
                 self._gout[:m].copy_(self._act_on(x))
-            torch.cuda.current_stream().wait_stream(s)
+            self._istream.wait_stream(s)
             self._graphs[m] = g
         except Exception as e:  # noqa: BLE001 - fall back to eager inference, once
             log.warning('Ape-X inference graphs disabled (%s); serving eagerly', e)
@@ -434,18 +440,22 @@ class ApexTrainer:
         with self._lock, torch.no_grad():
             if self._pin_in is None:
                 return self._act_on(torch.from_numpy(batch)).numpy()
-            # batch is a view of the pinned collect buffer: one async H2D copy
-            self._dev_in[:m].copy_(self._pin_in[:m], non_blocking=True)
             f32 = batch.dtype == np.float32
             g = self._infer_graph(m, batch.shape, f32)
-            if g is not None:
-                g.replay()
-            else:
-                d = self._dev_in[:m]
-                self._gout[:m].copy_(self._act_on(d.view(torch.float32).view(batch.shape) if f32
-                                                  else d.view(batch.shape)))
-            self._pin_out[:m].copy_(self._gout[:m], non_blocking=True)
-            self._done.record()
+            # own high-priority stream: acting overlaps the queued learner steps instead of
+            # waiting behind them (it reads the online weights while an update may be writing
+            # them: a mix of two consecutive steps' weights, as stale as Ape-X acting allows)
+            with torch.cuda.stream(self._istream):
+                # batch is a view of the pinned collect buffer: one async H2D copy
+                self._dev_in[:m].copy_(self._pin_in[:m], non_blocking=True)
+                if g is not None:
+                    g.replay()
+                else:
+                    d = self._dev_in[:m]
+                    self._gout[:m].copy_(self._act_on(d.view(torch.float32).view(batch.shape) if f32
+                                                      else d.view(batch.shape)))
+                self._pin_out[:m].copy_(self._gout[:m], non_blocking=True)
+                self._done.record()
             self._done.synchronize()         # (the actors wait for these actions)
             return self._pin_out[:m].numpy()
 
@@ -454,10 +464,11 @@ class ApexTrainer:
         while not self._stop.is_set():
             with trace('apex.serve'):
                 m = self.pool.serve(self._q_actions)
-            if m == 0:
-                time.sleep(0.0002)
-            else:
+            if m:
                 self.serve_calls += 1
+            # (a non-empty serve is followed by a short gap as well: requests accumulate into
+            # larger batches and the learner loop gets the GIL between serves)
+            time.sleep(self.serve_gap_s if m else 0.0002)
 
     def run(self, max_train_steps: int = 0, max_seconds: float = 0.0, supervisor=None, log_every: float = 10.0):
         from ..utils.trace import trace
@@ -502,13 +513,14 @@ class ApexTrainer:
                         self.learn_t0, self.learn_frames0 = time.time(), self.pool.frames
                     if cuda and len(inflight) >= self.max_inflight:
                         inflight.popleft().synchronize()
-                    self.learner.step()
+                    self.learner.step_many(self.graph_steps)
                     if cuda:
                         ev = torch.cuda.Event()
                         ev.record()
                         inflight.append(ev)
                     self.loop_time['step'] += time.perf_counter() - tb
-                    if self._snap is not None and self.learner.train_steps % self.sync_freq == 0:
+                    if self._snap is not None and self.learner.train_steps // self.sync_freq != self._synced:
+                        self._synced = self.learner.train_steps // self.sync_freq
                         with self._lock:
                             self._refresh_snapshot()
                     if supervisor is not None:

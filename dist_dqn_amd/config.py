@@ -33,11 +33,13 @@ ATARI = (
     "--frames_per_state=4 --update_freq=4 --replay_start_size=10000 "
     "--resize_width=84 --resize_height=84"
 )
-# North-star presets (BASELINE.json "configs").
-NATURE = ATARI.replace("--network=cnn", "--network=nature") + " --input_scale=0.00392156862745098"
+# North-star presets (BASELINE.json "configs": Nature-CNN in bf16, Rainbow on the fp16 MFMA
+# path). The reference presets above keep the reference's fp32 (--dtype default).
+NATURE = ATARI.replace("--network=cnn", "--network=nature") + " --input_scale=0.00392156862745098 --dtype=bf16"
 DOUBLE_DUELING = NATURE + " --double_dqn --dueling --loss=huber"
 APEX = DOUBLE_DUELING + " --prioritized_replay --n_step=3 --num_actors=256"
-RAINBOW = NATURE + " --double_dqn --dueling --distributional --noisy --prioritized_replay --n_step=3 --optimizer=adam --lr=0.0000625"
+RAINBOW = (NATURE + " --double_dqn --dueling --distributional --noisy --prioritized_replay --n_step=3 --optimizer=adam "
+           "--lr=0.0000625").replace("--dtype=bf16", "--dtype=fp16")
 
 PRESETS = {
     'control': CONTROL,
@@ -135,6 +137,11 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_eps_base', default=0.4, type=float, help='Ape-X per-actor epsilon base')
     a('--apex_eps_alpha', default=7.0, type=float, help='Ape-X per-actor epsilon exponent spread')
     a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
+    a('--apex_graph_steps', default=4, type=int,
+      help='Ape-X learner: SGD steps per replayed HIP graph (one host call per that many steps)')
+    a('--apex_serve_gap_us', default=100, type=int,
+      help='Ape-X inference service: pause after each served batch (us) so requests batch up and the '
+           'learner loop gets the GIL')
     a('--allreduce', default='auto', choices=['auto', 'rccl', 'xgmi'],
       help='gradient all-reduce transport: RCCL, the peer-to-peer xGMI kernel (in-graph), or auto '
            '(self-test + time both at start-up, keep the faster)')
@@ -229,6 +236,8 @@ class Config:
     apex_eps_base: float = 0.4
     apex_eps_alpha: float = 7.0
     apex_ring: int = 1024
+    apex_serve_gap_us: int = 100
+    apex_graph_steps: int = 4
     allreduce: str = 'auto'
     allreduce_dtype: str = 'fp32'
     grad_bucket_mb: float = 64.0

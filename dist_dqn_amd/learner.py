@@ -288,6 +288,33 @@ class Learner:
         torch.cuda.current_stream(self.device).wait_stream(s)
 
     # ------------------------------------------------------------- public
+    def step_many(self, k: int) -> torch.Tensor:
+        """k SGD steps with ONE host call: single-process graph mode replays a graph holding k
+        consecutive step bodies (host-light learner loops, e.g. Ape-X, whose Python thread
+        shares the GIL with the inference service); otherwise k ``step()`` calls."""
+        k = int(k)
+        single = self.ps is None and not self.ctx.enabled and self.actor is None
+        if k <= 1 or not single or not self.use_graph or self._graphs is None:
+            for _ in range(max(1, k)):
+                self.step()
+            return self.loss
+        g = getattr(self, '_graph_many', None)
+        if g is None or g[0] != k:
+            torch.cuda.synchronize(self.device)
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            gk = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s):
+                for _ in range(k):
+                    self._sample_and_grad()
+                    self._apply()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._graph_many = g = (k, gk)
+        with trace('learner.step_many'):
+            g[1].replay()
+        self.train_steps += k
+        return self.loss
+
     def step(self) -> torch.Tensor:
         """One SGD step. Returns the (device) TD-loss tensor; no host sync."""
         with trace('learner.step'):

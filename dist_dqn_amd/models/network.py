@@ -60,10 +60,8 @@ def make_executor(arch: ArchSpec, layout, config, device: torch.device):
     if device.type == 'cuda' and backend in ('auto', 'hip') and arch.is_conv:
         from ..ops.executor import make_hip_executor, supports
         if supports(arch):
-            if config.dtype == 'fp32':
-                log.warning('--dtype=fp32 on the HIP conv executor: the MFMA network kernels compute in '
-                            'bf16 (fp32 accumulation, fp32 master weights, gradients and optimizer state); '
-                            'pass --dtype=bf16 to silence this, or --backend=torch for fp32 compute')
+            # --dtype: bf16 / fp16 (16-bit MFMA builds) or fp32 (the reference's precision: the
+            # fp32-MFMA build of the same kernels, _C_f32)
             return make_hip_executor(arch, layout, dtype=config.dtype, **kw)
         if backend == 'hip':
             raise RuntimeError('HIP executor does not support %s' % (arch,))

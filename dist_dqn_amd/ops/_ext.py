@@ -15,9 +15,9 @@ _errs = {}
 
 def load(required: bool = False, variant: str = ''):
     """The native module: '' -> _C (bf16 network kernels), 'f16' -> _C_f16 (fp16 network
-    kernels, csrc/include/dqn_act.h). DQN_DEBUG_EXT=1 swaps in the bounds-checked debug
-    build (_C_debug, bf16) for the default variant."""
-    name = '_C_f16' if variant == 'f16' else '_C'
+    kernels), 'f32' -> _C_f32 (fp32 network kernels; csrc/include/dqn_act.h). DQN_DEBUG_EXT=1
+    swaps in the bounds-checked debug build (_C_debug, bf16) for the default variant."""
+    name = {'f16': '_C_f16', 'f32': '_C_f32'}.get(variant, '_C')
     if name == '_C' and os.environ.get('DQN_DEBUG_EXT', '0') == '1':
         name = '_C_debug'
     if name not in _mods and name not in _errs:

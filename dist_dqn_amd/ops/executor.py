@@ -68,12 +68,16 @@ class HipExecutor:
     def __init__(self, arch, layout, dtype: str = 'bf16', input_scale: float = 1.0, loss: str = 'mse',
                  huber_delta: float = 1.0, double_dqn: bool = False):
         assert supports(arch), 'HIP executor: unsupported architecture'
-        # fp16 (--dtype=fp16): the same kernels built with -DDQN_F16 (fp16 MFMA, static loss
-        # scale inside the kernels); everything else (bf16 default, fp32 master state) is shared
+        # fp16 (--dtype=fp16) / fp32 (--dtype=fp32, the reference's training precision): the same
+        # kernels built with -DDQN_F16 (fp16 MFMA, static loss scale inside the kernels) or
+        # -DDQN_F32 (fp32 MFMA); everything else (fp32 master state, layouts) is shared
+        assert dtype in ('bf16', 'fp16', 'fp32'), dtype
         self.fp16 = dtype == 'fp16'
-        self.compute_dtype = 'fp16' if self.fp16 else 'bf16'
-        self.act_dtype = torch.float16 if self.fp16 else torch.bfloat16
-        self.ext = _ext.load(required=True, variant='f16' if self.fp16 else '')
+        self.compute_dtype = dtype
+        self.act_dtype = {'bf16': torch.bfloat16, 'fp16': torch.float16, 'fp32': torch.float32}[dtype]
+        self.esz = torch.tensor([], dtype=self.act_dtype).element_size()   # bytes per packed / act element
+        self.fs = 4 // self.esz                  # act_t slots of one fp32 value inside the packed buffer
+        self.ext = _ext.load(required=True, variant={'bf16': '', 'fp16': 'f16', 'fp32': 'f32'}[dtype])
         self.arch, self.layout = arch, layout
         self.input_scale = float(input_scale)
         self.huber = loss == 'huber'
@@ -165,20 +169,20 @@ class HipExecutor:
                 dg.append(dict(src_off=lay.offsets['value/output/w'], K=self.atoms, N=H, ks_off=self.c51_VO // 32,
                                mode=2, p0=self.atoms))
             add('head/dgrad', self.c51_KD, self.HH, dg)
-        # concatenated fc bias (fp32, 2 bf16 slots per float)
+        # concatenated fc bias (fp32: self.fs act_t slots per float)
         self.poff['fc/bias'] = off
         for n, o in fcs:
-            jobs.append(_Job(src_off=lay.offsets[n + '/b'], K=H, dst_off=off + 2 * o, mode=3))
-        off += 2 * self.HH
+            jobs.append(_Job(src_off=lay.offsets[n + '/b'], K=H, dst_off=off + self.fs * o, mode=3))
+        off += self.fs * self.HH
         off = (off + 255) // 256 * 256
         if self.dist:
             # C51: the combined output layer's bias row (fp32): logits bias | pad | value bias at VO
             self.poff['head/bias'] = off
             jobs.append(_Job(src_off=lay.offsets[hb], K=self.NO, dst_off=off, mode=3))
             if self.dueling:
-                jobs.append(_Job(src_off=lay.offsets['value/output/b'], K=self.atoms, dst_off=off + 2 * self.c51_VO,
+                jobs.append(_Job(src_off=lay.offsets['value/output/b'], K=self.atoms, dst_off=off + self.fs * self.c51_VO,
                                  mode=3))
-            off += 2 * self.c51_KD
+            off += self.fs * self.c51_KD
             off = (off + 255) // 256 * 256
         self.packed_elems = off
         self.jobs = jobs
@@ -233,7 +237,7 @@ class HipExecutor:
             so, _, eo = nz.get(off, (-1, -1, -1))
             for s0 in range(0, n, 2048):
                 cnt = min(2048, n - s0)
-                items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + 2 * s0) if c else -1] + [0] * 9
+                items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + self.fs * s0) if c else -1] + [0] * 9
                              + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy)])
         self.upd_items = items
         self._upd_dev: Dict[torch.device, torch.Tensor] = {}
@@ -545,7 +549,7 @@ class HipExecutor:
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
         bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
-        pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
+        pk = lambda key: [p.data_ptr() + self.esz * self.poff[key] for p in packs]
         rows = lambda t, i: t[i].data_ptr()
         if self.fused_trunk:
             # ONE launch for conv1..conv3: a workgroup per (sample, instance), activations in LDS
@@ -579,9 +583,9 @@ class HipExecutor:
         self._fc_fwd(packs, flats, ws, B, ninst)
 
     def _fc_fwd(self, packs, flats, ws, B, ninst):
-        fcb = [p.data_ptr() + 2 * self.poff['fc/bias'] for p in packs]
+        fcb = [p.data_ptr() + self.esz * self.poff['fc/bias'] for p in packs]
         self.ext.qnet_igemm(_KIND['DFWD'], [ws['x3'][i].data_ptr() for i in range(ninst)],
-                            [p.data_ptr() + 2 * self.poff['fc/fwd'] for p in packs], fcb,
+                            [p.data_ptr() + self.esz * self.poff['fc/fwd'] for p in packs], fcb,
                             [ws['h'][i].data_ptr() for i in range(ninst)], [], [1.0] * ninst,
                             [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0])
 
@@ -685,10 +689,10 @@ class HipExecutor:
         """Scalar heads: the output layer's fragments (plain / advantage, dueling value); C51: the
         combined output layer's fragments and its fp32 bias row."""
         if self.dist:
-            return ([p.data_ptr() + 2 * self.poff['head/wc'] for p in packs],
-                    [p.data_ptr() + 2 * self.poff['head/bias'] for p in packs])
-        pw = [p.data_ptr() + 2 * self.poff['head/w'] for p in packs]
-        pwv = [p.data_ptr() + 2 * self.poff['head/v'] for p in packs] if self.dueling else []
+            return ([p.data_ptr() + self.esz * self.poff['head/wc'] for p in packs],
+                    [p.data_ptr() + self.esz * self.poff['head/bias'] for p in packs])
+        pw = [p.data_ptr() + self.esz * self.poff['head/w'] for p in packs]
+        pwv = [p.data_ptr() + self.esz * self.poff['head/v'] for p in packs] if self.dueling else []
         return pw, pwv
 
     def _fc_dgrad(self, ws, B, po, zero=(), draw_noise=None):
@@ -701,9 +705,9 @@ class HipExecutor:
         h0, dh = ws['h'][0].data_ptr(), ws['dh'].data_ptr()
         if self.dist:
             self.ext.qnet_igemm(_KIND['DDGRAD'], [ws['dq16'].data_ptr()],
-                                [po.data_ptr() + 2 * self.poff['head/dgrad']], [], [dh], [h0], [1.0],
+                                [po.data_ptr() + self.esz * self.poff['head/dgrad']], [], [dh], [h0], [1.0],
                                 [B, HH, self.c51_KD, HH // 16, HH, 0, 0, 0, 0, 0, 0])
-        pk = po.data_ptr() + 2 * self.poff['fc/dgrad']
+        pk = po.data_ptr() + self.esz * self.poff['fc/dgrad']
         x3, dz3 = ws['x3'][0].data_ptr(), ws['dz3'].data_ptr()
         zp, zn = (zero[0], zero[1]) if zero else (0, 0)
         aux = [zp, zn, ws['loss_parts'].data_ptr(), self._loss_parts(B), ws['loss'].data_ptr()]
@@ -840,7 +844,7 @@ class HipExecutor:
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
         H, HH, F = self.HID, self.HH, self.FLAT
-        pko = lambda key: po.data_ptr() + 2 * self.poff[key]
+        pko = lambda key: po.data_ptr() + self.esz * self.poff[key]
         if self.dueling:
             fw, fb, fw2, fb2 = g('value/fcl/w'), g('value/fcl/b'), g('advantage/fcl/w'), g('advantage/fcl/b')
         else:
@@ -968,7 +972,7 @@ class HipCnnExecutor(HipExecutor):
         assert sample is None, 'the cnn forward reads sampler-made slot tables'
         lay = self.layout
         pad = lambda v: list(v) + [0] * (4 - len(v))
-        pk = lambda key: [p.data_ptr() + 2 * self.poff[key] for p in packs]
+        pk = lambda key: [p.data_ptr() + self.esz * self.poff[key] for p in packs]
         bias = lambda name: [f.data_ptr() + 4 * lay.offsets[name] for f in flats]
         slots = [x.data_ptr() for x in xs] if frames is not None else []
         states = [] if frames is not None else [x.data_ptr() for x in xs]
@@ -984,7 +988,7 @@ class HipCnnExecutor(HipExecutor):
                       hmembers=(), hdims=()):
         ext = self.ext
         F, HH, H = self.FLAT, self.HH, self.HID
-        pko = lambda key: po.data_ptr() + 2 * self.poff[key]
+        pko = lambda key: po.data_ptr() + self.esz * self.poff[key]
         x3 = ws['x3'][0].data_ptr()
         # dp3 = (dh W_fc^T) * (pooled conv3 output > 0)
         fc_dgrad()

@@ -15,7 +15,7 @@ from dist_dqn_amd.replay import DeviceReplay  # noqa: E402
 
 extra = ' '.join(sys.argv[1:])
 dev = torch.device('cuda', 0)
-cfg = preset('nature', 'Pong-v0', '--seed=0 --backend=hip --replay_memory_capacity=200000 ' + extra)
+cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=0 --backend=hip --replay_memory_capacity=200000 ' + extra)
 net = Network.create_network(cfg, (84, 84, 4), 6, device=dev)
 rep = DeviceReplay(200000, (84, 84), 4, device=dev, seed=0)
 rep.fill_synthetic(200000, 6, seed=0)

@@ -10,6 +10,7 @@ A direct hipcc build (no hipify pass, no CUDA compatibility layer):
 Variants (same sources, one module each):
   * dist_dqn_amd/_C*.so       bf16 MFMA network kernels (default executor)
   * dist_dqn_amd/_C_f16*.so   -DDQN_F16: fp16 MFMA network kernels (--dtype=fp16; csrc/include/dqn_act.h)
+  * dist_dqn_amd/_C_f32*.so   -DDQN_F32: fp32 MFMA network kernels (--dtype=fp32, the reference precision)
   * dist_dqn_amd/_C_debug*.so only with DQN_DEBUG=1: -O1 -g, device DQN_ASSERTs (DQN_DEBUG_EXT=1 selects it)
   * dist_dqn_amd/libdqn_host.so  csrc/host/*.cpp without torch/HIP (CPU actor processes, ctypes)
 Objects go to build/<variant>/ and are rebuilt when the source, any csrc header or the
@@ -31,6 +32,7 @@ HOST_OUT = os.path.join(ROOT, 'dist_dqn_amd', 'libdqn_host.so')   # torch-free h
 VARIANTS = {
     'release': ('_C', 'obj', ['-O3']),
     'f16': ('_C_f16', 'obj_f16', ['-O3', '-DDQN_F16=1']),
+    'f32': ('_C_f32', 'obj_f32', ['-O3', '-DDQN_F32=1']),
     'debug': ('_C_debug', 'obj_debug', ['-O1', '-g', '-DDQN_DEBUG=1']),
 }
 
@@ -113,7 +115,7 @@ def _plan_host():
 
 def build(verbose=False, jobs=None, variants=None):
     if variants is None:
-        variants = ['debug'] if os.environ.get('DQN_DEBUG', '0') == '1' else ['release', 'f16']
+        variants = ['debug'] if os.environ.get('DQN_DEBUG', '0') == '1' else ['release', 'f16', 'f32']
 
     def run(cmd):
         if verbose:

@@ -118,7 +118,7 @@ def _worker(rank, world, port, network, extra, errq):
         for overlap in (1, 0):
             # a different init seed per rank: broadcast_state must carry EVERYTHING (params, target,
             # slots, noise stream) and every rank must rebuild its packed / premixed fragments
-            cfg = preset(network, 'Pong-v0', '--seed=%d --backend=hip --replay_memory_capacity=2048 '
+            cfg = preset(network, 'Pong-v0', '--dtype=bf16 --seed=%d --backend=hip --replay_memory_capacity=2048 '
                          '--overlap_allreduce=%d %s' % (3 + rank, overlap, extra))
             if ctx is None:
                 ctx = init_distributed(cfg, device='cuda')

@@ -14,12 +14,15 @@ def _setup(extra='', B=32, seed=0):
     # 'cnn:' prefix = the reference network (SAME convs + max-pools, no input scaling)
     kind = 'atari' if extra.startswith('cnn:') else 'nature'
     extra = extra[4:] if extra.startswith('cnn:') else extra
+    if '--dtype=' not in extra:           # (default: the bf16 production build; fp32 cases say so)
+        extra += ' --dtype=bf16'
     cfg = preset(kind, 'Pong-v0', '--seed=%d --backend=hip %s' % (seed, extra))
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     assert net.executor.name == 'hip'
-    assert net.executor.compute_dtype == ('fp16' if '--dtype=fp16' in extra else 'bf16')
-    if '--dtype=fp16' in extra:
-        assert net.executor.ext.__name__.endswith('_C_f16')
+    want = 'fp16' if '--dtype=fp16' in extra else 'fp32' if '--dtype=fp32' in extra else 'bf16'
+    assert net.executor.compute_dtype == want
+    if want != 'bf16':
+        assert net.executor.ext.__name__.endswith('_C_f16' if want == 'fp16' else '_C_f32')
     g = torch.Generator(device=DEV).manual_seed(seed)
     # larger-than-init weights so every layer carries signal
     net.online.flat.normal_(0.0, 0.03, generator=g)
@@ -49,15 +52,18 @@ RAINBOW = '--distributional --noisy --dueling --double_dqn'
 
 
 F16 = ' --dtype=fp16'
+F32 = ' --dtype=fp32'
 
 
 @pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', '--distributional', '--noisy --dueling',
-                                   RAINBOW, 'cnn:', 'cnn:--dueling', F16, RAINBOW + F16, 'cnn:' + F16])
+                                   RAINBOW, 'cnn:', 'cnn:--dueling', F16, RAINBOW + F16, 'cnn:' + F16,
+                                   F32, RAINBOW + F32, 'cnn:' + F32])
 def test_q_values_match_oracle(extra):
     net, oracle, batch = _setup(extra)
     q = net.q_values(batch['states'])
     q_ref = oracle.q_values(net.online.flat, batch['states'], net.noise)
-    assert _rel(q, q_ref) < 2e-2
+    # fp32 build (the reference precision): only the summation order differs from the oracle
+    assert _rel(q, q_ref) < (1e-4 if F32 in extra else 2e-2)
 
 
 @pytest.mark.parametrize('extra,B,weighted', [('', 32, False), ('--dueling --double_dqn --loss=huber', 32, True),
@@ -69,7 +75,10 @@ def test_q_values_match_oracle(extra):
                                              # fp16 MFMA build (_C_f16, static loss scale)
                                              (F16, 32, False), ('--dueling --double_dqn --loss=huber' + F16, 32, True),
                                              ('--double_dqn' + F16, 64, False), (RAINBOW + F16, 32, True),
-                                             ('cnn:' + F16, 32, False)])
+                                             ('cnn:' + F16, 32, False),
+                                             # fp32 build (_C_f32): the reference's precision
+                                             (F32, 32, False), ('--dueling --double_dqn --loss=huber' + F32, 32, True),
+                                             (RAINBOW + F32, 32, True), ('cnn:' + F32, 32, False)])
 def test_loss_and_grad_match_oracle(extra, B, weighted):
     net, oracle, batch = _setup(extra, B)
     if weighted:
@@ -81,6 +90,16 @@ def test_loss_and_grad_match_oracle(extra, B, weighted):
     loss_r, prio_r = oracle.loss_and_grad(net.online.flat, net.target.flat, batch, g_ref, net.noise,
                                           net.noise_target)
     torch.cuda.synchronize()
+    if F32 in extra:
+        # fp32 MFMA vs the fp32 oracle: summation order only (a ReLU input within rounding of
+        # zero may still flip, so the gradient checks stay per-tensor)
+        assert abs(float(loss) - float(loss_r)) / abs(float(loss_r)) < 1e-4
+        assert _rel(prio, prio_r) < 1e-4
+        assert _rel(g_hip, g_ref) < 1e-3
+        for name in net.layout.names:
+            o, n = net.layout.offsets[name], net.layout.numel(name)
+            assert _rel(g_hip[o:o + n], g_ref[o:o + n]) < 2e-3, name
+        return
     assert abs(float(loss) - float(loss_r)) / abs(float(loss_r)) < 3e-2
     assert _rel(prio, prio_r) < 3e-2
     # bf16 activations flip a few ReLU masks near zero; a flipped unit contributes its
@@ -161,7 +180,7 @@ def test_fused_hard_target_sync():
     from dist_dqn_amd.learner import Learner
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.replay import DeviceReplay
-    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 --target_update_freq=3')
+    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 --target_update_freq=3')
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
     rep.fill_synthetic(4096, 6, seed=5)
@@ -205,7 +224,7 @@ def test_cnn_learner_graph_equals_eager():
     from dist_dqn_amd.replay import DeviceReplay
     outs = []
     for graph in (False, True):
-        cfg = preset('atari', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096')
+        cfg = preset('atari', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096')
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         assert net.executor.name == 'hip' and type(net.executor).__name__ == 'HipCnnExecutor'
         rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
@@ -232,7 +251,7 @@ def test_fused_acting_matches_separate_actor(network, extra):
     outs = []
     for fused in (False, True):
         cfg = preset(network if network == 'nature' else 'atari', 'Pong-v0',
-                     '--seed=4 --backend=hip --replay_memory_capacity=65536 ' + extra)
+                     '--seed=4 --backend=hip --dtype=bf16 --replay_memory_capacity=65536 ' + extra)
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         rep = DeviceReplay(65536, (84, 84), 4, device=DEV, seed=5, prioritized=cfg.prioritized_replay)
         rep.fill_synthetic(65536, 6, seed=5)
@@ -385,7 +404,7 @@ def test_rainbow_learner_keeps_online_premixed():
     from dist_dqn_amd.models.executor import TorchExecutor
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.replay import DeviceReplay
-    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 ' + RAINBOW)
+    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 ' + RAINBOW)
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
     rep.fill_synthetic(4096, 6, seed=5)
@@ -413,7 +432,7 @@ def test_fused_sampling_equals_sampler_launch(extra, acting):
     from dist_dqn_amd.replay import DeviceReplay
     outs = []
     for fuse in (0, 1, 2):
-        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 '
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 '
                      '--fuse_sampling=%d %s' % (fuse, extra))
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5)
@@ -447,7 +466,7 @@ def test_per_fused_in_optimizer_equals_separate_launches(extra):
     from dist_dqn_amd.replay import DeviceReplay
     outs = []
     for fuse in (0, 2):
-        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 '
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 '
                      '--fuse_sampling=%d %s' % (fuse, extra))
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)
@@ -482,7 +501,7 @@ def test_device_actor_inserts_max_priority(network, extra):
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.replay import DeviceReplay
-    cfg = preset(network, 'Pong-v0', '--seed=3 --backend=hip --replay_memory_capacity=4096 --prioritized_replay '
+    cfg = preset(network, 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 --prioritized_replay '
                  + extra)
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)

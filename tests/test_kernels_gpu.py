@@ -210,7 +210,7 @@ def test_device_actor_appends_consistent_transitions():
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.replay import DeviceReplay
-    cfg = preset('nature', 'Pong-v0', '--seed=0 --replay_memory_capacity=1000')
+    cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=0 --replay_memory_capacity=1000')
     net = Network.create_network(cfg, (84, 84, 4), 6, device=torch.device(DEV))
     rep = DeviceReplay(1000, (84, 84), 4, device=DEV)
     actor = DeviceActor(net, rep, cfg, num_envs=8, steps_per_call=4, episode_len=5, use_graph=True)
