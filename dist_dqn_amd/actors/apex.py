@@ -383,7 +383,10 @@ class ApexTrainer:
         self._lock = threading.Lock()       # one forward at a time vs the snapshot refresh
         self._thread = threading.Thread(target=self._serve_loop, name='apex-inference', daemon=True)
         pool.flush_min, pool.flush_max_delay = 256, 0.005     # ship staging in batches (see _drain_native)
-        self.drain_every_s = 0.001          # ring drain cadence of the learner loop
+        if hasattr(replay, 'ensure_stage_sets'):
+            replay.ensure_stage_sets(6)     # flushes never wait on in-flight learner steps
+        self.drain_every_s = 0.003          # ring drain cadence of the learner loop (each drain
+                                            # costs GIL round trips with the inference thread)
         self.graph_steps = max(1, int(getattr(config, 'apex_graph_steps', 4)))   # SGD steps per host call
         self.max_inflight = max(2, 16 // self.graph_steps)   # queued launches before the loop waits
         self.gil_switch_s = 0.0005          # GIL hand-over interval while running

@@ -33,6 +33,9 @@ from .utils.trace import trace
 log = logging.getLogger(__name__)
 
 
+
+_CAPTURE_MODE = 'thread_local'
+
 class Learner:
     def __init__(self, network: Network, replay, config, ctx: Optional[DistContext] = None,
                  use_graph: Optional[bool] = None, ps_client=None, actor=None):
@@ -255,33 +258,36 @@ class Learner:
 
     # ------------------------------------------------------------ graph
     def _capture(self):
+        # (thread-local capture mode: other host threads of the process -- Ape-X inference, the
+        # async-PS client -- keep launching and synchronising their own streams meanwhile)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         g_pre, g_post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             if self.ps is not None:          # post-exchange work is host-driven (eager)
-                with torch.cuda.graph(g_pre, stream=s):
+                with torch.cuda.graph(g_pre, stream=s, capture_error_mode=_CAPTURE_MODE):
                     self._sample_and_grad()
                 self._graphs = (g_pre,)
             elif self.ctx.enabled and self.reducer.in_graph:
-                with torch.cuda.graph(g_pre, stream=s):      # the whole DP step: ONE graph
+                # the whole DP step: ONE graph
+                with torch.cuda.graph(g_pre, stream=s, capture_error_mode=_CAPTURE_MODE):
                     self._sample_and_grad()
                     self._kernel_allreduce()
                     self._apply()
                 self._graphs = (g_pre,)
             elif self.ctx.enabled:
-                with torch.cuda.graph(g_pre, stream=s):
+                with torch.cuda.graph(g_pre, stream=s, capture_error_mode=_CAPTURE_MODE):
                     self._sample_and_grad()
                 g_tail = None
                 if self._split and self._tail is not None:
                     g_tail = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g_tail, stream=s):
+                    with torch.cuda.graph(g_tail, stream=s, capture_error_mode=_CAPTURE_MODE):
                         self._tail()
-                with torch.cuda.graph(g_post, stream=s):
+                with torch.cuda.graph(g_post, stream=s, capture_error_mode=_CAPTURE_MODE):
                     self._apply()
                 self._graphs = (g_pre, g_post, g_tail)
             else:
-                with torch.cuda.graph(g_pre, stream=s):
+                with torch.cuda.graph(g_pre, stream=s, capture_error_mode=_CAPTURE_MODE):
                     self._sample_and_grad()
                     self._apply()
                 self._graphs = (g_pre,)
@@ -304,7 +310,7 @@ class Learner:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             gk = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s):
+            with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
                 for _ in range(k):
                     self._sample_and_grad()
                     self._apply()

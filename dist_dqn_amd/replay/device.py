@@ -139,6 +139,15 @@ class DeviceReplay:
     def _stage(self) -> '_StageSet':
         return self._sets[self._cur]
 
+    def ensure_stage_sets(self, n: int):
+        """At least n pinned staging sets in the rotation (default 2): a set is refilled only
+        after its H2D copies ran, and those are ordered after the learner work queued before
+        its flush, so a producer that flushes while many learner steps are in flight (Ape-X)
+        needs a deeper rotation to never wait on them."""
+        if self._pin:
+            while len(self._sets) < n:
+                self._sets.insert(self._cur + 1, _StageSet(self, self._stage_size))
+
     def _alloc_frame(self, frame) -> int:
         # frame slots are handed out sequentially, so staged frames are one
         # contiguous (wrap-split) range starting at _st_frame_first

@@ -139,6 +139,38 @@ def test_learner_step_graph_equals_eager(dtype):
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize('extra', ['', '--double_dqn --dueling --prioritized_replay --n_step=3'])
+def test_learner_step_many_equals_single_steps(extra):
+    """Learner.step_many(k) (ONE graph holding k step bodies, the Ape-X learner loop) ==
+    k separate step() replays."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    outs = []
+    for many in (False, True):
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 '
+                     '--target_update_freq=5 ' + extra)
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=cfg.prioritized_replay)
+        rep.fill_synthetic(4096, 6, seed=5)
+        ln = Learner(net, rep, cfg, use_graph=True)
+        for _ in range(3):                     # eager warm-up + the single-step capture
+            ln.step()
+        if many:
+            ln.step_many(4)
+            ln.step_many(4)
+        else:
+            for _ in range(8):
+                ln.step()
+        torch.cuda.synchronize()
+        assert int(net.global_step) == 11 and ln.train_steps == 11
+        outs.append((net.online.flat.clone(), net.target.flat.clone()))
+    # (conv weight gradients combine M-chunks with fp32 atomics: order-dependent last bits)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize('slots', [False, True])
 def test_fused_trunk_matches_layerwise(slots):
     """trunk.hip (conv1..conv3 in one launch, activations in LDS) == the three
