@@ -391,6 +391,7 @@ class ApexTrainer:
         self.max_inflight = max(2, 16 // self.graph_steps)   # queued launches before the loop waits
         self.gil_switch_s = 0.0005          # GIL hand-over interval while running
         self.serve_gap_s = float(getattr(config, 'apex_serve_gap_us', 100)) * 1e-6
+        self.native_serve = bool(getattr(config, 'apex_native_serve', 1))
         self.serve_calls = 0
         self.learn_t0 = None                # wall time / env frames when the learner took its first step
         self.learn_frames0 = 0
@@ -462,6 +463,44 @@ class ApexTrainer:
             self._done.synchronize()         # (the actors wait for these actions)
             return self._pin_out[:m].numpy()
 
+    def _start_native_server(self) -> bool:
+        """Serve the mailboxes from a C++ thread (csrc/infer_server.cpp) replaying per-bucket
+        inference graphs: the Python thread (and its GIL traffic) is not needed at all."""
+        ext = getattr(self.net.executor, 'ext', None)
+        if (self.device.type != 'cuda' or ext is None or not hasattr(ext, 'InferServer') or self._graphs_off
+                or not self.native_serve):
+            return False
+        pool = self.pool
+        n = pool.n
+        shape = (pool.frame_hw[0], pool.frame_hw[1], pool.k) if pool.frame_hw else (pool.obs_dim,)
+        f32 = pool.frame_hw is None
+        sizes = sorted({min(n, 1 << i) for i in range(n.bit_length() + 1)} | {n})
+        with self.torch.no_grad():
+            for m in sizes:
+                if self._infer_graph(m, (m,) + shape, f32) is None:
+                    return False
+        srv = ext.InferServer(int(pool.mbox.ctypes.data), n, pool.state_bytes, self._pin_in.data_ptr(),
+                              self._dev_in.data_ptr(), self._gout.data_ptr(), self._pin_out.data_ptr(),
+                              self.device.index if self.device.index is not None else 0,
+                              int(self.serve_gap_s * 1e6))
+        for m in sizes:
+            srv.set_graph(m, self._graphs[m].raw_cuda_graph_exec())
+        srv.start()
+        self._server = srv
+        log.info('Ape-X inference: native server thread, graph buckets %s', sizes)
+        return True
+
+    def _stop_native_server(self):
+        srv = getattr(self, '_server', None)
+        if srv is not None:
+            srv.stop()
+            served, calls, err = srv.stats()
+            self.pool.served += int(served)
+            self.serve_calls += int(calls)
+            if err:
+                log.error('Ape-X native inference server failed: %s', err)
+            self._server = None
+
     def _serve_loop(self):
         from ..utils.trace import trace
         while not self._stop.is_set():
@@ -478,7 +517,8 @@ class ApexTrainer:
         cfg = self.config
         start = max(cfg.minibatch_size, cfg.replay_start_size)
         self.pool.start()
-        self._thread.start()
+        if not self._start_native_server():
+            self._thread.start()
         t0 = last = time.time()
         steps_at_last = frames_at_last = 0
         # sync-DP Ape-X: every learner step is a collective, so local reasons to stop (time
@@ -561,6 +601,9 @@ class ApexTrainer:
         finally:
             sys.setswitchinterval(switch)
             self._stop.set()
-            self._thread.join(5.0)
+            if self._thread.is_alive():
+                self._thread.join(5.0)
+            self.pool.lib.mbox_set_stop(self.pool.mbox, 1)      # (releases actors and the native server)
+            self._stop_native_server()
             self.pool.stop()
         return self

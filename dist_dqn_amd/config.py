@@ -137,6 +137,8 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_eps_base', default=0.4, type=float, help='Ape-X per-actor epsilon base')
     a('--apex_eps_alpha', default=7.0, type=float, help='Ape-X per-actor epsilon exponent spread')
     a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
+    a('--apex_native_serve', default=1, type=int,
+      help='Ape-X: answer the actors from a C++ thread replaying captured inference graphs (GPU)')
     a('--apex_graph_steps', default=4, type=int,
       help='Ape-X learner: SGD steps per replayed HIP graph (one host call per that many steps)')
     a('--apex_serve_gap_us', default=100, type=int,
@@ -238,6 +240,7 @@ class Config:
     apex_ring: int = 1024
     apex_serve_gap_us: int = 100
     apex_graph_steps: int = 4
+    apex_native_serve: int = 1
     allreduce: str = 'auto'
     allreduce_dtype: str = 'fp32'
     grad_bucket_mb: float = 64.0
