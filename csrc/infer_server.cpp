@@ -126,7 +126,9 @@ class InferServer {
 }  // namespace
 
 void register_infer_server(pybind11::module_& m) {
-  pybind11::class_<InferServer>(m, "InferServer")
+  // module_local: every extension variant (_C, _C_f16, _C_f32) registers its own copy and one
+  // process may load several of them
+  pybind11::class_<InferServer>(m, "InferServer", pybind11::module_local())
       .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>())
       .def("set_graph", &InferServer::set_graph)
       .def("start", &InferServer::start)

@@ -1,0 +1,22 @@
+"""Every built native-extension variant (bf16 _C, fp16 _C_f16, fp32 _C_f32) imports, alone and
+all together in one process (module-local pybind types; -Bsymbolic kernel launchers)."""
+import importlib
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _built(name):
+    pkg = os.path.join(ROOT, 'dist_dqn_amd')
+    return any(f.startswith(name + '.') and f.endswith('.so') for f in os.listdir(pkg))
+
+
+def test_all_variants_import_together():
+    names = [n for n in ('_C', '_C_f16', '_C_f32') if _built(n)]
+    if not names:
+        pytest.skip('native extension not built')
+    mods = [importlib.import_module('dist_dqn_amd.' + n) for n in names]
+    for m in mods:
+        assert hasattr(m, 'qnet_igemm') and hasattr(m, 'optim_pack') and hasattr(m, 'InferServer')
