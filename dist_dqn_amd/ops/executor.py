@@ -20,6 +20,7 @@ kernels of csrc/kernels/cnn.hip (`HipCnnExecutor`). `simple` uses torch.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -103,9 +104,12 @@ class HipExecutor:
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
+        # DQN_OVERLAP_WGRAD=1: the fc + output-layer members on a parallel graph branch beside the
+        # dgrad chain instead. Measured on MI355X: 12.0k -> 9.9k steps/s (flagship), 6.7k -> 6.0k
+        # (Rainbow) -- the graph's cross-stream fork / join costs more than the overlap gains
+        self.overlap_dense_wgrad = os.environ.get('DQN_OVERLAP_WGRAD', '0') == '1'
         # fused optimizer+pack grid: <= 256 = grid-stride with a flat ticket; larger = one block
         # per 32x64 tile with the two-level ticket (DQN_OPT_GRID overrides, for A/B runs)
-        import os
         self.opt_max_grid = int(os.environ.get('DQN_OPT_GRID', '2048'))
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_head.py)
@@ -695,18 +699,23 @@ class HipExecutor:
         pwv = [p.data_ptr() + self.esz * self.poff['head/v'] for p in packs] if self.dueling else []
         return pw, pwv
 
-    def _fc_dgrad(self, ws, B, po, zero=(), draw_noise=None):
+    def _c51_dh(self, ws, B, po):
+        """C51: dH = (dout16 [W | Wv]^T) * (h > 0) on the igemm kernel (packed dgrad fragments)."""
+        HH = self.HH
+        self.ext.qnet_igemm(_KIND['DDGRAD'], [ws['dq16'].data_ptr()],
+                            [po.data_ptr() + self.esz * self.poff['head/dgrad']], [], [ws['dh'].data_ptr()],
+                            [ws['h'][0].data_ptr()], [1.0], [B, HH, self.c51_KD, HH // 16, HH, 0, 0, 0, 0, 0, 0])
+
+    def _fc_dgrad(self, ws, B, po, zero=(), draw_noise=None, dh_done=False):
         """dz3 = (dH W_fc^T) * (x3 > 0) on the igemm kernel; the launch also zeroes the conv
         weight-gradient range and sums the head's loss partials (side duties). Scalar heads: the
         head kernel wrote dH; C51: dH = (dout16 [W | Wv]^T) * (h > 0) is one more igemm launch
         before it, over the head's dL/dlogits rows. draw_noise = (out0, out1, rng): the launch
         also draws the next noisy-net samples (see ``loss_and_grad``)."""
         F, HH = self.FLAT, self.HH
-        h0, dh = ws['h'][0].data_ptr(), ws['dh'].data_ptr()
-        if self.dist:
-            self.ext.qnet_igemm(_KIND['DDGRAD'], [ws['dq16'].data_ptr()],
-                                [po.data_ptr() + self.esz * self.poff['head/dgrad']], [], [dh], [h0], [1.0],
-                                [B, HH, self.c51_KD, HH // 16, HH, 0, 0, 0, 0, 0, 0])
+        dh = ws['dh'].data_ptr()
+        if self.dist and not dh_done:
+            self._c51_dh(ws, B, po)
         pk = po.data_ptr() + self.esz * self.poff['fc/dgrad']
         x3, dz3 = ws['x3'][0].data_ptr(), ws['dz3'].data_ptr()
         zp, zn = (zero[0], zero[1]) if zero else (0, 0)
@@ -879,11 +888,26 @@ class HipExecutor:
                     [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]] + hdims
             scales = [self.input_scale] + [1.0] * (len(members) - 1)
             noisy = self.noisy and gnoise is not None
-            fc_dgrad()
+            side = None
             if split and not noisy:
+                fc_dgrad()
                 # dense weight gradients now (they need only dh, dQ and x3 / h): the dense range is final
                 ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
                 members, dims, scales = members[:3], dims[:3], scales[:3]
+            elif self.overlap_dense_wgrad and not split:
+                # fc + output-layer weight gradients on a parallel graph branch as soon as dH
+                # exists: they overlap the (latency-bound, few-CU) fc / conv3 / conv2 dgrad chain,
+                # and the closing grouped launch holds the conv members only
+                if self.dist:
+                    self._c51_dh(ws, B, po)
+                side = self._side_stream(dev)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
+                members, dims, scales = members[:3], dims[:3], scales[:3]
+                self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True)
+            else:
+                fc_dgrad()
 
             def tail():
                 ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [],
@@ -895,6 +919,8 @@ class HipExecutor:
                                [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
                                 0, 0])
                 ext.qnet_wgrad_group(members, dims, scales)
+                if side is not None:
+                    main.wait_stream(side)
                 if noisy:
                     ext.qnet_noisy_grad(grad_out.data_ptr(), gnoise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                         len(self.noisy_jobs), self._noisy_max)
