@@ -170,8 +170,13 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
   }
 }
 
-template <int OP, bool TMIX>
-__global__ void __launch_bounds__(kPackThreads)
+// MODE bits: kModeNoisy (noisy jobs in the work list), kModeTmix (+ the target's mix + pack),
+// kModePer (the sampler block runs the prioritized sum-tree path). Paths a mode excludes are
+// not instantiated: their registers would cost the plain nets occupancy (mode 0: 8 waves / SIMD,
+// so every block of the Nature-CNN work list is resident at once).
+constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4;
+template <int OP, int MODE>
+__global__ void __launch_bounds__(kPackThreads, MODE == 0 ? 8 : 1)
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
@@ -190,6 +195,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // tnoise (noisy nets, update calls): also mix + pack the TARGET under its next noise
   // sample into teff / tpk (the target's eff / packed buffers): no separate target mix launch.
   constexpr bool UPD = OP >= 0;
+  constexpr bool TMIX = (MODE & kModeTmix) != 0, NZOK = (MODE & kModeNoisy) != 0, PEROK = (MODE & kModePer) != 0;
   // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
   const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
   constexpr size_t kTileBytes = 32 * 72 * sizeof(act_t);
@@ -213,7 +219,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
   constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
-  if (sampler && per.sum != nullptr) {
+  if (PEROK && sampler && per.sum != nullptr) {
     // prioritized: this step's priorities into the tree (one wave), then the next step's
     // stratified sample from the updated tree (beta of the NEXT global_step)
     const int64_t step0 = per.step[0];                  // read before this block's ticket add
@@ -422,15 +428,17 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   using F_ = std::false_type;
   for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) {
     const UpdJob jb = jobs[ji];
-    const bool nz = jb.sig_off >= 0;
+    const bool nz = NZOK && jb.sig_off >= 0;
     // float4 rows: 16-byte aligned tensor (and sigma) offsets and a row / chunk length % 4 == 0
     const bool al = ((jb.src_off | (nz ? jb.sig_off : 0)) & 3) == 0 && ((jb.kind == 1 ? jb.K : jb.N) & 3) == 0;
     if (!nz) {
       if (al) item(jb, T_{}, F_{}, F_{}); else item(jb, F_{}, F_{}, F_{});
-    } else if (gnoise != nullptr) {
-      if (al) item(jb, T_{}, T_{}, T_{}); else item(jb, F_{}, T_{}, T_{});
-    } else {
-      if (al) item(jb, T_{}, T_{}, F_{}); else item(jb, F_{}, T_{}, F_{});
+    } else if constexpr (NZOK) {
+      if (gnoise != nullptr) {
+        if (al) item(jb, T_{}, T_{}, T_{}); else item(jb, F_{}, T_{}, T_{});
+      } else {
+        if (al) item(jb, T_{}, T_{}, F_{}); else item(jb, F_{}, T_{}, F_{});
+      }
     }
   }
   if (!UPD) return;
@@ -558,20 +566,22 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   act_t* P = reinterpret_cast<act_t*>(packed);
   act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
   const int tf = tfreq < 1 ? 1 : tfreq;
-#define OPK(N) do { if (tnoise != nullptr) \
-    hipLaunchKernelGGL((optim_pack_kernel<N, true>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
-                       ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe, tnoise, \
-                       teff, reinterpret_cast<act_t*>(tpk), noise_rng); \
-  else \
-    hipLaunchKernelGGL((optim_pack_kernel<N, false>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, beta_pow, step, \
-                       ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, sm, pe, tnoise, \
-                       teff, reinterpret_cast<act_t*>(tpk), noise_rng); } while (0)
+  // (a noisy net always passes its noise sample; plain nets pass none)
+  const int mode = (noise != nullptr ? kModeNoisy : 0) | (tnoise != nullptr ? kModeTmix : 0) |
+                   (pe.sum != nullptr ? kModePer : 0);
+#define OPM(N, M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, \
+                       beta_pow, step, ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, \
+                       sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng)
+#define OPK(N) do { switch (mode) { \
+    case 0: OPM(N, 0); break; case 1: OPM(N, 1); break; case 3: OPM(N, 3); break; \
+    case 4: OPM(N, 4); break; case 5: OPM(N, 5); break; default: OPM(N, 7); break; } } while (0)
   switch (op) {
-    case -1: OPK(-1); break;
+    case -1: OPM(-1, kModeNoisy); break;     // mix + pack only (noisy nets)
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
     case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break; case 7: OPK(7); break;
     default: break;
   }
+#undef OPM
 #undef OPK
 }
 
