@@ -102,6 +102,22 @@ DQN_DEV float row16_max(float v) {
   return v;
 }
 
+// 4x4 transpose inside each lane quad (DPP quad_perm [1,0,3,2] then [2,3,0,1]): lane p of a
+// quad holds row p of a 4x4 block on entry and column p on exit. VALU-only, all lanes active.
+DQN_DEV void quad_transpose4(float (&v)[4]) {
+  const int p = __lane_id() & 3;
+  const bool odd = (p & 1) != 0, hi = (p & 2) != 0;
+  float t0 = odd ? v[0] : v[1], t1 = odd ? v[2] : v[3];
+  t0 = dpp_f<0xB1>(t0);
+  t1 = dpp_f<0xB1>(t1);
+  if (odd) { v[0] = t0; v[2] = t1; } else { v[1] = t0; v[3] = t1; }
+  t0 = hi ? v[0] : v[2];
+  t1 = hi ? v[1] : v[3];
+  t0 = dpp_f<0x4E>(t0);
+  t1 = dpp_f<0x4E>(t1);
+  if (hi) { v[0] = t0; v[1] = t1; } else { v[2] = t0; v[3] = t1; }
+}
+
 // Whole-wave sum: DPP row sums, then the 4 row totals via readlane (uniform result).
 DQN_DEV float wave_sum_dpp(float v) {
   v = row16_sum(v);

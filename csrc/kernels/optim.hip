@@ -132,8 +132,11 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 // consecutive n of one row (one float4 per operand: few VGPRs, high occupancy). It
 // updates the tile in registers, writes fp32 weights + slots back, and emits the tile's
 // bf16 MFMA fragments straight away:
-//   * forward fragments ([K/32][N/16][64][8]: 8 consecutive k per lane) through
-//     one LDS transpose of the tile;
+//   * forward fragments ([K/32][N/16][64][8]: 8 consecutive k per lane): a wave owns an
+//     8 (k) x 32 (n) sub-tile with lane = 8 * col-group + row, so the 4 lanes of a quad hold
+//     4 consecutive rows x the same 4 columns; one 4x4 DPP transpose per quad leaves each
+//     lane 4 consecutive k of one column = half of a fragment slot, stored directly (no LDS
+//     round trip, no barrier; the LDS transpose it replaces ran at ~40% bank conflicts);
 //   * dgrad fragments (dense transpose, or conv (tap, co) x ci) directly from the
 //     thread's registers: its 4 consecutive K' ARE 4 consecutive n of one row (half
 //     of one lane's 8-value slot).
@@ -176,7 +179,7 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 // so every block of the Nature-CNN work list is resident at once).
 constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4;
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, MODE == 0 ? 8 : 1)
+__global__ void __launch_bounds__(kPackThreads, MODE == 0 ? 8 : (((MODE & kModeTmix) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
@@ -198,11 +201,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   constexpr bool TMIX = (MODE & kModeTmix) != 0, NZOK = (MODE & kModeNoisy) != 0, PEROK = (MODE & kModePer) != 0;
   // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
   const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
-  constexpr size_t kTileBytes = 32 * 72 * sizeof(act_t);
-  __shared__ __attribute__((aligned(16))) unsigned char smem[sizeof(SampleLds) > kTileBytes ? sizeof(SampleLds)
-                                                                                           : kTileBytes];
-  act_t* tile = reinterpret_cast<act_t*>(smem);
-  static_assert(sizeof(SumtreeLds) <= sizeof(smem), "sum-tree scratch fits");
+  // LDS: only the sampler block's scratch (the update items exchange through DPP)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[sizeof(SampleLds) > sizeof(SumtreeLds) ? sizeof(SampleLds)
+                                                                                                     : sizeof(SumtreeLds)];
   const bool extra = smp.size != nullptr || per.sum != nullptr;   // the grid has a sampler block
   // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
   const bool sampler = extra && blockIdx.x == 0;
@@ -267,8 +268,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       e0 = (int64_t)jb.src_off + n;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ok[j] = n + j < jb.K;
-    } else {                       // tile: row r, columns c4..c4+3
-      const int r = t >> 4, c4 = (t & 15) * 4;
+    } else {                       // tile: row r, columns c4..c4+3 (wave: 8 rows x 32 columns)
+      const int wv = t >> 6, l = t & 63;
+      const int r = (wv >> 1) * 8 + (l & 7), c4 = (wv & 1) * 32 + (l >> 3) * 4;
       k = jb.k0 + r;
       n = jb.n0 + c4;
       rowok = k < jb.K;
@@ -389,12 +391,15 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       return;                      // uniform per block: no barrier below is skipped unevenly
     }
     // bf16 fragments of this tile into dst (+ dst2): dgrad straight from the registers (4
-    // consecutive K' of one lane's slot), forward through an LDS transpose of the tile
+    // consecutive K' of one lane's slot), forward after a 4x4 transpose inside each lane quad
     auto emit = [&](const float* ev, act_t* dst, act_t* dst2, bool dgrad) {
-      bfx4 v;
+      float x[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (act_t)(ok[j] ? ev[j] : 0.f);
+      for (int j = 0; j < 4; ++j) x[j] = ok[j] ? ev[j] : 0.f;
       if (dgrad && jb.dg_mode != 0 && rowok && n < jb.N) {
+        bfx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (act_t)x[j];
         int kp, np;                                        // K' of the first of the 4 values, N'
         if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
         else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
@@ -405,21 +410,18 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         *reinterpret_cast<bfx4*>(dst + o) = v;
         if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = v;
       }
-      *reinterpret_cast<bfx4*>(tile + (t >> 4) * 72 + (t & 15) * 4) = v;
-      __syncthreads();
-      if (t < 256) {
-        const int nt = t >> 6, l = t & 63, nl = nt * 16 + (l & 15), kk = 8 * (l >> 4);
-        if (jb.n0 + nt * 16 < jb.N) {
-          bfx8 f;
+      quad_transpose4(x);          // lane: column (n - q) + q, rows 4 * half .. + 3 of its quad
+      const int l = t & 63, q = l & 3, half = (l >> 2) & 1, rg = (t >> 6) >> 1;
+      const int col = n + q;       // n: this lane's first column before the transpose (quad-uniform)
+      if ((col & ~15) < jb.N) {    // n-tile exists (columns past N inside it are zeros)
+        bfx4 f;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = tile[(kk + j) * 72 + nl];
-          const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
-                                                    ((jb.n0 >> 4) + nt)) * 64 + l) * 8;
-          *reinterpret_cast<bfx8*>(dst + o) = f;
-          if (dst2) *reinterpret_cast<bfx8*>(dst2 + o) = f;
-        }
+        for (int j = 0; j < 4; ++j) f[j] = (act_t)x[j];
+        const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
+                                                  (col >> 4)) * 64 + rg * 16 + (col & 15)) * 8 + half * 4;
+        *reinterpret_cast<bfx4*>(dst + o) = f;
+        if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = f;
       }
-      __syncthreads();
     };
     emit(e, packed, psync ? tgt_packed : nullptr, true);
     if (tmix) emit(te, tpk, nullptr, false);              // (the target runs forward only)

@@ -451,15 +451,42 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 // elements) so each lane's 8 consecutive m are one ds_read_b128; then
 // (KB/16)x(NB/16) output tiles x MC/32 MFMA k-steps. fp32 atomics only when
 // more than one M-chunk contributes to a weight.
+#if DQN_ACT_F32
 template <int MC, int KB, int NB>
 struct WgradTile {
   static constexpr int LR = MC + 8;
   static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(act_t);
 };
+#else
+// 16-bit builds: the chunk is staged ROW-major ([m][k] and [m][n], one ds_write_b128 per
+// loaded 8-element fragment) and the MFMA operands (8 m values of one k / n column per lane)
+// come from ds_read_b64_tr_b16 transposed reads. Row strides of X + 16 elements put the 8
+// rows one 32-lane half reads (32 B each) on disjoint 8-bank ranges (stride / 4 B = 8 * odd
+// banks for X = 32, 64, 128): conflict-free reads.
+template <int MC, int KB, int NB>
+struct WgradTile {
+  static constexpr int SA = KB + 16, SZ = NB + 16;
+  static constexpr size_t lds_bytes = (size_t)MC * (SA + SZ) * sizeof(act_t);
+};
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+// 4 rows x 16 columns of 16-bit elements, column-major into the lanes of each 16-lane group
+// (lane 4q + p addresses row q, columns 4p..4p+3; lane i receives column i, row q in element q)
+DQN_DEV s16x4 lds_tr16(const act_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(p)));
+}
+DQN_DEV bfx8 join_tr(s16x4 lo, s16x4 hi) {
+  union { s16x4 h[2]; bfx8 v; } u;
+  u.h[0] = lo;
+  u.h[1] = hi;
+  return u.v;
+}
+#endif
 
 // Body shared by the per-layer launch and the grouped launch (one block = one
 // (M-chunk, K-range, N-range) tile; LDS passed in so a grouped kernel can carve
 // every member's staging from one buffer).
+#if DQN_ACT_F32
 template <class LD, int MC, int KB, int NB>
 DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, act_t* lds) {
   constexpr int LR = MC + 8;
@@ -544,6 +571,90 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     }
   }
 }
+
+#else
+template <class LD, int MC, int KB, int NB>
+DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, act_t* lds) {
+  using Tl = WgradTile<MC, KB, NB>;
+  constexpr int SA = Tl::SA, SZ = Tl::SZ;
+  constexpr int TPR = 256 / MC;                  // threads per staged row
+  constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
+  constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
+  static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0, "tiling");
+  act_t* At = lds;                               // [MC][SA]
+  act_t* Zt = lds + MC * SA;                     // [MC][SZ]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
+  {
+    const int r = threadIdx.x % MC, p = threadIdx.x / MC;
+    const int m = m_lo + r;
+    const bool mok = m < a.M;
+    const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
+    LD ld(a, 0, m);
+    bfx8 va[GA], vz[GZ];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int k0 = k_lo + (p + i * TPR) * 8;
+      va[i] = sel8(k0 < a.K, ld.frag(min(k0, a.K - 8)));          // (clamped: no branch per load)
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;              // clamped into the dZ row
+      vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
+    }
+#pragma unroll
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (p + i * TPR) * 8) = va[i];
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[i];
+  }
+  __syncthreads();
+  const bool atomic = g.atomic != 0;
+  if (g.db != nullptr && by == 0) {
+    for (int n = threadIdx.x; n < NB; n += 256) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < MC; ++r) s += (float)Zt[r * SZ + n];
+      const int nn = n_lo + n;
+      if (nn < g.N) {
+        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        s *= kInvLossScale;
+        if (atomic) atomicAdd(pdb, s); else *pdb = s;
+      }
+    }
+  }
+  // operand lane map: k-group gq = lane >> 4 takes m rows {4 gq + q} (elements 0..3) and
+  // {16 + 4 gq + q} (elements 4..7) of each 32-row k-step -- the same permutation of the
+  // reduction index on both operands; one 32-lane half reads 8 consecutive rows per instruction
+  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+  constexpr int NTt = NB / 16;
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int tile = wave + 4 * i;
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
+    const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
+      const bfx8 bf = join_tr(lds_tr16(pz + 32 * s * SZ), lds_tr16(pz + (32 * s + 16) * SZ));
+      acc = mfma16(af, bf, acc);
+    }
+    const int n = n_lo + nt * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k_lo + kt * 16 + 4 * (lane >> 4) + r;
+      if (k < a.K && n < g.N) {
+        float* p = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
+                                : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
+        const float v = acc[r] * (g.scale * kInvLossScale);
+        if (atomic) atomicAdd(p, v); else *p = v;
+      }
+    }
+  }
+}
+#endif
 
 template <class LD, int MC, int KB, int NB>
 __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
@@ -919,16 +1030,22 @@ DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, 
   wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
 }
 
+#ifndef DQN_GRP_CONV_MC
+#define DQN_GRP_CONV_MC 128
+#endif
+// conv members' M-chunk: 128 rows keeps every block's LDS at <= 40 KB (4 blocks / CU), so the
+// whole grouped grid is resident at once (256-row chunks: 80 KB, 2 blocks / CU, a tail round)
+constexpr int kGrpConvMC = DQN_GRP_CONV_MC;
 __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
   extern __shared__ __attribute__((aligned(16))) act_t glds[];
   int b = blockIdx.x, i = 0;
   while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
   switch (G.kind[i]) {
     // 256-row M-chunks, K split over blocks: 2-4x fewer fp32 atomic partials than 128-row chunks
-    case L_NAT_CONV1_FWD: group_member<NatC1, 256, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV1_FRAMES: group_member<NatF1, 256, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV2_FWD: group_member<NatC2, 256, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV3_FWD: group_member<NatC3, 256, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV1_FWD: group_member<NatC1, kGrpConvMC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV1_FRAMES: group_member<NatF1, kGrpConvMC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV2_FWD: group_member<NatC2, kGrpConvMC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    case L_NAT_CONV3_FWD: group_member<NatC3, kGrpConvMC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     case L_DENSE_FWD_RELU: group_member<DenseLoader, 32, 64, 128>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     case L_HEAD_WGRAD: group_member<DenseLoader, 32, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     default: break;
@@ -938,14 +1055,18 @@ __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
 
 static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
   switch (kind) {
-    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = 256; KB = 64; NB = 32; break;
-    case L_NAT_CONV2_FWD: MC = 256; KB = 64; NB = 64; break;
-    case L_NAT_CONV3_FWD: MC = 256; KB = 64; NB = 64; break;
+    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = kGrpConvMC; KB = 64; NB = 32; break;
+    case L_NAT_CONV2_FWD: MC = kGrpConvMC; KB = 64; NB = 64; break;
+    case L_NAT_CONV3_FWD: MC = kGrpConvMC; KB = 64; NB = 64; break;
     case L_DENSE_FWD_RELU: MC = 32; KB = 64; NB = 128; break;
     case L_HEAD_WGRAD: MC = 32; KB = 64; NB = 64; break;
     default: return false;
   }
+#if DQN_ACT_F32
   lds = (size_t)(KB + NB) * (MC + 8) * sizeof(act_t);
+#else
+  lds = (size_t)MC * (KB + 16 + NB + 16) * sizeof(act_t);      // WgradTile<...>::lds_bytes
+#endif
   return true;
 }
 
@@ -962,6 +1083,10 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
     const int gz = (G.g[i].N + NB - 1) / NB;
     G.nblk[i] = G.gx[i] * G.gy[i] * gz;
     G.g[i].atomic = G.gx[i] > 1 ? 1 : 0;
+    // timing probe only (wrong gradients): DQN_WGRAD_PROBE_NOATOMIC=1 stores the M-chunk partials
+    // plainly, to price the fp32 atomics of the multi-chunk members
+    static const bool noatomic = getenv("DQN_WGRAD_PROBE_NOATOMIC") != nullptr;
+    if (noatomic) G.g[i].atomic = 0;
     total += G.nblk[i];
     lds = l > lds ? l : lds;
   }

@@ -61,51 +61,62 @@ DQN_DEV void sumtree_update_wave(float* __restrict__ sum, float* __restrict__ mn
     const uint64_t kn = lane < 63 ? L.sk[lane + 1] : ~0ull;
     bool act = ok && (lane == 63 || (kn >> 6) != (k >> 6));
     int c = P + leaf;
-    float sib_s[kMaxLevels], sib_m[kMaxLevels];
-  #pragma unroll
-    for (int l = 0; l < kMaxLevels; ++l) {
-      if (l < levels && act) {
-        const int sb = (c >> l) ^ 1;
-        sib_s[l] = sum[sb];
-        sib_m[l] = mn[sb];
-      } else {
-        sib_s[l] = 0.f;
-        sib_m[l] = INFINITY;
-      }
-    }
+    const int c0 = c;
     float vs = v0, vm = v0;
     if (act) {
       sum[c] = vs;
       mn[c] = vm;
     }
+    // siblings are loaded kSibBatch levels at a time (one batch of independent loads per
+    // chunk: kMaxLevels registers x2 would cost every block of the host launch occupancy).
+    // A sibling that another lane writes during the climb is taken from that lane's shuffle,
+    // so a load that raced with its store is never used.
+    constexpr int kSibBatch = 10;
+    for (int l0 = 0; l0 < kMaxLevels; l0 += kSibBatch) {
+      if (l0 >= levels) break;                                  // uniform
+      float sib_s[kSibBatch], sib_m[kSibBatch];
   #pragma unroll
-    for (int l = 0; l < kMaxLevels; ++l) {
-      if (l >= levels) break;                                 // uniform
-      const uint64_t am = __ballot(act);
-      // nearest active lanes below / above
-      const uint64_t below = am & ((1ull << lane) - 1ull);
-      const uint64_t above = lane < 63 ? am & ~((2ull << lane) - 1ull) : 0ull;
-      const int lo = below ? 63 - __clzll((long long)below) : lane;
-      const int hi = above ? __ffsll((long long)above) - 1 : lane;
-      const int nlo = __shfl(c, lo, 64), nhi = __shfl(c, hi, 64);
-      const float slo = __shfl(vs, lo, 64), shi = __shfl(vs, hi, 64);
-      const float mlo = __shfl(vm, lo, 64), mhi = __shfl(vm, hi, 64);
-      const bool right = c & 1;
-      const int sib = c ^ 1;
-      float os = sib_s[l], om = sib_m[l];
-      bool sib_act = false;
-      if (right && below && nlo == sib) { os = slo; om = mlo; sib_act = true; }
-      if (!right && above && nhi == sib) { os = shi; om = mhi; sib_act = true; }
-      const float ps = right ? os + vs : vs + os;
-      const float pm = fminf(vm, om);
-      // the left sibling of an active pair carries on; the right one retires
-      if (right && sib_act) act = false;
-      c >>= 1;
-      vs = ps;
-      vm = pm;
-      if (act) {
-        sum[c] = vs;
-        mn[c] = vm;
+      for (int u = 0; u < kSibBatch; ++u) {
+        const int l = l0 + u;
+        if (l < levels && act) {
+          const int sb = (c0 >> l) ^ 1;
+          sib_s[u] = sum[sb];
+          sib_m[u] = mn[sb];
+        } else {
+          sib_s[u] = 0.f;
+          sib_m[u] = INFINITY;
+        }
+      }
+  #pragma unroll
+      for (int u = 0; u < kSibBatch; ++u) {
+        const int l = l0 + u;
+        if (l >= levels) break;                                 // uniform
+        const uint64_t am = __ballot(act);
+        // nearest active lanes below / above
+        const uint64_t below = am & ((1ull << lane) - 1ull);
+        const uint64_t above = lane < 63 ? am & ~((2ull << lane) - 1ull) : 0ull;
+        const int lo = below ? 63 - __clzll((long long)below) : lane;
+        const int hi = above ? __ffsll((long long)above) - 1 : lane;
+        const int nlo = __shfl(c, lo, 64), nhi = __shfl(c, hi, 64);
+        const float slo = __shfl(vs, lo, 64), shi = __shfl(vs, hi, 64);
+        const float mlo = __shfl(vm, lo, 64), mhi = __shfl(vm, hi, 64);
+        const bool right = c & 1;
+        const int sib = c ^ 1;
+        float os = sib_s[u], om = sib_m[u];
+        bool sib_act = false;
+        if (right && below && nlo == sib) { os = slo; om = mlo; sib_act = true; }
+        if (!right && above && nhi == sib) { os = shi; om = mhi; sib_act = true; }
+        const float ps = right ? os + vs : vs + os;
+        const float pm = fminf(vm, om);
+        // the left sibling of an active pair carries on; the right one retires
+        if (right && sib_act) act = false;
+        c >>= 1;
+        vs = ps;
+        vm = pm;
+        if (act) {
+          sum[c] = vs;
+          mn[c] = vm;
+        }
       }
     }
   }

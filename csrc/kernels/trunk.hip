@@ -16,6 +16,7 @@
 //   stage 3  conv3: 49 x 64 x 576, A from act2 -> global x3 (the fc input)
 // x1 / x2 are also written to global (the backward's ReLU masks / wgrad inputs).
 // Everything is v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+#include <stdlib.h>
 #include "common.h"
 #include "fused_util.h"
 #include "sample_dev.h"
@@ -29,24 +30,45 @@ constexpr int O1 = 20, N1 = 32, K1 = 256, R1 = O1 * O1;       // conv1: 8x8/4
 constexpr int O2 = 9, N2 = 64, K2 = 512, R2 = O2 * O2;        // conv2: 4x4/2
 constexpr int O3 = 7, N3 = 64, K3 = 576, R3 = O3 * O3;        // conv3: 3x3/1
 constexpr int L1 = N1 + 8, L2 = N2 + 8;                       // padded LDS rows (elements)
+// Row split (gridDim.z == 2): part 0 computes conv3 rows 0-3, part 1 rows 4-6, each from its
+// own receptive field (conv2 rows 0-5 / 4-8, conv1 rows 0-13 / 8-19, input rows 0-59 / 32-83),
+// so one sample runs on two CUs (the learner's ~100 workgroups leave most of the 256 CUs idle;
+// the halo costs ~30% extra conv1 work per sample, not latency). Row starts / counts per part:
+constexpr int kIn0[2] = {0, 32}, kInN[2] = {60, 52};
+constexpr int kC10[2] = {0, 8}, kC1N[2] = {14, 12}, kC1Own[2] = {0, 10}, kC1OwnE[2] = {10, 20};
+constexpr int kC20[2] = {0, 4}, kC2N[2] = {6, 5}, kC2Own[2] = {0, 5}, kC2OwnE[2] = {5, 9};
+constexpr int kC30[2] = {0, 4}, kC3N[2] = {4, 3};
+constexpr int kInMax = 60, kC1Max = 14, kC2Max = 6;
 }  // namespace trunk
 
 __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   using namespace trunk;
-  // xin: the sample as bf16 NHWC [84*84][4] (converted once); dead after conv1, so
-  // act2 and the conv2/conv3 K-split partials live in the same bytes afterwards.
+  const int part = blockIdx.z, split = gridDim.z;               // split 1: whole image
+  const int in0 = split > 1 ? kIn0[part] : 0, inN = split > 1 ? kInN[part] : IH;
+  const int c10 = split > 1 ? kC10[part] : 0, c1n = split > 1 ? kC1N[part] : O1;
+  const int c1o = split > 1 ? kC1Own[part] - c10 : 0, c1e = split > 1 ? kC1OwnE[part] - c10 : O1;
+  const int c20 = split > 1 ? kC20[part] : 0, c2n = split > 1 ? kC2N[part] : O2;
+  const int c2o = split > 1 ? kC2Own[part] - c20 : 0, c2e = split > 1 ? kC2OwnE[part] - c20 : O2;
+  const int c30 = split > 1 ? kC30[part] : 0, c3n = split > 1 ? kC3N[part] : O3;
+  // xin: the sample's input rows as bf16 NHWC [rows*84][4] (converted once); dead after conv1,
+  // so act2 and the conv3 K-split partials live in the same bytes afterwards. Sized for the
+  // whole image (split 1); a part uses the first kInMax rows.
   __shared__ __attribute__((aligned(16))) in_t xin[HW * 4];
   __shared__ __attribute__((aligned(16))) act_t act1[R1 * L1];
+  // conv1's packed weights, loaded ONCE per block and handed to every wave through LDS (every
+  // wave needs all of them: direct per-wave loads moved 8 x 16 KB over the CU's ~30 B/clk L2 path)
+  __shared__ __attribute__((aligned(16))) bfx8 wl1[(K1 / 32) * 2 * 64];
   act_t* act2 = reinterpret_cast<act_t*>(xin);
   constexpr size_t kRedOff = (R2 * L2 * sizeof(act_t) + 255) / 256 * 256;   // conv3 k-half partials after act2
   float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(xin) + kRedOff);
   static_assert(kRedOff + 4 * 4 * 1024 <= sizeof(xin), "act2 + partials fit xin");
+  static_assert(kRedOff + 4 * 6 * 1024 <= sizeof(xin), "act2 + conv2 partials fit xin");
   static_assert(sizeof(SampleLds) <= sizeof(xin), "sampler scratch fits xin");
   const int b = blockIdx.x, inst = blockIdx.y;
   if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = lane & 15, kg = 8 * (lane >> 4);
-  int64_t* prof = a.prof != nullptr && tid == 0 ? a.prof + ((int64_t)inst * gridDim.x + b) * 16 : nullptr;
+  int64_t* prof = a.prof != nullptr && tid == 0 && part == 0 ? a.prof + ((int64_t)inst * gridDim.x + b) * 16 : nullptr;
 #define TRUNK_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
   TRUNK_MARK(0);
 
@@ -67,10 +89,10 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     const int32_t nx = a.smp.next_idx[tr];
     sl_s = inst == 0 ? st : make_int4(st.y, st.z, st.w, nx);
     if (tid == 0) {
-      if (inst == 0) write_sample_slots(a.smp, b, tr, st, nx);
+      if (inst == 0 && part == 0) write_sample_slots(a.smp, b, tr, st, nx);
       // relaxed ticket (as optim.hip): every workgroup read the counter before its add
       const int t = __hip_atomic_fetch_add(a.smp.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == a.smp.B * a.smp.ninst - 1) {
+      if (t == a.smp.B * a.smp.ninst * split - 1) {
         a.smp.rng[1] = (int64_t)(ctr + 1);
         __hip_atomic_store(a.smp.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -78,49 +100,59 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   }
 
   // ---------------------------------------------------------------- input loads (first)
-  // 1764 tasks of 4 pixels; a thread owns tasks tid + 512 j (j < 4)
+  // inN*21 tasks of 4 pixels (rows in0 .. in0+inN-1); a thread owns tasks tid + 512 j (j < 4)
   constexpr int NT = HW / 4;
+  const int nt_in = inN * (IW / 4), t_in0 = in0 * (IW / 4);
   uint32_t in[4][4];
   const bool slot_path = sampled || a.slots[inst] != nullptr;
   if (slot_path) {
-    const int4 sl = sampled ? sl_s : reinterpret_cast<const int4*>(a.slots[inst])[b];
-    const uint32_t* f0 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW);
-    const uint32_t* f1 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW);
-    const uint32_t* f2 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.z * HW);
-    const uint32_t* f3 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.w * HW);
+    // (component-wise select: a select between the register int4 and a loaded one put the
+    // sampled slots in scratch memory)
+    int4 sl = sl_s;
+    if (!sampled) {
+      const int4 v = reinterpret_cast<const int4*>(a.slots[inst])[b];
+      sl.x = v.x; sl.y = v.y; sl.z = v.z; sl.w = v.w;
+    }
+    const uint32_t* f0 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW) + t_in0;
+    const uint32_t* f1 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW) + t_in0;
+    const uint32_t* f2 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.z * HW) + t_in0;
+    const uint32_t* f3 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.w * HW) + t_in0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int t = tid + 512 * j;
-      if (t < NT) { in[j][0] = f0[t]; in[j][1] = f1[t]; in[j][2] = f2[t]; in[j][3] = f3[t]; }
+      if (t < nt_in) { in[j][0] = f0[t]; in[j][1] = f1[t]; in[j][2] = f2[t]; in[j][3] = f3[t]; }
     }
   } else {
-    const uint4* src = reinterpret_cast<const uint4*>(a.states[inst] + (int64_t)b * HW * 4);
+    const uint4* src = reinterpret_cast<const uint4*>(a.states[inst] + (int64_t)b * HW * 4) + t_in0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int t = tid + 512 * j;
-      if (t < NT) { const uint4 v = src[t]; in[j][0] = v.x; in[j][1] = v.y; in[j][2] = v.z; in[j][3] = v.w; }
+      if (t < nt_in) { const uint4 v = src[t]; in[j][0] = v.x; in[j][1] = v.y; in[j][2] = v.z; in[j][3] = v.w; }
     }
   }
+  static_assert(NT <= 4 * 512, "4 tasks per thread cover the image");
 
-  // Weight fragments (L2-resident packed bf16), held in VGPRs:
-  //   conv1 - every wave both n-tiles, all K (A fragments are read once per m-tile)
-  //   conv2 - wave owns n-tile (wave & 3), all K, m-tiles {wave>>2, +2, +4}
+  // Weight fragments (L2-resident packed bf16), each read from L2 by ONE wave of the block
+  // (the CU's L2 path, ~30 B/clk, is this kernel's bound; the input image is 28 KB):
+  //   conv1 - every wave both n-tiles, all K: the block loads the 16 KB once (2 fragments per
+  //           thread) and every wave takes its registers from LDS (wl1)
+  //   conv2 - wave owns n-tile (wave & 3) and k-half (wave >> 2), all m-tiles; the k-halves'
+  //           partial sums meet in LDS
   //   conv3 - wave owns n-tile (wave & 3) and k-half (wave >> 2); loaded after conv1
   //           into the registers conv1 no longer needs.
   const int nq = wave & 3, hi = wave >> 2;
-  bfx8 w1r[2][K1 / 32], w2r[K2 / 32];
+  bfx8 w1r[2][K1 / 32], w2r[K2 / 64];
   const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
+  bfx8 w1s[2];
   {
     const bfx8* W1 = reinterpret_cast<const bfx8*>(a.w1[inst]);
     const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
+    w1s[0] = W1[tid];
+    w1s[1] = W1[tid + 512];
 #pragma unroll
-    for (int ks = 0; ks < K1 / 32; ++ks) {
-      w1r[0][ks] = W1[(ks * 2 + 0) * 64 + lane];
-      w1r[1][ks] = W1[(ks * 2 + 1) * 64 + lane];
-    }
-#pragma unroll
-    for (int ks = 0; ks < K2 / 32; ++ks) w2r[ks] = W2[(ks * 4 + nq) * 64 + lane];
+    for (int j = 0; j < K2 / 64; ++j) w2r[j] = W2[((hi * (K2 / 64) + j) * 4 + nq) * 64 + lane];
   }
+  static_assert((K1 / 32) * 2 * 64 == 2 * 512, "two conv1 fragments per thread");
   // The MFMAs below run transposed (weights as the A operand): lane l then holds 4
   // consecutive output channels 4*(l>>4)..+3 of pixel (l & 15) -> one 8-byte store.
   const int cq = 4 * (lane >> 4);
@@ -134,13 +166,13 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int t = tid + 512 * j;
-      if (t < NT) planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], xin + 16 * t);
+      if (t < nt_in) planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], xin + 16 * t);
     }
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int t = tid + 512 * j;
-      if (t < NT) {   // NHWC word q = pixel 4t+q's 4 channels: transpose to planes then convert
+      if (t < nt_in) {   // NHWC word q = pixel 4t+q's 4 channels: transpose to planes then convert
         uint32_t c[4];
 #pragma unroll
         for (int ch = 0; ch < 4; ++ch)
@@ -150,24 +182,33 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       }
     }
   }
+  wl1[tid] = w1s[0];
+  wl1[tid + 512] = w1s[1];
   __syncthreads();
+#pragma unroll
+  for (int ks = 0; ks < K1 / 32; ++ks) {
+    w1r[0][ks] = wl1[(ks * 2 + 0) * 64 + lane];
+    w1r[1][ks] = wl1[(ks * 2 + 1) * 64 + lane];
+  }
   TRUNK_MARK(1);
 
   // ---------------------------------------------------------------- conv1 -> act1 (+x1)
-  // Every wave computes both n-tiles of its m-tiles (one LDS read per A fragment).
+  // Every wave computes both n-tiles of its m-tiles (one LDS read per A fragment). Positions
+  // are local to the part (row 0 = conv1 row c10; its input row 0 = image row 4 * c10 = in0).
   {
     const float scale = a.scale;
     const int kw = kg >> 2;                               // 0, 2, 4, 6: pixel pair of this lane
-    act_t* x1 = a.x1[inst] != nullptr ? a.x1[inst] + (int64_t)b * R1 * N1 : nullptr;
+    const int np1 = c1n * O1;
+    act_t* x1 = a.x1[inst] != nullptr ? a.x1[inst] + (int64_t)b * R1 * N1 + c10 * O1 * N1 : nullptr;
     auto load1 = [&](bfx8* f, int mt) {
-      const int p = mt * 16 + row, oy = p / O1, ox = p - oy * O1;
+      const int p = min(mt * 16 + row, np1 - 1), oy = p / O1, ox = p - oy * O1;   // (tail rows clamped)
       const in_t* base = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
 #pragma unroll
       for (int ks = 0; ks < K1 / 32; ++ks) f[ks] = ld_in8(base + ks * IW * 4);
     };
-    constexpr int MT = R1 / 16, ITER = (MT + 7) / 8;      // 25 m-tiles (no tail) over 8 waves
+    const int MT = (np1 + 15) / 16;                       // 25 m-tiles whole, 18 / 15 per part
 #pragma unroll
-    for (int i = 0; i < ITER; ++i) {
+    for (int i = 0; i < (R1 / 16 + 7) / 8; ++i) {
       const int mt = wave + 8 * i;
       if (mt >= MT) break;                                // wave-uniform
       bfx8 fa[K1 / 32];                                   // (single-buffered: VGPR budget)
@@ -179,12 +220,15 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
         c1 = tmfma(w1r[1][ks], fa[ks], c1);
       }
       const int p = mt * 16 + row;
-      const pk4_t v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
-      *reinterpret_cast<pk4_t*>(act1 + p * L1 + cq) = v0;
-      *reinterpret_cast<pk4_t*>(act1 + p * L1 + 16 + cq) = v1;
-      if (x1 != nullptr) {   // conv2 wgrad input + ReLU mask of the backward
-        *reinterpret_cast<pk4_t*>(x1 + p * N1 + cq) = v0;
-        *reinterpret_cast<pk4_t*>(x1 + p * N1 + 16 + cq) = v1;
+      if (p < np1) {
+        const pk4_t v0 = pack4(c0 * scale + f4(bias1a)), v1 = pack4(c1 * scale + f4(bias1b));
+        *reinterpret_cast<pk4_t*>(act1 + p * L1 + cq) = v0;
+        *reinterpret_cast<pk4_t*>(act1 + p * L1 + 16 + cq) = v1;
+        const int oy = p / O1;
+        if (x1 != nullptr && oy >= c1o && oy < c1e) {   // conv2 wgrad input + ReLU mask (owned rows)
+          *reinterpret_cast<pk4_t*>(x1 + p * N1 + cq) = v0;
+          *reinterpret_cast<pk4_t*>(x1 + p * N1 + 16 + cq) = v1;
+        }
       }
     }
   }
@@ -196,32 +240,53 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   TRUNK_MARK(2);
   // ---------------------------------------------------------------- conv2 -> act2 (+x2)
   {
-    constexpr int KS = K2 / 32;                           // 16 k-steps
-    act_t* x2 = a.x2[inst] != nullptr ? a.x2[inst] + (int64_t)b * R2 * N2 : nullptr;
+    constexpr int KH = K2 / 64;                           // 8 k-steps (taps) per k-half
+    constexpr int MTX = (R2 + 15) / 16;                   // 6 m-tiles whole (4 / 3 per part)
+    const int np2 = c2n * O2, MT = (np2 + 15) / 16;
+    float* red2 = red;                                    // xin is dead: k-half partials after act2
     auto load2 = [&](bfx8* f, int mt) {
       const int p = mt * 16 + row;
-      const bool ok = p < R2;
+      const bool ok = p < np2;
       const int oy = ok ? p / O2 : 0, ox = ok ? p - oy * O2 : 0;
       const act_t* base = act1 + ((oy * 2) * O1 + ox * 2) * L1 + kg;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {                   // k = (kh*4 + kw)*32 + ci, tap = ks
-        const int kh = ks >> 2, kw = ks & 3;
-        f[ks] = ok ? *reinterpret_cast<const bfx8*>(base + (kh * O1 + kw) * L1) : tz8();
+      for (int j = 0; j < KH; ++j) {                      // k = (kh*4 + kw)*32 + ci, tap = 8 hi + j
+        const int tap = hi * KH + j, kh = tap >> 2, kw = tap & 3;
+        f[j] = ok ? *reinterpret_cast<const bfx8*>(base + (kh * O1 + kw) * L1) : tz8();
       }
     };
+    f32x4 acc2[MTX];
+    bfx8 fa[2][KH];
+    load2(fa[0], 0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {                         // m-tiles hi, hi+2, hi+4 (6 = ceil(81/16))
-      const int mt = hi + 2 * i;
-      bfx8 fa[KS];
-      load2(fa, mt);
-      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MTX; ++mt) {
+      if (mt >= MT) break;                                // block-uniform
+      if (mt + 1 < MT) load2(fa[(mt + 1) & 1], mt + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) c = tmfma(w2r[ks], fa[ks], c);
-      const int p = mt * 16 + row;
-      if (p < R2) {
-        const pk4_t v = pack4(c + f4(bias2));
-        *reinterpret_cast<pk4_t*>(act2 + p * L2 + nq * 16 + cq) = v;
-        if (x2 != nullptr) *reinterpret_cast<pk4_t*>(x2 + p * N2 + nq * 16 + cq) = v;
+      for (int j = 0; j < KH; ++j) acc2[mt] = tmfma(w2r[j], fa[mt & 1][j], acc2[mt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (hi == 1) {
+#pragma unroll
+      for (int mt = 0; mt < MTX; ++mt)
+        if (mt < MT) park(red2, nq * MTX + mt, lane, acc2[mt]);
+    }
+    __syncthreads();
+    if (hi == 0) {
+      act_t* x2 = a.x2[inst] != nullptr ? a.x2[inst] + (int64_t)b * R2 * N2 + c20 * O2 * N2 : nullptr;
+#pragma unroll
+      for (int mt = 0; mt < MTX; ++mt) {
+        if (mt >= MT) break;
+        const f32x4 c = unpark(red2, nq * MTX + mt, lane, acc2[mt]);
+        const int p = mt * 16 + row;
+        if (p < np2) {
+          const pk4_t v = pack4(c + f4(bias2));
+          *reinterpret_cast<pk4_t*>(act2 + p * L2 + nq * 16 + cq) = v;
+          const int oy = p / O2;
+          if (x2 != nullptr && oy >= c2o && oy < c2e) *reinterpret_cast<pk4_t*>(x2 + p * N2 + nq * 16 + cq) = v;
+        }
       }
     }
   }
@@ -229,11 +294,12 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   TRUNK_MARK(6);
   // ---------------------------------------------------------------- conv3 -> x3 (global)
   {
-    constexpr int MT = (R3 + 15) / 16;                    // 4 m-tiles
+    constexpr int MT = (R3 + 15) / 16;                    // 4 m-tiles whole (2 per part)
     constexpr int KJ = K3 / 64;                           // 9 k-steps per k-half
+    const int np3 = c3n * O3, mtn = (np3 + 15) / 16;
     auto load3 = [&](bfx8* f, int mt) {
       const int p = mt * 16 + row;
-      const bool ok = p < R3;
+      const bool ok = p < np3;
       const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
       const act_t* base = act2 + (oy * O2 + ox) * L2 + kg;
 #pragma unroll
@@ -247,7 +313,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     load3(fa[0], 0);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      if (mt + 1 < MT) load3(fa[(mt + 1) & 1], mt + 1);
+      if (mt >= mtn) break;                               // block-uniform
+      if (mt + 1 < mtn) load3(fa[(mt + 1) & 1], mt + 1);
       __builtin_amdgcn_sched_barrier(0);
       acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -258,17 +325,19 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     // k-half exchange: hi waves park fp32 partials in the (dead) input region
     if (hi == 1) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) park(red, nq * MT + mt, lane, acc[mt]);
+      for (int mt = 0; mt < MT; ++mt)
+        if (mt < mtn) park(red, nq * MT + mt, lane, acc[mt]);
     }
     __syncthreads();
     TRUNK_MARK(9);
     if (hi == 0) {
-      act_t* x3 = a.x3[inst] + (int64_t)b * R3 * N3;
+      act_t* x3 = a.x3[inst] + (int64_t)b * R3 * N3 + c30 * O3 * N3;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
+        if (mt >= mtn) break;
         const f32x4 v = unpark(red, nq * MT + mt, lane, acc[mt]);
         const int p = mt * 16 + row;
-        if (p < R3) *reinterpret_cast<pk4_t*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
+        if (p < np3) *reinterpret_cast<pk4_t*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
       }
     }
   }
@@ -281,5 +350,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
 using namespace dqn;
 
 void launch_trunk_fwd(const TrunkArgs& a, int B, int ninst, hipStream_t st) {
-  hipLaunchKernelGGL(trunk_fwd_kernel, dim3(B, ninst), dim3(512), 0, st, a);
+  // row split whenever the per-sample grid leaves CUs idle (the learner's 3-4 x 32 samples)
+  static const int force = getenv("DQN_TRUNK_SPLIT") ? atoi(getenv("DQN_TRUNK_SPLIT")) : -1;
+  const int split = force >= 1 ? (force > 1 ? 2 : 1) : (B * ninst <= 192 ? 2 : 1);
+  hipLaunchKernelGGL(trunk_fwd_kernel, dim3(B, ninst, split), dim3(512), 0, st, a);
 }

@@ -32,6 +32,18 @@ for B, ninst in ((4, 1), (32, 2), (32, 3), (256, 1)):
     t = ex.trunk_prof.view(-1, 16)[:, [0, 1, 2, 6, 8, 9, 10]].double()
     d = (t[:, 1:] - t[:, :-1]).mean(0).tolist()
     names = ['stage', 'conv1', 'conv2', 'c3mma', 'c3park', 'c3fin']
-    print('B=%d ninst=%d  trunk+fc %.2f us/call | block cycles %.0f: %s' % (
-        B, ninst, st.elapsed_time(en) * 1e3 / 50, sum(d), ' '.join('%s %.0f' % kv for kv in zip(names, d))))
+    # per-XCD clocks are not synchronised: workgroup w runs on XCD w % 8 (part 0 only is stamped,
+    # linear id b + inst * B); span / start skew are taken within each XCD, then the max
+    xcd = torch.arange(t.shape[0], device=t.device) % 8
+    span, skew = 0.0, []
+    for x in range(8):
+        tx = t[xcd == x]
+        if tx.shape[0] == 0:
+            continue
+        span = max(span, float((tx[:, -1] - tx[:, 0].min()).max()))
+        skew.append(tx[:, 0] - tx[:, 0].min())
+    s0 = torch.cat(skew)
+    print('B=%d ninst=%d  trunk+fc %.2f us/call | block cycles %.0f: %s | span %.0f, start offsets p50 %.0f max %.0f'
+          % (B, ninst, st.elapsed_time(en) * 1e3 / 50, sum(d), ' '.join('%s %.0f' % kv for kv in zip(names, d)),
+             span, float(s0.median()), float(s0.max())))
 ex.trunk_prof = None
