@@ -443,6 +443,73 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   }
 }
 
+// ===================================================== stride-2 dgrad by parity
+// dX[b][iy][ix][ci] = sum_{kh,kw,co} dZ[b][(iy-kh)/2][(ix-kw)/2][co] W[kh][kw][ci][co] of a
+// VALID stride-2 conv: only the taps with kh = iy mod 2 (+2), kw = ix mod 2 (+2) reach a given
+// input pixel, so the implicit GEMM over all KH*KW taps (DgradLoader) multiplies 3 of every 4
+// A fragments by zero. Here the input pixels are grouped by parity class (iy & 1, ix & 1): a
+// class's rows share ONE 2x2 tap subset, K shrinks to (KH/2)(KW/2)*COUT (256 for Nature conv2,
+// 8 k-steps instead of 32) and every fragment is a real one. Block = 16 rows of one class x all
+// N (2 n-tiles) x the class's K in two halves (4 waves); the epilogue scatters the rows back
+// to NHWC with the ReLU mask of the layer input.
+template <int COUT, int KH, int KW>
+__global__ void __launch_bounds__(256) dgrad_s2_kernel(ConvArgs a) {
+  static_assert(KH % 2 == 0 && KW % 2 == 0 && COUT % 32 == 0, "2x2 tap classes, 32-deep k-steps");
+  constexpr int CK = COUT / 32;                            // k-steps per tap
+  constexpr int KSC = (KH / 2) * (KW / 2) * CK;            // the class's k-steps (8)
+  constexpr int KHALF = KSC / 2;
+  const int inst = blockIdx.z;
+  const int PH = a.IH / 2, PW = a.IW / 2, crow = PH * PW, cmt = (crow + 15) / 16;
+  int blk = blockIdx.x;
+  const int mt = blk % cmt;
+  blk /= cmt;
+  const int cls = blk & 3, b = blk >> 2, cy = cls >> 1, cx = cls & 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nt = wave & 1, kh2 = wave >> 1;                // n-tile, k-half
+  const int kg = 8 * (lane >> 4);
+  const int r = mt * 16 + (lane & 15);                     // this lane's A row within the class
+  const bool rok = r < crow;
+  const int py = rok ? r / PW : 0, px = rok ? r - py * PW : 0;
+  const act_t* dz = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)b * a.OH * a.OW * COUT;
+  const bfx8* __restrict__ Bp = reinterpret_cast<const bfx8*>(a.w[inst]);
+  const act_t* __restrict__ msrc = reinterpret_cast<const act_t*>(a.mask[inst]);
+  // epilogue mask operand first (its latency hides under the k-loop): rows 4 (lane >> 4) + i
+  float mk[4];
+  int64_t orow[4];
+  const int n = nt * 16 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = mt * 16 + 4 * (lane >> 4) + i;
+    const int q = rr < crow ? rr : 0, qy = q / PW, qx = q - qy * PW;
+    orow[i] = rr < crow ? ((int64_t)(b * a.IH + 2 * qy + cy) * a.IW + 2 * qx + cx) : -1;
+    mk[i] = kh2 == 0 && orow[i] >= 0 && n < a.N ? (float)msrc[orow[i] * a.ldo + n] : 0.f;
+  }
+  bfx8 af[KHALF], bf[KHALF];
+#pragma unroll
+  for (int u = 0; u < KHALF; ++u) {
+    const int sidx = kh2 * KHALF + u, t = sidx / CK, h = sidx - t * CK;
+    const int dh = t / (KW / 2), dw = t - dh * (KW / 2);
+    const int kh = cy + 2 * dh, kw = cx + 2 * dw;
+    const int oy = py - dh, ox = px - dw;
+    const bool ok = rok && oy >= 0 && ox >= 0 && oy < a.OH && ox < a.OW;
+    af[u] = ok ? *reinterpret_cast<const bfx8*>(dz + ((int64_t)oy * a.OW + ox) * COUT + h * 32 + kg) : zero8();
+    const int ks = (kh * KW + kw) * CK + h;                // packed dgrad k-step of (tap, co-half)
+    bf[u] = Bp[((int64_t)ks * a.N16 + nt) * 64 + lane];
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < KHALF; ++u) acc = mfma16(af[u], bf[u], acc);
+  __shared__ f32x4 red[2][64];
+  if (kh2 == 1) red[nt][lane] = acc;
+  __syncthreads();
+  if (kh2 == 1 || n >= a.N) return;
+  acc += red[nt][lane];
+  act_t* out = reinterpret_cast<act_t*>(a.out[inst]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (orow[i] >= 0) out[orow[i] * a.ldo + n] = (act_t)(mk[i] > 0.f ? acc[i] : 0.f);
+}
+
 // ================================================================ weight grad
 // dW[k][n] (+)= scale * sum_{m in chunk} A[m][k] * dZ[m][n];  db[n] (+)= sum_m dZ[m][n]
 // grid: x = M-chunk (MC rows), y = K-range (KB), z = N-range (NB). ONE staging
@@ -980,6 +1047,7 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case 200 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 4, 2, 4); return 0;
     case 100 + L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 4, 2, 1, 2, 2, 9); return 0;
     case 100 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 1, 1, 4, 2, 8); return 0;         // 16 rows, split-K 4
+    case 200 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;         // all 16 taps (pre-parity)
     default: break;
   }
   switch (kind) {
@@ -995,7 +1063,16 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     // ---- backward data, ReLU mask of the layer input
     case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 2, 2, 8); return 0;   // K 512-1024
     case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 2, 1, 2, 2, 2, 9); return 0;     // 18 k-steps, 16 x 64 blocks
-    case L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;     // 32 k-steps
+    case L_NAT_CONV2_DGRAD:
+      // parity-class dgrad (8 k-steps of real taps instead of 32 with 3/4 zeros); the generic
+      // igemm path stays as DQN_TILES="8:2" (A/B) and for shapes the class kernel does not cover
+      if (a.N16 == 2 && a.IH % 2 == 0 && a.IW % 2 == 0 && a.pad_t == 0 && a.pad_l == 0 && a.zero_ptr == nullptr &&
+          a.nz_out0 == nullptr && a.loss_parts == nullptr && 2 * a.OH + 2 == a.IH && 2 * a.OW + 2 == a.IW) {
+        const int cmt = ((a.IH / 2) * (a.IW / 2) + 15) / 16, B = a.M / (a.IH * a.IW);
+        hipLaunchKernelGGL((dgrad_s2_kernel<64, 4, 4>), dim3(B * 4 * cmt, 1, ninst), dim3(256), 0, st, a);
+        return 0;
+      }
+      IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;     // 32 k-steps
     default: return -1;
   }
 }
@@ -1030,34 +1107,38 @@ DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, 
   wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
 }
 
-#ifndef DQN_GRP_CONV_MC
-#define DQN_GRP_CONV_MC 128
-#endif
-// conv members' M-chunk: 128 rows keeps every block's LDS at <= 40 KB (4 blocks / CU), so the
-// whole grouped grid is resident at once (256-row chunks: 80 KB, 2 blocks / CU, a tail round)
-constexpr int kGrpConvMC = DQN_GRP_CONV_MC;
+// conv members' M-chunk: 128 rows (kind as is) keeps a block's LDS at <= 40 KB (4 blocks / CU);
+// 256 rows (kind | kGrpMC256: 80 KB, 2 blocks / CU, half the blocks and atomic partials) is the
+// launcher's other choice (DQN_WGRAD_MC=128|256, default chosen per group size)
+constexpr int kGrpMC256 = 0x40;
+#define GRP_CONV_CASES(OFF, MC)                                                                                    \
+  case L_NAT_CONV1_FWD + OFF: group_member<NatC1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
+  case L_NAT_CONV1_FRAMES + OFF: group_member<NatF1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break; \
+  case L_NAT_CONV2_FWD + OFF: group_member<NatC2, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
+  case L_NAT_CONV3_FWD + OFF: group_member<NatC3, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
 __global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
   extern __shared__ __attribute__((aligned(16))) act_t glds[];
   int b = blockIdx.x, i = 0;
   while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
   switch (G.kind[i]) {
-    // 256-row M-chunks, K split over blocks: 2-4x fewer fp32 atomic partials than 128-row chunks
-    case L_NAT_CONV1_FWD: group_member<NatC1, kGrpConvMC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV1_FRAMES: group_member<NatF1, kGrpConvMC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV2_FWD: group_member<NatC2, kGrpConvMC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-    case L_NAT_CONV3_FWD: group_member<NatC3, kGrpConvMC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
+    GRP_CONV_CASES(0, 128)
+    GRP_CONV_CASES(kGrpMC256, 256)
     case L_DENSE_FWD_RELU: group_member<DenseLoader, 32, 64, 128>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     case L_HEAD_WGRAD: group_member<DenseLoader, 32, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
     default: break;
   }
 }
+#undef GRP_CONV_CASES
 }  // namespace dqn
 
 static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
   switch (kind) {
-    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = kGrpConvMC; KB = 64; NB = 32; break;
-    case L_NAT_CONV2_FWD: MC = kGrpConvMC; KB = 64; NB = 64; break;
-    case L_NAT_CONV3_FWD: MC = kGrpConvMC; KB = 64; NB = 64; break;
+    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = 128; KB = 64; NB = 32; break;
+    case L_NAT_CONV2_FWD: MC = 128; KB = 64; NB = 64; break;
+    case L_NAT_CONV3_FWD: MC = 128; KB = 64; NB = 64; break;
+    case L_NAT_CONV1_FWD + kGrpMC256: case L_NAT_CONV1_FRAMES + kGrpMC256: MC = 256; KB = 64; NB = 32; break;
+    case L_NAT_CONV2_FWD + kGrpMC256: MC = 256; KB = 64; NB = 64; break;
+    case L_NAT_CONV3_FWD + kGrpMC256: MC = 256; KB = 64; NB = 64; break;
     case L_DENSE_FWD_RELU: MC = 32; KB = 64; NB = 128; break;
     case L_HEAD_WGRAD: MC = 32; KB = 64; NB = 64; break;
     default: return false;
@@ -1073,6 +1154,16 @@ static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
 int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   int total = 0;
   size_t lds = 0;
+  // conv M-chunk: 256 rows once the dense members alone fill the CUs' block slots (Rainbow's
+  // two 3136 x 512 noisy fc layers), else 128 (flagship: the whole grid resident at once)
+  static const int mc_env = getenv("DQN_WGRAD_MC") ? atoi(getenv("DQN_WGRAD_MC")) : 0;
+  int dense_blocks = 0;
+  for (int i = 0; i < G.n; ++i)
+    if (G.kind[i] == L_DENSE_FWD_RELU) dense_blocks += ((G.a[i].K + 63) / 64) * ((G.g[i].N + 127) / 128);
+  const bool mc256 = mc_env == 256 || (mc_env == 0 && dense_blocks > 256);
+  for (int i = 0; i < G.n; ++i)
+    if (mc256 && G.kind[i] >= L_NAT_CONV1_FWD && G.kind[i] <= L_NAT_CONV3_FWD) G.kind[i] += kGrpMC256;
+    else if (mc256 && G.kind[i] == L_NAT_CONV1_FRAMES) G.kind[i] += kGrpMC256;
   for (int i = 0; i < G.n; ++i) {
     int MC, KB, NB;
     size_t l;

@@ -50,8 +50,10 @@ class Learner:
         self.weights = torch.ones(B, dtype=torch.float32, device=self.device)
         self.prio = torch.zeros(B, dtype=torch.float32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
-        self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb, config.allreduce,
-                                      config.allreduce_dtype)
+        # (an async-PS worker all-reduces nothing: no xgmi transport and no start-up probe, whose
+        # collectives the parameter server rank -- inside serve() -- would never join)
+        self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb,
+                                      'rccl' if ps_client is not None else config.allreduce, config.allreduce_dtype)
         self.tau = min(1.0, float(config.target_update_tau))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:

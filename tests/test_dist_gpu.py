@@ -207,3 +207,59 @@ def test_bench_two_ranks_replicas_equal(tmp_path):
     assert d['n_gpus'] == 2 and d['config']['world_size'] == 2
     assert d['config']['replicas_equal'] is True and d['config']['replicas_diverged'] == []
     assert d['config']['dist_backend'] == 'gloo'
+
+
+def _worker_async_ps(rank, world, port, errq):
+    """--async_ps on the GPU: rank 0 is the parameter server (HIP fused optimizer on its HBM
+    copy), ranks 1..world-1 run the HIP Nature-CNN learner against it (push gradient, pull
+    parameters + int64 global_step). Three ranks share cuda:0 over gloo p2p."""
+    try:
+        _setup(rank, world, port)
+        from dist_dqn_amd.config import preset
+        from dist_dqn_amd.learner import Learner
+        from dist_dqn_amd.models.network import Network
+        from dist_dqn_amd.parallel import broadcast_state, init_distributed
+        from dist_dqn_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
+        from dist_dqn_amd.replay import DeviceReplay
+        cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=5 --backend=hip --replay_memory_capacity=2048 '
+                     '--async_ps --target_update_freq=3')
+        ctx = init_distributed(cfg, device='cuda')
+        net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
+        assert net.executor.name.startswith('hip'), net.executor.name
+        broadcast_state(ctx, net)
+        init = net.online.flat.clone()
+        steps = 5
+        if rank == 0:
+            srv = AsyncPSServer(ctx, net)
+            n = srv.serve()
+            torch.cuda.synchronize()
+            assert n == steps * (world - 1) and srv.per_worker == {w: steps for w in range(1, world)}
+            assert int(net.global_step) == n
+            assert torch.isfinite(net.online.flat).all()
+            assert not torch.equal(net.online.flat, init), 'the PS applied no update'
+        else:
+            rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
+            rep.fill_synthetic(2048, 6, seed=rank)
+            ps = AsyncPSClient(ctx, net.online.flat)
+            ps.pull(net.online.flat, net.global_step)
+            net.refresh_packed()
+            ln = Learner(net, rep, cfg, ctx, ps_client=ps)
+            seen = []
+            for _ in range(steps):
+                ln.step()
+                seen.append(int(net.global_step))
+            torch.cuda.synchronize()
+            assert torch.isfinite(ln.loss).all()
+            assert ps.pushes == steps
+            assert seen == sorted(seen) and len(set(seen)) == steps, seen    # the PS step only moves forward
+            ps.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 - report to the parent
+        import traceback
+        errq.put('rank %d: %s\n%s' % (rank, e, traceback.format_exc()))
+        raise
+
+
+def test_async_ps_hip_learners_one_gpu():
+    _run_ranks(_worker_async_ps, (), world=3, timeout=150)
