@@ -223,8 +223,8 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   }
   PerStep per{};
   if (!per_p.empty()) {
-    TORCH_CHECK(op >= 0 && sample.empty() && per_p.size() == 25 && per_f.size() == 4,
-                "optim_pack per: 25 ints + 4 floats (update calls only, not with a uniform sample)");
+    TORCH_CHECK(op >= 0 && sample.empty() && (per_p.size() == 25 || per_p.size() == 28) && per_f.size() == 4,
+                "optim_pack per: 25 (+3 insertion) ints + 4 floats (update calls only, not with a uniform sample)");
     for (int i : {0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23})
       TORCH_CHECK(per_p[i] != 0, "optim_pack per: null pointer ", i);
     per.sum = P<float*>(per_p[0]); per.mn = P<float*>(per_p[1]); per.maxp = P<float*>(per_p[2]);
@@ -237,11 +237,19 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                        P<int32_t*>(per_p[18]), P<float*>(per_p[19]), P<float*>(per_p[20]), P<float*>(per_p[21]),
                        P<int32_t*>(per_p[22]), P<int32_t*>(per_p[23])};
     per.B = (int)per_p[24];
+    if (per_p.size() == 28) {        // [cursor, n new transitions, capacity]: fused acting's PER insertion
+      per.ins_cursor = P<const int64_t*>(per_p[25]);
+      per.ins_n = (int)per_p[26];
+      per.ins_cap = (int)per_p[27];
+      TORCH_CHECK(per.ins_cursor != nullptr && per.ins_n >= 0 && per.ins_cap >= 1 && per.ins_n <= per.ins_cap &&
+                      per.ins_cap <= per.P, "optim_pack per: bad insertion spec");
+    }
     per.alpha = (float)per_f[0]; per.eps = (float)per_f[1]; per.beta0 = (float)per_f[2];
     per.beta_steps = (float)per_f[3];
     TORCH_CHECK(per.B >= 1 && per.B <= 64 && per.P >= 2 && (per.P & (per.P - 1)) == 0 &&
                 (1 << per.levels) == per.P && per.levels <= 30 && per.beta_steps >= 1.f,
                 "optim_pack per: 1 <= B <= 64 (one-wave tree update), P = 2^levels, beta_steps >= 1");
+    TORCH_CHECK(per.B + per.ins_n <= 64, "optim_pack per: batch + inserted transitions <= 64 (one wave)");
   }
   const float* tnz = nullptr;
   float* tef = nullptr;

@@ -22,6 +22,9 @@ struct PerStep {
   int64_t* rng; const int32_t* size; const int64_t* step;          // next sample: rng, replay size, global_step
   float beta0, beta_steps;
   int32_t* idx_out; float* w_out; SampleOut so; int B;
+  // fused acting: the actors' ins_n new transitions (ring slots ending at the advanced
+  // cursor ins_cursor[0], capacity ins_cap) enter the tree at max priority in the same climb
+  const int64_t* ins_cursor; int ins_n, ins_cap;
 };
 void launch_replay_sample_uniform(const int32_t* size, int64_t* rng, int32_t* out, int B, const SampleOut& so,
                                   hipStream_t st);

@@ -226,8 +226,10 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     const int64_t step0 = per.step[0];                  // read before this block's ticket add
     const uint64_t seed = (uint64_t)per.rng[0], ctr = (uint64_t)per.rng[1];
     SumtreeLds& L = *reinterpret_cast<SumtreeLds*>(smem);
+    int ins_first = 0;
+    if (per.ins_n > 0) ins_first = (int)((per.ins_cursor[0] - per.ins_n + per.ins_cap) % per.ins_cap);
     sumtree_update_wave(per.sum, per.mn, per.maxp, per.upd_idx, per.upd_td, per.alpha, per.eps, 0, per.B, per.P,
-                        per.levels, L);
+                        per.levels, L, 0, 1, per.ins_n, ins_first, per.ins_cap);
     __syncthreads();                                    // tree writes visible to every lane of the block
     if ((int)threadIdx.x < per.B) {
       const float beta = fminf(1.f, per.beta0 + (1.f - per.beta0) * (float)(step0 + 1) / per.beta_steps);
@@ -316,22 +318,36 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         if constexpr (TWO_LD) ld(S1, so, bs);
       }
     }
+    // the target's mu / sigma in the same batch (one memory round trip per item: the extra
+    // VGPRs keep the same 2 blocks / CU, the block is 8 waves and the budget 128 VGPRs)
+    if (tmix) {
+      ld(tgt, mo, tw);
+      if constexpr (NZ) ld(tgt, so, tws);
+    }
     // factorised-noise factors: f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
     float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
+    float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};     // (tmix: the target's next sample)
     const bool hin = NZ && !elem && jb.ein_off >= 0;
     const int ki = NZ ? jb.ein_off + (hin && rowok ? k : 0) : 0;     // clamped: always in range
     if constexpr (NZ) {
       const float* gn = DG ? gnoise : noise;             // (DG: the sample the forward used)
       const float ni = noise[hin ? ki : 0], gi = DG ? gn[hin ? ki : 0] : 1.f;
-      float no[4], go[4];
+      float no[4], go[4], to[4] = {1.f, 1.f, 1.f, 1.f}, ti = 1.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int oi = jb.eout_off + (ok[j] ? n + j : 0);
         no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f;
+        if (tmix) to[j] = tnoise[oi];
       }
+      if (tmix) ti = tnoise[hin ? ki : 0];
       if (hin) { nin = fnz(ni); gin = fnz(gi); }
 #pragma unroll
       for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); }
+      if (tmix) {
+        if (hin) tin = fnz(ti);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tout[j] = fnz(to[j]);
+      }
     }
     // ---- update
     if constexpr (UPD) {
@@ -360,17 +376,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       if constexpr (NZ) e[j] = w[j] + ws[j] * nin * nout[j];
     }
     if (tmix) {
-      // the target's loads come AFTER this net's stores: their registers are the update's
-      // (fewer live registers: mode-7 items at 91 instead of 98 VGPRs)
-      ld(tgt, mo, tw);
-      if constexpr (NZ) ld(tgt, so, tws);
-      float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};
-      if constexpr (NZ) {
-        const float ti = tnoise[hin ? ki : 0];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tout[j] = fnz(tnoise[jb.eout_off + (ok[j] ? n + j : 0)]);
-        if (hin) tin = fnz(ti);
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float mu = sync ? w[j] : tw[j];

@@ -25,21 +25,30 @@ struct SumtreeLds {                 // LDS scratch of the one-wave update
 DQN_DEV void sumtree_update_wave(float* __restrict__ sum, float* __restrict__ mn, float* __restrict__ maxp,
                                  const int32_t* __restrict__ idx, const float* __restrict__ td, float alpha,
                                  float eps, int use_max, int n, int P, int levels, SumtreeLds& L, int first = 0,
-                                 int cap = 1) {
-  // idx == nullptr: the n consecutive ring slots (first + lane) % cap
+                                 int cap = 1, int n_ins = 0, int ins_first = 0, int ins_cap = 1) {
+  // idx == nullptr: the n consecutive ring slots (first + lane) % cap.
+  // n_ins > 0: lanes [0, n_ins) first insert the ring slots (ins_first + lane) % ins_cap at the
+  // running max priority (new transitions), then lanes [n_ins, n_ins + n) are the n entries
+  // above -- one climb, same result as the insertion followed by the update (a later batch
+  // position wins a shared leaf; the inserted lanes' p = max_p leaves the running max alone).
   const int lane = threadIdx.x;
   const bool w0 = threadIdx.x < 64;
-  const bool valid = lane < n;
+  const bool ins = lane < n_ins;
+  const int j = lane - n_ins;
+  const bool valid = lane < n_ins + n;
+  DQN_ASSERT(n_ins + n <= 64);
   const float mp = maxp[0];
   float p = 0.f;
-  if (valid) p = use_max ? mp : powf(fabsf(td[lane]) + eps, alpha);
+  if (valid) p = (ins || use_max) ? mp : powf(fabsf(td[j]) + eps, alpha);
   if (w0) {
     if (!use_max) {
       const float m = wave_max(valid ? p : 0.f);
       if (lane == 0) maxp[0] = fmaxf(mp, m);
     }
     // unique keys (the lane breaks ties); padding lanes sort last with leaf field 0xffffffff
-    const uint32_t li = idx != nullptr ? (uint32_t)idx[lane] : (uint32_t)((first + lane) % cap);
+    uint32_t li = 0;
+    if (ins) li = (uint32_t)((ins_first + lane) % ins_cap);
+    else if (valid) li = idx != nullptr ? (uint32_t)idx[j] : (uint32_t)((first + j) % cap);
     L.keys[lane] = ((uint64_t)(valid ? li : 0xffffffffu) << 6) | (uint64_t)lane;
   }
   __syncthreads();

@@ -70,10 +70,20 @@ class DeviceActor:
         return (self.steps == 1 and self.E <= min(64, batch_size) and getattr(ex, 'consumes_slots', False)
                 and hasattr(ex, 'supports_fused_acting') and ex.supports_fused_acting())
 
-    def fused_args(self) -> dict:
-        """Arguments of the fused acting step (executor.loss_and_grad(acting=...))."""
+    def fused_args(self, defer_per: bool = False) -> dict:
+        """Arguments of the fused acting step (executor.loss_and_grad(acting=...)).
+        defer_per (prioritized replay): the acting launch does not insert the new transitions
+        into the sum-tree; the learner's optimizer launch does (`per_insert_spec`)."""
         ptrs, ints, f = self._actor_args()
+        if defer_per:
+            ints = ints[:6]
         return {'stacks': self.stacks, 'ptrs': ptrs, 'ints': ints, 'f': f}
+
+    def per_insert_spec(self) -> list:
+        """[cursor ptr, E, capacity]: where this step's E new transitions end (the acting
+        launch advances cursor[0] past them) -- `DeviceReplay.next_sample_spec(insert=...)`."""
+        r = self.replay
+        return [r.cursor.data_ptr(), self.E, r.capacity]
 
     def _one(self):
         r = self.replay

@@ -81,6 +81,7 @@ class Learner:
                                 and getattr(config, 'disable_target_replication', False))
         self._host_step = int(network.global_step) if self._own_target else 0
         self._xgmi_check_every = max(1, int(getattr(config, 'allreduce_check_steps', 1000)))
+        self.defer_per_insert = True   # see _defer_per_insert (False: the acting launch inserts)
 
     # ------------------------------------------------------------ step body
     def _sample_and_grad(self):
@@ -113,7 +114,7 @@ class Learner:
         acting = None
         if self.actor is not None:
             assert 'frames' in batch, 'fused acting needs the slot-batch sampler'
-            acting = self.actor.fused_args()
+            acting = self.actor.fused_args(defer_per=self._defer_per_insert())
         # noisy nets: the fused optimizer derives dL/dsigma itself (not for async-PS pushes)
         sg = not (self.ps is None and self.net.fuses_sigma_grads(self._target_freq()))
         if self._split:
@@ -139,6 +140,14 @@ class Learner:
             return 'trunk'
         return 'launch'
 
+    def _defer_per_insert(self) -> bool:
+        """Prioritized replay + fused acting + 'opt' sampling: the optimizer launch's sampler
+        block enters the actors' new transitions into the sum-tree (max priority) in the same
+        one-wave climb as this step's priorities, instead of a serial climb at the end of the
+        acting workgroup (the head launch's critical path)."""
+        return (self.defer_per_insert and self.actor is not None and getattr(self.replay, 'prioritized', False)
+                and self.B + self.actor.E <= 64 and self._sample_mode() == 'opt')
+
     def _target_freq(self):
         """target_freq argument of apply_grads: the hard sync rides in the optimizer launch."""
         return self.config.target_update_freq if self.tau >= 1.0 else None
@@ -153,7 +162,8 @@ class Learner:
         if self._sample_mode() == 'opt':
             nxt = self.replay.next_sample_spec(
                 self.B, per=(self.idx, self.prio, self.net.global_step, cfg.per_eps, cfg.per_beta0,
-                             cfg.per_beta_steps) if per else None)
+                             cfg.per_beta_steps) if per else None,
+                insert=self.actor.per_insert_spec() if per and self._defer_per_insert() else None)
         fused = self.net.apply_grads(self.reducer.scale, target_freq=self._target_freq(), next_sample=nxt)
         self._presampled = nxt is not None and fused
         if per and not self._presampled:

@@ -446,11 +446,15 @@ class DeviceReplay:
         ok = self.frame_mode and self.device.type == 'cuda' and self.k == 4 and 1 <= B <= 512
         return ok and (not self.prioritized or B <= 64)
 
-    def next_sample_spec(self, B: int, per=None) -> dict:
+    def next_sample_spec(self, B: int, per=None, insert=None) -> dict:
         """Arguments of the optimizer launch's sampler block (csrc/kernels/optim.hip): it draws
         the NEXT minibatch into ``slot_batch(B)``'s buffers. per (prioritized replay):
         (upd_idx, upd_td, global_step, per_eps, beta0, beta_steps) — the block first writes
-        this step's priorities |td| of upd_idx into the sum-tree, then samples from it."""
+        this step's priorities |td| of upd_idx into the sum-tree, then samples from it.
+        insert (prioritized, fused acting): [cursor ptr, E, capacity] of the device actors whose
+        E new transitions this step's launches appended -- the same block enters them into the
+        tree at max priority in the same climb, before this step's priorities (the acting
+        launch then skips its own insertion; `DeviceActor.fused_args(defer_per=True)`)."""
         buf = self._slot_buffers(B)
         if not self.prioritized:
             if getattr(self, '_sample_ticket', None) is None:
@@ -468,6 +472,9 @@ class DeviceReplay:
              ptr(self.next_idx), ptr(self.actions), ptr(self.rewards), ptr(self.dones), ptr(self.gammas),
              ptr(buf['actions']), ptr(buf['rewards']), ptr(buf['dones']), ptr(buf['gammas']),
              ptr(buf['state_slots']), ptr(buf['next_slots']), B]
+        if insert is not None:
+            assert B + int(insert[1]) <= 64, 'batch + inserted transitions must fit one wave'
+            p += [int(v) for v in insert]
         return {'kind': 'per', 'p': p, 'f': [float(self.alpha), float(eps), float(beta0), float(max(1, beta_steps))]}
 
     def can_defer_sampling(self) -> bool:

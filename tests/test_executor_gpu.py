@@ -544,6 +544,44 @@ def test_per_fused_in_optimizer_equals_separate_launches(extra):
         torch.testing.assert_close(f1, f0, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize('extra', ['--prioritized_replay --double_dqn --dueling',
+                                   '--prioritized_replay ' + RAINBOW + ' --optimizer=adam'])
+def test_fused_acting_per_insert_in_optimizer(extra):
+    """PER + fused acting: the actors' new transitions enter the sum-tree inside the optimizer
+    launch's sampler block (one climb with this step's priorities, lanes ordered insert-first)
+    == the acting launch inserting them itself: same tree, same next batch, same parameters."""
+    from dist_dqn_amd.actors.device_actor import DeviceActor
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    outs = []
+    for defer in (False, True):
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 '
+                     '--fuse_sampling=2 ' + extra)
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)
+        rep.fill_synthetic(4096, 6, seed=5)
+        actor = DeviceActor(net, rep, cfg, num_envs=4, steps_per_call=1, seed=1000)
+        ln = Learner(net, rep, cfg, use_graph=True, actor=actor)
+        ln.defer_per_insert = defer
+        assert ln.actor is not None and ln._sample_mode() == 'opt' and ln._defer_per_insert() == defer
+        for _ in range(6):
+            ln.step()
+        torch.cuda.synchronize()
+        b = rep.slot_batch(32)
+        outs.append((net.online.flat.clone(), rep.tree.sum.clone(), rep.tree.min.clone(), rep.tree.max_p.clone(),
+                     b['idx'].clone(), b['weights'].clone(), rep.cursor.clone()))
+    (f0, s0, m0, x0, i0, w0, c0), (f1, s1, m1, x1, i1, w1, c1) = outs
+    assert torch.equal(c0, c1) and torch.equal(i0, i1)
+    torch.testing.assert_close(x1, x0, rtol=1e-5, atol=0)     # (Adam: last bits, see below)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(w1, w0, rtol=1e-4, atol=1e-6)
+    if '--optimizer=adam' not in extra:       # (Adam: see the test above -- atomics' arrival order)
+        torch.testing.assert_close(f1, f0, rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize('network,extra', [('nature', ''), ('nature', RAINBOW)])
 def test_device_actor_inserts_max_priority(network, extra):
     """PER + device actors: each acting step's new transitions enter the sum-tree at the
