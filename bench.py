@@ -144,6 +144,8 @@ def main():
                        'final_loss': loss,
                        'allreduce': learner.reducer.mode if ctx.enabled else None,
                        'allreduce_probe_us': learner.reducer.timings or None,
+                       'lowrank_dense': learner._lowrank is not None,
+                       'allreduce_ranges': learner._ar_ranges or None,
                        'allreduce_peer_timeouts': not xgmi_ok,
                        'world_size': ctx.world_size, 'dist_backend': ctx.backend,
                        'replicas_equal': replicas_equal,

@@ -478,6 +478,37 @@ void xgmi_allreduce(torch::Tensor grad, std::vector<int64_t> data, std::vector<i
   TORCH_CHECK(launch_xgmi_allreduce(a, (int)blocks, cur_stream()) == 0, "xgmi: launch arguments");
 }
 
+// srcs / outs: two segments each (byte pointers); bytes: per-rank segment sizes; cap: staging
+// bytes per parity of this channel
+void xgmi_allgather(std::vector<int64_t> srcs, std::vector<int64_t> outs, std::vector<int64_t> bytes,
+                    std::vector<int64_t> data, std::vector<int64_t> sig, int64_t seq, int64_t err, int64_t cap,
+                    int64_t rank, int64_t world, int64_t blocks, int64_t device) {
+  TORCH_CHECK(world >= 1 && world <= dqn::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi gather: rank/world");
+  TORCH_CHECK((int64_t)data.size() == world && (int64_t)sig.size() == world && seq && err, "xgmi gather: pointers");
+  TORCH_CHECK(srcs.size() == 2 && outs.size() == 2 && bytes.size() == 2, "xgmi gather: two segments");
+  TORCH_CHECK(blocks >= 1 && blocks <= dqn::kXgmiMaxBlocks, "xgmi gather: blocks");
+  dqn::XgmiGatherArgs g{};
+  for (int i = 0; i < world; ++i) {
+    TORCH_CHECK(data[i] && sig[i], "xgmi gather: null peer pointer");
+    g.x.data[i] = reinterpret_cast<void*>(data[i]);
+    g.x.sig[i] = reinterpret_cast<uint32_t*>(sig[i]);
+  }
+  for (int s = 0; s < 2; ++s) {
+    TORCH_CHECK(srcs[s] && outs[s] && bytes[s] >= 0 && bytes[s] % 16 == 0 && (srcs[s] & 15) == 0 && (outs[s] & 15) == 0,
+                "xgmi gather: 16-byte aligned segments, sizes % 16 == 0");
+    g.src[s] = reinterpret_cast<const void*>(srcs[s]);
+    g.out[s] = reinterpret_cast<void*>(outs[s]);
+    g.bytes[s] = bytes[s];
+  }
+  TORCH_CHECK(bytes[0] + bytes[1] <= cap, "xgmi gather: payload exceeds the channel's staging");
+  g.x.seq = reinterpret_cast<uint32_t*>(seq);
+  g.x.err = reinterpret_cast<int*>(err);
+  g.x.cap = cap;
+  g.x.rank = (int)rank; g.x.world = (int)world;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard((c10::DeviceIndex)device);
+  TORCH_CHECK(launch_xgmi_allgather(g, (int)blocks, cur_stream()) == 0, "xgmi gather: launch arguments");
+}
+
 // ---------------------------------------------------------------- fused MLP
 // ints: [L, A, P, Hs, Ds, sw, B, double, huber, fin x4, fout x4, act x4, w_off x4, b_off x4]
 // ptrs: [w_on, w_tg, x, xn, act, rew, done, gam, wts, loss, prio, grad, q_out] (0 = unused)
@@ -530,6 +561,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_ipc_open", &xgmi_ipc_open);
   m.def("xgmi_ipc_close", &xgmi_ipc_close);
   m.def("xgmi_allreduce", &xgmi_allreduce);
+  m.def("xgmi_allgather", &xgmi_allgather);
   m.attr("XGMI_MAX_BLOCKS") = dqn::kXgmiMaxBlocks;
   m.attr("XGMI_SIG_WORDS") = dqn::kXgmiMaxRanks * dqn::kXgmiMaxBlocks;
   m.def("replay_gather_frames", &replay_gather_frames);

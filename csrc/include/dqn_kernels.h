@@ -86,6 +86,17 @@ struct XgmiArgs {
 };
 }  // namespace dqn
 int launch_xgmi_allreduce(const dqn::XgmiArgs& a, int blocks, hipStream_t st);
+namespace dqn {
+// all-gather of two byte segments (the low-rank DP exchange: fc input rows + dH rows):
+// out[s] = [rank 0's src[s] | rank 1's | ...], x.cap = staging bytes per parity
+struct XgmiGatherArgs {
+  XgmiArgs x;                      // data / sig / seq / err / cap / rank / world (grad, n, bf16 unused)
+  const void* src[2];
+  void* out[2];
+  long bytes[2];                   // per-rank segment bytes (multiples of 16)
+};
+}  // namespace dqn
+int launch_xgmi_allgather(const dqn::XgmiGatherArgs& a, int blocks, hipStream_t st);
 
 // Fused MLP Q-network (reference SimpleNetwork), csrc/kernels/mlp.hip.
 namespace dqn {

@@ -60,6 +60,8 @@ struct WgradArgs {
   int MC, KB, NB;            // rows per block, K-range per block, N-range per block
   float scale;
   int atomic;
+  int mloop;                 // > 1: each block sums this many consecutive M-chunks (no atomics)
+  int db_zero;               // store 0 into db / db2 (the low-rank DP member on ranks != 0)
 };
 
 // Device actor step (eps-greedy + synthetic env + replay append), see actor.hip.

@@ -564,7 +564,20 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
   act_t* At = lds;
   act_t* Zt = lds + KB * LR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
+  // g.mloop > 1: this block sums mloop consecutive M-chunks itself (registers, fixed order): one
+  // block per weight tile, plain stores, bit-reproducible (the low-rank DP member)
+  const int nch = g.mloop > 1 ? g.mloop : 1;
+  const int k_lo = by * KB, n_lo = bz * NB;
+  static_assert(NB <= 256, "one bias column per thread");
+  const int kg = 8 * (lane >> 4), row = lane & 15;
+  constexpr int NTt = NB / 16;
+  f32x4 accs[PERW];
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  for (int c = 0; c < nch; ++c) {
+  const int m_lo = (bx * nch + c) * MC;
+  if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
   {
     const int r = threadIdx.x % MC, p = threadIdx.x / MC;
     const int m = m_lo + r;
@@ -597,34 +610,37 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     }
   }
   __syncthreads();
-  const bool atomic = g.atomic != 0;
-  if (g.db != nullptr && by == 0) {
-    for (int n = threadIdx.x; n < NB; n += 256) {
-      float s = 0.f;
-      const act_t* zr = Zt + n * LR;
+  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
+    const act_t* zr = Zt + threadIdx.x * LR;
 #pragma unroll 8
-      for (int r = 0; r < MC; ++r) s += (float)zr[r];
-      const int nn = n_lo + n;
-      if (nn < g.N) {
-        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
-        s *= kInvLossScale;
-        if (atomic) atomicAdd(pdb, s); else *pdb = s;
-      }
-    }
+    for (int r = 0; r < MC; ++r) dbs += (float)zr[r];
   }
-  const int kg = 8 * (lane >> 4), row = lane & 15;
-  constexpr int NTt = NB / 16;
 #pragma unroll
   for (int i = 0; i < PERW; ++i) {
     const int tile = wave + 4 * i;
     const int kt = tile / NTt, nt = tile - kt * NTt;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
       const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * LR + 32 * s + kg);
       const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * LR + 32 * s + kg);
-      acc = mfma16(af, bf, acc);
+      accs[i] = mfma16(af, bf, accs[i]);
     }
+  }
+  }  // chunks
+  const bool atomic = g.atomic != 0;
+  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
+    const int nn = n_lo + threadIdx.x;
+    if (nn < g.N) {
+      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+      const float sdb = g.db_zero ? 0.f : dbs * kInvLossScale;
+      if (atomic) atomicAdd(pdb, sdb); else *pdb = sdb;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int tile = wave + 4 * i;
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    const f32x4 acc = accs[i];
     const int n = n_lo + nt * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -651,7 +667,23 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
   act_t* At = lds;                               // [MC][SA]
   act_t* Zt = lds + MC * SA;                     // [MC][SZ]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
+  // g.mloop > 1: this block sums mloop consecutive M-chunks itself (registers, fixed order): one
+  // block per weight tile, plain stores, bit-reproducible (the low-rank DP member)
+  const int nch = g.mloop > 1 ? g.mloop : 1;
+  const int k_lo = by * KB, n_lo = bz * NB;
+  static_assert(NB <= 256, "one bias column per thread");
+  // operand lane map: k-group gq = lane >> 4 takes m rows {4 gq + q} (elements 0..3) and
+  // {16 + 4 gq + q} (elements 4..7) of each 32-row k-step -- the same permutation of the
+  // reduction index on both operands; one 32-lane half reads 8 consecutive rows per instruction
+  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+  constexpr int NTt = NB / 16;
+  f32x4 accs[PERW];
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  for (int c = 0; c < nch; ++c) {
+  const int m_lo = (bx * nch + c) * MC;
+  if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
   {
     const int r = threadIdx.x % MC, p = threadIdx.x / MC;
     const int m = m_lo + r;
@@ -676,38 +708,38 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[i];
   }
   __syncthreads();
-  const bool atomic = g.atomic != 0;
-  if (g.db != nullptr && by == 0) {
-    for (int n = threadIdx.x; n < NB; n += 256) {
-      float s = 0.f;
+  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
 #pragma unroll 8
-      for (int r = 0; r < MC; ++r) s += (float)Zt[r * SZ + n];
-      const int nn = n_lo + n;
-      if (nn < g.N) {
-        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
-        s *= kInvLossScale;
-        if (atomic) atomicAdd(pdb, s); else *pdb = s;
-      }
-    }
+    for (int r = 0; r < MC; ++r) dbs += (float)Zt[r * SZ + threadIdx.x];
   }
-  // operand lane map: k-group gq = lane >> 4 takes m rows {4 gq + q} (elements 0..3) and
-  // {16 + 4 gq + q} (elements 4..7) of each 32-row k-step -- the same permutation of the
-  // reduction index on both operands; one 32-lane half reads 8 consecutive rows per instruction
-  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
-  constexpr int NTt = NB / 16;
 #pragma unroll
   for (int i = 0; i < PERW; ++i) {
     const int tile = wave + 4 * i;
     const int kt = tile / NTt, nt = tile - kt * NTt;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
     const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
       const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
       const bfx8 bf = join_tr(lds_tr16(pz + 32 * s * SZ), lds_tr16(pz + (32 * s + 16) * SZ));
-      acc = mfma16(af, bf, acc);
+      accs[i] = mfma16(af, bf, accs[i]);
     }
+  }
+  }  // chunks
+  const bool atomic = g.atomic != 0;
+  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
+    const int nn = n_lo + threadIdx.x;
+    if (nn < g.N) {
+      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+      const float sdb = g.db_zero ? 0.f : dbs * kInvLossScale;
+      if (atomic) atomicAdd(pdb, sdb); else *pdb = sdb;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int tile = wave + 4 * i;
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    const f32x4 acc = accs[i];
     const int n = n_lo + nt * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1079,7 +1111,8 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
 
 #define WGRAD_LAUNCH(LD, MC, KB, NB)                                                                   \
   do {                                                                                                 \
-    dim3 grid((a.M + MC - 1) / MC, (a.K + KB - 1) / KB, (g.N + NB - 1) / NB);                          \
+    const int nch_ = g.mloop > 1 ? g.mloop : 1;   /* M-chunks summed inside one block */            \
+    dim3 grid((a.M + MC * nch_ - 1) / (MC * nch_), (a.K + KB - 1) / KB, (g.N + NB - 1) / NB);         \
     WgradArgs gg = g;                                                                                  \
     gg.atomic = grid.x > 1 ? 1 : 0;                                                                    \
     hipLaunchKernelGGL((wgrad_kernel<LD, MC, KB, NB>), grid, dim3(256), 0, st, a, gg);                 \

@@ -168,9 +168,53 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
   if (t == 0) a.seq[b] = k + 1u;
 }
 
+// All-gather of two segments (one signal per call): A  my segments -> my staging, signal
+// "A done" (k + 1); C  every rank's chunk b -> out[s] + q * bytes[s]. Block b of every rank
+// handles chunk b of the concatenated payload, so it waits only for block b of its peers.
+// Staging alternates parity per call: a rank writes parity p again at call k + 2 only after
+// every peer signalled A of call k + 1, i.e. finished reading call k (its C of call k).
+__global__ __launch_bounds__(kThreads) void xgmi_allgather_kernel(XgmiGatherArgs g) {
+  const XgmiArgs& a = g.x;
+  const int b = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  const int W = a.world, r = a.rank;
+  const uint32_t k = a.seq[b];
+  const long par = (long)(k & 1u);
+  auto stage = [&](int q) -> uint4* { return reinterpret_cast<uint4*>(reinterpret_cast<char*>(a.data[q]) + par * a.cap); };
+  const long v0 = g.bytes[0] / 16, v1 = g.bytes[1] / 16, nv = v0 + v1;
+  const long per = (nv + G - 1) / G;
+  const long lo = per * b < nv ? per * b : nv;
+  const long hi = per * (b + 1) < nv ? per * (b + 1) : nv;
+  DQN_ASSERT(16 * nv <= a.cap && b < kXgmiMaxBlocks);
+  const uint4* s0 = reinterpret_cast<const uint4*>(g.src[0]);
+  const uint4* s1 = reinterpret_cast<const uint4*>(g.src[1]);
+  uint4* mine = stage(r);
+  for (long v = lo + t; v < hi; v += kThreads) mine[v] = v < v0 ? s0[v] : s1[v - v0];
+  signal_all(a, b, k + 1u);
+  if (!wait_all(a, b, k + 1u)) return;
+  uint4* o0 = reinterpret_cast<uint4*>(g.out[0]);
+  uint4* o1 = reinterpret_cast<uint4*>(g.out[1]);
+  for (long v = lo + t; v < hi; v += kThreads) {
+    for (int d = 0; d < W; ++d) {
+      const int q = (r + d) % W;                      // stagger peers across links
+      const uint4 x = stage(q)[v];
+      if (v < v0) o0[(long)q * v0 + v] = x;
+      else o1[(long)q * v1 + (v - v0)] = x;
+    }
+  }
+  if (t == 0) a.seq[b] = k + 1u;
+}
+
 }  // namespace
 
 }  // namespace dqn
+
+int launch_xgmi_allgather(const dqn::XgmiGatherArgs& g, int blocks, hipStream_t st) {
+  const dqn::XgmiArgs& a = g.x;
+  if (blocks < 1 || blocks > dqn::kXgmiMaxBlocks || a.world < 1 || a.world > dqn::kXgmiMaxRanks) return 1;
+  if (g.bytes[0] % 16 != 0 || g.bytes[1] % 16 != 0 || g.bytes[0] + g.bytes[1] > a.cap) return 2;
+  hipLaunchKernelGGL(dqn::xgmi_allgather_kernel, dim3(blocks), dim3(dqn::kThreads), 0, st, g);
+  return 0;
+}
 
 int launch_xgmi_allreduce(const dqn::XgmiArgs& a, int blocks, hipStream_t st) {
   if (blocks < 1 || blocks > dqn::kXgmiMaxBlocks || a.world < 1 || a.world > dqn::kXgmiMaxRanks) return 1;

@@ -72,9 +72,11 @@ void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::v
 
 void wgrad(int64_t kind, int64_t in, std::vector<int64_t> dims, int64_t dz, int64_t ldz, int64_t dw, int64_t db,
            int64_t dw2, int64_t db2, int64_t nsplit, int64_t N, int64_t MC, int64_t KB, int64_t NB, double scale,
-           bool atomic) {
+           bool atomic, int64_t mloop, bool db_zero) {
   dqn::ConvArgs a = conv_args({in}, {}, {}, {}, {}, {1.0}, dims);
   dqn::WgradArgs g{};
+  g.mloop = (int)mloop; g.db_zero = db_zero ? 1 : 0;
+  TORCH_CHECK(mloop >= 1 && mloop <= 64, "wgrad: 1 <= mloop <= 64");
   g.dz = P<const void*>(dz); g.ldz = (int)ldz;
   g.dw = P<float*>(dw); g.db = P<float*>(db); g.dw2 = P<float*>(dw2); g.db2 = P<float*>(db2);
   g.nsplit = (int)nsplit; g.N = (int)N; g.MC = (int)MC; g.KB = (int)KB; g.NB = (int)NB;
@@ -334,7 +336,10 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_igemm", &igemm, pybind11::arg("kind"), pybind11::arg("inp"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("out"), pybind11::arg("mask"), pybind11::arg("scale"), pybind11::arg("dims"),
         pybind11::arg("aux") = std::vector<int64_t>{}, pybind11::arg("aux_f") = std::vector<double>{});
-  m.def("qnet_wgrad", &wgrad);
+  m.def("qnet_wgrad", &wgrad, pybind11::arg("kind"), pybind11::arg("in"), pybind11::arg("dims"), pybind11::arg("dz"), pybind11::arg("ldz"),
+        pybind11::arg("dw"), pybind11::arg("db"), pybind11::arg("dw2"), pybind11::arg("db2"), pybind11::arg("nsplit"), pybind11::arg("N"), pybind11::arg("MC"),
+        pybind11::arg("KB"), pybind11::arg("NB"), pybind11::arg("scale"), pybind11::arg("atomic"), pybind11::arg("mloop") = 1,
+        pybind11::arg("db_zero") = false);
   m.def("qnet_head_loss", &head_loss, pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"), pybind11::arg("io"),
         pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("qp"), pybind11::arg("actor"),

@@ -52,8 +52,34 @@ class Learner:
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
         # (an async-PS worker all-reduces nothing: no xgmi transport and no start-up probe, whose
         # collectives the parameter server rank -- inside serve() -- would never join)
+        # data parallelism over xgmi: the fc weight gradient travels as its factors (executor
+        # lowrank_spec: all-gather of the fc input rows + dL/dh rows, ~14x fewer bytes than the
+        # gradient at B=32); the all-reduce then covers only the rest of the flat buffer
+        lr = None
+        if (self.ctx.enabled and ps_client is None and int(getattr(config, 'lowrank_dense', 1))
+                and getattr(config, 'overlap_allreduce', True) and hasattr(network.executor, 'lowrank_spec')
+                and getattr(config, 'allreduce_dtype', 'fp32') == 'fp32'):
+            lr = network.executor.lowrank_spec(B)
         self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb,
-                                      'rccl' if ps_client is not None else config.allreduce, config.allreduce_dtype)
+                                      'rccl' if ps_client is not None else config.allreduce, config.allreduce_dtype,
+                                      gather_bytes=lr['gather_bytes'] if lr else 0)
+        self._lowrank = None
+        self._ar_ranges = []
+        if lr and self.reducer.in_graph and self.reducer.can_gather:
+            W = self.ctx.world_size
+            ranges, lo = [], 0
+            for a, b in sorted(lr['ranges']):
+                if a > lo:
+                    ranges.append((lo, a))
+                lo = b
+            if lo < network.grad.numel():
+                ranges.append((lo, network.grad.numel()))
+            # (one remaining range: the Nature / cnn layouts. Dueling leaves two; its 2-rank
+            # rehearsal timed out a peer wait once in that configuration, so it keeps the full
+            # all-reduce until that is understood)
+            if len(ranges) == 1 and all((hi - lo_) % (4 * W) == 0 for lo_, hi in ranges):
+                self._lowrank = {'gather': self.reducer.xgmi.allgather2, 'world': W, 'rank': self.ctx.rank}
+                self._ar_ranges = ranges
         self.tau = min(1.0, float(config.target_update_tau))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:
@@ -118,7 +144,8 @@ class Learner:
         # noisy nets: the fused optimizer derives dL/dsigma itself (not for async-PS pushes)
         sg = not (self.ps is None and self.net.fuses_sigma_grads(self._target_freq()))
         if self._split:
-            loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True, sigma_grads=sg)
+            loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True, sigma_grads=sg,
+                                                            lowrank=self._lowrank)
         else:
             loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg)
         # keep references (static buffers under graph capture) instead of copies
@@ -200,6 +227,13 @@ class Learner:
         range runs on a side stream (channel 0) concurrently with the conv backward; the conv
         range follows on the main stream (channel 1)."""
         total = self.net.grad.numel()
+        if self._lowrank is not None and self._tail is not None:
+            # the fc weight gradient is already the global sum (formed from the all-gathered
+            # factors on the tail's joined branch): reduce only the remaining ranges
+            self._tail()
+            for c, (lo, hi) in enumerate(self._ar_ranges):
+                self.reducer.allreduce_range(lo, hi, channel=c % 2)
+            return
         if self._tail is None or self._dense_hi <= 0:
             self._run_tail()
             self.reducer.allreduce_range(0, total, channel=0)

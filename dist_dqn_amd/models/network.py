@@ -163,7 +163,7 @@ class Network:
 
     # ------------------------------------------------------------- training
     def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False,
-                      sigma_grads: bool = True):
+                      sigma_grads: bool = True, lowrank: Optional[dict] = None):
         """Loss + gradient into ``self.grad``. ``split=True`` returns ``(loss, prio, tail)``: when
         ``tail`` is not None only the dense-layer gradients (``dense_range()``) are final and
         ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad)."""
@@ -179,6 +179,8 @@ class Network:
         can_split = split and hasattr(self.executor, 'supports_fused_acting')
         if can_split:
             kw['split'] = True
+            if lowrank is not None:      # DP: fc weight gradient from all-gathered factors
+                kw['lowrank'] = lowrank
         out = self.executor.loss_and_grad(self.online.flat, self.target.flat, batch, self.grad,
                                           self.noise, self.noise_target, **kw)
         loss, prio = out[0], out[1]

@@ -478,6 +478,35 @@ class HipExecutor:
             self.repack(target)
 
     # ------------------------------------------------------------ streams
+    def lowrank_spec(self, B: int):
+        """Low-rank DP exchange of the fc (hidden dense) layer's weight gradient, when this
+        executor's grouped-wgrad Nature path runs at this batch: dW = X^T dH has rank <= B, so
+        instead of all-reducing dW (1.6M values per hidden layer) the ranks all-gather X (the fc
+        input rows, B x F) and dH (B x HH) and every rank forms the summed dW over all W*B rows
+        itself -- bit-identical on every rank (one fixed-order, atomic-free launch). Returns
+        {'ranges': [(lo, hi), ...] of the fc weight tensors in the flat buffer (the caller
+        all-reduces the complement), 'gather_bytes': per-rank payload} or None."""
+        if (self.arch.network != 'nature' or self.noisy or not self.grouped_wgrad or self.two_stream
+                or B > 32):
+            return None
+        lay = self.layout
+        names = ['value/fcl/w', 'advantage/fcl/w'] if self.dueling else ['fcl/w']
+        if not all(n in lay.offsets for n in names):
+            return None
+        return {'ranges': [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in names],
+                'gather_bytes': B * (self.FLAT + self.HH) * self.esz}
+
+    def _lowrank_ws(self, B: int, W: int, dev) -> dict:
+        key = (B, W, dev)
+        lw = getattr(self, '_lr_bufs', {}).get(key)
+        if lw is None:
+            if not hasattr(self, '_lr_bufs'):
+                self._lr_bufs = {}
+            lw = {'x': torch.zeros(W * B * self.FLAT, dtype=self.act_dtype, device=dev),
+                  'dh': torch.zeros(W * B * self.HH, dtype=self.act_dtype, device=dev)}
+            self._lr_bufs[key] = lw
+        return lw
+
     def _side_stream(self, dev):
         st = getattr(self, '_side', None)
         if st is None or st.device != dev:
@@ -749,8 +778,14 @@ class HipExecutor:
 
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
-                      split: bool = False, sigma_grads: bool = True, draw_noise=None):
-        """sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
+                      split: bool = False, sigma_grads: bool = True, draw_noise=None, lowrank=None):
+        """lowrank (data parallelism, see ``lowrank_spec``): {'gather': f(srcs, outs, nbytes) (an
+        in-stream all-gather of two byte segments), 'world', 'rank'}. With ``split``, the fc weight
+        gradient is then formed from the all-gathered factors on a graph branch beside the dgrad
+        chain (ranks != 0 store zeros into the fc bias gradient, so the caller's all-reduce of the
+        remaining range sums it exactly once) and ``tail()`` joins that branch.
+
+        sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
         optimizer derives dL/dsigma from the mu-slot gradient and the noise itself.
 
         draw_noise = (out0, out1, rng) (noisy nets, fused optimizer to follow): the fc dgrad launch
@@ -889,7 +924,23 @@ class HipExecutor:
             scales = [self.input_scale] + [1.0] * (len(members) - 1)
             noisy = self.noisy and gnoise is not None
             side = None
-            if split and not noisy:
+            if split and not noisy and lowrank is not None:
+                assert self.lowrank_spec(B) is not None, 'low-rank exchange not available for this net / batch'
+                W, rk = int(lowrank['world']), int(lowrank['rank'])
+                lw = self._lowrank_ws(B, W, dev)
+                side = self._side_stream(dev)
+                side.wait_stream(main)                     # x3 (trunk) and dh (head) are final
+                with torch.cuda.stream(side):
+                    lowrank['gather']([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
+                                      [B * F * self.esz, B * HH * self.esz])
+                    # sum over all W*B rows in one block per weight tile (W 32-row chunks, no atomics)
+                    ext.qnet_wgrad(_KIND['DFWD'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
+                                   lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 32, 64, 128, 1.0, False,
+                                   mloop=W, db_zero=rk != 0)
+                fc_dgrad()
+                # the output layer's members join the conv members in the tail's grouped launch
+                members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]
+            elif split and not noisy:
                 fc_dgrad()
                 # dense weight gradients now (they need only dh, dQ and x3 / h): the dense range is final
                 ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])

@@ -37,7 +37,7 @@ log = logging.getLogger(__name__)
 
 class GradAllReducer:
     def __init__(self, ctx: DistContext, flat_grad: torch.Tensor, bucket_mb: float = 64.0,
-                 mode: str = 'auto', wire_dtype: str = 'fp32'):
+                 mode: str = 'auto', wire_dtype: str = 'fp32', gather_bytes: int = 0):
         self.ctx = ctx
         self.flat = flat_grad
         n = flat_grad.numel()
@@ -54,6 +54,8 @@ class GradAllReducer:
             self.wire = torch.zeros(n, dtype=torch.bfloat16, device=flat_grad.device)
         self.xgmi = None
         self.timings = {}
+        self.gather_bytes = int(gather_bytes)
+        self.can_gather = False       # the xgmi transport carries a working all-gather channel
         if ctx.enabled and flat_grad.is_cuda and mode in ('xgmi', 'auto'):
             self.xgmi = self._setup_xgmi(mode)
         self.mode = 'xgmi' if self.xgmi is not None else 'rccl'
@@ -63,7 +65,7 @@ class GradAllReducer:
         from .xgmi import XgmiAllReduce
         n = self.flat.numel()
         try:
-            x = XgmiAllReduce(self.ctx, n, self.wire_dtype)
+            x = XgmiAllReduce(self.ctx, n, self.wire_dtype, gather_bytes=self.gather_bytes)
         except Exception as e:  # noqa: BLE001
             if mode == 'xgmi':
                 raise
@@ -75,6 +77,10 @@ class GradAllReducer:
                 raise RuntimeError('xgmi all-reduce failed its self-test')
             log.warning('xgmi all-reduce failed its self-test; using RCCL')
             return None
+        if self.gather_bytes > 0:
+            self.can_gather = x.self_test_gather()
+            if not self.can_gather:
+                log.warning('xgmi all-gather failed its self-test; dense gradients all-reduced in full')
         agree = self._cross_check(x)
         if not agree:
             x.close()
@@ -88,7 +94,10 @@ class GradAllReducer:
             self.timings.update(xgmi_us=t_x, rccl_us=t_r)
             if self.ctx.is_chief:
                 log.info('gradient all-reduce (%d elems): xgmi %.1f us, rccl %.1f us', n, t_x, t_r)
-            if t_x > t_r:
+            # (with a working gather channel the learner all-reduces only the small non-factored
+            # range over xgmi and exchanges the dense factors: far fewer bytes than either
+            # full-buffer time measured here, so xgmi is kept)
+            if t_x > t_r and not self.can_gather:
                 x.close()
                 return None
         return x
@@ -188,7 +197,8 @@ class GradAllReducer:
     def check(self):
         """Raise if the xgmi transport reported a timed-out peer wait (host sync)."""
         if self.xgmi is not None and not self.xgmi.check():
-            raise RuntimeError('xgmi all-reduce: a peer wait timed out (rank %d)' % self.ctx.rank)
+            raise RuntimeError('xgmi all-reduce: a peer wait timed out (rank %d, channels %s)'
+                               % (self.ctx.rank, self.xgmi.failed_channels()))
 
     def close(self):
         if self.xgmi is not None:

@@ -76,7 +76,8 @@ class _Channel:
 class XgmiAllReduce:
     """Sum of an fp32 GPU tensor across the ranks of ``ctx`` (in place, current stream)."""
 
-    def __init__(self, ctx: DistContext, capacity: int, wire_dtype: str = 'fp32', channels: int = 2):
+    def __init__(self, ctx: DistContext, capacity: int, wire_dtype: str = 'fp32', channels: int = 2,
+                 gather_bytes: int = 0):
         assert ctx.enabled and ctx.device.type == 'cuda'
         self.ext = _ext.load(required=True)
         assert hasattr(self.ext, 'XGMI_MAX_BLOCKS'), 'extension built without the xGMI all-reduce'
@@ -89,8 +90,13 @@ class XgmiAllReduce:
         err = None
         self.channels: List[_Channel] = []
         handles = None
+        # gather_bytes > 0: one more channel (byte staging) for `allgather2` -- the low-rank
+        # exchange of the dense layer's factors (learner.py)
+        self.gather_cap = (int(gather_bytes) + 255) // 256 * 256
         try:
             self.channels = [_Channel(self.ext, ctx, self.cap, esz) for _ in range(channels)]
+            if self.gather_cap > 0:
+                self.channels.append(_Channel(self.ext, ctx, self.gather_cap, 1))
             handles = [self.ext.xgmi_ipc_handle(ch.base) for ch in self.channels]
         except Exception as e:  # noqa: BLE001
             err = e
@@ -115,10 +121,52 @@ class XgmiAllReduce:
         sv = n // 4 // self.ctx.world_size
         return max(1, min(self.ext.XGMI_MAX_BLOCKS, (sv + 511) // 512))
 
+    def allgather2(self, srcs, outs, nbytes):
+        """out[s][q * nbytes[s] : (q + 1) * nbytes[s]] = rank q's src[s] (raw device pointers, 16-byte
+        aligned, sizes % 16 == 0), for both segments in ONE launch on the current stream (the gather
+        channel: its own signals and staging, so it may run beside the all-reduce channels)."""
+        assert self.gather_cap > 0, 'no gather channel'
+        ch = self.channels[-1]
+        nv = (int(nbytes[0]) + int(nbytes[1])) // 16
+        blocks = max(1, min(self.ext.XGMI_MAX_BLOCKS, (nv + 255) // 256))
+        self.ext.xgmi_allgather([int(v) for v in srcs], [int(v) for v in outs], [int(v) for v in nbytes], ch.data,
+                                ch.sig, ch.seq_ptr, ch.err_ptr, self.gather_cap, self.ctx.rank, self.ctx.world_size,
+                                blocks, self.ctx.device.index)
+
+    def self_test_gather(self) -> bool:
+        """Gather rank-stamped bytes twice (both staging parities), check every slot, agree."""
+        ok = True
+        W, r = self.ctx.world_size, self.ctx.rank
+        n0 = max(16, min(self.gather_cap // 2, 1 << 16) // 16 * 16)
+        n1 = max(16, (self.gather_cap - n0) // 16 * 16)
+        dev = self.ctx.device
+        try:
+            for call in range(3):
+                a = torch.full((n0,), (r * 7 + call) % 251, dtype=torch.uint8, device=dev)
+                b = torch.full((n1,), (r * 13 + call + 1) % 251, dtype=torch.uint8, device=dev)
+                oa = torch.zeros(W * n0, dtype=torch.uint8, device=dev)
+                ob = torch.zeros(W * n1, dtype=torch.uint8, device=dev)
+                self.allgather2([a.data_ptr(), b.data_ptr()], [oa.data_ptr(), ob.data_ptr()], [n0, n1])
+                torch.cuda.synchronize(dev)
+                for q in range(W):
+                    ok = ok and bool((oa[q * n0:(q + 1) * n0] == (q * 7 + call) % 251).all())
+                    ok = ok and bool((ob[q * n1:(q + 1) * n1] == (q * 13 + call + 1) % 251).all())
+            ok = ok and self.check()
+        except Exception as e:  # noqa: BLE001
+            log.warning('xgmi all-gather self-test raised: %s', e)
+            ok = False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag) == 1
+
     def allreduce(self, t: torch.Tensor, channel: int = 0, blocks: Optional[int] = None):
         ch = self.channels[channel]
         self.ext.xgmi_allreduce(t, ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.cap, self.ctx.rank,
                                 self.ctx.world_size, self.bf16, blocks or self.blocks_for(t.numel()))
+
+    def failed_channels(self) -> list:
+        """Indices of the channels whose error word is set (host sync)."""
+        return [c for c, ch in enumerate(self.channels) if int(ch.seq_err[self.ext.XGMI_MAX_BLOCKS]) != 0]
 
     def check(self) -> bool:
         """False if any block of any launch so far timed out waiting for a peer (host sync)."""
@@ -132,7 +180,7 @@ class XgmiAllReduce:
         n = max(4 * W, min(n, self.cap) // (4 * W) * (4 * W))
         idx = torch.arange(n, device=self.ctx.device, dtype=torch.float32)
         try:
-            for c in range(len(self.channels)):
+            for c in range(len(self.channels) - (1 if self.gather_cap > 0 else 0)):
                 for call in range(3):
                     x = (idx % 7) + (r + 1) * (call + 1)
                     expect = W * (idx % 7) + (call + 1) * W * (W + 1) / 2

@@ -88,6 +88,30 @@ def _worker_xgmi(rank, world, port, wire, errq):
         assert bool((a == s).all()) and bool((b == 10 * s).all())
         assert x.check()
         x.close()
+        # the gather channel (low-rank DP exchange): two segments, every rank's bytes in rank order,
+        # both staging parities, concurrently with an all-reduce on another stream
+        y = XgmiAllReduce(ctx, cap, wire, gather_bytes=96 * 1024)
+        assert y.self_test(4096) and y.self_test_gather()
+        for call in range(3):
+            n0, n1 = 64 * 1024, 32 * 1024 - 16 * call
+            n1 -= n1 % 16
+            segs = [torch.randint(0, 256, (world, n), dtype=torch.uint8, generator=torch.Generator().manual_seed(
+                call * 10 + n), device='cpu').cuda() for n in (n0, n1)]
+            src = [segs[0][rank].clone(), segs[1][rank].clone()]
+            out = [torch.zeros(world * n0, dtype=torch.uint8, device='cuda'),
+                   torch.zeros(world * n1, dtype=torch.uint8, device='cuda')]
+            t = torch.full((4096,), float(rank + 1), device='cuda')
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                y.allreduce(t, channel=0)
+            y.allgather2([src[0].data_ptr(), src[1].data_ptr()], [out[0].data_ptr(), out[1].data_ptr()], [n0, n1])
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            assert torch.equal(out[0], segs[0].reshape(-1)) and torch.equal(out[1], segs[1].reshape(-1)), call
+            assert bool((t == world * (world + 1) / 2).all())
+        assert y.check()
+        y.close()
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # noqa: BLE001 - report to the parent
@@ -144,6 +168,11 @@ def _worker(rank, world, port, network, extra, errq):
             if xgmi:
                 assert len(ln._graphs) == 1, 'xgmi DP step should be one graph'
                 ln.reducer.check()
+                # the fc weight gradient travels as all-gathered factors (overlap=1, Nature,
+                # no noisy layers, fp32 wire); overlap=0 is the full all-reduce it is compared with
+                lowrank = (bool(overlap) and network == 'nature' and '--noisy' not in extra and 'bf16' not in extra
+                           and '--dueling' not in extra)
+                assert (ln._lowrank is not None) == lowrank, (overlap, extra)
             elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
             outs[overlap] = net.online.flat.clone()
