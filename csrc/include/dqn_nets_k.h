@@ -192,6 +192,7 @@ enum LayerKind {
   L_NAT_CONV3_DGRAD = 7, L_NAT_CONV2_DGRAD = 8,
   L_NAT_CONV1_FRAMES = 9,   // conv1 reading the frame ring through a [B][4] slot table
   L_HEAD_WGRAD = 11,        // output layer weight gradient (grouped wgrad member: N <= 32)
+  L_DENSE_WGRAD_LR = 12,    // fc weight gradient over all-gathered rows (64-row chunks summed per block)
 };
 
 }  // namespace dqn

@@ -564,20 +564,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
   act_t* At = lds;
   act_t* Zt = lds + KB * LR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // g.mloop > 1: this block sums mloop consecutive M-chunks itself (registers, fixed order): one
-  // block per weight tile, plain stores, bit-reproducible (the low-rank DP member)
-  const int nch = g.mloop > 1 ? g.mloop : 1;
-  const int k_lo = by * KB, n_lo = bz * NB;
-  static_assert(NB <= 256, "one bias column per thread");
-  const int kg = 8 * (lane >> 4), row = lane & 15;
-  constexpr int NTt = NB / 16;
-  f32x4 accs[PERW];
-#pragma unroll
-  for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbs = 0.f;
-  for (int c = 0; c < nch; ++c) {
-  const int m_lo = (bx * nch + c) * MC;
-  if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
+  const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
   {
     const int r = threadIdx.x % MC, p = threadIdx.x / MC;
     const int m = m_lo + r;
@@ -610,37 +597,34 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     }
   }
   __syncthreads();
-  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
-    const act_t* zr = Zt + threadIdx.x * LR;
+  const bool atomic = g.atomic != 0;
+  if (g.db != nullptr && by == 0) {
+    for (int n = threadIdx.x; n < NB; n += 256) {
+      float s = 0.f;
+      const act_t* zr = Zt + n * LR;
 #pragma unroll 8
-    for (int r = 0; r < MC; ++r) dbs += (float)zr[r];
+      for (int r = 0; r < MC; ++r) s += (float)zr[r];
+      const int nn = n_lo + n;
+      if (nn < g.N) {
+        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        s *= kInvLossScale;
+        if (atomic) atomicAdd(pdb, s); else *pdb = s;
+      }
+    }
   }
+  const int kg = 8 * (lane >> 4), row = lane & 15;
+  constexpr int NTt = NB / 16;
 #pragma unroll
   for (int i = 0; i < PERW; ++i) {
     const int tile = wave + 4 * i;
     const int kt = tile / NTt, nt = tile - kt * NTt;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
       const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * LR + 32 * s + kg);
       const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * LR + 32 * s + kg);
-      accs[i] = mfma16(af, bf, accs[i]);
+      acc = mfma16(af, bf, acc);
     }
-  }
-  }  // chunks
-  const bool atomic = g.atomic != 0;
-  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
-    const int nn = n_lo + threadIdx.x;
-    if (nn < g.N) {
-      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
-      const float sdb = g.db_zero ? 0.f : dbs * kInvLossScale;
-      if (atomic) atomicAdd(pdb, sdb); else *pdb = sdb;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < PERW; ++i) {
-    const int tile = wave + 4 * i;
-    const int kt = tile / NTt, nt = tile - kt * NTt;
-    const f32x4 acc = accs[i];
     const int n = n_lo + nt * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -667,23 +651,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
   act_t* At = lds;                               // [MC][SA]
   act_t* Zt = lds + MC * SA;                     // [MC][SZ]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // g.mloop > 1: this block sums mloop consecutive M-chunks itself (registers, fixed order): one
-  // block per weight tile, plain stores, bit-reproducible (the low-rank DP member)
-  const int nch = g.mloop > 1 ? g.mloop : 1;
-  const int k_lo = by * KB, n_lo = bz * NB;
-  static_assert(NB <= 256, "one bias column per thread");
-  // operand lane map: k-group gq = lane >> 4 takes m rows {4 gq + q} (elements 0..3) and
-  // {16 + 4 gq + q} (elements 4..7) of each 32-row k-step -- the same permutation of the
-  // reduction index on both operands; one 32-lane half reads 8 consecutive rows per instruction
-  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
-  constexpr int NTt = NB / 16;
-  f32x4 accs[PERW];
-#pragma unroll
-  for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbs = 0.f;
-  for (int c = 0; c < nch; ++c) {
-  const int m_lo = (bx * nch + c) * MC;
-  if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
+  const int m_lo = bx * MC, k_lo = by * KB, n_lo = bz * NB;
   {
     const int r = threadIdx.x % MC, p = threadIdx.x / MC;
     const int m = m_lo + r;
@@ -708,38 +676,38 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[i];
   }
   __syncthreads();
-  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
+  const bool atomic = g.atomic != 0;
+  if (g.db != nullptr && by == 0) {
+    for (int n = threadIdx.x; n < NB; n += 256) {
+      float s = 0.f;
 #pragma unroll 8
-    for (int r = 0; r < MC; ++r) dbs += (float)Zt[r * SZ + threadIdx.x];
+      for (int r = 0; r < MC; ++r) s += (float)Zt[r * SZ + n];
+      const int nn = n_lo + n;
+      if (nn < g.N) {
+        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        s *= kInvLossScale;
+        if (atomic) atomicAdd(pdb, s); else *pdb = s;
+      }
+    }
   }
+  // operand lane map: k-group gq = lane >> 4 takes m rows {4 gq + q} (elements 0..3) and
+  // {16 + 4 gq + q} (elements 4..7) of each 32-row k-step -- the same permutation of the
+  // reduction index on both operands; one 32-lane half reads 8 consecutive rows per instruction
+  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+  constexpr int NTt = NB / 16;
 #pragma unroll
   for (int i = 0; i < PERW; ++i) {
     const int tile = wave + 4 * i;
     const int kt = tile / NTt, nt = tile - kt * NTt;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
     const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
       const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
       const bfx8 bf = join_tr(lds_tr16(pz + 32 * s * SZ), lds_tr16(pz + (32 * s + 16) * SZ));
-      accs[i] = mfma16(af, bf, accs[i]);
+      acc = mfma16(af, bf, acc);
     }
-  }
-  }  // chunks
-  const bool atomic = g.atomic != 0;
-  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
-    const int nn = n_lo + threadIdx.x;
-    if (nn < g.N) {
-      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
-      const float sdb = g.db_zero ? 0.f : dbs * kInvLossScale;
-      if (atomic) atomicAdd(pdb, sdb); else *pdb = sdb;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < PERW; ++i) {
-    const int tile = wave + 4 * i;
-    const int kt = tile / NTt, nt = tile - kt * NTt;
-    const f32x4 acc = accs[i];
     const int n = n_lo + nt * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -754,6 +722,110 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
   }
 }
 #endif
+
+
+// Multi-chunk variant (the low-rank DP member, L_DENSE_WGRAD_LR): ONE block per weight tile sums
+// g.mloop consecutive MC-row chunks in a fixed order, accumulators in registers, plain stores:
+// bit-identical on every rank that runs it on the same all-gathered rows. Staged like the
+// fp32 build's body ([k][m] / [n][m], m contiguous) for every element type; off the critical
+// path (a graph branch beside the dgrad chain), so simplicity over staging speed. g.db_zero:
+// store 0 into the bias gradient (ranks != 0: the caller's all-reduce then sums it once).
+template <class LD, int MC, int KB, int NB>
+DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, int bz, act_t* lds) {
+  constexpr int LR = MC + 8;
+  constexpr int TPR = 256 / MC;
+  constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
+  constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
+  static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0 && NB <= 256, "tiling");
+  act_t* At = lds;
+  act_t* Zt = lds + KB * LR;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k_lo = by * KB, n_lo = bz * NB;
+  const int kg = 8 * (lane >> 4), row = lane & 15;
+  constexpr int NTt = NB / 16;
+  const int nch = g.mloop > 1 ? g.mloop : 1;
+  f32x4 accs[PERW];
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  const int r = threadIdx.x % MC, p = threadIdx.x / MC;
+  for (int c = 0; c < nch; ++c) {
+    const int m = c * MC + r;
+    const bool mok = m < a.M;
+    const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
+    LD ld(a, 0, m);
+    bfx8 va[GA], vz[GZ];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int k0 = k_lo + (p + i * TPR) * 8;
+      va[i] = sel8(k0 < a.K, ld.frag(min(k0, a.K - 8)));
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;
+      vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
+    }
+    if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + r] = va[i][j];
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[i][j];
+    }
+    __syncthreads();
+    if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
+      const act_t* zr = Zt + threadIdx.x * LR;
+#pragma unroll 8
+      for (int q = 0; q < MC; ++q) dbs += (float)zr[q];
+    }
+#pragma unroll
+    for (int i = 0; i < PERW; ++i) {
+      const int tile = wave + 4 * i;
+      const int kt = tile / NTt, nt = tile - kt * NTt;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * LR + 32 * s + kg);
+        const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * LR + 32 * s + kg);
+        accs[i] = mfma16(af, bf, accs[i]);
+      }
+    }
+  }
+  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
+    const int nn = n_lo + threadIdx.x;
+    if (nn < g.N) {
+      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+      *pdb = g.db_zero ? 0.f : dbs * kInvLossScale;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int tile = wave + 4 * i;
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    const int n = n_lo + nt * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k_lo + kt * 16 + 4 * (lane >> 4) + q;
+      if (k < a.K && n < g.N) {
+        float* pw = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
+                                 : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
+        *pw = accs[i][q] * (g.scale * kInvLossScale);
+      }
+    }
+  }
+}
+
+template <class LD, int MC, int KB, int NB>
+__global__ void __launch_bounds__(256) wgrad_multi_kernel(ConvArgs a, WgradArgs g) {
+  __shared__ __attribute__((aligned(16))) act_t lds[(KB + NB) * (MC + 8)];
+  wgrad_block_multi<LD, MC, KB, NB>(a, g, blockIdx.y, blockIdx.z, lds);
+}
 
 template <class LD, int MC, int KB, int NB>
 __global__ void __launch_bounds__(256) wgrad_kernel(ConvArgs a, WgradArgs g) {
@@ -1111,8 +1183,7 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
 
 #define WGRAD_LAUNCH(LD, MC, KB, NB)                                                                   \
   do {                                                                                                 \
-    const int nch_ = g.mloop > 1 ? g.mloop : 1;   /* M-chunks summed inside one block */            \
-    dim3 grid((a.M + MC * nch_ - 1) / (MC * nch_), (a.K + KB - 1) / KB, (g.N + NB - 1) / NB);         \
+    dim3 grid((a.M + MC - 1) / MC, (a.K + KB - 1) / KB, (g.N + NB - 1) / NB);                          \
     WgradArgs gg = g;                                                                                  \
     gg.atomic = grid.x > 1 ? 1 : 0;                                                                    \
     hipLaunchKernelGGL((wgrad_kernel<LD, MC, KB, NB>), grid, dim3(256), 0, st, a, gg);                 \
@@ -1126,6 +1197,12 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
     case L_NAT_CONV3_FWD: WGRAD_LAUNCH(NatC3, 128, 192, 64); return 0;   // 13 x 3 blocks
     case L_DENSE_FWD_RELU: WGRAD_LAUNCH(DenseLoader, 32, 64, 128); return 0;
     case L_HEAD_WGRAD: WGRAD_LAUNCH(DenseLoader, 32, 64, 64); return 0;
+    case L_DENSE_WGRAD_LR: {                     // ONE block per weight tile over all g.mloop 64-row chunks
+      if (g.mloop < 1 || 64 * g.mloop < a.M) return -1;
+      dim3 grid(1, (a.K + 63) / 64, (g.N + 127) / 128);
+      hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 64, 128>), grid, dim3(256), 0, st, a, g);
+      return 0;
+    }
     default: return -1;
   }
 }

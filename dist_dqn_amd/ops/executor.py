@@ -27,7 +27,7 @@ import torch
 
 from . import _ext
 
-_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9, HW=11)
+_KIND = dict(C1=1, C2=2, C3=3, DFWD=4, DF32=5, DDGRAD=6, D3=7, D2=8, F1=9, HW=11, DLR=12)
 
 
 def supports(arch) -> bool:
@@ -933,10 +933,11 @@ class HipExecutor:
                 with torch.cuda.stream(side):
                     lowrank['gather']([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
                                       [B * F * self.esz, B * HH * self.esz])
-                    # sum over all W*B rows in one block per weight tile (W 32-row chunks, no atomics)
-                    ext.qnet_wgrad(_KIND['DFWD'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
-                                   lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 32, 64, 128, 1.0, False,
-                                   mloop=W, db_zero=rk != 0)
+                    # sum over all W*B rows in one block per weight tile (64-row chunks in a fixed
+                    # order, no atomics: bit-identical on every rank)
+                    ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
+                                   lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
+                                   mloop=(W * B + 63) // 64, db_zero=rk != 0)
                 fc_dgrad()
                 # the output layer's members join the conv members in the tail's grouped launch
                 members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]

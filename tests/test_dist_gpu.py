@@ -87,7 +87,12 @@ def _worker_xgmi(rank, world, port, wire, errq):
         s = world * (world + 1) / 2
         assert bool((a == s).all()) and bool((b == 10 * s).all())
         assert x.check()
+        # every rank done with x (a peer's phase C may still read my staging after my kernel
+        # returned) before any rank frees its buffers and maps new ones
+        torch.cuda.synchronize()
+        dist.barrier()
         x.close()
+        dist.barrier()
         # the gather channel (low-rank DP exchange): two segments, every rank's bytes in rank order,
         # both staging parities, concurrently with an all-reduce on another stream
         y = XgmiAllReduce(ctx, cap, wire, gather_bytes=96 * 1024)

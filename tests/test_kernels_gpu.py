@@ -230,3 +230,31 @@ def test_device_actor_appends_consistent_transitions():
             np.testing.assert_array_equal(si[t + E], nxt)
         else:
             assert len(set(si[t + E].tolist())) == 1        # new episode: duplicated reset frame
+
+
+@pytest.mark.parametrize('W', [2, 8])
+def test_lowrank_dense_wgrad_matches_fp32(W):
+    """The low-rank DP member (L_DENSE_WGRAD_LR): dW = X^T dH and db = sum dH over all W*32
+    all-gathered rows, summed in 64-row chunks inside ONE block per weight tile (no atomics) ==
+    the fp32 reference; db_zero stores zeros into the bias; two launches are bit-identical."""
+    from dist_dqn_amd.ops import _ext
+    ext = _ext.load(required=True)
+    M, F, H = W * 32, 3136, 512
+    g = torch.Generator(device=DEV).manual_seed(W)
+    x = torch.rand(M, F, device=DEV, generator=g).to(torch.bfloat16)
+    dh = (torch.randn(M, H, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    dw = torch.full((F, H), float('nan'), device=DEV)
+    db = torch.full((H,), float('nan'), device=DEV)
+    run = lambda zero: ext.qnet_wgrad(12, x.data_ptr(), [M, H, F, 0, 0, 0, 0, 0, 0, 0, 0], dh.data_ptr(), H,
+                                      dw.data_ptr(), db.data_ptr(), 0, 0, H, H, 64, 64, 128, 1.0, False,
+                                      mloop=(M + 63) // 64, db_zero=zero)
+    run(False)
+    torch.cuda.synchronize()
+    ref_w = x.float().t() @ dh.float()
+    ref_b = dh.float().sum(0)
+    torch.testing.assert_close(dw, ref_w, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db, ref_b, rtol=1e-4, atol=1e-4)
+    w1 = dw.clone()
+    run(True)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, w1) and bool((db == 0).all())
