@@ -20,6 +20,7 @@ between two captured graphs (pre: sample..backward, post: optimizer..target).
 from __future__ import annotations
 
 import logging
+import os
 from typing import Dict, Optional
 
 import torch
@@ -35,6 +36,7 @@ log = logging.getLogger(__name__)
 
 
 _CAPTURE_MODE = 'thread_local'
+_AR_FORK = os.environ.get('DQN_AR_FORK', '0') == '1'
 
 class Learner:
     def __init__(self, network: Network, replay, config, ctx: Optional[DistContext] = None,
@@ -97,7 +99,10 @@ class Learner:
         # data parallelism: all-reduce the dense-layer gradients (fc: ~95% of Nature-CNN's
         # bytes) while the conv backward runs, then the conv gradients (config.overlap_allreduce)
         self._tail = None
-        self._split = bool(self.ctx.enabled and ps_client is None and getattr(config, 'overlap_allreduce', True))
+        # (xgmi without the low-rank exchange: no split -- its all-reduce runs in stream order
+        # after the whole backward, see _kernel_allreduce -- unless DQN_AR_FORK=1)
+        self._split = bool(self.ctx.enabled and ps_client is None and getattr(config, 'overlap_allreduce', True)
+                           and (not self.reducer.in_graph or _AR_FORK or self._lowrank is not None))
         self._dense_hi = network.dense_range()[1] if self._split else 0
         self._ar_stream = None
         self._presampled = False    # this step's minibatch was drawn by the last optimizer launch
@@ -223,9 +228,11 @@ class Learner:
         self.reducer.wait_all([h1, h2])
 
     def _kernel_allreduce(self):
-        """xgmi transport: both all-reduces are kernel launches (graph-capturable). The dense
-        range runs on a side stream (channel 0) concurrently with the conv backward; the conv
-        range follows on the main stream (channel 1)."""
+        """xgmi transport: the all-reduces are kernel launches (graph-capturable), in stream
+        order after the conv backward: a fork / join inside a captured HIP graph costs ~25 us on
+        this ROCm (scripts/probe_graph_concurrency.py: one side kernel 11 -> 36 us), more than the
+        overlap saves. DQN_AR_FORK=1 keeps the dense range on a side stream (channel 0) beside the
+        conv backward instead (the conv range follows on channel 1)."""
         total = self.net.grad.numel()
         if self._lowrank is not None and self._tail is not None:
             # the fc weight gradient is already the global sum (formed from the all-gathered
@@ -234,7 +241,7 @@ class Learner:
             for c, (lo, hi) in enumerate(self._ar_ranges):
                 self.reducer.allreduce_range(lo, hi, channel=c % 2)
             return
-        if self._tail is None or self._dense_hi <= 0:
+        if self._tail is None or self._dense_hi <= 0 or not _AR_FORK:
             self._run_tail()
             self.reducer.allreduce_range(0, total, channel=0)
             return

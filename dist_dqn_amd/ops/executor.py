@@ -928,16 +928,15 @@ class HipExecutor:
                 assert self.lowrank_spec(B) is not None, 'low-rank exchange not available for this net / batch'
                 W, rk = int(lowrank['world']), int(lowrank['rank'])
                 lw = self._lowrank_ws(B, W, dev)
-                side = self._side_stream(dev)
-                side.wait_stream(main)                     # x3 (trunk) and dh (head) are final
-                with torch.cuda.stream(side):
-                    lowrank['gather']([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
-                                      [B * F * self.esz, B * HH * self.esz])
-                    # sum over all W*B rows in one block per weight tile (64-row chunks in a fixed
-                    # order, no atomics: bit-identical on every rank)
-                    ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
-                                   lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
-                                   mloop=(W * B + 63) // 64, db_zero=rk != 0)
+                # in stream order (a graph fork / join costs ~25 us on this ROCm: measured,
+                # scripts/probe_graph_concurrency.py), right after the head: x3 and dh are final
+                lowrank['gather']([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
+                                  [B * F * self.esz, B * HH * self.esz])
+                # sum over all W*B rows in one block per weight tile (64-row chunks in a fixed
+                # order, no atomics: bit-identical on every rank)
+                ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
+                               lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
+                               mloop=(W * B + 63) // 64, db_zero=rk != 0)
                 fc_dgrad()
                 # the output layer's members join the conv members in the tail's grouped launch
                 members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]
