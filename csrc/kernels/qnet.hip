@@ -749,12 +749,13 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
   for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
   const int r = threadIdx.x % MC, p = threadIdx.x / MC;
-  for (int c = 0; c < nch; ++c) {
+  bfx8 va[GA], vz[GZ];
+  // chunk c's fragments into registers (issued one chunk ahead: they fly under chunk c-1's MFMAs)
+  auto load = [&](int c) {
     const int m = c * MC + r;
     const bool mok = m < a.M;
     const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
     LD ld(a, 0, m);
-    bfx8 va[GA], vz[GZ];
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int k0 = k_lo + (p + i * TPR) * 8;
@@ -766,6 +767,9 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
       const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
+  };
+  load(0);
+  for (int c = 0; c < nch; ++c) {
     if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
@@ -779,6 +783,7 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
 #pragma unroll
       for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[i][j];
     }
+    if (c + 1 < nch) load(c + 1);
     __syncthreads();
     if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
       const act_t* zr = Zt + threadIdx.x * LR;
