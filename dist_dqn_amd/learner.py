@@ -76,10 +76,8 @@ class Learner:
                 lo = b
             if lo < network.grad.numel():
                 ranges.append((lo, network.grad.numel()))
-            # (one remaining range: the Nature / cnn layouts. Dueling leaves two; its 2-rank
-            # rehearsal timed out a peer wait once in that configuration, so it keeps the full
-            # all-reduce until that is understood)
-            if len(ranges) == 1 and all((hi - lo_) % (4 * W) == 0 for lo_, hi in ranges):
+            # (Nature: one remaining range; dueling: two, one launch each in stream order)
+            if all((hi - lo_) % (4 * W) == 0 for lo_, hi in ranges):
                 self._lowrank = {'gather': self.reducer.xgmi.allgather2, 'world': W, 'rank': self.ctx.rank}
                 self._ar_ranges = ranges
         self.tau = min(1.0, float(config.target_update_tau))

@@ -175,8 +175,7 @@ def _worker(rank, world, port, network, extra, errq):
                 ln.reducer.check()
                 # the fc weight gradient travels as all-gathered factors (overlap=1, Nature,
                 # no noisy layers, fp32 wire); overlap=0 is the full all-reduce it is compared with
-                lowrank = (bool(overlap) and network == 'nature' and '--noisy' not in extra and 'bf16' not in extra
-                           and '--dueling' not in extra)
+                lowrank = bool(overlap) and network == 'nature' and '--noisy' not in extra and 'bf16' not in extra
                 assert (ln._lowrank is not None) == lowrank, (overlap, extra)
             elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
