@@ -454,12 +454,28 @@ int64_t xgmi_ipc_open(torch::Tensor handle) {
 void xgmi_ipc_close(int64_t p) { if (p) (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); }
 
 // grad: fp32 GPU slice to reduce in place; data/sig: one pointer per rank (mine included)
+// ranges (optional): [lo0, hi0, lo1, hi1, ...] element ranges of grad summed as ONE vector
 void xgmi_allreduce(torch::Tensor grad, std::vector<int64_t> data, std::vector<int64_t> sig, int64_t seq,
-                    int64_t err, int64_t cap, int64_t rank, int64_t world, bool bf16, int64_t blocks) {
+                    int64_t err, int64_t cap, int64_t rank, int64_t world, bool bf16, int64_t blocks,
+                    std::vector<int64_t> ranges) {
   CHECK_T(grad, torch::kFloat32);
   TORCH_CHECK(world >= 1 && world <= dqn::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi: rank/world");
   TORCH_CHECK((int64_t)data.size() == world && (int64_t)sig.size() == world && seq && err, "xgmi: pointers");
-  TORCH_CHECK(grad.numel() % (4 * world) == 0 && grad.numel() <= cap, "xgmi: n % (4 world) and capacity");
+  int64_t n = grad.numel();
+  const int nr = (int)(ranges.size() / 2);
+  TORCH_CHECK(ranges.size() % 2 == 0 && nr <= dqn::kXgmiMaxRanges, "xgmi: at most ", dqn::kXgmiMaxRanges, " ranges");
+  if (nr > 0) {
+    n = 0;
+    int64_t prev = 0;
+    for (int r = 0; r < nr; ++r) {
+      const int64_t lo = ranges[2 * r], hi = ranges[2 * r + 1];
+      TORCH_CHECK(lo >= prev && hi > lo && hi <= grad.numel() && lo % 4 == 0 && (hi - lo) % 4 == 0,
+                  "xgmi: ranges ascending, disjoint, inside the buffer, multiples of 4");
+      prev = hi;
+      n += hi - lo;
+    }
+  }
+  TORCH_CHECK(n % (4 * world) == 0 && n <= cap, "xgmi: n % (4 world) and capacity");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(grad.data_ptr()) & 15) == 0, "xgmi: 16-byte aligned gradient");
   TORCH_CHECK(blocks >= 1 && blocks <= dqn::kXgmiMaxBlocks, "xgmi: blocks");
   dqn::XgmiArgs a{};
@@ -471,7 +487,15 @@ void xgmi_allreduce(torch::Tensor grad, std::vector<int64_t> data, std::vector<i
   a.seq = reinterpret_cast<uint32_t*>(seq);
   a.err = reinterpret_cast<int*>(err);
   a.grad = ptr<float>(grad);
-  a.n = grad.numel();
+  a.n = n;
+  a.nr = nr;
+  int64_t pre = 0;
+  for (int r = 0; r < nr; ++r) {
+    a.rlo[r] = ranges[2 * r];
+    a.rpre[r] = pre;
+    pre += ranges[2 * r + 1] - ranges[2 * r];
+  }
+  a.rpre[nr] = pre;
   a.cap = cap;
   a.rank = (int)rank; a.world = (int)world; a.bf16 = bf16 ? 1 : 0;
   c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
@@ -560,7 +584,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_ipc_handle", &xgmi_ipc_handle);
   m.def("xgmi_ipc_open", &xgmi_ipc_open);
   m.def("xgmi_ipc_close", &xgmi_ipc_close);
-  m.def("xgmi_allreduce", &xgmi_allreduce);
+  m.def("xgmi_allreduce", &xgmi_allreduce, pybind11::arg("grad"), pybind11::arg("data"), pybind11::arg("sig"),
+        pybind11::arg("seq"), pybind11::arg("err"), pybind11::arg("cap"), pybind11::arg("rank"), pybind11::arg("world"),
+        pybind11::arg("bf16"), pybind11::arg("blocks"), pybind11::arg("ranges") = std::vector<int64_t>{});
   m.def("xgmi_allgather", &xgmi_allgather);
   m.attr("XGMI_MAX_BLOCKS") = dqn::kXgmiMaxBlocks;
   m.attr("XGMI_SIG_WORDS") = dqn::kXgmiMaxRanks * dqn::kXgmiMaxBlocks;

@@ -74,6 +74,7 @@ void launch_stack_states(const uint8_t* frames, const int32_t* stacks, uint8_t* 
 namespace dqn {
 constexpr int kXgmiMaxRanks = 16;
 constexpr int kXgmiMaxBlocks = 256;
+constexpr int kXgmiMaxRanges = 8;
 struct XgmiArgs {
   void* data[kXgmiMaxRanks];       // every rank's staging buffer (2 parities x cap elements), peer-mapped
   uint32_t* sig[kXgmiMaxRanks];    // every rank's signal words [kXgmiMaxRanks][kXgmiMaxBlocks], peer-mapped
@@ -81,6 +82,12 @@ struct XgmiArgs {
   int* err;                        // set to 1 by a block whose wait timed out
   float* grad;                     // local gradient (in: my addend, out: the sum)
   long n;                          // elements to reduce (n % (4 * world) == 0)
+  // nr > 0: the reduced vector is the concatenation of nr ranges grad[rlo[r], rlo[r] + len_r)
+  // (rpre: exclusive prefix sums of the lengths, rpre[nr] = n; every length % 4 == 0), so several
+  // disjoint pieces of one flat buffer are summed in ONE launch
+  int nr;
+  long rlo[kXgmiMaxRanges];
+  long rpre[kXgmiMaxRanges + 1];
   long cap;                        // staging capacity per parity, elements
   int rank, world, bf16;
 };

@@ -116,7 +116,14 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
   const int par = (int)(k & 1u);
   const long esz = BF16 ? 2 : 4;
   auto stage = [&](int q) -> char* { return reinterpret_cast<char*>(a.data[q]) + (long)par * a.cap * esz; };
-  float4* grad = reinterpret_cast<float4*>(a.grad);
+  // float4 vector i of the reduced vector (ranged: the concatenation of a.nr pieces of a.grad)
+  auto gv = [&](long i) -> float4* {
+    if (a.nr <= 0) return reinterpret_cast<float4*>(a.grad) + i;
+    const long e = 4 * i;
+    int r = 0;
+    while (r + 1 < a.nr && e >= a.rpre[r + 1]) ++r;
+    return reinterpret_cast<float4*>(a.grad + a.rlo[r] + (e - a.rpre[r]));
+  };
   const long nv = a.n / 4;                           // float4 vectors (host: n % (4 W) == 0)
   const long sv = nv / W;                            // vectors per slice
   // block b's share of every slice: [lo, hi) in slice-local vector units
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
   for (int s = 0; s < W; ++s) {
     for (long v = lo + t; v < hi; v += kThreads) {
       const long i = (long)s * sv + v;
-      const float4 g = grad[i];
+      const float4 g = *gv(i);
       put4<BF16>(mine, i, F4{g.x, g.y, g.z, g.w});
     }
   }
@@ -149,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
     }
     acc = round_wire<BF16>(acc);
     put4<BF16>(mine, i, acc);
-    grad[i] = make_float4(acc.x, acc.y, acc.z, acc.w);
+    *gv(i) = make_float4(acc.x, acc.y, acc.z, acc.w);
   }
   signal_all(a, b, 2u * k + 2u);
   if (!wait_all(a, b, 2u * k + 2u)) return;
@@ -162,7 +169,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
       const int q = (r + d) % W;                      // stagger peers across links
       const long i = (long)q * sv + v;
       const F4 x = get4<BF16>(stage(q), i);
-      grad[i] = make_float4(x.x, x.y, x.z, x.w);
+      *gv(i) = make_float4(x.x, x.y, x.z, x.w);
     }
   }
   if (t == 0) a.seq[b] = k + 1u;

@@ -38,6 +38,40 @@ log = logging.getLogger(__name__)
 _CAPTURE_MODE = 'thread_local'
 _AR_FORK = os.environ.get('DQN_AR_FORK', '0') == '1'
 
+def _reduce_ranges(layout, total: int, excluded, forbidden=(), max_ranges: int = 8):
+    """The pieces of the flat gradient a data-parallel step still all-reduces: every layout
+    tensor not inside an ``excluded`` range, each rounded up to 64 elements (tensor offsets are
+    64-aligned, so the padding stays inside the tensor's slot), adjacent pieces merged, and while
+    more than ``max_ranges`` remain the two pieces with the smallest gap between them merged --
+    never across a ``forbidden`` range (values that are already the global sum). None when that
+    cannot get below ``max_ranges``."""
+    ex = sorted(excluded)
+    keep = []
+    for n in layout.names:
+        lo = layout.offsets[n]
+        hi = lo + layout.numel(n)
+        if any(a <= lo and hi <= b for a, b in ex):
+            continue
+        assert lo % 64 == 0, 'layout offsets are 64-aligned'
+        keep.append([lo, min(total, (hi + 63) // 64 * 64)])
+    keep.sort()
+    out = []
+    for lo, hi in keep:
+        if out and lo <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], hi)
+        else:
+            out.append([lo, hi])
+    while len(out) > max_ranges:
+        ok = [j for j in range(len(out) - 1)
+              if not any(out[j][1] < b and a < out[j + 1][0] for a, b in forbidden)]
+        if not ok:
+            return None
+        i = min(ok, key=lambda j: out[j + 1][0] - out[j][1])
+        out[i][1] = out[i + 1][1]
+        del out[i + 1]
+    return [tuple(r) for r in out]
+
+
 class Learner:
     def __init__(self, network: Network, replay, config, ctx: Optional[DistContext] = None,
                  use_graph: Optional[bool] = None, ps_client=None, actor=None):
@@ -61,7 +95,9 @@ class Learner:
         if (self.ctx.enabled and ps_client is None and int(getattr(config, 'lowrank_dense', 1))
                 and getattr(config, 'overlap_allreduce', True) and hasattr(network.executor, 'lowrank_spec')
                 and getattr(config, 'allreduce_dtype', 'fp32') == 'fp32'):
-            lr = network.executor.lowrank_spec(B)
+            tau = min(1.0, float(config.target_update_tau))
+            lr = network.executor.lowrank_spec(
+                B, sigma_fused=network.fuses_sigma_grads(config.target_update_freq if tau >= 1.0 else None))
         self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb,
                                       'rccl' if ps_client is not None else config.allreduce, config.allreduce_dtype,
                                       gather_bytes=lr['gather_bytes'] if lr else 0)
@@ -69,15 +105,10 @@ class Learner:
         self._ar_ranges = []
         if lr and self.reducer.in_graph and self.reducer.can_gather:
             W = self.ctx.world_size
-            ranges, lo = [], 0
-            for a, b in sorted(lr['ranges']):
-                if a > lo:
-                    ranges.append((lo, a))
-                lo = b
-            if lo < network.grad.numel():
-                ranges.append((lo, network.grad.numel()))
+            ranges = _reduce_ranges(network.layout, network.grad.numel(), lr['ranges'] + lr.get('skip', []),
+                                    forbidden=lr['ranges'])
             # (Nature: one remaining range; dueling: two, one launch each in stream order)
-            if all((hi - lo_) % (4 * W) == 0 for lo_, hi in ranges):
+            if ranges and all((hi - lo_) % (4 * W) == 0 for lo_, hi in ranges):
                 self._lowrank = {'gather': self.reducer.xgmi.allgather2, 'world': W, 'rank': self.ctx.rank}
                 self._ar_ranges = ranges
         self.tau = min(1.0, float(config.target_update_tau))
@@ -236,8 +267,10 @@ class Learner:
             # the fc weight gradient is already the global sum (formed from the all-gathered
             # factors on the tail's joined branch): reduce only the remaining ranges
             self._tail()
-            for c, (lo, hi) in enumerate(self._ar_ranges):
-                self.reducer.allreduce_range(lo, hi, channel=c % 2)
+            if len(self._ar_ranges) == 1:
+                self.reducer.allreduce_range(*self._ar_ranges[0], channel=0)
+            else:                                    # every remaining piece in ONE launch
+                self.reducer.xgmi.allreduce_ranges(self.net.grad, self._ar_ranges, channel=0)
             return
         if self._tail is None or self._dense_hi <= 0 or not _AR_FORK:
             self._run_tail()

@@ -478,22 +478,27 @@ class HipExecutor:
             self.repack(target)
 
     # ------------------------------------------------------------ streams
-    def lowrank_spec(self, B: int):
+    def lowrank_spec(self, B: int, sigma_fused: bool = False):
         """Low-rank DP exchange of the fc (hidden dense) layer's weight gradient, when this
         executor's grouped-wgrad Nature path runs at this batch: dW = X^T dH has rank <= B, so
         instead of all-reducing dW (1.6M values per hidden layer) the ranks all-gather X (the fc
         input rows, B x F) and dH (B x HH) and every rank forms the summed dW over all W*B rows
         itself -- bit-identical on every rank (one fixed-order, atomic-free launch). Returns
         {'ranges': [(lo, hi), ...] of the fc weight tensors in the flat buffer (the caller
-        all-reduces the complement), 'gather_bytes': per-rank payload} or None."""
-        if (self.arch.network != 'nature' or self.noisy or not self.grouped_wgrad or self.two_stream
-                or B > 32):
+        all-reduces the complement), 'skip': ranges whose gradient is never read (noisy nets with
+        ``sigma_fused``: the sigma tensors, whose gradient the fused optimizer derives from the
+        all-reduced mu gradient), 'gather_bytes': per-rank payload} or None. Noisy nets: the
+        factors are those of dL/dW_eff, which IS the mu gradient."""
+        if (self.arch.network != 'nature' or (self.noisy and not sigma_fused) or not self.grouped_wgrad
+                or self.two_stream or B > 32):
             return None
         lay = self.layout
         names = ['value/fcl/w', 'advantage/fcl/w'] if self.dueling else ['fcl/w']
         if not all(n in lay.offsets for n in names):
             return None
-        return {'ranges': [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in names],
+        skip = [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in lay.names
+                if self.noisy and (n.endswith('/w_sigma') or n.endswith('/b_sigma'))]
+        return {'ranges': [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in names], 'skip': skip,
                 'gather_bytes': B * (self.FLAT + self.HH) * self.esz}
 
     def _lowrank_ws(self, B: int, W: int, dev) -> dict:
@@ -781,9 +786,9 @@ class HipExecutor:
                       split: bool = False, sigma_grads: bool = True, draw_noise=None, lowrank=None):
         """lowrank (data parallelism, see ``lowrank_spec``): {'gather': f(srcs, outs, nbytes) (an
         in-stream all-gather of two byte segments), 'world', 'rank'}. With ``split``, the fc weight
-        gradient is then formed from the all-gathered factors on a graph branch beside the dgrad
-        chain (ranks != 0 store zeros into the fc bias gradient, so the caller's all-reduce of the
-        remaining range sums it exactly once) and ``tail()`` joins that branch.
+        gradient is then formed from the all-gathered factors right after the head, in stream order
+        (ranks != 0 store zeros into the fc bias gradient, so the caller's all-reduce of the
+        remaining range sums it exactly once).
 
         sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
         optimizer derives dL/dsigma from the mu-slot gradient and the noise itself.
@@ -925,9 +930,12 @@ class HipExecutor:
             noisy = self.noisy and gnoise is not None
             side = None
             if split and not noisy and lowrank is not None:
-                assert self.lowrank_spec(B) is not None, 'low-rank exchange not available for this net / batch'
+                # (noisy nets reach here only with the sigma gradients left to the fused optimizer)
+                assert self.lowrank_spec(B, sigma_fused=True) is not None, 'low-rank exchange not available here'
                 W, rk = int(lowrank['world']), int(lowrank['rank'])
                 lw = self._lowrank_ws(B, W, dev)
+                if self.dist:                              # C51: dH = dlogits [W | Wv]^T * (h > 0) first
+                    self._c51_dh(ws, B, po)
                 # in stream order (a graph fork / join costs ~25 us on this ROCm: measured,
                 # scripts/probe_graph_concurrency.py), right after the head: x3 and dh are final
                 lowrank['gather']([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
@@ -937,7 +945,7 @@ class HipExecutor:
                 ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
                                lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
                                mloop=(W * B + 63) // 64, db_zero=rk != 0)
-                fc_dgrad()
+                self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True)
                 # the output layer's members join the conv members in the tail's grouped launch
                 members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]
             elif split and not noisy:

@@ -159,6 +159,15 @@ class XgmiAllReduce:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return int(flag) == 1
 
+    def allreduce_ranges(self, flat: torch.Tensor, ranges, channel: int = 0):
+        """Sum of several disjoint element ranges [(lo, hi), ...] of ``flat`` (ascending, each a
+        multiple of 4 long, total % (4 world) == 0) as ONE vector in ONE launch."""
+        ch = self.channels[channel]
+        flat_r = [int(v) for lo, hi in ranges for v in (lo, hi)]
+        n = sum(hi - lo for lo, hi in ranges)
+        self.ext.xgmi_allreduce(flat, ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.cap, self.ctx.rank,
+                                self.ctx.world_size, self.bf16, self.blocks_for(n), flat_r)
+
     def allreduce(self, t: torch.Tensor, channel: int = 0, blocks: Optional[int] = None):
         ch = self.channels[channel]
         self.ext.xgmi_allreduce(t, ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.cap, self.ctx.rank,

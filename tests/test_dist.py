@@ -290,3 +290,30 @@ def _worker_sync_owned_target(rank, world, port, tmpdir):
 
 def test_sync_dp_owned_target_broadcast(tmp_path):
     mp.spawn(_worker_sync_owned_target, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn', '--dueling --double_dqn --distributional --noisy'])
+def test_lowrank_reduce_ranges_cover_every_summed_tensor(extra):
+    """Low-rank DP: the all-reduce pieces cover every tensor whose gradient is still per-rank,
+    never touch the fc weights (already the global sum), skip the noisy sigma tensors (derived in
+    the optimizer), stay 64-element multiples and fit one multi-range launch."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import _reduce_ranges
+    from dist_dqn_amd.models.network import Network
+    cfg = preset('nature', 'Pong-v0', '--seed=0 --backend=torch ' + extra)
+    lay = Network.create_network(cfg, (84, 84, 4), 6).layout
+    names = ['value/fcl/w', 'advantage/fcl/w'] if '--dueling' in extra else ['fcl/w']
+    fc = [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in names]
+    skip = [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in lay.names if n.endswith('_sigma')]
+    r = _reduce_ranges(lay, lay.total, fc + skip, forbidden=fc)
+    assert r and len(r) <= 8
+    assert all(lo % 64 == 0 and (hi - lo) % 64 == 0 for lo, hi in r)
+    assert all(hi <= a or lo >= b for lo, hi in r for a, b in fc)
+    for n in lay.names:
+        lo, hi = lay.offsets[n], lay.offsets[n] + lay.numel(n)
+        if (lo, hi) in fc or (lo, hi) in skip:
+            continue
+        assert any(a <= lo and hi <= b for a, b in r), n
+    # forced merging never crosses an fc range
+    r2 = _reduce_ranges(lay, lay.total, fc + skip, forbidden=fc, max_ranges=2)
+    assert r2 is None or all(hi <= a or lo >= b for lo, hi in r2 for a, b in fc)

@@ -115,6 +115,16 @@ def _worker_xgmi(rank, world, port, wire, errq):
             torch.cuda.synchronize()
             assert torch.equal(out[0], segs[0].reshape(-1)) and torch.equal(out[1], segs[1].reshape(-1)), call
             assert bool((t == world * (world + 1) / 2).all())
+        # several disjoint pieces of one buffer summed as ONE vector (the low-rank step's remainder)
+        flat = torch.full((8192,), float(rank + 1), device='cuda')
+        pieces = [(64, 192), (1024, 1088), (4096, 8192)]
+        y.allreduce_ranges(flat, pieces, channel=1)
+        torch.cuda.synchronize()
+        mask = torch.zeros(8192, dtype=torch.bool, device='cuda')
+        for lo, hi in pieces:
+            mask[lo:hi] = True
+        s = world * (world + 1) / 2
+        assert bool((flat[mask] == s).all()) and bool((flat[~mask] == rank + 1).all())
         assert y.check()
         y.close()
         dist.barrier()
@@ -175,7 +185,7 @@ def _worker(rank, world, port, network, extra, errq):
                 ln.reducer.check()
                 # the fc weight gradient travels as all-gathered factors (overlap=1, Nature,
                 # no noisy layers, fp32 wire); overlap=0 is the full all-reduce it is compared with
-                lowrank = bool(overlap) and network == 'nature' and '--noisy' not in extra and 'bf16' not in extra
+                lowrank = bool(overlap) and network == 'nature' and 'bf16' not in extra
                 assert (ln._lowrank is not None) == lowrank, (overlap, extra)
             elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
