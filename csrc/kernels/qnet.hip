@@ -732,13 +732,15 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
 // store 0 into the bias gradient (ranks != 0: the caller's all-reduce then sums it once).
 template <class LD, int MC, int KB, int NB>
 DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, int bz, act_t* lds) {
-  constexpr int LR = MC + 8;
+  constexpr int LR = MC + 8;                     // fp32 build: [k][m] / [n][m] rows
+  constexpr int SA = KB + 16, SZ = NB + 16;      // 16-bit builds: row-major [m][k] / [m][n] (see WgradTile)
   constexpr int TPR = 256 / MC;
   constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
   constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
-  static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0 && NB <= 256, "tiling");
+  static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0 && 256 % NB == 0,
+                "tiling");
   act_t* At = lds;
-  act_t* Zt = lds + KB * LR;
+  act_t* Zt = lds + (DQN_ACT_F32 ? KB * LR : MC * SA);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int k_lo = by * KB, n_lo = bz * NB;
   const int kg = 8 * (lane >> 4), row = lane & 15;
@@ -749,9 +751,10 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
   for (int i = 0; i < PERW; ++i) accs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
   const int r = threadIdx.x % MC, p = threadIdx.x / MC;
-  bfx8 va[GA], vz[GZ];
-  // chunk c's fragments into registers (issued one chunk ahead: they fly under chunk c-1's MFMAs)
-  auto load = [&](int c) {
+  // chunk c's fragments into registers; the loads of up to kGrp chunks are issued in ONE batch
+  // (one memory round trip per kGrp chunks instead of one per chunk)
+  constexpr int kGrp = 4;
+  auto load = [&](int c, bfx8* va, bfx8* vz) {
     const int m = c * MC + r;
     const bool mok = m < a.M;
     const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
@@ -768,27 +771,42 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
   };
-  load(0);
-  for (int c = 0; c < nch; ++c) {
+  for (int c0 = 0; c0 < nch; c0 += kGrp) {
+    bfx8 va[kGrp][GA], vz[kGrp][GZ];
+#pragma unroll
+    for (int u = 0; u < kGrp; ++u)
+      if (c0 + u < nch) load(c0 + u, va[u], vz[u]);
+#pragma unroll
+    for (int u = 0; u < kGrp; ++u) {
+    const int c = c0 + u;
+    if (c >= nch) break;
     if (c > 0) __syncthreads();                    // the previous chunk's LDS reads are done
+#if DQN_ACT_F32
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int c8 = (p + i * TPR) * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + r] = va[i][j];
+      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + r] = va[u][i][j];
     }
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[i][j];
+      for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[u][i][j];
     }
-    if (c + 1 < nch) load(c + 1);
+#else
+    // one ds_write_b128 per fragment; the MFMA operands come back through transposed reads
+#pragma unroll
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (p + i * TPR) * 8) = va[u][i];
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[u][i];
+#endif
     __syncthreads();
-    if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
-      const act_t* zr = Zt + threadIdx.x * LR;
-#pragma unroll 8
-      for (int q = 0; q < MC; ++q) dbs += (float)zr[q];
+#if DQN_ACT_F32
+    if (g.db != nullptr && by == 0) {           // column tid % NB, rows tid / NB + k * (256 / NB)
+      const act_t* zr = Zt + ((int)threadIdx.x % NB) * LR;
+#pragma unroll 4
+      for (int q = (int)threadIdx.x / NB; q < MC; q += 256 / NB) dbs += (float)zr[q];
     }
 #pragma unroll
     for (int i = 0; i < PERW; ++i) {
@@ -801,12 +819,43 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
         accs[i] = mfma16(af, bf, accs[i]);
       }
     }
+#else
+    if (g.db != nullptr && by == 0) {           // column tid % NB, rows tid / NB + k * (256 / NB)
+#pragma unroll 4
+      for (int q = (int)threadIdx.x / NB; q < MC; q += 256 / NB) dbs += (float)Zt[q * SZ + (int)threadIdx.x % NB];
+    }
+    // (the same reduction-index permutation on both operands as wgrad_block's 16-bit body)
+    const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+#pragma unroll
+    for (int i = 0; i < PERW; ++i) {
+      const int tile = wave + 4 * i;
+      const int kt = tile / NTt, nt = tile - kt * NTt;
+      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
+      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
+        const bfx8 bf = join_tr(lds_tr16(pz + 32 * s * SZ), lds_tr16(pz + (32 * s + 16) * SZ));
+        accs[i] = mfma16(af, bf, accs[i]);
+      }
+    }
+#endif
+    }
   }
-  if (g.db != nullptr && by == 0 && (int)threadIdx.x < NB) {
-    const int nn = n_lo + threadIdx.x;
-    if (nn < g.N) {
-      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
-      *pdb = g.db_zero ? 0.f : dbs * kInvLossScale;
+  if (g.db != nullptr && by == 0) {
+    // the 256 / NB row-group partials of each column, summed in a fixed order
+    __syncthreads();                               // every chunk's LDS reads are done
+    float* red = reinterpret_cast<float*>(lds);
+    red[threadIdx.x] = dbs;
+    __syncthreads();
+    if ((int)threadIdx.x < NB) {
+      float sum = 0.f;
+      for (int q = 0; q < 256 / NB; ++q) sum += red[q * NB + threadIdx.x];
+      const int nn = n_lo + threadIdx.x;
+      if (nn < g.N) {
+        float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+        *pdb = g.db_zero ? 0.f : sum * kInvLossScale;
+      }
     }
   }
 #pragma unroll
@@ -828,7 +877,7 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
 
 template <class LD, int MC, int KB, int NB>
 __global__ void __launch_bounds__(256) wgrad_multi_kernel(ConvArgs a, WgradArgs g) {
-  __shared__ __attribute__((aligned(16))) act_t lds[(KB + NB) * (MC + 8)];
+  __shared__ __attribute__((aligned(16))) act_t lds[DQN_ACT_F32 ? (KB + NB) * (MC + 8) : MC * (KB + NB + 32)];
   wgrad_block_multi<LD, MC, KB, NB>(a, g, blockIdx.y, blockIdx.z, lds);
 }
 
@@ -1204,8 +1253,16 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
     case L_HEAD_WGRAD: WGRAD_LAUNCH(DenseLoader, 32, 64, 64); return 0;
     case L_DENSE_WGRAD_LR: {                     // ONE block per weight tile over all g.mloop 64-row chunks
       if (g.mloop < 1 || 64 * g.mloop < a.M) return -1;
-      dim3 grid(1, (a.K + 63) / 64, (g.N + 127) / 128);
-      hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 64, 128>), grid, dim3(256), 0, st, a, g);
+      // tiles per block: 32 x 64 (default: 784 blocks for Nature's fc, measured 11.0 vs 11.7 us at
+      // W = 8 alone) or 64 x 128 (DQN_LR_KB=64)
+      static const int kb = getenv("DQN_LR_KB") ? atoi(getenv("DQN_LR_KB")) : 32;
+      if (kb == 32) {
+        dim3 grid(1, (a.K + 31) / 32, (g.N + 63) / 64);
+        hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 32, 64>), grid, dim3(256), 0, st, a, g);
+      } else {
+        dim3 grid(1, (a.K + 63) / 64, (g.N + 127) / 128);
+        hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 64, 128>), grid, dim3(256), 0, st, a, g);
+      }
       return 0;
     }
     default: return -1;
