@@ -59,6 +59,9 @@ def main():
                          'rainbow = C51 + noisy nets + dueling + double + PER + Adam')
     ap.add_argument('--fuse_acting', type=int, default=1,
                     help='run the device actors\' step inside the learner step\'s launches when possible')
+    ap.add_argument('--graph_steps', type=int, default=8,
+                    help='SGD steps per HIP-graph launch (Learner.step_many: the same per-step work, one host '
+                         'launch per G steps -- the inter-graph gap is amortised); 1 = one graph per step')
     args = ap.parse_args()
 
     import shlex
@@ -98,14 +101,29 @@ def main():
             actor.step()
         learner.step()
 
-    for _ in range(args.warmup):
+    # G steps per graph launch when the whole step is one in-graph body (fused or no acting)
+    G = max(1, args.graph_steps) if (actor is None or fused) and args.graph else 1
+
+    def run(n):
+        if G > 1:
+            for _ in range(n // G):
+                learner.step_many(G)
+            n %= G
+        for _ in range(n):
+            step()
+
+    # warm-up: eager steps, the one-step graph capture, then (G > 1) the G-step graph's capture
+    # and first replay -- W steps in all when W >= G + 3, else W single steps + one G-step launch
+    w1 = args.warmup - G if G > 1 and args.warmup >= G + 3 else args.warmup
+    for _ in range(w1):
         step()
+    if G > 1:
+        learner.step_many(G)
     ctx.barrier()
     torch.cuda.synchronize(dev)
     frames0 = actor.env_frames if actor is not None else 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run(args.steps)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     el = time.perf_counter() - t0
@@ -137,7 +155,7 @@ def main():
                        'global_batch': args.batch * ctx.world_size, 'seq_len': None,
                        'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
                        'frames_per_state': 4, 'optimizer': cfg.optimizer + '(tf)', 'executor': net.executor.name,
-                       'hip_graph': bool(args.graph), 'actor_envs': args.actor_envs,
+                       'hip_graph': bool(args.graph), 'steps_per_graph_launch': G, 'actor_envs': args.actor_envs,
                        'acting': 'fused into the learner launches' if fused else 'separate launches',
                        'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
                        'num_actions': args.actions, 'variant': args.variant, 'extra': args.extra,

@@ -383,7 +383,9 @@ class Learner:
         consecutive step bodies (host-light learner loops, e.g. Ape-X, whose Python thread
         shares the GIL with the inference service); otherwise k ``step()`` calls."""
         k = int(k)
-        single = self.ps is None and not self.ctx.enabled and self.actor is None
+        # (the whole step must be ONE in-graph body: single process, or sync DP over the xgmi
+        # kernels; fused acting rides along -- its state is device-side)
+        single = (self.ps is None and (not self.ctx.enabled or self.reducer.in_graph) and not self._own_target)
         if k <= 1 or not single or not self.use_graph or self._graphs is None:
             for _ in range(max(1, k)):
                 self.step()
@@ -397,11 +399,16 @@ class Learner:
             with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
                 for _ in range(k):
                     self._sample_and_grad()
+                    if self.ctx.enabled:
+                        self._kernel_allreduce()
                     self._apply()
             torch.cuda.current_stream(self.device).wait_stream(s)
             self._graph_many = g = (k, gk)
         with trace('learner.step_many'):
             g[1].replay()
+        if self.reducer.xgmi is not None and (self.train_steps + k) // self._xgmi_check_every \
+                != self.train_steps // self._xgmi_check_every:
+            self.reducer.check()
         self.train_steps += k
         return self.loss
 

@@ -616,3 +616,44 @@ def test_device_actor_inserts_max_priority(network, extra):
         mn = mn.view(-1, 2).min(1).values
     torch.testing.assert_close(s[1], lvl[0], rtol=1e-5, atol=1e-3)
     assert float(m[1]) == float(mn[0])
+
+
+@pytest.mark.parametrize('extra', ['', '--prioritized_replay ' + RAINBOW + ' --optimizer=adam'])
+def test_step_many_with_fused_acting_equals_single_steps(extra):
+    """k SGD steps replayed from ONE k-step graph (Learner.step_many, fused device acting riding
+    in every step) == k one-step graph replays: same replay cursor / actor frames / global step,
+    parameters equal up to the conv-gradient atomics' arrival order."""
+    from dist_dqn_amd.actors.device_actor import DeviceActor
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    outs = []
+    for many in (False, True):
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 ' + extra)
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized='--prioritized_replay' in extra)
+        rep.fill_synthetic(4096, 6, seed=5)
+        actor = DeviceActor(net, rep, cfg, num_envs=4, steps_per_call=1, seed=1000)
+        ln = Learner(net, rep, cfg, use_graph=True, actor=actor)
+        assert ln.actor is not None
+        init = net.online.flat.clone()
+        for _ in range(4):
+            ln.step()
+        if many:
+            ln.step_many(8)
+            ln.step_many(8)
+        else:
+            for _ in range(16):
+                ln.step()
+        torch.cuda.synchronize()
+        assert ln.train_steps == 20 and int(net.global_step) == 20
+        outs.append((net.online.flat.clone(), rep.cursor.clone(), actor.env_frames))
+    (f0, c0, e0), (f1, c1, e1) = outs
+    assert torch.equal(c0, c1) and e0 == e1 == 20 * 4
+    if '--optimizer=adam' in extra:     # (see test_per_fused_in_optimizer_equals_separate_launches)
+        cos = float(torch.nn.functional.cosine_similarity(f1 - init, f0 - init, dim=0))
+        ratio = float((f1 - init).norm() / ((f0 - init).norm() + 1e-30))
+        assert cos > 0.98 and abs(ratio - 1) < 0.03, (cos, ratio)
+    else:
+        torch.testing.assert_close(f1, f0, rtol=1e-4, atol=1e-6)
