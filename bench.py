@@ -101,8 +101,9 @@ def main():
             actor.step()
         learner.step()
 
-    # G steps per graph launch when the whole step is one in-graph body (fused or no acting)
-    G = max(1, args.graph_steps) if (actor is None or fused) and args.graph else 1
+    # G steps per graph launch when the whole step is one in-graph body (fused or no acting) of
+    # ONE process (data parallelism keeps one graph per step: Learner.step_many)
+    G = max(1, args.graph_steps) if (actor is None or fused) and args.graph and not ctx.enabled else 1
 
     def run(n):
         if G > 1:

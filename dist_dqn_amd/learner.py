@@ -383,9 +383,11 @@ class Learner:
         consecutive step bodies (host-light learner loops, e.g. Ape-X, whose Python thread
         shares the GIL with the inference service); otherwise k ``step()`` calls."""
         k = int(k)
-        # (the whole step must be ONE in-graph body: single process, or sync DP over the xgmi
-        # kernels; fused acting rides along -- its state is device-side)
-        single = (self.ps is None and (not self.ctx.enabled or self.reducer.in_graph) and not self._own_target)
+        # (single process only -- fused acting rides along, its state is device-side. Sync DP
+        # over the xgmi kernels would capture too, but measured with 2 ranks (one GPU, shared or
+        # disjoint CU masks: profiles/r2_dp_multistep_graphs.md) 8-step graphs ran 3x SLOWER than
+        # one-step graphs, so DP keeps one graph per step)
+        single = self.ps is None and not self.ctx.enabled
         if k <= 1 or not single or not self.use_graph or self._graphs is None:
             for _ in range(max(1, k)):
                 self.step()
