@@ -119,7 +119,11 @@ def main():
     for _ in range(w1):
         step()
     if G > 1:
-        learner.step_many(G)
+        for _ in range(3):                      # (tiny W: the one-step graph must exist first)
+            if learner._graphs is not None:
+                break
+            step()
+        learner.step_many(G)                    # captures the G-step graph outside the timed region
     ctx.barrier()
     torch.cuda.synchronize(dev)
     frames0 = actor.env_frames if actor is not None else 0
