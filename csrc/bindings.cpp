@@ -533,6 +533,37 @@ void xgmi_allgather(std::vector<int64_t> srcs, std::vector<int64_t> outs, std::v
   TORCH_CHECK(launch_xgmi_allgather(g, (int)blocks, cur_stream()) == 0, "xgmi gather: launch arguments");
 }
 
+// the XgmiGatherArgs bytes (CPU uint8) of a gather over this channel: the fc dgrad launch's
+// gather side duty reads them from device memory (copied there by the caller)
+torch::Tensor xgmi_gather_args(std::vector<int64_t> srcs, std::vector<int64_t> outs, std::vector<int64_t> bytes,
+                               std::vector<int64_t> data, std::vector<int64_t> sig, int64_t seq, int64_t err,
+                               int64_t cap, int64_t rank, int64_t world) {
+  TORCH_CHECK(world >= 1 && world <= dqn::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi gather: rank/world");
+  TORCH_CHECK((int64_t)data.size() == world && (int64_t)sig.size() == world && seq && err, "xgmi gather: pointers");
+  TORCH_CHECK(srcs.size() == 2 && outs.size() == 2 && bytes.size() == 2, "xgmi gather: two segments");
+  dqn::XgmiGatherArgs g{};
+  for (int i = 0; i < world; ++i) {
+    TORCH_CHECK(data[i] && sig[i], "xgmi gather: null peer pointer");
+    g.x.data[i] = reinterpret_cast<void*>(data[i]);
+    g.x.sig[i] = reinterpret_cast<uint32_t*>(sig[i]);
+  }
+  for (int q = 0; q < 2; ++q) {
+    TORCH_CHECK(srcs[q] && outs[q] && bytes[q] >= 0 && bytes[q] % 16 == 0 && (srcs[q] & 15) == 0 && (outs[q] & 15) == 0,
+                "xgmi gather: 16-byte aligned segments, sizes % 16 == 0");
+    g.src[q] = reinterpret_cast<const void*>(srcs[q]);
+    g.out[q] = reinterpret_cast<void*>(outs[q]);
+    g.bytes[q] = bytes[q];
+  }
+  TORCH_CHECK(bytes[0] + bytes[1] <= cap, "xgmi gather: payload exceeds the channel's staging");
+  g.x.seq = reinterpret_cast<uint32_t*>(seq);
+  g.x.err = reinterpret_cast<int*>(err);
+  g.x.cap = cap;
+  g.x.rank = (int)rank; g.x.world = (int)world;
+  auto out = torch::empty({(int64_t)sizeof(g)}, torch::kUInt8);
+  std::memcpy(out.data_ptr(), &g, sizeof(g));
+  return out;
+}
+
 // ---------------------------------------------------------------- fused MLP
 // ints: [L, A, P, Hs, Ds, sw, B, double, huber, fin x4, fout x4, act x4, w_off x4, b_off x4]
 // ptrs: [w_on, w_tg, x, xn, act, rew, done, gam, wts, loss, prio, grad, q_out] (0 = unused)
@@ -588,6 +619,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("seq"), pybind11::arg("err"), pybind11::arg("cap"), pybind11::arg("rank"), pybind11::arg("world"),
         pybind11::arg("bf16"), pybind11::arg("blocks"), pybind11::arg("ranges") = std::vector<int64_t>{});
   m.def("xgmi_allgather", &xgmi_allgather);
+  m.def("xgmi_gather_args", &xgmi_gather_args);
   m.attr("XGMI_MAX_BLOCKS") = dqn::kXgmiMaxBlocks;
   m.attr("XGMI_SIG_WORDS") = dqn::kXgmiMaxRanks * dqn::kXgmiMaxBlocks;
   m.def("replay_gather_frames", &replay_gather_frames);

@@ -49,6 +49,9 @@ struct ConvArgs {
   // advanced later by the fused optimizer's last block (every block of this launch read it)
   float* nz_out0; float* nz_out1; int nz_n;
   const int64_t* nz_rng;
+  // data parallelism, low-rank exchange: the blocks of grid.z == gth_z run the xgmi all-gather of
+  // the fc factors (the first gth_blocks of them; args: a device XgmiGatherArgs) beside the GEMM
+  const void* gth; int gth_blocks, gth_z;
 };
 
 struct WgradArgs {

@@ -22,6 +22,7 @@
 #include "common.h"
 #include "actor_dev.h"
 #include "../include/dqn_nets_k.h"
+#include "xgmi_dev.h"
 
 namespace dqn {
 
@@ -300,6 +301,13 @@ template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U =
 __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   static_assert(WM * WN * KSPLIT == 4 || WM * WN * KSPLIT == 8, "4 or 8 waves per block");
   __shared__ float red[KSPLIT > 1 ? WM * WN * (KSPLIT - 1) * MT * NT * 256 : 1];
+  if (a.gth != nullptr && (int)blockIdx.z == a.gth_z) {
+    // side duty: the low-rank DP all-gather (its own grid.z slice; every block of it returns
+    // here, uniformly, before any barrier of the GEMM body)
+    const int gb = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    if (gb < a.gth_blocks) xgmi_gather_block(*reinterpret_cast<const XgmiGatherArgs*>(a.gth), gb, a.gth_blocks);
+    return;
+  }
   const int inst = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wk = wave % KSPLIT, wn = (wave / KSPLIT) % WN, wm = wave / (KSPLIT * WN);
@@ -371,7 +379,7 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   }
   // noise duty (every thread of the block, before the split-K waves retire)
   if (a.nz_out0 != nullptr) {
-    const int nblk = gridDim.x * gridDim.y * gridDim.z;
+    const int nblk = gridDim.x * gridDim.y * (gridDim.z - (a.gth != nullptr ? 1 : 0));   // (GEMM blocks only)
     const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     const int nq = ((a.nz_out1 != nullptr ? 2 : 1) * a.nz_n + 3) / 4;
     const int nt = blockDim.x, tq = (int)threadIdx.x;
@@ -404,7 +412,7 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   // side duties of the launch (ConvArgs aux): zero a gradient range (the conv weight gradients
   // accumulate into it with atomics later in the step) and sum the head's per-tile loss partials
   if (a.zero_ptr != nullptr) {
-    const int nblk = gridDim.x * gridDim.y * gridDim.z;
+    const int nblk = gridDim.x * gridDim.y * (gridDim.z - (a.gth != nullptr ? 1 : 0));   // (GEMM blocks only)
     const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
     for (int t = blk * 64 + lane; t < a.zero_n / 4; t += nblk * 64) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1165,7 +1173,9 @@ void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs
 constexpr int kLoadBatch(int u) { return DQN_ACT_F32 ? (u + 1) / 2 : u; }
 #define IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, U)                                                \
   do {                                                                                                  \
-    dim3 grid((a.M + WM * MT * 16 - 1) / (WM * MT * 16), (a.N + WN * NT * 16 - 1) / (WN * NT * 16), ninst); \
+    dim3 grid((a.M + WM * MT * 16 - 1) / (WM * MT * 16), (a.N + WN * NT * 16 - 1) / (WN * NT * 16),             \
+              ninst + (a.gth != nullptr ? 1 : 0));                                                                \
+    if (a.gth != nullptr && (a.gth_z != ninst || (int)(grid.x * grid.y) < a.gth_blocks)) return -2;                \
     hipLaunchKernelGGL((igemm_kernel<LD, MT, NT, WM, WN, KS, EPI, kLoadBatch(U)>), grid, dim3(64 * WM * WN * KS), 0, st, a); \
   } while (0)
 #define IGEMM_LAUNCH(LD, MT, NT, WM, WN, KS, EPI) IGEMM_LAUNCH_U(LD, MT, NT, WM, WN, KS, EPI, 4)

@@ -1,0 +1,88 @@
+// Peer-to-peer signalling over xGMI shared by the all-reduce / all-gather kernels
+// (xgmi_ar.hip) and the fc dgrad launch's gather side duty (qnet.hip): system-scope release
+// stores into the peers' signal words, bounded acquire polls of one's own.
+#pragma once
+#include "common.h"
+#include "../include/dqn_kernels.h"
+
+namespace dqn {
+
+constexpr uint64_t kXgmiTimeoutTicks = 1000000000ull;   // 10 s at 100 MHz
+
+DQN_DEV uint32_t load_acq(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+DQN_DEV void store_rel(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// publish this block's writes, then raise flag `val` for block b in every peer's signal words
+DQN_DEV void signal_all(const XgmiArgs& a, int b, uint32_t val) {
+  __threadfence_system();
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < a.world) store_rel(a.sig[t] + a.rank * kXgmiMaxBlocks + b, val);
+}
+
+// wait until every peer raised flag >= val for block b; false on timeout
+DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val) {
+  const int t = threadIdx.x;
+  __shared__ int timed_out;
+  if (t == 0) timed_out = 0;
+  __syncthreads();
+  if (t < a.world) {
+    const uint32_t* f = a.sig[a.rank] + t * kXgmiMaxBlocks + b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(load_acq(f) - val) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kXgmiTimeoutTicks) {
+        atomicExch(a.err, 1);
+        timed_out = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // system-scope acquire for every thread
+  return timed_out == 0;
+}
+
+
+// All-gather of two segments (one signal per call): A  my segments -> my staging, signal
+// "A done" (k + 1); C  every rank's chunk b -> out[s] + q * bytes[s]. Block b of every rank
+// handles chunk b of the concatenated payload, so it waits only for block b of its peers.
+// Staging alternates parity per call: a rank writes parity p again at call k + 2 only after
+// every peer signalled A of call k + 1, i.e. finished reading call k (its C of call k).
+DQN_DEV void xgmi_gather_block(const XgmiGatherArgs& g, int b, int G) {
+  const XgmiArgs& a = g.x;
+  const int t = threadIdx.x, NT = blockDim.x;
+  const int W = a.world, r = a.rank;
+  const uint32_t k = a.seq[b];
+  const long par = (long)(k & 1u);
+  auto stage = [&](int q) -> uint4* { return reinterpret_cast<uint4*>(reinterpret_cast<char*>(a.data[q]) + par * a.cap); };
+  const long v0 = g.bytes[0] / 16, v1 = g.bytes[1] / 16, nv = v0 + v1;
+  const long per = (nv + G - 1) / G;
+  const long lo = per * b < nv ? per * b : nv;
+  const long hi = per * (b + 1) < nv ? per * (b + 1) : nv;
+  DQN_ASSERT(16 * nv <= a.cap && b < kXgmiMaxBlocks);
+  const uint4* s0 = reinterpret_cast<const uint4*>(g.src[0]);
+  const uint4* s1 = reinterpret_cast<const uint4*>(g.src[1]);
+  uint4* mine = stage(r);
+  for (long v = lo + t; v < hi; v += NT) mine[v] = v < v0 ? s0[v] : s1[v - v0];
+  signal_all(a, b, k + 1u);
+  if (!wait_all(a, b, k + 1u)) return;
+  uint4* o0 = reinterpret_cast<uint4*>(g.out[0]);
+  uint4* o1 = reinterpret_cast<uint4*>(g.out[1]);
+  for (long v = lo + t; v < hi; v += NT) {
+    for (int d = 0; d < W; ++d) {
+      const int q = (r + d) % W;                      // stagger peers across links
+      const uint4 x = stage(q)[v];
+      if (v < v0) o0[(long)q * v0 + v] = x;
+      else o1[(long)q * v1 + (v - v0)] = x;
+    }
+  }
+  if (t == 0) a.seq[b] = k + 1u;
+}
+
+
+}  // namespace dqn

@@ -54,9 +54,18 @@ void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::v
   dqn::ConvArgs a = conv_args(in, w, bias, out, mask, scale, dims);
   if (!aux.empty()) {
     // + optional noise duty [out0, out1, n, rng]: the next noisy-net samples at the stream's counter
+    // + optional gather duty [gth (device XgmiGatherArgs), gth_blocks] at the end
+    size_t na = aux.size();
+    if (na == 7 || na == 11) {
+      TORCH_CHECK(aux[na - 2] != 0 && aux[na - 1] >= 1 && aux[na - 1] <= 256, "igemm gather duty: args, 1..256 blocks");
+      a.gth = P<const void*>(aux[na - 2]);
+      a.gth_blocks = (int)aux[na - 1];
+      a.gth_z = (int)in.size();
+      aux.resize(na - 2);
+    }
     TORCH_CHECK((aux.size() == 5 || aux.size() == 9) && aux_f.size() == 1 && aux[0] % 16 == 0 && aux[1] % 4 == 0 &&
                 aux[3] <= 64, "igemm aux = [zero_ptr, zero_n, loss_parts, nparts, loss_out(, nz_out0, nz_out1, "
-                "nz_n, nz_rng)], [loss_mul]");
+                "nz_n, nz_rng)(, gth, gth_blocks)], [loss_mul]");
     if (aux.size() == 9) {
       TORCH_CHECK(aux[5] != 0 && aux[7] >= 1 && aux[8] != 0, "igemm noise duty: out0, n, rng");
       a.nz_out0 = P<float*>(aux[5]); a.nz_out1 = P<float*>(aux[6]); a.nz_n = (int)aux[7];

@@ -109,7 +109,8 @@ class Learner:
                                     forbidden=lr['ranges'])
             # (Nature: one remaining range; dueling: two, one launch each in stream order)
             if ranges and all((hi - lo_) % (4 * W) == 0 for lo_, hi in ranges):
-                self._lowrank = {'gather': self.reducer.xgmi.allgather2, 'world': W, 'rank': self.ctx.rank}
+                self._lowrank = {'gather': self.reducer.xgmi.allgather2, 'gather_args': self.reducer.xgmi.gather_args,
+                                 'world': W, 'rank': self.ctx.rank}
                 self._ar_ranges = ranges
         self.tau = min(1.0, float(config.target_update_tau))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)

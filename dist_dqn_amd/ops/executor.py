@@ -740,7 +740,7 @@ class HipExecutor:
                             [po.data_ptr() + self.esz * self.poff['head/dgrad']], [], [ws['dh'].data_ptr()],
                             [ws['h'][0].data_ptr()], [1.0], [B, HH, self.c51_KD, HH // 16, HH, 0, 0, 0, 0, 0, 0])
 
-    def _fc_dgrad(self, ws, B, po, zero=(), draw_noise=None, dh_done=False):
+    def _fc_dgrad(self, ws, B, po, zero=(), draw_noise=None, dh_done=False, gather=None):
         """dz3 = (dH W_fc^T) * (x3 > 0) on the igemm kernel; the launch also zeroes the conv
         weight-gradient range and sums the head's loss partials (side duties). Scalar heads: the
         head kernel wrote dH; C51: dH = (dout16 [W | Wv]^T) * (h > 0) is one more igemm launch
@@ -758,6 +758,8 @@ class HipExecutor:
             o0, o1, rng = draw_noise
             assert o0.dtype == torch.float32 and (o1 is None or o1.numel() == o0.numel()) and rng.dtype == torch.int64
             aux += [o0.data_ptr(), o1.data_ptr() if o1 is not None else 0, o0.numel(), rng.data_ptr()]
+        if gather is not None:          # (device XgmiGatherArgs ptr, blocks): the low-rank all-gather duty
+            aux += [int(gather[0]), int(gather[1])]
         self.ext.qnet_igemm(_KIND['DDGRAD'], [dh], [pk], [], [dz3], [x3], [1.0],
                             [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0], aux, [1.0 / B])
 
@@ -937,15 +939,29 @@ class HipExecutor:
                 if self.dist:                              # C51: dH = dlogits [W | Wv]^T * (h > 0) first
                     self._c51_dh(ws, B, po)
                 # in stream order (a graph fork / join costs ~25 us on this ROCm: measured,
-                # scripts/probe_graph_concurrency.py), right after the head: x3 and dh are final
-                lowrank['gather']([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
-                                  [B * F * self.esz, B * HH * self.esz])
+                # scripts/probe_graph_concurrency.py), right after the head: x3 and dh are final.
+                # The all-gather runs as a side duty of the fc dgrad launch (its own grid.z slice)
+                # when the transport can hand out device args; else as its own launch first.
+                seg = ([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
+                       [B * F * self.esz, B * HH * self.esz])
+                ga = None
+                if lowrank.get('gather_args') is not None and os.environ.get('DQN_LR_FUSED_GATHER', '0') == '1':
+                    key = tuple(seg[0] + seg[1] + seg[2])
+                    cache = self.__dict__.setdefault('_lr_gargs', {})
+                    if key not in cache:
+                        cache[key] = lowrank['gather_args'](*seg)
+                    dev_args, nblk = cache[key]
+                    ga = (dev_args.data_ptr(), nblk)
+                    self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True, gather=ga)
+                else:
+                    lowrank['gather'](*seg)
                 # sum over all W*B rows in one block per weight tile (64-row chunks in a fixed
                 # order, no atomics: bit-identical on every rank)
                 ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
                                lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
                                mloop=(W * B + 63) // 64, db_zero=rk != 0)
-                self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True)
+                if ga is None:
+                    self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True)
                 # the output layer's members join the conv members in the tail's grouped launch
                 members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]
             elif split and not noisy:
