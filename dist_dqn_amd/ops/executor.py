@@ -945,7 +945,7 @@ class HipExecutor:
                 seg = ([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
                        [B * F * self.esz, B * HH * self.esz])
                 ga = None
-                if lowrank.get('gather_args') is not None and os.environ.get('DQN_LR_FUSED_GATHER', '0') == '1':
+                if lowrank.get('gather_args') is not None and os.environ.get('DQN_LR_FUSED_GATHER', '1') == '1':
                     key = tuple(seg[0] + seg[1] + seg[2])
                     cache = self.__dict__.setdefault('_lr_gargs', {})
                     if key not in cache:
