@@ -946,7 +946,8 @@ class HipExecutor:
                        [B * F * self.esz, B * HH * self.esz])
                 ga = None
                 if lowrank.get('gather_args') is not None and os.environ.get('DQN_LR_FUSED_GATHER', '1') == '1':
-                    key = tuple(seg[0] + seg[1] + seg[2])
+                    # (keyed by the transport object too: a new transport has new channel buffers)
+                    key = (id(getattr(lowrank['gather_args'], '__self__', None)),) + tuple(seg[0] + seg[1] + seg[2])
                     cache = self.__dict__.setdefault('_lr_gargs', {})
                     if key not in cache:
                         cache[key] = lowrank['gather_args'](*seg)
