@@ -946,12 +946,7 @@ class HipExecutor:
                        [B * F * self.esz, B * HH * self.esz])
                 ga = None
                 if lowrank.get('gather_args') is not None and os.environ.get('DQN_LR_FUSED_GATHER', '1') == '1':
-                    # (keyed by the transport object too: a new transport has new channel buffers)
-                    key = (id(getattr(lowrank['gather_args'], '__self__', None)),) + tuple(seg[0] + seg[1] + seg[2])
-                    cache = self.__dict__.setdefault('_lr_gargs', {})
-                    if key not in cache:
-                        cache[key] = lowrank['gather_args'](*seg)
-                    dev_args, nblk = cache[key]
+                    dev_args, nblk = lowrank['gather_args'](*seg)      # (cached by the transport)
                     ga = (dev_args.data_ptr(), nblk)
                     self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True, gather=ga)
                 else:

@@ -138,13 +138,18 @@ class XgmiAllReduce:
         blocks): for a launch that runs the gather as a side duty (the fc dgrad igemm). The
         pointers are static, so the tensor is built once per buffer set."""
         assert self.gather_cap > 0, 'no gather channel'
+        key = tuple(int(v) for v in list(srcs) + list(outs) + list(nbytes))
+        cache = self.__dict__.setdefault('_gather_args', {})
+        if key in cache:
+            return cache[key]
         ch = self.channels[-1]
         host = self.ext.xgmi_gather_args([int(v) for v in srcs], [int(v) for v in outs], [int(v) for v in nbytes],
                                          ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.gather_cap, self.ctx.rank,
                                          self.ctx.world_size)
         nv = (int(nbytes[0]) + int(nbytes[1])) // 16
         blocks = max(1, min(self.ext.XGMI_MAX_BLOCKS, (nv + 255) // 256))
-        return host.to(self.ctx.device), blocks
+        cache[key] = (host.to(self.ctx.device), blocks)
+        return cache[key]
 
     def self_test_gather(self) -> bool:
         """Gather rank-stamped bytes twice (both staging parities), check every slot, agree."""
