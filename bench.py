@@ -123,7 +123,12 @@ def main():
             if learner._graphs is not None:
                 break
             step()
-        learner.step_many(G)                    # captures the G-step graph outside the timed region
+        try:
+            learner.step_many(G)                # captures the G-step graph outside the timed region
+        except RuntimeError as e:               # (e.g. capture refused): one graph per step instead
+            print('bench: %d-step graph unavailable (%s); one graph per step' % (G, e), file=sys.stderr, flush=True)
+            torch.cuda.synchronize(dev)
+            G = 1
     ctx.barrier()
     torch.cuda.synchronize(dev)
     frames0 = actor.env_frames if actor is not None else 0
