@@ -101,11 +101,12 @@ def main():
             actor.step()
         learner.step()
 
-    # G steps per graph launch when the whole step is one in-graph body (fused or no acting) of
-    # ONE process (data parallelism keeps one graph per step: Learner.step_many)
-    G = max(1, args.graph_steps) if (actor is None or fused) and args.graph and not ctx.enabled else 1
+    # G steps per graph launch (Learner.step_many) when the whole step is one in-graph body (fused or
+    # no acting; one process, or DP with in-graph xgmi collectives). Whether G > 1 pays is decided
+    # by a start-up probe (below), identically on every rank.
+    G_max = max(1, args.graph_steps) if (actor is None or fused) and args.graph else 1
 
-    def run(n):
+    def run(n, G):
         if G > 1:
             for _ in range(n // G):
                 learner.step_many(G)
@@ -113,27 +114,50 @@ def main():
         for _ in range(n):
             step()
 
-    # warm-up: eager steps, the one-step graph capture, then (G > 1) the G-step graph's capture
-    # and first replay -- W steps in all when W >= G + 3, else W single steps + one G-step launch
-    w1 = args.warmup - G if G > 1 and args.warmup >= G + 3 else args.warmup
+    def timed(fn):
+        ctx.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if ctx.enabled:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el)
+
+    # warm-up: eager steps and the one-step graph capture, then (G_max > 1) the G-step graph's
+    # capture and first replay -- W steps in all when W >= G + 3, else W single steps + one G-step launch
+    w1 = args.warmup - G_max if G_max > 1 and args.warmup >= G_max + 3 else args.warmup
     for _ in range(w1):
         step()
-    if G > 1:
-        for _ in range(3):                      # (tiny W: the one-step graph must exist first)
-            if learner._graphs is not None:
-                break
-            step()
+    for _ in range(3):                          # (tiny W: the one-step graph must exist first)
+        if learner._graphs is not None or not args.graph:
+            break
+        step()
+    if G_max > 1 and not learner.can_step_many():
+        G_max = 1
+    if G_max > 1:
         try:
-            learner.step_many(G)                # captures the G-step graph outside the timed region
-        except RuntimeError as e:               # (e.g. capture refused): one graph per step instead
-            print('bench: %d-step graph unavailable (%s); one graph per step' % (G, e), file=sys.stderr, flush=True)
+            learner.step_many(G_max)            # captures the G-step graph outside the timed region
+        except RuntimeError as e:               # (capture refused): one graph per step instead
+            print('bench: %d-step graph unavailable (%s); one graph per step' % (G_max, e), file=sys.stderr,
+                  flush=True)
             torch.cuda.synchronize(dev)
-            G = 1
+            G_max = 1
+            step()                              # host step state restored by step_many: one clean step
+    # probe (untimed, identical decision on every rank: MAX-reduced times): G = 1 vs G = G_max
+    probe_steps = 4 * G_max if G_max > 1 else 16
+    t_g1 = timed(lambda: run(probe_steps, 1))
+    G = 1
+    if G_max > 1:
+        t_gm = timed(lambda: run(probe_steps, G_max))
+        G = G_max if t_gm < t_g1 else 1
+    ms_g1 = 1000.0 * t_g1 / probe_steps
     ctx.barrier()
     torch.cuda.synchronize(dev)
     frames0 = actor.env_frames if actor is not None else 0
     t0 = time.perf_counter()
-    run(args.steps)
+    run(args.steps, G)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     el = time.perf_counter() - t0
@@ -157,7 +181,8 @@ def main():
         out = {
             'metric': METRIC, 'value': round(sps, 2), 'unit': 'SGD steps/s (all GPUs)',
             'n_gpus': ctx.world_size, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': round(1000.0 * el / args.steps, 4), 'higher_is_better': True, 'scaling': 'weak',
+            'ms_per_step': round(1000.0 * el / args.steps, 4), 'ms_per_step_g1': round(ms_g1, 4),
+            'graph_steps': G, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': getattr(net.executor, 'compute_dtype', 'fp32'), 'data': 'synthetic (random uint8 84x84 frames, random init)',
             'env_frames_per_sec': round(frames / el, 1),
             'samples_per_sec': round(sps * args.batch, 1),
@@ -165,7 +190,10 @@ def main():
                        'global_batch': args.batch * ctx.world_size, 'seq_len': None,
                        'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
                        'frames_per_state': 4, 'optimizer': cfg.optimizer + '(tf)', 'executor': net.executor.name,
-                       'hip_graph': bool(args.graph), 'steps_per_graph_launch': G, 'actor_envs': args.actor_envs,
+                       'hip_graph': bool(args.graph), 'steps_per_graph_launch': G,
+                       'graph_steps_probe': {'candidates': sorted({1, G_max}), 'probe_steps': probe_steps,
+                                             'ms_per_step_g1': round(ms_g1, 4)},
+                       'actor_envs': args.actor_envs,
                        'acting': 'fused into the learner launches' if fused else 'separate launches',
                        'update_freq': args.update_freq, 'replay_capacity': cfg.replay_memory_capacity,
                        'num_actions': args.actions, 'variant': args.variant, 'extra': args.extra,

@@ -123,6 +123,7 @@ void optimizer_step(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tens
   TORCH_CHECK(s1.numel() == w.numel() || s1.data_ptr() == w.data_ptr(), "slot 1 size");
   TORCH_CHECK(reg_end % 4 == 0 && reg_end <= w.numel(), "reg_end");
   TORCH_CHECK(hp.size() == 9, "9 hyper-parameters expected");
+  TORCH_CHECK(ticket.numel() >= 2, "optimizer_step: ticket[1] is the slot flag word");
   if (has_step) { CHECK_T(step, torch::kInt64); }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
@@ -148,7 +149,9 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
                 std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
-                c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng) {
+                c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng, std::vector<int64_t> fc) {
+  // fc: [] or [x ptr, dh ptr, M, ldx, ldh]: the launch forms the fc weight / bias gradient of the
+  // jobs carrying a dH column from those act_t rows (optim.hip FcFuse) instead of reading `grad`
   // noise_rng (noisy nets): [seed, counter] of the noise stream whose next samples an earlier
   // launch of this step drew (the fc dgrad's noise duty); the last block advances the counter
   // tnoise / teff / tpk (noisy nets): mix + pack the target under tnoise in the same launch
@@ -273,6 +276,16 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
     TORCH_CHECK(op >= 0 && noise_rng->numel() >= 2, "optim_pack: noise_rng = [seed, counter] (update calls)");
     nrng = ptr<int64_t>(*noise_rng);
   }
+  FcFuse ff{nullptr, nullptr, 0, 0, 0};
+  if (!fc.empty()) {
+    TORCH_CHECK(op >= 0 && fc.size() == 5 && fc[0] != 0 && fc[1] != 0 && fc[2] >= 1 && fc[2] <= 4096 &&
+                    fc[3] % 8 == 0 && fc[4] % 8 == 0 && (fc[0] % 16) == 0 && (fc[1] % 16) == 0,
+                "optim_pack fc: [x, dh, 1 <= M <= 4096, ldx % 8 == 0, ldh % 8 == 0], 16-byte aligned rows");
+    TORCH_CHECK(optim_fc_fuse(), "optim_pack fc: not available in this build");
+    TORCH_CHECK(ticket.numel() >= 17 * 32, "optim_pack fc: one block per job needs the 17x32-word ticket");
+    ff = FcFuse{P<const void*>(fc[0]), P<const void*>(fc[1]), (int)fc[2], (int)fc[3], (int)fc[4]};
+  }
+  TORCH_CHECK(ticket.numel() >= 2, "optim_pack: ticket[1] is the slot flag word");
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
@@ -280,7 +293,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
-                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, cur_stream());
+                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, fc.empty() ? nullptr : &ff, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {
@@ -634,6 +647,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_pack", &optim_pack);
   m.def("noise_normal", &noise_normal);
   m.attr("UPD_JOB_INTS") = upd_job_ints();
+  m.attr("OPTIM_FC_FUSE") = optim_fc_fuse();
   m.def("td_loss_scalar", &td_loss_scalar);
   m.def("td_loss_c51", &td_loss_c51);
   m.def("preprocess_batch", &preprocess_batch);

@@ -43,12 +43,24 @@ void launch_sumtree_sample(const float* sum, const float* mn, int64_t* rng, cons
 void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
                            int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
                            float grad_scale, int n, float* tgt, int tfreq, hipStream_t st);
+// The fc (hidden dense) layer's weight gradient formed inside the optimizer launch (optim.hip):
+// dW[k][n] = sum_{m < M} x[m][k] dh[m][col + n] for the update jobs that carry a dH column
+// (UpdJob.fc_col >= 0), and the fc bias gradient sum_m dh[m][col + n] -- never written to the
+// flat gradient. x / dh are act_t rows (the fc input rows and dL/d(fc pre-activation) rows of
+// this rank, or the all-gathered rows of every rank under the low-rank DP exchange).
+struct FcFuse {
+  const void* x;
+  const void* dh;
+  int M, ldx, ldh;
+};
 void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
-                       int64_t* noise_rng, hipStream_t st);
+                       int64_t* noise_rng, const FcFuse* fc, hipStream_t st);
+// 1 when this build's optimizer launch can form the fc weight gradient itself (16-bit builds)
+int optim_fc_fuse();
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
 void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();

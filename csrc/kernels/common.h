@@ -156,5 +156,24 @@ DQN_DEV f32x4 mfma_f32_k32(const f32x8_frag& a, const f32x8_frag& b, f32x4 c) {
 }
 #endif
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+typedef __attribute__((ext_vector_type(8))) act_t bfx8;     // one MFMA operand (8 act_t per lane)
+
+#if !DQN_ACT_F32
+// 16-bit builds: MFMA operands of a row-major LDS tile through transposed reads.
+// lds_tr16: 4 rows x 16 columns of 16-bit elements, column-major into the lanes of each
+// 16-lane group (lane 4q + p addresses row q, columns 4p..4p+3; lane i receives column i,
+// row q in element q); join_tr: two of them (rows r and r + 16) as one 8-element operand.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+DQN_DEV s16x4 lds_tr16(const act_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(p)));
+}
+DQN_DEV bfx8 join_tr(s16x4 lo, s16x4 hi) {
+  union { s16x4 h[2]; bfx8 v; } u;
+  u.h[0] = lo;
+  u.h[1] = hi;
+  return u.v;
+}
+#endif
 
 }  // namespace dqn

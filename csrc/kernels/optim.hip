@@ -80,6 +80,7 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
   // fused hard target sync: this update makes global_step s+1; the reference copies
   // target <- online after the train step when (s+1) % target_update_freq == 0
   const bool sync = tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  const bool wmom = OP != 7 || ticket[1] != 0;     // (see kSlotFlag)
   float4* T = reinterpret_cast<float4*>(tgt);
   if constexpr (OP == 3) {
     const float b1p = beta_pow[0], b2p = beta_pow[1];
@@ -105,7 +106,8 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
     W[i] = nw;
     if (sync) T[i] = nw;
     if constexpr (OP != 0) S0[i] = make_float4(aa[0], aa[1], aa[2], aa[3]);
-    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7) S1[i] = make_float4(bb[0], bb[1], bb[2], bb[3]);
+    if constexpr (OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7)
+      if (wmom) S1[i] = make_float4(bb[0], bb[1], bb[2], bb[3]);
   }
   // last block advances global_step and (Adam) the beta powers. Every block
   // read beta_pow above, before its ticket add, so the update cannot race.
@@ -143,11 +145,26 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 // Elementwise items (biases, ...) carry an optional fp32 copy into the packed
 // buffer (the concatenated fc bias). Same ticket as optim_kernel; the hard target
 // sync writes the target's fp32 master and packed fragments under the predicate.
-typedef __attribute__((ext_vector_type(8))) act_t bfx8;
 typedef __attribute__((ext_vector_type(4))) act_t bfx4;
 
 constexpr int kTicketSubs = 16, kTicketStride = 32;    // hierarchical ticket: int32 words
 constexpr int kPackThreads = 512;
+// ticket[kSlotFlag] != 0: momentum-0 RMSProp also stores its `mom` slot this step. That slot
+// (mom = 0 * mom + update) is never read by the update, only saved under its TF name, so the
+// hot path skips its 4 bytes / parameter and the checkpoint manager raises the flag for the
+// step before a save (optim.py Optimizer.request_slots).
+constexpr int kSlotFlag = 1;
+
+#if !DQN_ACT_F32
+// Fused fc weight gradient (FcFuse): a 32 (k) x 64 (n) update tile's dW = X^T dH over M rows,
+// 32-row chunks staged ROW-major in LDS (strides + 16 elements: conflict-free transposed reads,
+// as the grouped wgrad), wave w owning the 16 x 16 sub-tile (k: w >> 2, n: w & 3) as dW^T =
+// dH^T X on one v_mfma_f32_16x16x32 per chunk (lane: one k, 4 consecutive n), then through
+// an fp32 LDS tile into the update's own thread map (row r, 4 consecutive n).
+constexpr int kFcSX = 32 + 16, kFcSH = 64 + 16, kFcRS = 64 + 4;
+constexpr int kFcLds = 32 * kFcRS * 4;          // >= staging (32 * (SX + SH) * 2 B) and 4 x 512 fp32
+static_assert(32 * (kFcSX + kFcSH) * 2 <= kFcLds && 4 * 512 * 4 <= kFcLds, "fc LDS plan");
+#endif
 
 struct UpdJob {
   int kind;                      // 0 = tile, 1 = elementwise chunk
@@ -159,6 +176,9 @@ struct UpdJob {
   // (ein < 0: f = 1, biases; elem chunks: eout already offset to the chunk start)
   int sig_off, ein_off, eout_off;
   int eff;                       // 1: also store the effective fp32 value at eff[src index]
+  // fc weight tile / fc bias chunk whose gradient the launch forms from FcFuse rows: the
+  // tensor's first column in dH (-1: read the flat gradient)
+  int fc_col;
 };
 
 DQN_DEV float fnz(float x) { return copysignf(sqrtf(fabsf(x)), x); }
@@ -177,16 +197,17 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 // kModePer (the sampler block runs the prioritized sum-tree path). Paths a mode excludes are
 // not instantiated: their registers would cost the plain nets occupancy (mode 0: 8 waves / SIMD,
 // so every block of the Nature-CNN work list is resident at once).
-constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4;
+// kModeFc: some jobs form their gradient from FcFuse rows (16-bit builds).
+constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8;
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, MODE == 0 ? 8 : (((MODE & kModeTmix) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+__global__ void __launch_bounds__(kPackThreads, (MODE & ~kModeFc) == 0 ? 8 : (((MODE & kModeTmix) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
                   act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
                   int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
-                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng) {
+                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
@@ -199,6 +220,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // sample into teff / tpk (the target's eff / packed buffers): no separate target mix launch.
   constexpr bool UPD = OP >= 0;
   constexpr bool TMIX = (MODE & kModeTmix) != 0, NZOK = (MODE & kModeNoisy) != 0, PEROK = (MODE & kModePer) != 0;
+  constexpr bool FC = (MODE & kModeFc) != 0 && !DQN_ACT_F32 && OP >= 0;
   // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
   const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
   // LDS: only the sampler block's scratch (the update items exchange through DPP)
@@ -217,6 +239,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   const bool sync = UPD && tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
   const bool psync = sync && tgt_packed != nullptr;
   constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7;   // second slot written
+  const bool wtwo = OP != 7 || ticket[kSlotFlag] != 0;                         // (momentum-0 RMSProp: flagged)
   constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
   constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
@@ -249,6 +272,83 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     if (threadIdx.x == 0) smp.rng[1] = (int64_t)(ctr + 1);   // every lane read it before the barriers
   }
+#if !DQN_ACT_F32
+  __shared__ __attribute__((aligned(16))) unsigned char fcl[FC ? kFcLds : 16];
+  // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
+  auto fc_tile_grad = [&](const UpdJob& jb, float* g) {
+    act_t* Xs = reinterpret_cast<act_t*>(fcl);           // [32][kFcSX]: x[m][k0 .. k0 + 32)
+    act_t* Hs = Xs + 32 * kFcSX;                         // [32][kFcSH]: dh[m][col + n0 .. + 64)
+    float* R = reinterpret_cast<float*>(fcl);            // [32][kFcRS] fp32 dW tile (after the MFMAs)
+    const int wv = t >> 6, lane = t & 63;
+    const int kt = wv >> 2, nt = wv & 3;
+    // loaders: t < 128 one 8-element piece of an x row, 128 <= t < 384 one of a dh row
+    const bool lx = t < 128, lh = t >= 128 && t < 384;
+    const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
+    const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
+    const act_t* X = reinterpret_cast<const act_t*>(ff.x);
+    const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
+    auto load = [&](int m0) {
+      const int m = m0 + lr;
+      bfx8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (act_t)0.f;
+      // (32-bit element offsets off the uniform bases: no per-thread 64-bit address kept live)
+      if (m < ff.M) {
+        if (lx && jb.k0 + lc < jb.K)
+          v = *reinterpret_cast<const bfx8*>(X + (uint32_t)(m * ff.ldx + jb.k0 + lc));
+        else if (lh && jb.n0 + lc < jb.N)
+          v = *reinterpret_cast<const bfx8*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + jb.n0 + lc));
+      }
+      return v;
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+    const act_t* ph = Hs + (4 * gq + rq) * kFcSH + nt * 16 + cp;
+    const act_t* px = Xs + (4 * gq + rq) * kFcSX + kt * 16 + cp;
+    for (int m0 = 0; m0 < ff.M; m0 += 32) {
+      const bfx8 v = load(m0);
+      __syncthreads();                 // previous chunk's operand reads / previous item's R reads done
+      if (lx) *reinterpret_cast<bfx8*>(Xs + lr * kFcSX + lc) = v;
+      else if (lh) *reinterpret_cast<bfx8*>(Hs + lr * kFcSH + lc) = v;
+      __syncthreads();
+      // A = dh^T (rows n), B = x (columns k); the same row permutation on both operands
+      acc = DQN_MFMA16_BUILTIN(join_tr(lds_tr16(ph), lds_tr16(ph + 16 * kFcSH)),
+                               join_tr(lds_tr16(px), lds_tr16(px + 16 * kFcSX)), acc, 0, 0, 0);
+    }
+    __syncthreads();                   // operand reads done before R overwrites the staging
+    // acc[r] = dW[k = kt * 16 + (lane & 15)][n = nt * 16 + 4 * (lane >> 4) + r]
+    *reinterpret_cast<float4*>(R + (kt * 16 + (lane & 15)) * kFcRS + nt * 16 + 4 * (lane >> 4)) =
+        make_float4(acc[0] * kInvLossScale, acc[1] * kInvLossScale, acc[2] * kInvLossScale, acc[3] * kInvLossScale);
+    __syncthreads();
+    const int r = (wv >> 1) * 8 + (lane & 7), c4 = (wv & 1) * 32 + (lane >> 3) * 4;
+    const float4 gv = *reinterpret_cast<const float4*>(R + r * kFcRS + c4);
+    g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
+  };
+  // fc bias chunk (<= 512 values, thread t < 128 owns n = 4t..4t+3): sum_m dh[m][col + n] over 4
+  // row phases, combined in a fixed order
+  auto fc_bias_grad = [&](const UpdJob& jb, float* g) {
+    float* R = reinterpret_cast<float*>(fcl);            // [4][512]
+    const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
+    const int cg = t & 127, ph = t >> 7, c = 4 * cg;
+    float sm[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < jb.K) {
+#pragma unroll 4
+      for (int m = ph; m < ff.M; m += 4) {
+        const bfx4 v = *reinterpret_cast<const bfx4*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + c));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm[j] += (float)v[j];
+      }
+    }
+    __syncthreads();                   // previous item's LDS reads done
+    *reinterpret_cast<float4*>(R + ph * 512 + c) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = (4 * t + j) & 511;
+      g[j] = ((R[i] + R[512 + i]) + (R[1024 + i] + R[1536 + i])) * kInvLossScale;
+    }
+  };
+#endif
   // One job item = a 32x64 tile (or a 2048-element chunk) updated by 4 consecutive elements per
   // thread. The body is instantiated per (AL = 16-byte aligned float4 rows, NZ = noisy) so that
   // every global load of the item (mu / sigma / grad / slots / target / noise factors) is an
@@ -259,6 +359,8 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read
     constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value, DG = decltype(dg_c)::value;
     const bool elem = jb.kind == 1;
+    float g[4];
+    const bool fcj = FC && jb.fc_col >= 0;
     bool ok[4];
     int k, n;                      // row (tile) and column / element index within the tensor
     bool rowok;
@@ -304,10 +406,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
     };
     const int64_t mo = jb.src_off, so = NZ ? jb.sig_off : jb.src_off;
+    float w[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], tw[4], tws[4], e[4], te[4];
     // ---- every load of the item, issued before any math
-    float w[4], g[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], tw[4], tws[4], e[4], te[4];
     ld(W, mo, w);
-    if constexpr (UPD) ld(G, mo, g);
     if constexpr (ONE) ld(S0, mo, a);
     if constexpr (TWO_LD) ld(S1, mo, b);
     if constexpr (NZ) {
@@ -323,6 +424,18 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     if (tmix) {
       ld(tgt, mo, tw);
       if constexpr (NZ) ld(tgt, so, tws);
+    }
+    if constexpr (UPD) {
+#if !DQN_ACT_F32
+      // fused fc weight / bias gradient (block-uniform), formed while the item's HBM loads
+      // above are in flight (its X / dH rows are L2-resident)
+      if constexpr (FC) {
+        if (fcj) {
+          if (elem) fc_bias_grad(jb, g); else fc_tile_grad(jb, g);
+        }
+      }
+#endif
+      if (!fcj) ld(G, mo, g);
     }
     // factorised-noise factors: f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
     float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
@@ -358,13 +471,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       upd4<OP>(w, g, a, b, e0, h.reg_end, h, lr_t, ok);
       st(W, mo, w);
       if constexpr (ONE) st(S0, mo, a);
-      if constexpr (TWO) st(S1, mo, b);
+      if constexpr (TWO) if (wtwo) st(S1, mo, b);
       if (sync) st(tgt, mo, w);
       if constexpr (NZ) {
         upd4<OP>(ws, gs, as, bs, so + d0, h.reg_end, h, lr_t, ok);
         st(W, so, ws);
         if constexpr (ONE) st(S0, so, as);
-        if constexpr (TWO) st(S1, so, bs);
+        if constexpr (TWO) if (wtwo) st(S1, so, bs);
         if (sync) st(tgt, so, ws);
       }
     }
@@ -438,7 +551,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) {
+  auto run = [&](int ji) {
     const UpdJob jb = jobs[ji];
     const bool nz = NZOK && jb.sig_off >= 0;
     // float4 rows: 16-byte aligned tensor (and sigma) offsets and a row / chunk length % 4 == 0
@@ -452,6 +565,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         if (al) item(jb, T_{}, T_{}, F_{}); else item(jb, F_{}, T_{}, F_{});
       }
     }
+  };
+  if constexpr (FC) {
+    // one job per block (the launcher sizes the grid for it): no job loop, so no per-thread loop
+    // invariants are hoisted and kept live across the fc barriers
+    if (!sampler && wid < njobs) run(wid);
+  } else {
+    for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) run(ji);
   }
   if (!UPD) return;
   __shared__ int s_last;
@@ -562,14 +682,16 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
                        int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
-                       void* tpk, int64_t* noise_rng, hipStream_t st) {
+                       void* tpk, int64_t* noise_rng, const FcFuse* fc, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
   // max_grid <= 256: grid-stride over the jobs with a flat ticket (<= 256 arrivals);
   // larger: one block per job (up to max_grid) with the two-level ticket
-  const int cap = max_grid > 256 ? max_grid : 256;
+  const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};
+  // (the FC modes run exactly one job per block)
+  const int cap = ff.x != nullptr ? (njobs > 256 ? njobs : 256) : (max_grid > 256 ? max_grid : 256);
   const TrunkSample sm = smp != nullptr ? *smp : TrunkSample{};
   const PerStep pe = per != nullptr ? *per : PerStep{};
   const int grid = (njobs < cap ? njobs : cap) + (sm.size != nullptr || pe.sum != nullptr ? 1 : 0);   // + sampler
@@ -580,13 +702,21 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   const int tf = tfreq < 1 ? 1 : tfreq;
   // (a noisy net always passes its noise sample; plain nets pass none)
   const int mode = (noise != nullptr ? kModeNoisy : 0) | (tnoise != nullptr ? kModeTmix : 0) |
-                   (pe.sum != nullptr ? kModePer : 0);
+                   (pe.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0);
 #define OPM(N, M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, \
                        beta_pow, step, ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, \
-                       sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng)
+                       sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng, ff)
+#if DQN_ACT_F32
 #define OPK(N) do { switch (mode) { \
     case 0: OPM(N, 0); break; case 1: OPM(N, 1); break; case 3: OPM(N, 3); break; \
     case 4: OPM(N, 4); break; case 5: OPM(N, 5); break; default: OPM(N, 7); break; } } while (0)
+#else
+#define OPK(N) do { switch (mode) { \
+    case 0: OPM(N, 0); break; case 1: OPM(N, 1); break; case 3: OPM(N, 3); break; \
+    case 4: OPM(N, 4); break; case 5: OPM(N, 5); break; case 7: OPM(N, 7); break; \
+    case 8: OPM(N, 8); break; case 9: OPM(N, 9); break; case 11: OPM(N, 11); break; \
+    case 12: OPM(N, 12); break; case 13: OPM(N, 13); break; default: OPM(N, 15); break; } } while (0)
+#endif
   switch (op) {
     case -1: OPM(-1, kModeNoisy); break;     // mix + pack only (noisy nets)
     case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
@@ -598,6 +728,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
 }
 
 int upd_job_ints() { return (int)(sizeof(UpdJob) / sizeof(int)); }
+int optim_fc_fuse() { return DQN_ACT_F32 ? 0 : 1; }
 
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
                           float* dst2, const float* src2, int n2, hipStream_t st) {

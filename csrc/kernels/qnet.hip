@@ -95,14 +95,9 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src
 // ================================================================== A loaders
 // Each loader is built per (instance, row m) and returns the 8 consecutive
 // K-values [k0, k0+8) of row m as a bf16x8 MFMA A-fragment.
-// DQN_BRANCHFREE_LOADERS=1: every load goes to a clamped (always valid) address and
-// out-of-range values are replaced by a select, so the loads of a whole k-batch issue back
-// to back. Measured slower on the flagship step (82.7 -> 88.0 us: the strided dgrad then
-// loads the 3 of 4 invalid taps the early returns skip, and the selects cost the fc GEMM
-// ~0.7 us), so the default keeps the early-return loaders (docs/experiments/README.md).
-#ifndef DQN_BRANCHFREE_LOADERS
-#define DQN_BRANCHFREE_LOADERS 0
-#endif
+// (Round 2 measured branch-free loaders -- clamped addresses + selects -- slower on the flagship
+// step, 82.7 -> 88.0 us: the strided dgrad then loads the 3 of 4 invalid taps the early returns
+// skip. The early-return loaders stay.)
 DQN_DEV bfx8 sel8(bool keep, const bfx8& v) {
   bfx8 r;
 #pragma unroll
@@ -127,7 +122,6 @@ struct ConvLoader {
     base = reinterpret_cast<const Tin*>(a.in[inst]) + (int64_t)b * IH * IW * CIN;
   }
   DQN_DEV bfx8 frag(int k0) const {
-#if !DQN_BRANCHFREE_LOADERS
     if (!ok) return zero8();
     const int kh = k0 / (KW * CIN), rem = k0 - kh * (KW * CIN), kw = rem / CIN, ci = rem - kw * CIN;
     const int iy = iy0 + kh, ix = ix0 + kw;
@@ -144,23 +138,6 @@ struct ConvLoader {
       if (iy < 0 || iy >= IH || ix < 0 || ix >= IW) return zero8();
       return *reinterpret_cast<const bfx8*>(base + ((int64_t)iy * IW + ix) * CIN + ci);
     }
-#else
-    const int kh = k0 / (KW * CIN), rem = k0 - kh * (KW * CIN), kw = rem / CIN, ci = rem - kw * CIN;
-    const int iy = iy0 + kh, ix = ix0 + kw;
-    const bool yok = ok && iy >= 0 && iy < IH;
-    const int iyc = min(max(iy, 0), IH - 1);
-    if constexpr (sizeof(Tin) == 1) {
-      static_assert(CIN == 4, "uint8 input path expects 4 stacked frames");
-      // 8 bytes = pixels (ix, ix+1) x 4 frames
-      const uint32_t* row = reinterpret_cast<const uint32_t*>(base + (int64_t)iyc * IW * CIN);
-      const uint32_t lo = row[min(max(ix, 0), IW - 1)], hi = row[min(max(ix + 1, 0), IW - 1)];
-      return u8x8_to_bf(yok && ix >= 0 && ix < IW ? lo : 0u, yok && ix + 1 >= 0 && ix + 1 < IW ? hi : 0u);
-    } else {
-      const bool in = yok && ix >= 0 && ix < IW;
-      const int ixc = min(max(ix, 0), IW - 1);
-      return sel8(in, *reinterpret_cast<const bfx8*>(base + ((int64_t)iyc * IW + ixc) * CIN + ci));
-    }
-#endif
   }
 };
 
@@ -193,7 +170,6 @@ struct FrameLoader {
     fb[3] = fr + (int64_t)sl.w * a.frame_hw;
   }
   DQN_DEV bfx8 frag(int k0) const {
-#if !DQN_BRANCHFREE_LOADERS
     if (!ok) return zero8();
     const int kh = k0 / (KW * 4), kw = (k0 - kh * (KW * 4)) / 4;   // k0 % 8 == 0 -> kw even, c = 0
     const int iy = iy0 + kh, ix = ix0 + kw;
@@ -216,21 +192,6 @@ struct FrameLoader {
       }
     }
     return r;
-#else
-    const int kh = k0 / (KW * 4), kw = (k0 - kh * (KW * 4)) / 4;   // k0 % 8 == 0 -> kw even, c = 0
-    const int iy = iy0 + kh, ix = ix0 + kw;
-    DQN_ASSERT((ix & 1) == 0 && (IW & 1) == 0);
-    const bool in = ok && iy >= 0 && iy < IH && ix >= 0 && ix + 1 < IW;
-    const int off = in ? iy * IW + ix : 0;
-    bfx8 r;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint32_t v = in ? (uint32_t)*reinterpret_cast<const uint16_t*>(fb[c] + off) : 0u;
-      r[c] = (act_t)(float)(v & 0xffu);                               // pixel ix of frame c
-      r[4 + c] = (act_t)(float)(v >> 8);                              // pixel ix + 1
-    }
-    return r;
-#endif
   }
 };
 
@@ -253,7 +214,6 @@ struct DgradLoader {
     base = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)b * OH * OW * COUT;
   }
   DQN_DEV bfx8 frag(int k0) const {
-#if !DQN_BRANCHFREE_LOADERS
     if (!ok) return zero8();
     const int tap = k0 / COUT, co = k0 - tap * COUT, kh = tap / KW, kw = tap - kh * KW;
     const int ny = ty - kh, nx = tx - kw;
@@ -261,15 +221,6 @@ struct DgradLoader {
     const int oy = ny / S, ox = nx / S;
     if (oy * S != ny || ox * S != nx || oy >= OH || ox >= OW) return zero8();   // (invalid taps: no load)
     return *reinterpret_cast<const bfx8*>(base + ((int64_t)oy * OW + ox) * COUT + co);
-#else
-    const int tap = k0 / COUT, co = k0 - tap * COUT, kh = tap / KW, kw = tap - kh * KW;
-    const int ny = ty - kh, nx = tx - kw;
-    const int nyc = max(ny, 0), nxc = max(nx, 0);
-    const int oy = nyc / S, ox = nxc / S;
-    const bool in = ok && ny >= 0 && nx >= 0 && oy * S == ny && ox * S == nx && oy < OH && ox < OW;
-    const int oyc = min(oy, OH - 1), oxc = min(ox, OW - 1);
-    return sel8(in, *reinterpret_cast<const bfx8*>(base + ((int64_t)oyc * OW + oxc) * COUT + co));
-#endif
   }
 };
 
@@ -284,12 +235,8 @@ struct DenseLoader {
     row = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)(ok ? m : 0) * (a.IW > 0 ? a.IW : a.K);
   }
   DQN_DEV bfx8 frag(int k0) const {
-#if !DQN_BRANCHFREE_LOADERS
     if (!ok) return zero8();
     return *reinterpret_cast<const bfx8*>(row + k0);
-#else
-    return sel8(ok, *reinterpret_cast<const bfx8*>(row + k0));    // (row is clamped to row 0)
-#endif
   }
 };
 
@@ -356,19 +303,10 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool kok = ks + u < ks_hi;
-#if DQN_BRANCHFREE_LOADERS
-      // a partial last batch: clamped k-step (valid addresses), zeroed by select -- no branch
-      const int kc = min(ks + u, ks_hi - 1);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) af[u][i] = sel8(kok, ld[i].frag(kc * 32 + kg));
-#pragma unroll
-      for (int j = 0; j < NT; ++j) bf[u][j] = sel8(kok, Bp[((int64_t)kc * a.N16 + nt_base + j) * 64 + lane]);
-#else
 #pragma unroll
       for (int i = 0; i < MT; ++i) af[u][i] = kok ? ld[i].frag((ks + u) * 32 + kg) : zero8();
 #pragma unroll
       for (int j = 0; j < NT; ++j) bf[u][j] = kok ? Bp[((int64_t)(ks + u) * a.N16 + nt_base + j) * 64 + lane] : zero8();
-#endif
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -543,19 +481,7 @@ struct WgradTile {
   static constexpr int SA = KB + 16, SZ = NB + 16;
   static constexpr size_t lds_bytes = (size_t)MC * (SA + SZ) * sizeof(act_t);
 };
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-// 4 rows x 16 columns of 16-bit elements, column-major into the lanes of each 16-lane group
-// (lane 4q + p addresses row q, columns 4p..4p+3; lane i receives column i, row q in element q)
-DQN_DEV s16x4 lds_tr16(const act_t* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(p)));
-}
-DQN_DEV bfx8 join_tr(s16x4 lo, s16x4 hi) {
-  union { s16x4 h[2]; bfx8 v; } u;
-  u.h[0] = lo;
-  u.h[1] = hi;
-  return u.v;
-}
+// (operands through lds_tr16 / join_tr transposed reads: common.h)
 #endif
 
 // Body shared by the per-layer launch and the grouped launch (one block = one

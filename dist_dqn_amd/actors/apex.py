@@ -604,7 +604,16 @@ class ApexTrainer:
                 if self.pool.alive() == 0 and self.pool.procs:
                     self.pool.drain(self.replay)
                     self.replay.flush()
-                    if self.replay.size() < start or want_stop('all actors exited'):
+                    if self.replay.size() < start:
+                        if coordinated:
+                            # this rank can never step again, so it cannot reach the agreed stop
+                            # either: fail loudly (the peers' next collective fails, no final save)
+                            raise RuntimeError('rank %d: all Ape-X actors exited before the replay reached %d '
+                                               'transitions; cannot take part in the synchronous steps'
+                                               % (getattr(supervisor, 'rank', 0), start))
+                        log.warning('all actors exited')
+                        break
+                    if want_stop('all actors exited'):
                         log.warning('all actors exited')
                         break
         finally:

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import logging
 import random
+import time
 from functools import partial
 from typing import Optional
 
@@ -76,6 +77,7 @@ class DQNAgent:
         self._nstep = NStepAccumulator(config.n_step, config.reward_discount) if config.n_step > 1 else None
         self._prefill_replay_memory(config.replay_start_size)
         self._update_target_network()
+        self.t_train0 = time.perf_counter()       # (after prefill: throughput meters' origin)
 
     # ------------------------------------------------------------ train loop
     def train(self, num_episodes, max_steps_per_episode, supervisor=None):

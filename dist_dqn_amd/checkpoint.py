@@ -95,18 +95,31 @@ def load_sidecar(path: str) -> Optional[dict]:
 
 
 class CheckpointManager:
-    """Chief-only periodic saver (TF Supervisor's ``save_model_secs`` = 600 by default)."""
+    """Chief-only periodic saver (TF Supervisor's ``save_model_secs`` = 600 by default).
+
+    A periodic save costs the training thread one device-side snapshot (D2D copies on a side
+    stream, ``Network.snapshot``); a writer thread does the D2H transfer and the file write.
+    Before a save ``check_fn`` (e.g. the xgmi transport's error-word read) must pass: a state
+    that may hold a partly reduced gradient is never written. Momentum-0 RMSProp defers its
+    never-read ``mom`` slot (``FlatOptimizer.defers_slots``): a due save first asks the next
+    step to store it and is written after that step."""
 
     def __init__(self, logdir: str, network, is_chief: bool = True, save_secs: int = 600,
-                 max_to_keep: int = 5, agent_state_fn=None):
+                 max_to_keep: int = 5, agent_state_fn=None, check_fn=None, async_write: bool = True):
         self.logdir = logdir
         self.network = network
         self.is_chief = is_chief
         self.save_secs = save_secs
         self.max_to_keep = max_to_keep
         self.agent_state_fn = agent_state_fn
+        self.check_fn = check_fn
+        self.async_write = async_write
         self._last = time.time()
         self._lock = threading.Lock()
+        self._armed = False
+        self._writer: Optional[threading.Thread] = None
+        self._write_error: Optional[BaseException] = None
+        self.last_path: Optional[str] = None
 
     def restore(self) -> Optional[str]:
         path = latest_checkpoint(self.logdir)
@@ -115,15 +128,62 @@ class CheckpointManager:
         self.network.load_state_dict(load(path))
         return path
 
+    def _opt(self):
+        return getattr(self.network, 'optimizer', None)
+
     def maybe_save(self, force: bool = False) -> Optional[str]:
+        """Save when due (or ``force``: synchronous). Returns the checkpoint path, or None when
+        nothing was saved yet or the writer thread is writing it (``wait()`` joins it and returns
+        the path)."""
         if not self.is_chief:
             return None
         now = time.time()
         if not force and (self.save_secs <= 0 or now - self._last < self.save_secs):
             return None
+        opt = self._opt()
+        if not force and not self._armed and getattr(opt, 'defers_slots', False):
+            opt.request_slots(True)      # the next step stores the deferred slot; save after it
+            self._armed = True
+            return None
+        if self.check_fn is not None:
+            self.check_fn()              # raises: this state is not written
         with self._lock:
             self._last = now
-            sd = self.network.state_dict()
-            step = int(sd['global_step'])
+            self.wait()                  # one write in flight at a time
+            snap, ev = self.network.snapshot() if hasattr(self.network, 'snapshot') else (None, None)
+            if self._armed:
+                opt.request_slots(False)
+                self._armed = False
             side = self.agent_state_fn() if self.agent_state_fn else None
-            return save(self.logdir, sd, step, self.max_to_keep, side)
+            if snap is None:
+                sd = self.network.state_dict()
+                self.last_path = save(self.logdir, sd, int(sd['global_step']), self.max_to_keep, side)
+                return self.last_path
+            if not self.async_write or force or ev is None:
+                if ev is not None:
+                    ev.synchronize()
+                sd = self.network.state_dict_from(snap)
+                self.last_path = save(self.logdir, sd, int(sd['global_step']), self.max_to_keep, side)
+                return self.last_path
+
+            def write():
+                try:
+                    ev.synchronize()
+                    sd = self.network.state_dict_from(snap)
+                    self.last_path = save(self.logdir, sd, int(sd['global_step']), self.max_to_keep, side)
+                except BaseException as e:  # pragma: no cover - reported by wait()
+                    self._write_error = e
+
+            self._writer = threading.Thread(target=write, name='ckpt-writer', daemon=True)
+            self._writer.start()
+            return None                  # (the path is known once the writer has the step: wait())
+
+    def wait(self) -> Optional[str]:
+        """Join the writer thread of the last asynchronous save (re-raising its error)."""
+        w, self._writer = self._writer, None
+        if w is not None:
+            w.join()
+        if self._write_error is not None:
+            e, self._write_error = self._write_error, None
+            raise e
+        return self.last_path

@@ -52,13 +52,15 @@ def run_worker(config: Config):
     sv = RunSupervisor(is_chief=ctx.is_chief, logdir=config.logdir, network=network, rank=ctx.rank,
                        world_size=ctx.world_size, save_secs=config.checkpoint_secs,
                        max_to_keep=config.max_to_keep, ctx=ctx, coordinated=coordinated,
-                       stop_sync_steps=config.stop_sync_steps)
+                       stop_sync_steps=config.stop_sync_steps, summary_secs=config.summary_secs)
     sv.prepare(broadcast_fn=lambda: broadcast_state(ctx, network))
 
     if config.async_ps and ctx.enabled and ctx.rank == 0:
         return _run_parameter_server(config, ctx, network, sv)
     if config.num_actors > 1:
         return _run_apex(config, ctx, env, network, sv, seed)
+    if config.device_envs > 0:
+        return _run_device_envs(config, ctx, env, network, sv, seed)
     use_device_replay = ctx.device.type == 'cuda' or ctx.enabled
     if use_device_replay:
         frames = config.resize_width > 0 and config.resize_height > 0
@@ -75,6 +77,7 @@ def run_worker(config: Config):
                     target=network.target.flat if config.disable_target_replication else None)
             network.refresh_packed()
         session = Learner(network, replay, config, ctx, ps_client=ps)
+        sv.attach_learner(session)
     else:
         replay = ReplayMemory(config.replay_memory_capacity, rng=random.Random(seed + 7919 * (ctx.rank + 1)))
         session = None
@@ -139,6 +142,7 @@ def _run_apex(config: Config, ctx, env, network, sv, seed: int):
                           device=ctx.device, num_actors=config.num_actors, prioritized=config.prioritized_replay,
                           alpha=config.per_alpha, seed=seed + ctx.rank)
     learner = Learner(network, replay, config, ctx)
+    sv.attach_learner(learner)
     learner.update_target_now()
     pool = ApexActorPool(config.env, config.num_actors, config.frames_per_state if frames else 1, hw, obs_dim,
                          env.action_space.n, config.max_steps_per_episode, seed=seed + 100003 * ctx.rank,
@@ -150,6 +154,82 @@ def _run_apex(config: Config, ctx, env, network, sv, seed: int):
         trainer = ApexTrainer(network, replay, learner, pool, config, metrics=metrics)
         trainer.run(max_train_steps=config.max_train_steps, supervisor=sv)
     return trainer
+
+
+def _run_device_envs(config: Config, ctx, env, network, sv, seed: int):
+    """--device_envs=E: E GPU-resident synthetic Atari envs (DeviceActor) whose eps-greedy / env /
+    replay-append step rides inside the learner's launches (fused acting: one more trunk / fc
+    instance and one head workgroup per env) -- the path bench.py times -- under the Supervisor
+    (checkpoints, stop agreement, fault injection), with the reference metrics. The replay is
+    prefilled with ``replay_start_size`` random transitions (the synthetic env's frames are random
+    anyway: reference prefill, `dqn_agent.py:191-213`); ``update_freq`` env frames are stepped per
+    SGD step (``update_freq / E`` fused acting steps; fused only at one step per SGD step)."""
+    import time
+    from .actors.device_actor import DeviceActor
+    from .envs import is_atari
+    from .learner import Learner
+    from .replay import DeviceReplay
+    from .utils.metrics import JsonlWriter, SummaryWriter
+    frames = config.resize_width > 0 and config.resize_height > 0
+    if not (ctx.device.type == 'cuda' and frames and is_atari(config.env)):
+        raise ValueError('--device_envs needs a GPU and a (synthetic) Atari id with frame preprocessing, '
+                         'got env=%s device=%s' % (config.env, ctx.device))
+    E = int(config.device_envs)
+    A = env.action_space.n
+    replay = DeviceReplay(config.replay_memory_capacity, (config.resize_height, config.resize_width),
+                          config.frames_per_state, device=ctx.device, prioritized=config.prioritized_replay,
+                          alpha=config.per_alpha, seed=seed + ctx.rank)
+    replay.fill_synthetic(max(config.replay_start_size, config.minibatch_size), A, seed=seed + ctx.rank)
+    actor = DeviceActor(network, replay, config, num_envs=E, steps_per_call=max(1, config.update_freq // E),
+                        seed=seed + 1000 * (ctx.rank + 1))
+    fused = actor.can_fuse(config.minibatch_size)
+    learner = Learner(network, replay, config, ctx, actor=actor if fused else None)
+    sv.attach_learner(learner)
+    learner.update_target_now()
+    G = max(1, int(config.device_graph_steps)) if fused and learner.use_graph and not ctx.enabled else 1
+    metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))
+    writer = SummaryWriter(config.logdir) if ctx.is_chief else None
+    metrics.write(kind='start', rank=ctx.rank, world_size=ctx.world_size, restored_from=sv.restored_from,
+                  global_step=int(network.global_step), executor=network.executor.name, device_envs=E,
+                  fused_acting=fused, steps_per_graph_launch=G)
+    log.info('device envs: %d GPU envs, acting %s, %d SGD steps per graph launch', E,
+             'fused into the learner launches' if fused else 'separate launches', G)
+    budget = int(config.max_train_steps)
+    t0 = t_log = time.time()
+    f0 = f_log = actor.env_frames
+    s_log = 0
+    with sv.managed():
+        while not sv.should_stop():
+            if budget and learner.train_steps >= budget:
+                break
+            if G > 1 and (not budget or budget - learner.train_steps >= G) and learner._graphs is not None:
+                learner.step_many(G)
+            else:
+                if not fused:
+                    actor.step()
+                learner.step()
+            sv.on_train_step(learner.train_steps)
+            now = time.time()
+            if now - t_log >= 10.0 or (budget and learner.train_steps >= budget):
+                fr = actor.env_frames
+                loss = float(learner.loss)
+                rate = (learner.train_steps - s_log) / max(now - t_log, 1e-9)
+                fps = (fr - f_log) / max(now - t_log, 1e-9)
+                metrics.write(kind='progress', training_steps=learner.train_steps,
+                              global_step=int(network.global_step), loss=loss, epsilon=actor.epsilon,
+                              sgd_steps_per_sec=rate, env_frames_per_sec=fps, env_frames=fr,
+                              replay_size=replay.size())
+                if writer is not None:
+                    writer.add_scalar('loss', loss, learner.train_steps)
+                log.info('training steps = %d, %.0f SGD steps/s, %.0f env frames/s, epsilon = %.3f, loss = %.4f',
+                         learner.train_steps, rate, fps, actor.epsilon, loss)
+                t_log, f_log, s_log = now, fr, learner.train_steps
+    el = max(time.time() - t0, 1e-9)
+    metrics.write(kind='done', training_steps=learner.train_steps, sgd_steps_per_sec=learner.train_steps / el,
+                  env_frames_per_sec=(actor.env_frames - f0) / el, global_step=int(network.global_step))
+    if ctx.enabled and not config.async_ps and config.replica_check:
+        _replica_check(ctx, network, metrics, learner.train_steps)
+    return learner
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:

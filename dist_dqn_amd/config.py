@@ -139,6 +139,13 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
     a('--apex_native_serve', default=1, type=int,
       help='Ape-X: answer the actors from a C++ thread replaying captured inference graphs (GPU)')
+    a('--device_envs', default=0, type=int,
+      help='Synthetic Atari ids on a GPU: run this many GPU-resident envs whose acting step rides inside '
+           'the learner\'s launches (fused acting; the path bench.py measures) instead of the host agent '
+           'loop. update_freq / device_envs acting steps per SGD step; runs until --max_train_steps or a '
+           'stop request')
+    a('--device_graph_steps', default=8, type=int,
+      help='--device_envs (one process): SGD steps per replayed HIP graph')
     a('--apex_graph_steps', default=4, type=int,
       help='Ape-X learner: SGD steps per replayed HIP graph (one host call per that many steps)')
     a('--apex_serve_gap_us', default=100, type=int,
@@ -161,6 +168,11 @@ def build_parser() -> argparse.ArgumentParser:
     a('--fuse_sampling', default=2, type=int, choices=[0, 1, 2],
       help='Uniform GPU replay: 0 = sampler launch per step, 1 = the Nature trunk draws the minibatch, '
            '2 = the previous step\'s optimizer launch draws it (one extra block, off the critical path)')
+    a('--summary_secs', default=120.0, type=float,
+      help='chief: seconds between global_step/sec summaries (TF Supervisor step counter: 120)')
+    a('--fuse_fc_wgrad', default=1, type=int,
+      help='HIP executor (16-bit builds): form the fc weight gradient (X^T dH, rank <= B) inside the '
+           'fused optimizer launch instead of writing and re-reading it as an fp32 gradient')
     a('--checkpoint_secs', default=600, type=float,
       help='chief: seconds between periodic checkpoints (reference Supervisor: 600; <= 0 disables)')
     a('--max_to_keep', default=5, type=int)
@@ -244,6 +256,8 @@ class Config:
     apex_ring: int = 1024
     apex_serve_gap_us: int = 100
     apex_graph_steps: int = 4
+    device_envs: int = 0
+    device_graph_steps: int = 8
     apex_native_serve: int = 1
     allreduce: str = 'auto'
     allreduce_dtype: str = 'fp32'
@@ -252,6 +266,8 @@ class Config:
     lowrank_dense: int = 1
     hip_graph: int = 1
     fuse_sampling: int = 2
+    fuse_fc_wgrad: int = 1
+    summary_secs: float = 120.0
     checkpoint_secs: float = 600
     max_to_keep: int = 5
     save_agent_state: bool = False

@@ -3,8 +3,8 @@
 `observation_space.shape`, `spec.id`).
 
 gym/ALE are not available, so:
-  * CartPole-v0/v1: a numpy re-implementation of the classic-control dynamics
-    with the registry TimeLimit (200 / 500 steps) that gym applies;
+  * CartPole-v0/v1, Acrobot-v1, MountainCar-v0: numpy re-implementations of the
+    classic-control dynamics with the registry TimeLimit that gym applies;
   * Atari ids (``*-v0``, ``*NoFrameskip-v4`` ...): `SyntheticAtariEnv`, random
     210x160x3 frames with the real game's action count, for throughput work;
   * `VectorSyntheticAtari` (device.py): a GPU-resident batched synthetic env
@@ -12,5 +12,6 @@ gym/ALE are not available, so:
 """
 from .spaces import Box, Discrete, EnvSpec  # noqa: F401
 from .cartpole import CartPoleEnv  # noqa: F401
+from .classic_control import AcrobotEnv, MountainCarEnv  # noqa: F401
 from .synthetic import BlockBanditEnv, SyntheticAtariEnv, ATARI_ACTIONS  # noqa: F401
 from .registry import make, is_atari  # noqa: F401

@@ -20,7 +20,6 @@ between two captured graphs (pre: sample..backward, post: optimizer..target).
 from __future__ import annotations
 
 import logging
-import os
 from typing import Dict, Optional
 
 import torch
@@ -36,7 +35,6 @@ log = logging.getLogger(__name__)
 
 
 _CAPTURE_MODE = 'thread_local'
-_AR_FORK = os.environ.get('DQN_AR_FORK', '0') == '1'
 
 def _reduce_ranges(layout, total: int, excluded, forbidden=(), max_ranges: int = 8):
     """The pieces of the flat gradient a data-parallel step still all-reduces: every layout
@@ -91,13 +89,21 @@ class Learner:
         # data parallelism over xgmi: the fc weight gradient travels as its factors (executor
         # lowrank_spec: all-gather of the fc input rows + dL/dh rows, ~14x fewer bytes than the
         # gradient at B=32); the all-reduce then covers only the rest of the flat buffer
+        self.tau = min(1.0, float(config.target_update_tau))
+        tfreq = self._target_freq()
+        ex = network.executor
+        # the fc weight / bias gradient formed inside the fused optimizer launch from the fc input
+        # rows and dH rows (executor.can_defer_fc): no fp32 fc gradient round trip through HBM.
+        # Under DP only with the low-rank exchange (the rows are then every rank's)
+        sg = not (ps_client is None and network.fuses_sigma_grads(tfreq))
+        self._defer_fc = bool(ps_client is None and int(getattr(config, 'fuse_fc_wgrad', 1))
+                              and network.fuses_update(tfreq) and hasattr(ex, 'can_defer_fc')
+                              and ex.can_defer_fc(B, sg))
         lr = None
         if (self.ctx.enabled and ps_client is None and int(getattr(config, 'lowrank_dense', 1))
-                and getattr(config, 'overlap_allreduce', True) and hasattr(network.executor, 'lowrank_spec')
+                and getattr(config, 'overlap_allreduce', True) and hasattr(ex, 'lowrank_spec')
                 and getattr(config, 'allreduce_dtype', 'fp32') == 'fp32'):
-            tau = min(1.0, float(config.target_update_tau))
-            lr = network.executor.lowrank_spec(
-                B, sigma_fused=network.fuses_sigma_grads(config.target_update_freq if tau >= 1.0 else None))
+            lr = ex.lowrank_spec(B, sigma_fused=network.fuses_sigma_grads(tfreq), fused_fc=self._defer_fc)
         self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb,
                                       'rccl' if ps_client is not None else config.allreduce, config.allreduce_dtype,
                                       gather_bytes=lr['gather_bytes'] if lr else 0)
@@ -112,7 +118,8 @@ class Learner:
                 self._lowrank = {'gather': self.reducer.xgmi.allgather2, 'gather_args': self.reducer.xgmi.gather_args,
                                  'world': W, 'rank': self.ctx.rank}
                 self._ar_ranges = ranges
-        self.tau = min(1.0, float(config.target_update_tau))
+        if self.ctx.enabled and self._lowrank is None:
+            self._defer_fc = False         # (an all-reduced fc gradient must exist in the flat buffer)
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:
             use_graph = bool(config.hip_graph) and self.device.type == 'cuda'
@@ -130,11 +137,10 @@ class Learner:
         # bytes) while the conv backward runs, then the conv gradients (config.overlap_allreduce)
         self._tail = None
         # (xgmi without the low-rank exchange: no split -- its all-reduce runs in stream order
-        # after the whole backward, see _kernel_allreduce -- unless DQN_AR_FORK=1)
+        # after the whole backward, see _kernel_allreduce)
         self._split = bool(self.ctx.enabled and ps_client is None and getattr(config, 'overlap_allreduce', True)
-                           and (not self.reducer.in_graph or _AR_FORK or self._lowrank is not None))
+                           and (not self.reducer.in_graph or self._lowrank is not None))
         self._dense_hi = network.dense_range()[1] if self._split else 0
-        self._ar_stream = None
         self._presampled = False    # this step's minibatch was drawn by the last optimizer launch
         # sync DP + --disable_target_replication: rank 0's target is broadcast after each hard
         # sync; the host mirrors the device global_step to know when (one read, here)
@@ -180,9 +186,9 @@ class Learner:
         sg = not (self.ps is None and self.net.fuses_sigma_grads(self._target_freq()))
         if self._split:
             loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True, sigma_grads=sg,
-                                                            lowrank=self._lowrank)
+                                                            lowrank=self._lowrank, defer_fc=self._defer_fc)
         else:
-            loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg)
+            loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg, defer_fc=self._defer_fc)
         # keep references (static buffers under graph capture) instead of copies
         self.loss = loss.view(1)
         self.prio = prio.view(-1)
@@ -261,8 +267,8 @@ class Learner:
         """xgmi transport: the all-reduces are kernel launches (graph-capturable), in stream
         order after the conv backward: a fork / join inside a captured HIP graph costs ~25 us on
         this ROCm (scripts/probe_graph_concurrency.py: one side kernel 11 -> 36 us), more than the
-        overlap saves. DQN_AR_FORK=1 keeps the dense range on a side stream (channel 0) beside the
-        conv backward instead (the conv range follows on channel 1)."""
+        overlap saves (round 2 measured the dense range on a side stream beside the conv backward:
+        slower)."""
         total = self.net.grad.numel()
         if self._lowrank is not None and self._tail is not None:
             # the fc weight gradient is already the global sum (formed from the all-gathered
@@ -273,20 +279,8 @@ class Learner:
             else:                                    # every remaining piece in ONE launch
                 self.reducer.xgmi.allreduce_ranges(self.net.grad, self._ar_ranges, channel=0)
             return
-        if self._tail is None or self._dense_hi <= 0 or not _AR_FORK:
-            self._run_tail()
-            self.reducer.allreduce_range(0, total, channel=0)
-            return
-        main = torch.cuda.current_stream(self.device)
-        if self._ar_stream is None:
-            self._ar_stream = torch.cuda.Stream(device=self.device)
-        side = self._ar_stream
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self.reducer.allreduce_range(0, self._dense_hi, channel=0)
-        self._tail()
-        self.reducer.allreduce_range(self._dense_hi, total, channel=1)
-        main.wait_stream(side)
+        self._run_tail()
+        self.reducer.allreduce_range(0, total, channel=0)
 
     def _eager_step(self):
         self._sample_and_grad()
@@ -379,17 +373,22 @@ class Learner:
         torch.cuda.current_stream(self.device).wait_stream(s)
 
     # ------------------------------------------------------------- public
+    def can_step_many(self) -> bool:
+        """Whether ``step_many(k)`` replays ONE graph of k step bodies: one process, or data
+        parallelism whose collectives are in-graph kernels (xgmi). (Round 2 measured 8-step graphs
+        3x slower than one-step graphs with 2 ranks sharing ONE GPU, profiles/
+        r2_dp_multistep_graphs.md; with one GPU per rank the benchmark decides by a start-up
+        probe.)"""
+        return (self.ps is None and self.use_graph and self._graphs is not None
+                and (not self.ctx.enabled or self.reducer.in_graph) and not self._own_target)
+
     def step_many(self, k: int) -> torch.Tensor:
-        """k SGD steps with ONE host call: single-process graph mode replays a graph holding k
-        consecutive step bodies (host-light learner loops, e.g. Ape-X, whose Python thread
-        shares the GIL with the inference service); otherwise k ``step()`` calls."""
+        """k SGD steps with ONE host call when ``can_step_many()``: a graph holding k consecutive
+        step bodies (host-light learner loops, e.g. Ape-X, whose Python thread shares the GIL
+        with the inference service; the benchmark); otherwise k ``step()`` calls. A refused
+        capture raises with the host-side step state as before the attempt."""
         k = int(k)
-        # (single process only -- fused acting rides along, its state is device-side. Sync DP
-        # over the xgmi kernels would capture too, but measured with 2 ranks (one GPU, shared or
-        # disjoint CU masks: profiles/r2_dp_multistep_graphs.md) 8-step graphs ran 3x SLOWER than
-        # one-step graphs, so DP keeps one graph per step)
-        single = self.ps is None and not self.ctx.enabled
-        if k <= 1 or not single or not self.use_graph or self._graphs is None:
+        if k <= 1 or not self.can_step_many():
             for _ in range(max(1, k)):
                 self.step()
             return self.loss
@@ -399,12 +398,23 @@ class Learner:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             gk = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
-                for _ in range(k):
-                    self._sample_and_grad()
-                    if self.ctx.enabled:
-                        self._kernel_allreduce()
-                    self._apply()
+            # host-side state a step body advances (restored if the capture is refused midway)
+            ex = self.net.executor
+            saved = (self._presampled, getattr(self.net, '_noise_drawn', False), getattr(ex, '_fc_pending', None))
+            try:
+                with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
+                    for _ in range(k):
+                        self._sample_and_grad()
+                        if self.ctx.enabled:
+                            self._kernel_allreduce()
+                        self._apply()
+            except Exception:
+                self._presampled = saved[0]
+                self.net._noise_drawn = saved[1]
+                if hasattr(ex, '_fc_pending'):
+                    ex._fc_pending = saved[2]
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                raise
             torch.cuda.current_stream(self.device).wait_stream(s)
             self._graph_many = g = (k, gk)
         with trace('learner.step_many'):

@@ -163,11 +163,15 @@ class Network:
 
     # ------------------------------------------------------------- training
     def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False,
-                      sigma_grads: bool = True, lowrank: Optional[dict] = None):
+                      sigma_grads: bool = True, lowrank: Optional[dict] = None, defer_fc: bool = False):
         """Loss + gradient into ``self.grad``. ``split=True`` returns ``(loss, prio, tail)``: when
         ``tail`` is not None only the dense-layer gradients (``dense_range()``) are final and
-        ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad)."""
+        ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad). ``defer_fc``:
+        the fc weight / bias gradient is left to the next fused ``apply_grads`` (it forms them
+        inside the optimizer launch; ``HipExecutor.can_defer_fc``)."""
         kw = {}
+        if defer_fc:
+            kw['defer_fc'] = True
         if self._premixed and not sigma_grads:
             # the fused noisy optimizer follows: it derives dL/dsigma itself, and the next samples
             # are drawn by a launch of this backward (no noise launch of their own)
@@ -232,6 +236,8 @@ class Network:
                                target=self.target.flat, target_freq=int(target_freq), next_sample=next_sample, **kw)
             return True
         assert next_sample is None or not fuse, 'next_sample needs the fused optimizer+pack launch'
+        assert not (hasattr(ex, 'pending_fc') and ex.pending_fc()), \
+            'compute_grads(defer_fc=True) needs the fused optimizer+pack update'
         if fuse:
             self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,
                                 target=self.target.flat, target_freq=int(target_freq))
@@ -289,13 +295,59 @@ class Network:
         return float(self.last_loss) + self.config.reg_param * float(reg)
 
     # ----------------------------------------------------------- checkpoint
-    def state_dict(self) -> Dict[str, torch.Tensor]:
-        sd = dict(self.online.state_dict())
-        sd.update(self.optimizer.state_dict())
-        sd['global_step'] = self.global_step.cpu().view(()).clone()
+    def _flats(self) -> Dict[str, torch.Tensor]:
+        """The flat buffers a checkpoint holds (see ``state_dict``)."""
+        fl = {'online': self.online.flat, 'step': self.global_step, 'beta': self.optimizer.beta_powers}
+        for i, sl in enumerate(self.optimizer.slots):
+            fl['slot%d' % i] = sl
         if self.config.disable_target_replication:
-            sd.update({'target/' + k: v for k, v in self.target.state_dict().items()})
+            fl['target'] = self.target.flat
+        return fl
+
+    def snapshot(self):
+        """Device copies of the checkpointed buffers, taken on a side stream in stream order after
+        the work queued so far (the next step waits for the copies, ~tens of us of D2D, not for a
+        host transfer). Returns ``(snap, event)``: ``state_dict_from(snap)`` after ``event`` —
+        a writer thread can do the D2H and the file write off the training thread."""
+        fl = self._flats()
+        if not self.online.flat.is_cuda:
+            return {k: v.detach().clone() for k, v in fl.items()}, None
+        dev = self.online.flat.device
+        main = torch.cuda.current_stream(dev)
+        side = getattr(self, '_ckpt_stream', None)
+        if side is None:
+            side = self._ckpt_stream = torch.cuda.Stream(device=dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            snap = {k: v.detach().clone() for k, v in fl.items()}
+            ev = torch.cuda.Event()
+            ev.record(side)
+        main.wait_stream(side)        # the next update must not overwrite a buffer mid-copy
+        for v in snap.values():
+            v.record_stream(side)
+        return snap, ev
+
+    def state_dict_from(self, fl: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """TF-named CPU tensors from flat buffers (``_flats()`` or a ``snapshot``)."""
+        lay = self.layout
+        host = {k: v.detach().cpu() for k, v in fl.items()}
+        views = lay.views(host['online'])
+        sd = {n: views[n].clone() for n in lay.tf_order}
+        opt = self.optimizer
+        for i, suffix in enumerate(opt.slot_names()):
+            for name, v in lay.views(host['slot%d' % i]).items():
+                sd['%s/%s' % (name, suffix)] = v.clone()
+        if opt.name == 'adam':
+            sd['beta1_power'] = host['beta'][0:1].view(()).clone()
+            sd['beta2_power'] = host['beta'][1:2].view(()).clone()
+        sd['global_step'] = host['step'].view(()).clone()
+        if 'target' in host:
+            tv = lay.views(host['target'])
+            sd.update({'target/' + n: tv[n].clone() for n in lay.tf_order})
         return sd
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return self.state_dict_from(self._flats())
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]):
         self.online.load_state_dict(sd)

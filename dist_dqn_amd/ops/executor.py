@@ -104,10 +104,8 @@ class HipExecutor:
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
-        # DQN_OVERLAP_WGRAD=1: the fc + output-layer members on a parallel graph branch beside the
-        # dgrad chain instead. Measured on MI355X: 12.0k -> 9.9k steps/s (flagship), 6.7k -> 6.0k
-        # (Rainbow) -- the graph's cross-stream fork / join costs more than the overlap gains
-        self.overlap_dense_wgrad = os.environ.get('DQN_OVERLAP_WGRAD', '0') == '1'
+        # (round 2 measured the fc + output-layer members on a parallel graph branch beside the dgrad
+        # chain: 12.0k -> 9.9k steps/s, the captured fork / join costs more than the overlap gains)
         # fused optimizer+pack grid: <= 256 = grid-stride with a flat ticket; larger = one block
         # per 32x64 tile with the two-level ticket (DQN_OPT_GRID overrides, for A/B runs)
         self.opt_max_grid = int(os.environ.get('DQN_OPT_GRID', '2048'))
@@ -222,29 +220,43 @@ class HipExecutor:
                     nz[lay.offsets[d.name + '/b']] = (lay.offsets[d.name + '/b_sigma'], -1, noff + d.fin)
                     sig |= {lay.offsets[d.name + '/w_sigma'], lay.offsets[d.name + '/b_sigma']}
                     noff += d.fin + d.fout
-        fc_w = {lay.offsets[n + '/w'] for n in ('fcl', 'value/fcl', 'advantage/fcl') if n + '/w' in lay.offsets}
+        fc_names = [('value/fcl', 0), ('advantage/fcl', self.HID)] if self.dueling else [('fcl', 0)]
+        fc_w = {lay.offsets[n + '/w'] for n, _ in fc_names if n + '/w' in lay.offsets}
+        # fused fc weight gradient (optim.hip FcFuse): the dH column of each fc weight / bias tensor
+        fc_col = {}
+        for n, col in fc_names:
+            if n + '/w' in lay.offsets:
+                fc_col[lay.offsets[n + '/w']] = col
+                fc_col[lay.offsets[n + '/b']] = col
         items = []
         for src, f in sorted(fwd.items()):
             d = dg.get(src)
             so, ei, eo = nz.get(src, (-1, -1, -1))
             eff = int(self.noisy and src not in fc_w)
+            fcc = fc_col.get(src, -1)
+            assert fcc < 0 or (f.K % 8 == 0 and f.N % 8 == 0)
             for k0 in range(0, f.K, 32):
                 for n0 in range(0, f.N, 64):
                     items.append([0, src, f.K, f.N, k0, n0, f.dst_off, f.dst_N16, f.nt_off, f.ks_off,
                                   d.mode if d else 0, d.dst_off if d else 0, d.dst_N16 if d else 0,
-                                  d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0, so, ei, eo, eff])
+                                  d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0, so, ei, eo, eff,
+                                  fcc])
         for name in lay.names:
             off, n = lay.offsets[name], lay.numel(name)
             if off in fwd or off in sig:
                 continue
             c = copy.get(off)
             so, _, eo = nz.get(off, (-1, -1, -1))
+            fcc = fc_col.get(off, -1)
+            assert fcc < 0 or n <= 512, 'fused fc bias gradient: one chunk of <= 512 values'
             for s0 in range(0, n, 2048):
                 cnt = min(2048, n - s0)
                 items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + self.fs * s0) if c else -1] + [0] * 9
-                             + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy)])
+                             + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy), fcc])
         self.upd_items = items
         self._upd_dev: Dict[torch.device, torch.Tensor] = {}
+        # (x ptr, dh ptr, rows) of a step whose fc weight gradient the next update_and_pack forms
+        self._fc_pending = None
         self._bound: Dict[int, torch.Tensor] = {}   # flat ptr -> noise its packed/eff buffers reflect
         self._dummies: Dict[torch.device, tuple] = {}
 
@@ -280,7 +292,7 @@ class HipExecutor:
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
                             self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [], [],
-                            [], None, None, None, None)
+                            [], None, None, None, None, [])
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
@@ -300,7 +312,8 @@ class HipExecutor:
                         global_step: torch.Tensor, target: Optional[torch.Tensor] = None, target_freq: int = 1,
                         noise: Optional[torch.Tensor] = None, grad_noise: Optional[torch.Tensor] = None,
                         noise_dst: Optional[torch.Tensor] = None, next_sample=None,
-                        target_noise: Optional[torch.Tensor] = None, noise_rng: Optional[torch.Tensor] = None):
+                        target_noise: Optional[torch.Tensor] = None, noise_rng: Optional[torch.Tensor] = None,
+                        fc=None):
         """Optimizer step + repack in ONE launch (+ the hard target sync under the device
         predicate when ``target`` is given). Noisy nets: ``noise`` (the next sample for this
         flat) is mixed in and bound (see ``premix``); the target's packed copy is not written
@@ -313,7 +326,9 @@ class HipExecutor:
         ``target_noise`` (noisy nets): the target is mixed + packed under it in the same launch
         and bound to it (no target mix launch next step). ``noise_rng``: the stream whose next
         samples ``loss_and_grad(draw_noise=...)`` drew this step; the last block advances its
-        counter. Returns True."""
+        counter. ``fc``: the pending fused fc weight gradient of ``loss_and_grad(defer_fc=True)``
+        (default: taken from this executor; the launch forms dW = X^T dH and the fc bias gradient
+        from those rows instead of reading them from ``grad``). Returns True."""
         from ..optim import kernel_op
         dev = flat.device
         jobs = self._upd_jobs(dev)
@@ -345,12 +360,29 @@ class HipExecutor:
                              if next_sample is not None and next_sample['kind'] == 'uniform' else []),
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
-                            target_noise, teff, tpk, noise_rng)
+                            target_noise, teff, tpk, noise_rng, self._take_fc(fc))
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:
                 self._bound[target.data_ptr()] = target_noise
         return True
+
+    def _take_fc(self, fc=None):
+        if fc is None:
+            fc, self._fc_pending = self._fc_pending, None
+        if fc is None:
+            return []
+        x, dh, M = fc
+        return [int(x), int(dh), int(M), self.FLAT, self.HH]
+
+    def can_defer_fc(self, B: int, sigma_grads: bool = False) -> bool:
+        """True when ``loss_and_grad(defer_fc=True)`` at this batch leaves the fc weight / bias
+        gradient to the fused optimizer launch (16-bit builds, grouped-wgrad path)."""
+        return (bool(getattr(self.ext, 'OPTIM_FC_FUSE', 0)) and self.grouped_wgrad and not self.two_stream
+                and B <= 32 and not (self.noisy and sigma_grads))
+
+    def pending_fc(self) -> bool:
+        return self._fc_pending is not None
 
     def _plan_noisy(self):
         """Mix jobs (rainbow.hip NoisyJob): every mu tensor -> the effective buffer;
@@ -478,7 +510,7 @@ class HipExecutor:
             self.repack(target)
 
     # ------------------------------------------------------------ streams
-    def lowrank_spec(self, B: int, sigma_fused: bool = False):
+    def lowrank_spec(self, B: int, sigma_fused: bool = False, fused_fc: bool = False):
         """Low-rank DP exchange of the fc (hidden dense) layer's weight gradient, when this
         executor's grouped-wgrad Nature path runs at this batch: dW = X^T dH has rank <= B, so
         instead of all-reducing dW (1.6M values per hidden layer) the ranks all-gather X (the fc
@@ -488,7 +520,9 @@ class HipExecutor:
         all-reduces the complement), 'skip': ranges whose gradient is never read (noisy nets with
         ``sigma_fused``: the sigma tensors, whose gradient the fused optimizer derives from the
         all-reduced mu gradient), 'gather_bytes': per-rank payload} or None. Noisy nets: the
-        factors are those of dL/dW_eff, which IS the mu gradient."""
+        factors are those of dL/dW_eff, which IS the mu gradient. ``fused_fc``: the optimizer launch
+        forms dW (and the fc bias gradient) from the gathered rows itself, so the fc biases leave
+        the all-reduce as well ('skip')."""
         if (self.arch.network != 'nature' or (self.noisy and not sigma_fused) or not self.grouped_wgrad
                 or self.two_stream or B > 32):
             return None
@@ -498,6 +532,8 @@ class HipExecutor:
             return None
         skip = [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in lay.names
                 if self.noisy and (n.endswith('/w_sigma') or n.endswith('/b_sigma'))]
+        if fused_fc:
+            skip += [(lay.offsets[n[:-2] + '/b'], lay.offsets[n[:-2] + '/b'] + lay.numel(n[:-2] + '/b')) for n in names]
         return {'ranges': [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in names], 'skip': skip,
                 'gather_bytes': B * (self.FLAT + self.HH) * self.esz}
 
@@ -785,12 +821,17 @@ class HipExecutor:
 
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
-                      split: bool = False, sigma_grads: bool = True, draw_noise=None, lowrank=None):
+                      split: bool = False, sigma_grads: bool = True, draw_noise=None, lowrank=None,
+                      defer_fc: bool = False):
         """lowrank (data parallelism, see ``lowrank_spec``): {'gather': f(srcs, outs, nbytes) (an
         in-stream all-gather of two byte segments), 'world', 'rank'}. With ``split``, the fc weight
         gradient is then formed from the all-gathered factors right after the head, in stream order
         (ranks != 0 store zeros into the fc bias gradient, so the caller's all-reduce of the
         remaining range sums it exactly once).
+
+        defer_fc (``can_defer_fc``): the fc weight and bias gradients are NOT written to grad_out;
+        the next ``update_and_pack`` forms them from the fc input rows and dH rows (this rank's, or
+        the all-gathered ones under ``lowrank``) inside the optimizer launch.
 
         sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
         optimizer derives dL/dsigma from the mu-slot gradient and the noise itself.
@@ -904,8 +945,10 @@ class HipExecutor:
         hmembers, hdims = self._head_wgrad_members(ws, B, ws['h'][0].data_ptr(), (dw, db, dwv, dbv))
         fc_dgrad = lambda: self._fc_dgrad(ws, B, po, zero, draw_noise)
         if self.arch.network == 'cnn':
+            defer = bool(defer_fc) and self.can_defer_fc(B, gnoise is not None)
+            assert defer or not defer_fc, 'defer_fc: not available for this executor / batch'
             out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, gnoise, dev, fc_dgrad,
-                                     hmembers, hdims)
+                                     hmembers, hdims, defer=defer)
             return out + (None,) if split else out
         x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         mc_fc = (B + 31) // 32 * 32
@@ -930,7 +973,12 @@ class HipExecutor:
                     [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]] + hdims
             scales = [self.input_scale] + [1.0] * (len(members) - 1)
             noisy = self.noisy and gnoise is not None
-            side = None
+            defer = bool(defer_fc) and self.can_defer_fc(B, gnoise is not None)
+            assert defer or not defer_fc, 'defer_fc: not available for this executor / batch'
+            if defer and not (split and lowrank is not None):
+                # the optimizer launch forms dW_fc = x3^T dH from this rank's rows
+                self._fc_pending = (x3, ws['dh'].data_ptr(), B)
+                members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]
             if split and not noisy and lowrank is not None:
                 # (noisy nets reach here only with the sigma gradients left to the fused optimizer)
                 assert self.lowrank_spec(B, sigma_fused=True) is not None, 'low-rank exchange not available here'
@@ -951,32 +999,25 @@ class HipExecutor:
                     self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True, gather=ga)
                 else:
                     lowrank['gather'](*seg)
-                # sum over all W*B rows in one block per weight tile (64-row chunks in a fixed
-                # order, no atomics: bit-identical on every rank)
-                ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
-                               lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
-                               mloop=(W * B + 63) // 64, db_zero=rk != 0)
+                if defer:
+                    # the optimizer launch forms dW_fc and the fc bias gradient from all W*B rows
+                    self._fc_pending = (lw['x'].data_ptr(), lw['dh'].data_ptr(), W * B)
+                else:
+                    # sum over all W*B rows in one block per weight tile (64-row chunks in a fixed
+                    # order, no atomics: bit-identical on every rank)
+                    ext.qnet_wgrad(_KIND['DLR'], lw['x'].data_ptr(), [W * B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0],
+                                   lw['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH, 64, 64, 128, 1.0, False,
+                                   mloop=(W * B + 63) // 64, db_zero=rk != 0)
                 if ga is None:
                     self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True)
                 # the output layer's members join the conv members in the tail's grouped launch
                 members, dims, scales = members[:3] + members[4:], dims[:3] + dims[4:], scales[:3] + scales[4:]
             elif split and not noisy:
+                assert not defer, 'defer_fc under data parallelism needs the low-rank exchange'
                 fc_dgrad()
                 # dense weight gradients now (they need only dh, dQ and x3 / h): the dense range is final
                 ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
                 members, dims, scales = members[:3], dims[:3], scales[:3]
-            elif self.overlap_dense_wgrad and not split:
-                # fc + output-layer weight gradients on a parallel graph branch as soon as dH
-                # exists: they overlap the (latency-bound, few-CU) fc / conv3 / conv2 dgrad chain,
-                # and the closing grouped launch holds the conv members only
-                if self.dist:
-                    self._c51_dh(ws, B, po)
-                side = self._side_stream(dev)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
-                members, dims, scales = members[:3], dims[:3], scales[:3]
-                self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True)
             else:
                 fc_dgrad()
 
@@ -990,8 +1031,6 @@ class HipExecutor:
                                [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
                                 0, 0])
                 ext.qnet_wgrad_group(members, dims, scales)
-                if side is not None:
-                    main.wait_stream(side)
                 if noisy:
                     ext.qnet_noisy_grad(grad_out.data_ptr(), gnoise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                         len(self.noisy_jobs), self._noisy_max)
@@ -1082,7 +1121,7 @@ class HipCnnExecutor(HipExecutor):
         self._fc_fwd(packs, flats, ws, B, ninst)
 
     def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev, fc_dgrad,
-                      hmembers=(), hdims=()):
+                      hmembers=(), hdims=(), defer=False):
         ext = self.ext
         F, HH, H = self.FLAT, self.HH, self.HID
         pko = lambda key: po.data_ptr() + self.esz * self.poff[key]
@@ -1102,17 +1141,22 @@ class HipCnnExecutor(HipExecutor):
         if frames is not None:
             d1 += [frames.data_ptr(), 84 * 84]
             kind1 = _KIND['F1']
-        ext.qnet_wgrad_group(
-            [[kind1, s.data_ptr(), ws['dc1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout, c1.cout],
-             [_KIND['C3'], ws['p2'].data_ptr(), ws['dc3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0,
-              c3.cout, c3.cout],
-             [_KIND['C2'], ws['p1'].data_ptr(), ws['dc2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0,
-              c2.cout, c2.cout],
-             [_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH]] + list(hmembers),
-            [d1, [B * 9, c3.cout, c3.k * c3.k * c3.cin, 0, 0, 3, 3, 3, 3, t3, l3],
-             [B * 36, c2.cout, c2.k * c2.k * c2.cin, 0, 0, 11, 11, 6, 6, t2, l2],
-             [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]] + list(hdims),
-            [self.input_scale] + [1.0] * (3 + len(hmembers)))
+        members = [[kind1, s.data_ptr(), ws['dc1'].data_ptr(), c1.cout, g('conv1/w'), g('conv1/b'), 0, 0, c1.cout,
+                    c1.cout],
+                   [_KIND['C3'], ws['p2'].data_ptr(), ws['dc3'].data_ptr(), c3.cout, g('conv3/w'), g('conv3/b'), 0, 0,
+                    c3.cout, c3.cout],
+                   [_KIND['C2'], ws['p1'].data_ptr(), ws['dc2'].data_ptr(), c2.cout, g('conv2/w'), g('conv2/b'), 0, 0,
+                    c2.cout, c2.cout]]
+        dims = [d1, [B * 9, c3.cout, c3.k * c3.k * c3.cin, 0, 0, 3, 3, 3, 3, t3, l3],
+                [B * 36, c2.cout, c2.k * c2.k * c2.cin, 0, 0, 11, 11, 6, 6, t2, l2]]
+        if defer:                       # dW_fc = x3^T dH inside the optimizer launch
+            self._fc_pending = (x3, ws['dh'].data_ptr(), B)
+        else:
+            members.append([_KIND['DFWD'], x3, ws['dh'].data_ptr(), HH, fw, fb, fw2, fb2, H, HH])
+            dims.append([B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0])
+        members += list(hmembers)
+        dims += list(hdims)
+        ext.qnet_wgrad_group(members, dims, [self.input_scale] + [1.0] * (len(members) - 1))
         if self.noisy and noise is not None:
             ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                 len(self.noisy_jobs), self._noisy_max)

@@ -153,7 +153,7 @@ def optimizer_step(opt, param: torch.Tensor, grad: torch.Tensor, grad_scale: flo
     s0 = opt.slots[0] if len(opt.slots) > 0 else param
     s1 = opt.slots[1] if len(opt.slots) > 1 else param
     if getattr(opt, 'ticket', None) is None or opt.ticket.device != param.device:
-        opt.ticket = torch.zeros(1, dtype=torch.int32, device=param.device)
+        opt.ticket = torch.zeros(17 * 32, dtype=torch.int32, device=param.device)
     ext.optimizer_step(kernel_op(opt), param, grad, s0, s1, opt.beta_powers, opt.ticket,
                        float(opt.lr), float(opt.reg_param), int(opt.layout.reg_end),
                        float(grad_scale), global_step if global_step is not None else opt.beta_powers,

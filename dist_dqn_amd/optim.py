@@ -68,6 +68,24 @@ class FlatOptimizer:
         # Adam's beta powers are TF non-slot variables (beta1_power, beta2_power).
         self.beta_powers = torch.tensor([adam_b1, adam_b2], dtype=torch.float32, device=self.device)
         self.backend = backend
+        # HIP kernels: arrival tickets (1 + 16 sub-tickets, 128 B apart) and, word 1, the slot flag
+        self.ticket = (torch.zeros(17 * 32, dtype=torch.int32, device=self.device)
+                       if self.device.type == 'cuda' else None)
+        self._slots_on = False
+
+    @property
+    def defers_slots(self) -> bool:
+        """Momentum-0 RMSProp on the HIP kernels stores its ``mom`` slot (TF ``RMSProp_1``, never
+        read by the update) only on steps after ``request_slots(True)``: one fp32 write per
+        parameter less per step. The checkpoint manager raises the flag one step before a save."""
+        return (self.device.type == 'cuda' and self.backend != 'torch' and self.name == 'rmsprop'
+                and float(self.hp['rms_mom']) == 0.0)
+
+    def request_slots(self, on: bool = True):
+        """Store the deferred slot on the following steps (device flag read by every launch)."""
+        if self.defers_slots and bool(on) != self._slots_on:
+            self.ticket[1].fill_(1 if on else 0)
+            self._slots_on = bool(on)
 
     # ------------------------------------------------------------------ API
     def slot_names(self) -> List[str]:

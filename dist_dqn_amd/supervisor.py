@@ -9,6 +9,8 @@ re-done for a torch.distributed job:
     recovery_wait_secs=3" loop), plus the restored path and agent sidecar;
   * periodic checkpoints (CheckpointManager, chief only) driven from the training
     loops through ``on_train_step`` and a final save on stop;
+  * the step counter: ``global_step/sec`` written to the chief's TF event file every
+    ``summary_secs`` (TF Supervisor default 120 s; reference `main.py:136-143`, SURVEY §5.1);
   * per-rank heartbeat files under ``<logdir>/heartbeat/`` so an external
     watchdog (or ``stale_ranks()``) can see dead/hung ranks;
   * fault injection for tests: ``DQN_FAULT_INJECT="step:N[,rank:R][,mode:raise|exit|stop]"``
@@ -23,7 +25,10 @@ every ``stop_sync_steps`` train steps all ranks agree on it with one max-reduce 
 CPU control-plane group (gloo: no GPU sync), and ``should_stop()`` turns true on every
 rank at the same step. A rank that crashes instead (``raise``/``exit``, a real fault) makes
 the survivors' next collective fail (gloo: connection closed; RCCL: the process-group
-timeout); the managed block then stops them and the chief saves its last consistent state.
+timeout); the managed block then stops them WITHOUT a final save: the newest checkpoint is the
+last periodic one, written from a state that passed the consistency check (``attach_learner``:
+the in-graph xgmi transport reports a timed-out peer wait only through its error word, read
+before every save, so no checkpoint is written from a partly reduced gradient).
 """
 from __future__ import annotations
 
@@ -61,7 +66,8 @@ class RunSupervisor:
     def __init__(self, is_chief: bool = True, logdir: str = '/tmp/train_logs', network=None,
                  rank: int = 0, world_size: int = 1, save_secs: int = 600, max_to_keep: int = 5,
                  heartbeat_secs: float = 5.0, install_signal_handlers: bool = True,
-                 agent_state_fn=None, ctx=None, coordinated: bool = False, stop_sync_steps: int = 10):
+                 agent_state_fn=None, ctx=None, coordinated: bool = False, stop_sync_steps: int = 10,
+                 summary_secs: float = 120.0):
         self.is_chief = is_chief
         self.logdir = logdir
         self.rank, self.world_size = rank, world_size
@@ -80,6 +86,10 @@ class RunSupervisor:
         self.last_step = 0
         self.restored_from: Optional[str] = None
         self.agent_state: Optional[dict] = None
+        self.network = network
+        self.summary_secs = float(summary_secs)
+        self._sc_writer = None
+        self._sc_last = None            # (time, global_step) of the last step-counter sample
         if install_signal_handlers and threading.current_thread() is threading.main_thread():
             for sig in (signal.SIGINT, signal.SIGTERM):
                 try:
@@ -178,6 +188,7 @@ class RunSupervisor:
             else:
                 raise FaultInjected('injected fault at step %d (rank %d)' % (step, self.rank))
         self.heartbeat(step)
+        self._step_counter()
         if self.ckpt is not None:
             self.ckpt.maybe_save()
         if self.coordinated and step % self.stop_sync_steps == 0:
@@ -185,6 +196,25 @@ class RunSupervisor:
                 if not self._stop.is_set():
                     log.warning('Stopping at train step %d (agreed across %d ranks)', step, self.world_size)
                 self._stop.set()
+
+    def _step_counter(self):
+        """TF Supervisor's step-counter service: ``global_step/sec`` into the chief's event file
+        (one device read of global_step per ``summary_secs``)."""
+        if not self.is_chief or self.network is None or self.summary_secs <= 0:
+            return
+        now = time.time()
+        if self._sc_last is None:
+            self._sc_last = (now, int(self.network.global_step))
+            return
+        t, g = self._sc_last
+        if now - t < self.summary_secs:
+            return
+        gs = int(self.network.global_step)
+        if self._sc_writer is None:
+            from .utils.metrics import SummaryWriter
+            self._sc_writer = SummaryWriter(self.logdir)
+        self._sc_writer.add_scalar('global_step/sec', (gs - g) / (now - t), gs)
+        self._sc_last = (now, gs)
 
     # --------------------------------------------------------- managed run
     def prepare(self, broadcast_fn=None) -> Optional[str]:
@@ -205,24 +235,51 @@ class RunSupervisor:
                 (self.restored_from, self.agent_state))
         return self.restored_from
 
+    def attach_learner(self, learner):
+        """Checkpoint consistency check of this run: before every save the learner's in-graph
+        all-reduce transport (xgmi) must report a clean error word; a failure is logged with the
+        train step and the save is refused."""
+        red = getattr(learner, 'reducer', None)
+        if self.ckpt is None or red is None or getattr(red, 'xgmi', None) is None:
+            return
+
+        def check():
+            try:
+                red.check()
+            except Exception as e:
+                log.error('rank %d: gradient all-reduce failed at or before train step %d (%r): not saving a '
+                          'checkpoint from this state', self.rank, self.last_step, e)
+                raise
+        self.ckpt.check_fn = check
+
     @contextmanager
     def managed(self):
+        failed = False
         try:
             yield self
         except FaultInjected:
+            failed = True
             self._stop_now('fault injected')
             raise
         except Exception as e:
+            failed = True
             self._stop_now('exception: %r' % (e,))
             log.error('rank %d: training loop failed (%r); stopping', self.rank, e)
             raise
         finally:
-            self.stop()
+            self.stop(failed=failed)
 
-    def stop(self):
+    def stop(self, failed: bool = False):
+        """Final save on a graceful stop (not after a failure: the state may be inconsistent, the
+        last periodic checkpoint stays the newest)."""
         if self.ckpt is not None and self.is_chief:
             try:
-                self.ckpt.maybe_save(force=True)
+                if failed:
+                    self.ckpt.wait()
+                    log.warning('rank %d: no final checkpoint after a failure; newest is %s', self.rank,
+                                self.ckpt.last_path)
+                else:
+                    self.ckpt.maybe_save(force=True)
             except Exception as e:  # pragma: no cover
                 log.error('final checkpoint failed: %r', e)
         self._write_hb(self.last_step, stopping=True)

@@ -124,7 +124,8 @@ def test_supervisor_fault_injection_and_resume(tmp_path, monkeypatch):
     cfg = _cfg(tmp_path)
     net = Network.create_network(cfg, (4,), 2)
     monkeypatch.setenv('DQN_FAULT_INJECT', 'step:3,rank:0')
-    sv = RunSupervisor(True, str(tmp_path), net, save_secs=0, install_signal_handlers=False)
+    # a periodic save after every step (save_secs > 0 but tiny)
+    sv = RunSupervisor(True, str(tmp_path), net, save_secs=1e-9, install_signal_handlers=False)
     sv.prepare()
     with pytest.raises(FaultInjected):
         with sv.managed():
@@ -133,13 +134,15 @@ def test_supervisor_fault_injection_and_resume(tmp_path, monkeypatch):
                 sv.on_train_step(step)
     assert sv.should_stop()
     path = ckpt.latest_checkpoint(str(tmp_path))
-    assert path is not None and path.endswith('-3')              # final save on the failure
+    # no final save after a failure: the newest checkpoint is the last periodic one (step 2; the
+    # fault fires at step 3 before that step's save)
+    assert path is not None and path.endswith('-2')
     # relaunch: chief restores global_step and params
     monkeypatch.delenv('DQN_FAULT_INJECT')
     net2 = Network.create_network(cfg.replace(seed=9), (4,), 2)
     sv2 = RunSupervisor(True, str(tmp_path), net2, save_secs=0, install_signal_handlers=False)
     assert sv2.prepare() == path
-    assert int(net2.global_step) == 3 and torch.equal(net2.online.flat, net.online.flat)
+    assert int(net2.global_step) == 2 and torch.equal(net2.online.flat, net.online.flat)
     hb = json.load(open(os.path.join(tmp_path, 'heartbeat', 'rank0.json')))
     assert hb['rank'] == 0
     assert sv2.stale_ranks(timeout_s=3600) == []
@@ -181,5 +184,25 @@ def test_cli_ps_job_and_env_registry():
     assert main(['--job=ps']) == 0
     assert make('CartPole-v1').spec.max_episode_steps == 500
     assert make('BreakoutNoFrameskip-v4').action_space.n == 4
+    assert make('MountainCar-v0').action_space.n == 3
     with pytest.raises(ValueError):
-        make('MountainCar-v0')
+        make('LunarLander-v2')
+
+
+def test_step_counter_writes_global_step_per_sec(tmp_path):
+    """TF Supervisor's step counter (`/root/reference/src/main.py:136-143`): the chief writes
+    ``global_step/sec`` into its event file every summary_secs."""
+    import glob
+    import time
+    cfg = _cfg(tmp_path)
+    net = Network.create_network(cfg, (4,), 2)
+    sv = RunSupervisor(True, str(tmp_path), net, save_secs=0, install_signal_handlers=False, summary_secs=0.02)
+    sv.prepare()
+    with sv.managed():
+        for step in range(1, 6):
+            net.global_step.fill_(10 * step)
+            sv.on_train_step(step)
+            time.sleep(0.03)
+    recs = [r for p in glob.glob(os.path.join(tmp_path, 'events.out.tfevents.*')) for r in read_tfrecords(p)]
+    tagged = [r for r in recs if b'global_step/sec' in r]
+    assert len(tagged) >= 3, len(tagged)

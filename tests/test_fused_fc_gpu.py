@@ -1,0 +1,211 @@
+"""The fc weight gradient formed inside the fused optimizer launch (optim.hip FcFuse) and the
+production head kernels' loss / dL/dQ against a loss computed purely in torch.
+
+* deferred fc gradient: a learner step whose optimizer launch forms dW_fc = X^T dH (and the fc
+  bias gradient) from the rows, vs the same step with the gradient written by the grouped
+  weight-gradient launch and read back (``--fuse_fc_wgrad=0``); every parameter, slot and
+  packed fragment must agree (the fc bias to summation order);
+* the same against the pure-torch fp32 oracle gradient of the fc layer;
+* head_loss_kernel / c51_train_kernel: loss, dL/dQ (dL/dlogits) and dH of the kernel vs torch
+  autograd of ``models/losses.py`` on the very hidden rows the kernel consumed (fp32 output
+  layer in torch; the kernel's output layer runs on bf16 MFMA fragments).
+
+Reference: the optimizer site `/root/reference/src/network.py:198-202` (``minimize``) and the
+loss `/root/reference/src/network.py:141-157`.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda', 0)
+RAINBOW = '--distributional --noisy --dueling --double_dqn --optimizer=adam'
+
+
+def _learner(extra, fuse, seed=0, B=32):
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    kind = 'atari' if extra.startswith('cnn:') else 'nature'
+    extra = extra[4:] if extra.startswith('cnn:') else extra
+    cfg = preset(kind, 'Pong-v0', '--seed=%d --backend=hip --dtype=bf16 --minibatch_size=%d --fuse_fc_wgrad=%d '
+                 '--replay_memory_capacity=4096 --reg_param=0.001 %s' % (seed, B, int(fuse), extra))
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(seed + 1)
+    # larger-than-init weights so every layer carries signal
+    net.online.flat.normal_(0.0, 0.03, generator=g)
+    net.target.flat.copy_(net.online.flat)
+    net.refresh_packed()
+    rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=seed + 5, prioritized=cfg.prioritized_replay)
+    rep.fill_synthetic(4096, 6)
+    return net, Learner(net, rep, cfg, use_graph=False)
+
+
+def _state(net):
+    out = {'flat': net.online.flat.clone(), 'step': net.global_step.clone()}
+    for i, s in enumerate(net.optimizer.slots):
+        out['slot%d' % i] = s.clone()
+    return out
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', 'cnn:', RAINBOW,
+                                   '--optimizer=rmsprop --prioritized_replay --double_dqn'])
+def test_deferred_fc_grad_matches_materialised(extra):
+    runs = []
+    for fuse in (True, False):
+        net, learner = _learner(extra, fuse)
+        assert learner._defer_fc == fuse
+        learner.step()
+        torch.cuda.synchronize()
+        assert not net.executor.pending_fc()
+        one = _state(net)
+        for _ in range(2):
+            learner.step()
+        torch.cuda.synchronize()
+        runs.append((net, one, _state(net)))
+    (na, a1, a3), (_, b1, b3) = runs
+    lay = na.layout
+    fc = {n for n in lay.names if 'fcl/' in n}
+    assert fc, lay.names
+    for n in lay.names:
+        o, k = lay.offsets[n], lay.numel(n)
+        for key in a1:
+            if key == 'step':
+                continue
+            x, y = a1[key][o:o + k], b1[key][o:o + k]
+            if n not in fc:
+                # after one step the other gradients come from the same launches (up to the conv
+                # weight gradients' fp32 atomics: their summation order varies run to run)
+                torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-9, msg='%s %s' % (key, n))
+            elif n.endswith('/w') or n.endswith('/w_sigma'):
+                # dW: the same MFMA dot products over the same rows
+                torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-9, msg='%s %s' % (key, n))
+            else:                      # the fc bias sums its rows in another order
+                torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-7, msg='%s %s' % (key, n))
+            # two more steps carry that rounding downstream (Adam's normalised steps amplify it
+            # elementwise: compare the tensors' relative L2 distance)
+            u, w = a3[key][o:o + k].double(), b3[key][o:o + k].double()
+            assert float((u - w).norm() / (w.norm() + 1e-30)) < 1e-3, ('3 steps', key, n)
+    assert torch.equal(a3['step'], b3['step'])
+
+
+def test_rmsprop_mom_slot_written_only_when_requested():
+    """Momentum-0 RMSProp: the `mom` slot (TF RMSProp_1, never read) is stored only on steps
+    after request_slots(True) -- then it holds that step's update, w_before - w_after."""
+    net, learner = _learner('--optimizer=rmsprop', True)
+    opt = net.optimizer
+    assert opt.defers_slots
+    mom = opt.slots[1]
+    learner.step()
+    torch.cuda.synchronize()
+    assert float(mom.abs().max()) == 0.0
+    opt.request_slots(True)
+    w0 = net.online.flat.clone()
+    learner.step()
+    torch.cuda.synchronize()
+    upd = w0 - net.online.flat
+    lay = net.layout
+    for n in lay.names:
+        o, k = lay.offsets[n], lay.numel(n)
+        torch.testing.assert_close(mom[o:o + k], upd[o:o + k], rtol=1e-3, atol=1e-9, msg=n)
+    assert float(mom.abs().max()) > 0.0
+    opt.request_slots(False)
+    before = mom.clone()
+    learner.step()
+    torch.cuda.synchronize()
+    assert torch.equal(before, mom)
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling', 'cnn:'])
+def test_deferred_fc_update_matches_fp32_oracle(extra):
+    """One step's fc update (SGD, so w' = w - lr * g exactly) from the fused launch vs the
+    PyTorch fp32 oracle's fc gradient on the same minibatch."""
+    from dist_dqn_amd.models.executor import TorchExecutor
+    net, learner = _learner(extra + ' --optimizer=sgd --lr=0.5 --fuse_sampling=0', True)
+    cfg = net.config
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+                           huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
+    w0 = net.online.flat.clone()
+    tgt = net.target.flat.clone()
+    learner.step()
+    torch.cuda.synchronize()
+    # the minibatch the step used: the learner's sampled indices, gathered as materialised states
+    batch = learner.replay.gather(learner.idx)
+    g_ref = torch.zeros_like(w0)
+    oracle.loss_and_grad(w0, tgt, batch, g_ref, None, None)
+    lay = net.layout
+    for n in lay.names:
+        if 'fcl/' not in n:
+            continue
+        o, k = lay.offsets[n], lay.numel(n)
+        g = (w0[o:o + k] - net.online.flat[o:o + k]) / 0.5
+        if n.endswith('/w'):
+            g = g - 0.001 * w0[o:o + k]           # decoupled L2 on the fc weights (reg_param)
+        ref = g_ref[o:o + k]
+        cos = float(torch.nn.functional.cosine_similarity(g, ref, dim=0))
+        ratio = float(g.norm() / (ref.norm() + 1e-12))
+        assert cos > 0.985 and abs(ratio - 1.0) < 0.05, (n, cos, ratio)
+
+
+def _head_torch(net, ws, B, batch, dist):
+    """Pure-torch loss on the kernel's own hidden rows: (loss, dL/dout, dH)."""
+    from dist_dqn_amd.models import losses
+    ex, lay = net.executor, net.layout
+    HH, A = ex.HH, ex.A
+    hs = [ws['h'][i][:B * HH].view(B, HH).float() for i in range(3 if ex.double else 2)]
+    flats = [net.online.flat, net.target.flat, net.online.flat]
+    W = lambda f: f[lay.offsets['output/w']:lay.offsets['output/w'] + lay.numel('output/w')].view(HH, -1)
+    bias = lambda f: f[lay.offsets['output/b']:lay.offsets['output/b'] + lay.numel('output/b')]
+    outs = [h @ W(f) + bias(f) for h, f in zip(hs, flats)]
+    o0 = outs[0].detach().requires_grad_(True)
+    if dist:
+        N = ex.atoms
+        v = net.arch
+        loss, _ = losses.c51_loss(o0.view(B, A, N), batch['actions'], batch['rewards'], batch['dones'],
+                                  outs[1].view(B, A, N), outs[2].view(B, A, N) if ex.double else None,
+                                  batch['gammas'].view(-1, 1), v.v_min, v.v_max)
+    else:
+        loss, _ = losses.scalar_td_loss(o0, batch['actions'], batch['rewards'], batch['dones'], outs[1],
+                                        outs[2] if ex.double else None, batch['gammas'],
+                                        net.config.loss, net.config.huber_delta)
+    loss.backward()
+    dout = o0.grad
+    dh = (dout @ W(net.online.flat).t()) * (hs[0] > 0).float()
+    return float(loss), dout, dh
+
+
+@pytest.mark.parametrize('extra', ['', '--double_dqn --loss=huber', '--distributional', '--distributional --double_dqn'])
+def test_head_kernels_match_pure_torch_loss(extra):
+    """head_loss_kernel / c51_train_kernel vs torch autograd on the same hidden rows: the loss,
+    the dL/dQ (dL/dlogits) rows the kernel hands to the output layer's weight gradient, and dH."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.models.network import Network
+    B = 32
+    cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 %s' % extra)
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    net.online.flat.normal_(0.0, 0.03, generator=g)
+    net.target.flat.normal_(0.0, 0.03, generator=g)
+    net.refresh_packed()
+    batch = {
+        'states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
+        'next_states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
+        'actions': torch.randint(0, 6, (B,), dtype=torch.int32, device=DEV, generator=g),
+        'rewards': torch.randn(B, device=DEV, generator=g) * 5.0,
+        'dones': (torch.rand(B, device=DEV, generator=g) < 0.2).float(),
+        'gammas': torch.full((B,), 0.99, device=DEV),
+    }
+    ex = net.executor
+    grad = torch.zeros_like(net.online.flat)
+    loss, _ = ex.loss_and_grad(net.online.flat, net.target.flat, batch, grad, None, None)
+    torch.cuda.synchronize()
+    ws = ex._workspace(B, DEV)
+    dist = ex.dist
+    loss_ref, dout_ref, dh_ref = _head_torch(net, ws, B, batch, dist)
+    assert abs(float(loss) - loss_ref) / abs(loss_ref) < 1e-2, (float(loss), loss_ref)
+    width = ex.c51_KD if dist else 64
+    dq = ws['dq16'][:B * width].view(B, width)[:, :dout_ref.shape[1]].float()
+    rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-12))
+    assert rel(dq, dout_ref) < 2e-2, rel(dq, dout_ref)
+    dh = ws['dh'][:B * ex.HH].view(B, ex.HH).float()
+    assert rel(dh, dh_ref) < 3e-2, rel(dh, dh_ref)
