@@ -617,6 +617,7 @@ int64_t mlp_lds_bytes(std::vector<int64_t> ints) {
 }  // namespace
 
 void register_infer_server(pybind11::module_& m);   // infer_server.cpp
+void register_ingest_server(pybind11::module_& m);  // ingest_server.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dist_dqn_amd native extension (gfx950 HIP kernels + C++ host runtime)";
@@ -662,4 +663,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ring_size", &ring_size);
   register_net_ops(m);
   register_infer_server(m);
+  register_ingest_server(m);
 }

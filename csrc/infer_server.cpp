@@ -6,7 +6,9 @@
 // The reference answers each actor with a batch-1 session.run against the PS parameters
 // (/root/reference/src/dqn_agent.py:155-189).
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <pybind11/pybind11.h>
+#include <sched.h>
 
 #include <atomic>
 #include <chrono>
@@ -49,6 +51,9 @@ class InferServer {
     execs_[m] = reinterpret_cast<hipGraphExec_t>(exec);
   }
 
+  // pin the serving thread to one CPU (-1: no pinning); before start()
+  void set_cpu(int64_t cpu) { cpu_ = (int)cpu; }
+
   void start() {
     if (running_) return;
     bucket_.assign(n_ + 1, 0);                      // bucket lookup table: smallest graph >= m
@@ -78,6 +83,12 @@ class InferServer {
   void run() {
     try {
       HIPCK(hipSetDevice(device_));
+      if (cpu_ >= 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(cpu_, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof(set), &set);   // (best effort)
+      }
       int lo = 0, hi = 0;
       HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
       hipStream_t st;
@@ -111,6 +122,7 @@ class InferServer {
   void* dev_out_;
   int32_t* pin_out_;
   int device_;
+  int cpu_ = -1;
   int64_t gap_us_;
   std::vector<hipGraphExec_t> execs_;
   std::vector<int64_t> bucket_;
@@ -131,6 +143,7 @@ void register_infer_server(pybind11::module_& m) {
   pybind11::class_<InferServer>(m, "InferServer", pybind11::module_local())
       .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>())
       .def("set_graph", &InferServer::set_graph)
+      .def("set_cpu", &InferServer::set_cpu)
       .def("start", &InferServer::start)
       .def("stop", &InferServer::stop, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("stats", &InferServer::stats);

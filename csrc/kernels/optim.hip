@@ -10,6 +10,7 @@
 // then the TF update rule. Adam's beta powers (TF non-slot variables) are
 // read by every block and advanced by the LAST block to finish (arrival
 // ticket), together with global_step, so no extra launch is needed.
+#include <stdlib.h>
 #include <type_traits>
 #include "common.h"
 #include "sample_dev.h"
@@ -22,6 +23,7 @@ struct OptHP {
   float lr, reg, grad_scale;
   float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
   int reg_end;
+  int nt;            // probe: 1 = fp32 weight / slot stores non-temporal (DQN_OPT_NT)
 };
 
 // Contraction is pinned off in the update math so every kernel that inlines it
@@ -398,7 +400,11 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     };
     auto st = [&](float* base, int64_t off, const float* v) {
       if constexpr (AL) {
-        if (ok[0]) *reinterpret_cast<float4*>(base + off + d0) = make_float4(v[0], v[1], v[2], v[3]);
+        if (ok[0]) {
+          f32x4* p = reinterpret_cast<f32x4*>(base + off + d0);
+          const f32x4 x = {v[0], v[1], v[2], v[3]};
+          if (h.nt) __builtin_nontemporal_store(x, p); else *p = x;
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -662,6 +668,7 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
+  h.nt = 0;
   const int n4 = n / 4;
   dim3 grid(grid_for_ticket(n4)), block(256);
   switch (op) {
@@ -687,6 +694,8 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
+  static const int nt_env = getenv("DQN_OPT_NT") ? atoi(getenv("DQN_OPT_NT")) : 0;
+  h.nt = nt_env;
   // max_grid <= 256: grid-stride over the jobs with a flat ticket (<= 256 arrivals);
   // larger: one block per job (up to max_grid) with the two-level ticket
   const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};

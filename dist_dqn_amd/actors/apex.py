@@ -12,9 +12,13 @@ MI355X-native design:
     forward on the GPU (``serve``) using the live online weights, so actors
     never hold stale parameter copies and nothing is broadcast;
   * transitions travel through a lock-free SPSC ring per actor in shared
-    memory (csrc/host/spsc_ring.cpp); ``drain`` moves them into the HBM
-    replay's pinned staging buffers, which flush as H2D copies on a side
-    stream (replay/device.py), frames stored once (slot stacks per actor);
+    memory (csrc/host/spsc_ring.cpp); a native ingest thread (csrc/ingest_server.cpp)
+    moves them into pinned staging and ships them as H2D copies on its own stream
+    ordered against the learner stream with events (frames stored once, slot stacks
+    per actor), so the learner's Python thread only replays learner graphs (without the
+    native thread: ``drain`` on the learner thread, replay/device.py);
+  * CPU reservation (``--apex_reserve_cpus``): the learner thread, the ingest thread and
+    the inference-server thread each get a core of their own; the actors share the rest;
   * under data parallelism every rank runs its own pool into its own replay
     shard (sharded replay; gradients all-reduced as usual).
 
@@ -72,6 +76,7 @@ class ActorSpec:
     state_bytes: int
     reward_clip: float = 0.0
     max_frames: int = 0                     # stop after this many env steps (0 = until told)
+    cpus: Optional[Sequence[int]] = None    # CPUs the actor process may run on (None: inherited)
 
 
 def _map(path: str, nbytes: int, create: bool = False) -> np.memmap:
@@ -90,6 +95,11 @@ def actor_main(spec: ActorSpec):
         try:
             os.nice(nice)
         except OSError:
+            pass
+    if spec.cpus:
+        try:
+            os.sched_setaffinity(0, set(spec.cpus))
+        except (OSError, AttributeError):
             pass
     lib = load()
     ring_all = _map(spec.ring_path, spec.ring_offset + spec.ring_bytes)
@@ -225,6 +235,11 @@ class ApexActorPool:
         self._closed = False
 
     # -------------------------------------------------------------- life
+    def set_actor_cpus(self, cpus: Optional[Sequence[int]]):
+        """Restrict the actor processes to these CPUs (before ``start``)."""
+        for sp in self.specs:
+            sp.cpus = tuple(cpus) if cpus else None
+
     def start(self):
         for s in self.specs:
             p = self._ctx.Process(target=actor_main, args=(s,), daemon=True, name='apex-actor-%d' % s.index)
@@ -404,6 +419,10 @@ class ApexTrainer:
         self.serve_calls = 0
         self.learn_t0 = None                # wall time / env frames when the learner took its first step
         self.learn_frames0 = 0
+        self.native_ingest = bool(getattr(config, 'apex_native_ingest', 1))
+        self.reserve_cpus = int(getattr(config, 'apex_reserve_cpus', 3))
+        self._ingest = None                 # native ingest server (csrc/ingest_server.cpp)
+        self._cpus = None                   # (learner, ingest, inference) CPUs when reserved
         self.loop_time = {'drain': 0.0, 'step': 0.0, 'iters': 0}   # main-loop wall split (bench)
 
     def _refresh_snapshot(self):
@@ -494,6 +513,8 @@ class ApexTrainer:
                               int(self.serve_gap_s * 1e6))
         for m in sizes:
             srv.set_graph(m, self._graphs[m].raw_cuda_graph_exec())
+        if self._cpus is not None and hasattr(srv, 'set_cpu'):
+            srv.set_cpu(self._cpus[2])
         srv.start()
         self._server = srv
         log.info('Ape-X inference: native server thread, graph buckets %s', sizes)
@@ -510,6 +531,90 @@ class ApexTrainer:
                 log.error('Ape-X native inference server failed: %s', err)
             self._server = None
 
+    # ----------------------------------------------------------- native ingest
+    def _plan_cpus(self):
+        """Reserve one CPU each for the learner thread, the ingest thread and the inference
+        thread out of this process's allowed set (when it leaves the actors at least 4); the
+        actor processes are restricted to the rest."""
+        try:
+            cpus = sorted(os.sched_getaffinity(0))
+        except AttributeError:
+            return
+        r = self.reserve_cpus
+        if r <= 0 or len(cpus) < r + 4:
+            return
+        res = cpus[:r] + [cpus[r - 1]] * (3 - r) if r < 3 else cpus[:3]
+        self._cpus = (res[0], res[1], res[2])
+        self.pool.set_actor_cpus(cpus[r:])
+        try:
+            os.sched_setaffinity(0, {self._cpus[0]})      # this (learner) thread; restored by run()
+            self._cpus_prev = cpus
+        except OSError:
+            self._cpus = None
+            return
+        log.info('Ape-X CPUs: learner %d, ingest %d, inference %d; %d actors on %d CPUs', self._cpus[0],
+                 self._cpus[1], self._cpus[2], self.pool.n, len(cpus) - r)
+
+    def _start_native_ingest(self) -> bool:
+        """Ring ingest + H2D shipping on a C++ thread (csrc/ingest_server.cpp): the replay's
+        host cursors are handed to it until ``_stop_native_ingest``."""
+        r, pool = self.replay, self.pool
+        ext = getattr(self.net.executor, 'ext', None)
+        if (not self.native_ingest or self.device.type != 'cuda' or ext is None or not hasattr(ext, 'IngestServer')
+                or pool.frame_hw is None or not getattr(r, 'frame_mode', False) or r.device_writer):
+            return False
+        torch = self.torch
+        assert r.staged() == 0, 'native ingest starts with empty host staging'
+        words = r.ingest_state_size(pool.k, pool.n_step)
+        self._ing_state = np.zeros((pool.n, words), dtype=np.int32)
+        base = pool.rings.ctypes.data
+        self._ing_rings = np.array([base + i * pool.ring_stride for i in range(pool.n)], dtype=np.int64)
+        H, W = r.obs_shape
+        dev = [r.frames.data_ptr(), r.state_idx.data_ptr(), r.next_idx.data_ptr(), r.actions.data_ptr(),
+               r.rewards.data_ptr(), r.dones.data_ptr(), r.gammas.data_ptr(), r.size_dev.data_ptr()]
+        per = ([r.tree.sum.data_ptr(), r.tree.min.data_ptr(), r.tree.max_p.data_ptr(), r.tree.P]
+               if r.prioritized else [0, 0, 0, 0])
+        cfg = [pool.k, pool.n_step, H * W, r.capacity, r.num_frames, 1024, 6, 256, 5000,
+               self.device.index if self.device.index is not None else 0,
+               self._cpus[1] if self._cpus is not None else -1]
+        stream = torch.cuda.current_stream(self.device)
+        torch.cuda.synchronize(self.device)
+        self._ingest = ext.IngestServer(int(self._ing_rings.ctypes.data), pool.n, int(self._ing_state.ctypes.data),
+                                        words, float(pool.gamma), dev, per, [r._f_next, r._t_next, r._size], cfg,
+                                        int(stream.cuda_stream))
+        self._ingest_stream = stream
+        self._ing_seen = (0, 0)
+        self._ingest.start()
+        log.info('Ape-X ingest: native thread (%d rings -> %d-transition pinned staging sets)', pool.n, 1024)
+        return True
+
+    def _ingest_poll(self):
+        """Fold the native ingest's counters into the pool's (frames, episodes, returns)."""
+        consumed, frames, eps, flushes, size, err = self._ingest.stats()
+        if err:
+            raise RuntimeError('Ape-X native ingest failed: %s' % err)
+        f0, e0 = self._ing_seen
+        self.pool.frames += frames - f0
+        self.pool.episodes += eps - e0
+        self._ing_seen = (frames, eps)
+        self.pool.returns.extend(self._ingest.pop_returns())
+        return size
+
+    def _stop_native_ingest(self):
+        srv, self._ingest = self._ingest, None
+        if srv is None:
+            return
+        srv.stop()
+        f, t, sz = srv.cursors()
+        self._ingest = srv
+        try:
+            self._ingest_poll()
+        finally:
+            self._ingest = None
+        r = self.replay
+        r._f_next, r._t_next, r._size = int(f), int(t), int(sz)
+        r._reset_stage()
+
     def _serve_loop(self):
         from ..utils.trace import trace
         while not self._stop.is_set():
@@ -525,9 +630,11 @@ class ApexTrainer:
         from ..utils.trace import trace
         cfg = self.config
         start = max(cfg.minibatch_size, cfg.replay_start_size)
+        self._plan_cpus()
         self.pool.start()
         if not self._start_native_server():
             self._thread.start()
+        native = self._start_native_ingest()
         t0 = last = time.time()
         steps_at_last = frames_at_last = 0
         # sync-DP Ape-X: every learner step is a collective, so local reasons to stop (time
@@ -551,16 +658,23 @@ class ApexTrainer:
         sys.setswitchinterval(self.gil_switch_s)
         last_drain = 0.0
         try:
+            size = 0
             while True:
                 ta = time.perf_counter()
-                if ta - last_drain >= self.drain_every_s or self.replay.size() < start:
+                if native:
+                    if ta - last_drain >= 0.01 or size < start:      # counters only: the thread ingests
+                        size = self._ingest_poll()
+                        last_drain = ta
+                elif ta - last_drain >= self.drain_every_s or self.replay.size() < start:
                     with trace('apex.drain'):
                         self.pool.drain(self.replay)
                     last_drain = ta
+                if not native:
+                    size = self.replay.size()
                 tb = time.perf_counter()
                 self.loop_time['drain'] += tb - ta
                 self.loop_time['iters'] += 1
-                if self.replay.size() >= start:
+                if size >= start:
                     if self.learn_t0 is None:
                         self.learn_t0, self.learn_frames0 = time.time(), self.pool.frames
                     if cuda and len(inflight) >= self.max_inflight:
@@ -587,12 +701,12 @@ class ApexTrainer:
                     mean = float(np.mean(self.pool.returns)) if self.pool.returns else 0.0
                     log.info('apex: %d actors alive, frames %d (%.0f/s), sgd steps %d (%.1f/s), episodes %d, '
                              'last-100 mean return %.2f, replay %d', self.pool.alive(), self.pool.frames, fps,
-                             self.learner.train_steps, sps, self.pool.episodes, mean, self.replay.size())
+                             self.learner.train_steps, sps, self.pool.episodes, mean, size)
                     if self.metrics is not None:
                         self.metrics.write(kind='apex', frames=self.pool.frames, env_frames_per_sec=fps,
                                            training_steps=self.learner.train_steps, sgd_steps_per_sec=sps,
                                            episodes=self.pool.episodes, mean100=mean,
-                                           replay_size=self.replay.size(), actors_alive=self.pool.alive())
+                                           replay_size=size, actors_alive=self.pool.alive())
                     last, steps_at_last, frames_at_last = now, self.learner.train_steps, self.pool.frames
                 if max_train_steps and self.learner.train_steps >= max_train_steps:
                     break
@@ -602,9 +716,13 @@ class ApexTrainer:
                     log.warning('Received signal to stop. Exiting Ape-X loop.')
                     break
                 if self.pool.alive() == 0 and self.pool.procs:
+                    if native:
+                        self._stop_native_ingest()          # (its final pass drains the rings)
+                        native = False
                     self.pool.drain(self.replay)
                     self.replay.flush()
-                    if self.replay.size() < start:
+                    size = self.replay.size()
+                    if size < start:
                         if coordinated:
                             # this rank can never step again, so it cannot reach the agreed stop
                             # either: fail loudly (the peers' next collective fails, no final save)
@@ -623,5 +741,12 @@ class ApexTrainer:
                 self._thread.join(5.0)
             self.pool.lib.mbox_set_stop(self.pool.mbox, 1)      # (releases actors and the native server)
             self._stop_native_server()
+            self._stop_native_ingest()
             self.pool.stop()
+            prev = getattr(self, '_cpus_prev', None)
+            if prev:
+                try:
+                    os.sched_setaffinity(0, set(prev))
+                except OSError:
+                    pass
         return self

@@ -146,6 +146,12 @@ def build_parser() -> argparse.ArgumentParser:
            'stop request')
     a('--device_graph_steps', default=8, type=int,
       help='--device_envs (one process): SGD steps per replayed HIP graph')
+    a('--apex_native_ingest', default=1, type=int,
+      help='Ape-X (GPU, image envs): move the actors\' ring records into the HBM replay from a C++ thread '
+           '(csrc/ingest_server.cpp) instead of the learner\'s Python thread')
+    a('--apex_reserve_cpus', default=3, type=int,
+      help='Ape-X: CPUs reserved for the learner, ingest and inference threads (one each; the actor '
+           'processes run on the rest); 0 = no pinning')
     a('--apex_graph_steps', default=4, type=int,
       help='Ape-X learner: SGD steps per replayed HIP graph (one host call per that many steps)')
     a('--apex_serve_gap_us', default=100, type=int,
@@ -256,6 +262,8 @@ class Config:
     apex_ring: int = 1024
     apex_serve_gap_us: int = 100
     apex_graph_steps: int = 4
+    apex_native_ingest: int = 1
+    apex_reserve_cpus: int = 3
     device_envs: int = 0
     device_graph_steps: int = 8
     apex_native_serve: int = 1

@@ -1,8 +1,10 @@
-"""Multi-rank learner on ONE MI355X: two ranks share cuda:0 over a gloo process group
+"""Multi-rank learner on ONE MI355X: 2, 4 or 8 ranks share cuda:0 over a gloo process group
 (DQN_DIST_BACKEND=gloo; RCCL refuses two ranks per device). This runs the exact
 world > 1 code path of the learner that RCCL runs on an 8-GPU node — split HIP
 graphs, dense-range all-reduce started before the conv-backward graph, second
-collective, optimizer graph — with real GPU tensors, and checks it against the
+collective, optimizer graph; with --allreduce=xgmi the peer-to-peer kernels at their
+world-size instantiations (WC = 2 / 4 / 8), the 8-peer gather and the low-rank fc exchange
+feeding the fused optimizer with W*B rows — with real GPU tensors, and checks it against the
 non-overlapped single-collective path and across replicas.
 """
 import os
@@ -135,10 +137,11 @@ def _worker_xgmi(rank, world, port, wire, errq):
         raise
 
 
-@pytest.mark.parametrize('wire', ['fp32', 'bf16'])
-def test_xgmi_allreduce_two_ranks_one_gpu(wire):
-    """The peer-to-peer kernel (IPC-mapped fine-grained buffers) against exact sums."""
-    _run_ranks(_worker_xgmi, (wire,))
+@pytest.mark.parametrize('world,wire', [(2, 'fp32'), (2, 'bf16'), (4, 'fp32'), (8, 'fp32'), (8, 'bf16')])
+def test_xgmi_allreduce_ranks_one_gpu(world, wire):
+    """The peer-to-peer kernel (IPC-mapped fine-grained buffers) against exact sums, at the
+    world sizes the node runs (the WC = 2 / 4 / 8 instantiations, the 8-peer gather)."""
+    _run_ranks(_worker_xgmi, (wire,), world=world, timeout=100 + 20 * world)
 
 
 RAINBOW_DP = '--distributional --noisy --dueling --double_dqn --optimizer=adam --lr=0.0000625'
@@ -187,6 +190,8 @@ def _worker(rank, world, port, network, extra, errq):
                 # no noisy layers, fp32 wire); overlap=0 is the full all-reduce it is compared with
                 lowrank = bool(overlap) and network == 'nature' and 'bf16' not in extra
                 assert (ln._lowrank is not None) == lowrank, (overlap, extra)
+                # ... and then feeds the fused optimizer (fc dW from the W*B gathered rows)
+                assert ln._defer_fc == lowrank, (overlap, extra)
             elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
             outs[overlap] = net.online.flat.clone()
@@ -214,40 +219,49 @@ def _worker(rank, world, port, network, extra, errq):
         raise
 
 
-@pytest.mark.parametrize('network,extra', [('nature', '--allreduce=rccl'),
-                                           ('nature', '--allreduce=rccl --dueling --double_dqn --loss=huber'),
-                                           ('atari', '--allreduce=rccl'),
-                                           ('nature', '--allreduce=rccl --allreduce_dtype=bf16'),
-                                           ('nature', '--allreduce=xgmi'),
-                                           ('nature', '--allreduce=xgmi --dueling --double_dqn --loss=huber'),
-                                           ('atari', '--allreduce=xgmi'),
-                                           ('nature', '--allreduce=xgmi --allreduce_dtype=bf16'),
-                                           # Rainbow minus PER: noisy sigma gradients are derived in the
-                                           # optimizer from the all-reduced mu gradients under the
-                                           # rank-shared noise stream, so replicas stay bit-identical
-                                           ('nature', '--allreduce=rccl ' + RAINBOW_DP),
-                                           ('nature', '--allreduce=xgmi ' + RAINBOW_DP)])
-def test_dp_learner_two_ranks_one_gpu(network, extra):
+@pytest.mark.parametrize('world,network,extra', [
+    (2, 'nature', '--allreduce=rccl'),
+    (2, 'nature', '--allreduce=rccl --dueling --double_dqn --loss=huber'),
+    (2, 'atari', '--allreduce=rccl'),
+    (2, 'nature', '--allreduce=rccl --allreduce_dtype=bf16'),
+    (2, 'nature', '--allreduce=xgmi'),
+    (2, 'nature', '--allreduce=xgmi --dueling --double_dqn --loss=huber'),
+    (2, 'atari', '--allreduce=xgmi'),
+    (2, 'nature', '--allreduce=xgmi --allreduce_dtype=bf16'),
+    # Rainbow minus PER: noisy sigma gradients are derived in the optimizer from the all-reduced
+    # mu gradients under the rank-shared noise stream, so replicas stay bit-identical
+    (2, 'nature', '--allreduce=rccl ' + RAINBOW_DP),
+    (2, 'nature', '--allreduce=xgmi ' + RAINBOW_DP),
+    # the node's world sizes: W*B = 128 / 256 all-gathered rows into the fused optimizer, the
+    # WC = 4 / 8 all-reduce of the remaining ranges
+    (4, 'nature', '--allreduce=xgmi'),
+    (4, 'nature', '--allreduce=rccl'),
+    (4, 'nature', '--allreduce=xgmi --dueling --double_dqn --loss=huber'),
+    (8, 'nature', '--allreduce=xgmi'),
+    (8, 'nature', '--allreduce=xgmi ' + RAINBOW_DP)])
+def test_dp_learner_ranks_one_gpu(world, network, extra):
     """(--allreduce=rccl means the process group's collective: gloo in this rehearsal.)"""
-    _run_ranks(_worker, (network, extra))
+    _run_ranks(_worker, (network, extra), world=world, timeout=100 + 25 * world)
 
 
-def test_bench_two_ranks_replicas_equal(tmp_path):
-    """bench.py under torchrun (2 ranks on one GPU over gloo): the JSON line reports the
-    end-of-run replica check, the world size and the transport."""
+@pytest.mark.parametrize('world', [2, 4])
+def test_bench_ranks_replicas_equal(tmp_path, world):
+    """bench.py under torchrun (2 / 4 ranks on one GPU over gloo): the JSON line reports the
+    end-of-run replica check, the world size, the transport and the graph-steps probe."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, DQN_DIST_BACKEND='gloo', OMP_NUM_THREADS='4')
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % world,
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(root, 'bench.py'),
-           '--gpus', '2', '--steps', '20', '--warmup', '5', '--replay', '20000']
-    out = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=110)
+           '--gpus', str(world), '--steps', '20', '--warmup', '5', '--replay', '20000']
+    out = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=200)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith('{')][-1]
     d = json.loads(line)
-    assert d['n_gpus'] == 2 and d['config']['world_size'] == 2
+    assert d['n_gpus'] == world and d['config']['world_size'] == world
+    assert d['graph_steps'] in (1, 8) and d['ms_per_step_g1'] > 0
     assert d['config']['replicas_equal'] is True and d['config']['replicas_diverged'] == []
     assert d['config']['dist_backend'] == 'gloo'
 

@@ -107,7 +107,8 @@ def test_rmsprop_mom_slot_written_only_when_requested():
     lay = net.layout
     for n in lay.names:
         o, k = lay.offsets[n], lay.numel(n)
-        torch.testing.assert_close(mom[o:o + k], upd[o:o + k], rtol=1e-3, atol=1e-9, msg=n)
+        # (w_before - w_after rounds to the weights' ulp, ~2e-9 at |w| ~ 0.03)
+        torch.testing.assert_close(mom[o:o + k], upd[o:o + k], rtol=1e-3, atol=2e-8, msg=n)
     assert float(mom.abs().max()) > 0.0
     opt.request_slots(False)
     before = mom.clone()
