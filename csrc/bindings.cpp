@@ -466,6 +466,73 @@ int64_t xgmi_ipc_open(torch::Tensor handle) {
 }
 void xgmi_ipc_close(int64_t p) { if (p) (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); }
 
+// ------------------------------------------------------ async PS over xGMI (async_ps.hip)
+// A page-aligned host range (e.g. a shared /dev/shm mapping) registered for GPU access:
+// returns its device address (kernels poll / publish the PS control words there).
+int64_t host_register(int64_t p, int64_t nbytes) {
+  TORCH_CHECK(p && nbytes > 0 && (p & 4095) == 0, "host_register: page-aligned range");
+  TORCH_CHECK(hipHostRegister(reinterpret_cast<void*>(p), (size_t)nbytes, hipHostRegisterMapped) == hipSuccess,
+              "hipHostRegister failed");
+  void* d = nullptr;
+  TORCH_CHECK(hipHostGetDevicePointer(&d, reinterpret_cast<void*>(p), 0) == hipSuccess,
+              "hipHostGetDevicePointer failed");
+  return reinterpret_cast<int64_t>(d);
+}
+void host_unregister(int64_t p) { if (p) (void)hipHostUnregister(reinterpret_cast<void*>(p)); }
+
+// non-owning fp32 view of n floats of device memory at p (a peer-mapped / fine-grained region)
+torch::Tensor tensor_from_ptr(int64_t p, int64_t n, int64_t device) {
+  TORCH_CHECK(p && n > 0 && (p & 15) == 0, "tensor_from_ptr: 16-byte aligned pointer");
+  return torch::from_blob(reinterpret_cast<void*>(p), {n},
+                          torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, (int)device));
+}
+
+void ps_push(torch::Tensor grad, int64_t slot, int64_t push_word, torch::Tensor seq, int64_t kind,
+             torch::Tensor ticket) {
+  CHECK_T(grad, torch::kFloat32); CHECK_T(seq, torch::kInt64); CHECK_T(ticket, torch::kInt32);
+  TORCH_CHECK(grad.numel() % 4 == 0 && slot && push_word && (slot & 15) == 0 && kind >= 0 && kind < 16,
+              "ps_push args");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
+  launch_ps_push(ptr<float>(grad), reinterpret_cast<float*>(slot), (long)grad.numel(),
+                 reinterpret_cast<uint64_t*>(push_word), ptr<int64_t>(seq), (int)kind, ptr<int32_t>(ticket),
+                 cur_stream());
+}
+
+// seq: int64 [2] = (push number, gate number) device words of this worker
+void ps_pull(torch::Tensor flat, int64_t snap, torch::Tensor step, int64_t snap_step, int64_t done_word,
+             torch::Tensor seq, torch::Tensor gate, torch::Tensor err, torch::Tensor stopped, int64_t timeout_ns) {
+  CHECK_T(flat, torch::kFloat32); CHECK_T(step, torch::kInt64); CHECK_T(seq, torch::kInt64);
+  CHECK_T(gate, torch::kInt64); CHECK_T(err, torch::kInt32); CHECK_T(stopped, torch::kInt32);
+  TORCH_CHECK(gate.numel() >= 2, "ps_pull: gate = [seq, status]");
+  TORCH_CHECK(flat.numel() % 4 == 0 && snap && snap_step && done_word && (snap & 15) == 0, "ps_pull args");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(flat.device());
+  launch_ps_pull(ptr<float>(flat), reinterpret_cast<const float*>(snap), (long)flat.numel(), ptr<int64_t>(step),
+                 reinterpret_cast<const int64_t*>(snap_step), reinterpret_cast<const uint64_t*>(done_word),
+                 ptr<int64_t>(seq), ptr<int64_t>(gate), ptr<int32_t>(err), ptr<int32_t>(stopped), (long long)timeout_ns,
+                 cur_stream());
+}
+
+// flat / step undefined: signal only (e.g. STOP)
+void ps_publish(int64_t snap, c10::optional<torch::Tensor> flat, int64_t snap_step, c10::optional<torch::Tensor> step,
+                int64_t done_word, int64_t value, torch::Tensor ticket, int64_t n) {
+  CHECK_T(ticket, torch::kInt32);
+  const float* f = nullptr;
+  const int64_t* s = nullptr;
+  if (flat.has_value() && flat->defined()) {
+    CHECK_T((*flat), torch::kFloat32);
+    TORCH_CHECK(flat->numel() == n && n % 4 == 0 && snap && (snap & 15) == 0, "ps_publish: flat");
+    f = ptr<float>(*flat);
+  }
+  if (step.has_value() && step->defined()) {
+    CHECK_T((*step), torch::kInt64);
+    s = ptr<int64_t>(*step);
+  }
+  TORCH_CHECK(done_word && (s == nullptr || snap_step), "ps_publish args");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ticket.device());
+  launch_ps_publish(reinterpret_cast<float*>(snap), f, (long)n, reinterpret_cast<int64_t*>(snap_step), s,
+                    reinterpret_cast<uint64_t*>(done_word), (uint64_t)value, ptr<int32_t>(ticket), cur_stream());
+}
+
 // grad: fp32 GPU slice to reduce in place; data/sig: one pointer per rank (mine included)
 // ranges (optional): [lo0, hi0, lo1, hi1, ...] element ranges of grad summed as ONE vector
 void xgmi_allreduce(torch::Tensor grad, std::vector<int64_t> data, std::vector<int64_t> sig, int64_t seq,
@@ -625,6 +692,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp", &mlp);
   m.def("mlp_lds_bytes", &mlp_lds_bytes);
   m.def("xgmi_alloc", &xgmi_alloc);
+  m.def("host_register", &host_register);
+  m.def("host_unregister", &host_unregister);
+  m.def("tensor_from_ptr", &tensor_from_ptr);
+  m.def("ps_push", &ps_push);
+  m.def("ps_pull", &ps_pull);
+  m.def("ps_publish", &ps_publish);
   m.def("xgmi_free", &xgmi_free);
   m.def("xgmi_ipc_handle", &xgmi_ipc_handle);
   m.def("xgmi_ipc_open", &xgmi_ipc_open);

@@ -117,6 +117,15 @@ struct XgmiGatherArgs {
 }  // namespace dqn
 int launch_xgmi_allgather(const dqn::XgmiGatherArgs& a, int blocks, hipStream_t st);
 
+// Asynchronous parameter server over xGMI peer memory, csrc/kernels/async_ps.hip.
+void launch_ps_push(const float* grad, float* slot, long n, uint64_t* push_word, int64_t* seq, int kind,
+                    int32_t* ticket, hipStream_t st);
+void launch_ps_pull(float* flat, const float* snap, long n, int64_t* step, const int64_t* snap_step,
+                    const uint64_t* done_word, const int64_t* seq, int64_t* gate, int32_t* err, int32_t* stopped,
+                    long long timeout_ns, hipStream_t st);
+void launch_ps_publish(float* snap, const float* flat, long n, int64_t* snap_step, const int64_t* step,
+                       uint64_t* done_word, uint64_t value, int32_t* ticket, hipStream_t st);
+
 // Fused MLP Q-network (reference SimpleNetwork), csrc/kernels/mlp.hip.
 namespace dqn {
 constexpr int kMlpMaxLayers = 4;

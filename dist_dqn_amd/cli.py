@@ -70,8 +70,8 @@ def run_worker(config: Config):
                               alpha=config.per_alpha, seed=seed + ctx.rank)
         ps = None
         if config.async_ps and ctx.enabled:
-            from .parallel.async_ps import AsyncPSClient
-            ps = AsyncPSClient(ctx, network.online.flat)
+            from .parallel.async_ps import make_ps_client
+            ps = make_ps_client(ctx, network.online.flat, config)
             # start from the PS parameters (and the PS-owned target under --disable_target_replication)
             ps.pull(network.online.flat, network.global_step,
                     target=network.target.flat if config.disable_target_replication else None)
@@ -118,12 +118,21 @@ def _replica_check(ctx, network, metrics, steps: int):
 def _run_parameter_server(config: Config, ctx, network, sv):
     """--async_ps rank 0: the parameter server (no env, no replay): applies every
     worker's gradient push in arrival order and answers with fresh parameters."""
-    from .parallel.async_ps import AsyncPSServer
-    server = AsyncPSServer(ctx, network)
-    log.info('async PS on rank 0 serving %d workers', len(server.workers))
-    with sv.managed():
-        server.serve(supervisor=sv)
-    log.info('async PS done: %d updates %s', server.updates, server.per_worker)
+    import time
+    from .parallel.async_ps import make_ps_server
+    server = make_ps_server(ctx, network, config)
+    log.info('async PS on rank 0 serving %d workers (%s transport)', len(server.workers),
+             getattr(server, 'transport', 'p2p'))
+    t0 = time.perf_counter()
+    try:
+        with sv.managed():
+            server.serve(supervisor=sv)
+    finally:
+        if hasattr(server, 'close'):
+            server.close()
+    el = time.perf_counter() - t0
+    log.info('async PS done: %d updates (%.0f updates/s) %s', server.updates, server.updates / max(el, 1e-9),
+             server.per_worker)
     return server
 
 

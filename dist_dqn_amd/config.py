@@ -184,6 +184,9 @@ def build_parser() -> argparse.ArgumentParser:
     a('--max_to_keep', default=5, type=int)
     a('--save_agent_state', action='store_true', help='Checkpoint epsilon/step sidecar')
     a('--async_ps', action='store_true', help='Emulate async parameter-server updates')
+    a('--ps_transport', default='auto', choices=['auto', 'p2p', 'xgmi'],
+      help='--async_ps transport: one-sided xGMI peer memory (GPU; replicated targets) or '
+           'torch.distributed point-to-point; auto = xgmi when available')
     a('--max_train_steps', default=0, type=int, help='Stop after N learner steps (0 = no limit)')
     a('--allreduce_check_steps', default=1000, type=int,
       help='xgmi transport: read its peer-timeout error word every N learner steps (host sync)')
@@ -280,6 +283,7 @@ class Config:
     max_to_keep: int = 5
     save_agent_state: bool = False
     async_ps: bool = False
+    ps_transport: str = 'auto'
     max_train_steps: int = 0
     allreduce_check_steps: int = 1000
     stop_sync_steps: int = 10

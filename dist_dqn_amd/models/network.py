@@ -205,15 +205,19 @@ class Network:
                 break
         return 0, end
 
-    def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None, next_sample=None) -> bool:
+    def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None, next_sample=None,
+                    grad: Optional[torch.Tensor] = None) -> bool:
         """Optimizer step (global_step += 1 inside it) + executor repack.
 
         target_freq: also do the hard target sync (target <- online when the new
         global_step % target_freq == 0, device predicate) inside those same two
         launches. Returns True when it was fused that way; otherwise the caller
         still owes the target update (``hard_target_update``). next_sample: ``(spec, B)`` — the
-        fused launch also draws the next uniform minibatch (only honoured when it returns True)."""
+        fused launch also draws the next uniform minibatch (only honoured when it returns True).
+        grad: the gradient buffer to apply (default ``self.grad``; the xgmi parameter server passes
+        a worker's peer-written slot)."""
         ex = self.executor
+        g = self.grad if grad is None else grad
         fuse = (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
                 and hasattr(ex, 'packed'))
         if fuse and hasattr(ex, 'update_and_pack') and (self._premixed or not getattr(ex, 'noisy', False)):
@@ -232,21 +236,21 @@ class Network:
                     self.executor.draw_noise(self.noise_next, self.noise_target, self.noise_rng)
                 kw.update(noise=self.noise_next, grad_noise=self.noise, noise_dst=self.noise,
                           target_noise=self.noise_target)
-            ex.update_and_pack(self.optimizer, self.online.flat, self.grad, grad_scale, self.global_step,
+            ex.update_and_pack(self.optimizer, self.online.flat, g, grad_scale, self.global_step,
                                target=self.target.flat, target_freq=int(target_freq), next_sample=next_sample, **kw)
             return True
         assert next_sample is None or not fuse, 'next_sample needs the fused optimizer+pack launch'
         assert not (hasattr(ex, 'pending_fc') and ex.pending_fc()), \
             'compute_grads(defer_fc=True) needs the fused optimizer+pack update'
         if fuse:
-            self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step,
+            self.optimizer.step(self.online.flat, g, grad_scale, self.global_step,
                                 target=self.target.flat, target_freq=int(target_freq))
             # (noisy nets: every consumer re-mixes + repacks under its own noise sample)
             if not getattr(ex, 'noisy', False):
                 ex.repack(self.online.flat, target=self.target.flat, step=self.global_step,
                           freq=int(target_freq))
             return True
-        self.optimizer.step(self.online.flat, self.grad, grad_scale, self.global_step)
+        self.optimizer.step(self.online.flat, g, grad_scale, self.global_step)
         self._repack()
         return False
 

@@ -212,3 +212,263 @@ class AsyncPSClient:
             return                     # the PS already dropped this worker
         self._out.hdr[0] = BYE
         dist.send(self._out.buf, dst=0)
+
+
+# ----------------------------------------------------------------------------------------------
+# Transport over xGMI peer memory (csrc/kernels/async_ps.hip): one-sided device writes of the
+# gradient into the PS's per-worker slot, device reads of the PS's per-worker parameter
+# snapshot, control words in a host page shared by every rank and mapped into their GPUs.
+_CTL_STRIDE = 128                     # bytes per worker: push word @0, done word @64
+_BYE = 15                             # push kind: the worker leaves
+_STOP_STATUS = 1                      # done status: the PS stopped
+
+
+class _PSShared:
+    """Rank 0's fine-grained HBM region ([W-1] gradient slots, [W-1] parameter snapshots, [W-1]
+    int64 step words) exported over IPC, and the shared host control page, mapped by every rank."""
+
+    def __init__(self, ctx: DistContext, n: int):
+        import os
+        import uuid
+
+        import numpy as np
+        from ..ops import _ext
+        self.ext = ext = _ext.load(required=True)
+        self.ctx, self.n = ctx, n
+        self.W = ctx.world_size
+        self.slot_bytes = (4 * n + 255) // 256 * 256
+        nw = self.W - 1
+        total = 2 * nw * self.slot_bytes + 64 * nw
+        err, handle = None, None
+        self.base, self.opened = 0, False
+        if ctx.rank == 0:
+            try:
+                self.base = ext.xgmi_alloc(total)
+                handle = ext.xgmi_ipc_handle(self.base)
+            except Exception as e:  # noqa: BLE001
+                err = e
+        path = None
+        if ctx.rank == 0 and err is None:
+            shm = '/dev/shm' if os.path.isdir('/dev/shm') else '/tmp'
+            path = os.path.join(shm, 'dqn_ps_ctl_%s' % uuid.uuid4().hex[:12])
+        self.ctl_bytes = (self.W * _CTL_STRIDE + 4095) // 4096 * 4096
+        if path is not None:
+            try:
+                np.memmap(path, dtype=np.uint8, mode='w+', shape=(self.ctl_bytes,))[:] = 0
+            except Exception as e:  # noqa: BLE001
+                err, path = e, None
+        handle, path = ctx.ctrl_broadcast_object((handle, path))
+        self.path = path
+        self.ctl = None
+        self.ctl_dev = 0
+        if handle is not None and path is not None and err is None:
+            try:
+                self.ctl = np.memmap(path, dtype=np.uint8, mode='r+', shape=(self.ctl_bytes,))
+                self.ctl_dev = ext.host_register(int(self.ctl.ctypes.data), self.ctl_bytes)
+                if ctx.rank != 0:
+                    self.base = ext.xgmi_ipc_open(handle)
+                    self.opened = True
+            except Exception as e:  # noqa: BLE001
+                err = e
+        ok = torch.tensor([0 if err is not None or handle is None else 1], dtype=torch.int32, device=ctx.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok) != 1:
+            self.close()
+            raise RuntimeError('async PS over xgmi: setup failed on some rank (here: %s)' % (err,))
+        self.words = self.ctl.view(np.uint64)
+
+    def slot(self, w: int) -> int:
+        return self.base + (w - 1) * self.slot_bytes
+
+    def snap(self, w: int) -> int:
+        return self.base + (self.W - 1 + w - 1) * self.slot_bytes
+
+    def snap_step(self, w: int) -> int:
+        return self.base + 2 * (self.W - 1) * self.slot_bytes + 64 * (w - 1)
+
+    def push_word(self, w: int, dev: bool = True):
+        return (self.ctl_dev if dev else 0) + w * _CTL_STRIDE
+
+    def done_word(self, w: int, dev: bool = True):
+        return (self.ctl_dev if dev else 0) + w * _CTL_STRIDE + 64
+
+    def read_push(self, w: int) -> int:
+        return int(self.words[w * _CTL_STRIDE // 8])
+
+    def read_done(self, w: int) -> int:
+        return int(self.words[(w * _CTL_STRIDE + 64) // 8])
+
+    def close(self):
+        import os
+        if self.ctl_dev:
+            self.ext.host_unregister(int(self.ctl.ctypes.data))
+            self.ctl_dev = 0
+        self.ctl = None
+        if self.opened:
+            self.ext.xgmi_ipc_close(self.base)
+            self.opened = False
+        elif self.base:
+            self.ext.xgmi_free(self.base)
+        self.base = 0
+        if self.ctx.rank == 0 and self.path:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+class XgmiPSServer:
+    """Rank 0 of ``--async_ps`` over xGMI peer memory: the same arrival-order semantics as
+    `AsyncPSServer` (each push is applied with the fused optimizer to whatever the PS holds,
+    then that worker gets the fresh parameters and int64 global_step), with no message copies:
+    the optimizer reads the worker's gradient slot in place and one kernel writes the worker's
+    snapshot and raises its done word. The host loop only polls the shared control page."""
+
+    transport = 'xgmi'
+
+    def __init__(self, ctx: DistContext, network, shared: Optional[_PSShared] = None):
+        assert ctx.enabled and ctx.rank == 0 and ctx.world_size >= 2
+        assert not getattr(network.config, 'disable_target_replication', False), \
+            'the xgmi PS transport keeps replicated targets (use --ps_transport=p2p)'
+        self.ctx, self.net = ctx, network
+        self.n = network.online.flat.numel()
+        self.sh = shared or _PSShared(ctx, self.n)
+        self.workers = list(range(1, ctx.world_size))
+        dev = network.online.flat.device
+        self._grads = {w: self.sh.ext.tensor_from_ptr(self.sh.slot(w), self.n, dev.index or 0) for w in self.workers}
+        self._ticket = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.updates = 0
+        self.per_worker = {w: 0 for w in self.workers}
+        self.stopped_workers = 0
+        self.busy_s = 0.0
+
+    def _publish(self, w: int, seq: int, status: int = 0):
+        st = status == 0
+        self.sh.ext.ps_publish(self.sh.snap(w), self.net.online.flat if st else None, self.sh.snap_step(w),
+                               self.net.global_step if st else None, self.sh.done_word(w), (seq << 4) | status,
+                               self._ticket, self.n)
+
+    def serve(self, max_updates: int = 0, idle_sleep: float = 2e-5, supervisor=None) -> int:
+        seen = {}
+        for w in self.workers:                # initial pull (push number 1): the PS parameters
+            self._publish(w, 1)
+            seen[w] = 1
+        active = set(self.workers)
+        t_busy = time.perf_counter()
+        while active and not (max_updates and self.updates >= max_updates):
+            got = False
+            for w in sorted(active):
+                v = self.sh.read_push(w)
+                s, kind = v >> 4, v & 15
+                if s <= seen[w]:
+                    continue
+                got = True
+                seen[w] = s
+                if kind == _BYE:
+                    active.discard(w)
+                    continue
+                if supervisor is not None and supervisor.should_stop():
+                    self._publish(w, s, _STOP_STATUS)
+                    active.discard(w)
+                    self.stopped_workers += 1
+                    continue
+                # arrival-order apply, the gradient read in place from the worker's slot
+                self.net.apply_grads(1.0, grad=self._grads[w])
+                self._publish(w, s)
+                self.updates += 1
+                self.per_worker[w] += 1
+                if supervisor is not None:
+                    supervisor.on_train_step(self.updates)
+            if not got:
+                time.sleep(idle_sleep)
+        torch.cuda.synchronize(self.net.online.flat.device)
+        self.busy_s = time.perf_counter() - t_busy
+        return self.updates
+
+    def close(self):
+        self.sh.close()
+
+
+class XgmiPSClient:
+    """Ranks >= 1 of ``--async_ps`` over xGMI: ``exchange`` enqueues the push (peer stores into
+    the PS slot + push word) and the pull (wait for the done word, snapshot -> local parameters
+    and global_step) on the current stream with no host synchronisation."""
+
+    transport = 'xgmi'
+
+    def __init__(self, ctx: DistContext, flat: torch.Tensor, shared: Optional[_PSShared] = None,
+                 timeout_s: float = 60.0):
+        assert ctx.enabled and ctx.rank >= 1
+        self.ctx, self.w = ctx, ctx.rank
+        self.n = flat.numel()
+        self.sh = shared or _PSShared(ctx, self.n)
+        dev = flat.device
+        self._seq = torch.ones(1, dtype=torch.int64, device=dev)      # push number 1 = the initial pull
+        self._gate = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._stopped = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._ticket = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._empty = torch.zeros(0, dtype=torch.float32, device=dev)
+        self.timeout_ns = int(timeout_s * 1e9)
+        self.pushes = 0
+        self.target_updated = False
+        self._host_pushes = 1
+
+    @property
+    def stopped(self) -> bool:
+        """The PS answered STOP (host read of the shared done word, no GPU sync)."""
+        return (self.sh.read_done(self.w) & 15) == _STOP_STATUS
+
+    def _pull(self, flat, global_step):
+        step = global_step if global_step is not None else torch.zeros(1, dtype=torch.int64, device=flat.device)
+        self.sh.ext.ps_pull(flat, self.sh.snap(self.w), step, self.sh.snap_step(self.w), self.sh.done_word(self.w),
+                            self._seq, self._gate, self._err, self._stopped, self.timeout_ns)
+
+    def pull(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None, target=None):
+        self._pull(flat, global_step)
+
+    def exchange(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None,
+                 sync_target: bool = False, target: Optional[torch.Tensor] = None) -> bool:
+        if self.stopped:
+            return False
+        self.sh.ext.ps_push(grad, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
+        self._pull(flat, global_step)
+        self.pushes += 1
+        return True
+
+    def check(self) -> bool:
+        """False if a pull timed out waiting for the PS (host sync)."""
+        return int(self._err[0]) == 0
+
+    def close(self):
+        if not self.stopped:
+            self.sh.ext.ps_push(self._empty, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, _BYE,
+                                self._ticket)
+        torch.cuda.synchronize(self._seq.device)
+        self.sh.close()
+
+
+def ps_transport(ctx: DistContext, config) -> str:
+    """'xgmi' or 'p2p' for --async_ps (identical on every rank: decided from the config)."""
+    want = getattr(config, 'ps_transport', 'auto')
+    if want == 'p2p' or ctx.device.type != 'cuda' or getattr(config, 'disable_target_replication', False):
+        return 'p2p'
+    return 'xgmi'
+
+
+def make_ps_server(ctx: DistContext, network, config):
+    if ps_transport(ctx, config) == 'xgmi':
+        try:
+            return XgmiPSServer(ctx, network)
+        except RuntimeError as e:
+            log.warning('async PS over xgmi unavailable (%s): torch.distributed p2p instead', e)
+    return AsyncPSServer(ctx, network)
+
+
+def make_ps_client(ctx: DistContext, flat: torch.Tensor, config):
+    if ps_transport(ctx, config) == 'xgmi':
+        try:
+            return XgmiPSClient(ctx, flat)
+        except RuntimeError as e:
+            log.warning('async PS over xgmi unavailable (%s): torch.distributed p2p instead', e)
+    return AsyncPSClient(ctx, flat)

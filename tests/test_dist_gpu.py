@@ -266,20 +266,22 @@ def test_bench_ranks_replicas_equal(tmp_path, world):
     assert d['config']['dist_backend'] == 'gloo'
 
 
-def _worker_async_ps(rank, world, port, errq):
+def _worker_async_ps(rank, world, port, transport, errq):
     """--async_ps on the GPU: rank 0 is the parameter server (HIP fused optimizer on its HBM
     copy), ranks 1..world-1 run the HIP Nature-CNN learner against it (push gradient, pull
-    parameters + int64 global_step). Three ranks share cuda:0 over gloo p2p."""
+    parameters + int64 global_step). Three ranks share cuda:0 over gloo (p2p: the messages;
+    xgmi: setup only -- the data moves by one-sided peer access, the control words through a
+    host-shared page)."""
     try:
         _setup(rank, world, port)
         from dist_dqn_amd.config import preset
         from dist_dqn_amd.learner import Learner
         from dist_dqn_amd.models.network import Network
         from dist_dqn_amd.parallel import broadcast_state, init_distributed
-        from dist_dqn_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
+        from dist_dqn_amd.parallel.async_ps import make_ps_client, make_ps_server
         from dist_dqn_amd.replay import DeviceReplay
         cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=5 --backend=hip --replay_memory_capacity=2048 '
-                     '--async_ps --target_update_freq=3')
+                     '--async_ps --target_update_freq=3 --ps_transport=%s' % transport)
         ctx = init_distributed(cfg, device='cuda')
         net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
         assert net.executor.name.startswith('hip'), net.executor.name
@@ -287,17 +289,23 @@ def _worker_async_ps(rank, world, port, errq):
         init = net.online.flat.clone()
         steps = 5
         if rank == 0:
-            srv = AsyncPSServer(ctx, net)
+            srv = make_ps_server(ctx, net, cfg)
+            assert getattr(srv, 'transport', 'p2p') == transport, srv
             n = srv.serve()
             torch.cuda.synchronize()
             assert n == steps * (world - 1) and srv.per_worker == {w: steps for w in range(1, world)}
             assert int(net.global_step) == n
             assert torch.isfinite(net.online.flat).all()
             assert not torch.equal(net.online.flat, init), 'the PS applied no update'
+            ps_params = net.online.flat.clone()
+            if hasattr(srv, 'close'):
+                dist.barrier()                            # (workers verified their last pull)
+                srv.close()
         else:
             rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
             rep.fill_synthetic(2048, 6, seed=rank)
-            ps = AsyncPSClient(ctx, net.online.flat)
+            ps = make_ps_client(ctx, net.online.flat, cfg)
+            assert getattr(ps, 'transport', 'p2p') == transport, ps
             ps.pull(net.online.flat, net.global_step)
             net.refresh_packed()
             ln = Learner(net, rep, cfg, ctx, ps_client=ps)
@@ -309,8 +317,15 @@ def _worker_async_ps(rank, world, port, errq):
             assert torch.isfinite(ln.loss).all()
             assert ps.pushes == steps
             assert seen == sorted(seen) and len(set(seen)) == steps, seen    # the PS step only moves forward
-            ps.close()
-        dist.barrier()
+            assert all(1 <= s <= steps * (world - 1) for s in seen), seen
+            if transport == 'xgmi':
+                assert ps.check()
+                ps.close()
+                dist.barrier()
+            else:
+                ps.close()
+        if transport != 'xgmi':
+            dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # noqa: BLE001 - report to the parent
         import traceback
@@ -318,5 +333,6 @@ def _worker_async_ps(rank, world, port, errq):
         raise
 
 
-def test_async_ps_hip_learners_one_gpu():
-    _run_ranks(_worker_async_ps, (), world=3, timeout=150)
+@pytest.mark.parametrize('transport', ['p2p', 'xgmi'])
+def test_async_ps_hip_learners_one_gpu(transport):
+    _run_ranks(_worker_async_ps, (transport,), world=3, timeout=150)
