@@ -149,7 +149,9 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 c10::optional<torch::Tensor> eff, c10::optional<torch::Tensor> grad_noise,
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
                 std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
-                c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng, std::vector<int64_t> fc) {
+                c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng, std::vector<int64_t> fc,
+                int64_t part) {
+  // part: 0 or the base of the grouped conv wgrad's partial buffer (jobs with part_n > 0 sum it)
   // fc: [] or [x ptr, dh ptr, M, ldx, ldh]: the launch forms the fc weight / bias gradient of the
   // jobs carrying a dH column from those act_t rows (optim.hip FcFuse) instead of reading `grad`
   // noise_rng (noisy nets): [seed, counter] of the noise stream whose next samples an earlier
@@ -293,7 +295,8 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     ptr<int64_t>(step), ptr<int32_t>(ticket), h, (float)lr, (float)reg, (int)reg_end,
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
-                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, fc.empty() ? nullptr : &ff, cur_stream());
+                    per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, fc.empty() ? nullptr : &ff,
+                    reinterpret_cast<const float*>(part), cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {

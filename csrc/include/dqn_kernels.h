@@ -58,7 +58,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
-                       int64_t* noise_rng, const FcFuse* fc, hipStream_t st);
+                       int64_t* noise_rng, const FcFuse* fc, const float* part, hipStream_t st);
 // 1 when this build's optimizer launch can form the fc weight gradient itself (16-bit builds)
 int optim_fc_fuse();
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)

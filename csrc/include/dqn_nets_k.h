@@ -65,6 +65,11 @@ struct WgradArgs {
   int atomic;
   int mloop;                 // > 1: each block sums this many consecutive M-chunks (no atomics)
   int db_zero;               // store 0 into db / db2 (the low-rank DP member on ranks != 0)
+  // deterministic partials (grouped conv members): chunk group c (mloop consecutive M-chunks)
+  // stores its sum plainly at part + c * pstride ([K][N] weights, then [N] bias); the fused
+  // optimizer sums the groups in a fixed order (no atomics: run-to-run bit-identical)
+  float* part;
+  int pstride;
 };
 
 // Device actor step (eps-greedy + synthetic env + replay append), see actor.hip.

@@ -181,6 +181,9 @@ struct UpdJob {
   // fc weight tile / fc bias chunk whose gradient the launch forms from FcFuse rows: the
   // tensor's first column in dH (-1: read the flat gradient)
   int fc_col;
+  // gradient = sum of part_n partial slices (the grouped conv wgrad's deterministic chunk-group
+  // sums, qnet.hip): element d of the tensor at part[part_off + p * part_stride + d], p ascending
+  int part_off, part_n, part_stride;
 };
 
 DQN_DEV float fnz(float x) { return copysignf(sqrtf(fabsf(x)), x); }
@@ -209,7 +212,8 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                   act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
                   int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
-                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff) {
+                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff,
+                  const float* __restrict__ part) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
@@ -441,7 +445,19 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         }
       }
 #endif
-      if (!fcj) ld(G, mo, g);
+      if (part != nullptr && jb.part_n > 0) {
+        // fixed-order sum of the chunk-group partials (block-uniform branch), 4 loads in flight
+        float pv[4];
+        ld(part, jb.part_off, g);
+#pragma unroll 4
+        for (int p = 1; p < jb.part_n; ++p) {
+          ld(part, jb.part_off + (int64_t)p * jb.part_stride, pv);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[j] += pv[j];
+        }
+      } else if (!fcj) {
+        ld(G, mo, g);
+      }
     }
     // factorised-noise factors: f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
     float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
@@ -689,7 +705,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
                        int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
-                       void* tpk, int64_t* noise_rng, const FcFuse* fc, hipStream_t st) {
+                       void* tpk, int64_t* noise_rng, const FcFuse* fc, const float* part, hipStream_t st) {
   OptHP h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
@@ -714,7 +730,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                    (pe.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0);
 #define OPM(N, M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, \
                        beta_pow, step, ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, \
-                       sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng, ff)
+                       sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng, ff, part)
 #if DQN_ACT_F32
 #define OPK(N) do { switch (mode) { \
     case 0: OPM(N, 0); break; case 1: OPM(N, 1); break; case 3: OPM(N, 3); break; \

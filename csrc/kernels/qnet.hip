@@ -655,6 +655,100 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     }
   }
 }
+
+// Deterministic grouped mode (no atomics): chunks bx .. bx + nch - 1 summed in registers in
+// ascending order, then plain stores (the caller points dw / db at its partial slice)
+template <class LD, int MC, int KB, int NB>
+DQN_DEV void wgrad_block_det(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, act_t* lds, int nch) {
+  using Tl = WgradTile<MC, KB, NB>;
+  constexpr int SA = Tl::SA, SZ = Tl::SZ;
+  constexpr int TPR = 256 / MC;                  // threads per staged row
+  constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
+  constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
+  static_assert(256 % MC == 0 && (KB / 8) % TPR == 0 && (NB / 8) % TPR == 0 && TILES % 4 == 0 && NB <= 256,
+                "tiling");
+  act_t* At = lds;                               // [MC][SA]
+  act_t* Zt = lds + MC * SA;                     // [MC][SZ]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k_lo = by * KB, n_lo = bz * NB;
+  const bool dob = g.db != nullptr && by == 0;
+  // operand lane map: k-group gq = lane >> 4 takes m rows {4 gq + q} (elements 0..3) and
+  // {16 + 4 gq + q} (elements 4..7) of each 32-row k-step -- the same permutation of the
+  // reduction index on both operands; one 32-lane half reads 8 consecutive rows per instruction
+  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+  constexpr int NTt = NB / 16;
+  f32x4 acc[PERW];
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    const int r = threadIdx.x % MC, p = threadIdx.x / MC;
+    const int m = (bx + c) * MC + r;
+    const bool mok = m < a.M;
+    const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
+    LD ld(a, 0, m);
+    bfx8 va[GA], vz[GZ];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int k0 = k_lo + (p + i * TPR) * 8;
+      va[i] = sel8(k0 < a.K, ld.frag(min(k0, a.K - 8)));          // (clamped: no branch per load)
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;              // clamped into the dZ row
+      vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
+    }
+    if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (p + i * TPR) * 8) = va[i];
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[i];
+    __syncthreads();
+    if (dob && (int)threadIdx.x < NB) {
+#pragma unroll 8
+      for (int q = 0; q < MC; ++q) dbs += (float)Zt[q * SZ + threadIdx.x];
+    }
+#pragma unroll
+    for (int i = 0; i < PERW; ++i) {
+      const int tile = wave + 4 * i;
+      const int kt = tile / NTt, nt = tile - kt * NTt;
+      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
+      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
+        const bfx8 bf = join_tr(lds_tr16(pz + 32 * s * SZ), lds_tr16(pz + (32 * s + 16) * SZ));
+        acc[i] = mfma16(af, bf, acc[i]);
+      }
+    }
+  }
+  const bool atomic = g.atomic != 0;
+  if (dob && (int)threadIdx.x < NB) {
+    const int nn = n_lo + threadIdx.x;
+    if (nn < g.N) {
+      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+      const float s = dbs * kInvLossScale;
+      if (atomic) atomicAdd(pdb, s); else *pdb = s;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int tile = wave + 4 * i;
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    const int n = n_lo + nt * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k_lo + kt * 16 + 4 * (lane >> 4) + q;
+      if (k < a.K && n < g.N) {
+        float* o = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
+                                : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
+        const float v = acc[i][q] * (g.scale * kInvLossScale);
+        if (atomic) atomicAdd(o, v); else *o = v;
+      }
+    }
+  }
+}
 #endif
 
 
@@ -1212,7 +1306,24 @@ namespace dqn {
 template <class LD, int MC, int KB, int NB>
 DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, int gy, act_t* lds) {
   const int bx = b % gx, r = b / gx, by = r % gy, bz = r / gy;
+#if DQN_ACT_F32
   wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
+#else
+  constexpr bool kPart = MC == 128 && !std::is_same<LD, DenseLoader>::value;
+  if (!kPart || g.part == nullptr) {
+    wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
+    return;
+  }
+  // deterministic: chunk group bx -> its partial slice ([K][N] weights, then [N] bias), as the
+  // member's own dW / db with no split (plain stores)
+  WgradArgs gp = g;
+  const int nch = (a.M + MC - 1) / MC, c0 = bx * g.mloop;
+  gp.dw = g.part + (int64_t)bx * g.pstride;
+  gp.db = gp.dw + (int64_t)a.K * g.N;
+  gp.nsplit = g.N;
+  gp.atomic = 0;
+  if constexpr (kPart) wgrad_block_det<LD, MC, KB, NB>(a, gp, c0, by, bz, lds, min(nch, c0 + g.mloop) - c0);
+#endif
 }
 
 // conv members' M-chunk: 128 rows (kind as is) keeps a block's LDS at <= 40 KB (4 blocks / CU);
@@ -1224,8 +1335,13 @@ constexpr int kGrpMC256 = 0x40;
   case L_NAT_CONV1_FRAMES + OFF: group_member<NatF1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break; \
   case L_NAT_CONV2_FWD + OFF: group_member<NatC2, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
   case L_NAT_CONV3_FWD + OFF: group_member<NatC3, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-__global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup G) {
+__global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup Gv) {
   extern __shared__ __attribute__((aligned(16))) act_t glds[];
+  // members are read straight from the kernel-argument segment (the group is the only, offset-0
+  // argument): indexing the by-value parameter with the runtime member index otherwise lets the
+  // compiler copy all ~2.7 KB of it to scratch once the members' bodies grow
+  (void)Gv;
+  const WgradGroup& G = *(const WgradGroup*)__builtin_amdgcn_kernarg_segment_ptr();
   int b = blockIdx.x, i = 0;
   while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
   switch (G.kind[i]) {
@@ -1269,19 +1385,25 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   for (int i = 0; i < G.n; ++i)
     if (G.kind[i] == L_DENSE_FWD_RELU) dense_blocks += ((G.a[i].K + 63) / 64) * ((G.g[i].N + 127) / 128);
   const bool mc256 = mc_env == 256 || (mc_env == 0 && dense_blocks > 256);
-  for (int i = 0; i < G.n; ++i)
+  for (int i = 0; i < G.n; ++i) {
+    if (G.g[i].part != nullptr) continue;       // (partial members: 128-row chunks, see below)
     if (mc256 && G.kind[i] >= L_NAT_CONV1_FWD && G.kind[i] <= L_NAT_CONV3_FWD) G.kind[i] += kGrpMC256;
     else if (mc256 && G.kind[i] == L_NAT_CONV1_FRAMES) G.kind[i] += kGrpMC256;
+  }
   for (int i = 0; i < G.n; ++i) {
     int MC, KB, NB;
     size_t l;
     if (!wgrad_tiles(G.kind[i], MC, KB, NB, l)) return -1;
     if (l > 160 * 1024) return -2;
     G.gx[i] = (G.a[i].M + MC - 1) / MC;
+    if (G.g[i].part != nullptr) {               // chunk groups of mloop chunks, one partial each
+      if (DQN_ACT_F32 || MC != 128 || G.g[i].mloop < 1 || G.g[i].pstride < G.a[i].K * G.g[i].N + G.g[i].N) return -3;
+      G.gx[i] = (G.gx[i] + G.g[i].mloop - 1) / G.g[i].mloop;
+    }
     G.gy[i] = (G.a[i].K + KB - 1) / KB;
     const int gz = (G.g[i].N + NB - 1) / NB;
     G.nblk[i] = G.gx[i] * G.gy[i] * gz;
-    G.g[i].atomic = G.gx[i] > 1 ? 1 : 0;
+    G.g[i].atomic = G.gx[i] > 1 && G.g[i].part == nullptr ? 1 : 0;
     // timing probe only (wrong gradients): DQN_WGRAD_PROBE_NOATOMIC=1 stores the M-chunk partials
     // plainly, to price the fp32 atomics of the multi-chunk members
     static const bool noatomic = getenv("DQN_WGRAD_PROBE_NOATOMIC") != nullptr;

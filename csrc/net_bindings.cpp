@@ -170,15 +170,23 @@ void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vec
   G.n = (int)members.size();
   for (int i = 0; i < G.n; ++i) {
     const auto& m = members[i];
-    TORCH_CHECK(m.size() == 10, "member = [kind, in, dz, ldz, dw, db, dw2, db2, nsplit, N]");
+    TORCH_CHECK(m.size() == 10 || m.size() == 13,
+                "member = [kind, in, dz, ldz, dw, db, dw2, db2, nsplit, N] (+ [part, pstride, mloop])");
     G.kind[i] = (int)m[0];
     G.a[i] = conv_args({m[1]}, {}, {}, {}, {}, {1.0}, dims[i]);
     dqn::WgradArgs& g = G.g[i];
     g.dz = P<const void*>(m[2]); g.ldz = (int)m[3];
     g.dw = P<float*>(m[4]); g.db = P<float*>(m[5]); g.dw2 = P<float*>(m[6]); g.db2 = P<float*>(m[7]);
     g.nsplit = (int)m[8]; g.N = (int)m[9]; g.scale = (float)scales[i];
+    g.mloop = 1;
+    if (m.size() == 13 && m[10] != 0) {          // deterministic partial member
+      g.part = P<float*>(m[10]); g.pstride = (int)m[11]; g.mloop = (int)m[12];
+      TORCH_CHECK(g.mloop >= 1 && g.mloop <= 64 && g.nsplit == g.N && g.dw2 == nullptr, "partial member args");
+    }
   }
-  TORCH_CHECK(launch_wgrad_group(G, cur_stream()) == 0, "unknown wgrad kind in group");
+  const int rc = launch_wgrad_group(G, cur_stream());
+  TORCH_CHECK(rc != -3, "wgrad group: partial members need 128-row chunks and pstride >= K*N + N");
+  TORCH_CHECK(rc == 0, "unknown wgrad kind in group");
 }
 
 // ptrs (4 per group): slots, states, w1, w2, w3, b1, b2, b3, x3, then a1, p1, a2, p2, a3; M as in trunk

@@ -120,6 +120,12 @@ class Learner:
                 self._ar_ranges = ranges
         if self.ctx.enabled and self._lowrank is None:
             self._defer_fc = False         # (an all-reduced fc gradient must exist in the flat buffer)
+        # conv weight gradients as deterministic chunk-group partials summed inside the fused
+        # optimizer launch (executor.can_det_wgrad): one process only (DP all-reduces the flat
+        # gradient, whose conv range then must hold the sums)
+        self._det_wgrad = bool(not self.ctx.enabled and ps_client is None and int(getattr(config, 'det_wgrad', 1))
+                               and network.fuses_update(tfreq) and hasattr(ex, 'can_det_wgrad')
+                               and ex.can_det_wgrad(B))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:
             use_graph = bool(config.hip_graph) and self.device.type == 'cuda'
@@ -186,9 +192,11 @@ class Learner:
         sg = not (self.ps is None and self.net.fuses_sigma_grads(self._target_freq()))
         if self._split:
             loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True, sigma_grads=sg,
-                                                            lowrank=self._lowrank, defer_fc=self._defer_fc)
+                                                            lowrank=self._lowrank, defer_fc=self._defer_fc,
+                                                            det_wgrad=self._det_wgrad)
         else:
-            loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg, defer_fc=self._defer_fc)
+            loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg, defer_fc=self._defer_fc,
+                                                det_wgrad=self._det_wgrad)
         # keep references (static buffers under graph capture) instead of copies
         self.loss = loss.view(1)
         self.prio = prio.view(-1)
@@ -400,7 +408,8 @@ class Learner:
             gk = torch.cuda.CUDAGraph()
             # host-side state a step body advances (restored if the capture is refused midway)
             ex = self.net.executor
-            saved = (self._presampled, getattr(self.net, '_noise_drawn', False), getattr(ex, '_fc_pending', None))
+            saved = (self._presampled, getattr(self.net, '_noise_drawn', False), getattr(ex, '_fc_pending', None),
+                     getattr(ex, '_parts_pending', None))
             try:
                 with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
                     for _ in range(k):
@@ -412,7 +421,7 @@ class Learner:
                 self._presampled = saved[0]
                 self.net._noise_drawn = saved[1]
                 if hasattr(ex, '_fc_pending'):
-                    ex._fc_pending = saved[2]
+                    ex._fc_pending, ex._parts_pending = saved[2], saved[3]
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 raise
             torch.cuda.current_stream(self.device).wait_stream(s)

@@ -163,15 +163,20 @@ class Network:
 
     # ------------------------------------------------------------- training
     def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False,
-                      sigma_grads: bool = True, lowrank: Optional[dict] = None, defer_fc: bool = False):
+                      sigma_grads: bool = True, lowrank: Optional[dict] = None, defer_fc: bool = False,
+                      det_wgrad: bool = False):
         """Loss + gradient into ``self.grad``. ``split=True`` returns ``(loss, prio, tail)``: when
         ``tail`` is not None only the dense-layer gradients (``dense_range()``) are final and
         ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad). ``defer_fc``:
         the fc weight / bias gradient is left to the next fused ``apply_grads`` (it forms them
-        inside the optimizer launch; ``HipExecutor.can_defer_fc``)."""
+        inside the optimizer launch; ``HipExecutor.can_defer_fc``). ``det_wgrad``: the conv weight
+        gradients stay as deterministic partials the next fused ``apply_grads`` sums
+        (``HipExecutor.can_det_wgrad``)."""
         kw = {}
         if defer_fc:
             kw['defer_fc'] = True
+        if det_wgrad:
+            kw['det_wgrad'] = True
         if self._premixed and not sigma_grads:
             # the fused noisy optimizer follows: it derives dL/dsigma itself, and the next samples
             # are drawn by a launch of this backward (no noise launch of their own)
@@ -241,7 +246,7 @@ class Network:
             return True
         assert next_sample is None or not fuse, 'next_sample needs the fused optimizer+pack launch'
         assert not (hasattr(ex, 'pending_fc') and ex.pending_fc()), \
-            'compute_grads(defer_fc=True) needs the fused optimizer+pack update'
+            'compute_grads(defer_fc / det_wgrad) needs the fused optimizer+pack update'
         if fuse:
             self.optimizer.step(self.online.flat, g, grad_scale, self.global_step,
                                 target=self.target.flat, target_freq=int(target_freq))

@@ -240,7 +240,7 @@ class HipExecutor:
                     items.append([0, src, f.K, f.N, k0, n0, f.dst_off, f.dst_N16, f.nt_off, f.ks_off,
                                   d.mode if d else 0, d.dst_off if d else 0, d.dst_N16 if d else 0,
                                   d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0, so, ei, eo, eff,
-                                  fcc])
+                                  fcc, 0, 0, 0])
         for name in lay.names:
             off, n = lay.offsets[name], lay.numel(name)
             if off in fwd or off in sig:
@@ -252,11 +252,16 @@ class HipExecutor:
             for s0 in range(0, n, 2048):
                 cnt = min(2048, n - s0)
                 items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + self.fs * s0) if c else -1] + [0] * 9
-                             + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy), fcc])
+                             + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy), fcc,
+                                0, 0, 0])
         self.upd_items = items
         self._upd_dev: Dict[torch.device, torch.Tensor] = {}
         # (x ptr, dh ptr, rows) of a step whose fc weight gradient the next update_and_pack forms
         self._fc_pending = None
+        # (job table, partial buffer ptr) of a step whose conv weight gradients the next
+        # update_and_pack sums from the grouped wgrad's deterministic partials
+        self._parts_pending = None
+        self._det: Dict[tuple, dict] = {}
         self._bound: Dict[int, torch.Tensor] = {}   # flat ptr -> noise its packed/eff buffers reflect
         self._dummies: Dict[torch.device, tuple] = {}
 
@@ -292,7 +297,7 @@ class HipExecutor:
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
                             self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [], [],
-                            [], None, None, None, None, [])
+                            [], None, None, None, None, [], 0)
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
@@ -331,7 +336,9 @@ class HipExecutor:
         from those rows instead of reading them from ``grad``). Returns True."""
         from ..optim import kernel_op
         dev = flat.device
-        jobs = self._upd_jobs(dev)
+        jobs, part = self._upd_jobs(dev), 0
+        if self._parts_pending is not None:
+            (jobs, part), self._parts_pending = self._parts_pending, None
         hp = opt.hp
         s0 = opt.slots[0] if len(opt.slots) > 0 else flat
         s1 = opt.slots[1] if len(opt.slots) > 1 else flat
@@ -360,7 +367,7 @@ class HipExecutor:
                              if next_sample is not None and next_sample['kind'] == 'uniform' else []),
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
-                            target_noise, teff, tpk, noise_rng, self._take_fc(fc))
+                            target_noise, teff, tpk, noise_rng, self._take_fc(fc), part)
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:
@@ -382,7 +389,62 @@ class HipExecutor:
                 and B <= 32 and not (self.noisy and sigma_grads))
 
     def pending_fc(self) -> bool:
-        return self._fc_pending is not None
+        return self._fc_pending is not None or self._parts_pending is not None
+
+    def can_det_wgrad(self, B: int) -> bool:
+        """True when ``loss_and_grad(det_wgrad=True)`` leaves the conv weight / bias gradients as
+        deterministic chunk-group partials for the fused optimizer launch to sum (no fp32 atomics;
+        the flagship Nature trunk's grouped-wgrad path)."""
+        return (bool(getattr(self.ext, 'OPTIM_FC_FUSE', 0)) and self.grouped_wgrad and not self.two_stream
+                and B <= 32 and self.arch.network == 'nature')
+
+    def _det_plan(self, B: int, dev) -> dict:
+        """Deterministic conv weight gradients (qnet.hip group_member partial mode): member i's
+        M rows split into 128-row chunks, ``mloop`` consecutive chunks per chunk group summed in
+        registers in a fixed order, each group's [K][N] weights + [N] bias stored plainly into
+        its own partial slice; the optimizer's conv jobs then sum the slices in ascending order.
+        Same result on every run (and every rank) for the same inputs. ``DQN_DET_GROUPS`` caps
+        the partial slices per layer (fewer: fewer bytes summed, longer wgrad blocks)."""
+        key = (B, dev.index if dev.index is not None else 0)
+        pl = self._det.get(key)
+        if pl is not None:
+            return pl
+        lay = self.layout
+        cap = max(1, int(os.environ.get('DQN_DET_GROUPS', '26')))
+        info, base = {}, 0
+        for c in self.arch.convs:
+            h, w = c.conv_hw
+            K, N = c.k * c.k * c.cin, c.cout
+            nch = (B * h * w + 127) // 128
+            mloop = (nch + cap - 1) // cap
+            ng = (nch + mloop - 1) // mloop
+            stride = (K * N + N + 63) // 64 * 64
+            info[c.name] = (base, K, N, ng, stride, mloop)
+            base += ng * stride
+        buf = torch.zeros(base, dtype=torch.float32, device=dev)
+        by_off = {}
+        for name, (b0, K, N, ng, stride, _) in info.items():
+            by_off[lay.offsets[name + '/w']] = (b0, ng, stride)
+            by_off[lay.offsets[name + '/b']] = (b0 + K * N, ng, stride)
+        first, rest = [], []
+        for it in self.upd_items:
+            it = list(it)
+            # tile jobs: src_off is the tensor's; chunk jobs: the chunk's (bias chunks start at 0)
+            hit = by_off.get(it[1])
+            if hit is not None:
+                it[-3:] = list(hit)
+                first.append(it)     # the long-latency summing jobs first in the launch
+            else:
+                rest.append(it)
+        ints = [v for it in first + rest for v in it]
+        pl = {'buf': buf, 'info': info,
+              'jobs': torch.tensor(ints, dtype=torch.int32, device=dev)}
+        self._det[key] = pl
+        return pl
+
+    def _det_member(self, pl, name):
+        b0, _, _, _, stride, mloop = pl['info'][name]
+        return [pl['buf'].data_ptr() + 4 * b0, stride, mloop]
 
     def _plan_noisy(self):
         """Mix jobs (rainbow.hip NoisyJob): every mu tensor -> the effective buffer;
@@ -822,7 +884,7 @@ class HipExecutor:
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
                       split: bool = False, sigma_grads: bool = True, draw_noise=None, lowrank=None,
-                      defer_fc: bool = False):
+                      defer_fc: bool = False, det_wgrad: bool = False):
         """lowrank (data parallelism, see ``lowrank_spec``): {'gather': f(srcs, outs, nbytes) (an
         in-stream all-gather of two byte segments), 'world', 'rank'}. With ``split``, the fc weight
         gradient is then formed from the all-gathered factors right after the head, in stream order
@@ -832,6 +894,11 @@ class HipExecutor:
         defer_fc (``can_defer_fc``): the fc weight and bias gradients are NOT written to grad_out;
         the next ``update_and_pack`` forms them from the fc input rows and dH rows (this rank's, or
         the all-gathered ones under ``lowrank``) inside the optimizer launch.
+
+        det_wgrad (``can_det_wgrad``, one process): the conv weight / bias gradients are NOT
+        written to grad_out either; the grouped wgrad launch stores per-chunk-group partials
+        (``_det_plan``) and the next ``update_and_pack`` sums them in a fixed order: no fp32
+        atomics, no zeroing of the conv range, bit-reproducible.
 
         sigma_grads=False (noisy nets): leave the sigma slots of grad_out alone — the fused
         optimizer derives dL/dsigma from the mu-slot gradient and the noise itself.
@@ -908,7 +975,9 @@ class HipExecutor:
                             M=[B] * ninst + [E], sample=sample)
         if not zero_in_head:
             main.wait_event(ev_zero)
-        zero = [grad_out.data_ptr() + 4 * conv_lo, conv_hi - conv_lo] if zero_in_head else []
+        det = bool(det_wgrad)
+        assert not det or (self.can_det_wgrad(B) and lowrank is None), 'det_wgrad: not available here'
+        zero = [grad_out.data_ptr() + 4 * conv_lo, conv_hi - conv_lo] if zero_in_head and not det else []
         # ---- fused head + TD loss + head backward
         w, b, wv, bv = self._head_ptrs(flats)
         g = lambda n: grad_out.data_ptr() + 4 * lay.offsets[n]
@@ -972,6 +1041,11 @@ class HipExecutor:
             dims = [d1, [B * h3 * w3, c3.cout, K3, 0, 0, h2, w2, h3, w3, 0, 0],
                     [B * h2 * w2, c2.cout, K2, 0, 0, h1, w1, h2, w2, 0, 0], [B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0]] + hdims
             scales = [self.input_scale] + [1.0] * (len(members) - 1)
+            if det:
+                pl = self._det_plan(B, dev)
+                for m, c in zip(members[:3], (c1, c3, c2)):
+                    m += self._det_member(pl, c.name)
+                self._parts_pending = (pl['jobs'], pl['buf'].data_ptr())
             noisy = self.noisy and gnoise is not None
             defer = bool(defer_fc) and self.can_defer_fc(B, gnoise is not None)
             assert defer or not defer_fc, 'defer_fc: not available for this executor / batch'

@@ -8,7 +8,10 @@ production head kernels' loss / dL/dQ against a loss computed purely in torch.
 * the same against the pure-torch fp32 oracle gradient of the fc layer;
 * head_loss_kernel / c51_train_kernel: loss, dL/dQ (dL/dlogits) and dH of the kernel vs torch
   autograd of ``models/losses.py`` on the very hidden rows the kernel consumed (fp32 output
-  layer in torch; the kernel's output layer runs on bf16 MFMA fragments).
+  layer in torch; the kernel's output layer runs on bf16 MFMA fragments);
+* deterministic conv weight gradients (``--det_wgrad``: chunk-group partials summed by the
+  optimizer launch in a fixed order): two identical runs are bit-identical, the result matches
+  the fp32-atomics path to summation order and the fp32 oracle's conv gradients.
 
 Reference: the optimizer site `/root/reference/src/network.py:198-202` (``minimize``) and the
 loss `/root/reference/src/network.py:141-157`.
@@ -210,3 +213,57 @@ def test_head_kernels_match_pure_torch_loss(extra):
     assert rel(dq, dout_ref) < 2e-2, rel(dq, dout_ref)
     dh = ws['dh'][:B * ex.HH].view(B, ex.HH).float()
     assert rel(dh, dh_ref) < 3e-2, rel(dh, dh_ref)
+
+
+@pytest.mark.parametrize('extra', ['', RAINBOW])
+def test_det_wgrad_bitwise_reproducible(extra):
+    """Same seed, same minibatches: with the deterministic conv weight gradients every parameter
+    and slot is bit-identical after several steps (the atomics path differs run to run in the
+    last bits); against the atomics path the first step agrees to summation order."""
+    states = []
+    for det in (1, 1, 0):
+        net, learner = _learner(extra + ' --det_wgrad=%d' % det, True)
+        assert learner._det_wgrad == bool(det)
+        learner.step()
+        torch.cuda.synchronize()
+        assert not net.executor.pending_fc()
+        one = _state(net)
+        for _ in range(3):
+            learner.step()
+        torch.cuda.synchronize()
+        states.append((one, _state(net)))
+    (a1, a4), (b1, b4), (c1, _) = states
+    for key in a4:
+        assert torch.equal(a1[key], b1[key]) and torch.equal(a4[key], b4[key]), key
+        torch.testing.assert_close(a1[key], c1[key], rtol=1e-5, atol=1e-9, msg=key)
+
+
+def test_det_wgrad_conv_update_matches_fp32_oracle():
+    """One SGD step's conv weight / bias updates from the partial sums vs the PyTorch fp32
+    oracle's gradient on the same minibatch."""
+    from dist_dqn_amd.models.executor import TorchExecutor
+    net, learner = _learner('--optimizer=sgd --lr=0.5 --fuse_sampling=0 --det_wgrad=1', True)
+    assert learner._det_wgrad
+    cfg = net.config
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+                           huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
+    w0 = net.online.flat.clone()
+    tgt = net.target.flat.clone()
+    learner.step()
+    torch.cuda.synchronize()
+    batch = learner.replay.gather(learner.idx)
+    g_ref = torch.zeros_like(w0)
+    oracle.loss_and_grad(w0, tgt, batch, g_ref, None, None)
+    lay = net.layout
+    seen = 0
+    for n in lay.names:
+        if not n.startswith('conv'):
+            continue
+        o, k = lay.offsets[n], lay.numel(n)
+        g = (w0[o:o + k] - net.online.flat[o:o + k]) / 0.5
+        ref = g_ref[o:o + k]
+        cos = float(torch.nn.functional.cosine_similarity(g, ref, dim=0))
+        ratio = float(g.norm() / (ref.norm() + 1e-12))
+        assert cos > 0.98 and abs(ratio - 1.0) < 0.05, (n, cos, ratio)
+        seen += 1
+    assert seen == 6
