@@ -123,7 +123,7 @@ class Learner:
         # conv weight gradients as deterministic chunk-group partials summed inside the fused
         # optimizer launch (executor.can_det_wgrad): one process only (DP all-reduces the flat
         # gradient, whose conv range then must hold the sums)
-        self._det_wgrad = bool(not self.ctx.enabled and ps_client is None and int(getattr(config, 'det_wgrad', 1))
+        self._det_wgrad = bool(not self.ctx.enabled and ps_client is None and int(getattr(config, 'det_wgrad', 0))
                                and network.fuses_update(tfreq) and hasattr(ex, 'can_det_wgrad')
                                and ex.can_det_wgrad(B))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
