@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <sched.h>
 
 #include <algorithm>

@@ -482,6 +482,11 @@ struct WgradTile {
   static constexpr size_t lds_bytes = (size_t)MC * (SA + SZ) * sizeof(act_t);
 };
 // (operands through lds_tr16 / join_tr transposed reads: common.h)
+// Staging swizzle: the 16-byte slots of rows 4..7 mod 8 are swapped in pairs (element offset ^ 8).
+// The ds_write_b128 of 8 consecutive rows (8-lane groups, banks mod 32) then hits distinct banks
+// (row strides of 24 / 40 / 72 dwords otherwise put rows r and r + 4 on the same banks), and a
+// transposed read still covers the same 32-byte half-row: its banks are unchanged.
+DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
 #endif
 
 // Body shared by the per-layer launch and the grouped launch (one block = one
@@ -605,9 +610,9 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
 #pragma unroll
-    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (p + i * TPR) * 8) = va[i];
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (((p + i * TPR) * 8) ^ wsw(r))) = va[i];
 #pragma unroll
-    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[i];
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[i];
   }
   __syncthreads();
   const bool atomic = g.atomic != 0;
@@ -615,7 +620,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     for (int n = threadIdx.x; n < NB; n += 256) {
       float s = 0.f;
 #pragma unroll 8
-      for (int r = 0; r < MC; ++r) s += (float)Zt[r * SZ + n];
+      for (int r = 0; r < MC; ++r) s += (float)Zt[r * SZ + (n ^ wsw(r))];
       const int nn = n_lo + n;
       if (nn < g.N) {
         float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
@@ -634,8 +639,8 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
     const int tile = wave + 4 * i;
     const int kt = tile / NTt, nt = tile - kt * NTt;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
-    const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
+    const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + (cp ^ wsw(4 * gq));
+    const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + (cp ^ wsw(4 * gq));
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
       const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
@@ -701,20 +706,20 @@ DQN_DEV void wgrad_block_det(const ConvArgs& a, const WgradArgs& g, int bx, int 
     }
     if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (p + i * TPR) * 8) = va[i];
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (((p + i * TPR) * 8) ^ wsw(r))) = va[i];
 #pragma unroll
-    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[i];
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[i];
     __syncthreads();
     if (dob && (int)threadIdx.x < NB) {
 #pragma unroll 8
-      for (int q = 0; q < MC; ++q) dbs += (float)Zt[q * SZ + threadIdx.x];
+      for (int q = 0; q < MC; ++q) dbs += (float)Zt[q * SZ + ((int)threadIdx.x ^ wsw(q))];
     }
 #pragma unroll
     for (int i = 0; i < PERW; ++i) {
       const int tile = wave + 4 * i;
       const int kt = tile / NTt, nt = tile - kt * NTt;
-      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
-      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
+      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + (cp ^ wsw(4 * gq));
+      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + (cp ^ wsw(4 * gq));
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
         const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
@@ -825,9 +830,9 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
 #else
     // one ds_write_b128 per fragment; the MFMA operands come back through transposed reads
 #pragma unroll
-    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (p + i * TPR) * 8) = va[u][i];
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (((p + i * TPR) * 8) ^ wsw(r))) = va[u][i];
 #pragma unroll
-    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (p + i * TPR) * 8) = vz[u][i];
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[u][i];
 #endif
     __syncthreads();
 #if DQN_ACT_F32
@@ -850,7 +855,7 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
 #else
     if (g.db != nullptr && by == 0) {           // column tid % NB, rows tid / NB + k * (256 / NB)
 #pragma unroll 4
-      for (int q = (int)threadIdx.x / NB; q < MC; q += 256 / NB) dbs += (float)Zt[q * SZ + (int)threadIdx.x % NB];
+      for (int q = (int)threadIdx.x / NB; q < MC; q += 256 / NB) dbs += (float)Zt[q * SZ + (((int)threadIdx.x % NB) ^ wsw(q))];
     }
     // (the same reduction-index permutation on both operands as wgrad_block's 16-bit body)
     const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
@@ -858,8 +863,8 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
     for (int i = 0; i < PERW; ++i) {
       const int tile = wave + 4 * i;
       const int kt = tile / NTt, nt = tile - kt * NTt;
-      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + cp;
-      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + cp;
+      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + (cp ^ wsw(4 * gq));
+      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + (cp ^ wsw(4 * gq));
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
         const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
@@ -1335,7 +1340,8 @@ constexpr int kGrpMC256 = 0x40;
   case L_NAT_CONV1_FRAMES + OFF: group_member<NatF1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break; \
   case L_NAT_CONV2_FWD + OFF: group_member<NatC2, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
   case L_NAT_CONV3_FWD + OFF: group_member<NatC3, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
-__global__ void __launch_bounds__(256) wgrad_group_kernel(WgradGroup Gv) {
+// (<= 128 VGPRs: 4 waves / SIMD, the 4 blocks / CU the conv members' LDS allows)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) wgrad_group_kernel(WgradGroup Gv) {
   extern __shared__ __attribute__((aligned(16))) act_t glds[];
   // members are read straight from the kernel-argument segment (the group is the only, offset-0
   // argument): indexing the by-value parameter with the runtime member index otherwise lets the

@@ -15,11 +15,14 @@
 //            lane) -> LDS act2 [81][72]
 //   stage 3  conv3: 49 x 64 x 576, A from act2 -> global x3 (the fc input)
 // x1 / x2 are also written to global (the backward's ReLU masks / wgrad inputs).
-// Everything is v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+// Everything is v_mfma_f32_16x16x32_bf16 with fp32 accumulation. The conv2 / conv3 m-tiles take
+// their pixels in the order of trunk_perm.h (scripts/gen_trunk_perm.py), chosen so the im2col
+// ds_read_b128 of a tile hits distinct LDS banks (row-major tiles: 1.8x / 2.5x the read cycles).
 #include <stdlib.h>
 #include "common.h"
 #include "fused_util.h"
 #include "sample_dev.h"
+#include "trunk_perm.h"
 #include "../include/dqn_nets_k.h"
 
 namespace dqn {
@@ -141,6 +144,13 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   //   conv3 - wave owns n-tile (wave & 3) and k-half (wave >> 2); loaded after conv1
   //           into the registers conv1 no longer needs.
   const int nq = wave & 3, hi = wave >> 2;
+  // this lane's tile-row pixels of conv2 / conv3 (-1: padding row), loaded with the inputs
+  const int pv = split > 1 ? 1 + part : 0;
+  int p2r[(R2 + 15) / 16], p3r[(R3 + 15) / 16];
+#pragma unroll
+  for (int mt = 0; mt < (R2 + 15) / 16; ++mt) p2r[mt] = kTrunkP2[pv][mt * 16 + row];
+#pragma unroll
+  for (int mt = 0; mt < (R3 + 15) / 16; ++mt) p3r[mt] = kTrunkP3[pv][mt * 16 + row];
   bfx8 w1r[2][K1 / 32], w2r[K2 / 64];
   const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
   bfx8 w1s[2];
@@ -245,8 +255,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     const int np2 = c2n * O2, MT = (np2 + 15) / 16;
     float* red2 = red;                                    // xin is dead: k-half partials after act2
     auto load2 = [&](bfx8* f, int mt) {
-      const int p = mt * 16 + row;
-      const bool ok = p < np2;
+      const int p = p2r[mt];
+      const bool ok = p >= 0;
       const int oy = ok ? p / O2 : 0, ox = ok ? p - oy * O2 : 0;
       const act_t* base = act1 + ((oy * 2) * O1 + ox * 2) * L1 + kg;
 #pragma unroll
@@ -280,8 +290,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int mt = 0; mt < MTX; ++mt) {
         if (mt >= MT) break;
         const f32x4 c = unpark(red2, nq * MTX + mt, lane, acc2[mt]);
-        const int p = mt * 16 + row;
-        if (p < np2) {
+        const int p = p2r[mt];
+        if (p >= 0) {
           const pk4_t v = pack4(c + f4(bias2));
           *reinterpret_cast<pk4_t*>(act2 + p * L2 + nq * 16 + cq) = v;
           const int oy = p / O2;
@@ -298,8 +308,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     constexpr int KJ = K3 / 64;                           // 9 k-steps per k-half
     const int np3 = c3n * O3, mtn = (np3 + 15) / 16;
     auto load3 = [&](bfx8* f, int mt) {
-      const int p = mt * 16 + row;
-      const bool ok = p < np3;
+      const int p = p3r[mt];
+      const bool ok = p >= 0;
       const int oy = ok ? p / O3 : 0, ox = ok ? p - oy * O3 : 0;
       const act_t* base = act2 + (oy * O2 + ox) * L2 + kg;
 #pragma unroll
@@ -336,8 +346,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int mt = 0; mt < MT; ++mt) {
         if (mt >= mtn) break;
         const f32x4 v = unpark(red, nq * MT + mt, lane, acc[mt]);
-        const int p = mt * 16 + row;
-        if (p < np3) *reinterpret_cast<pk4_t*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
+        const int p = p3r[mt];
+        if (p >= 0) *reinterpret_cast<pk4_t*>(x3 + p * N3 + nq * 16 + cq) = pack4(v + f4(bias3));
       }
     }
   }

@@ -534,26 +534,33 @@ class ApexTrainer:
     # ----------------------------------------------------------- native ingest
     def _plan_cpus(self):
         """Reserve one CPU each for the learner thread, the ingest thread and the inference
-        thread out of this process's allowed set (when it leaves the actors at least 4); the
-        actor processes are restricted to the rest."""
+        thread out of this process's CPU budget (the allowed set capped by the container's CFS
+        quota, utils/cpus.py; when it leaves the actors at least 4); the actor processes are
+        restricted to the rest, so together they never outrun the quota."""
+        from ..utils.cpus import cfs_quota_cpus, usable_cpus
         try:
-            cpus = sorted(os.sched_getaffinity(0))
+            allowed = sorted(os.sched_getaffinity(0))
         except AttributeError:
             return
+        cpus = usable_cpus()
         r = self.reserve_cpus
         if r <= 0 or len(cpus) < r + 4:
+            if len(cpus) < len(allowed):      # no reservation, but stay within the quota
+                self.pool.set_actor_cpus(cpus)
+                log.info('Ape-X: %d actors on %d CPUs (CFS quota %s)', self.pool.n, len(cpus), cfs_quota_cpus())
             return
         res = cpus[:r] + [cpus[r - 1]] * (3 - r) if r < 3 else cpus[:3]
         self._cpus = (res[0], res[1], res[2])
         self.pool.set_actor_cpus(cpus[r:])
         try:
             os.sched_setaffinity(0, {self._cpus[0]})      # this (learner) thread; restored by run()
-            self._cpus_prev = cpus
+            self._cpus_prev = allowed
         except OSError:
             self._cpus = None
             return
-        log.info('Ape-X CPUs: learner %d, ingest %d, inference %d; %d actors on %d CPUs', self._cpus[0],
-                 self._cpus[1], self._cpus[2], self.pool.n, len(cpus) - r)
+        log.info('Ape-X CPUs: learner %d, ingest %d, inference %d; %d actors on %d CPUs (%d visible, CFS quota %s)',
+                 self._cpus[0], self._cpus[1], self._cpus[2], self.pool.n, len(cpus) - r, len(allowed),
+                 cfs_quota_cpus())
 
     def _start_native_ingest(self) -> bool:
         """Ring ingest + H2D shipping on a C++ thread (csrc/ingest_server.cpp): the replay's

@@ -31,6 +31,7 @@ def main():
     from dist_dqn_amd.learner import Learner
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.replay import DeviceReplay
+    from dist_dqn_amd.utils.cpus import cfs_quota_cpus
     dev = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
     cfg = preset('apex', 'Pong-v0', '--num_actors=%d --replay_memory_capacity=%d --replay_start_size=2000 '
                  '--logdir=%s %s' % (args.actors, args.capacity, tempfile.mkdtemp(), args.extra))
@@ -56,6 +57,7 @@ def main():
         'learner_env_frames_per_sec': round((pool.frames - tr.learn_frames0) / lw, 1) if lw > 0 else None,
         'greedy_actions_served': pool.served, 'serve_calls': tr.serve_calls,
         'mean_serve_batch': round(pool.served / max(1, tr.serve_calls), 2), 'executor': net.executor.name,
+        'cpus_visible': len(os.sched_getaffinity(0)), 'cfs_quota_cpus': cfs_quota_cpus(),
         'main_loop_s': {k: round(v, 2) for k, v in tr.loop_time.items()},
         'config': 'apex preset: double+dueling, PER, n_step=3, nature-cnn', 'dtype': net.executor.compute_dtype,
         'device': str(dev)}))
