@@ -61,7 +61,7 @@ def _worker_xgmi(rank, world, port, wire, errq):
         ctx = init_distributed(None, device='cuda')
         cap = 1 << 20
         x = XgmiAllReduce(ctx, cap, wire)
-        assert x.self_test(cap)
+        assert x.self_test(cap), x.self_test_log
         g = torch.Generator(device='cuda').manual_seed(1234)
         for n in (8 * world, 4096 + 8 * world, cap):
             for call in range(3):                          # both staging parities, then again
