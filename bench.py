@@ -209,6 +209,11 @@ def main():
                        'sampling': learner._sample_mode()},
         }
         print(json.dumps(out), flush=True)
+        if os.environ.get('DQN_OPT_PROF'):            # optimizer phase stamps of the last launch
+            t = net.executor.ext.optim_prof()
+            print('optim_pack stamps (cycles from block start): block0 %s | block1 %s'
+                  % ([t[i] - t[0] for i in range(1, 5)], [t[8 + i] - t[8] if t[8 + i] else 0 for i in range(1, 8)]),
+                  file=sys.stderr, flush=True)
     if ctx.enabled:
         dist.destroy_process_group()
     if not replicas_equal or not xgmi_ok:

@@ -170,7 +170,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, DQN_ACT_F32 ? torch::kFloat32 : DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
   TORCH_CHECK(grad.numel() == w.numel() && hp.size() == 9, "optim_pack args");
   TORCH_CHECK(jobs.numel() % upd_job_ints() == 0, "optim_pack: job table size");
-  TORCH_CHECK(max_grid <= 256 || ticket.numel() >= 17 * 32, "optim_pack: wide grid needs the 17x32-word ticket");
+  TORCH_CHECK(ticket.numel() >= 17 * 32, "optim_pack: the end-of-launch arrival counters need the 17x32-word ticket");
   TORCH_CHECK(max_grid >= 1 && max_grid <= 65535, "optim_pack: max_grid");
   TORCH_CHECK(op >= -1 && op <= 7, "optim_pack: op (7 = rmsprop without momentum)");
   float* tgt = nullptr;
@@ -724,6 +724,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_pack", &optim_pack);
   m.def("noise_normal", &noise_normal);
   m.attr("UPD_JOB_INTS") = upd_job_ints();
+  m.def("optim_prof", []() {
+    std::vector<int64_t> v(16, 0);
+    optim_prof_read(v.data());
+    return v;
+  }, "optim_pack s_memtime phase stamps of blocks 0 and 1 (DQN_OPT_PROF=1 launches)");
   m.attr("OPTIM_FC_FUSE") = optim_fc_fuse();
   m.def("td_loss_scalar", &td_loss_scalar);
   m.def("td_loss_c51", &td_loss_c51);

@@ -64,6 +64,7 @@ int optim_fc_fuse();
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
 void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();
+void optim_prof_read(int64_t* out16);   // optim_pack phase stamps (DQN_OPT_PROF=1)
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
                           float* dst2, const float* src2, int n2, hipStream_t st);
 void launch_step_bump(int64_t* step, hipStream_t st);

@@ -24,7 +24,11 @@ struct OptHP {
   float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
   int reg_end;
   int nt;            // probe: 1 = fp32 weight / slot stores non-temporal (DQN_OPT_NT)
+  int prof;          // probe: 1 = s_memtime phase stamps of blocks 0 and 1 into g_opt_prof (DQN_OPT_PROF)
 };
+
+// optim_pack phase stamps (scripts/probe_optim.py --prof): [0..7] block 0, [8..15] block 1
+__device__ int64_t g_opt_prof[16];
 
 // Contraction is pinned off in the update math so every kernel that inlines it
 // (optim_kernel's float4 loop, optim_pack_kernel's tiles) rounds identically:
@@ -156,6 +160,9 @@ constexpr int kPackThreads = 512;
 // hot path skips its 4 bytes / parameter and the checkpoint manager raises the flag for the
 // step before a save (optim.py Optimizer.request_slots).
 constexpr int kSlotFlag = 1;
+// ticket[kErrFlag] != 0: an optim_pack launch's end-of-launch wait gave up (lost arrival; never
+// expected -- the learner's periodic check reads it)
+constexpr int kErrFlag = 2;
 
 #if !DQN_ACT_F32
 // Fused fc weight gradient (FcFuse): a 32 (k) x 64 (n) update tile's dW = X^T dH over M rows,
@@ -249,6 +256,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
   constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
+  int64_t* prof = (h.prof && t == 0 && blockIdx.x < 2) ? g_opt_prof + 8 * blockIdx.x : nullptr;
+#define OPT_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
+  OPT_MARK(0);
   if (PEROK && sampler && per.sum != nullptr) {
     // prioritized: this step's priorities into the tree (one wave), then the next step's
     // stratified sample from the updated tree (beta of the NEXT global_step)
@@ -278,6 +288,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     if (threadIdx.x == 0) smp.rng[1] = (int64_t)(ctr + 1);   // every lane read it before the barriers
   }
+  OPT_MARK(1);
 #if !DQN_ACT_F32
   __shared__ __attribute__((aligned(16))) unsigned char fcl[FC ? kFcLds : 16];
   // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
@@ -441,7 +452,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       // above are in flight (its X / dH rows are L2-resident)
       if constexpr (FC) {
         if (fcj) {
+          OPT_MARK(5);
           if (elem) fc_bias_grad(jb, g); else fc_tile_grad(jb, g);
+          OPT_MARK(6);
         }
       }
 #endif
@@ -568,6 +581,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = f;
       }
     };
+    OPT_MARK(7);
     emit(e, packed, psync ? tgt_packed : nullptr, true);
     if (tmix) emit(te, tpk, nullptr, false);              // (the target runs forward only)
   };
@@ -595,43 +609,51 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   } else {
     for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) run(ji);
   }
+  OPT_MARK(2);
   if (!UPD) return;
-  __shared__ int s_last;
+  // ---- end-of-launch bookkeeping (global_step, Adam beta powers, noise counter / copy) once
+  //      every block has consumed the old values. Block 0 (the sampler block, or the first work
+  //      block) does it: every other block makes ONE no-return arrival add on one of 16 counters
+  //      (blockIdx & 15, own 128-byte lines) and exits at once -- no returned atomic keeps its CU
+  //      slot (measured: a returning ticket per block cost Rainbow's 1714-block launch ~5 us) --
+  //      while lanes 0..15 of block 0 poll the counters. Nothing waits on block 0, so the wait
+  //      always ends (bounded anyway: a lost arrival flags ticket[kErrFlag] instead of hanging).
+  int32_t* cnt = ticket + kTicketStride;
+  if (blockIdx.x != 0) {
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(cnt + kTicketStride * (blockIdx.x & (kTicketSubs - 1)), 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (threadIdx.x < kTicketSubs) {
+    const int j = threadIdx.x;
+    const int want = ((int)gridDim.x - j + kTicketSubs - 1) / kTicketSubs - (j == 0 ? 1 : 0);
+    int32_t* c = cnt + kTicketStride * j;
+    int spins = 0;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins > (1 << 22)) {                          // >> any launch: flag, do not hang
+        ticket[kErrFlag] = 1;
+        break;
+      }
+    }
+    __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  OPT_MARK(3);
   if (threadIdx.x == 0) {
-    bool last;
-    if (hier) {
-      // two-level arrival ticket (one block per job: ~1k arrivals): blocks count into one
-      // of 16 sub-tickets on their own 128-byte lines; each sub-ticket's last arriver
-      // counts into the top ticket, whose last arriver is the grid's last block
-      const int j = blockIdx.x & (kTicketSubs - 1);
-      const int members = ((int)gridDim.x - j + kTicketSubs - 1) / kTicketSubs;
-      int32_t* sub = ticket + kTicketStride * (1 + j);
-      last = false;
-      if (__hip_atomic_fetch_add(sub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
-        __hip_atomic_store(sub, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int nsub = (int)gridDim.x < kTicketSubs ? (int)gridDim.x : kTicketSubs;
-        last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1;
-      }
-    } else {
-      last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    if (step) step[0] += 1;
+    if constexpr (OP == 3) {
+      beta_pow[0] *= h.b1;
+      beta_pow[1] *= h.b2;
     }
-    if (last) {
-      if (step) step[0] += 1;
-      if constexpr (OP == 3) {
-        beta_pow[0] *= h.b1;
-        beta_pow[1] *= h.b2;
-      }
-      if (noise_rng != nullptr) noise_rng[1] += 1;      // (the drawing launch completed before this one)
-      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_last = last ? 1 : 0;
+    if (noise_rng != nullptr) noise_rng[1] += 1;        // (the drawing launch completed before this one)
   }
-  if (noise_dst != nullptr) {
-    // every other block consumed gnoise before its ticket add: the last block may overwrite it
-    __syncthreads();
-    if (s_last)
-      for (int i = threadIdx.x; i < noise_n; i += blockDim.x) noise_dst[i] = noise[i];
-  }
+  // every other block consumed gnoise before its arrival add: block 0 may overwrite it now
+  if (noise_dst != nullptr)
+    for (int i = threadIdx.x; i < noise_n; i += blockDim.x) noise_dst[i] = noise[i];
+  OPT_MARK(4);
+#undef OPT_MARK
 }
 
 // target <- tau * online + (1 - tau) * target, optionally only when step % freq == 0.
@@ -712,6 +734,8 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
   static const int nt_env = getenv("DQN_OPT_NT") ? atoi(getenv("DQN_OPT_NT")) : 0;
   h.nt = nt_env;
+  static const int prof_env = getenv("DQN_OPT_PROF") ? atoi(getenv("DQN_OPT_PROF")) : 0;
+  h.prof = prof_env;
   // max_grid <= 256: grid-stride over the jobs with a flat ticket (<= 256 arrivals);
   // larger: one block per job (up to max_grid) with the two-level ticket
   const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};
@@ -753,6 +777,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
 }
 
 int upd_job_ints() { return (int)(sizeof(UpdJob) / sizeof(int)); }
+void optim_prof_read(int64_t* out16) { (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_opt_prof), 16 * sizeof(int64_t)); }
 int optim_fc_fuse() { return DQN_ACT_F32 ? 0 : 1; }
 
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,

@@ -1315,6 +1315,17 @@ DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, 
   wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
 #else
   constexpr bool kPart = MC == 128 && !std::is_same<LD, DenseLoader>::value;
+  constexpr bool kMulti = kPart;
+  if constexpr (kMulti) {
+    if (g.part == nullptr && g.mloop > 1) {
+      // chunk group bx: mloop consecutive M-chunks summed in registers, ONE set of fp32 atomics
+      // per group (the atomic bytes of the member / mloop: they run at the memory side, ~1.3 TB/s
+      // chip-wide, the grouped launch's floor with one set per chunk)
+      const int nch = (a.M + MC - 1) / MC, c0 = bx * g.mloop;
+      wgrad_block_det<LD, MC, KB, NB>(a, g, c0, by, bz, lds, min(nch, c0 + g.mloop) - c0);
+      return;
+    }
+  }
   if (!kPart || g.part == nullptr) {
     wgrad_block<LD, MC, KB, NB>(a, g, bx, by, bz, lds);
     return;
@@ -1335,6 +1346,8 @@ DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, 
 // 256 rows (kind | kGrpMC256: 80 KB, 2 blocks / CU, half the blocks and atomic partials) is the
 // launcher's other choice (DQN_WGRAD_MC=128|256, default chosen per group size)
 constexpr int kGrpMC256 = 0x40;
+// default M-chunks per block of the conv members with atomics (conv1, conv2, conv3)
+constexpr int kWgradMloop[3] = {1, 1, 1};
 #define GRP_CONV_CASES(OFF, MC)                                                                                    \
   case L_NAT_CONV1_FWD + OFF: group_member<NatC1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
   case L_NAT_CONV1_FRAMES + OFF: group_member<NatF1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break; \
@@ -1396,6 +1409,14 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
     if (mc256 && G.kind[i] >= L_NAT_CONV1_FWD && G.kind[i] <= L_NAT_CONV3_FWD) G.kind[i] += kGrpMC256;
     else if (mc256 && G.kind[i] == L_NAT_CONV1_FRAMES) G.kind[i] += kGrpMC256;
   }
+  // conv members' M-chunks per block with atomics (DQN_WGRAD_MLOOP="conv1,conv2,conv3", default
+  // kWgradMloop): one set of fp32 atomics per chunk group instead of per chunk
+  static int mlo[3] = {-1, -1, -1};
+  if (mlo[0] < 0) {
+    mlo[0] = kWgradMloop[0]; mlo[1] = kWgradMloop[1]; mlo[2] = kWgradMloop[2];
+    if (const char* e = getenv("DQN_WGRAD_MLOOP")) sscanf(e, "%d,%d,%d", &mlo[0], &mlo[1], &mlo[2]);
+    for (int q = 0; q < 3; ++q) mlo[q] = mlo[q] < 1 ? 1 : (mlo[q] > 64 ? 64 : mlo[q]);
+  }
   for (int i = 0; i < G.n; ++i) {
     int MC, KB, NB;
     size_t l;
@@ -1405,6 +1426,15 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
     if (G.g[i].part != nullptr) {               // chunk groups of mloop chunks, one partial each
       if (DQN_ACT_F32 || MC != 128 || G.g[i].mloop < 1 || G.g[i].pstride < G.a[i].K * G.g[i].N + G.g[i].N) return -3;
       G.gx[i] = (G.gx[i] + G.g[i].mloop - 1) / G.g[i].mloop;
+    } else if (!DQN_ACT_F32) {
+      const int kb = G.kind[i] & ~kGrpMC256;
+      const int li = (kb == L_NAT_CONV1_FWD || kb == L_NAT_CONV1_FRAMES) ? 0 : kb == L_NAT_CONV2_FWD ? 1
+                     : kb == L_NAT_CONV3_FWD ? 2 : -1;
+      G.g[i].mloop = 1;
+      if (li >= 0 && mlo[li] > 1 && (G.kind[i] & kGrpMC256) == 0) {     // (128-row members only)
+        G.g[i].mloop = mlo[li];
+        G.gx[i] = (G.gx[i] + mlo[li] - 1) / mlo[li];
+      }
     }
     G.gy[i] = (G.a[i].K + KB - 1) / KB;
     const int gz = (G.g[i].N + NB - 1) / NB;

@@ -40,6 +40,8 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
+from ..utils.capture import quiet_capture
+
 log = logging.getLogger(__name__)
 
 # transition record: 16-byte header + observation payload
@@ -456,7 +458,7 @@ class ApexTrainer:
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(self._istream)
-            with torch.cuda.stream(s), torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+            with quiet_capture(), torch.cuda.stream(s), torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
                 self._gout[:m].copy_(self._act_on(x))
             self._istream.wait_stream(s)
             self._graphs[m] = g

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import torch
 
+from ..utils.capture import quiet_capture
 from ..ops import _ext
 from ..replay.device import DeviceReplay
 from ..utils.trace import trace
@@ -119,7 +120,7 @@ class DeviceActor:
             s.wait_stream(torch.cuda.current_stream(self.dev))
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with quiet_capture(), torch.cuda.graph(g, stream=s):
                     self._body()
             torch.cuda.current_stream(self.dev).wait_stream(s)
             self._graph = g

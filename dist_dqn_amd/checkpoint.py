@@ -24,6 +24,7 @@ import json
 import os
 import re
 import threading
+import weakref
 import time
 from typing import Dict, Optional
 
@@ -94,6 +95,17 @@ def load_sidecar(path: str) -> Optional[dict]:
     return None
 
 
+_MANAGERS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def quiesce_writers():
+    """Join every live manager's asynchronous checkpoint writer (``Learner`` before a HIP graph
+    capture: the writer's D2H copies, event waits and snapshot frees must not interleave with a
+    capture on the training thread)."""
+    for m in list(_MANAGERS):
+        m.join_writer()
+
+
 class CheckpointManager:
     """Chief-only periodic saver (TF Supervisor's ``save_model_secs`` = 600 by default).
 
@@ -118,6 +130,7 @@ class CheckpointManager:
         self._lock = threading.Lock()
         self._armed = False
         self._writer: Optional[threading.Thread] = None
+        _MANAGERS.add(self)
         self._write_error: Optional[BaseException] = None
         self.last_path: Optional[str] = None
 
@@ -177,6 +190,14 @@ class CheckpointManager:
             self._writer = threading.Thread(target=write, name='ckpt-writer', daemon=True)
             self._writer.start()
             return None                  # (the path is known once the writer has the step: wait())
+
+    def join_writer(self):
+        """Join the writer thread of the last asynchronous save, keeping its error (if any) for the
+        next ``wait()``: afterwards no host thread of this manager touches the GPU or frees a
+        snapshot buffer (the learner calls this before a graph capture)."""
+        w = self._writer
+        if w is not None:
+            w.join()
 
     def wait(self) -> Optional[str]:
         """Join the writer thread of the last asynchronous save (re-raising its error)."""

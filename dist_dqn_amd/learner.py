@@ -28,6 +28,7 @@ from .models.network import Network
 from .ops import kernels
 from .parallel.dist import DistContext
 from .parallel.dp import GradAllReducer
+from .utils.capture import quiet_capture
 from .utils.trace import trace
 
 log = logging.getLogger(__name__)
@@ -345,6 +346,10 @@ class Learner:
 
     # ------------------------------------------------------------ graph
     def _capture(self):
+        with quiet_capture():
+            self._capture_graphs()
+
+    def _capture_graphs(self):
         # (thread-local capture mode: other host threads of the process -- Ape-X inference, the
         # async-PS client -- keep launching and synchronising their own streams meanwhile)
         s = torch.cuda.Stream(device=self.device)
@@ -411,7 +416,8 @@ class Learner:
             saved = (self._presampled, getattr(self.net, '_noise_drawn', False), getattr(ex, '_fc_pending', None),
                      getattr(ex, '_parts_pending', None))
             try:
-                with torch.cuda.stream(s), torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
+                with quiet_capture(), torch.cuda.stream(s), \
+                        torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
                     for _ in range(k):
                         self._sample_and_grad()
                         if self.ctx.enabled:
@@ -428,9 +434,8 @@ class Learner:
             self._graph_many = g = (k, gk)
         with trace('learner.step_many'):
             g[1].replay()
-        if self.reducer.xgmi is not None and (self.train_steps + k) // self._xgmi_check_every \
-                != self.train_steps // self._xgmi_check_every:
-            self.reducer.check()
+        if (self.train_steps + k) // self._xgmi_check_every != self.train_steps // self._xgmi_check_every:
+            self._device_checks()
         self.train_steps += k
         return self.loss
 
@@ -463,12 +468,21 @@ class Learner:
         if self._own_target:
             self._broadcast_owned_target()
         self.train_steps += 1
-        if self.reducer.xgmi is not None and self.train_steps % self._xgmi_check_every == 0:
-            # the in-graph xgmi kernel reports a timed-out peer wait through an error word (its
-            # gradient is then only partly reduced): read it off the hot path, fail loudly so the
-            # supervisor stops the run and the chief keeps its last consistent checkpoint
-            self.reducer.check()
+        if self.train_steps % self._xgmi_check_every == 0:
+            self._device_checks()
         return self.loss
+
+    def _device_checks(self):
+        """Error words the in-graph kernels leave instead of hanging, read off the hot path (one
+        host sync per ``allreduce_check_steps``): the xgmi kernel's timed-out peer wait (its
+        gradient is then only partly reduced) and the fused optimizer's end-of-launch wait
+        (optim.hip kErrFlag). Fails loudly so the supervisor stops the run and the chief keeps
+        its last consistent checkpoint."""
+        if self.reducer.xgmi is not None:
+            self.reducer.check()
+        t = getattr(self.net.optimizer, 'ticket', None)
+        if t is not None and t.is_cuda and t.numel() > 2 and int(t[2].item()) != 0:
+            raise RuntimeError('fused optimizer: an end-of-launch arrival wait gave up (step %d)' % self.train_steps)
 
     def update_target_now(self, tau: float = 1.0):
         """Unconditional target sync (reference `_update_target_network` at init, `dqn_agent.py:50`)."""

@@ -237,15 +237,15 @@ class RunSupervisor:
 
     def attach_learner(self, learner):
         """Checkpoint consistency check of this run: before every save the learner's in-graph
-        all-reduce transport (xgmi) must report a clean error word; a failure is logged with the
-        train step and the save is refused."""
-        red = getattr(learner, 'reducer', None)
-        if self.ckpt is None or red is None or getattr(red, 'xgmi', None) is None:
+        error words (the xgmi all-reduce transport's, the fused optimizer's end-of-launch wait)
+        must be clean; a failure is logged with the train step and the save is refused."""
+        dev_checks = getattr(learner, '_device_checks', None)
+        if self.ckpt is None or dev_checks is None:
             return
 
         def check():
             try:
-                red.check()
+                dev_checks()
             except Exception as e:
                 log.error('rank %d: gradient all-reduce failed at or before train step %d (%r): not saving a '
                           'checkpoint from this state', self.rank, self.last_step, e)

@@ -70,6 +70,20 @@ def main():
         out['fc_fused'] = timeit(lambda: launch(True, False))
         out['plain+sampler'] = timeit(lambda: launch(False, True))
         out['fc_fused+sampler'] = timeit(lambda: launch(True, True))
+        # the launch without the fc weight tiles (what remains if they run elsewhere)
+        items_all = ex.upd_items
+        ex.upd_items = [it for it in items_all if not (it[0] == 0 and it[20] >= 0)]
+        ex._upd_dev = {}
+        out['no_fc_tiles+sampler'] = timeit(lambda: launch(True, True))
+        out['jobs_no_fc_tiles'] = len(ex.upd_items)
+        ex.upd_items = items_all
+        ex._upd_dev = {}
+        if os.environ.get('DQN_OPT_PROF'):
+            launch(True, True)
+            torch.cuda.synchronize()
+            t = ex.ext.optim_prof()
+            out['stamps_block0'] = [t[i] - t[0] for i in range(1, 5)]
+            out['stamps_block1'] = [t[8 + i] - t[8] if t[8 + i] else 0 for i in range(1, 8)]
         net.optimizer.request_slots(True)
         out['fc_fused+sampler+mom'] = timeit(lambda: launch(True, True))
         net.optimizer.request_slots(False)
