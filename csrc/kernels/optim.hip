@@ -212,7 +212,7 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 // kModeFc: some jobs form their gradient from FcFuse rows (16-bit builds).
 constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8;
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, (MODE & ~kModeFc) == 0 ? 8 : (((MODE & kModeTmix) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+__global__ void __launch_bounds__(kPackThreads, (MODE & ~kModeFc) == 0 ? 8 : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
@@ -446,6 +446,32 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       ld(tgt, mo, tw);
       if constexpr (NZ) ld(tgt, so, tws);
     }
+    // factorised-noise factors (loaded with the item's batch, before the fc gradient: a separate
+    // round trip after it cost Rainbow's items ~1 us each): f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
+    float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
+    float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};     // (tmix: the target's next sample)
+    const bool hin = NZ && !elem && jb.ein_off >= 0;
+    const int ki = NZ ? jb.ein_off + (hin && rowok ? k : 0) : 0;     // clamped: always in range
+    if constexpr (NZ) {
+      const float* gn = DG ? gnoise : noise;             // (DG: the sample the forward used)
+      const float ni = noise[hin ? ki : 0], gi = DG ? gn[hin ? ki : 0] : 1.f;
+      float no[4], go[4], to[4] = {1.f, 1.f, 1.f, 1.f}, ti = 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int oi = jb.eout_off + (ok[j] ? n + j : 0);
+        no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f;
+        if (tmix) to[j] = tnoise[oi];
+      }
+      if (tmix) ti = tnoise[hin ? ki : 0];
+      if (hin) { nin = fnz(ni); gin = fnz(gi); }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); }
+      if (tmix) {
+        if (hin) tin = fnz(ti);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tout[j] = fnz(to[j]);
+      }
+    }
     if constexpr (UPD) {
 #if !DQN_ACT_F32
       // fused fc weight / bias gradient (block-uniform), formed while the item's HBM loads
@@ -470,31 +496,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         }
       } else if (!fcj) {
         ld(G, mo, g);
-      }
-    }
-    // factorised-noise factors: f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
-    float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
-    float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};     // (tmix: the target's next sample)
-    const bool hin = NZ && !elem && jb.ein_off >= 0;
-    const int ki = NZ ? jb.ein_off + (hin && rowok ? k : 0) : 0;     // clamped: always in range
-    if constexpr (NZ) {
-      const float* gn = DG ? gnoise : noise;             // (DG: the sample the forward used)
-      const float ni = noise[hin ? ki : 0], gi = DG ? gn[hin ? ki : 0] : 1.f;
-      float no[4], go[4], to[4] = {1.f, 1.f, 1.f, 1.f}, ti = 1.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int oi = jb.eout_off + (ok[j] ? n + j : 0);
-        no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f;
-        if (tmix) to[j] = tnoise[oi];
-      }
-      if (tmix) ti = tnoise[hin ? ki : 0];
-      if (hin) { nin = fnz(ni); gin = fnz(gi); }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); }
-      if (tmix) {
-        if (hin) tin = fnz(ti);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tout[j] = fnz(to[j]);
       }
     }
     // ---- update
@@ -649,9 +650,25 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     if (noise_rng != nullptr) noise_rng[1] += 1;        // (the drawing launch completed before this one)
   }
-  // every other block consumed gnoise before its arrival add: block 0 may overwrite it now
-  if (noise_dst != nullptr)
-    for (int i = threadIdx.x; i < noise_n; i += blockDim.x) noise_dst[i] = noise[i];
+  // every other block consumed gnoise before its arrival add: block 0 may overwrite it now --
+  // float4 pieces, every load of a round issued before its stores (a load -> store chain per
+  // element cost Rainbow's launch ~6.5 us at its end: 15.6k cycles for ~8.7k floats)
+  if (noise_dst != nullptr) {
+    const bool al16 = ((reinterpret_cast<uintptr_t>(noise) | reinterpret_cast<uintptr_t>(noise_dst)) & 15) == 0;
+    const int n4 = al16 ? noise_n >> 2 : 0, tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    const float4* s4 = reinterpret_cast<const float4*>(noise);
+    float4* d4 = reinterpret_cast<float4*>(noise_dst);
+    constexpr int kU = 8;
+    for (int base = 0; base < n4; base += kU * nt) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] = s4[min(base + u * nt + tid, n4 - 1)];     // (clamped: no branch)
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (base + u * nt + tid < n4) d4[base + u * nt + tid] = v[u];
+    }
+    for (int i = 4 * n4 + tid; i < noise_n; i += nt) noise_dst[i] = noise[i];
+  }
   OPT_MARK(4);
 #undef OPT_MARK
 }

@@ -139,13 +139,39 @@ DQN_DEV int per_sample_lane(const float* __restrict__ sum, const float* __restri
   const float total = sum[1];
   u32x4 r = philox(seed ^ 0x5bd1e995ull, ctr, (uint32_t)i, 0x7u);
   float u = ((float)i + u01(r.x)) * (total / (float)B);
-  int node = 1;
+  // descent kPerDepth levels per memory round trip: every (left, right) child pair of the
+  // kPerDepth-deep subtree under `node` (2^kPerDepth - 1 pairs, one 8-byte load each: the two
+  // children are adjacent) is loaded in one batch, then the walk through it is ALU + selects.
+  // 20 levels (P = 2^20) take 5 dependent loads instead of 20 (~1 us each from the MALL: the
+  // prioritized sampler block was the longest block of Rainbow's optimizer launch). Same
+  // decisions as one level at a time, so the same leaves.
+  constexpr int kPerDepth = 4, kPairs = (1 << kPerDepth) - 1;
+  int node = 1, depth = 0;
+  const int L = 31 - __clz(P);                      // log2(P): P is a power of two
+  const float2* __restrict__ pairs = reinterpret_cast<const float2*>(sum);   // pairs[n] = (sum[2n], sum[2n+1])
   while (node < P) {
-    const int left = 2 * node;
-    const float ls = sum[left];
-    const bool right = (u >= ls) && (sum[left + 1] > 0.f);
-    u = right ? u - ls : u;
-    node = right ? left + 1 : left;
+    const int d = min(kPerDepth, L - depth);          // (uniform: every lane descends in step)
+    float2 v[kPairs];
+#pragma unroll
+    for (int r = 0; r < kPerDepth; ++r)
+#pragma unroll
+      for (int j = 0; j < (1 << r); ++j)
+        v[(1 << r) - 1 + j] = r < d ? pairs[(node << r) + j] : make_float2(0.f, 0.f);
+    int cur = node;
+#pragma unroll
+    for (int r = 0; r < kPerDepth; ++r) {
+      if (r >= d) break;
+      const int j = cur - (node << r);
+      float2 c = v[(1 << r) - 1];
+#pragma unroll
+      for (int q = 1; q < (1 << r); ++q)
+        if (j == q) c = v[(1 << r) - 1 + q];
+      const bool right = (u >= c.x) && (c.y > 0.f);
+      u = right ? u - c.x : u;
+      cur = 2 * cur + (right ? 1 : 0);
+    }
+    node = cur;
+    depth += d;
   }
   const int n = max(nsize, 1);
   int leaf = min(node - P, n - 1);

@@ -233,9 +233,16 @@ def test_det_wgrad_bitwise_reproducible(extra):
         torch.cuda.synchronize()
         states.append((one, _state(net)))
     (a1, a4), (b1, b4), (c1, _) = states
+    lr = float(net.optimizer.lr)
     for key in a4:
         assert torch.equal(a1[key], b1[key]) and torch.equal(a4[key], b4[key]), key
-        torch.testing.assert_close(a1[key], c1[key], rtol=1e-5, atol=1e-9, msg=key)
+        # against the atomics path: summation order only. Adam's first step is ~lr * sign(g) where
+        # a conv gradient cancels to ~eps, so a few such elements may move by up to ~lr; every
+        # other element agrees to 1e-5
+        d = (a1[key] - c1[key]).abs()
+        bad = d > 1e-9 + 1e-5 * c1[key].abs()
+        assert float(bad.float().mean()) < 1e-4 and float(d.max()) <= 2.5 * lr, \
+            (key, int(bad.sum()), float(d.max()))
 
 
 def test_det_wgrad_conv_update_matches_fp32_oracle():
