@@ -292,38 +292,44 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
 #if !DQN_ACT_F32
   __shared__ __attribute__((aligned(16))) unsigned char fcl[FC ? kFcLds : 16];
   // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
-  auto fc_tile_grad = [&](const UpdJob& jb, float* g) {
-    act_t* Xs = reinterpret_cast<act_t*>(fcl);           // [32][kFcSX]: x[m][k0 .. k0 + 32)
-    act_t* Hs = Xs + 32 * kFcSX;                         // [32][kFcSH]: dh[m][col + n0 .. + 64)
-    float* R = reinterpret_cast<float*>(fcl);            // [32][kFcRS] fp32 dW tile (after the MFMAs)
-    const int wv = t >> 6, lane = t & 63;
-    const int kt = wv >> 2, nt = wv & 3;
-    // loaders: t < 128 one 8-element piece of an x row, 128 <= t < 384 one of a dh row
+  // this thread's 8-element piece of fc operand rows m0 .. m0 + 31 of the item's 32 (k) x 64 (n)
+  // tile: t < 128 a piece of an x row, 128 <= t < 384 one of a dh row
+  auto fc_load = [&](const UpdJob& jb, int m0) {
     const bool lx = t < 128, lh = t >= 128 && t < 384;
     const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
     const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
     const act_t* X = reinterpret_cast<const act_t*>(ff.x);
     const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
-    auto load = [&](int m0) {
-      const int m = m0 + lr;
-      bfx8 v;
+    const int m = m0 + lr;
+    bfx8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (act_t)0.f;
-      // (32-bit element offsets off the uniform bases: no per-thread 64-bit address kept live)
-      if (m < ff.M) {
-        if (lx && jb.k0 + lc < jb.K)
-          v = *reinterpret_cast<const bfx8*>(X + (uint32_t)(m * ff.ldx + jb.k0 + lc));
-        else if (lh && jb.n0 + lc < jb.N)
-          v = *reinterpret_cast<const bfx8*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + jb.n0 + lc));
-      }
-      return v;
-    };
+    for (int j = 0; j < 8; ++j) v[j] = (act_t)0.f;
+    // (32-bit element offsets off the uniform bases: no per-thread 64-bit address kept live)
+    if (m < ff.M) {
+      if (lx && jb.k0 + lc < jb.K)
+        v = *reinterpret_cast<const bfx8*>(X + (uint32_t)(m * ff.ldx + jb.k0 + lc));
+      else if (lh && jb.n0 + lc < jb.N)
+        v = *reinterpret_cast<const bfx8*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + jb.n0 + lc));
+    }
+    return v;
+  };
+  // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows;
+  // v0: this thread's piece of the first 32-row chunk, loaded with the item's HBM batch
+  auto fc_tile_grad = [&](const UpdJob& jb, float* g, bfx8 v0) {
+    act_t* Xs = reinterpret_cast<act_t*>(fcl);           // [32][kFcSX]: x[m][k0 .. k0 + 32)
+    act_t* Hs = Xs + 32 * kFcSX;                         // [32][kFcSH]: dh[m][col + n0 .. + 64)
+    float* R = reinterpret_cast<float*>(fcl);            // [32][kFcRS] fp32 dW tile (after the MFMAs)
+    const int wv = t >> 6, lane = t & 63;
+    const int kt = wv >> 2, nt = wv & 3;
+    const bool lx = t < 128, lh = t >= 128 && t < 384;
+    const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
+    const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
     const act_t* ph = Hs + (4 * gq + rq) * kFcSH + nt * 16 + cp;
     const act_t* px = Xs + (4 * gq + rq) * kFcSX + kt * 16 + cp;
     for (int m0 = 0; m0 < ff.M; m0 += 32) {
-      const bfx8 v = load(m0);
+      const bfx8 v = m0 == 0 ? v0 : fc_load(jb, m0);
       __syncthreads();                 // previous chunk's operand reads / previous item's R reads done
       if (lx) *reinterpret_cast<bfx8*>(Xs + lr * kFcSX + lc) = v;
       else if (lh) *reinterpret_cast<bfx8*>(Hs + lr * kFcSH + lc) = v;
@@ -446,6 +452,14 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       ld(tgt, mo, tw);
       if constexpr (NZ) ld(tgt, so, tws);
     }
+    // the fc tile's first 32 operand rows (L2 / MALL) join the batch: fc_tile_grad then waits on
+    // one round trip instead of issuing its own after the batch has drained
+    bfx8 fx0;
+#if !DQN_ACT_F32
+    if constexpr (FC && UPD) {
+      if (fcj && !elem) fx0 = fc_load(jb, 0);
+    }
+#endif
     // factorised-noise factors (loaded with the item's batch, before the fc gradient: a separate
     // round trip after it cost Rainbow's items ~1 us each): f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
     float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
@@ -479,7 +493,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       if constexpr (FC) {
         if (fcj) {
           OPT_MARK(5);
-          if (elem) fc_bias_grad(jb, g); else fc_tile_grad(jb, g);
+          if (elem) fc_bias_grad(jb, g); else fc_tile_grad(jb, g, fx0);
           OPT_MARK(6);
         }
       }
