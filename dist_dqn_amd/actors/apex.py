@@ -79,6 +79,10 @@ class ActorSpec:
     reward_clip: float = 0.0
     max_frames: int = 0                     # stop after this many env steps (0 = until told)
     cpus: Optional[Sequence[int]] = None    # CPUs the actor process may run on (None: inherited)
+    # CPU pacing (--apex_pace): this actor's share of one CPU (0 = unpaced). The actor sleeps
+    # whenever its CPU time runs ahead of share x wall time, so all actors together stay under
+    # the container's CFS quota while spread over every visible CPU (no pinning)
+    cpu_share: float = 0.0
 
 
 def _map(path: str, nbytes: int, create: bool = False) -> np.memmap:
@@ -137,6 +141,15 @@ def actor_main(spec: ActorSpec):
         return True
 
     frames = 0
+    share = float(spec.cpu_share)
+    cpu0, wall0 = time.process_time(), time.monotonic()
+
+    def pace():
+        # (every 8 env steps) sleep off CPU time used beyond share x wall time
+        over = (time.process_time() - cpu0) / share - (time.monotonic() - wall0)
+        if over > 0.0:
+            time.sleep(min(over, 0.05))
+
     while not lib.mbox_stopped(mbox):
         obs = observe(env.reset())
         hdr['kind'], hdr['done'], hdr['action'], hdr['reward'], hdr['ret'] = KIND_RESET, 0, 0, 0.0, 0.0
@@ -174,6 +187,8 @@ def actor_main(spec: ActorSpec):
                 state = o.copy()
             if spec.max_frames and frames >= spec.max_frames:
                 return
+            if share > 0.0 and (frames & 7) == 0:
+                pace()
 
 
 class ApexActorPool:
@@ -241,6 +256,12 @@ class ApexActorPool:
         """Restrict the actor processes to these CPUs (before ``start``)."""
         for sp in self.specs:
             sp.cpus = tuple(cpus) if cpus else None
+
+    def set_actor_pacing(self, total_cpus: float):
+        """Unpinned actors whose CPU time together stays under ``total_cpus`` (before ``start``)."""
+        for sp in self.specs:
+            sp.cpus = None
+            sp.cpu_share = max(1e-3, float(total_cpus) / max(1, self.n))
 
     def start(self):
         for s in self.specs:
@@ -423,6 +444,7 @@ class ApexTrainer:
         self.learn_frames0 = 0
         self.native_ingest = bool(getattr(config, 'apex_native_ingest', 1))
         self.reserve_cpus = int(getattr(config, 'apex_reserve_cpus', 3))
+        self.pace = float(getattr(config, 'apex_pace', 0.0))
         self._ingest = None                 # native ingest server (csrc/ingest_server.cpp)
         self._cpus = None                   # (learner, ingest, inference) CPUs when reserved
         self.loop_time = {'drain': 0.0, 'step': 0.0, 'iters': 0}   # main-loop wall split (bench)
@@ -546,6 +568,15 @@ class ApexTrainer:
             return
         cpus = usable_cpus()
         r = self.reserve_cpus
+        q = cfs_quota_cpus()
+        if self.pace > 0 and q is not None and q < len(allowed):
+            # paced, unpinned actors: their CPU time together <= pace x (quota - reserved), spread
+            # over every visible CPU; the learner / ingest / inference threads keep no pinning
+            budget = self.pace * max(1.0, float(q - max(r, 0)))
+            self.pool.set_actor_pacing(budget)
+            log.info('Ape-X: %d paced actors, %.1f CPUs of a %d-CPU CFS quota over %d visible CPUs',
+                     self.pool.n, budget, q, len(allowed))
+            return
         if r <= 0 or len(cpus) < r + 4:
             if len(cpus) < len(allowed):      # no reservation, but stay within the quota
                 self.pool.set_actor_cpus(cpus)
