@@ -152,9 +152,11 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_reserve_cpus', default=3, type=int,
       help='Ape-X: CPUs reserved for the learner, ingest and inference threads (one each; the actor '
            'processes run on the rest); 0 = no pinning')
-    a('--apex_pace', default=0.0, type=float,
-      help='Ape-X: > 0 = unpinned actors paced so their CPU time together stays under this fraction of '
-           '(CFS quota - reserved CPUs), instead of pinning them to quota-many CPU ids (0 = pinning)')
+    a('--apex_pace', default=0.9, type=float,
+      help='Ape-X under a CFS CPU quota smaller than the visible CPUs: > 0 = unpinned actors paced so '
+           'their CPU time together stays under this fraction of (quota - reserved CPUs) (measured, 256 '
+           'actors on a 16-CPU quota: learner 8.4k SGD steps/s at 0.9 vs 0.8k with pinning); '
+           '0 = pin the actors to quota-many CPU ids and reserve CPUs for the learner threads')
     a('--apex_graph_steps', default=4, type=int,
       help='Ape-X learner: SGD steps per replayed HIP graph (one host call per that many steps)')
     a('--apex_serve_gap_us', default=100, type=int,
@@ -274,7 +276,7 @@ class Config:
     apex_graph_steps: int = 4
     apex_native_ingest: int = 1
     apex_reserve_cpus: int = 3
-    apex_pace: float = 0.0
+    apex_pace: float = 0.9
     device_envs: int = 0
     device_graph_steps: int = 8
     apex_native_serve: int = 1
