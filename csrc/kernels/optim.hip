@@ -153,7 +153,7 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 // sync writes the target's fp32 master and packed fragments under the predicate.
 typedef __attribute__((ext_vector_type(4))) act_t bfx4;
 
-constexpr int kTicketSubs = 16, kTicketStride = 32;    // hierarchical ticket: int32 words
+constexpr int kTicketSubs = 16, kTicketStride = 32;    // sharded arrival counters: int32 words, 128 B apart
 constexpr int kPackThreads = 512;
 // ticket[kSlotFlag] != 0: momentum-0 RMSProp also stores its `mom` slot this step. That slot
 // (mom = 0 * mom + update) is never read by the update, only saved under its TF name, so the
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(kPackThreads, (MODE & ~kModeFc) == 0 ? 8 : (((
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
-                  act_t* __restrict__ tgt_packed, int tfreq, int hier, const float* __restrict__ noise,
+                  act_t* __restrict__ tgt_packed, int tfreq, const float* __restrict__ noise,
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
                   int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
                   float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff,
@@ -767,15 +767,14 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   h.nt = nt_env;
   static const int prof_env = getenv("DQN_OPT_PROF") ? atoi(getenv("DQN_OPT_PROF")) : 0;
   h.prof = prof_env;
-  // max_grid <= 256: grid-stride over the jobs with a flat ticket (<= 256 arrivals);
-  // larger: one block per job (up to max_grid) with the two-level ticket
+  // one block per job up to max_grid (grid-stride beyond it); block 0 (+1 sampler block when the
+  // launch draws the next minibatch) closes the launch once every other block has arrived
   const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};
   // (the FC modes run exactly one job per block)
   const int cap = ff.x != nullptr ? (njobs > 256 ? njobs : 256) : (max_grid > 256 ? max_grid : 256);
   const TrunkSample sm = smp != nullptr ? *smp : TrunkSample{};
   const PerStep pe = per != nullptr ? *per : PerStep{};
   const int grid = (njobs < cap ? njobs : cap) + (sm.size != nullptr || pe.sum != nullptr ? 1 : 0);   // + sampler
-  const int hier = grid > 256 ? 1 : 0;
   const UpdJob* J = reinterpret_cast<const UpdJob*>(jobs);
   act_t* P = reinterpret_cast<act_t*>(packed);
   act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
@@ -784,7 +783,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   const int mode = (noise != nullptr ? kModeNoisy : 0) | (tnoise != nullptr ? kModeTmix : 0) |
                    (pe.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0);
 #define OPM(N, M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, \
-                       beta_pow, step, ticket, h, J, njobs, P, tgt, TP, tf, hier, noise, eff, gnoise, noise_dst, noise_n, \
+                       beta_pow, step, ticket, h, J, njobs, P, tgt, TP, tf, noise, eff, gnoise, noise_dst, noise_n, \
                        sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng, ff, part)
 #if DQN_ACT_F32
 #define OPK(N) do { switch (mode) { \
