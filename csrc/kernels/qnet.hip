@@ -1397,13 +1397,12 @@ static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
 int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   int total = 0;
   size_t lds = 0;
-  // conv M-chunk: 256 rows once the dense members alone fill the CUs' block slots (Rainbow's
-  // two 3136 x 512 noisy fc layers), else 128 (flagship: the whole grid resident at once)
+  // conv M-chunk: 256 rows (half the blocks and half the fp32 atomic bytes of 128-row chunks;
+  // measured round 3, alternating on one box: flagship 13.87k vs 13.60k SGD steps/s, Rainbow
+  // 7.88k vs 7.77k, profiles/r3_wgrad_mc.md) in the 16-bit builds; 128 in the fp32 build (its
+  // 256-row staging is 135 KB of LDS: one block per CU). DQN_WGRAD_MC=128|256 overrides.
   static const int mc_env = getenv("DQN_WGRAD_MC") ? atoi(getenv("DQN_WGRAD_MC")) : 0;
-  int dense_blocks = 0;
-  for (int i = 0; i < G.n; ++i)
-    if (G.kind[i] == L_DENSE_FWD_RELU) dense_blocks += ((G.a[i].K + 63) / 64) * ((G.g[i].N + 127) / 128);
-  const bool mc256 = mc_env == 256 || (mc_env == 0 && dense_blocks > 256);
+  const bool mc256 = mc_env == 256 || (mc_env == 0 && !DQN_ACT_F32);
   for (int i = 0; i < G.n; ++i) {
     if (G.g[i].part != nullptr) continue;       // (partial members: 128-row chunks, see below)
     if (mc256 && G.kind[i] >= L_NAT_CONV1_FWD && G.kind[i] <= L_NAT_CONV3_FWD) G.kind[i] += kGrpMC256;
