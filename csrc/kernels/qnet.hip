@@ -1237,7 +1237,9 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case 100 + L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 0, 13); return 0;   // 32-row blocks
     case 200 + L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 4, 0, 13); return 0;   // 16 x 32, split-K 4
     case 100 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 2, 2, 2, 8); return 0;
-    case 200 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 2, 2, 8); return 0;   // 16 x 32, split-K 2 (r2 default)
+    // 16 x 16 blocks, split-K 4: round-3 A/B +0.8-1.0% (profiles/r3_tile_sweep.md); default once the
+    // GPU suite has run with it
+    case 200 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 4, 2, 4); return 0;
     case 100 + L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 4, 2, 1, 2, 2, 9); return 0;
     case 100 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 1, 1, 4, 2, 8); return 0;         // 16 rows, split-K 4
     case 200 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;         // all 16 taps (pre-parity)
@@ -1254,9 +1256,7 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 8, 0, 13); return 0;
     case L_DENSE_FWD_F32: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 1, 13); return 0;
     // ---- backward data, ReLU mask of the layer input
-    // K 512-1024: 16 x 16 blocks, split-K 4 (2x the blocks of 16 x 32; round-3 A/B alternating on
-    // one box: flagship +0.8%, dd +0.8%, Rainbow +1.0%, profiles/r3_tile_sweep.md)
-    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 4, 2, 4); return 0;
+    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 2, 2, 8); return 0;   // K 512-1024
     case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 2, 1, 2, 2, 2, 9); return 0;     // 18 k-steps, 16 x 64 blocks
     case L_NAT_CONV2_DGRAD:
       // parity-class dgrad (8 k-steps of real taps instead of 32 with 3/4 zeros); the generic
