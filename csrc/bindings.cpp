@@ -150,7 +150,10 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
                 std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
                 c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng, std::vector<int64_t> fc,
-                int64_t part) {
+                int64_t part, int64_t wg, int64_t wg_blocks, int64_t wg_jobs) {
+  // wg / wg_blocks: the launch also computes the grouped weight gradients -- a device WgradGroup
+  // (qnet_wgrad_plan) whose wg_blocks tiles follow the lead block; jobs with dep >= 0 wait for
+  // their member (needs fc: the launch forms the fc gradients from FcFuse rows)
   // part: 0 or the base of the grouped conv wgrad's partial buffer (jobs with part_n > 0 sum it)
   // fc: [] or [x ptr, dh ptr, M, ldx, ldh]: the launch forms the fc weight / bias gradient of the
   // jobs carrying a dH column from those act_t rows (optim.hip FcFuse) instead of reading `grad`
@@ -288,6 +291,11 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
     ff = FcFuse{P<const void*>(fc[0]), P<const void*>(fc[1]), (int)fc[2], (int)fc[3], (int)fc[4]};
   }
   TORCH_CHECK(ticket.numel() >= 2, "optim_pack: ticket[1] is the slot flag word");
+  if (wg != 0) {
+    TORCH_CHECK(wg_blocks >= 1 && wg_blocks <= 16384 && !fc.empty() && op >= 0 && part == 0 && (wg % 16) == 0 &&
+                    wg_jobs >= 1 && wg_jobs <= jobs.numel() / upd_job_ints(),
+                "optim_pack wg: needs fc rows and an update, no partials; 1 <= wg_jobs <= jobs");
+  }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
@@ -296,7 +304,8 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     (float)grad_scale, jobs.data_ptr(), (int)(jobs.numel() / upd_job_ints()), packed.data_ptr(), tgt,
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
                     per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, fc.empty() ? nullptr : &ff,
-                    reinterpret_cast<const float*>(part), cur_stream());
+                    reinterpret_cast<const float*>(part), reinterpret_cast<const void*>(wg), (int)wg_blocks,
+                    (int)wg_jobs, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {
@@ -721,7 +730,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("has_step"), pybind11::arg("hp"), pybind11::arg("target") = pybind11::none(),
         pybind11::arg("target_freq") = 1);
   m.def("target_update", &target_update);
-  m.def("optim_pack", &optim_pack);
+  m.def("optim_pack", &optim_pack, pybind11::arg("op"), pybind11::arg("w"), pybind11::arg("grad"),
+        pybind11::arg("s0"), pybind11::arg("s1"), pybind11::arg("beta_pow"), pybind11::arg("ticket"),
+        pybind11::arg("lr"), pybind11::arg("reg"), pybind11::arg("reg_end"), pybind11::arg("grad_scale"),
+        pybind11::arg("step"), pybind11::arg("hp"), pybind11::arg("jobs"), pybind11::arg("packed"),
+        pybind11::arg("target"), pybind11::arg("target_packed"), pybind11::arg("target_freq"),
+        pybind11::arg("max_grid"), pybind11::arg("noise"), pybind11::arg("eff"), pybind11::arg("grad_noise"),
+        pybind11::arg("noise_dst"), pybind11::arg("sample"), pybind11::arg("per_p"), pybind11::arg("per_f"),
+        pybind11::arg("tnoise"), pybind11::arg("teff"), pybind11::arg("tpk"), pybind11::arg("noise_rng"),
+        pybind11::arg("fc"), pybind11::arg("part"), pybind11::arg("wg") = 0, pybind11::arg("wg_blocks") = 0,
+        pybind11::arg("wg_jobs") = 0);
   m.def("noise_normal", &noise_normal);
   m.attr("UPD_JOB_INTS") = upd_job_ints();
   m.def("optim_prof", []() {
@@ -729,6 +747,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     optim_prof_read(v.data());
     return v;
   }, "optim_pack s_memtime phase stamps of blocks 0 and 1 (DQN_OPT_PROF=1 launches)");
+  m.def("optim_timeline", [](int64_t nblocks) {
+    std::vector<int64_t> v(3 * (size_t)std::max<int64_t>(nblocks, 0), 0);
+    const int n = optim_timeline_read(v.data(), (int)nblocks);
+    v.resize(3 * (size_t)n);
+    return v;
+  }, "per-block [start, ready, end] s_memrealtime stamps (100 MHz) of the last DQN_OPT_PROF=1 optim_pack launch");
+  m.def("optim_tile_phases", [](int64_t nblocks) {
+    std::vector<int64_t> v(8 * (size_t)std::max<int64_t>(nblocks, 0), 0);
+    const int n = optim_tile_phases_read(v.data(), (int)nblocks);
+    v.resize(8 * (size_t)n);
+    return v;
+  }, "[8] s_memrealtime phase stamps of each of the first weight-gradient tiles of the last probe launch");
   m.attr("OPTIM_FC_FUSE") = optim_fc_fuse();
   m.def("td_loss_scalar", &td_loss_scalar);
   m.def("td_loss_c51", &td_loss_c51);

@@ -58,9 +58,14 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
-                       int64_t* noise_rng, const FcFuse* fc, const float* part, hipStream_t st);
+                       int64_t* noise_rng, const FcFuse* fc, const float* part, const void* wg, int wg_blocks,
+                       int wg_jobs, hipStream_t st);
 // 1 when this build's optimizer launch can form the fc weight gradient itself (16-bit builds)
 int optim_fc_fuse();
+// probe launches (DQN_OPT_PROF=1): per-block [start, ready, end] s_memrealtime stamps of the last launch
+int optim_timeline_read(int64_t* out, int nblocks);
+// ... and [8] phase stamps inside each of the first weight-gradient tiles of a fused launch
+int optim_tile_phases_read(int64_t* out, int nblocks);
 // standard-normal noise (Box-Muller over Philox keyed by rng[0], counter rng[1], bumped)
 void launch_noise_normal(float* out0, float* out1, int n, int64_t* rng, hipStream_t st);
 int upd_job_ints();

@@ -192,7 +192,17 @@ struct WgradGroup {
   int kind[kMaxWgradMembers];
   int nblk[kMaxWgradMembers], gx[kMaxWgradMembers], gy[kMaxWgradMembers];     // filled by the launcher
   int n;
+  // fused launches (optim.hip kModeWg): done counters (int32, 32 words apart, zero between
+  // launches: [m] per member, then [kMaxWgradMembers + m * kWgSlots + s] per member K-range s <
+  // kWgSlots - 1 and the member's bias, s = kWgSlots - 1), the member reading the current
+  // minibatch's frame-slot tables (-1: none), and per (member, slot) the optimizer jobs its last
+  // tile runs once that slot's gradient is complete (a contiguous range of the launch's job table)
+  int32_t* done;
+  int slots_member;
+  int dep_first[kMaxWgradMembers][16 + 1], dep_count[kMaxWgradMembers][16 + 1];
 };
+constexpr int kWgSlots = 16 + 1;            // K-ranges (<= 16) + the bias
+constexpr int kWgCounters = kMaxWgradMembers * (1 + kWgSlots);
 
 enum LayerKind {
   L_NAT_CONV1_FWD = 1, L_NAT_CONV2_FWD = 2, L_NAT_CONV3_FWD = 3,
@@ -210,6 +220,11 @@ void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int 
 int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
 int launch_wgrad_group(dqn::WgradGroup G, hipStream_t st);
+// Plans G for the fused weight-gradient range of a split optimizer update (optim.hip kModeWg):
+// fills nblk / gx / gy and every member's chunk grouping (conv members: conv_chunks 128-row chunks
+// summed in registers per tile, one set of fp32 atomics per group) and atomic flag. Returns the
+// total block count, or -1 when a member kind has no fused tile (16-bit builds only).
+int wgrad_fused_plan(dqn::WgradGroup& G, int conv_chunks);
 void launch_cnn_fwd(const dqn::CnnFwdArgs& a, int B, int ninst, hipStream_t st);
 void launch_cnn_bwd(const dqn::CnnBwdArgs& a, int B, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);

@@ -10,72 +10,9 @@
 // then the TF update rule. Adam's beta powers (TF non-slot variables) are
 // read by every block and advanced by the LAST block to finish (arrival
 // ticket), together with global_step, so no extra launch is needed.
-#include <stdlib.h>
-#include <type_traits>
-#include "common.h"
-#include "sample_dev.h"
-#include "sumtree_dev.h"
-#include "../include/dqn_kernels.h"
+#include "optim_pack.h"
 
 namespace dqn {
-
-struct OptHP {
-  float lr, reg, grad_scale;
-  float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
-  int reg_end;
-  int nt;            // probe: 1 = fp32 weight / slot stores non-temporal (DQN_OPT_NT)
-  int prof;          // probe: 1 = s_memtime phase stamps of blocks 0 and 1 into g_opt_prof (DQN_OPT_PROF)
-};
-
-// optim_pack phase stamps (scripts/probe_optim.py --prof): [0..7] block 0, [8..15] block 1
-__device__ int64_t g_opt_prof[16];
-
-// Contraction is pinned off in the update math so every kernel that inlines it
-// (optim_kernel's float4 loop, optim_pack_kernel's tiles) rounds identically:
-// with fp-contract=fast the backend fuses differently per call site.
-DQN_DEV float opt_grad(float g, float w, bool reg, const OptHP& h) {
-#pragma clang fp contract(off)
-  float x = g * h.grad_scale;
-  if (reg) x += h.reg * w;
-  return x;
-}
-
-template <int OP>
-DQN_DEV void update_one(float& w, float g, float& s0, float& s1, const OptHP& h, float lr_t) {
-#pragma clang fp contract(off)
-  if constexpr (OP == 0) {            // sgd
-    w -= h.lr * g;
-  } else if constexpr (OP == 1) {     // momentum (non-Nesterov)
-    s0 = h.momentum * s0 + g;
-    w -= h.lr * s0;
-  } else if constexpr (OP == 2) {     // rmsprop: ms (init 1), mom
-    s0 = h.rho * s0 + (1.f - h.rho) * g * g;
-    s1 = h.rms_mom * s1 + h.lr * g / sqrtf(s0 + h.rms_eps);
-    w -= s1;
-  } else if constexpr (OP == 7) {     // rmsprop with momentum 0 (the TF / reference default):
-    s0 = h.rho * s0 + (1.f - h.rho) * g * g;   // mom = 0 * mom + u == u exactly, so mom is
-    s1 = h.lr * g / sqrtf(s0 + h.rms_eps);     // written (checkpoint slot) but never read
-    w -= s1;
-  } else if constexpr (OP == 3) {     // adam (TF epsilon-hat form)
-    s0 = h.b1 * s0 + (1.f - h.b1) * g;
-    s1 = h.b2 * s1 + (1.f - h.b2) * g * g;
-    w -= lr_t * s0 / (sqrtf(s1) + h.adam_eps);
-  } else if constexpr (OP == 4) {     // adagrad (accumulator init 0.1)
-    s0 += g * g;
-    w -= h.lr * g / sqrtf(s0);
-  } else if constexpr (OP == 5) {     // adadelta
-    s0 = h.ad_rho * s0 + (1.f - h.ad_rho) * g * g;
-    const float upd = sqrtf(s1 + h.ad_eps) / sqrtf(s0 + h.ad_eps) * g;
-    s1 = h.ad_rho * s1 + (1.f - h.ad_rho) * upd * upd;
-    w -= h.lr * upd;
-  } else {                            // ftrl (lr_power -0.5, l1 = l2 = 0)
-    const float na = s0 + g * g;
-    s1 += g - (sqrtf(na) - sqrtf(s0)) / h.lr * w;
-    const float quad = sqrtf(na) / h.lr;
-    w = fabsf(s1) > 0.f ? -s1 / quad : 0.f;
-    s0 = na;
-  }
-}
 
 template <int OP>
 __global__ void __launch_bounds__(256)
@@ -134,559 +71,6 @@ optim_kernel(float* __restrict__ w, const float* __restrict__ grad, float* __res
 }
 
 
-// ------------------------------------------------------------- update + pack
-// The optimizer step fused with the executor's weight packing: a 512-thread workgroup
-// owns a 32 (k) x 64 (n) tile of a weight matrix (TF layout [K][N]), each thread 4
-// consecutive n of one row (one float4 per operand: few VGPRs, high occupancy). It
-// updates the tile in registers, writes fp32 weights + slots back, and emits the tile's
-// bf16 MFMA fragments straight away:
-//   * forward fragments ([K/32][N/16][64][8]: 8 consecutive k per lane): a wave owns an
-//     8 (k) x 32 (n) sub-tile with lane = 8 * col-group + row, so the 4 lanes of a quad hold
-//     4 consecutive rows x the same 4 columns; one 4x4 DPP transpose per quad leaves each
-//     lane 4 consecutive k of one column = half of a fragment slot, stored directly (no LDS
-//     round trip, no barrier; the LDS transpose it replaces ran at ~40% bank conflicts);
-//   * dgrad fragments (dense transpose, or conv (tap, co) x ci) directly from the
-//     thread's registers: its 4 consecutive K' ARE 4 consecutive n of one row (half
-//     of one lane's 8-value slot).
-// Elementwise items (biases, ...) carry an optional fp32 copy into the packed
-// buffer (the concatenated fc bias). Same ticket as optim_kernel; the hard target
-// sync writes the target's fp32 master and packed fragments under the predicate.
-typedef __attribute__((ext_vector_type(4))) act_t bfx4;
-
-constexpr int kTicketSubs = 16, kTicketStride = 32;    // sharded arrival counters: int32 words, 128 B apart
-constexpr int kPackThreads = 512;
-// ticket[kSlotFlag] != 0: momentum-0 RMSProp also stores its `mom` slot this step. That slot
-// (mom = 0 * mom + update) is never read by the update, only saved under its TF name, so the
-// hot path skips its 4 bytes / parameter and the checkpoint manager raises the flag for the
-// step before a save (optim.py Optimizer.request_slots).
-constexpr int kSlotFlag = 1;
-// ticket[kErrFlag] != 0: an optim_pack launch's end-of-launch wait gave up (lost arrival; never
-// expected -- the learner's periodic check reads it)
-constexpr int kErrFlag = 2;
-
-#if !DQN_ACT_F32
-// Fused fc weight gradient (FcFuse): a 32 (k) x 64 (n) update tile's dW = X^T dH over M rows,
-// 32-row chunks staged ROW-major in LDS (strides + 16 elements: conflict-free transposed reads,
-// as the grouped wgrad), wave w owning the 16 x 16 sub-tile (k: w >> 2, n: w & 3) as dW^T =
-// dH^T X on one v_mfma_f32_16x16x32 per chunk (lane: one k, 4 consecutive n), then through
-// an fp32 LDS tile into the update's own thread map (row r, 4 consecutive n).
-constexpr int kFcSX = 32 + 16, kFcSH = 64 + 16, kFcRS = 64 + 4;
-constexpr int kFcLds = 32 * kFcRS * 4;          // >= staging (32 * (SX + SH) * 2 B) and 4 x 512 fp32
-static_assert(32 * (kFcSX + kFcSH) * 2 <= kFcLds && 4 * 512 * 4 <= kFcLds, "fc LDS plan");
-#endif
-
-struct UpdJob {
-  int kind;                      // 0 = tile, 1 = elementwise chunk
-  int src_off, K, N, k0, n0;     // tile: tensor offset / shape / origin; elem: offset, count (K)
-  int fwd_off, fwd_N16, fwd_nt_off, fwd_ks_off;   // forward fragments (elem: fp32 copy offset or -1)
-  int dg_mode, dg_off, dg_N16, dg_nt_off, dg_ks_off, dg_cin;   // dgrad: 0 none, 1 conv, 2 dense
-  // noisy nets (factorised Gaussian): the sigma tensor is updated in the same thread as mu
-  // and the packed / eff values are mu + sigma * f(noise[ein + k]) f(noise[eout + n])
-  // (ein < 0: f = 1, biases; elem chunks: eout already offset to the chunk start)
-  int sig_off, ein_off, eout_off;
-  int eff;                       // 1: also store the effective fp32 value at eff[src index]
-  // fc weight tile / fc bias chunk whose gradient the launch forms from FcFuse rows: the
-  // tensor's first column in dH (-1: read the flat gradient)
-  int fc_col;
-  // gradient = sum of part_n partial slices (the grouped conv wgrad's deterministic chunk-group
-  // sums, qnet.hip): element d of the tensor at part[part_off + p * part_stride + d], p ascending
-  int part_off, part_n, part_stride;
-};
-
-DQN_DEV float fnz(float x) { return copysignf(sqrtf(fabsf(x)), x); }
-
-template <int OP>
-DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, int reg_end, const OptHP& h,
-                  float lr_t, const bool* ok) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!ok[j]) continue;
-    update_one<OP>(w[j], opt_grad(g[j], w[j], k0flat + j < reg_end, h), a[j], b[j], h, lr_t);
-  }
-}
-
-// MODE bits: kModeNoisy (noisy jobs in the work list), kModeTmix (+ the target's mix + pack),
-// kModePer (the sampler block runs the prioritized sum-tree path). Paths a mode excludes are
-// not instantiated: their registers would cost the plain nets occupancy (mode 0: 8 waves / SIMD,
-// so every block of the Nature-CNN work list is resident at once).
-// kModeFc: some jobs form their gradient from FcFuse rows (16-bit builds).
-constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8;
-template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, (MODE & ~kModeFc) == 0 ? 8 : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
-optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
-                  float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
-                  const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
-                  act_t* __restrict__ tgt_packed, int tfreq, const float* __restrict__ noise,
-                  float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
-                  int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
-                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff,
-                  const float* __restrict__ part) {
-  // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
-  // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
-  // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
-  // noise on every DP rank makes that exact for the all-reduced sum), instead of being read.
-  // noise_dst: the grid's last block copies noise[0, noise_n) there (next sample -> current).
-  // smp.size != nullptr: the grid's extra block (block 0) draws the NEXT step's uniform minibatch
-  // (sample_dev.h) while the others update: the replay is quiet during this launch, and
-  // the sampler leaves the next step's critical path.
-  // tnoise (noisy nets, update calls): also mix + pack the TARGET under its next noise
-  // sample into teff / tpk (the target's eff / packed buffers): no separate target mix launch.
-  constexpr bool UPD = OP >= 0;
-  constexpr bool TMIX = (MODE & kModeTmix) != 0, NZOK = (MODE & kModeNoisy) != 0, PEROK = (MODE & kModePer) != 0;
-  constexpr bool FC = (MODE & kModeFc) != 0 && !DQN_ACT_F32 && OP >= 0;
-  // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
-  const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
-  // LDS: only the sampler block's scratch (the update items exchange through DPP)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[sizeof(SampleLds) > sizeof(SumtreeLds) ? sizeof(SampleLds)
-                                                                                                     : sizeof(SumtreeLds)];
-  const bool extra = smp.size != nullptr || per.sum != nullptr;   // the grid has a sampler block
-  // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
-  const bool sampler = extra && blockIdx.x == 0;
-  const int nwork = (int)gridDim.x - (extra ? 1 : 0);
-  const int wid = (int)blockIdx.x - (extra ? 1 : 0);      // work index of an update block
-  float lr_t = h.lr;
-  if constexpr (OP == 3) {
-    const float b1p = beta_pow[0], b2p = beta_pow[1];
-    lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-  }
-  const bool sync = UPD && tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
-  const bool psync = sync && tgt_packed != nullptr;
-  constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7;   // second slot written
-  const bool wtwo = OP != 7 || ticket[kSlotFlag] != 0;                         // (momentum-0 RMSProp: flagged)
-  constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
-  constexpr bool ONE = UPD && OP != 0;
-  const int t = threadIdx.x;
-  int64_t* prof = (h.prof && t == 0 && blockIdx.x < 2) ? g_opt_prof + 8 * blockIdx.x : nullptr;
-#define OPT_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
-  OPT_MARK(0);
-  if (PEROK && sampler && per.sum != nullptr) {
-    // prioritized: this step's priorities into the tree (one wave), then the next step's
-    // stratified sample from the updated tree (beta of the NEXT global_step)
-    const int64_t step0 = per.step[0];                  // read before this block's ticket add
-    const uint64_t seed = (uint64_t)per.rng[0], ctr = (uint64_t)per.rng[1];
-    SumtreeLds& L = *reinterpret_cast<SumtreeLds*>(smem);
-    int ins_first = 0;
-    if (per.ins_n > 0) ins_first = (int)((per.ins_cursor[0] - per.ins_n + per.ins_cap) % per.ins_cap);
-    sumtree_update_wave(per.sum, per.mn, per.maxp, per.upd_idx, per.upd_td, per.alpha, per.eps, 0, per.B, per.P,
-                        per.levels, L, 0, 1, per.ins_n, ins_first, per.ins_cap);
-    __syncthreads();                                    // tree writes visible to every lane of the block
-    if ((int)threadIdx.x < per.B) {
-      const float beta = fminf(1.f, per.beta0 + (1.f - per.beta0) * (float)(step0 + 1) / per.beta_steps);
-      per_sample_lane(per.sum, per.mn, seed, ctr, per.size[0], threadIdx.x, per.B, per.P, beta, per.idx_out,
-                      per.w_out, per.so);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) per.rng[1] = (int64_t)(ctr + 1);
-  } else if (sampler) {
-    SampleLds& sls = *reinterpret_cast<SampleLds*>(smem);
-    const uint32_t n = (uint32_t)max(smp.size[0], 1);
-    const uint64_t seed = (uint64_t)smp.rng[0], ctr = (uint64_t)smp.rng[1];
-    const int32_t v = draw_distinct(seed, ctr, n, smp.B, sls);
-    if ((int)threadIdx.x < smp.B) {
-      DQN_ASSERT(v >= 0 && (uint32_t)v < n);
-      write_sample_slots(smp, threadIdx.x, v, reinterpret_cast<const int4*>(smp.state_idx)[v], smp.next_idx[v]);
-    }
-    if (threadIdx.x == 0) smp.rng[1] = (int64_t)(ctr + 1);   // every lane read it before the barriers
-  }
-  OPT_MARK(1);
-#if !DQN_ACT_F32
-  __shared__ __attribute__((aligned(16))) unsigned char fcl[FC ? kFcLds : 16];
-  // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
-  // this thread's 8-element piece of fc operand rows m0 .. m0 + 31 of the item's 32 (k) x 64 (n)
-  // tile: t < 128 a piece of an x row, 128 <= t < 384 one of a dh row
-  auto fc_load = [&](const UpdJob& jb, int m0) {
-    const bool lx = t < 128, lh = t >= 128 && t < 384;
-    const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
-    const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
-    const act_t* X = reinterpret_cast<const act_t*>(ff.x);
-    const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
-    const int m = m0 + lr;
-    bfx8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (act_t)0.f;
-    // (32-bit element offsets off the uniform bases: no per-thread 64-bit address kept live)
-    if (m < ff.M) {
-      if (lx && jb.k0 + lc < jb.K)
-        v = *reinterpret_cast<const bfx8*>(X + (uint32_t)(m * ff.ldx + jb.k0 + lc));
-      else if (lh && jb.n0 + lc < jb.N)
-        v = *reinterpret_cast<const bfx8*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + jb.n0 + lc));
-    }
-    return v;
-  };
-  // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows;
-  // v0: this thread's piece of the first 32-row chunk, loaded with the item's HBM batch
-  auto fc_tile_grad = [&](const UpdJob& jb, float* g, bfx8 v0) {
-    act_t* Xs = reinterpret_cast<act_t*>(fcl);           // [32][kFcSX]: x[m][k0 .. k0 + 32)
-    act_t* Hs = Xs + 32 * kFcSX;                         // [32][kFcSH]: dh[m][col + n0 .. + 64)
-    float* R = reinterpret_cast<float*>(fcl);            // [32][kFcRS] fp32 dW tile (after the MFMAs)
-    const int wv = t >> 6, lane = t & 63;
-    const int kt = wv >> 2, nt = wv & 3;
-    const bool lx = t < 128, lh = t >= 128 && t < 384;
-    const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
-    const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
-    const act_t* ph = Hs + (4 * gq + rq) * kFcSH + nt * 16 + cp;
-    const act_t* px = Xs + (4 * gq + rq) * kFcSX + kt * 16 + cp;
-    for (int m0 = 0; m0 < ff.M; m0 += 32) {
-      const bfx8 v = m0 == 0 ? v0 : fc_load(jb, m0);
-      __syncthreads();                 // previous chunk's operand reads / previous item's R reads done
-      if (lx) *reinterpret_cast<bfx8*>(Xs + lr * kFcSX + lc) = v;
-      else if (lh) *reinterpret_cast<bfx8*>(Hs + lr * kFcSH + lc) = v;
-      __syncthreads();
-      // A = dh^T (rows n), B = x (columns k); the same row permutation on both operands
-      acc = DQN_MFMA16_BUILTIN(join_tr(lds_tr16(ph), lds_tr16(ph + 16 * kFcSH)),
-                               join_tr(lds_tr16(px), lds_tr16(px + 16 * kFcSX)), acc, 0, 0, 0);
-    }
-    __syncthreads();                   // operand reads done before R overwrites the staging
-    // acc[r] = dW[k = kt * 16 + (lane & 15)][n = nt * 16 + 4 * (lane >> 4) + r]
-    *reinterpret_cast<float4*>(R + (kt * 16 + (lane & 15)) * kFcRS + nt * 16 + 4 * (lane >> 4)) =
-        make_float4(acc[0] * kInvLossScale, acc[1] * kInvLossScale, acc[2] * kInvLossScale, acc[3] * kInvLossScale);
-    __syncthreads();
-    const int r = (wv >> 1) * 8 + (lane & 7), c4 = (wv & 1) * 32 + (lane >> 3) * 4;
-    const float4 gv = *reinterpret_cast<const float4*>(R + r * kFcRS + c4);
-    g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
-  };
-  // fc bias chunk (<= 512 values, thread t < 128 owns n = 4t..4t+3): sum_m dh[m][col + n] over 4
-  // row phases, combined in a fixed order
-  auto fc_bias_grad = [&](const UpdJob& jb, float* g) {
-    float* R = reinterpret_cast<float*>(fcl);            // [4][512]
-    const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
-    const int cg = t & 127, ph = t >> 7, c = 4 * cg;
-    float sm[4] = {0.f, 0.f, 0.f, 0.f};
-    if (c < jb.K) {
-#pragma unroll 4
-      for (int m = ph; m < ff.M; m += 4) {
-        const bfx4 v = *reinterpret_cast<const bfx4*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + c));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sm[j] += (float)v[j];
-      }
-    }
-    __syncthreads();                   // previous item's LDS reads done
-    *reinterpret_cast<float4*>(R + ph * 512 + c) = make_float4(sm[0], sm[1], sm[2], sm[3]);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = (4 * t + j) & 511;
-      g[j] = ((R[i] + R[512 + i]) + (R[1024 + i] + R[1536 + i])) * kInvLossScale;
-    }
-  };
-#endif
-  // One job item = a 32x64 tile (or a 2048-element chunk) updated by 4 consecutive elements per
-  // thread. The body is instantiated per (AL = 16-byte aligned float4 rows, NZ = noisy) so that
-  // every global load of the item (mu / sigma / grad / slots / target / noise factors) is an
-  // UNCONDITIONAL load issued in one batch: out-of-range threads read the job's first element
-  // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
-  // vmcnt wait between loads and serialise the item on memory latency.)
-  auto item = [&](const UpdJob& jb, auto al_c, auto nz_c, auto dg_c) {
-    // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read
-    constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value, DG = decltype(dg_c)::value;
-    const bool elem = jb.kind == 1;
-    float g[4];
-    const bool fcj = FC && jb.fc_col >= 0;
-    bool ok[4];
-    int k, n;                      // row (tile) and column / element index within the tensor
-    bool rowok;
-    int64_t e0;
-    if (elem) {                    // chunk of up to 2048 elements: 4 per thread
-      k = 0;
-      n = 4 * t;
-      rowok = true;
-      e0 = (int64_t)jb.src_off + n;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ok[j] = n + j < jb.K;
-    } else {                       // tile: row r, columns c4..c4+3 (wave: 8 rows x 32 columns)
-      const int wv = t >> 6, l = t & 63;
-      const int r = (wv >> 1) * 8 + (l & 7), c4 = (wv & 1) * 32 + (l >> 3) * 4;
-      k = jb.k0 + r;
-      n = jb.n0 + c4;
-      rowok = k < jb.K;
-      e0 = (int64_t)jb.src_off + (int64_t)k * jb.N + n;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ok[j] = rowok && n + j < jb.N;
-    }
-    const int64_t d0 = e0 - jb.src_off;                  // offset within the tensor
-    // clamped element indices: AL -> all 4 in range or none (one float4), else per element
-    int64_t ix[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ix[j] = (AL ? ok[0] : ok[j]) ? d0 + j : 0;
-    auto ld = [&](const float* base, int64_t off, float* v) {
-      if constexpr (AL) {
-        const float4 x = *reinterpret_cast<const float4*>(base + off + ix[0]);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = base[off + ix[j]];
-      }
-    };
-    auto st = [&](float* base, int64_t off, const float* v) {
-      if constexpr (AL) {
-        if (ok[0]) {
-          f32x4* p = reinterpret_cast<f32x4*>(base + off + d0);
-          const f32x4 x = {v[0], v[1], v[2], v[3]};
-          if (h.nt) __builtin_nontemporal_store(x, p); else *p = x;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (ok[j]) base[off + d0 + j] = v[j];
-      }
-    };
-    const int64_t mo = jb.src_off, so = NZ ? jb.sig_off : jb.src_off;
-    float w[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], tw[4], tws[4], e[4], te[4];
-    // ---- every load of the item, issued before any math
-    ld(W, mo, w);
-    if constexpr (ONE) ld(S0, mo, a);
-    if constexpr (TWO_LD) ld(S1, mo, b);
-    if constexpr (NZ) {
-      ld(W, so, ws);
-      if constexpr (UPD) {
-        if constexpr (!DG) ld(G, so, gs);
-        if constexpr (ONE) ld(S0, so, as);
-        if constexpr (TWO_LD) ld(S1, so, bs);
-      }
-    }
-    // the target's mu / sigma in the same batch (one memory round trip per item: the extra
-    // VGPRs keep the same 2 blocks / CU, the block is 8 waves and the budget 128 VGPRs)
-    if (tmix) {
-      ld(tgt, mo, tw);
-      if constexpr (NZ) ld(tgt, so, tws);
-    }
-    // the fc tile's first 32 operand rows (L2 / MALL) join the batch: fc_tile_grad then waits on
-    // one round trip instead of issuing its own after the batch has drained
-    bfx8 fx0;
-#if !DQN_ACT_F32
-    if constexpr (FC && UPD) {
-      if (fcj && !elem) fx0 = fc_load(jb, 0);
-    }
-#endif
-    // factorised-noise factors (loaded with the item's batch, before the fc gradient: a separate
-    // round trip after it cost Rainbow's items ~1 us each): f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
-    float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
-    float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};     // (tmix: the target's next sample)
-    const bool hin = NZ && !elem && jb.ein_off >= 0;
-    const int ki = NZ ? jb.ein_off + (hin && rowok ? k : 0) : 0;     // clamped: always in range
-    if constexpr (NZ) {
-      const float* gn = DG ? gnoise : noise;             // (DG: the sample the forward used)
-      const float ni = noise[hin ? ki : 0], gi = DG ? gn[hin ? ki : 0] : 1.f;
-      float no[4], go[4], to[4] = {1.f, 1.f, 1.f, 1.f}, ti = 1.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int oi = jb.eout_off + (ok[j] ? n + j : 0);
-        no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f;
-        if (tmix) to[j] = tnoise[oi];
-      }
-      if (tmix) ti = tnoise[hin ? ki : 0];
-      if (hin) { nin = fnz(ni); gin = fnz(gi); }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); }
-      if (tmix) {
-        if (hin) tin = fnz(ti);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tout[j] = fnz(to[j]);
-      }
-    }
-    if constexpr (UPD) {
-#if !DQN_ACT_F32
-      // fused fc weight / bias gradient (block-uniform), formed while the item's HBM loads
-      // above are in flight (its X / dH rows are L2-resident)
-      if constexpr (FC) {
-        if (fcj) {
-          OPT_MARK(5);
-          if (elem) fc_bias_grad(jb, g); else fc_tile_grad(jb, g, fx0);
-          OPT_MARK(6);
-        }
-      }
-#endif
-      if (part != nullptr && jb.part_n > 0) {
-        // fixed-order sum of the chunk-group partials (block-uniform branch), 4 loads in flight
-        float pv[4];
-        ld(part, jb.part_off, g);
-#pragma unroll 4
-        for (int p = 1; p < jb.part_n; ++p) {
-          ld(part, jb.part_off + (int64_t)p * jb.part_stride, pv);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) g[j] += pv[j];
-        }
-      } else if (!fcj) {
-        ld(G, mo, g);
-      }
-    }
-    // ---- update
-    if constexpr (UPD) {
-      if constexpr (NZ && DG) {                           // dL/dsigma from the mu-slot gradient
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gs[j] = ok[j] ? g[j] * gin * gout[j] : 0.f;
-      }
-      upd4<OP>(w, g, a, b, e0, h.reg_end, h, lr_t, ok);
-      st(W, mo, w);
-      if constexpr (ONE) st(S0, mo, a);
-      if constexpr (TWO) if (wtwo) st(S1, mo, b);
-      if (sync) st(tgt, mo, w);
-      if constexpr (NZ) {
-        upd4<OP>(ws, gs, as, bs, so + d0, h.reg_end, h, lr_t, ok);
-        st(W, so, ws);
-        if constexpr (ONE) st(S0, so, as);
-        if constexpr (TWO) if (wtwo) st(S1, so, bs);
-        if (sync) st(tgt, so, ws);
-      }
-    }
-    // ---- effective values (noisy: mu + sigma f(eps_in) f(eps_out)) of this net and, tmix,
-    //      of the TARGET under its own next noise sample
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      e[j] = w[j];
-      if constexpr (NZ) e[j] = w[j] + ws[j] * nin * nout[j];
-    }
-    if (tmix) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float mu = sync ? w[j] : tw[j];
-        te[j] = mu;
-        if constexpr (NZ) te[j] = mu + (sync ? ws[j] : tws[j]) * tin * tout[j];
-      }
-      if (jb.eff) st(teff, mo, te);
-    }
-    if (jb.eff) st(eff, mo, e);
-    if (elem) {
-      if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
-        float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
-        float* tf = psync ? reinterpret_cast<float*>(tgt_packed + jb.fwd_off) + n : nullptr;
-        float* mf = tmix ? reinterpret_cast<float*>(tpk + jb.fwd_off) + n : nullptr;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (!ok[j]) continue;
-          pf[j] = e[j];
-          if (tf) tf[j] = e[j];
-          if (mf) mf[j] = te[j];
-        }
-      }
-      return;                      // uniform per block: no barrier below is skipped unevenly
-    }
-    // bf16 fragments of this tile into dst (+ dst2): dgrad straight from the registers (4
-    // consecutive K' of one lane's slot), forward after a 4x4 transpose inside each lane quad
-    auto emit = [&](const float* ev, act_t* dst, act_t* dst2, bool dgrad) {
-      float x[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = ok[j] ? ev[j] : 0.f;
-      if (dgrad && jb.dg_mode != 0 && rowok && n < jb.N) {
-        bfx4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (act_t)x[j];
-        int kp, np;                                        // K' of the first of the 4 values, N'
-        if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
-        else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
-        const int lane = ((kp & 31) >> 3) * 16 + (np & 15);
-        const int64_t o = jb.dg_off +
-                          ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8 +
-                          (kp & 7);
-        *reinterpret_cast<bfx4*>(dst + o) = v;
-        if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = v;
-      }
-      quad_transpose4(x);          // lane: column (n - q) + q, rows 4 * half .. + 3 of its quad
-      const int l = t & 63, q = l & 3, half = (l >> 2) & 1, rg = (t >> 6) >> 1;
-      const int col = n + q;       // n: this lane's first column before the transpose (quad-uniform)
-      if ((col & ~15) < jb.N) {    // n-tile exists (columns past N inside it are zeros)
-        bfx4 f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] = (act_t)x[j];
-        const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
-                                                  (col >> 4)) * 64 + rg * 16 + (col & 15)) * 8 + half * 4;
-        *reinterpret_cast<bfx4*>(dst + o) = f;
-        if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = f;
-      }
-    };
-    OPT_MARK(7);
-    emit(e, packed, psync ? tgt_packed : nullptr, true);
-    if (tmix) emit(te, tpk, nullptr, false);              // (the target runs forward only)
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  auto run = [&](int ji) {
-    const UpdJob jb = jobs[ji];
-    const bool nz = NZOK && jb.sig_off >= 0;
-    // float4 rows: 16-byte aligned tensor (and sigma) offsets and a row / chunk length % 4 == 0
-    const bool al = ((jb.src_off | (nz ? jb.sig_off : 0)) & 3) == 0 && ((jb.kind == 1 ? jb.K : jb.N) & 3) == 0;
-    if (!nz) {
-      if (al) item(jb, T_{}, F_{}, F_{}); else item(jb, F_{}, F_{}, F_{});
-    } else if constexpr (NZOK) {
-      if (gnoise != nullptr) {
-        if (al) item(jb, T_{}, T_{}, T_{}); else item(jb, F_{}, T_{}, T_{});
-      } else {
-        if (al) item(jb, T_{}, T_{}, F_{}); else item(jb, F_{}, T_{}, F_{});
-      }
-    }
-  };
-  if constexpr (FC) {
-    // one job per block (the launcher sizes the grid for it): no job loop, so no per-thread loop
-    // invariants are hoisted and kept live across the fc barriers
-    if (!sampler && wid < njobs) run(wid);
-  } else {
-    for (int ji = sampler ? njobs : wid; ji < njobs; ji += nwork) run(ji);
-  }
-  OPT_MARK(2);
-  if (!UPD) return;
-  // ---- end-of-launch bookkeeping (global_step, Adam beta powers, noise counter / copy) once
-  //      every block has consumed the old values. Block 0 (the sampler block, or the first work
-  //      block) does it: every other block makes ONE no-return arrival add on one of 16 counters
-  //      (blockIdx & 15, own 128-byte lines) and exits at once -- no returned atomic keeps its CU
-  //      slot (measured: a returning ticket per block cost Rainbow's 1714-block launch ~5 us) --
-  //      while lanes 0..15 of block 0 poll the counters. Nothing waits on block 0, so the wait
-  //      always ends (bounded anyway: a lost arrival flags ticket[kErrFlag] instead of hanging).
-  int32_t* cnt = ticket + kTicketStride;
-  if (blockIdx.x != 0) {
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(cnt + kTicketStride * (blockIdx.x & (kTicketSubs - 1)), 1, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (threadIdx.x < kTicketSubs) {
-    const int j = threadIdx.x;
-    const int want = ((int)gridDim.x - j + kTicketSubs - 1) / kTicketSubs - (j == 0 ? 1 : 0);
-    int32_t* c = cnt + kTicketStride * j;
-    int spins = 0;
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++spins > (1 << 22)) {                          // >> any launch: flag, do not hang
-        ticket[kErrFlag] = 1;
-        break;
-      }
-    }
-    __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  OPT_MARK(3);
-  if (threadIdx.x == 0) {
-    if (step) step[0] += 1;
-    if constexpr (OP == 3) {
-      beta_pow[0] *= h.b1;
-      beta_pow[1] *= h.b2;
-    }
-    if (noise_rng != nullptr) noise_rng[1] += 1;        // (the drawing launch completed before this one)
-  }
-  // every other block consumed gnoise before its arrival add: block 0 may overwrite it now --
-  // float4 pieces, every load of a round issued before its stores (a load -> store chain per
-  // element cost Rainbow's launch ~6.5 us at its end: 15.6k cycles for ~8.7k floats)
-  if (noise_dst != nullptr) {
-    const bool al16 = ((reinterpret_cast<uintptr_t>(noise) | reinterpret_cast<uintptr_t>(noise_dst)) & 15) == 0;
-    const int n4 = al16 ? noise_n >> 2 : 0, tid = (int)threadIdx.x, nt = (int)blockDim.x;
-    const float4* s4 = reinterpret_cast<const float4*>(noise);
-    float4* d4 = reinterpret_cast<float4*>(noise_dst);
-    constexpr int kU = 8;
-    for (int base = 0; base < n4; base += kU * nt) {
-      float4 v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) v[u] = s4[min(base + u * nt + tid, n4 - 1)];     // (clamped: no branch)
-#pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (base + u * nt + tid < n4) d4[base + u * nt + tid] = v[u];
-    }
-    for (int i = 4 * n4 + tid; i < noise_n; i += nt) noise_dst[i] = noise[i];
-  }
-  OPT_MARK(4);
-#undef OPT_MARK
-}
-
 // target <- tau * online + (1 - tau) * target, optionally only when step % freq == 0.
 __global__ void __launch_bounds__(256)
 target_update_kernel(float* __restrict__ dst, const float* __restrict__ src, float tau,
@@ -718,6 +102,17 @@ __global__ void step_bump_kernel(int64_t* step) { step[0] += 1; }
 
 using namespace dqn;
 
+// The probe buffer of DQN_OPT_PROF=1 runs (scripts/probe_optim.py, probe_split.py): allocated at the
+// first launch (eager, before any capture); nullptr otherwise.
+static int64_t* optim_prof_buffer() {
+  static int64_t* buf = nullptr;
+  static const bool on = getenv("DQN_OPT_PROF") != nullptr && atoi(getenv("DQN_OPT_PROF")) != 0;
+  if (on && buf == nullptr &&
+      hipMalloc(&buf, (kProfPhases + 3 * (size_t)kTlBlocks + 8 * (size_t)kTilePhBlocks) * sizeof(int64_t)) != hipSuccess)
+    buf = nullptr;
+  return buf;
+}
+
 static int grid_for(int n4) {
   int g = (n4 + 255) / 256;
   return g < 1 ? 1 : (g > 2048 ? 2048 : g);
@@ -737,7 +132,7 @@ void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
-  h.nt = 0;
+  h.prof = nullptr;
   const int n4 = n / 4;
   dim3 grid(grid_for_ticket(n4)), block(256);
   switch (op) {
@@ -758,56 +153,79 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq,
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
                        int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
-                       void* tpk, int64_t* noise_rng, const FcFuse* fc, const float* part, hipStream_t st) {
-  OptHP h;
+                       void* tpk, int64_t* noise_rng, const FcFuse* fc, const float* part, const void* wg,
+                       int wg_blocks, int wg_jobs, hipStream_t st) {
+  OptPackLaunch L{};
+  OptHP& h = L.h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
-  static const int nt_env = getenv("DQN_OPT_NT") ? atoi(getenv("DQN_OPT_NT")) : 0;
-  h.nt = nt_env;
-  static const int prof_env = getenv("DQN_OPT_PROF") ? atoi(getenv("DQN_OPT_PROF")) : 0;
-  h.prof = prof_env;
+  h.prof = optim_prof_buffer();
   // one block per job up to max_grid (grid-stride beyond it); block 0 (+1 sampler block when the
   // launch draws the next minibatch) closes the launch once every other block has arrived
   const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};
   // (the FC modes run exactly one job per block)
   const int cap = ff.x != nullptr ? (njobs > 256 ? njobs : 256) : (max_grid > 256 ? max_grid : 256);
-  const TrunkSample sm = smp != nullptr ? *smp : TrunkSample{};
-  const PerStep pe = per != nullptr ? *per : PerStep{};
-  const int grid = (njobs < cap ? njobs : cap) + (sm.size != nullptr || pe.sum != nullptr ? 1 : 0);   // + sampler
-  const UpdJob* J = reinterpret_cast<const UpdJob*>(jobs);
-  act_t* P = reinterpret_cast<act_t*>(packed);
-  act_t* TP = reinterpret_cast<act_t*>(tgt_packed);
-  const int tf = tfreq < 1 ? 1 : tfreq;
+  L.smp = smp != nullptr ? *smp : TrunkSample{};
+  L.per = per != nullptr ? *per : PerStep{};
+  // WG: the launch also computes the grouped weight gradients (tiles after the lead block)
+  const bool wgm = wg != nullptr && ff.x != nullptr && op >= 0;
+  if (wg != nullptr && !wgm) return;      // (binding checks: a WG launch needs FcFuse rows and an update)
+  if (wgm) njobs = wg_jobs;               // (the rest of the table: jobs the weight-gradient tiles run)
+  // + the lead block (sampler / closer) + the weight-gradient tiles
+  L.grid = (njobs < cap ? njobs : cap) + (L.smp.size != nullptr || L.per.sum != nullptr || wgm ? 1 : 0) +
+           (wgm ? wg_blocks : 0);
   // (a noisy net always passes its noise sample; plain nets pass none)
-  const int mode = (noise != nullptr ? kModeNoisy : 0) | (tnoise != nullptr ? kModeTmix : 0) |
-                   (pe.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0);
-#define OPM(N, M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(grid), dim3(kPackThreads), 0, st, w, g, s0, s1, \
-                       beta_pow, step, ticket, h, J, njobs, P, tgt, TP, tf, noise, eff, gnoise, noise_dst, noise_n, \
-                       sm, pe, tnoise, teff, reinterpret_cast<act_t*>(tpk), noise_rng, ff, part)
+  L.mode = (noise != nullptr ? kModeNoisy : 0) | (tnoise != nullptr ? kModeTmix : 0) |
+           (L.per.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0) | (wgm ? kModeWg : 0);
+  // few work blocks (16-bit builds, the common optimizers): no spills, returning-ticket close
+  L.few = !DQN_ACT_F32 && !wgm && ff.x == nullptr && njobs <= 256 && (op == 0 || op == 3 || op == 7);
 #if DQN_ACT_F32
-#define OPK(N) do { switch (mode) { \
-    case 0: OPM(N, 0); break; case 1: OPM(N, 1); break; case 3: OPM(N, 3); break; \
-    case 4: OPM(N, 4); break; case 5: OPM(N, 5); break; default: OPM(N, 7); break; } } while (0)
+  L.dyn = 0;
 #else
-#define OPK(N) do { switch (mode) { \
-    case 0: OPM(N, 0); break; case 1: OPM(N, 1); break; case 3: OPM(N, 3); break; \
-    case 4: OPM(N, 4); break; case 5: OPM(N, 5); break; case 7: OPM(N, 7); break; \
-    case 8: OPM(N, 8); break; case 9: OPM(N, 9); break; case 11: OPM(N, 11); break; \
-    case 12: OPM(N, 12); break; case 13: OPM(N, 13); break; default: OPM(N, 15); break; } } while (0)
+  L.dyn = wgm ? (size_t)kFusedWgLds : 0;
 #endif
+  L.st = st;
+  L.w = w; L.g = g; L.s0 = s0; L.s1 = s1; L.beta_pow = beta_pow; L.step = step; L.ticket = ticket;
+  L.jobs = reinterpret_cast<const UpdJob*>(jobs); L.njobs = njobs;
+  L.packed = reinterpret_cast<act_t*>(packed); L.tgt = tgt; L.tgt_packed = reinterpret_cast<act_t*>(tgt_packed);
+  L.tfreq = tfreq < 1 ? 1 : tfreq;
+  L.noise = noise; L.eff = eff; L.gnoise = gnoise; L.noise_dst = noise_dst; L.noise_n = noise_n;
+  L.tnoise = tnoise; L.teff = teff; L.tpk = reinterpret_cast<act_t*>(tpk); L.noise_rng = noise_rng; L.ff = ff;
+  L.part = part; L.wg = reinterpret_cast<const WgradGroup*>(wg); L.wg_blocks = wgm ? wg_blocks : 0;
   switch (op) {
-    case -1: OPM(-1, kModeNoisy); break;     // mix + pack only (noisy nets)
-    case 0: OPK(0); break; case 1: OPK(1); break; case 2: OPK(2); break; case 3: OPK(3); break;
-    case 4: OPK(4); break; case 5: OPK(5); break; case 6: OPK(6); break; case 7: OPK(7); break;
+    case -1: optim_pack_op<-1>(L); break;
+    case 0: optim_pack_op<0>(L); break;
+    case 1: optim_pack_op<1>(L); break;
+    case 2: optim_pack_op<2>(L); break;
+    case 3: optim_pack_op<3>(L); break;
+    case 4: optim_pack_op<4>(L); break;
+    case 5: optim_pack_op<5>(L); break;
+    case 6: optim_pack_op<6>(L); break;
+    case 7: optim_pack_op<7>(L); break;
     default: break;
   }
-#undef OPM
-#undef OPK
 }
 
 int upd_job_ints() { return (int)(sizeof(UpdJob) / sizeof(int)); }
-void optim_prof_read(int64_t* out16) { (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_opt_prof), 16 * sizeof(int64_t)); }
+void optim_prof_read(int64_t* out16) {
+  int64_t* b = optim_prof_buffer();
+  if (b != nullptr) (void)hipMemcpy(out16, b, kProfPhases * sizeof(int64_t), hipMemcpyDeviceToHost);
+}
+int optim_tile_phases_read(int64_t* out, int nblocks) {
+  int64_t* b = optim_prof_buffer();
+  nblocks = b == nullptr ? 0 : (nblocks < kTilePhBlocks ? nblocks : kTilePhBlocks);
+  if (nblocks > 0)
+    (void)hipMemcpy(out, b + kProfPhases + 3 * kTlBlocks, 8 * (size_t)nblocks * sizeof(int64_t), hipMemcpyDeviceToHost);
+  return nblocks;
+}
+int optim_timeline_read(int64_t* out, int nblocks) {
+  int64_t* b = optim_prof_buffer();
+  nblocks = b == nullptr ? 0 : (nblocks < kTlBlocks ? nblocks : kTlBlocks);
+  if (nblocks > 0)
+    (void)hipMemcpy(out, b + kProfPhases, 3 * (size_t)nblocks * sizeof(int64_t), hipMemcpyDeviceToHost);
+  return nblocks;
+}
 int optim_fc_fuse() { return DQN_ACT_F32 ? 0 : 1; }
 
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,

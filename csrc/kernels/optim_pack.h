@@ -1,0 +1,818 @@
+// Fused multi-tensor optimizer + weight packing kernel (optim_pack_kernel) and its launch
+// descriptor. Included by optim.hip (launchers) and by the optim_ops_*.hip translation units,
+// which instantiate it per optimizer (DQN_OPTIM_DEFINE_OPS) so the build compiles them in parallel.
+//
+// Reference: tf.train.{GradientDescent,Momentum,RMSProp,Adam,Adagrad,Adadelta,Ftrl}
+// Optimizer.minimize() colocated with the variables on the parameter server
+// (/root/reference/src/network.py:159-203) -- one ApplyX op per variable plus the separate L2
+// term in the loss (network.py:151-152,311,407).
+#pragma once
+#include <stdlib.h>
+#include <type_traits>
+#include "common.h"
+#include "sample_dev.h"
+#include "sumtree_dev.h"
+#include "wgrad_dev.h"
+#include "../include/dqn_kernels.h"
+
+namespace dqn {
+
+struct OptHP {
+  float lr, reg, grad_scale;
+  float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
+  int reg_end;
+  // probe launches only (DQN_OPT_PROF=1, nullptr otherwise): [0, 16) s_memtime phase stamps of
+  // blocks 0 and 1, then per block [start, ready, end] s_memrealtime (100 MHz) for blocks < kTlBlocks
+  // (ready: a dependent job's wait is over / the sampler's draw is done)
+  int64_t* prof;
+};
+constexpr int kProfPhases = 16, kTlBlocks = 4096, kTilePhBlocks = 512;   // (+ [8] tile phases per wgrad block)
+
+// Contraction is pinned off in the update math so every kernel that inlines it
+// (optim_kernel's float4 loop, optim_pack_kernel's tiles) rounds identically:
+// with fp-contract=fast the backend fuses differently per call site.
+DQN_DEV float opt_grad(float g, float w, bool reg, const OptHP& h) {
+#pragma clang fp contract(off)
+  float x = g * h.grad_scale;
+  if (reg) x += h.reg * w;
+  return x;
+}
+
+template <int OP>
+DQN_DEV void update_one(float& w, float g, float& s0, float& s1, const OptHP& h, float lr_t) {
+#pragma clang fp contract(off)
+  if constexpr (OP == 0) {            // sgd
+    w -= h.lr * g;
+  } else if constexpr (OP == 1) {     // momentum (non-Nesterov)
+    s0 = h.momentum * s0 + g;
+    w -= h.lr * s0;
+  } else if constexpr (OP == 2) {     // rmsprop: ms (init 1), mom
+    s0 = h.rho * s0 + (1.f - h.rho) * g * g;
+    s1 = h.rms_mom * s1 + h.lr * g / sqrtf(s0 + h.rms_eps);
+    w -= s1;
+  } else if constexpr (OP == 7) {     // rmsprop with momentum 0 (the TF / reference default):
+    s0 = h.rho * s0 + (1.f - h.rho) * g * g;   // mom = 0 * mom + u == u exactly, so mom is
+    s1 = h.lr * g / sqrtf(s0 + h.rms_eps);     // written (checkpoint slot) but never read
+    w -= s1;
+  } else if constexpr (OP == 3) {     // adam (TF epsilon-hat form)
+    s0 = h.b1 * s0 + (1.f - h.b1) * g;
+    s1 = h.b2 * s1 + (1.f - h.b2) * g * g;
+    w -= lr_t * s0 / (sqrtf(s1) + h.adam_eps);
+  } else if constexpr (OP == 4) {     // adagrad (accumulator init 0.1)
+    s0 += g * g;
+    w -= h.lr * g / sqrtf(s0);
+  } else if constexpr (OP == 5) {     // adadelta
+    s0 = h.ad_rho * s0 + (1.f - h.ad_rho) * g * g;
+    const float upd = sqrtf(s1 + h.ad_eps) / sqrtf(s0 + h.ad_eps) * g;
+    s1 = h.ad_rho * s1 + (1.f - h.ad_rho) * upd * upd;
+    w -= h.lr * upd;
+  } else {                            // ftrl (lr_power -0.5, l1 = l2 = 0)
+    const float na = s0 + g * g;
+    s1 += g - (sqrtf(na) - sqrtf(s0)) / h.lr * w;
+    const float quad = sqrtf(na) / h.lr;
+    w = fabsf(s1) > 0.f ? -s1 / quad : 0.f;
+    s0 = na;
+  }
+}
+
+// ------------------------------------------------------------- update + pack
+// The optimizer step fused with the executor's weight packing: a 512-thread workgroup
+// owns a 32 (k) x 64 (n) tile of a weight matrix (TF layout [K][N]), each thread 4
+// consecutive n of one row (one float4 per operand: few VGPRs, high occupancy). It
+// updates the tile in registers, writes fp32 weights + slots back, and emits the tile's
+// bf16 MFMA fragments straight away:
+//   * forward fragments ([K/32][N/16][64][8]: 8 consecutive k per lane): a wave owns an
+//     8 (k) x 32 (n) sub-tile with lane = 8 * col-group + row, so the 4 lanes of a quad hold
+//     4 consecutive rows x the same 4 columns; one 4x4 DPP transpose per quad leaves each
+//     lane 4 consecutive k of one column = half of a fragment slot, stored directly (no LDS
+//     round trip, no barrier; the LDS transpose it replaces ran at ~40% bank conflicts);
+//   * dgrad fragments (dense transpose, or conv (tap, co) x ci) directly from the
+//     thread's registers: its 4 consecutive K' ARE 4 consecutive n of one row (half
+//     of one lane's 8-value slot).
+// Elementwise items (biases, ...) carry an optional fp32 copy into the packed
+// buffer (the concatenated fc bias). Same ticket as optim_kernel; the hard target
+// sync writes the target's fp32 master and packed fragments under the predicate.
+typedef __attribute__((ext_vector_type(4))) act_t bfx4;
+
+constexpr int kTicketSubs = 16, kTicketStride = 32;    // sharded arrival counters: int32 words, 128 B apart
+constexpr int kPackThreads = 512;
+// ticket[kSlotFlag] != 0: momentum-0 RMSProp also stores its `mom` slot this step. That slot
+// (mom = 0 * mom + update) is never read by the update, only saved under its TF name, so the
+// hot path skips its 4 bytes / parameter and the checkpoint manager raises the flag for the
+// step before a save (optim.py Optimizer.request_slots).
+constexpr int kSlotFlag = 1;
+// ticket[kErrFlag] != 0: an optim_pack launch's end-of-launch wait gave up (lost arrival; never
+// expected -- the learner's periodic check reads it)
+constexpr int kErrFlag = 2;
+
+#if !DQN_ACT_F32
+// Fused fc weight gradient (FcFuse): a 32 (k) x 64 (n) update tile's dW = X^T dH over M rows,
+// 32-row chunks staged ROW-major in LDS (strides + 16 elements: conflict-free transposed reads,
+// as the grouped wgrad), wave w owning the 16 x 16 sub-tile (k: w >> 2, n: w & 3) as dW^T =
+// dH^T X on one v_mfma_f32_16x16x32 per chunk (lane: one k, 4 consecutive n), then through
+// an fp32 LDS tile into the update's own thread map (row r, 4 consecutive n).
+constexpr int kFcSX = 32 + 16, kFcSH = 64 + 16, kFcRS = 64 + 4;
+constexpr int kFcLds = 32 * kFcRS * 4;          // >= staging (32 * (SX + SH) * 2 B) and 4 x 512 fp32
+static_assert(32 * (kFcSX + kFcSH) * 2 <= kFcLds && 4 * 512 * 4 <= kFcLds, "fc LDS plan");
+#endif
+
+#if !DQN_ACT_F32
+// dynamic LDS of a WG launch: the largest fused weight-gradient tile and the FcFuse staging
+constexpr int kFusedWgLds = (int)WgradTile<kFusedWgMC, 64, 64>::lds_bytes > kFcLds ? (int)WgradTile<kFusedWgMC, 64, 64>::lds_bytes
+                                                                                    : kFcLds;
+static_assert(kFusedWgLds <= 40 * 1024, "WG launch LDS: 4 blocks / CU");
+static_assert((int)WgradTile<64, 64, 64>::lds_bytes <= kFusedWgLds && (int)WgradTile<kFusedWgMC, 64, 32>::lds_bytes <= kFusedWgLds,
+              "every fused tile fits");
+#endif
+
+struct UpdJob {
+  int kind;                      // 0 = tile, 1 = elementwise chunk
+  int src_off, K, N, k0, n0;     // tile: tensor offset / shape / origin; elem: offset, count (K)
+  int fwd_off, fwd_N16, fwd_nt_off, fwd_ks_off;   // forward fragments (elem: fp32 copy offset or -1)
+  int dg_mode, dg_off, dg_N16, dg_nt_off, dg_ks_off, dg_cin;   // dgrad: 0 none, 1 conv, 2 dense
+  // noisy nets (factorised Gaussian): the sigma tensor is updated in the same thread as mu
+  // and the packed / eff values are mu + sigma * f(noise[ein + k]) f(noise[eout + n])
+  // (ein < 0: f = 1, biases; elem chunks: eout already offset to the chunk start)
+  int sig_off, ein_off, eout_off;
+  int eff;                       // 1: also store the effective fp32 value at eff[src index]
+  // fc weight tile / fc bias chunk whose gradient the launch forms from FcFuse rows: the
+  // tensor's first column in dH (-1: read the flat gradient)
+  int fc_col;
+  // WG launches: the gradient is produced by weight-gradient member `dep` of this launch (-1:
+  // final at launch start); the block waits for that member's done counter first
+  int dep;
+  // gradient = sum of part_n partial slices (the grouped conv wgrad's deterministic chunk-group
+  // sums, qnet.hip): element d of the tensor at part[part_off + p * part_stride + d], p ascending
+  int part_off, part_n, part_stride;
+};
+
+DQN_DEV float fnz(float x) { return copysignf(sqrtf(fabsf(x)), x); }
+
+template <int OP>
+DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, int reg_end, const OptHP& h,
+                  float lr_t, const bool* ok) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!ok[j]) continue;
+    update_one<OP>(w[j], opt_grad(g[j], w[j], k0flat + j < reg_end, h), a[j], b[j], h, lr_t);
+  }
+}
+
+// MODE bits: kModeNoisy (noisy jobs in the work list), kModeTmix (+ the target's mix + pack),
+// kModePer (the sampler block runs the prioritized sum-tree path). Paths a mode excludes are
+// not instantiated: their registers would cost the plain nets occupancy (mode 0: 8 waves / SIMD,
+// so every block of the Nature-CNN work list is resident at once).
+// kModeFc: some jobs form their gradient from FcFuse rows (16-bit builds).
+// kModeWg (16-bit builds): the launch also computes the grouped weight gradients. Grid: [the lead
+// block: sampler + closer] [the WgradGroup's tiles (device memory, wgrad_dev.h)] [the jobs whose
+// gradient is final at launch start: the fc layers, from FcFuse rows]. Each tile, once its fp32
+// atomics have completed, adds to its (member, K-range) counter (and, K-range 0, the member's bias
+// counter); the tile whose add completes a count acquires (agent scope) and runs the optimizer
+// jobs of those rows itself (WgradGroup dep ranges of the job table, past the block-assigned
+// jobs). Nothing waits while holding a CU slot, except the sampler block: it writes the next
+// minibatch's frame-slot tables only after the member reading the current ones (conv1 from the
+// frame ring) is done -- the lowest block id, so every producer it waits for is already resident.
+// LDS: one dynamic buffer (<= 40 KB: 4 blocks / CU, as the plain update).
+// kModeFew: a launch of few work blocks (the second launch of a split update): 4 waves / SIMD
+// (128 VGPRs: no spills in the item body, occupancy is moot) and a returning arrival ticket per
+// block -- the last block to arrive closes the launch, nobody polls.
+constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8, kModeWg = 16, kModeFew = 32;
+template <int OP, int MODE>
+__global__ void __launch_bounds__(kPackThreads, (MODE & kModeFew) ? 4 : (MODE & ~(kModeFc | kModeWg)) == 0 ? 8 : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
+                  float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
+                  const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
+                  act_t* __restrict__ tgt_packed, int tfreq, const float* __restrict__ noise,
+                  float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
+                  int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
+                  float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff,
+                  const float* __restrict__ part, const WgradGroup* __restrict__ wg, int wg_blocks) {
+  // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
+  // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
+  // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
+  // noise on every DP rank makes that exact for the all-reduced sum), instead of being read.
+  // noise_dst: the grid's last block copies noise[0, noise_n) there (next sample -> current).
+  // smp.size != nullptr: the grid's extra block (block 0) draws the NEXT step's uniform minibatch
+  // (sample_dev.h) while the others update: the replay is quiet during this launch, and
+  // the sampler leaves the next step's critical path.
+  // tnoise (noisy nets, update calls): also mix + pack the TARGET under its next noise
+  // sample into teff / tpk (the target's eff / packed buffers): no separate target mix launch.
+  constexpr bool UPD = OP >= 0;
+  constexpr bool TMIX = (MODE & kModeTmix) != 0, NZOK = (MODE & kModeNoisy) != 0, PEROK = (MODE & kModePer) != 0;
+  constexpr bool FC = (MODE & kModeFc) != 0 && !DQN_ACT_F32 && OP >= 0;
+  constexpr bool WG = (MODE & kModeWg) != 0 && !DQN_ACT_F32 && OP >= 0;
+  constexpr bool FEW = (MODE & kModeFew) != 0 && OP >= 0;
+  // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
+  const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
+  // LDS: the sampler block's scratch (the update items exchange through DPP); WG launches carve
+  // everything (weight-gradient staging, FcFuse staging) from the dynamic buffer instead
+  constexpr size_t kSmpLds = sizeof(SampleLds) > sizeof(SumtreeLds) ? sizeof(SampleLds) : sizeof(SumtreeLds);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[WG ? 16 : kSmpLds];
+  extern __shared__ __attribute__((aligned(16))) unsigned char opt_dyn[];
+  int64_t* tl = (h.prof != nullptr && threadIdx.x == 0 && blockIdx.x < kTlBlocks) ? h.prof + kProfPhases + 3 * blockIdx.x
+                                                                                    : nullptr;
+  if (tl) { tl[0] = (int64_t)__builtin_amdgcn_s_memrealtime(); tl[1] = 0; tl[2] = 0; }
+  // block 0 leads (the sampler when the launch draws the next minibatch; always in WG launches,
+  // whose block 0 then only closes the launch)
+  const bool smp_on = smp.size != nullptr || per.sum != nullptr;
+  const bool extra = smp_on || WG;
+  const int wg0 = WG ? wg_blocks : 0;
+  int32_t* cnt = ticket + kTicketStride;        // end-of-launch arrival counters (see the closing step)
+  // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
+  const bool sampler = smp_on && blockIdx.x == 0;
+  const int nwork = (int)gridDim.x - (extra ? 1 : 0) - wg0;
+  const int wid = (int)blockIdx.x - (extra ? 1 : 0) - wg0;      // work index of an update block
+  float lr_t = h.lr;
+  if constexpr (OP == 3) {
+    const float b1p = beta_pow[0], b2p = beta_pow[1];
+    lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  }
+  const bool sync = UPD && tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  const bool psync = sync && tgt_packed != nullptr;
+  constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7;   // second slot written
+  const bool wtwo = OP != 7 || ticket[kSlotFlag] != 0;                         // (momentum-0 RMSProp: flagged)
+  constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
+  constexpr bool ONE = UPD && OP != 0;
+  const int t = threadIdx.x;
+  int64_t* prof = (h.prof != nullptr && t == 0 && blockIdx.x < 2) ? h.prof + 8 * blockIdx.x : nullptr;
+#define OPT_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
+  OPT_MARK(0);
+  // WG: thread 0 polls member m's done counter (bounded: a lost arrival flags the error word
+  // instead of hanging), then acquires; the caller's barrier releases the block's other waves
+  auto wg_wait = [&](int m) {
+#if !DQN_ACT_F32
+    if (m < 0 || threadIdx.x != 0) return;
+    const int32_t* dc = wg->done + kTicketStride * m;
+    const int want = wg->nblk[m];
+    int spins = 0;
+    while (__hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 23)) {
+        ticket[kErrFlag] = 1;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tl) tl[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#else
+    (void)m;
+#endif
+  };
+  if (PEROK && sampler && per.sum != nullptr) {
+    // prioritized: this step's priorities into the tree (one wave), then the next step's
+    // stratified sample from the updated tree (beta of the NEXT global_step)
+    const int64_t step0 = per.step[0];                  // read before this block's ticket add
+    const uint64_t seed = (uint64_t)per.rng[0], ctr = (uint64_t)per.rng[1];
+    SumtreeLds& L = *reinterpret_cast<SumtreeLds*>(smem);
+    int ins_first = 0;
+    if (per.ins_n > 0) ins_first = (int)((per.ins_cursor[0] - per.ins_n + per.ins_cap) % per.ins_cap);
+    sumtree_update_wave(per.sum, per.mn, per.maxp, per.upd_idx, per.upd_td, per.alpha, per.eps, 0, per.B, per.P,
+                        per.levels, L, 0, 1, per.ins_n, ins_first, per.ins_cap);
+    if constexpr (WG) wg_wait(wg->slots_member);        // (the current slot tables' reader is done)
+    __syncthreads();                                    // tree writes visible to every lane of the block
+    if ((int)threadIdx.x < per.B) {
+      const float beta = fminf(1.f, per.beta0 + (1.f - per.beta0) * (float)(step0 + 1) / per.beta_steps);
+      per_sample_lane(per.sum, per.mn, seed, ctr, per.size[0], threadIdx.x, per.B, per.P, beta, per.idx_out,
+                      per.w_out, per.so);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) per.rng[1] = (int64_t)(ctr + 1);
+  } else if (sampler) {
+    SampleLds& sls = *reinterpret_cast<SampleLds*>(smem);
+    const uint32_t n = (uint32_t)max(smp.size[0], 1);
+    const uint64_t seed = (uint64_t)smp.rng[0], ctr = (uint64_t)smp.rng[1];
+    const int32_t v = draw_distinct(seed, ctr, n, smp.B, sls);
+    if constexpr (WG) {
+      wg_wait(wg->slots_member);                        // (the current slot tables' reader is done)
+      __syncthreads();
+    }
+    if ((int)threadIdx.x < smp.B) {
+      DQN_ASSERT(v >= 0 && (uint32_t)v < n);
+      write_sample_slots(smp, threadIdx.x, v, reinterpret_cast<const int4*>(smp.state_idx)[v], smp.next_idx[v]);
+    }
+    if (threadIdx.x == 0) smp.rng[1] = (int64_t)(ctr + 1);   // every lane read it before the barriers
+    if (tl) tl[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
+  OPT_MARK(1);
+#if !DQN_ACT_F32
+  __shared__ __attribute__((aligned(16))) unsigned char fcl_s[FC && !WG ? kFcLds : 16];
+  unsigned char* fcl = WG ? opt_dyn : fcl_s;
+  // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
+  // this thread's 8-element piece of fc operand rows m0 .. m0 + 31 of the item's 32 (k) x 64 (n)
+  // tile: t < 128 a piece of an x row, 128 <= t < 384 one of a dh row
+  auto fc_load = [&](const UpdJob& jb, int m0) {
+    const bool lx = t < 128, lh = t >= 128 && t < 384;
+    const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
+    const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
+    const act_t* X = reinterpret_cast<const act_t*>(ff.x);
+    const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
+    const int m = m0 + lr;
+    bfx8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (act_t)0.f;
+    // (32-bit element offsets off the uniform bases: no per-thread 64-bit address kept live)
+    if (m < ff.M) {
+      if (lx && jb.k0 + lc < jb.K)
+        v = *reinterpret_cast<const bfx8*>(X + (uint32_t)(m * ff.ldx + jb.k0 + lc));
+      else if (lh && jb.n0 + lc < jb.N)
+        v = *reinterpret_cast<const bfx8*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + jb.n0 + lc));
+    }
+    return v;
+  };
+  // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows;
+  // v0: this thread's piece of the first 32-row chunk, loaded with the item's HBM batch
+  auto fc_tile_grad = [&](const UpdJob& jb, float* g, bfx8 v0) {
+    act_t* Xs = reinterpret_cast<act_t*>(fcl);           // [32][kFcSX]: x[m][k0 .. k0 + 32)
+    act_t* Hs = Xs + 32 * kFcSX;                         // [32][kFcSH]: dh[m][col + n0 .. + 64)
+    float* R = reinterpret_cast<float*>(fcl);            // [32][kFcRS] fp32 dW tile (after the MFMAs)
+    const int wv = t >> 6, lane = t & 63;
+    const int kt = wv >> 2, nt = wv & 3;
+    const bool lx = t < 128, lh = t >= 128 && t < 384;
+    const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
+    const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+    const act_t* ph = Hs + (4 * gq + rq) * kFcSH + nt * 16 + cp;
+    const act_t* px = Xs + (4 * gq + rq) * kFcSX + kt * 16 + cp;
+    for (int m0 = 0; m0 < ff.M; m0 += 32) {
+      const bfx8 v = m0 == 0 ? v0 : fc_load(jb, m0);
+      __syncthreads();                 // previous chunk's operand reads / previous item's R reads done
+      if (lx) *reinterpret_cast<bfx8*>(Xs + lr * kFcSX + lc) = v;
+      else if (lh) *reinterpret_cast<bfx8*>(Hs + lr * kFcSH + lc) = v;
+      __syncthreads();
+      // A = dh^T (rows n), B = x (columns k); the same row permutation on both operands
+      acc = DQN_MFMA16_BUILTIN(join_tr(lds_tr16(ph), lds_tr16(ph + 16 * kFcSH)),
+                               join_tr(lds_tr16(px), lds_tr16(px + 16 * kFcSX)), acc, 0, 0, 0);
+    }
+    __syncthreads();                   // operand reads done before R overwrites the staging
+    // acc[r] = dW[k = kt * 16 + (lane & 15)][n = nt * 16 + 4 * (lane >> 4) + r]
+    *reinterpret_cast<float4*>(R + (kt * 16 + (lane & 15)) * kFcRS + nt * 16 + 4 * (lane >> 4)) =
+        make_float4(acc[0] * kInvLossScale, acc[1] * kInvLossScale, acc[2] * kInvLossScale, acc[3] * kInvLossScale);
+    __syncthreads();
+    const int r = (wv >> 1) * 8 + (lane & 7), c4 = (wv & 1) * 32 + (lane >> 3) * 4;
+    const float4 gv = *reinterpret_cast<const float4*>(R + r * kFcRS + c4);
+    g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
+  };
+  // fc bias chunk (<= 512 values, thread t < 128 owns n = 4t..4t+3): sum_m dh[m][col + n] over 4
+  // row phases, combined in a fixed order
+  auto fc_bias_grad = [&](const UpdJob& jb, float* g) {
+    float* R = reinterpret_cast<float*>(fcl);            // [4][512]
+    const act_t* H = reinterpret_cast<const act_t*>(ff.dh);
+    const int cg = t & 127, ph = t >> 7, c = 4 * cg;
+    float sm[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < jb.K) {
+#pragma unroll 4
+      for (int m = ph; m < ff.M; m += 4) {
+        const bfx4 v = *reinterpret_cast<const bfx4*>(H + (uint32_t)(m * ff.ldh + jb.fc_col + c));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm[j] += (float)v[j];
+      }
+    }
+    __syncthreads();                   // previous item's LDS reads done
+    *reinterpret_cast<float4*>(R + ph * 512 + c) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = (4 * t + j) & 511;
+      g[j] = ((R[i] + R[512 + i]) + (R[1024 + i] + R[1536 + i])) * kInvLossScale;
+    }
+  };
+#endif
+  // One job item = a 32x64 tile (or a 2048-element chunk) updated by 4 consecutive elements per
+  // thread. The body is instantiated per (AL = 16-byte aligned float4 rows, NZ = noisy) so that
+  // every global load of the item (mu / sigma / grad / slots / target / noise factors) is an
+  // UNCONDITIONAL load issued in one batch: out-of-range threads read the job's first element
+  // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
+  // vmcnt wait between loads and serialise the item on memory latency.)
+  auto item = [&](const UpdJob& jb, auto al_c, auto nz_c, auto dg_c) {
+    // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read
+    constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value, DG = decltype(dg_c)::value;
+    const bool elem = jb.kind == 1;
+    float g[4];
+    const bool fcj = FC && jb.fc_col >= 0;
+    bool ok[4];
+    int k, n;                      // row (tile) and column / element index within the tensor
+    bool rowok;
+    int64_t e0;
+    if (elem) {                    // chunk of up to 2048 elements: 4 per thread
+      k = 0;
+      n = 4 * t;
+      rowok = true;
+      e0 = (int64_t)jb.src_off + n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ok[j] = n + j < jb.K;
+    } else {                       // tile: row r, columns c4..c4+3 (wave: 8 rows x 32 columns)
+      const int wv = t >> 6, l = t & 63;
+      const int r = (wv >> 1) * 8 + (l & 7), c4 = (wv & 1) * 32 + (l >> 3) * 4;
+      k = jb.k0 + r;
+      n = jb.n0 + c4;
+      rowok = k < jb.K;
+      e0 = (int64_t)jb.src_off + (int64_t)k * jb.N + n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ok[j] = rowok && n + j < jb.N;
+    }
+    const int64_t d0 = e0 - jb.src_off;                  // offset within the tensor
+    // clamped element indices: AL -> all 4 in range or none (one float4), else per element
+    int64_t ix[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ix[j] = (AL ? ok[0] : ok[j]) ? d0 + j : 0;
+    auto ld = [&](const float* base, int64_t off, float* v) {
+      if constexpr (AL) {
+        const float4 x = *reinterpret_cast<const float4*>(base + off + ix[0]);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = base[off + ix[j]];
+      }
+    };
+    auto st = [&](float* base, int64_t off, const float* v) {
+      if constexpr (AL) {
+        if (ok[0]) {
+          f32x4* p = reinterpret_cast<f32x4*>(base + off + d0);
+          const f32x4 x = {v[0], v[1], v[2], v[3]};
+          *p = x;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (ok[j]) base[off + d0 + j] = v[j];
+      }
+    };
+    const int64_t mo = jb.src_off, so = NZ ? jb.sig_off : jb.src_off;
+    float w[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], tw[4], tws[4], e[4], te[4];
+    // ---- every load of the item, issued before any math
+    ld(W, mo, w);
+    if constexpr (ONE) ld(S0, mo, a);
+    if constexpr (TWO_LD) ld(S1, mo, b);
+    if constexpr (NZ) {
+      ld(W, so, ws);
+      if constexpr (UPD) {
+        if constexpr (!DG) ld(G, so, gs);
+        if constexpr (ONE) ld(S0, so, as);
+        if constexpr (TWO_LD) ld(S1, so, bs);
+      }
+    }
+    // the target's mu / sigma in the same batch (one memory round trip per item: the extra
+    // VGPRs keep the same 2 blocks / CU, the block is 8 waves and the budget 128 VGPRs)
+    if (tmix) {
+      ld(tgt, mo, tw);
+      if constexpr (NZ) ld(tgt, so, tws);
+    }
+    // the fc tile's first 32 operand rows (L2 / MALL) join the batch: fc_tile_grad then waits on
+    // one round trip instead of issuing its own after the batch has drained
+    bfx8 fx0;
+#if !DQN_ACT_F32
+    if constexpr (FC && UPD) {
+      if (fcj && !elem) fx0 = fc_load(jb, 0);
+    }
+#endif
+    // factorised-noise factors (loaded with the item's batch, before the fc gradient: a separate
+    // round trip after it cost Rainbow's items ~1 us each): f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
+    float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
+    float tin = 1.f, tout[4] = {1.f, 1.f, 1.f, 1.f};     // (tmix: the target's next sample)
+    const bool hin = NZ && !elem && jb.ein_off >= 0;
+    const int ki = NZ ? jb.ein_off + (hin && rowok ? k : 0) : 0;     // clamped: always in range
+    if constexpr (NZ) {
+      const float* gn = DG ? gnoise : noise;             // (DG: the sample the forward used)
+      const float ni = noise[hin ? ki : 0], gi = DG ? gn[hin ? ki : 0] : 1.f;
+      float no[4], go[4], to[4] = {1.f, 1.f, 1.f, 1.f}, ti = 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int oi = jb.eout_off + (ok[j] ? n + j : 0);
+        no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f;
+        if (tmix) to[j] = tnoise[oi];
+      }
+      if (tmix) ti = tnoise[hin ? ki : 0];
+      if (hin) { nin = fnz(ni); gin = fnz(gi); }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); }
+      if (tmix) {
+        if (hin) tin = fnz(ti);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tout[j] = fnz(to[j]);
+      }
+    }
+    if constexpr (UPD) {
+#if !DQN_ACT_F32
+      // fused fc weight / bias gradient (block-uniform), formed while the item's HBM loads
+      // above are in flight (its X / dH rows are L2-resident)
+      if constexpr (FC) {
+        if (fcj) {
+          OPT_MARK(5);
+          if (elem) fc_bias_grad(jb, g); else fc_tile_grad(jb, g, fx0);
+          OPT_MARK(6);
+        }
+      }
+#endif
+      if (part != nullptr && jb.part_n > 0) {
+        // fixed-order sum of the chunk-group partials (block-uniform branch), 4 loads in flight
+        float pv[4];
+        ld(part, jb.part_off, g);
+#pragma unroll 4
+        for (int p = 1; p < jb.part_n; ++p) {
+          ld(part, jb.part_off + (int64_t)p * jb.part_stride, pv);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[j] += pv[j];
+        }
+      } else if (!fcj) {
+        ld(G, mo, g);
+      }
+    }
+    // ---- update
+    if constexpr (UPD) {
+      if constexpr (NZ && DG) {                           // dL/dsigma from the mu-slot gradient
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gs[j] = ok[j] ? g[j] * gin * gout[j] : 0.f;
+      }
+      upd4<OP>(w, g, a, b, e0, h.reg_end, h, lr_t, ok);
+      st(W, mo, w);
+      if constexpr (ONE) st(S0, mo, a);
+      if constexpr (TWO) if (wtwo) st(S1, mo, b);
+      if (sync) st(tgt, mo, w);
+      if constexpr (NZ) {
+        upd4<OP>(ws, gs, as, bs, so + d0, h.reg_end, h, lr_t, ok);
+        st(W, so, ws);
+        if constexpr (ONE) st(S0, so, as);
+        if constexpr (TWO) if (wtwo) st(S1, so, bs);
+        if (sync) st(tgt, so, ws);
+      }
+    }
+    // ---- effective values (noisy: mu + sigma f(eps_in) f(eps_out)) of this net and, tmix,
+    //      of the TARGET under its own next noise sample
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      e[j] = w[j];
+      if constexpr (NZ) e[j] = w[j] + ws[j] * nin * nout[j];
+    }
+    if (tmix) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float mu = sync ? w[j] : tw[j];
+        te[j] = mu;
+        if constexpr (NZ) te[j] = mu + (sync ? ws[j] : tws[j]) * tin * tout[j];
+      }
+      if (jb.eff) st(teff, mo, te);
+    }
+    if (jb.eff) st(eff, mo, e);
+    if (elem) {
+      if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
+        float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
+        float* tf = psync ? reinterpret_cast<float*>(tgt_packed + jb.fwd_off) + n : nullptr;
+        float* mf = tmix ? reinterpret_cast<float*>(tpk + jb.fwd_off) + n : nullptr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!ok[j]) continue;
+          pf[j] = e[j];
+          if (tf) tf[j] = e[j];
+          if (mf) mf[j] = te[j];
+        }
+      }
+      return;                      // uniform per block: no barrier below is skipped unevenly
+    }
+    // bf16 fragments of this tile into dst (+ dst2): dgrad straight from the registers (4
+    // consecutive K' of one lane's slot), forward after a 4x4 transpose inside each lane quad
+    auto emit = [&](const float* ev, act_t* dst, act_t* dst2, bool dgrad) {
+      float x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = ok[j] ? ev[j] : 0.f;
+      if (dgrad && jb.dg_mode != 0 && rowok && n < jb.N) {
+        bfx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (act_t)x[j];
+        int kp, np;                                        // K' of the first of the 4 values, N'
+        if (jb.dg_mode == 2) { kp = n; np = k; }           // dense: K' = out (n), N' = in (k)
+        else { const int tap = k / jb.dg_cin, ci = k - tap * jb.dg_cin; kp = tap * jb.N + n; np = ci; }
+        const int lane = ((kp & 31) >> 3) * 16 + (np & 15);
+        const int64_t o = jb.dg_off +
+                          ((int64_t)((jb.dg_ks_off + (kp >> 5)) * jb.dg_N16 + jb.dg_nt_off + (np >> 4)) * 64 + lane) * 8 +
+                          (kp & 7);
+        *reinterpret_cast<bfx4*>(dst + o) = v;
+        if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = v;
+      }
+      quad_transpose4(x);          // lane: column (n - q) + q, rows 4 * half .. + 3 of its quad
+      const int l = t & 63, q = l & 3, half = (l >> 2) & 1, rg = (t >> 6) >> 1;
+      const int col = n + q;       // n: this lane's first column before the transpose (quad-uniform)
+      if ((col & ~15) < jb.N) {    // n-tile exists (columns past N inside it are zeros)
+        bfx4 f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f[j] = (act_t)x[j];
+        const int64_t o = jb.fwd_off + ((int64_t)((jb.fwd_ks_off + (jb.k0 >> 5)) * jb.fwd_N16 + jb.fwd_nt_off +
+                                                  (col >> 4)) * 64 + rg * 16 + (col & 15)) * 8 + half * 4;
+        *reinterpret_cast<bfx4*>(dst + o) = f;
+        if (dst2) *reinterpret_cast<bfx4*>(dst2 + o) = f;
+      }
+    };
+    OPT_MARK(7);
+    emit(e, packed, psync ? tgt_packed : nullptr, true);
+    if (tmix) emit(te, tpk, nullptr, false);              // (the target runs forward only)
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  auto run = [&](int ji) {
+    const UpdJob jb = jobs[ji];
+    const bool nz = NZOK && jb.sig_off >= 0;
+    // float4 rows: 16-byte aligned tensor (and sigma) offsets and a row / chunk length % 4 == 0
+    const bool al = ((jb.src_off | (nz ? jb.sig_off : 0)) & 3) == 0 && ((jb.kind == 1 ? jb.K : jb.N) & 3) == 0;
+    if (!nz) {
+      if (al) item(jb, T_{}, F_{}, F_{}); else item(jb, F_{}, F_{}, F_{});
+    } else if constexpr (NZOK) {
+      if (gnoise != nullptr) {
+        if (al) item(jb, T_{}, T_{}, T_{}); else item(jb, F_{}, T_{}, T_{});
+      } else {
+        if (al) item(jb, T_{}, T_{}, F_{}); else item(jb, F_{}, T_{}, F_{});
+      }
+    }
+  };
+#if !DQN_ACT_F32
+  if constexpr (WG) {
+    const int b = (int)blockIdx.x - 1;
+    if (b >= 0 && b < wg_blocks) {
+      // ---- a weight-gradient tile; the LAST tile of a (member, K-range) -- and of the member's
+      //      bias, for the K-range-0 tiles -- then runs the optimizer jobs of those tensors itself:
+      //      no block waits for a gradient while holding its CU slot
+      int64_t* ph = (h.prof != nullptr && b < kTilePhBlocks) ? h.prof + kProfPhases + 3 * kTlBlocks + 8 * b : nullptr;
+      const int mb = fused_wgrad_block<kPackThreads>(*wg, b, reinterpret_cast<act_t*>(opt_dyn), ph);
+      const int m = mb >> 8, by = mb & 255;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's atomics / write-through stores done
+      if (ph != nullptr && threadIdx.x == 0) ph[7] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      __shared__ int wg_last[2];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        if (tl) { tl[1] = m; tl[2] = (int64_t)__builtin_amdgcn_s_memrealtime(); }
+        const int want = wg->nblk[m] / wg->gy[m];        // tiles per K-range (chunk groups x N-ranges)
+        int32_t* ck = wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + by);
+        int32_t* cb = wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + kWgSlots - 1);
+        const int lk = __hip_atomic_fetch_add(ck, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want - 1;
+        const int lb = by == 0 && __hip_atomic_fetch_add(cb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want - 1;
+        if (lk) __hip_atomic_store(ck, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lb) __hip_atomic_store(cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (member-level count: the sampler waits for the frame-slot reader)
+        __hip_atomic_fetch_add(wg->done + kTicketStride * m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wg_last[0] = lk;
+        wg_last[1] = lb;
+        if (lk || lb) {                                   // the other tiles' atomics are visible now
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __syncthreads();
+      if (wg_last[0]) {
+        const int j0 = wg->dep_first[m][by], nj = wg->dep_count[m][by];
+        for (int j = 0; j < nj; ++j) run(j0 + j);
+      }
+      if (wg_last[1]) {
+        const int j0 = wg->dep_first[m][kWgSlots - 1], nj = wg->dep_count[m][kWgSlots - 1];
+        for (int j = 0; j < nj; ++j) run(j0 + j);
+      }
+    }
+  }
+#endif
+  if constexpr (FC) {
+    // one job per block (the launcher sizes the grid for it): no job loop, so no per-thread loop
+    // invariants are hoisted and kept live across the fc barriers
+    if (wid >= 0 && wid < njobs) run(wid);
+  } else {
+    for (int ji = wid < 0 ? njobs : wid; ji < njobs; ji += nwork) run(ji);
+  }
+  OPT_MARK(2);
+  if (!UPD) return;
+  // ---- end-of-launch bookkeeping (global_step, Adam beta powers, noise counter / copy) once
+  //      every block has consumed the old values. Block 0 (the sampler block, or the first work
+  //      block) does it: every other block makes ONE no-return arrival add on one of 16 counters
+  //      (blockIdx & 15, own 128-byte lines) and exits at once -- no returned atomic keeps its CU
+  //      slot (measured: a returning ticket per block cost Rainbow's 1714-block launch ~5 us) --
+  //      while lanes 0..15 of block 0 poll the counters. Nothing waits on block 0, so the wait
+  //      always ends (bounded anyway: a lost arrival flags ticket[kErrFlag] instead of hanging).
+  if constexpr (FEW) {
+    // every wave of this block consumed the old step / beta powers / noise in its item: one
+    // returning add per block; the last arriver closes (counter 0 back to zero for the next launch)
+    __shared__ int last_blk;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int k = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_blk = k == (int)gridDim.x - 1;
+      if (last_blk) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_blk) return;
+  } else if (blockIdx.x != 0) {
+    __syncthreads();                                      // every wave of the block is past its reads
+    if (tl) tl[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(cnt + kTicketStride * (blockIdx.x & (kTicketSubs - 1)), 1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (!FEW && threadIdx.x < kTicketSubs) {
+    const int j = threadIdx.x;
+    const int want = ((int)gridDim.x - j + kTicketSubs - 1) / kTicketSubs - (j == 0 ? 1 : 0);
+    int32_t* c = cnt + kTicketStride * j;
+    int spins = 0;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins > (1 << 22)) {                          // >> any launch: flag, do not hang
+        ticket[kErrFlag] = 1;
+        break;
+      }
+    }
+    __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  OPT_MARK(3);
+#if !DQN_ACT_F32
+  if constexpr (WG) {                                     // the sampler is past its wait
+    if ((int)threadIdx.x < wg->n)
+      __hip_atomic_store(wg->done + kTicketStride * threadIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
+  if (threadIdx.x == 0) {
+    if (step) step[0] += 1;
+    if constexpr (OP == 3) {
+      beta_pow[0] *= h.b1;
+      beta_pow[1] *= h.b2;
+    }
+    if (noise_rng != nullptr) noise_rng[1] += 1;        // (the drawing launch completed before this one)
+  }
+  // every other block consumed gnoise before its arrival add: block 0 may overwrite it now --
+  // float4 pieces, every load of a round issued before its stores (a load -> store chain per
+  // element cost Rainbow's launch ~6.5 us at its end: 15.6k cycles for ~8.7k floats)
+  if (noise_dst != nullptr) {
+    const bool al16 = ((reinterpret_cast<uintptr_t>(noise) | reinterpret_cast<uintptr_t>(noise_dst)) & 15) == 0;
+    const int n4 = al16 ? noise_n >> 2 : 0, tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    const float4* s4 = reinterpret_cast<const float4*>(noise);
+    float4* d4 = reinterpret_cast<float4*>(noise_dst);
+    constexpr int kU = 8;
+    for (int base = 0; base < n4; base += kU * nt) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] = s4[min(base + u * nt + tid, n4 - 1)];     // (clamped: no branch)
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (base + u * nt + tid < n4) d4[base + u * nt + tid] = v[u];
+    }
+    for (int i = 4 * n4 + tid; i < noise_n; i += nt) noise_dst[i] = noise[i];
+  }
+  OPT_MARK(4);
+  if (tl) tl[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#undef OPT_MARK
+}
+
+
+// All arguments of one optim_pack_kernel launch (the launcher in optim.hip fills it; the
+// per-optimizer instantiations live in optim_ops_*.hip so the build compiles them in parallel).
+struct OptPackLaunch {
+  int grid; size_t dyn; hipStream_t st;
+  int mode; bool few;
+  float* w; const float* g; float* s0; float* s1; float* beta_pow; int64_t* step; int32_t* ticket; OptHP h;
+  const UpdJob* jobs; int njobs; act_t* packed; float* tgt; act_t* tgt_packed; int tfreq;
+  const float* noise; float* eff; const float* gnoise; float* noise_dst; int noise_n;
+  TrunkSample smp; PerStep per; const float* tnoise; float* teff; act_t* tpk; int64_t* noise_rng; FcFuse ff;
+  const float* part; const WgradGroup* wg; int wg_blocks;
+};
+
+template <int N>
+void optim_pack_op(const OptPackLaunch& L);
+
+#ifdef DQN_OPTIM_DEFINE_OPS
+template <int N>
+void optim_pack_op(const OptPackLaunch& L) {
+#define OPM(M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(L.grid), dim3(kPackThreads), L.dyn, L.st, L.w, L.g, \
+                                  L.s0, L.s1, L.beta_pow, L.step, L.ticket, L.h, L.jobs, L.njobs, L.packed, L.tgt, \
+                                  L.tgt_packed, L.tfreq, L.noise, L.eff, L.gnoise, L.noise_dst, L.noise_n, L.smp, L.per, \
+                                  L.tnoise, L.teff, L.tpk, L.noise_rng, L.ff, L.part, L.wg, L.wg_blocks)
+  if constexpr (N < 0) {
+    OPM(kModeNoisy);                                    // mix + pack only (noisy nets)
+  } else {
+#if DQN_ACT_F32
+    switch (L.mode) {
+      case 0: OPM(0); break; case 1: OPM(1); break; case 3: OPM(3); break;
+      case 4: OPM(4); break; case 5: OPM(5); break; default: OPM(7); break;
+    }
+#else
+    constexpr bool kFew = N == 0 || N == 3 || N == 7;   // (the common optimizers' few-block variants)
+    if (kFew && L.few) {
+      if constexpr (kFew) {
+        switch (L.mode) {
+          case 0: OPM(32); break; case 1: OPM(33); break; case 3: OPM(35); break;
+          case 4: OPM(36); break; case 5: OPM(37); break; default: OPM(39); break;
+        }
+      }
+    } else {
+      switch (L.mode) {
+        case 0: OPM(0); break; case 1: OPM(1); break; case 3: OPM(3); break;
+        case 4: OPM(4); break; case 5: OPM(5); break; case 7: OPM(7); break;
+        case 8: OPM(8); break; case 9: OPM(9); break; case 11: OPM(11); break;
+        case 12: OPM(12); break; case 13: OPM(13); break; case 15: OPM(15); break;
+        case 24: OPM(24); break; case 25: OPM(25); break; case 27: OPM(27); break;
+        case 28: OPM(28); break; case 29: OPM(29); break; case 31: OPM(31); break;
+        default: break;
+      }
+    }
+#endif
+  }
+#undef OPM
+}
+#endif
+
+}  // namespace dqn

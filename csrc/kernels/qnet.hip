@@ -23,31 +23,9 @@
 #include "actor_dev.h"
 #include "../include/dqn_nets_k.h"
 #include "xgmi_dev.h"
+#include "wgrad_dev.h"
 
 namespace dqn {
-
-typedef __attribute__((ext_vector_type(8))) act_t bfx8;
-
-DQN_DEV bfx8 zero8() {
-  bfx8 z;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (act_t)0.f;
-  return z;
-}
-
-DQN_DEV bfx8 u8x8_to_bf(uint32_t lo, uint32_t hi) {
-  bfx8 r;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[j] = (act_t)(float)((lo >> (8 * j)) & 0xffu);
-    r[4 + j] = (act_t)(float)((hi >> (8 * j)) & 0xffu);
-  }
-  return r;
-}
-
-DQN_DEV f32x4 mfma16(const bfx8& a, const bfx8& b, const f32x4& c) {
-  return DQN_MFMA16_BUILTIN(a, b, c, 0, 0, 0);
-}
 
 // ============================================================== weight packing
 // dst2 (optional): the target network's packed copy, written too when step % freq == 0
@@ -91,154 +69,6 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src
   *reinterpret_cast<bfx8*>(dst + o) = v;
   if (sync) *reinterpret_cast<bfx8*>(dst2 + o) = v;
 }
-
-// ================================================================== A loaders
-// Each loader is built per (instance, row m) and returns the 8 consecutive
-// K-values [k0, k0+8) of row m as a bf16x8 MFMA A-fragment.
-// (Round 2 measured branch-free loaders -- clamped addresses + selects -- slower on the flagship
-// step, 82.7 -> 88.0 us: the strided dgrad then loads the 3 of 4 invalid taps the early returns
-// skip. The early-return loaders stay.)
-DQN_DEV bfx8 sel8(bool keep, const bfx8& v) {
-  bfx8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = keep ? v[j] : (act_t)0.f;
-  return r;
-}
-
-template <typename Tin, int CIN, int KH, int KW, int S>
-struct ConvLoader {
-  const Tin* base;
-  int IH, IW, iy0, ix0;
-  bool ok;
-  DQN_DEV ConvLoader() {}
-  DQN_DEV ConvLoader(const ConvArgs& a, int inst, int m) {
-    const int ohw = a.OH * a.OW;
-    ok = m < a.M;
-    const int mm = ok ? m : 0;
-    const int b = mm / ohw, r = mm - b * ohw, oy = r / a.OW, ox = r - oy * a.OW;
-    IH = a.IH; IW = a.IW;
-    iy0 = oy * S - a.pad_t;
-    ix0 = ox * S - a.pad_l;
-    base = reinterpret_cast<const Tin*>(a.in[inst]) + (int64_t)b * IH * IW * CIN;
-  }
-  DQN_DEV bfx8 frag(int k0) const {
-    if (!ok) return zero8();
-    const int kh = k0 / (KW * CIN), rem = k0 - kh * (KW * CIN), kw = rem / CIN, ci = rem - kw * CIN;
-    const int iy = iy0 + kh, ix = ix0 + kw;
-    if constexpr (sizeof(Tin) == 1) {
-      static_assert(CIN == 4, "uint8 input path expects 4 stacked frames");
-      uint32_t lo = 0, hi = 0;                 // 8 bytes = pixels (ix, ix+1) x 4 frames
-      if (iy >= 0 && iy < IH) {
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + (int64_t)iy * IW * CIN);
-        if (ix >= 0 && ix < IW) lo = row[ix];
-        if (ix + 1 >= 0 && ix + 1 < IW) hi = row[ix + 1];
-      }
-      return u8x8_to_bf(lo, hi);
-    } else {
-      if (iy < 0 || iy >= IH || ix < 0 || ix >= IW) return zero8();
-      return *reinterpret_cast<const bfx8*>(base + ((int64_t)iy * IW + ix) * CIN + ci);
-    }
-  }
-};
-
-// conv1 straight from the replay's frame ring: row m = (b, oy, ox), k = (kh, kw, c)
-// with the 4 stacked frames of sample b given by a slot table slots[b][4]
-// (replay state_idx rows / actor stacks). Fuses the frame-stack gather into
-// the first layer: no materialised [B, 84, 84, 4] copy. A k-group of 8 is the pixel
-// pair (ix, ix+1) x 4 frames with ix even (S, pad_l and IW even: Nature VALID and the
-// reference's SAME geometry), so the pair is one aligned 16-bit load per frame and is
-// either wholly inside or wholly outside the image.
-template <int KH, int KW, int S>
-struct FrameLoader {
-  const uint8_t* fb[4];
-  int IH, IW, iy0, ix0;
-  bool ok;
-  DQN_DEV FrameLoader() {}
-  DQN_DEV FrameLoader(const ConvArgs& a, int inst, int m) {
-    const int ohw = a.OH * a.OW;
-    ok = m < a.M;
-    const int mm = ok ? m : 0;
-    const int b = mm / ohw, r = mm - b * ohw, oy = r / a.OW, ox = r - oy * a.OW;
-    IH = a.IH; IW = a.IW;
-    iy0 = oy * S - a.pad_t;
-    ix0 = ox * S - a.pad_l;
-    const int4 sl = reinterpret_cast<const int4*>(a.in[inst])[b];
-    const uint8_t* fr = reinterpret_cast<const uint8_t*>(a.frames);
-    fb[0] = fr + (int64_t)sl.x * a.frame_hw;
-    fb[1] = fr + (int64_t)sl.y * a.frame_hw;
-    fb[2] = fr + (int64_t)sl.z * a.frame_hw;
-    fb[3] = fr + (int64_t)sl.w * a.frame_hw;
-  }
-  DQN_DEV bfx8 frag(int k0) const {
-    if (!ok) return zero8();
-    const int kh = k0 / (KW * 4), kw = (k0 - kh * (KW * 4)) / 4;   // k0 % 8 == 0 -> kw even, c = 0
-    const int iy = iy0 + kh, ix = ix0 + kw;
-    bfx8 r = zero8();
-    if (iy < 0 || iy >= IH) return r;
-    const int off = iy * IW + ix;
-    const bool in0 = ix >= 0 && ix < IW, in1 = ix + 1 >= 0 && ix + 1 < IW;
-    if (in0 && in1 && ((off & 1) == 0)) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint32_t v = *reinterpret_cast<const uint16_t*>(fb[c] + off);   // pixels ix, ix+1 of frame c
-        r[c] = (act_t)(float)(v & 0xffu);
-        r[4 + c] = (act_t)(float)(v >> 8);
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (in0) r[c] = (act_t)(float)fb[c][off];
-        if (in1) r[4 + c] = (act_t)(float)fb[c][off + 1];
-      }
-    }
-    return r;
-  }
-};
-
-// dgrad gather: row m = (b, iy, ix) of the conv INPUT, k = (kh, kw, co);
-// A[m][k] = dZ[b][oy][ox][co] where iy + pad_t - kh = S*oy (else 0).
-template <int COUT, int KH, int KW, int S>
-struct DgradLoader {
-  const act_t* base;
-  int OH, OW, ty, tx;
-  bool ok;
-  DQN_DEV DgradLoader() {}
-  DQN_DEV DgradLoader(const ConvArgs& a, int inst, int m) {
-    const int ihw = a.IH * a.IW;
-    ok = m < a.M;
-    const int mm = ok ? m : 0;
-    const int b = mm / ihw, r = mm - b * ihw, iy = r / a.IW, ix = r - iy * a.IW;
-    OH = a.OH; OW = a.OW;
-    ty = iy + a.pad_t;
-    tx = ix + a.pad_l;
-    base = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)b * OH * OW * COUT;
-  }
-  DQN_DEV bfx8 frag(int k0) const {
-    if (!ok) return zero8();
-    const int tap = k0 / COUT, co = k0 - tap * COUT, kh = tap / KW, kw = tap - kh * KW;
-    const int ny = ty - kh, nx = tx - kw;
-    if (ny < 0 || nx < 0) return zero8();
-    const int oy = ny / S, ox = nx / S;
-    if (oy * S != ny || ox * S != nx || oy >= OH || ox >= OW) return zero8();   // (invalid taps: no load)
-    return *reinterpret_cast<const bfx8*>(base + ((int64_t)oy * OW + ox) * COUT + co);
-  }
-};
-
-struct DenseLoader {
-  const act_t* row;
-  bool ok;
-  DQN_DEV DenseLoader() {}
-  DQN_DEV DenseLoader(const ConvArgs& a, int inst, int m) {
-    ok = m < a.M;
-    // row stride: a.IW when given (a K-wide slice of wider rows, e.g. one half of the
-    // dueling [value | advantage] hidden layer), else K
-    row = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)(ok ? m : 0) * (a.IW > 0 ? a.IW : a.K);
-  }
-  DQN_DEV bfx8 frag(int k0) const {
-    if (!ok) return zero8();
-    return *reinterpret_cast<const bfx8*>(row + k0);
-  }
-};
 
 // ============================================================ implicit GEMM
 // Block = WM x WN x KSPLIT waves (4 or 8); wave tile = (MT*16) x (NT*16).
@@ -464,31 +294,6 @@ __global__ void __launch_bounds__(256) dgrad_s2_kernel(ConvArgs a) {
 // elements) so each lane's 8 consecutive m are one ds_read_b128; then
 // (KB/16)x(NB/16) output tiles x MC/32 MFMA k-steps. fp32 atomics only when
 // more than one M-chunk contributes to a weight.
-#if DQN_ACT_F32
-template <int MC, int KB, int NB>
-struct WgradTile {
-  static constexpr int LR = MC + 8;
-  static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(act_t);
-};
-#else
-// 16-bit builds: the chunk is staged ROW-major ([m][k] and [m][n], one ds_write_b128 per
-// loaded 8-element fragment) and the MFMA operands (8 m values of one k / n column per lane)
-// come from ds_read_b64_tr_b16 transposed reads. Row strides of X + 16 elements put the 8
-// rows one 32-lane half reads (32 B each) on disjoint 8-bank ranges (stride / 4 B = 8 * odd
-// banks for X = 32, 64, 128): conflict-free reads.
-template <int MC, int KB, int NB>
-struct WgradTile {
-  static constexpr int SA = KB + 16, SZ = NB + 16;
-  static constexpr size_t lds_bytes = (size_t)MC * (SA + SZ) * sizeof(act_t);
-};
-// (operands through lds_tr16 / join_tr transposed reads: common.h)
-// Staging swizzle: the 16-byte slots of rows 4..7 mod 8 are swapped in pairs (element offset ^ 8).
-// The ds_write_b128 of 8 consecutive rows (8-lane groups, banks mod 32) then hits distinct banks
-// (row strides of 24 / 40 / 72 dwords otherwise put rows r and r + 4 on the same banks), and a
-// transposed read still covers the same 32-byte half-row: its banks are unchanged.
-DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
-#endif
-
 // Body shared by the per-layer launch and the grouped launch (one block = one
 // (M-chunk, K-range, N-range) tile; LDS passed in so a grouped kernel can carve
 // every member's staging from one buffer).
@@ -519,7 +324,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
-      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;              // clamped into the dZ row
+      const int cz = (n_lo + c8 < g.N ? n_lo + c8 : 0) - n_lo;     // masked groups read column 0
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
 #pragma unroll
@@ -606,7 +411,7 @@ DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, 
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
-      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;              // clamped into the dZ row
+      const int cz = (n_lo + c8 < g.N ? n_lo + c8 : 0) - n_lo;     // masked groups read column 0
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
 #pragma unroll
@@ -701,7 +506,7 @@ DQN_DEV void wgrad_block_det(const ConvArgs& a, const WgradArgs& g, int bx, int 
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
-      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;              // clamped into the dZ row
+      const int cz = (n_lo + c8 < g.N ? n_lo + c8 : 0) - n_lo;     // masked groups read column 0
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
     if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
@@ -800,7 +605,7 @@ DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, in
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
-      const int cz = min(n_lo + c8, g.ldz - 8) - n_lo;
+      const int cz = (n_lo + c8 < g.N ? n_lo + c8 : 0) - n_lo;
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
   };
@@ -1450,6 +1255,31 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   }
   hipLaunchKernelGGL(wgrad_group_kernel, dim3(total), dim3(256), lds, st, G);
   return 0;
+}
+
+int wgrad_fused_plan(WgradGroup& G, int conv_chunks) {
+#if DQN_ACT_F32
+  (void)G;
+  (void)conv_chunks;
+  return -1;
+#else
+  int total = 0;
+  G.slots_member = -1;
+  for (int i = 0; i < G.n; ++i) {
+    int MC, KB, NB;
+    if (!fused_wgrad_tiles(G.kind[i], MC, KB, NB) || G.g[i].part != nullptr) return -1;
+    if (G.kind[i] == L_NAT_CONV1_FRAMES) G.slots_member = i;
+    const int nch = (G.a[i].M + MC - 1) / MC;
+    const int per = G.kind[i] == L_HEAD_WGRAD ? 1 : conv_chunks;
+    G.g[i].mloop = per;
+    G.gx[i] = (nch + per - 1) / per;
+    G.gy[i] = (G.a[i].K + KB - 1) / KB;
+    G.nblk[i] = G.gx[i] * G.gy[i] * ((G.g[i].N + NB - 1) / NB);
+    G.g[i].atomic = G.gx[i] > 1 ? 1 : 0;
+    total += G.nblk[i];
+  }
+  return total;
+#endif
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {

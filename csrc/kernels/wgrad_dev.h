@@ -1,0 +1,366 @@
+// Weight-gradient building blocks shared by the layer kernels (qnet.hip) and the fused
+// optimizer launch (optim.hip): the implicit-GEMM A loaders (conv im2col from NHWC u8 / act_t,
+// conv1 straight from the replay frame ring, conv dgrad gather, dense rows), the row-major LDS
+// staging of a weight-gradient chunk and, for the optimizer's fused "wgrad + update" launch, an
+// NTH-thread tile that sums several M-chunks in registers.
+//
+// Reference: the autodiff weight gradients of the TF conv2d / matmul ops
+// (/root/reference/src/network.py:389-409, minimize at :198-202).
+#pragma once
+#include "common.h"
+#include "../include/dqn_nets_k.h"
+
+namespace dqn {
+
+typedef __attribute__((ext_vector_type(8))) act_t bfx8;
+
+DQN_DEV bfx8 zero8() {
+  bfx8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (act_t)0.f;
+  return z;
+}
+
+DQN_DEV bfx8 u8x8_to_bf(uint32_t lo, uint32_t hi) {
+  bfx8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (act_t)(float)((lo >> (8 * j)) & 0xffu);
+    r[4 + j] = (act_t)(float)((hi >> (8 * j)) & 0xffu);
+  }
+  return r;
+}
+
+DQN_DEV f32x4 mfma16(const bfx8& a, const bfx8& b, const f32x4& c) {
+  return DQN_MFMA16_BUILTIN(a, b, c, 0, 0, 0);
+}
+
+// ================================================================== A loaders
+// Each loader is built per (instance, row m) and returns the 8 consecutive
+// K-values [k0, k0+8) of row m as a bf16x8 MFMA A-fragment.
+// (Round 2 measured branch-free loaders -- clamped addresses + selects -- slower on the flagship
+// step, 82.7 -> 88.0 us: the strided dgrad then loads the 3 of 4 invalid taps the early returns
+// skip. The early-return loaders stay.)
+DQN_DEV bfx8 sel8(bool keep, const bfx8& v) {
+  bfx8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = keep ? v[j] : (act_t)0.f;
+  return r;
+}
+
+template <typename Tin, int CIN, int KH, int KW, int S>
+struct ConvLoader {
+  const Tin* base;
+  int IH, IW, iy0, ix0;
+  bool ok;
+  DQN_DEV ConvLoader() {}
+  DQN_DEV ConvLoader(const ConvArgs& a, int inst, int m) {
+    const int ohw = a.OH * a.OW;
+    ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / ohw, r = mm - b * ohw, oy = r / a.OW, ox = r - oy * a.OW;
+    IH = a.IH; IW = a.IW;
+    iy0 = oy * S - a.pad_t;
+    ix0 = ox * S - a.pad_l;
+    base = reinterpret_cast<const Tin*>(a.in[inst]) + (int64_t)b * IH * IW * CIN;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    const int kh = k0 / (KW * CIN), rem = k0 - kh * (KW * CIN), kw = rem / CIN, ci = rem - kw * CIN;
+    const int iy = iy0 + kh, ix = ix0 + kw;
+    if constexpr (sizeof(Tin) == 1) {
+      static_assert(CIN == 4, "uint8 input path expects 4 stacked frames");
+      uint32_t lo = 0, hi = 0;                 // 8 bytes = pixels (ix, ix+1) x 4 frames
+      if (iy >= 0 && iy < IH) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + (int64_t)iy * IW * CIN);
+        if (ix >= 0 && ix < IW) lo = row[ix];
+        if (ix + 1 >= 0 && ix + 1 < IW) hi = row[ix + 1];
+      }
+      return u8x8_to_bf(lo, hi);
+    } else {
+      if (iy < 0 || iy >= IH || ix < 0 || ix >= IW) return zero8();
+      return *reinterpret_cast<const bfx8*>(base + ((int64_t)iy * IW + ix) * CIN + ci);
+    }
+  }
+};
+
+// conv1 straight from the replay's frame ring: row m = (b, oy, ox), k = (kh, kw, c)
+// with the 4 stacked frames of sample b given by a slot table slots[b][4]
+// (replay state_idx rows / actor stacks). Fuses the frame-stack gather into
+// the first layer: no materialised [B, 84, 84, 4] copy. A k-group of 8 is the pixel
+// pair (ix, ix+1) x 4 frames with ix even (S, pad_l and IW even: Nature VALID and the
+// reference's SAME geometry), so the pair is one aligned 16-bit load per frame and is
+// either wholly inside or wholly outside the image.
+template <int KH, int KW, int S>
+struct FrameLoader {
+  const uint8_t* fb[4];
+  int IH, IW, iy0, ix0;
+  bool ok;
+  DQN_DEV FrameLoader() {}
+  DQN_DEV FrameLoader(const ConvArgs& a, int inst, int m) {
+    const int ohw = a.OH * a.OW;
+    ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / ohw, r = mm - b * ohw, oy = r / a.OW, ox = r - oy * a.OW;
+    IH = a.IH; IW = a.IW;
+    iy0 = oy * S - a.pad_t;
+    ix0 = ox * S - a.pad_l;
+    const int4 sl = reinterpret_cast<const int4*>(a.in[inst])[b];
+    const uint8_t* fr = reinterpret_cast<const uint8_t*>(a.frames);
+    fb[0] = fr + (int64_t)sl.x * a.frame_hw;
+    fb[1] = fr + (int64_t)sl.y * a.frame_hw;
+    fb[2] = fr + (int64_t)sl.z * a.frame_hw;
+    fb[3] = fr + (int64_t)sl.w * a.frame_hw;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    const int kh = k0 / (KW * 4), kw = (k0 - kh * (KW * 4)) / 4;   // k0 % 8 == 0 -> kw even, c = 0
+    const int iy = iy0 + kh, ix = ix0 + kw;
+    bfx8 r = zero8();
+    if (iy < 0 || iy >= IH) return r;
+    const int off = iy * IW + ix;
+    const bool in0 = ix >= 0 && ix < IW, in1 = ix + 1 >= 0 && ix + 1 < IW;
+    if (in0 && in1 && ((off & 1) == 0)) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t v = *reinterpret_cast<const uint16_t*>(fb[c] + off);   // pixels ix, ix+1 of frame c
+        r[c] = (act_t)(float)(v & 0xffu);
+        r[4 + c] = (act_t)(float)(v >> 8);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (in0) r[c] = (act_t)(float)fb[c][off];
+        if (in1) r[4 + c] = (act_t)(float)fb[c][off + 1];
+      }
+    }
+    return r;
+  }
+};
+
+// dgrad gather: row m = (b, iy, ix) of the conv INPUT, k = (kh, kw, co);
+// A[m][k] = dZ[b][oy][ox][co] where iy + pad_t - kh = S*oy (else 0).
+template <int COUT, int KH, int KW, int S>
+struct DgradLoader {
+  const act_t* base;
+  int OH, OW, ty, tx;
+  bool ok;
+  DQN_DEV DgradLoader() {}
+  DQN_DEV DgradLoader(const ConvArgs& a, int inst, int m) {
+    const int ihw = a.IH * a.IW;
+    ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int b = mm / ihw, r = mm - b * ihw, iy = r / a.IW, ix = r - iy * a.IW;
+    OH = a.OH; OW = a.OW;
+    ty = iy + a.pad_t;
+    tx = ix + a.pad_l;
+    base = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)b * OH * OW * COUT;
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    const int tap = k0 / COUT, co = k0 - tap * COUT, kh = tap / KW, kw = tap - kh * KW;
+    const int ny = ty - kh, nx = tx - kw;
+    if (ny < 0 || nx < 0) return zero8();
+    const int oy = ny / S, ox = nx / S;
+    if (oy * S != ny || ox * S != nx || oy >= OH || ox >= OW) return zero8();   // (invalid taps: no load)
+    return *reinterpret_cast<const bfx8*>(base + ((int64_t)oy * OW + ox) * COUT + co);
+  }
+};
+
+struct DenseLoader {
+  const act_t* row;
+  bool ok;
+  DQN_DEV DenseLoader() {}
+  DQN_DEV DenseLoader(const ConvArgs& a, int inst, int m) {
+    ok = m < a.M;
+    // row stride: a.IW when given (a K-wide slice of wider rows, e.g. one half of the
+    // dueling [value | advantage] hidden layer), else K
+    row = reinterpret_cast<const act_t*>(a.in[inst]) + (int64_t)(ok ? m : 0) * (a.IW > 0 ? a.IW : a.K);
+  }
+  DQN_DEV bfx8 frag(int k0) const {
+    if (!ok) return zero8();
+    return *reinterpret_cast<const bfx8*>(row + k0);
+  }
+};
+
+#if DQN_ACT_F32
+template <int MC, int KB, int NB>
+struct WgradTile {
+  static constexpr int LR = MC + 8;
+  static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(act_t);
+};
+#else
+// 16-bit builds: the chunk is staged ROW-major ([m][k] and [m][n], one ds_write_b128 per
+// loaded 8-element fragment) and the MFMA operands (8 m values of one k / n column per lane)
+// come from ds_read_b64_tr_b16 transposed reads. Row strides of X + 16 elements put the 8
+// rows one 32-lane half reads (32 B each) on disjoint 8-bank ranges (stride / 4 B = 8 * odd
+// banks for X = 32, 64, 128): conflict-free reads.
+template <int MC, int KB, int NB>
+struct WgradTile {
+  static constexpr int SA = KB + 16, SZ = NB + 16;
+  static constexpr size_t lds_bytes = (size_t)MC * (SA + SZ) * sizeof(act_t);
+};
+// (operands through lds_tr16 / join_tr transposed reads: common.h)
+// Staging swizzle: the 16-byte slots of rows 4..7 mod 8 are swapped in pairs (element offset ^ 8).
+// The ds_write_b128 of 8 consecutive rows (8-lane groups, banks mod 32) then hits distinct banks
+// (row strides of 24 / 40 / 72 dwords otherwise put rows r and r + 4 on the same banks), and a
+// transposed read still covers the same 32-byte half-row: its banks are unchanged.
+DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
+#endif
+
+
+#if !DQN_ACT_F32
+// ------------------------------------------------------------- fused-launch tile
+// One weight-gradient tile (K-range by, N-range bz) over chunk group bx = nper consecutive
+// MC-row chunks of M, run by NTH threads: the chunks are summed in registers (chunk c + 1's
+// operands are loaded while chunk c's MFMAs run), then ONE set of fp32 atomics per group (plain
+// stores when g.atomic == 0: one group covers M). Staging as the 16-bit wgrad_block: row-major
+// [m][k] / [m][n] tiles with the slot swizzle, operands through transposed LDS reads. LDS:
+// WgradTile<MC, KB, NB>::lds_bytes. Every thread of the block calls it (2 barriers per chunk).
+template <class LD, int MC, int KB, int NB, int NTH>
+DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, int nper, act_t* lds,
+                        int64_t* ph = nullptr) {
+  // ph (probe launches): s_memrealtime at tile start | each chunk staged | each chunk's MFMAs done |
+  // results issued (thread 0; the caller stamps the drain)
+#define WG_MARK(i) if (ph != nullptr && threadIdx.x == 0 && (i) < 7) ph[i] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  WG_MARK(0);
+  using Tl = WgradTile<MC, KB, NB>;
+  constexpr int SA = Tl::SA, SZ = Tl::SZ;
+  constexpr int NW = NTH / 64, TPR = NTH / MC;
+  constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
+  constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / NW, KSTEPS = MC / 32;
+  static_assert(NTH % MC == 0 && GA >= 1 && GZ >= 1 && GA * TPR * 8 == KB && GZ * TPR * 8 == NB &&
+                TILES % NW == 0 && NB <= NTH, "fused wgrad tiling");
+  act_t* At = lds;                               // [MC][SA]
+  act_t* Zt = lds + MC * SA;                     // [MC][SZ]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k_lo = by * KB, n_lo = bz * NB;
+  const int nchunks = (a.M + MC - 1) / MC, c0 = bx * nper;
+  const int nch = min(nchunks, c0 + nper) - c0;
+  const bool dob = g.db != nullptr && by == 0;
+  const int r = tid % MC, p = tid / MC;
+  bfx8 va[GA], vz[GZ];
+  auto load = [&](int c) {
+    const int m = (c0 + c) * MC + r;
+    const bool mok = m < a.M;
+    const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
+    LD ld(a, 0, m);
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int k0 = k_lo + (p + i * TPR) * 8;
+      va[i] = sel8(k0 < a.K, ld.frag(min(k0, a.K - 8)));          // (clamped: no branch per load)
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+      const int cz = (n_lo + c8 < g.N ? n_lo + c8 : 0) - n_lo;     // masked groups read column 0
+      vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
+    }
+  };
+  const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
+  constexpr int NTt = NB / 16;
+  f32x4 acc[PERW];
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  load(0);
+  for (int c = 0; c < nch; ++c) {
+    if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (((p + i * TPR) * 8) ^ wsw(r))) = va[i];
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[i];
+    __syncthreads();
+    WG_MARK(1 + 2 * c);
+    if (c + 1 < nch) load(c + 1);                // in flight under this chunk's MFMAs
+    if (dob && tid < NB) {
+#pragma unroll 8
+      for (int q = 0; q < MC; ++q) dbs += (float)Zt[q * SZ + (tid ^ wsw(q))];
+    }
+#pragma unroll
+    for (int i = 0; i < PERW; ++i) {
+      const int tile = wave + NW * i;
+      const int kt = tile / NTt, nt = tile - kt * NTt;
+      const act_t* pa = At + (4 * gq + rq) * SA + kt * 16 + (cp ^ wsw(4 * gq));
+      const act_t* pz = Zt + (4 * gq + rq) * SZ + nt * 16 + (cp ^ wsw(4 * gq));
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const bfx8 af = join_tr(lds_tr16(pa + 32 * s * SA), lds_tr16(pa + (32 * s + 16) * SA));
+        const bfx8 bf = join_tr(lds_tr16(pz + 32 * s * SZ), lds_tr16(pz + (32 * s + 16) * SZ));
+        acc[i] = mfma16(af, bf, acc[i]);
+      }
+    }
+    WG_MARK(2 + 2 * c);
+  }
+  const bool atomic = g.atomic != 0;
+  if (dob && tid < NB) {
+    const int nn = n_lo + tid;
+    if (nn < g.N) {
+      float* pdb = nn < g.nsplit ? g.db + nn : g.db2 + (nn - g.nsplit);
+      const float s = dbs * kInvLossScale;
+      // (plain results are written through to memory: a consumer in the same launch reads them)
+      if (atomic) atomicAdd(pdb, s); else __hip_atomic_store(pdb, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PERW; ++i) {
+    const int tile = wave + NW * i;
+    const int kt = tile / NTt, nt = tile - kt * NTt;
+    const int n = n_lo + nt * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k_lo + kt * 16 + 4 * (lane >> 4) + q;
+      if (k < a.K && n < g.N) {
+        float* o = n < g.nsplit ? g.dw + (int64_t)k * g.nsplit + n
+                                : g.dw2 + (int64_t)k * (g.N - g.nsplit) + (n - g.nsplit);
+        const float v = acc[i][q] * (g.scale * kInvLossScale);
+        if (atomic) atomicAdd(o, v); else __hip_atomic_store(o, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  if (ph != nullptr && threadIdx.x == 0) ph[6] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#undef WG_MARK
+}
+
+// The fused launch's tiles per member kind (NTH = 512 threads, 128-row chunks, <= 40 KB of
+// LDS: the optimizer blocks beside them keep 4 blocks / CU). Returns false for a kind the fused
+// launch does not run.
+constexpr int kFusedWgMC = 128;
+DQN_DEV_HOST_INLINE bool fused_wgrad_tiles(int kind, int& MC, int& KB, int& NB) {
+  switch (kind) {
+    case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = kFusedWgMC; KB = 64; NB = 32; return true;
+    case L_NAT_CONV2_FWD: case L_NAT_CONV3_FWD: MC = kFusedWgMC; KB = 64; NB = 64; return true;
+    case L_HEAD_WGRAD: MC = 64; KB = 64; NB = 64; return true;
+    default: return false;
+  }
+}
+
+using FwC1 = ConvLoader<uint8_t, 4, 8, 8, 4>;
+using FwC2 = ConvLoader<act_t, 32, 4, 4, 2>;
+using FwC3 = ConvLoader<act_t, 64, 3, 3, 1>;
+using FwF1 = FrameLoader<8, 8, 4>;
+
+// Block b of the fused launch's weight-gradient range: find its member (block ranges in member
+// order, longest first) and run the member's tile. G lives in device memory (built once per
+// workspace by the host planner, wgrad_fused_plan). Returns member * 256 + K-range.
+template <int NTH>
+DQN_DEV int fused_wgrad_block(const WgradGroup& G, int b, act_t* lds, int64_t* ph = nullptr) {
+  int i = 0;
+  while (i < G.n - 1 && b >= G.nblk[i]) { b -= G.nblk[i]; ++i; }
+  const int gx = G.gx[i], gy = G.gy[i];
+  const int bx = b % gx, rr = b / gx, by = rr % gy, bz = rr / gy;
+  const ConvArgs& a = G.a[i];
+  const WgradArgs& g = G.g[i];
+  switch (G.kind[i]) {
+    case L_NAT_CONV1_FWD: wgrad_tile<FwC1, kFusedWgMC, 64, 32, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
+    case L_NAT_CONV1_FRAMES: wgrad_tile<FwF1, kFusedWgMC, 64, 32, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
+    case L_NAT_CONV2_FWD: wgrad_tile<FwC2, kFusedWgMC, 64, 64, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
+    case L_NAT_CONV3_FWD: wgrad_tile<FwC3, kFusedWgMC, 64, 64, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
+    case L_HEAD_WGRAD: wgrad_tile<DenseLoader, 64, 64, 64, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
+    default: break;
+  }
+  return i * 256 + by;                           // (member, K-range) of the tile
+}
+#endif
+
+}  // namespace dqn

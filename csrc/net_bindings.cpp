@@ -162,8 +162,8 @@ dqn::HeadArgs head_args(const std::vector<int64_t>& ints, const std::vector<int6
 }
 
 // members: per layer [kind, in, dz, ldz, dw, db, dw2, db2, nsplit, N] + dims (11 or 13) + scale
-void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vector<int64_t>> dims,
-                 std::vector<double> scales) {
+static dqn::WgradGroup build_group(const std::vector<std::vector<int64_t>>& members,
+                                   const std::vector<std::vector<int64_t>>& dims, const std::vector<double>& scales) {
   TORCH_CHECK(members.size() >= 1 && members.size() <= (size_t)dqn::kMaxWgradMembers &&
               dims.size() == members.size() && scales.size() == members.size(), "1..6 group members");
   dqn::WgradGroup G{};
@@ -184,9 +184,44 @@ void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vec
       TORCH_CHECK(g.mloop >= 1 && g.mloop <= 64 && g.nsplit == g.N && g.dw2 == nullptr, "partial member args");
     }
   }
+  return G;
+}
+
+void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vector<int64_t>> dims,
+                 std::vector<double> scales) {
+  const dqn::WgradGroup G = build_group(members, dims, scales);
   const int rc = launch_wgrad_group(G, cur_stream());
   TORCH_CHECK(rc != -3, "wgrad group: partial members need 128-row chunks and pstride >= K*N + N");
   TORCH_CHECK(rc == 0, "unknown wgrad kind in group");
+}
+
+// The fused weight-gradient range of a split optimizer update (optim.hip kModeWg): the planned
+// group as bytes (the caller keeps a device copy for the launches) and its block count.
+// done: device int32 counters (>= 32 * kWgCounters words, zeroed; the launch leaves them zero).
+// deps: [member, slot, first job, job count] per (member, K-range slot / bias slot kWgSlots - 1):
+// the job-table ranges the slot's last tile runs.
+std::tuple<torch::Tensor, int64_t> wgrad_plan(std::vector<std::vector<int64_t>> members,
+                                              std::vector<std::vector<int64_t>> dims, std::vector<double> scales,
+                                              torch::Tensor done, std::vector<std::vector<int64_t>> deps,
+                                              int64_t conv_chunks) {
+  TORCH_CHECK(conv_chunks >= 1 && conv_chunks <= 64, "wgrad_plan: conv_chunks");
+  TORCH_CHECK(done.is_cuda() && done.scalar_type() == torch::kInt32 && done.is_contiguous() &&
+                  done.numel() >= 32 * (int64_t)dqn::kWgCounters, "wgrad_plan: done counters");
+  dqn::WgradGroup G = build_group(members, dims, scales);
+  G.done = done.data_ptr<int32_t>();
+  for (const auto& d : deps) {
+    TORCH_CHECK(d.size() == 4 && d[0] >= 0 && d[0] < G.n && d[1] >= 0 && d[1] < dqn::kWgSlots && d[2] >= 0 && d[3] >= 1,
+                "wgrad_plan: dep = [member, slot, first, count]");
+    G.dep_first[d[0]][d[1]] = (int)d[2];
+    G.dep_count[d[0]][d[1]] = (int)d[3];
+  }
+  const int total = wgrad_fused_plan(G, (int)conv_chunks);
+  TORCH_CHECK(total > 0, "wgrad_plan: a member has no fused tile (16-bit builds; conv / head members only)");
+  for (int i = 0; i < G.n; ++i)
+    TORCH_CHECK(G.gy[i] <= dqn::kWgSlots - 1, "wgrad_plan: more K-ranges than counter slots");
+  torch::Tensor t = torch::empty({(int64_t)sizeof(dqn::WgradGroup)}, torch::kUInt8);
+  memcpy(t.data_ptr(), &G, sizeof(G));
+  return {t, (int64_t)total};
 }
 
 // ptrs (4 per group): slots, states, w1, w2, w3, b1, b2, b3, x3, then a1, p1, a2, p2, a3; M as in trunk
@@ -362,6 +397,10 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("qp"), pybind11::arg("actor"),
         pybind11::arg("actor_f"), pybind11::arg("act_h") = 0, pybind11::arg("prof") = 0);
   m.def("qnet_wgrad_group", &wgrad_group);
+  m.def("qnet_wgrad_plan", &wgrad_plan, pybind11::arg("members"), pybind11::arg("dims"), pybind11::arg("scales"),
+        pybind11::arg("done"), pybind11::arg("deps"), pybind11::arg("conv_chunks") = 2);
+  m.attr("WG_COUNTERS") = (int)dqn::kWgCounters;
+  m.attr("WG_SLOTS") = (int)dqn::kWgSlots;
   m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
         pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{});
   m.def("qnet_cnn_bwd", &cnn_bwd);

@@ -184,6 +184,10 @@ def build_parser() -> argparse.ArgumentParser:
     a('--fuse_fc_wgrad', default=1, type=int,
       help='HIP executor (16-bit builds): form the fc weight gradient (X^T dH, rank <= B) inside the '
            'fused optimizer launch instead of writing and re-reading it as an fp32 gradient')
+    a('--fuse_wgrad_update', default=1, type=int,
+      help='HIP executor (one process, 16-bit builds, with --fuse_fc_wgrad): compute the conv / '
+           'output-layer weight gradients in the leading blocks of the fused optimizer\'s first '
+           'launch, beside the fc update, instead of a launch of their own before it')
     a('--det_wgrad', default=0, type=int,
       help='HIP executor (one process, 16-bit builds): conv weight gradients as deterministic '
            'chunk-group partials summed in a fixed order by the fused optimizer launch (no fp32 '
@@ -288,6 +292,7 @@ class Config:
     hip_graph: int = 1
     fuse_sampling: int = 2
     fuse_fc_wgrad: int = 1
+    fuse_wgrad_update: int = 1
     det_wgrad: int = 0
     summary_secs: float = 120.0
     checkpoint_secs: float = 600

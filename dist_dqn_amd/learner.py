@@ -127,6 +127,12 @@ class Learner:
         self._det_wgrad = bool(not self.ctx.enabled and ps_client is None and int(getattr(config, 'det_wgrad', 0))
                                and network.fuses_update(tfreq) and hasattr(ex, 'can_det_wgrad')
                                and ex.can_det_wgrad(B))
+        # the grouped conv / output-layer weight gradients run in the leading blocks of the fused
+        # update's first launch, beside the fc update (executor.can_defer_wgrad): one process only
+        # (DP all-reduces those gradients between the backward and the update)
+        self._defer_wgrad = bool(not self.ctx.enabled and ps_client is None and self._defer_fc
+                                 and not self._det_wgrad and int(getattr(config, 'fuse_wgrad_update', 1))
+                                 and hasattr(ex, 'can_defer_wgrad') and ex.can_defer_wgrad(B, sg))
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:
             use_graph = bool(config.hip_graph) and self.device.type == 'cuda'
@@ -197,7 +203,7 @@ class Learner:
                                                             det_wgrad=self._det_wgrad)
         else:
             loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg, defer_fc=self._defer_fc,
-                                                det_wgrad=self._det_wgrad)
+                                                det_wgrad=self._det_wgrad, defer_wgrad=self._defer_wgrad)
         # keep references (static buffers under graph capture) instead of copies
         self.loss = loss.view(1)
         self.prio = prio.view(-1)
@@ -414,7 +420,7 @@ class Learner:
             # host-side state a step body advances (restored if the capture is refused midway)
             ex = self.net.executor
             saved = (self._presampled, getattr(self.net, '_noise_drawn', False), getattr(ex, '_fc_pending', None),
-                     getattr(ex, '_parts_pending', None))
+                     getattr(ex, '_parts_pending', None), getattr(ex, '_wg_pending', None))
             try:
                 with quiet_capture(), torch.cuda.stream(s), \
                         torch.cuda.graph(gk, stream=s, capture_error_mode=_CAPTURE_MODE):
@@ -427,7 +433,7 @@ class Learner:
                 self._presampled = saved[0]
                 self.net._noise_drawn = saved[1]
                 if hasattr(ex, '_fc_pending'):
-                    ex._fc_pending, ex._parts_pending = saved[2], saved[3]
+                    ex._fc_pending, ex._parts_pending, ex._wg_pending = saved[2], saved[3], saved[4]
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 raise
             torch.cuda.current_stream(self.device).wait_stream(s)

@@ -164,15 +164,19 @@ class Network:
     # ------------------------------------------------------------- training
     def compute_grads(self, batch: Dict[str, torch.Tensor], acting: Optional[dict] = None, split: bool = False,
                       sigma_grads: bool = True, lowrank: Optional[dict] = None, defer_fc: bool = False,
-                      det_wgrad: bool = False):
+                      det_wgrad: bool = False, defer_wgrad: bool = False):
         """Loss + gradient into ``self.grad``. ``split=True`` returns ``(loss, prio, tail)``: when
         ``tail`` is not None only the dense-layer gradients (``dense_range()``) are final and
         ``tail()`` queues the rest of the backward (see HipExecutor.loss_and_grad). ``defer_fc``:
         the fc weight / bias gradient is left to the next fused ``apply_grads`` (it forms them
         inside the optimizer launch; ``HipExecutor.can_defer_fc``). ``det_wgrad``: the conv weight
         gradients stay as deterministic partials the next fused ``apply_grads`` sums
-        (``HipExecutor.can_det_wgrad``)."""
+        (``HipExecutor.can_det_wgrad``). ``defer_wgrad`` (with ``defer_fc``): the grouped conv /
+        output-layer weight gradients are computed by the next fused ``apply_grads`` beside the
+        fc update (``HipExecutor.can_defer_wgrad``)."""
         kw = {}
+        if defer_wgrad:
+            kw['defer_wgrad'] = True
         if defer_fc:
             kw['defer_fc'] = True
         if det_wgrad:

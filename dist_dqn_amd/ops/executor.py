@@ -240,7 +240,7 @@ class HipExecutor:
                     items.append([0, src, f.K, f.N, k0, n0, f.dst_off, f.dst_N16, f.nt_off, f.ks_off,
                                   d.mode if d else 0, d.dst_off if d else 0, d.dst_N16 if d else 0,
                                   d.nt_off if d else 0, d.ks_off if d else 0, d.p1 if d else 0, so, ei, eo, eff,
-                                  fcc, 0, 0, 0])
+                                  fcc, -1, 0, 0, 0])
         for name in lay.names:
             off, n = lay.offsets[name], lay.numel(name)
             if off in fwd or off in sig:
@@ -253,11 +253,18 @@ class HipExecutor:
                 cnt = min(2048, n - s0)
                 items.append([1, off + s0, cnt, 0, 0, 0, (c.dst_off + self.fs * s0) if c else -1] + [0] * 9
                              + [so + s0 if so >= 0 else -1, -1, eo + s0 if so >= 0 else -1, int(self.noisy), fcc,
-                                0, 0, 0])
+                                -1, 0, 0, 0])
         self.upd_items = items
         self._upd_dev: Dict[torch.device, torch.Tensor] = {}
         # (x ptr, dh ptr, rows) of a step whose fc weight gradient the next update_and_pack forms
         self._fc_pending = None
+        # (members, dims, scales) of a step whose grouped conv / output-layer weight gradients the
+        # next update_and_pack computes in its first launch (loss_and_grad(defer_wgrad=True))
+        self._wg_pending = None
+        self._wg_plans: Dict[tuple, tuple] = {}
+        # 128-row chunks per conv weight-gradient tile of the fused launch (summed in registers, one
+        # set of fp32 atomics per tile)
+        self.wg_conv_chunks = 2
         # (job table, partial buffer ptr) of a step whose conv weight gradients the next
         # update_and_pack sums from the grouped wgrad's deterministic partials
         self._parts_pending = None
@@ -336,6 +343,9 @@ class HipExecutor:
         from those rows instead of reading them from ``grad``). Returns True."""
         from ..optim import kernel_op
         dev = flat.device
+        if self._wg_pending is not None:
+            return self._update_split(opt, flat, grad, grad_scale, global_step, target, target_freq, noise, grad_noise,
+                                      noise_dst, next_sample, target_noise, noise_rng, fc)
         jobs, part = self._upd_jobs(dev), 0
         if self._parts_pending is not None:
             (jobs, part), self._parts_pending = self._parts_pending, None
@@ -374,6 +384,114 @@ class HipExecutor:
                 self._bound[target.data_ptr()] = target_noise
         return True
 
+    def _wg_plan(self, wg, grad, dev):
+        """The fused weight-gradient launch plan for these members (fixed workspace pointers: built
+        once, outside any graph capture): (device WgradGroup, its tile count, job table, number of
+        block-assigned jobs, done counters). Job table: the fc jobs (gradient from FcFuse rows,
+        final at launch start; one block each), then every other job grouped by the member tile
+        range that completes its gradient -- (member, 64-row K-range) for weight tiles, the
+        member's K-range-0 tiles for its bias -- which the last tile of that range runs."""
+        members, dims, scales = wg
+        key = (tuple(tuple(m) for m in members), tuple(tuple(d) for d in dims), tuple(scales), grad.data_ptr(),
+               self.wg_conv_chunks, dev)
+        pl = self._wg_plans.get(key)
+        if pl is None:
+            assert not torch.cuda.is_current_stream_capturing(), 'fused wgrad plan: build it before capturing'
+            ext = self.ext
+            done = torch.zeros(32 * ext.WG_COUNTERS, dtype=torch.int32, device=dev)
+            g0 = grad.data_ptr()
+            lay = self.layout
+            span = {}                        # tensor offset -> (member, end, is weight)
+            for mi, m in enumerate(members):
+                for j, ptr in enumerate(m[4:8]):           # dw, db, dw2, db2
+                    if ptr:
+                        o = (int(ptr) - g0) // 4
+                        name = next(n for n in lay.names if lay.offsets[n] == o)
+                        span[o] = (mi, o + lay.numel(name), j % 2 == 0)
+            fcj, groups = [], {}
+            for it in self.upd_items:
+                if it[20] >= 0:
+                    fcj.append(list(it))
+                    continue
+                src = it[1]
+                owner = [(mi, w) for o, (mi, hi, w) in span.items() if o <= src < hi]
+                assert len(owner) == 1, 'fused wgrad: no member writes the gradient of job at %d' % src
+                mi, w = owner[0]
+                if w:
+                    assert it[0] == 0, 'weight gradients of fused members come as tile jobs'
+                    slot = it[4] // 64                  # the tile's K-range (64 rows per fused tile)
+                else:
+                    slot = ext.WG_SLOTS - 1
+                groups.setdefault((mi, slot), []).append(list(it))
+            table, deps = list(fcj), []
+            for (mi, slot), its in sorted(groups.items()):
+                deps.append([mi, slot, len(table), len(its)])
+                table += its
+            host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
+            jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
+            pl = (host.to(dev), int(total), jobs, len(fcj), done)
+            self._wg_plans[key] = pl
+        return pl
+
+    def _update_split(self, opt, flat, grad, grad_scale, global_step, target, target_freq, noise, grad_noise,
+                      noise_dst, next_sample, target_noise, noise_rng, fc):
+        """``update_and_pack`` after ``loss_and_grad(defer_wgrad=True)``: ONE launch that also
+        computes the grouped weight gradients (conv layers + output layer, fp32 atomics into
+        ``grad``, optim_pack.h kModeWg). Its grid: the lead block (next minibatch + end-of-launch
+        bookkeeping), the weight-gradient tiles, the fc jobs (gradient formed from the FcFuse
+        rows: independent of the tiles -- the fc update, ~90% of the optimizer's bytes, runs
+        beside the weight-gradient work). Every other job is run by the tile that completes its
+        gradient (the last of its member's K-range)."""
+        from ..optim import kernel_op
+        dev = flat.device
+        wg, self._wg_pending = self._wg_pending, None
+        fcargs = self._take_fc(fc)
+        assert fcargs, 'deferred weight gradients need the fused fc gradient (defer_fc)'
+        plan, nwg, jobs, nfc, _ = self._wg_plan(wg, grad, dev)
+        hp = opt.hp
+        s0 = opt.slots[0] if len(opt.slots) > 0 else flat
+        s1 = opt.slots[1] if len(opt.slots) > 1 else flat
+        if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev or opt.ticket.numel() < 17 * 32:
+            opt.ticket = torch.zeros(17 * 32, dtype=torch.int32, device=dev)
+        eff = teff = tpk = None
+        if self.noisy:
+            assert noise is not None and noise.dtype == torch.float32
+            k = flat.data_ptr()
+            p, eff = self._packed_for(k, flat), self._eff_for(k, flat)
+            pt = None
+            if target_noise is not None:
+                assert target is not None and target_noise.dtype == torch.float32
+                tk = target.data_ptr()
+                tpk, teff = self._packed_for(tk, target), self._eff_for(tk, target)
+        else:
+            p = self.packed(flat)
+            pt = self.packed(target) if target is not None else None
+        hps = [float(hp['momentum']), float(hp['rho']), float(hp['rms_mom']), float(hp['rms_eps']), float(hp['b1']),
+               float(hp['b2']), float(hp['adam_eps']), float(hp['ad_rho']), float(hp['ad_eps'])]
+        op = kernel_op(opt)
+        args = (flat, grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr), float(opt.reg_param),
+                int(opt.layout.reg_end), float(grad_scale), global_step, hps)
+        self.ext.optim_pack(op, *args, jobs, p, target, pt, int(target_freq), self.opt_max_grid, noise, eff,
+                            grad_noise, noise_dst,
+                            (list(next_sample['spec']) + [int(next_sample['B'])]
+                             if next_sample is not None and next_sample['kind'] == 'uniform' else []),
+                            (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
+                            (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
+                            target_noise, teff, tpk, noise_rng, fcargs, 0, wg=plan.data_ptr(), wg_blocks=nwg,
+                            wg_jobs=nfc)
+        if self.noisy:
+            self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
+            if target_noise is not None:
+                self._bound[target.data_ptr()] = target_noise
+        return True
+
+    def can_defer_wgrad(self, B: int, sigma_grads: bool = False) -> bool:
+        """True when ``loss_and_grad(defer_fc=True, defer_wgrad=True)`` at this batch leaves the
+        grouped conv / output-layer weight gradients to the next ``update_and_pack`` (which then
+        runs them beside the fc update, ``_update_split``): the Nature trunk's grouped-wgrad path
+        in the 16-bit builds, one process (no all-reduce between the gradients and the update)."""
+        return self.can_defer_fc(B, sigma_grads) and self.arch.network == 'nature' and not (self.noisy and sigma_grads)
+
     def _take_fc(self, fc=None):
         if fc is None:
             fc, self._fc_pending = self._fc_pending, None
@@ -389,7 +507,7 @@ class HipExecutor:
                 and B <= 32 and not (self.noisy and sigma_grads))
 
     def pending_fc(self) -> bool:
-        return self._fc_pending is not None or self._parts_pending is not None
+        return self._fc_pending is not None or self._parts_pending is not None or self._wg_pending is not None
 
     def can_det_wgrad(self, B: int) -> bool:
         """True when ``loss_and_grad(det_wgrad=True)`` leaves the conv weight / bias gradients as
@@ -884,7 +1002,7 @@ class HipExecutor:
     def loss_and_grad(self, online: torch.Tensor, target: torch.Tensor, batch: Dict[str, torch.Tensor],
                       grad_out: torch.Tensor, noise=None, noise_target=None, acting: Optional[dict] = None,
                       split: bool = False, sigma_grads: bool = True, draw_noise=None, lowrank=None,
-                      defer_fc: bool = False, det_wgrad: bool = False):
+                      defer_fc: bool = False, det_wgrad: bool = False, defer_wgrad: bool = False):
         """lowrank (data parallelism, see ``lowrank_spec``): {'gather': f(srcs, outs, nbytes) (an
         in-stream all-gather of two byte segments), 'world', 'rank'}. With ``split``, the fc weight
         gradient is then formed from the all-gathered factors right after the head, in stream order
@@ -894,6 +1012,11 @@ class HipExecutor:
         defer_fc (``can_defer_fc``): the fc weight and bias gradients are NOT written to grad_out;
         the next ``update_and_pack`` forms them from the fc input rows and dH rows (this rank's, or
         the all-gathered ones under ``lowrank``) inside the optimizer launch.
+
+        defer_wgrad (``can_defer_wgrad``, with defer_fc, one process): the grouped conv and
+        output-layer weight / bias gradients are NOT launched here either; the next
+        ``update_and_pack`` computes them in the leading blocks of its first launch, beside the fc
+        update (``_update_split``). ``grad_out`` holds them only after that call.
 
         det_wgrad (``can_det_wgrad``, one process): the conv weight / bias gradients are NOT
         written to grad_out either; the grouped wgrad launch stores per-chunk-group partials
@@ -1049,6 +1172,9 @@ class HipExecutor:
             noisy = self.noisy and gnoise is not None
             defer = bool(defer_fc) and self.can_defer_fc(B, gnoise is not None)
             assert defer or not defer_fc, 'defer_fc: not available for this executor / batch'
+            dwg = bool(defer_wgrad)
+            assert not dwg or (defer and not det and not split and self.can_defer_wgrad(B, gnoise is not None)), \
+                'defer_wgrad: needs defer_fc, one process, no det_wgrad'
             if defer and not (split and lowrank is not None):
                 # the optimizer launch forms dW_fc = x3^T dH from this rank's rows
                 self._fc_pending = (x3, ws['dh'].data_ptr(), B)
@@ -1104,7 +1230,10 @@ class HipExecutor:
                                [ws['dz1'].data_ptr()], [x1], [1.0],
                                [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
                                 0, 0])
-                ext.qnet_wgrad_group(members, dims, scales)
+                if dwg:                 # the next update_and_pack runs the group beside the fc update
+                    self._wg_pending = (members, dims, scales)
+                else:
+                    ext.qnet_wgrad_group(members, dims, scales)
                 if noisy:
                     ext.qnet_noisy_grad(grad_out.data_ptr(), gnoise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                         len(self.noisy_jobs), self._noisy_max)

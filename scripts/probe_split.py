@@ -1,0 +1,161 @@
+"""Probe: the fused weight-gradient + optimizer launch (executor._update_split) of the flagship
+step, timed alone (HIP events over back-to-back launches):
+
+  wgrad_group      the grouped weight-gradient launch it replaces (256-row chunks)
+  F                the fused launch: lead block, weight-gradient tiles, fc jobs, dependent jobs
+  F_nosampler      the same without the next-minibatch block
+  F_wgrad_only     the weight-gradient tiles + one fc job
+  F_fc_only        the fc jobs alone (FcFuse launch, no weight-gradient tiles)
+  fused_old        the previous update launch (every job, sampler block; gradients read)
+
+    python scripts/probe_split.py [--iters 200] [extra config flags...]
+
+Prints one JSON line of mean us per launch.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.optim import kernel_op
+    from dist_dqn_amd.replay import DeviceReplay
+    args = sys.argv[1:]
+    iters = 200
+    if args[:1] == ['--iters']:
+        iters, args = int(args[1]), args[2:]
+    dev = torch.device('cuda', 0)
+    cfg = preset('nature', 'Pong-v0', '--seed=0 --dtype=bf16 --replay_memory_capacity=65536 ' + ' '.join(args))
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=dev)
+    rep = DeviceReplay(65536, (84, 84), 4, device=dev, prioritized=cfg.prioritized_replay)
+    rep.fill_synthetic(65536, 6)
+    learner = Learner(net, rep, cfg, use_graph=False)
+    assert learner._defer_wgrad, 'the split update is not active for this config'
+    ex = net.executor
+    seen = {}
+    orig = ex._update_split
+
+    def spy(*a, **k):
+        seen['wg'], seen['fc'] = ex._wg_pending, ex._fc_pending
+        return orig(*a, **k)
+
+    ex._update_split = spy
+    for _ in range(3):
+        learner.step()
+    torch.cuda.synchronize()
+    ex._update_split = orig
+    wg, fc = seen['wg'], seen['fc']
+    members, dims, scales = wg
+    opt = net.optimizer
+    hp = opt.hp
+    hps = [float(hp[k]) for k in ('momentum', 'rho', 'rms_mom', 'rms_eps', 'b1', 'b2', 'adam_eps', 'ad_rho', 'ad_eps')]
+    plan, nwg, jobs, nfc, _ = ex._wg_plan(wg, net.grad, dev)
+    nint = ex.ext.UPD_JOB_INTS
+    jf = jobs[:nfc * nint]
+    s0 = opt.slots[0] if opt.slots else net.online.flat
+    s1 = opt.slots[1] if len(opt.slots) > 1 else net.online.flat
+    base = (net.online.flat, net.grad, s0, s1, opt.beta_powers, opt.ticket, float(opt.lr), float(opt.reg_param),
+            int(opt.layout.reg_end), 1.0, net.global_step, hps)
+    p, pt = ex.packed(net.online.flat), ex.packed(net.target.flat)
+    fca = [int(fc[0]), int(fc[1]), int(fc[2]), ex.FLAT, ex.HH]
+    spec = rep.next_sample_spec(32)
+    smp = list(spec['spec']) + [int(spec['B'])] if spec['kind'] == 'uniform' else []
+    op = kernel_op(opt)
+
+    def launch(jobs, fcx, wgp=0, nb=0, sample=(), nj=None):
+        ex.ext.optim_pack(op, *base, jobs, p, net.target.flat, pt, 1 << 30, ex.opt_max_grid, None, None, None, None,
+                          list(sample), [], [], None, None, None, None, fcx, 0, wg=wgp, wg_blocks=nb,
+                          wg_jobs=nfc if nj is None else nj)
+
+    def timeit(fn):
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return round(a.elapsed_time(b) * 1000.0 / iters, 2)
+
+    out = {'wg_blocks': nwg, 'fc_jobs': nfc, 'jobs': jobs.numel() // nint}
+    out['wgrad_group'] = timeit(lambda: ex.ext.qnet_wgrad_group(members, dims, scales))
+    out['F'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg, sample=smp))
+    out['F_nosampler'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg))
+    out['F_wgrad_only'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg, nj=1))
+    out['F_fc_only'] = timeit(lambda: launch(jf, fca))
+    # (the previous single launch reads every gradient from the flat buffer: fc jobs as well)
+    jall = ex._upd_jobs(dev)
+    out['fused_old'] = timeit(lambda: launch(jall, fca, sample=smp))
+    for cc in (1, 4):                     # chunks per conv tile (the executor's default: 2)
+        ex.wg_conv_chunks = cc
+        ex._wg_plans = {}
+        pl2, n2, j2, _, _ = ex._wg_plan(wg, net.grad, dev)
+        out['F_chunks%d' % cc] = timeit(lambda: launch(j2, fca, pl2.data_ptr(), n2, sample=smp))
+        out['wg_blocks_chunks%d' % cc] = n2
+    ex.wg_conv_chunks = 2
+    ex._wg_plans = {}
+    plan, nwg, jobs, nfc, _ = ex._wg_plan(wg, net.grad, dev)
+    if os.environ.get('DQN_OPT_PROF'):
+        out['timeline_us'] = timeline(ex, plan, nwg, jf, nfc, nint, lambda: launch(jobs, fca, plan.data_ptr(), nwg,
+                                                                                 sample=smp))
+        out['timeline_wgrad_only_us'] = timeline(ex, plan, nwg, jf[:nint], 1, nint,
+                                                 lambda: launch(jobs, fca, plan.data_ptr(), nwg, nj=1))
+        # phases inside the tiles of that launch (us after each tile's start): staged chunk 0 |
+        # chunk 0 MFMAs | staged chunk 1 | chunk 1 MFMAs | results issued | drained
+        ph = ex.ext.optim_tile_phases(min(nwg, 512))
+        rows = [[(ph[8 * b + i] - ph[8 * b]) / 100.0 if ph[8 * b + i] else None for i in (1, 2, 3, 4, 6, 7)]
+                for b in range(len(ph) // 8)]
+        mem = [int(m[0]) for m in members]
+        def med(v):
+            v = sorted(x for x in v if x is not None)
+            return round(v[len(v) // 2], 2) if v else None
+        bounds, lo = [], 0
+        for m in members:
+            pass
+        out['tile_phases_us'] = {'first_conv1_tiles': rows[:3],
+                                 'median_all': [med([r[i] for r in rows]) for i in range(6)]}
+    print(json.dumps(out))
+
+
+def timeline(ex, plan, nwg, jobs, nfc, nint, fn):
+    """Per-block [start, ready, end] (us from the first start) of one launch, summarised: the lead
+    block, each weight-gradient member (start / duration / end percentiles), the fc jobs, the
+    dependent jobs."""
+    import torch
+    if True:
+        fn()
+        torch.cuda.synchronize()
+        ngrid = 1 + nwg + jobs.numel() // nint
+        t = ex.ext.optim_timeline(ngrid)
+        st = [t[3 * b] for b in range(ngrid)]
+        t0 = min(st)
+        us = lambda v: round((v - t0) / 100.0, 2)          # s_memrealtime: 100 MHz
+        tl = {'lead': [us(t[0]), us(t[1]) if t[1] else None, us(t[2])]}
+        pct = lambda v: [round(sorted(v)[int(q * (len(v) - 1))], 2) for q in (0.0, 0.5, 1.0)]
+        mem = {}
+        for b in range(1, 1 + nwg):
+            mem.setdefault(int(t[3 * b + 1]), []).append((us(t[3 * b]), (t[3 * b + 2] - t[3 * b]) / 100.0,
+                                                          us(t[3 * b + 2])))
+        tl['members'] = {str(m): {'n': len(v), 'start': pct([x[0] for x in v]), 'dur': pct([x[1] for x in v]),
+                                  'end': pct([x[2] for x in v])} for m, v in sorted(mem.items())}
+        fcb = range(1 + nwg, 1 + nwg + nfc)
+        tl['fc_jobs'] = {'start': pct([us(t[3 * b]) for b in fcb]), 'dur': pct([(t[3 * b + 2] - t[3 * b]) / 100.0
+                                                                                for b in fcb]),
+                         'end': pct([us(t[3 * b + 2]) for b in fcb])}
+        dep = range(1 + nwg + nfc, ngrid)
+        if len(dep):
+            tl['dep_jobs'] = {'start': pct([us(t[3 * b]) for b in dep]), 'ready': pct([us(t[3 * b + 1]) for b in dep]),
+                              'end': pct([us(t[3 * b + 2]) for b in dep])}
+        return tl
+
+
+if __name__ == '__main__':
+    main()

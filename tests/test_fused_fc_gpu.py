@@ -56,7 +56,9 @@ def _state(net):
 def test_deferred_fc_grad_matches_materialised(extra):
     runs = []
     for fuse in (True, False):
-        net, learner = _learner(extra, fuse)
+        # (the conv / output-layer weight gradients in their own launch in both runs: the fused
+        # weight-gradient launch is compared by test_split_update_matches_separate_wgrad)
+        net, learner = _learner(extra + ' --fuse_wgrad_update=0', fuse)
         assert learner._defer_fc == fuse
         learner.step()
         torch.cuda.synchronize()
@@ -90,6 +92,69 @@ def test_deferred_fc_grad_matches_materialised(extra):
             u, w = a3[key][o:o + k].double(), b3[key][o:o + k].double()
             assert float((u - w).norm() / (w.norm() + 1e-30)) < 1e-3, ('3 steps', key, n)
     assert torch.equal(a3['step'], b3['step'])
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', RAINBOW + ' --prioritized_replay',
+                                   '--optimizer=adam --prioritized_replay'])
+def test_split_update_matches_separate_wgrad(extra):
+    """Split update (``--fuse_wgrad_update=1``): the conv / output-layer weight gradients run in
+    the leading blocks of the optimizer's first launch beside the fc update, the other tensors
+    in a second launch -- vs the grouped weight-gradient launch before one optimizer launch.
+    Same math; the conv gradients' fp32 atomics sum 256-row chunk groups in another order."""
+    runs = []
+    for fw in (1, 0):
+        net, learner = _learner(extra + ' --fuse_wgrad_update=%d' % fw, True)
+        assert learner._defer_wgrad == bool(fw)
+        learner.step()
+        torch.cuda.synchronize()
+        assert not net.executor.pending_fc()
+        one = _state(net)
+        for _ in range(2):
+            learner.step()
+        torch.cuda.synchronize()
+        runs.append((net, one, _state(net)))
+    (na, a1, a3), (_, b1, b3) = runs
+    lay = na.layout
+    for n in lay.names:
+        o, k = lay.offsets[n], lay.numel(n)
+        for key in a1:
+            if key == 'step':
+                continue
+            x, y = a1[key][o:o + k], b1[key][o:o + k]
+            torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-7, msg=lambda m: '%s %s: %s' % (key, n, m))
+            if 'prioritized' in extra:
+                # (prioritized sampling turns the first step's rounding differences in |TD| into a
+                # different next minibatch: only the first step is comparable)
+                continue
+            u, w = a3[key][o:o + k].double(), b3[key][o:o + k].double()
+            assert float((u - w).norm() / (w.norm() + 1e-30)) < 1e-3, ('3 steps', key, n)
+    assert torch.equal(a3['step'], b3['step'])
+    assert int(a3['step']) == 3
+
+
+def test_split_update_graph_many_matches_eager():
+    """The split update captured as one-step and 8-step HIP graphs == eager steps (same
+    minibatches: the optimizer's second launch draws the next one)."""
+    states = []
+    for graph in (False, True):
+        net, learner = _learner('--fuse_wgrad_update=1', True, seed=3)
+        learner.use_graph = graph
+        for _ in range(3):                          # (graph: 2 eager warm-up steps, then a one-step graph)
+            learner.step()
+        if graph:
+            assert learner.can_step_many()
+            learner.step_many(8)
+        else:
+            for _ in range(8):
+                learner.step()
+        torch.cuda.synchronize()
+        states.append(_state(net))
+    a, b = states
+    assert torch.equal(a['step'], b['step'])
+    for key in a:
+        if key != 'step':
+            u, w = a[key].double(), b[key].double()
+            assert float((u - w).norm() / (w.norm() + 1e-30)) < 1e-3, key
 
 
 def test_rmsprop_mom_slot_written_only_when_requested():
