@@ -525,8 +525,9 @@ void ps_pull(torch::Tensor flat, int64_t snap, torch::Tensor step, int64_t snap_
 }
 
 // flat / step undefined: signal only (e.g. STOP)
+// echo != 0: the done word takes the push number from that (host-shared) push word, see the kernel
 void ps_publish(int64_t snap, c10::optional<torch::Tensor> flat, int64_t snap_step, c10::optional<torch::Tensor> step,
-                int64_t done_word, int64_t value, torch::Tensor ticket, int64_t n) {
+                int64_t done_word, int64_t value, torch::Tensor ticket, int64_t n, int64_t echo) {
   CHECK_T(ticket, torch::kInt32);
   const float* f = nullptr;
   const int64_t* s = nullptr;
@@ -542,7 +543,8 @@ void ps_publish(int64_t snap, c10::optional<torch::Tensor> flat, int64_t snap_st
   TORCH_CHECK(done_word && (s == nullptr || snap_step), "ps_publish args");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ticket.device());
   launch_ps_publish(reinterpret_cast<float*>(snap), f, (long)n, reinterpret_cast<int64_t*>(snap_step), s,
-                    reinterpret_cast<uint64_t*>(done_word), (uint64_t)value, ptr<int32_t>(ticket), cur_stream());
+                    reinterpret_cast<uint64_t*>(done_word), (uint64_t)value, ptr<int32_t>(ticket),
+                    reinterpret_cast<const uint64_t*>(echo), cur_stream());
 }
 
 // grad: fp32 GPU slice to reduce in place; data/sig: one pointer per rank (mine included)
@@ -697,6 +699,7 @@ int64_t mlp_lds_bytes(std::vector<int64_t> ints) {
 
 void register_infer_server(pybind11::module_& m);   // infer_server.cpp
 void register_ingest_server(pybind11::module_& m);  // ingest_server.cpp
+void register_ps_server(pybind11::module_& m);      // ps_server.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dist_dqn_amd native extension (gfx950 HIP kernels + C++ host runtime)";
@@ -709,7 +712,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tensor_from_ptr", &tensor_from_ptr);
   m.def("ps_push", &ps_push);
   m.def("ps_pull", &ps_pull);
-  m.def("ps_publish", &ps_publish);
+  m.def("ps_publish", &ps_publish, pybind11::arg("snap"), pybind11::arg("flat"), pybind11::arg("snap_step"),
+        pybind11::arg("step"), pybind11::arg("done_word"), pybind11::arg("value"), pybind11::arg("ticket"),
+        pybind11::arg("n"), pybind11::arg("echo") = 0);
   m.def("xgmi_free", &xgmi_free);
   m.def("xgmi_ipc_handle", &xgmi_ipc_handle);
   m.def("xgmi_ipc_open", &xgmi_ipc_open);
@@ -775,4 +780,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_net_ops(m);
   register_infer_server(m);
   register_ingest_server(m);
+  register_ps_server(m);
 }

@@ -97,7 +97,7 @@ struct XgmiArgs {
   void* data[kXgmiMaxRanks];       // every rank's staging buffer (2 parities x cap elements), peer-mapped
   uint32_t* sig[kXgmiMaxRanks];    // every rank's signal words [kXgmiMaxRanks][kXgmiMaxBlocks], peer-mapped
   uint32_t* seq;                   // this rank's per-block call counters [kXgmiMaxBlocks]
-  int* err;                        // set to 1 by a block whose wait timed out
+  int* err;                        // [4]: the first timed-out wait (xgmi_dev.h wait_all), 0 = none
   float* grad;                     // local gradient (in: my addend, out: the sum)
   long n;                          // elements to reduce (n % (4 * world) == 0)
   // nr > 0: the reduced vector is the concatenation of nr ranges grad[rlo[r], rlo[r] + len_r)
@@ -130,7 +130,7 @@ void launch_ps_pull(float* flat, const float* snap, long n, int64_t* step, const
                     const uint64_t* done_word, const int64_t* seq, int64_t* gate, int32_t* err, int32_t* stopped,
                     long long timeout_ns, hipStream_t st);
 void launch_ps_publish(float* snap, const float* flat, long n, int64_t* snap_step, const int64_t* step,
-                       uint64_t* done_word, uint64_t value, int32_t* ticket, hipStream_t st);
+                       uint64_t* done_word, uint64_t value, int32_t* ticket, const uint64_t* echo, hipStream_t st);
 
 // Fused MLP Q-network (reference SimpleNetwork), csrc/kernels/mlp.hip.
 namespace dqn {

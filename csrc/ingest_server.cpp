@@ -2,11 +2,13 @@
 // their SPSC rings (csrc/host/spsc_ring.cpp) into the HBM replay, so the learner's Python thread
 // only replays learner graphs. Per staging set (pinned host memory, several in rotation):
 //   dqn_apex_ingest per actor ring (frames, frame-slot stacks, n-step fold: apex_ingest.cpp)
-//   -> on flush: an event recorded on the learner stream makes the copy stream wait for the
-//      learner work queued so far (it may still read the ring slots being overwritten), the
-//      H2D copies of the frame range and the transition columns (wrap-split), the PER insert
-//      at max priority, the new size into the device size word, then an event the learner
-//      stream waits on (its next launches see the new transitions).
+//   -> on flush: the H2D copies of the frame range and the transition columns (wrap-split), the
+//      PER insert at max priority and the new size into the device size word, all submitted ON
+//      THE LEARNER STREAM: in stream order with every learner graph, so no learner launch can
+//      sample a half-overwritten slot or race the sum-tree insert (a side stream ordered by
+//      events is not enough: launches the learner thread submits between the two events would
+//      run beside the copies). Copies from pinned memory are cheap to submit; the learner
+//      thread keeps submitting its graphs meanwhile (HIP serialises submissions per stream).
 // A staging set is refilled only after its copies completed (its event). Semantics match
 // DeviceReplay.ingest_rings + flush (replay/device.py), which the Python path keeps.
 // The reference's actor is the worker's own episode loop feeding a Python deque
@@ -188,18 +190,16 @@ class IngestServer {
   void ring_copy(T* dst, int64_t cap, int64_t first, const T* src, int64_t n, int64_t row) {
     const int64_t end = first + n;
     if (end <= cap) {
-      HIPCK(hipMemcpyAsync(dst + first * row, src, sizeof(T) * (size_t)(n * row), hipMemcpyHostToDevice, cs_));
+      HIPCK(hipMemcpyAsync(dst + first * row, src, sizeof(T) * (size_t)(n * row), hipMemcpyHostToDevice, learner_));
     } else {
       const int64_t a = cap - first;
-      HIPCK(hipMemcpyAsync(dst + first * row, src, sizeof(T) * (size_t)(a * row), hipMemcpyHostToDevice, cs_));
-      HIPCK(hipMemcpyAsync(dst, src + a * row, sizeof(T) * (size_t)((n - a) * row), hipMemcpyHostToDevice, cs_));
+      HIPCK(hipMemcpyAsync(dst + first * row, src, sizeof(T) * (size_t)(a * row), hipMemcpyHostToDevice, learner_));
+      HIPCK(hipMemcpyAsync(dst, src + a * row, sizeof(T) * (size_t)((n - a) * row), hipMemcpyHostToDevice, learner_));
     }
   }
 
   void flush(StageSet& s) {
     if (s.nf == 0 && s.nt == 0) return;
-    HIPCK(hipEventRecord(ev_learner_, learner_));        // the learner work queued so far ...
-    HIPCK(hipStreamWaitEvent(cs_, ev_learner_, 0));      // ... runs before the slots are overwritten
     if (s.nf) ring_copy(frames_d_, num_frames_, s.f_first, s.frames, s.nf, hw_);
     const int64_t n = s.nt;
     if (n) {
@@ -219,15 +219,14 @@ class IngestServer {
       size_ = std::min(cap_, size_ + n);
       if (P_ > 0) {                                      // new transitions enter at max priority
         for (int64_t i = 0; i < n; ++i) s.pidx[i] = (int32_t)((first + i) % cap_);
-        HIPCK(hipMemcpyAsync(s.pidx_dev, s.pidx, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, cs_));
-        launch_sumtree_set(sum_, mn_, maxp_, s.pidx_dev, maxp_, 0.f, 0.f, 1, (int)n, P_, cs_);
+        HIPCK(hipMemcpyAsync(s.pidx_dev, s.pidx, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, learner_));
+        launch_sumtree_set(sum_, mn_, maxp_, s.pidx_dev, maxp_, 0.f, 0.f, 1, (int)n, P_, learner_);
       }
       int32_t* sw = s.cols + 5 * stage_cap_;
       *sw = (int32_t)size_;
-      HIPCK(hipMemcpyAsync(size_d_, sw, sizeof(int32_t), hipMemcpyHostToDevice, cs_));
+      HIPCK(hipMemcpyAsync(size_d_, sw, sizeof(int32_t), hipMemcpyHostToDevice, learner_));
     }
-    HIPCK(hipEventRecord(s.done, cs_));
-    HIPCK(hipStreamWaitEvent(learner_, s.done, 0));      // the learner's next launches see them
+    HIPCK(hipEventRecord(s.done, learner_));            // (the staging set is reusable after it)
     s.busy = true;
     size_pub_.store(size_, std::memory_order_relaxed);
     flushes_ += 1;
@@ -242,8 +241,6 @@ class IngestServer {
         CPU_SET(cpu_, &set);
         pthread_setaffinity_np(pthread_self(), sizeof(set), &set);   // (best effort)
       }
-      HIPCK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
-      HIPCK(hipEventCreateWithFlags(&ev_learner_, hipEventDisableTiming));
       int cur = 0;
       StageSet* s = &acquire(cur);
       int64_t first_actor = 0;
@@ -297,8 +294,6 @@ class IngestServer {
       }
       for (auto& t : sets_)
         if (t.busy) HIPCK(hipEventSynchronize(t.done));
-      hipStreamDestroy(cs_);
-      hipEventDestroy(ev_learner_);
     } catch (const std::exception& e) {
       err_ = e.what();
     }
@@ -310,8 +305,6 @@ class IngestServer {
   int64_t words_;
   double gamma_;
   hipStream_t learner_;
-  hipStream_t cs_ = nullptr;
-  hipEvent_t ev_learner_ = nullptr;
   uint8_t* frames_d_;
   int32_t *sidx_d_, *nidx_d_, *act_d_, *size_d_;
   float *rew_d_, *done_d_, *gam_d_;

@@ -96,10 +96,13 @@ ps_pull_kernel(float4* __restrict__ flat, const float4* __restrict__ snap, long 
   if (blockIdx.x == 0 && threadIdx.x == 0) step[0] = snap_step[0];
 }
 
-// PS: flat -> worker snapshot (+ step), then done word = value (system-scope release, last block)
+// PS: flat -> worker snapshot (+ step), then done word = value (system-scope release, last block).
+// echo != nullptr: value = (*echo & ~15) | (value & 15), i.e. the push number the worker published in
+// its push word -- the launch then has fixed arguments and replays from a captured graph per worker
+// (the native server thread, csrc/ps_server.cpp); the worker pushes again only after this answer.
 __global__ void __launch_bounds__(kPsThreads)
 ps_publish_kernel(float4* __restrict__ snap, const float4* __restrict__ flat, long n4, int64_t* snap_step,
-                  const int64_t* step, uint64_t* done_word, uint64_t value, int32_t* ticket) {
+                  const int64_t* step, uint64_t* done_word, uint64_t value, int32_t* ticket, const uint64_t* echo) {
   if (flat != nullptr)
     for (long i = (long)blockIdx.x * kPsThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kPsThreads)
       snap[i] = flat[i];
@@ -110,6 +113,7 @@ ps_publish_kernel(float4* __restrict__ snap, const float4* __restrict__ flat, lo
     const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {
       __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (echo != nullptr) value = (ld_acquire_sys(echo) & ~(uint64_t)15) | (value & 15);
       __threadfence_system();
       st_release_sys(done_word, value);
     }
@@ -142,9 +146,9 @@ void launch_ps_pull(float* flat, const float* snap, long n, int64_t* step, const
 }
 
 void launch_ps_publish(float* snap, const float* flat, long n, int64_t* snap_step, const int64_t* step,
-                       uint64_t* done_word, uint64_t value, int32_t* ticket, hipStream_t st) {
+                       uint64_t* done_word, uint64_t value, int32_t* ticket, const uint64_t* echo, hipStream_t st) {
   const long n4 = n / 4;
   hipLaunchKernelGGL(dqn::ps_publish_kernel, dim3(flat != nullptr ? dqn::ps_grid(n4) : 1), dim3(dqn::kPsThreads),
                      0, st, reinterpret_cast<float4*>(snap), reinterpret_cast<const float4*>(flat), n4, snap_step,
-                     step, done_word, value, ticket);
+                     step, done_word, value, ticket, echo);
 }

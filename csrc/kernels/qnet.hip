@@ -1017,39 +1017,8 @@ using NatD3 = DgradLoader<64, 3, 3, 1>;
 using NatD2 = DgradLoader<64, 4, 4, 2>;
 using NatF1 = FrameLoader<8, 8, 4>;
 
-// Tile-variant sweep (DQN_TILES="kind:variant,..." read once): A/B measurements of the
-// latency-bound layer GEMMs without a rebuild; variant 0 = the default tiles below.
-static int tile_variant(int kind) {
-  static int v[16] = {-1};
-  if (v[0] == -1) {
-    for (int i = 0; i < 16; ++i) v[i] = 0;
-    if (const char* s = getenv("DQN_TILES")) {
-      int k, x, n = 0;
-      while (sscanf(s, "%d:%d%n", &k, &x, &n) == 2) {
-        if (k > 0 && k < 16) v[k] = x;
-        s += n;
-        if (*s == ',') ++s;
-      }
-    }
-  }
-  return kind > 0 && kind < 16 ? v[kind] : 0;
-}
-
 // layer kinds: see dqn_nets_k.h.  Tiles: (MT, NT, WM, WN, KSPLIT, EPI)
 int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
-  switch (tile_variant(kind) * 100 + kind) {
-    // ---- sweep variants (DQN_TILES; r2 sweep: profiles/r2_tile_sweep.md): the previous defaults
-    case 100 + L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 0, 13); return 0;   // 32-row blocks
-    case 200 + L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 4, 0, 13); return 0;   // 16 x 32, split-K 4
-    case 100 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 2, 2, 2, 8); return 0;
-    // 16 x 16 blocks, split-K 4: round-3 A/B +0.8-1.0% (profiles/r3_tile_sweep.md); default once the
-    // GPU suite has run with it
-    case 200 + L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 4, 2, 4); return 0;
-    case 100 + L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 4, 2, 1, 2, 2, 9); return 0;
-    case 100 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 1, 1, 4, 2, 8); return 0;         // 16 rows, split-K 4
-    case 200 + L_NAT_CONV2_DGRAD: IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;         // all 16 taps (pre-parity)
-    default: break;
-  }
   switch (kind) {
     // ---- forward, fused bias + ReLU, bf16 NHWC out
     case L_NAT_CONV1_FWD: IGEMM_LAUNCH(NatC1, 1, 2, 4, 1, 1, 0); return 0;       // K 256: 8 k-steps
@@ -1065,7 +1034,7 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 2, 1, 2, 2, 2, 9); return 0;     // 18 k-steps, 16 x 64 blocks
     case L_NAT_CONV2_DGRAD:
       // parity-class dgrad (8 k-steps of real taps instead of 32 with 3/4 zeros); the generic
-      // igemm path stays as DQN_TILES="8:2" (A/B) and for shapes the class kernel does not cover
+      // igemm path for shapes the class kernel does not cover
       if (a.N16 == 2 && a.IH % 2 == 0 && a.IW % 2 == 0 && a.pad_t == 0 && a.pad_l == 0 && a.zero_ptr == nullptr &&
           a.nz_out0 == nullptr && a.loss_parts == nullptr && 2 * a.OH + 2 == a.IH && 2 * a.OW + 2 == a.IW) {
         const int cmt = ((a.IH / 2) * (a.IW / 2) + 15) / 16, B = a.M / (a.IH * a.IW);
@@ -1095,16 +1064,10 @@ int launch_wgrad(int kind, const ConvArgs& a, const WgradArgs& g, hipStream_t st
     case L_HEAD_WGRAD: WGRAD_LAUNCH(DenseLoader, 32, 64, 64); return 0;
     case L_DENSE_WGRAD_LR: {                     // ONE block per weight tile over all g.mloop 64-row chunks
       if (g.mloop < 1 || 64 * g.mloop < a.M) return -1;
-      // tiles per block: 32 x 64 (default: 784 blocks for Nature's fc, measured 11.0 vs 11.7 us at
-      // W = 8 alone) or 64 x 128 (DQN_LR_KB=64)
-      static const int kb = getenv("DQN_LR_KB") ? atoi(getenv("DQN_LR_KB")) : 32;
-      if (kb == 32) {
-        dim3 grid(1, (a.K + 31) / 32, (g.N + 63) / 64);
-        hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 32, 64>), grid, dim3(256), 0, st, a, g);
-      } else {
-        dim3 grid(1, (a.K + 63) / 64, (g.N + 127) / 128);
-        hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 64, 128>), grid, dim3(256), 0, st, a, g);
-      }
+      // tiles per block: 32 x 64 (784 blocks for Nature's fc; measured 11.0 vs 11.7 us for 64 x 128
+      // at W = 8 alone, round 2)
+      dim3 grid(1, (a.K + 31) / 32, (g.N + 63) / 64);
+      hipLaunchKernelGGL((wgrad_multi_kernel<DenseLoader, 64, 32, 64>), grid, dim3(256), 0, st, a, g);
       return 0;
     }
     default: return -1;
@@ -1149,12 +1112,10 @@ DQN_DEV void group_member(const ConvArgs& a, const WgradArgs& g, int b, int gx, 
 #endif
 }
 
-// conv members' M-chunk: 128 rows (kind as is) keeps a block's LDS at <= 40 KB (4 blocks / CU);
-// 256 rows (kind | kGrpMC256: 80 KB, 2 blocks / CU, half the blocks and atomic partials) is the
-// launcher's other choice (DQN_WGRAD_MC=128|256, default chosen per group size)
+// conv members' M-chunk: 128 rows (kind as is: the fp32 build, whose 256-row staging would not
+// fit twice per CU, and the deterministic partial members) or 256 rows (kind | kGrpMC256: 80 KB,
+// 2 blocks / CU, half the blocks and atomic partials: the 16-bit builds)
 constexpr int kGrpMC256 = 0x40;
-// default M-chunks per block of the conv members with atomics (conv1, conv2, conv3)
-constexpr int kWgradMloop[3] = {1, 1, 1};
 #define GRP_CONV_CASES(OFF, MC)                                                                                    \
   case L_NAT_CONV1_FWD + OFF: group_member<NatC1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
   case L_NAT_CONV1_FRAMES + OFF: group_member<NatF1, MC, 64, 32>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break; \
@@ -1207,21 +1168,12 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
   // conv M-chunk: 256 rows (half the blocks and half the fp32 atomic bytes of 128-row chunks;
   // measured round 3, alternating on one box: flagship 13.87k vs 13.60k SGD steps/s, Rainbow
   // 7.88k vs 7.77k, profiles/r3_wgrad_mc.md) in the 16-bit builds; 128 in the fp32 build (its
-  // 256-row staging is 135 KB of LDS: one block per CU). DQN_WGRAD_MC=128|256 overrides.
-  static const int mc_env = getenv("DQN_WGRAD_MC") ? atoi(getenv("DQN_WGRAD_MC")) : 0;
-  const bool mc256 = mc_env == 256 || (mc_env == 0 && !DQN_ACT_F32);
+  // 256-row staging is 135 KB of LDS: one block per CU).
+  const bool mc256 = !DQN_ACT_F32;
   for (int i = 0; i < G.n; ++i) {
     if (G.g[i].part != nullptr) continue;       // (partial members: 128-row chunks, see below)
     if (mc256 && G.kind[i] >= L_NAT_CONV1_FWD && G.kind[i] <= L_NAT_CONV3_FWD) G.kind[i] += kGrpMC256;
     else if (mc256 && G.kind[i] == L_NAT_CONV1_FRAMES) G.kind[i] += kGrpMC256;
-  }
-  // conv members' M-chunks per block with atomics (DQN_WGRAD_MLOOP="conv1,conv2,conv3", default
-  // kWgradMloop): one set of fp32 atomics per chunk group instead of per chunk
-  static int mlo[3] = {-1, -1, -1};
-  if (mlo[0] < 0) {
-    mlo[0] = kWgradMloop[0]; mlo[1] = kWgradMloop[1]; mlo[2] = kWgradMloop[2];
-    if (const char* e = getenv("DQN_WGRAD_MLOOP")) sscanf(e, "%d,%d,%d", &mlo[0], &mlo[1], &mlo[2]);
-    for (int q = 0; q < 3; ++q) mlo[q] = mlo[q] < 1 ? 1 : (mlo[q] > 64 ? 64 : mlo[q]);
   }
   for (int i = 0; i < G.n; ++i) {
     int MC, KB, NB;
@@ -1232,24 +1184,13 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
     if (G.g[i].part != nullptr) {               // chunk groups of mloop chunks, one partial each
       if (DQN_ACT_F32 || MC != 128 || G.g[i].mloop < 1 || G.g[i].pstride < G.a[i].K * G.g[i].N + G.g[i].N) return -3;
       G.gx[i] = (G.gx[i] + G.g[i].mloop - 1) / G.g[i].mloop;
-    } else if (!DQN_ACT_F32) {
-      const int kb = G.kind[i] & ~kGrpMC256;
-      const int li = (kb == L_NAT_CONV1_FWD || kb == L_NAT_CONV1_FRAMES) ? 0 : kb == L_NAT_CONV2_FWD ? 1
-                     : kb == L_NAT_CONV3_FWD ? 2 : -1;
-      G.g[i].mloop = 1;
-      if (li >= 0 && mlo[li] > 1 && (G.kind[i] & kGrpMC256) == 0) {     // (128-row members only)
-        G.g[i].mloop = mlo[li];
-        G.gx[i] = (G.gx[i] + mlo[li] - 1) / mlo[li];
-      }
+    } else {
+      G.g[i].mloop = 1;                          // (one M-chunk per block, fp32 atomics across chunks)
     }
     G.gy[i] = (G.a[i].K + KB - 1) / KB;
     const int gz = (G.g[i].N + NB - 1) / NB;
     G.nblk[i] = G.gx[i] * G.gy[i] * gz;
     G.g[i].atomic = G.gx[i] > 1 && G.g[i].part == nullptr ? 1 : 0;
-    // timing probe only (wrong gradients): DQN_WGRAD_PROBE_NOATOMIC=1 stores the M-chunk partials
-    // plainly, to price the fp32 atomics of the multi-chunk members
-    static const bool noatomic = getenv("DQN_WGRAD_PROBE_NOATOMIC") != nullptr;
-    if (noatomic) G.g[i].atomic = 0;
     total += G.nblk[i];
     lds = l > lds ? l : lds;
   }

@@ -361,7 +361,6 @@ using namespace dqn;
 
 void launch_trunk_fwd(const TrunkArgs& a, int B, int ninst, hipStream_t st) {
   // row split whenever the per-sample grid leaves CUs idle (the learner's 3-4 x 32 samples)
-  static const int force = getenv("DQN_TRUNK_SPLIT") ? atoi(getenv("DQN_TRUNK_SPLIT")) : -1;
-  const int split = force >= 1 ? (force > 1 ? 2 : 1) : (B * ninst <= 192 ? 2 : 1);
+  const int split = B * ninst <= 192 ? 2 : 1;
   hipLaunchKernelGGL(trunk_fwd_kernel, dim3(B, ninst, split), dim3(512), 0, st, a);
 }

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
     }
   }
   signal_all(a, b, 2u * k + 1u);
-  if (!wait_all(a, b, 2u * k + 1u)) return;
+  if (!wait_all(a, b, 2u * k + 1u, kXgmiPhaseReduceScatter)) return;
 
   // ---- B: reduce my slice over all ranks' staging (fixed rank order: identical sums everywhere)
   int rcb = first_range((long)r * sv + lo);
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(XgmiArgs a) {
     *gv(i, rcb) = make_float4(acc.x, acc.y, acc.z, acc.w);
   }
   signal_all(a, b, 2u * k + 2u);
-  if (!wait_all(a, b, 2u * k + 2u)) return;
+  if (!wait_all(a, b, 2u * k + 2u, kXgmiPhaseAllGather)) return;
 
   // ---- C: gather the other slices from their owners (one range cursor per peer slice)
   int rcs[WC ? WC : kXgmiMaxRanks];

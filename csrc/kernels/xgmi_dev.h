@@ -24,8 +24,13 @@ DQN_DEV void signal_all(const XgmiArgs& a, int b, uint32_t val) {
   if (t < a.world) store_rel(a.sig[t] + a.rank * kXgmiMaxBlocks + b, val);
 }
 
+// Which wait of which call timed out (the error word's first report wins; err[1..3] then hold the
+// expected flag value, the value last seen and the call's per-block counter):
+//   err[0] = 1 << 31 | phase << 24 | peer << 16 | block
+constexpr int kXgmiPhaseReduceScatter = 1, kXgmiPhaseAllGather = 2, kXgmiPhaseGather = 3;
+
 // wait until every peer raised flag >= val for block b; false on timeout
-DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val) {
+DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val, int phase) {
   const int t = threadIdx.x;
   __shared__ int timed_out;
   if (t == 0) timed_out = 0;
@@ -33,10 +38,16 @@ DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val) {
   if (t < a.world) {
     const uint32_t* f = a.sig[a.rank] + t * kXgmiMaxBlocks + b;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(load_acq(f) - val) < 0) {
+    uint32_t seen;
+    while ((int32_t)((seen = load_acq(f)) - val) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kXgmiTimeoutTicks) {
-        atomicExch(a.err, 1);
+        const int code = (int)(0x80000000u | ((uint32_t)phase << 24) | ((uint32_t)t << 16) | (uint32_t)b);
+        if (atomicCAS(a.err, 0, code) == 0) {
+          a.err[1] = (int)val;
+          a.err[2] = (int)seen;
+          a.err[3] = (int)a.seq[b];
+        }
         timed_out = 1;
         break;
       }
@@ -70,7 +81,7 @@ DQN_DEV void xgmi_gather_block(const XgmiGatherArgs& g, int b, int G) {
   uint4* mine = stage(r);
   for (long v = lo + t; v < hi; v += NT) mine[v] = v < v0 ? s0[v] : s1[v - v0];
   signal_all(a, b, k + 1u);
-  if (!wait_all(a, b, k + 1u)) return;
+  if (!wait_all(a, b, k + 1u, kXgmiPhaseGather)) return;
   uint4* o0 = reinterpret_cast<uint4*>(g.out[0]);
   uint4* o1 = reinterpret_cast<uint4*>(g.out[1]);
   for (long v = lo + t; v < hi; v += NT) {

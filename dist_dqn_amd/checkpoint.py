@@ -144,6 +144,13 @@ class CheckpointManager:
     def _opt(self):
         return getattr(self.network, 'optimizer', None)
 
+    def arm_slots(self):
+        """Store the optimizer's deferred slots on the following steps (until the next save)."""
+        opt = self._opt()
+        if self.is_chief and not self._armed and getattr(opt, 'defers_slots', False):
+            opt.request_slots(True)
+            self._armed = True
+
     def maybe_save(self, force: bool = False) -> Optional[str]:
         """Save when due (or ``force``: synchronous). Returns the checkpoint path, or None when
         nothing was saved yet or the writer thread is writing it (``wait()`` joins it and returns

@@ -486,6 +486,12 @@ class Learner:
         its last consistent checkpoint."""
         if self.reducer.xgmi is not None:
             self.reducer.check()
+        # async PS over xgmi: a pull / push whose peer wait timed out left this worker's
+        # parameters un-pulled (the kernel flags it instead of hanging)
+        chk = getattr(self.ps, 'check', None)
+        if chk is not None and not chk():
+            raise RuntimeError('async parameter server: a peer wait timed out (server stalled or gone) '
+                               'at step %d' % self.train_steps)
         t = getattr(self.net.optimizer, 'ticket', None)
         if t is not None and t.is_cuda and t.numel() > 2 and int(t[2].item()) != 0:
             raise RuntimeError('fused optimizer: an end-of-launch arrival wait gave up (step %d)' % self.train_steps)

@@ -20,10 +20,14 @@ class TorchExecutor:
     compute_dtype = 'fp32'
 
     def __init__(self, arch: ArchSpec, layout: FlatLayout, input_scale: float = 1.0,
-                 loss: str = 'mse', huber_delta: float = 1.0, double_dqn: bool = False):
+                 loss: str = 'mse', huber_delta: float = 1.0, double_dqn: bool = False, oracle: bool = False):
+        """oracle=True: every op in PyTorch, the TD loss included (the numerics reference the HIP
+        kernels are tested against); otherwise the TD loss on cuda tensors runs the fused
+        td_loss kernel (the `simple` MLP's GPU training path)."""
         self.arch, self.layout = arch, layout
         self.input_scale = input_scale
         self.loss_kind, self.delta, self.double = loss, huber_delta, double_dqn
+        self.oracle = bool(oracle)
 
     def forward(self, flat: torch.Tensor, x: torch.Tensor, noise: Optional[torch.Tensor] = None):
         with torch.no_grad():
@@ -46,7 +50,7 @@ class TorchExecutor:
         from ..ops.td import td_loss
         loss, prio = td_loss(out, batch['actions'], batch['rewards'], batch['dones'], batch['gammas'], nt, no,
                              batch.get('weights'), self.loss_kind, self.delta, arch.distributional,
-                             arch.v_min, arch.v_max)
+                             arch.v_min, arch.v_max, pure_torch=self.oracle)
         g, = torch.autograd.grad(loss, flat)
         grad_out.copy_(g)
         return loss.detach().view(1), prio

@@ -106,9 +106,8 @@ class HipExecutor:
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
         # (round 2 measured the fc + output-layer members on a parallel graph branch beside the dgrad
         # chain: 12.0k -> 9.9k steps/s, the captured fork / join costs more than the overlap gains)
-        # fused optimizer+pack grid: <= 256 = grid-stride with a flat ticket; larger = one block
-        # per 32x64 tile with the two-level ticket (DQN_OPT_GRID overrides, for A/B runs)
-        self.opt_max_grid = int(os.environ.get('DQN_OPT_GRID', '2048'))
+        # fused optimizer+pack grid cap (one block per 32x64 tile; grid-stride beyond it)
+        self.opt_max_grid = 2048
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_head.py)
         self._events = {}

@@ -42,9 +42,10 @@ class _TDLossHip(torch.autograd.Function):
 
 def td_loss(out: torch.Tensor, actions, rewards, dones, gammas, next_t, next_o=None,
             weights: Optional[torch.Tensor] = None, kind: str = 'mse', delta: float = 1.0,
-            distributional: bool = False, v_min: float = -10.0, v_max: float = 10.0):
-    """Returns (mean loss [scalar], per-sample priority [B])."""
-    if out.is_cuda:
+            distributional: bool = False, v_min: float = -10.0, v_max: float = 10.0, pure_torch: bool = False):
+    """Returns (mean loss [scalar], per-sample priority [B]). pure_torch: the torch oracle on any
+    device (the numerics reference of the HIP kernels)."""
+    if out.is_cuda and not pure_torch:
         loss, prio = _TDLossHip.apply(out, actions, rewards, dones, gammas, next_t, next_o, weights, kind, delta,
                                       distributional, v_min, v_max)
         return loss.view(()), prio

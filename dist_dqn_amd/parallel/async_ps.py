@@ -348,7 +348,14 @@ class XgmiPSServer:
                                self.net.global_step if st else None, self.sh.done_word(w), (seq << 4) | status,
                                self._ticket, self.n)
 
-    def serve(self, max_updates: int = 0, idle_sleep: float = 2e-5, supervisor=None) -> int:
+    def serve(self, max_updates: int = 0, idle_sleep: float = 2e-5, supervisor=None, native: bool = True) -> int:
+        """Answer the workers' pushes until every worker left (or ``max_updates``). native: a C++
+        thread (csrc/ps_server.cpp) polls the control page and replays one captured graph per
+        push (fused optimizer on the slot in place + snapshot / step / done word); the Python
+        thread only relays the supervisor (stop requests, step-count hooks). Otherwise the
+        polling loop below, one eager optimizer + publish per push."""
+        if native and hasattr(self.sh.ext, 'PsServer'):
+            return self._serve_native(max_updates, supervisor)
         seen = {}
         for w in self.workers:                # initial pull (push number 1): the PS parameters
             self._publish(w, 1)
@@ -383,6 +390,54 @@ class XgmiPSServer:
                 time.sleep(idle_sleep)
         torch.cuda.synchronize(self.net.online.flat.device)
         self.busy_s = time.perf_counter() - t_busy
+        return self.updates
+
+    def _serve_native(self, max_updates: int, supervisor) -> int:
+        ext, sh, net = self.sh.ext, self.sh, self.net
+        dev = net.online.flat.device
+        for w in self.workers:                # initial pull (push number 1): the PS parameters
+            self._publish(w, 1)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        graphs = {}
+        from ..utils.capture import quiet_capture
+        with quiet_capture(), torch.cuda.stream(s):
+            for w in self.workers:
+                ga, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, stream=s, capture_error_mode='thread_local'):
+                    # arrival-order apply, the gradient read in place from worker w's slot; the
+                    # answer's push number comes from w's push word (the kernel echoes it)
+                    net.apply_grads(1.0, grad=self._grads[w])
+                    ext.ps_publish(sh.snap(w), net.online.flat, sh.snap_step(w), net.global_step, sh.done_word(w), 0,
+                                   self._ticket, self.n, echo=sh.push_word(w))
+                with torch.cuda.graph(gs, stream=s, capture_error_mode='thread_local'):
+                    ext.ps_publish(sh.snap(w), None, sh.snap_step(w), None, sh.done_word(w), _STOP_STATUS,
+                                   self._ticket, self.n, echo=sh.push_word(w))
+                graphs[w] = (ga, gs)
+        self._native_graphs = graphs          # (alive while the server replays them)
+        srv = ext.PsServer(int(sh.ctl.ctypes.data), len(self.workers), _CTL_STRIDE, s.cuda_stream, dev.index or 0)
+        for w, (ga, gs) in graphs.items():
+            srv.set_graphs(w, ga.raw_cuda_graph_exec(), gs.raw_cuda_graph_exec())
+        srv.start(int(max_updates), 1)
+        last = 0
+        try:
+            while srv.running():
+                if supervisor is not None:
+                    u = srv.updates()
+                    if u != last:
+                        last = u
+                        supervisor.on_train_step(u)
+                    if supervisor.should_stop():
+                        srv.request_stop()
+                time.sleep(1e-3)
+        finally:
+            self.updates = srv.wait()
+        _, per, stopped, busy = srv.stats()
+        self.per_worker = {w: int(per[w]) for w in self.workers}
+        self.stopped_workers = int(stopped)
+        self.busy_s = float(busy)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
         return self.updates
 
     def close(self):

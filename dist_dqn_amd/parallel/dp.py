@@ -197,8 +197,8 @@ class GradAllReducer:
     def check(self):
         """Raise if the xgmi transport reported a timed-out peer wait (host sync)."""
         if self.xgmi is not None and not self.xgmi.check():
-            raise RuntimeError('xgmi all-reduce: a peer wait timed out (rank %d, channels %s)'
-                               % (self.ctx.rank, self.xgmi.failed_channels()))
+            raise RuntimeError('xgmi all-reduce: a peer wait timed out (rank %d: %s)'
+                               % (self.ctx.rank, self.xgmi.error_info()))
 
     def close(self):
         if self.xgmi is not None:

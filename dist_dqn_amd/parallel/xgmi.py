@@ -195,6 +195,23 @@ class XgmiAllReduce:
         """Indices of the channels whose error word is set (host sync)."""
         return [c for c, ch in enumerate(self.channels) if int(ch.seq_err[self.ext.XGMI_MAX_BLOCKS]) != 0]
 
+    _PHASES = {1: 'reduce-scatter (phase A)', 2: 'all-gather (phase B)', 3: 'gather'}
+
+    def error_info(self) -> list:
+        """Per failed channel, the FIRST timed-out wait: {'channel', 'phase', 'peer', 'block',
+        'expected', 'seen', 'call'} (host sync; xgmi_dev.h wait_all)."""
+        out = []
+        M = self.ext.XGMI_MAX_BLOCKS
+        for c, ch in enumerate(self.channels):
+            w = [int(v) for v in ch.seq_err[M:M + 4].tolist()]
+            if w[0] == 0:
+                continue
+            code = w[0] & 0xffffffff
+            out.append({'channel': c, 'phase': self._PHASES.get((code >> 24) & 0x7f, (code >> 24) & 0x7f),
+                        'peer': (code >> 16) & 0xff, 'block': code & 0xffff, 'expected': w[1] & 0xffffffff,
+                        'seen': w[2] & 0xffffffff, 'call': w[3] & 0xffffffff, 'rank': self.ctx.rank})
+        return out
+
     def check(self) -> bool:
         """False if any block of any launch so far timed out waiting for a peer (host sync)."""
         return all(int(ch.seq_err[self.ext.XGMI_MAX_BLOCKS]) == 0 for ch in self.channels)

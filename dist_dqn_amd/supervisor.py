@@ -190,6 +190,11 @@ class RunSupervisor:
         self.heartbeat(step)
         self._step_counter()
         if self.ckpt is not None:
+            if self._local.is_set():
+                # a stop is pending: the final forced save follows within a few steps -- store the
+                # deferred optimizer slot (momentum-0 RMSProp `mom`, TF RMSProp_1) from now on, so
+                # that save holds the last update's value like every periodic one
+                self.ckpt.arm_slots()
             self.ckpt.maybe_save()
         if self.coordinated and step % self.stop_sync_steps == 0:
             if self.ctx.ctrl_allreduce_max(1 if self._local.is_set() else 0):

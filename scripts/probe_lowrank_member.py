@@ -28,4 +28,4 @@ for W in (1, 2, 4, 8):
         run()
     e1.record()
     torch.cuda.synchronize()
-    print('W=%d  M=%3d  kb=%s  %.2f us/launch' % (W, M, os.environ.get('DQN_LR_KB', '64'), e0.elapsed_time(e1) * 1000 / 200))
+    print('W=%d  M=%3d  %.2f us/launch' % (W, M, e0.elapsed_time(e1) * 1000 / 200))

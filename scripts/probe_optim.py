@@ -88,7 +88,6 @@ def main():
         out['fc_fused+sampler+mom'] = timeit(lambda: launch(True, True))
         net.optimizer.request_slots(False)
         out['jobs'] = len(ex.upd_items)
-    out['nt'] = int(os.environ.get('DQN_OPT_NT', '0'))
     print(json.dumps(out), flush=True)
 
 

@@ -30,7 +30,7 @@ def _setup(extra='', B=32, seed=0):
     net.executor.repack(net.online.flat)
     net.executor.repack(net.target.flat)
     net.reset_noise(generator=g)          # noisy nets: a fresh factorised noise sample
-    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss, oracle=True,
                            huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
     batch = {
         'states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
@@ -451,7 +451,7 @@ def test_rainbow_learner_keeps_online_premixed():
         ln.step()
     torch.cuda.synchronize()
     assert int(net.global_step) == 6 and bool(torch.isfinite(net.online.flat).all())
-    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss, oracle=True,
                            huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
     x = torch.randint(0, 256, (16, 84, 84, 4), dtype=torch.uint8, device=DEV)
     assert _rel(net.q_values(x), oracle.q_values(net.online.flat, x, net.noise)) < 2e-2

@@ -192,7 +192,7 @@ def test_deferred_fc_update_matches_fp32_oracle(extra):
     from dist_dqn_amd.models.executor import TorchExecutor
     net, learner = _learner(extra + ' --optimizer=sgd --lr=0.5 --fuse_sampling=0', True)
     cfg = net.config
-    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss, oracle=True,
                            huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
     w0 = net.online.flat.clone()
     tgt = net.target.flat.clone()
@@ -317,7 +317,7 @@ def test_det_wgrad_conv_update_matches_fp32_oracle():
     net, learner = _learner('--optimizer=sgd --lr=0.5 --fuse_sampling=0 --det_wgrad=1', True)
     assert learner._det_wgrad
     cfg = net.config
-    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss, oracle=True,
                            huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
     w0 = net.online.flat.clone()
     tgt = net.target.flat.clone()

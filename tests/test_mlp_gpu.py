@@ -18,7 +18,7 @@ def _setup(extra='', B=100, A=2, D=4, seed=0, weighted=False):
     g = torch.Generator(device=DEV).manual_seed(seed)
     net.online.flat.normal_(0.0, 0.4, generator=g)
     net.target.flat.normal_(0.0, 0.4, generator=g)
-    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss,
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss, oracle=True,
                            huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
     batch = {
         'states': torch.randn(B, D, device=DEV, generator=g),
