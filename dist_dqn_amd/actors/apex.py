@@ -278,6 +278,15 @@ class ApexActorPool:
     def alive(self) -> int:
         return sum(p.is_alive() for p in self.procs)
 
+    def kill_actors(self):
+        """SIGKILL every actor process this pool started (fault injection: the actors of one
+        rank die; published ring records stay valid, a half-written one is never published)."""
+        for p in self.procs:            # exact processes we started
+            if p.is_alive():
+                p.kill()
+        for p in self.procs:
+            p.join(5.0)
+
     def stop(self, timeout: float = 10.0):
         if self._closed:
             return
@@ -685,6 +694,10 @@ class ApexTrainer:
         # sync-DP Ape-X: every learner step is a collective, so local reasons to stop (time
         # budget, dead actors) become stop requests the ranks agree on (supervisor.py)
         coordinated = bool(getattr(supervisor, 'coordinated', False))
+        ctx = supervisor.ctx if coordinated else None
+        started = not coordinated
+        if supervisor is not None and hasattr(supervisor, 'fault_hooks'):
+            supervisor.fault_hooks['actors'] = self.pool.kill_actors
 
         def want_stop(reason):
             if not coordinated:
@@ -719,7 +732,14 @@ class ApexTrainer:
                 tb = time.perf_counter()
                 self.loop_time['drain'] += tb - ta
                 self.loop_time['iters'] += 1
-                if size >= start:
+                ready = size >= start
+                if not started:
+                    # sync-DP: every step is a collective, so the ranks take their first step
+                    # together, once every rank's replay shard holds `start` transitions (one
+                    # control-plane max per pre-start iteration: the ranks' collective sequences
+                    # stay matched, and no in-graph xgmi wait spins on a peer still filling)
+                    started = ready = ctx.ctrl_allreduce_max(0 if ready else 1) == 0
+                if ready:
                     if self.learn_t0 is None:
                         self.learn_t0, self.learn_frames0 = time.time(), self.pool.frames
                     if cuda and len(inflight) >= self.max_inflight:
@@ -780,6 +800,7 @@ class ApexTrainer:
                         log.warning('all actors exited')
                         break
         finally:
+            self.end_t = time.time()
             sys.setswitchinterval(switch)
             self._stop.set()
             if self._thread.is_alive():

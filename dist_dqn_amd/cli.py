@@ -159,10 +159,61 @@ def _run_apex(config: Config, ctx, env, network, sv, seed: int):
                          ring_capacity=config.apex_ring, reward_clip=config.reward_clip,
                          n_step=config.n_step, gamma=config.reward_discount)
     metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))
+    metrics.write(kind='start', rank=ctx.rank, world_size=ctx.world_size, restored_from=sv.restored_from,
+                  global_step=int(network.global_step), executor=network.executor.name,
+                  num_actors=config.num_actors)
     with sv.managed():
         trainer = ApexTrainer(network, replay, learner, pool, config, metrics=metrics)
-        trainer.run(max_train_steps=config.max_train_steps, supervisor=sv)
+        trainer.run(max_train_steps=config.max_train_steps, max_seconds=config.apex_seconds, supervisor=sv)
+    # this rank's shard: what its own actors delivered (replay contents differ across ranks)
+    metrics.write(kind='done', training_steps=learner.train_steps, global_step=int(network.global_step),
+                  env_frames=trainer.pool.frames, episodes=trainer.pool.episodes, replay_size=replay.size(),
+                  replay_digest=replay.digest() if hasattr(replay, 'digest') else None,
+                  stop_reason=sv.stop_reason, step_many=learner.can_step_many(),
+                  graph_steps=trainer.graph_steps,
+                  learn_seconds=(trainer.end_t - trainer.learn_t0) if trainer.learn_t0 is not None else 0.0,
+                  learn_frames=trainer.pool.frames - trainer.learn_frames0)
+    if ctx.enabled and not config.async_ps and config.replica_check:
+        _replica_check(ctx, network, metrics, learner.train_steps)
     return trainer
+
+
+def _probe_graph_steps(ctx, learner, G_max: int) -> int:
+    """bench.py's start-up probe for data parallelism: G = 1 vs G = ``G_max`` SGD steps per graph
+    launch (``Learner.step_many``: one graph of G step bodies whose collectives are in-graph
+    kernels), timed on every rank and MAX-reduced over the control plane so every rank takes
+    the same decision. The probe's steps are ordinary training steps."""
+    import time
+    dev = learner.device
+    for _ in range(3):                       # eager warm-up + the one-step graph capture
+        if learner._graphs is not None:
+            break
+        learner.step()
+    if not learner.can_step_many():
+        return 1
+    try:
+        learner.step_many(G_max)             # capture the G-step graph outside the timing
+    except RuntimeError as e:
+        log.warning('%d-step graph unavailable (%s); one graph per step', G_max, e)
+        torch.cuda.synchronize(dev)
+        learner.step()
+        return 1
+
+    def timed(fn):
+        ctx.ctrl_allreduce_max(0)            # line the ranks up
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        return ctx.ctrl_allreduce_max(int(1e6 * (time.perf_counter() - t0)))
+
+    n = 4 * G_max
+    t1 = timed(lambda: [learner.step() for _ in range(n)])
+    tg = timed(lambda: [learner.step_many(G_max) for _ in range(n // G_max)])
+    G = G_max if tg < t1 else 1
+    log.info('graph-steps probe (%d ranks): G=1 %.1f us/step, G=%d %.1f us/step -> G=%d', ctx.world_size,
+             t1 / n, G_max, tg / n, G)
+    return G
 
 
 def _run_device_envs(config: Config, ctx, env, network, sv, seed: int):
@@ -195,7 +246,9 @@ def _run_device_envs(config: Config, ctx, env, network, sv, seed: int):
     learner = Learner(network, replay, config, ctx, actor=actor if fused else None)
     sv.attach_learner(learner)
     learner.update_target_now()
-    G = max(1, int(config.device_graph_steps)) if fused and learner.use_graph and not ctx.enabled else 1
+    G = max(1, int(config.device_graph_steps)) if fused and learner.use_graph else 1
+    if G > 1 and ctx.enabled:
+        G = _probe_graph_steps(ctx, learner, G)
     metrics = JsonlWriter(os.path.join(config.logdir, 'metrics.rank%d.jsonl' % ctx.rank))
     writer = SummaryWriter(config.logdir) if ctx.is_chief else None
     metrics.write(kind='start', rank=ctx.rank, world_size=ctx.world_size, restored_from=sv.restored_from,

@@ -137,6 +137,8 @@ def build_parser() -> argparse.ArgumentParser:
     a('--apex_eps_base', default=0.4, type=float, help='Ape-X per-actor epsilon base')
     a('--apex_eps_alpha', default=7.0, type=float, help='Ape-X per-actor epsilon exponent spread')
     a('--apex_ring', default=1024, type=int, help='Ape-X transition ring capacity per actor (records)')
+    a('--apex_seconds', default=0.0, type=float,
+      help='Ape-X: wall-clock budget of the run (0 = none); under sync DP a coordinated stop')
     a('--apex_native_serve', default=1, type=int,
       help='Ape-X: answer the actors from a C++ thread replaying captured inference graphs (GPU)')
     a('--device_envs', default=0, type=int,
@@ -276,6 +278,7 @@ class Config:
     apex_eps_base: float = 0.4
     apex_eps_alpha: float = 7.0
     apex_ring: int = 1024
+    apex_seconds: float = 0.0
     apex_serve_gap_us: int = 100
     apex_graph_steps: int = 4
     apex_native_ingest: int = 1

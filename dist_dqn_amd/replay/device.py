@@ -187,6 +187,16 @@ class DeviceReplay:
     def __len__(self):
         return self.size()
 
+    def digest(self) -> str:
+        """Content fingerprint of the stored transitions (actions + rewards of the filled slots;
+        one device sync): tells two shards fed by different actors apart."""
+        import hashlib
+        n = min(self.size(), self.capacity)
+        h = hashlib.sha1()
+        h.update(self.actions[:n].cpu().numpy().tobytes())
+        h.update(self.rewards[:n].cpu().numpy().tobytes())
+        return h.hexdigest()[:16]
+
     # ------------------------------------------------------------- write API
     def begin_episode(self, obs, actor: int = 0):
         """Start an episode: first frame duplicated k times (reference FrameBuffer semantics)."""

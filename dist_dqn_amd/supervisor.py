@@ -57,8 +57,8 @@ def parse_fault_spec(spec: Optional[str]):
     for part in spec.split(','):
         k, _, v = part.partition(':')
         out[k.strip()] = v.strip() if k.strip() == 'mode' else int(v)
-    if out['mode'] not in ('raise', 'exit', 'stop'):
-        raise ValueError('DQN_FAULT_INJECT mode must be raise, exit or stop: %r' % spec)
+    if out['mode'] not in ('raise', 'exit', 'stop', 'actors'):
+        raise ValueError('DQN_FAULT_INJECT mode must be raise, exit, stop or actors: %r' % spec)
     return out
 
 
@@ -80,6 +80,7 @@ class RunSupervisor:
         self.ckpt = (CheckpointManager(logdir, network, is_chief, save_secs, max_to_keep, agent_state_fn)
                      if network is not None else None)
         self.fault = parse_fault_spec(os.environ.get('DQN_FAULT_INJECT'))
+        self.fault_hooks = {}                   # mode -> callable (e.g. 'actors': kill the actor pool)
         self.hb_dir = os.path.join(logdir, 'heartbeat')
         self.heartbeat_secs = heartbeat_secs
         self._last_hb = 0.0
@@ -185,6 +186,13 @@ class RunSupervisor:
                 os._exit(17)
             if f.get('mode') == 'stop':
                 self.request_stop('DQN_FAULT_INJECT stop at step %d' % step)
+            elif f.get('mode') == 'actors':
+                # this rank's actor processes die (Ape-X); the trainer notices and asks to stop
+                hook = self.fault_hooks.get('actors')
+                log.error('DQN_FAULT_INJECT: killing this rank\'s actors at step %d%s', step,
+                          '' if hook else ' (no actor pool registered: ignored)')
+                if hook:
+                    hook()
             else:
                 raise FaultInjected('injected fault at step %d (rank %d)' % (step, self.rank))
         self.heartbeat(step)
