@@ -301,7 +301,11 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     if config.job == 'ps':
         log.warning('--job=ps: no parameter server is needed (synchronous RCCL data parallelism); exiting.')
         return 0
-    run_worker(config)
+    from .parallel.dist import shutdown
+    try:
+        run_worker(config)
+    finally:
+        shutdown()      # tear the process group down before interpreter exit (gloo's threads)
     return 0
 
 

@@ -85,7 +85,8 @@ def test_cnn_forward_matches_tf_semantics():
     h = h.reshape(2, -1)
     h = np.maximum(h @ p['fcl/w'] + p['fcl/b'], 0)
     ref = h @ p['output/w'] + p['output/b']
-    np.testing.assert_allclose(q.double().numpy(), ref, rtol=1e-4, atol=1e-6)
+    # fp32 forward vs float64: errors scale with the output magnitude (~1e3), not per element
+    np.testing.assert_allclose(q.double().numpy(), ref, rtol=1e-4, atol=1e-6 * np.abs(ref).max())
 
 
 def test_grad_through_unflatten_is_flat():
