@@ -130,6 +130,17 @@ struct HeadArgs {
   void* dq16;
 };
 
+// Fused fc forward + scalar head (fc_head.hip): the output layer is folded into the fc launch's
+// epilogue (per-tile partial Q values stored into qacc [instance][Mpad][32][N / 16]), the last
+// block to arrive on a row group's counter (cnt [ngroups + 1], zero on entry and left zero; the
+// last one is the fused actors') sums them in tile order and runs the TD loss / dQ / dH tail.
+struct FoldArgs {
+  float* qacc;
+  int32_t* cnt;
+  int Mpad, ngroups, nlearn;
+  int64_t* prof;             // optional: s_memrealtime stamps [block][8] (scripts/probe_fold.py)
+};
+
 // One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =
 // mu + sigma * f(noise[ein_off + k]) * f(noise[eout_off + n]); sigma_off < 0: plain
 // copy; ein_off < 0: bias (no input factor).
@@ -228,6 +239,8 @@ int wgrad_fused_plan(dqn::WgradGroup& G, int conv_chunks);
 void launch_cnn_fwd(const dqn::CnnFwdArgs& a, int B, int ninst, hipStream_t st);
 void launch_cnn_bwd(const dqn::CnnBwdArgs& a, int B, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
+// -1: shape outside the fused kernel's range (A <= 18, HID <= 512, E <= 16, 2-3 learner instances)
+int launch_fc_head(const dqn::ConvArgs& a, const dqn::HeadArgs& h, const dqn::FoldArgs& f, hipStream_t st);
 void launch_trunk_fwd(const dqn::TrunkArgs& a, int B, int ninst, hipStream_t st);
 void launch_c51_head(const dqn::HeadArgs& a, hipStream_t st);
 size_t c51_head_lds_bytes(const dqn::HeadArgs& a);

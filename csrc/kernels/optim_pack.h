@@ -173,12 +173,14 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 // minibatch's frame-slot tables only after the member reading the current ones (conv1 from the
 // frame ring) is done -- the lowest block id, so every producer it waits for is already resident.
 // LDS: one dynamic buffer (<= 40 KB: 4 blocks / CU, as the plain update).
+// kModeWg: the weight-gradient tiles beside the update items need ~165 VGPRs: 3 waves / SIMD (at the
+// 8-blocks-per-CU bound of the plain update they spilled to scratch: 4.5x slower tiles, measured).
 // kModeFew: a launch of few work blocks (the second launch of a split update): 4 waves / SIMD
 // (128 VGPRs: no spills in the item body, occupancy is moot) and a returning arrival ticket per
 // block -- the last block to arrive closes the launch, nobody polls.
 constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8, kModeWg = 16, kModeFew = 32;
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, (MODE & kModeFew) ? 4 : (MODE & ~(kModeFc | kModeWg)) == 0 ? 8 : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+__global__ void __launch_bounds__(kPackThreads, (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? 8 : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
@@ -628,42 +630,26 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   if constexpr (WG) {
     const int b = (int)blockIdx.x - 1;
     if (b >= 0 && b < wg_blocks) {
-      // ---- a weight-gradient tile; the LAST tile of a (member, K-range) -- and of the member's
-      //      bias, for the K-range-0 tiles -- then runs the optimizer jobs of those tensors itself:
-      //      no block waits for a gradient while holding its CU slot
+      // ---- a weight-gradient tile, counted on its (member, K-range) when done (the last tile of a
+      //      range ran that range's jobs serially: ~4 of them, 8-15 us each, measured; the jobs
+      //      now wait in blocks of their own at the end of the grid and run in parallel)
       int64_t* ph = (h.prof != nullptr && b < kTilePhBlocks) ? h.prof + kProfPhases + 3 * kTlBlocks + 8 * b : nullptr;
       const int mb = fused_wgrad_block<kPackThreads>(*wg, b, reinterpret_cast<act_t*>(opt_dyn), ph);
       const int m = mb >> 8, by = mb & 255;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's atomics / write-through stores done
       if (ph != nullptr && threadIdx.x == 0) ph[7] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      __shared__ int wg_last[2];
       __syncthreads();
       if (threadIdx.x == 0) {
         if (tl) { tl[1] = m; tl[2] = (int64_t)__builtin_amdgcn_s_memrealtime(); }
-        const int want = wg->nblk[m] / wg->gy[m];        // tiles per K-range (chunk groups x N-ranges)
-        int32_t* ck = wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + by);
-        int32_t* cb = wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + kWgSlots - 1);
-        const int lk = __hip_atomic_fetch_add(ck, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want - 1;
-        const int lb = by == 0 && __hip_atomic_fetch_add(cb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want - 1;
-        if (lk) __hip_atomic_store(ck, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lb) __hip_atomic_store(cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // count the tile on its (member, K-range) and -- K-range 0 -- the member's bias range; the
+        // jobs of a range wait for its count in their own blocks (end of the grid), in parallel
+        __hip_atomic_fetch_add(wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + by), 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (by == 0)
+          __hip_atomic_fetch_add(wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + kWgSlots - 1), 1,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (member-level count: the sampler waits for the frame-slot reader)
         __hip_atomic_fetch_add(wg->done + kTicketStride * m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        wg_last[0] = lk;
-        wg_last[1] = lb;
-        if (lk || lb) {                                   // the other tiles' atomics are visible now
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      }
-      __syncthreads();
-      if (wg_last[0]) {
-        const int j0 = wg->dep_first[m][by], nj = wg->dep_count[m][by];
-        for (int j = 0; j < nj; ++j) run(j0 + j);
-      }
-      if (wg_last[1]) {
-        const int j0 = wg->dep_first[m][kWgSlots - 1], nj = wg->dep_count[m][kWgSlots - 1];
-        for (int j = 0; j < nj; ++j) run(j0 + j);
       }
     }
   }
@@ -671,7 +657,38 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   if constexpr (FC) {
     // one job per block (the launcher sizes the grid for it): no job loop, so no per-thread loop
     // invariants are hoisted and kept live across the fc barriers
-    if (wid >= 0 && wid < njobs) run(wid);
+    if (wid >= 0 && wid < njobs) {
+#if !DQN_ACT_F32
+      if constexpr (WG) {
+        // a job whose gradient a weight-gradient range of this launch produces (its blocks come
+        // after every tile in the grid, so the tiles are resident or done: the wait ends)
+        const int d = jobs[wid].dep;
+        if (d >= 0) {
+          __shared__ int wg_wait_err;
+          if (threadIdx.x == 0) {
+            const int m = d / kWgSlots;
+            const int want = wg->nblk[m] / wg->gy[m];        // tiles per K-range
+            const int32_t* c = wg->done + kTicketStride * (kMaxWgradMembers + d);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            wg_wait_err = 0;
+            while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+              __builtin_amdgcn_s_sleep(2);
+              if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s: flag, do not hang
+                ticket[kErrFlag] = 1;
+                wg_wait_err = 1;
+                break;
+              }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the tiles' atomics are visible
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          __syncthreads();
+          (void)wg_wait_err;
+        }
+      }
+#endif
+      run(wid);
+    }
   } else {
     for (int ji = wid < 0 ? njobs : wid; ji < njobs; ji += nwork) run(ji);
   }
@@ -721,9 +738,10 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   __syncthreads();
   OPT_MARK(3);
 #if !DQN_ACT_F32
-  if constexpr (WG) {                                     // the sampler is past its wait
-    if ((int)threadIdx.x < wg->n)
-      __hip_atomic_store(wg->done + kTicketStride * threadIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (WG) {            // every block has arrived: the sampler / range waits are over
+    for (int t = threadIdx.x; t < kMaxWgradMembers + wg->n * kWgSlots; t += blockDim.x)
+      if (t < wg->n || t >= kMaxWgradMembers)
+        __hip_atomic_store(wg->done + kTicketStride * t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #endif
   if (threadIdx.x == 0) {

@@ -199,7 +199,7 @@ void wgrad_group(std::vector<std::vector<int64_t>> members, std::vector<std::vec
 // group as bytes (the caller keeps a device copy for the launches) and its block count.
 // done: device int32 counters (>= 32 * kWgCounters words, zeroed; the launch leaves them zero).
 // deps: [member, slot, first job, job count] per (member, K-range slot / bias slot kWgSlots - 1):
-// the job-table ranges the slot's last tile runs.
+// the job-table ranges waiting on the slot (recorded in the plan; the jobs carry UpdJob.dep).
 std::tuple<torch::Tensor, int64_t> wgrad_plan(std::vector<std::vector<int64_t>> members,
                                               std::vector<std::vector<int64_t>> dims, std::vector<double> scales,
                                               torch::Tensor done, std::vector<std::vector<int64_t>> deps,
@@ -286,6 +286,42 @@ void head_loss(std::vector<int64_t> ints, std::vector<double> flts, std::vector<
   TORCH_CHECK(a.HID <= 512 && a.A <= 32, "scalar head: hidden width <= 512, A <= 32");
   TORCH_CHECK(!a.has_actor || a.actor.E <= 64, "head: acting E <= 64");
   launch_head_loss(a, cur_stream());
+}
+
+// Fused fc forward + scalar head (fc_head.hip): fc args as igemm (instances: the learner's, then
+// the fused actors'), head args as head_loss (h = the learner instances' hidden rows = the fc
+// outputs), fold = [qacc, cnt, Mpad, nlearn]: the fp32 partial-Q slots ([ninst][Mpad][32][N / 16])
+// and the row-group counters (>= Mpad / 16 + 1 int32, zeroed; left zero).
+void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_t> bias, std::vector<int64_t> out,
+             std::vector<int64_t> dims, std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h,
+             std::vector<int64_t> hw, std::vector<int64_t> hb, std::vector<int64_t> hwv, std::vector<int64_t> hbv,
+             std::vector<int64_t> io, std::vector<int64_t> qp, std::vector<int64_t> actor, std::vector<double> actor_f,
+             int64_t act_h, std::vector<int64_t> fold, int64_t prof) {
+  dqn::ConvArgs a = conv_args(in, w, bias, out, {}, std::vector<double>(in.size(), 1.0), dims);
+  TORCH_CHECK(flts.size() == 1 && qp.size() == 2 && fold.size() == 4, "fc_head: flts = [delta], qp, fold");
+  dqn::HeadArgs hd = head_args(ints, h, hw, hb, hwv, hbv, io, {}, {}, {}, actor, actor_f, act_h);
+  TORCH_CHECK(!hd.infer, "fc_head: training launches only");
+  hd.delta = (float)flts[0];
+  hd.loss_parts = P<float*>(qp[0]);
+  hd.dq16 = P<void*>(qp[1]);
+  dqn::FoldArgs f{};
+  f.qacc = P<float*>(fold[0]);
+  f.cnt = P<int32_t*>(fold[1]);
+  f.Mpad = (int)fold[2];
+  f.nlearn = (int)fold[3];
+  f.ngroups = (a.M + 15) / 16;
+  f.prof = P<int64_t*>(prof);
+  TORCH_CHECK(f.qacc && f.cnt && (f.nlearn == 2 || f.nlearn == 3), "fc_head: fold buffers, 2-3 learner instances");
+  TORCH_CHECK((int)in.size() == f.nlearn + (hd.act_E > 0 ? 1 : 0) && out.size() == in.size() && bias.size() == in.size() &&
+                  w.size() == in.size(), "fc_head: one fc input / weights / bias / output per instance");
+  TORCH_CHECK(a.M == hd.B && a.ldo == a.N, "fc_head: fc rows = the minibatch, dense output rows");
+  for (int i = 0; i < f.nlearn; ++i)
+    TORCH_CHECK(hd.h[i] == a.out[i] && hd.w[i] && hd.b[i] && (!hd.dueling || (hd.wv[i] && hd.bv[i])),
+                "fc_head: instance ", i, " head pointers (h = the fc output)");
+  TORCH_CHECK(hd.act_E == 0 || hd.act_h == a.out[f.nlearn], "fc_head: the actors' h is the last fc output");
+  TORCH_CHECK(hd.dq16 && hd.loss_parts && hd.dh && hd.prio, "fc_head: training outputs");
+  TORCH_CHECK(launch_fc_head(a, hd, f, cur_stream()) == 0,
+              "fc_head: shape outside the fused kernel (A <= 18, HID <= 512 and % 64 == 0, E <= 16)");
 }
 
 // C51 head: ints as head_loss; dist = [atoms]; flts = [v_min, v_max]; lg = the instances' logits
@@ -392,6 +428,11 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("dw"), pybind11::arg("db"), pybind11::arg("dw2"), pybind11::arg("db2"), pybind11::arg("nsplit"), pybind11::arg("N"), pybind11::arg("MC"),
         pybind11::arg("KB"), pybind11::arg("NB"), pybind11::arg("scale"), pybind11::arg("atomic"), pybind11::arg("mloop") = 1,
         pybind11::arg("db_zero") = false);
+  m.def("qnet_fc_head", &fc_head, pybind11::arg("inp"), pybind11::arg("w"), pybind11::arg("bias"),
+        pybind11::arg("out"), pybind11::arg("dims"), pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
+        pybind11::arg("hw"), pybind11::arg("hb"), pybind11::arg("hwv"), pybind11::arg("hbv"), pybind11::arg("io"),
+        pybind11::arg("qp"), pybind11::arg("actor"), pybind11::arg("actor_f"), pybind11::arg("act_h"),
+        pybind11::arg("fold"), pybind11::arg("prof") = 0);
   m.def("qnet_head_loss", &head_loss, pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"), pybind11::arg("io"),
         pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("qp"), pybind11::arg("actor"),

@@ -183,6 +183,9 @@ def build_parser() -> argparse.ArgumentParser:
            '2 = the previous step\'s optimizer launch draws it (one extra block, off the critical path)')
     a('--summary_secs', default=120.0, type=float,
       help='chief: seconds between global_step/sec summaries (TF Supervisor step counter: 120)')
+    a('--fold_head', default=1, type=int,
+      help='HIP executor, scalar heads: fc forward + output layer + TD loss + dQ / dH (+ the fused acting '
+           'step) in ONE launch (csrc/kernels/fc_head.hip) instead of the fc launch + the head launch')
     a('--fuse_fc_wgrad', default=1, type=int,
       help='HIP executor (16-bit builds): form the fc weight gradient (X^T dH, rank <= B) inside the '
            'fused optimizer launch instead of writing and re-reading it as an fp32 gradient')
@@ -295,6 +298,7 @@ class Config:
     hip_graph: int = 1
     fuse_sampling: int = 2
     fuse_fc_wgrad: int = 1
+    fold_head: int = 1
     fuse_wgrad_update: int = 1
     det_wgrad: int = 0
     summary_secs: float = 120.0

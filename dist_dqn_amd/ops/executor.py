@@ -103,6 +103,7 @@ class HipExecutor:
         self._ws: Dict[Tuple[int, int], dict] = {}
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
+        self.fold_head = True       # training: fc forward + scalar head in one launch (fc_head.hip)
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
         # (round 2 measured the fc + output-layer members on a parallel graph branch beside the dgrad
         # chain: 12.0k -> 9.9k steps/s, the captured fork / join costs more than the overlap gains)
@@ -110,6 +111,7 @@ class HipExecutor:
         self.opt_max_grid = 2048
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_head.py)
+        self.fold_prof = None       # int64 [blocks * 8] fused fc + head stamps (scripts/probe_fold.py)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -389,7 +391,8 @@ class HipExecutor:
         block-assigned jobs, done counters). Job table: the fc jobs (gradient from FcFuse rows,
         final at launch start; one block each), then every other job grouped by the member tile
         range that completes its gradient -- (member, 64-row K-range) for weight tiles, the
-        member's K-range-0 tiles for its bias -- which the last tile of that range runs."""
+        member's K-range-0 tiles for its bias; each such job's block (after every tile in the grid)
+        waits for its range's count (UpdJob.dep = member * WG_SLOTS + slot)."""
         members, dims, scales = wg
         key = (tuple(tuple(m) for m in members), tuple(tuple(d) for d in dims), tuple(scales), grad.data_ptr(),
                self.wg_conv_chunks, dev)
@@ -425,6 +428,8 @@ class HipExecutor:
             table, deps = list(fcj), []
             for (mi, slot), its in sorted(groups.items()):
                 deps.append([mi, slot, len(table), len(its)])
+                for it in its:                 # the job's block waits for that range's tiles
+                    it[21] = mi * ext.WG_SLOTS + slot
                 table += its
             host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
             jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
@@ -439,8 +444,8 @@ class HipExecutor:
         ``grad``, optim_pack.h kModeWg). Its grid: the lead block (next minibatch + end-of-launch
         bookkeeping), the weight-gradient tiles, the fc jobs (gradient formed from the FcFuse
         rows: independent of the tiles -- the fc update, ~90% of the optimizer's bytes, runs
-        beside the weight-gradient work). Every other job is run by the tile that completes its
-        gradient (the last of its member's K-range)."""
+        beside the weight-gradient work). Every other job has a block at the end of the grid that
+        waits for the tiles of its gradient's K-range."""
         from ..optim import kernel_op
         dev = flat.device
         wg, self._wg_pending = self._wg_pending, None
@@ -791,10 +796,11 @@ class HipExecutor:
         """The fused trunk can draw the uniform minibatch itself (replay.sample_slots(defer))."""
         return self.fused_trunk
 
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=(), sample=None):
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=(), sample=None, fc=True):
         """conv1..fc for `ninst` instances -> ws['h'] (M: valid rows per instance, e.g. the
         fused actor instance's E < B). sample: (spec pointers, sampled instances) — the
         trunk draws the uniform batch itself (the slot tables of those instances are outputs).
+        fc=False: stop at conv3 (the caller's fused fc + head launch follows, ``_fc_head``).
 
         xs: uint8 NHWC [B, 84, 84, 4] inputs, or (frames given) int32 [B, 4] slot
         tables into the frame ring ``frames`` [F, 84, 84] (fused gather)."""
@@ -818,7 +824,8 @@ class HipExecutor:
             smp = list(sample[0]) + [int(sample[1])] if sample is not None else []
             ext.qnet_trunk(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale, prof,
                            list(M), smp)
-            self._fc_fwd(packs, flats, ws, B, ninst)
+            if fc:
+                self._fc_fwd(packs, flats, ws, B, ninst)
             return
         d1 = [B * h1 * w1, c1.cout, c1.k * c1.k * c1.cin, (c1.cout + 15) // 16, c1.cout, 84, 84, h1, w1, 0, 0]
         kind1 = _KIND['C1']
@@ -833,7 +840,8 @@ class HipExecutor:
         ext.qnet_igemm(_KIND['C3'], [rows(ws['x2'], i) for i in range(ninst)], pk('conv3/fwd'), bias('conv3/b'),
                        [rows(ws['x3'], i) for i in range(ninst)], [], [1.0] * ninst,
                        [B * h3 * w3, c3.cout, c3.k * c3.k * c3.cin, c3.cout // 16, c3.cout, h2, w2, h3, w3, 0, 0])
-        self._fc_fwd(packs, flats, ws, B, ninst)
+        if fc:
+            self._fc_fwd(packs, flats, ws, B, ninst)
 
     def _fc_fwd(self, packs, flats, ws, B, ninst):
         fcb = [p.data_ptr() + self.esz * self.poff['fc/bias'] for p in packs]
@@ -841,6 +849,38 @@ class HipExecutor:
                             [p.data_ptr() + self.esz * self.poff['fc/fwd'] for p in packs], fcb,
                             [ws['h'][i].data_ptr() for i in range(ninst)], [], [1.0] * ninst,
                             [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0])
+
+    def can_fold_head(self, B: int, E: int = 0) -> bool:
+        """Whether the training step's fc forward and scalar head run as ONE launch
+        (csrc/kernels/fc_head.hip): scalar heads with A <= 18, hidden width <= 512, <= 16 fused
+        actors, a hidden width % 64 == 0."""
+        return (self.fold_head and not self.dist and self.A <= 18 and self.HID <= 512 and self.HID % 64 == 0
+                and E <= 16 and B <= 1024)
+
+    def _fold_ws(self, B, dev) -> dict:
+        key = ('fold', B, dev.index if dev.index is not None else 0)
+        ws = self._ws.get(key)
+        if ws is None:
+            mpad = (B + 15) // 16 * 16
+            ws = {'q': torch.zeros(4 * mpad * 32 * (self.HH // 16), dtype=torch.float32, device=dev),
+                  'cnt': torch.zeros(mpad // 16 + 2, dtype=torch.int32, device=dev), 'mpad': mpad}
+            self._ws[key] = ws
+        return ws
+
+    def _fc_head(self, packs, ws, B, nlearn, ints, w, b, wv, bv, io, actor, actor_f, act_h, dev):
+        """fc forward of every instance (learners', then the fused actors') + the scalar head's
+        loss / dQ / dH (+ the fused acting step) in ONE launch (``can_fold_head``)."""
+        n = len(packs)
+        fw = self._fold_ws(B, dev)
+        self.ext.qnet_fc_head([ws['x3'][i].data_ptr() for i in range(n)],
+                              [p.data_ptr() + self.esz * self.poff['fc/fwd'] for p in packs],
+                              [p.data_ptr() + self.esz * self.poff['fc/bias'] for p in packs],
+                              [ws['h'][i].data_ptr() for i in range(n)],
+                              [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0],
+                              ints, [self.delta], [ws['h'][i].data_ptr() for i in range(nlearn)], w, b, wv, bv, io,
+                              [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()], actor, actor_f, act_h,
+                              [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn],
+                              self.fold_prof.data_ptr() if self.fold_prof is not None else 0)
 
     def _head_ptrs(self, flats):
         lay = self.layout
@@ -1090,11 +1130,12 @@ class HipExecutor:
         if spec is not None:
             assert self.fused_trunk and frames is not None, 'deferred sampling needs the fused trunk'
         sample = (spec, ninst) if spec is not None else None
+        fold = self.can_fold_head(B, 0 if acting is None else E)
         if acting is None:
-            self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames, sample=sample)
+            self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames, sample=sample, fc=not fold)
         else:
             self._fwd_trunk(xs + [acting['stacks']], packs + [po], flats + [eo], ws, B, ninst + 1, frames=frames,
-                            M=[B] * ninst + [E], sample=sample)
+                            M=[B] * ninst + [E], sample=sample, fc=not fold)
         if not zero_in_head:
             main.wait_event(ev_zero)
         det = bool(det_wgrad)
@@ -1114,15 +1155,21 @@ class HipExecutor:
                           batch['gammas'].contiguous())
         wts = batch.get('weights')
         self._c51_dev = dev
-        self._head([B, self.A, self.HID, int(self.dueling), int(self.huber), 0],
-                   [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv,
-                   [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
-                    wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
-                    ws['q'].data_ptr() if not self.dist else 0, dw, db, dwv, dbv, ws['dh'].data_ptr()],
-                   *self._head_packs(packs), [],              # (the conv grad range is zeroed by the fc dgrad)
-                   [] if acting is None else list(acting['ptrs']) + list(acting['ints']),
-                   [] if acting is None else list(acting['f']),
-                   act_h=0 if acting is None else ws['h'][ninst].data_ptr(), ws=ws)
+        hints = [B, self.A, self.HID, int(self.dueling), int(self.huber), 0]
+        hio = [act.data_ptr(), rew.data_ptr(), done.data_ptr(), gam.data_ptr(),
+               wts.data_ptr() if wts is not None else 0, ws['loss'].data_ptr(), ws['prio'].data_ptr(),
+               ws['q'].data_ptr() if not self.dist else 0, dw, db, dwv, dbv, ws['dh'].data_ptr()]
+        hactor = [] if acting is None else list(acting['ptrs']) + list(acting['ints'])
+        hactor_f = [] if acting is None else list(acting['f'])
+        act_h = 0 if acting is None else ws['h'][ninst].data_ptr()
+        if fold:
+            # fc forward + output layer + TD loss + dQ / dH (+ the fused acting step): one launch
+            self._fc_head(packs if acting is None else packs + [po], ws, B, ninst, hints, w, b, wv, bv, hio,
+                          hactor, hactor_f, act_h, dev)
+        else:
+            self._head(hints, [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv, hio,
+                       *self._head_packs(packs), [],          # (the conv grad range is zeroed by the fc dgrad)
+                       hactor, hactor_f, act_h=act_h, ws=ws)
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
@@ -1306,7 +1353,7 @@ class HipCnnExecutor(HipExecutor):
         self._ws[key] = ws
         return ws
 
-    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=(), sample=None):
+    def _fwd_trunk(self, xs, packs, flats, ws, B, ninst, frames=None, keep_acts=True, M=(), sample=None, fc=True):
         assert sample is None, 'the cnn forward reads sampler-made slot tables'
         lay = self.layout
         pad = lambda v: list(v) + [0] * (4 - len(v))
@@ -1320,7 +1367,8 @@ class HipCnnExecutor(HipExecutor):
                 + pad([ws['x3'][i].data_ptr() for i in range(ninst)]) + keep)
         self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale,
                               list(M))
-        self._fc_fwd(packs, flats, ws, B, ninst)
+        if fc:
+            self._fc_fwd(packs, flats, ws, B, ninst)
 
     def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev, fc_dgrad,
                       hmembers=(), hdims=(), defer=False):

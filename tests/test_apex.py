@@ -66,6 +66,26 @@ def test_host_runtime_under_thread_sanitizer(tmp_path):
     assert 'ring errors 0, mailbox errors 0' in run.stdout
 
 
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+def test_ingest_service_under_thread_sanitizer(tmp_path):
+    """The native ingest service's core (csrc/host/ingest_core.h, the code the GPU binding runs)
+    with a fake device whose stream is a worker thread: actor threads -> rings -> rotating
+    staging sets -> late "H2D" copies, stats polled during the run, stop + cursor hand-back."""
+    exe = str(tmp_path / 'ingest_stress')
+    src = [os.path.join(ROOT, 'csrc', 'host', f) for f in ('tests/ingest_stress.cpp', 'apex_ingest.cpp',
+                                                           'spsc_ring.cpp')]
+    r = subprocess.run(['g++', '-std=c++17', '-O1', '-g', '-fsanitize=thread', '-I' + os.path.join(ROOT, 'csrc'),
+                        '-o', exe] + src + ['-lpthread'], capture_output=True, text=True)
+    if r.returncode != 0 and 'tsan' in (r.stderr + r.stdout).lower():
+        pytest.skip('ThreadSanitizer runtime unavailable')
+    assert r.returncode == 0, r.stderr
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, TSAN_OPTIONS='halt_on_error=1'))
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert 'ThreadSanitizer' not in run.stderr, run.stderr
+    assert 'errors 0' in run.stdout, run.stdout
+
+
 def test_apex_epsilons():
     e = apex_epsilons(8)
     assert e[0] == pytest.approx(0.4) and e[-1] == pytest.approx(0.4 ** 8)

@@ -217,12 +217,32 @@ def test_deferred_fc_update_matches_fp32_oracle(extra):
 
 
 def _head_torch(net, ws, B, batch, dist):
-    """Pure-torch loss on the kernel's own hidden rows: (loss, dL/dout, dH)."""
+    """Pure-torch loss on the kernel's own hidden rows: (loss, dL/dout, dH). Dueling (scalar):
+    dout = dL/dQ, dH = dL/dh through Q = V + A - mean(A) by autograd."""
     from dist_dqn_amd.models import losses
     ex, lay = net.executor, net.layout
     HH, A = ex.HH, ex.A
     hs = [ws['h'][i][:B * HH].view(B, HH).float() for i in range(3 if ex.double else 2)]
     flats = [net.online.flat, net.target.flat, net.online.flat]
+    T = lambda f, n, *shape: f[lay.offsets[n]:lay.offsets[n] + lay.numel(n)].view(*shape)
+    if ex.dueling and not dist:
+        H = ex.HID
+
+        def q_of(h, f):
+            v = h[:, :H] @ T(f, 'value/output/w', H, 1) + T(f, 'value/output/b', 1)
+            a = h[:, H:] @ T(f, 'advantage/output/w', H, A) + T(f, 'advantage/output/b', A)
+            return v + a - a.mean(1, keepdim=True)
+        h0 = hs[0].detach().requires_grad_(True)
+        o0 = q_of(h0, flats[0])
+        o0.retain_grad()
+        outs = [None] + [q_of(h, f) for h, f in zip(hs[1:], flats[1:])]
+        loss, _ = losses.scalar_td_loss(o0, batch['actions'], batch['rewards'], batch['dones'], outs[1].detach(),
+                                        outs[2].detach() if ex.double else None, batch['gammas'],
+                                        net.config.loss, net.config.huber_delta)
+        loss.backward()
+        # the kernels hand the advantage stream's dL/dA = dQ - mean(dQ) to the output layer
+        dq = o0.grad
+        return float(loss), dq - dq.mean(1, keepdim=True), h0.grad * (hs[0] > 0).float()
     W = lambda f: f[lay.offsets['output/w']:lay.offsets['output/w'] + lay.numel('output/w')].view(HH, -1)
     bias = lambda f: f[lay.offsets['output/b']:lay.offsets['output/b'] + lay.numel('output/b')]
     outs = [h @ W(f) + bias(f) for h, f in zip(hs, flats)]
@@ -243,10 +263,14 @@ def _head_torch(net, ws, B, batch, dist):
     return float(loss), dout, dh
 
 
-@pytest.mark.parametrize('extra', ['', '--double_dqn --loss=huber', '--distributional', '--distributional --double_dqn'])
-def test_head_kernels_match_pure_torch_loss(extra):
-    """head_loss_kernel / c51_train_kernel vs torch autograd on the same hidden rows: the loss,
-    the dL/dQ (dL/dlogits) rows the kernel hands to the output layer's weight gradient, and dH."""
+@pytest.mark.parametrize('extra,fold', [('', True), ('', False), ('--double_dqn --loss=huber', True),
+                                        ('--double_dqn --loss=huber', False), ('--dueling --double_dqn', True),
+                                        ('--dueling', False), ('--distributional', False),
+                                        ('--distributional --double_dqn', False)])
+def test_head_kernels_match_pure_torch_loss(extra, fold):
+    """The scalar head folded into the fc launch (fc_head.hip, fold) / head_loss_kernel /
+    c51_train_kernel vs torch autograd on the same hidden rows: the loss, the dL/dQ
+    (dL/dlogits) rows the kernel hands to the output layer's weight gradient, and dH."""
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.models.network import Network
     B = 32
@@ -265,6 +289,8 @@ def test_head_kernels_match_pure_torch_loss(extra):
         'gammas': torch.full((B,), 0.99, device=DEV),
     }
     ex = net.executor
+    ex.fold_head = fold
+    assert ex.can_fold_head(B) == (fold and not ex.dist)
     grad = torch.zeros_like(net.online.flat)
     loss, _ = ex.loss_and_grad(net.online.flat, net.target.flat, batch, grad, None, None)
     torch.cuda.synchronize()
@@ -278,6 +304,59 @@ def test_head_kernels_match_pure_torch_loss(extra):
     assert rel(dq, dout_ref) < 2e-2, rel(dq, dout_ref)
     dh = ws['dh'][:B * ex.HH].view(B, ex.HH).float()
     assert rel(dh, dh_ref) < 3e-2, rel(dh, dh_ref)
+    dh_bits, dq_bits = ws['dh'][:B * ex.HH].clone(), ws['dq16'][:B * width].clone()
+    if fold:
+        # the fold leaves its row-group counters zero: a second call is bit-identical
+        fw = ex._fold_ws(B, DEV)
+        assert not fw['cnt'].any()
+        grad2 = torch.zeros_like(grad)
+        loss2, _ = ex.loss_and_grad(net.online.flat, net.target.flat, batch, grad2, None, None)
+        torch.cuda.synchronize()
+        assert float(loss2) == float(loss)
+        assert torch.equal(ws['dh'][:B * ex.HH], dh_bits) and torch.equal(ws['dq16'][:B * width], dq_bits)
+
+
+@pytest.mark.parametrize('extra', ['', '--double_dqn --loss=huber', '--dueling --double_dqn', 'cnn:--dueling'])
+def test_folded_head_gradient_matches_separate_head(extra):
+    """One launch for fc + output layer + TD loss + dQ / dH (fc_head.hip) vs the fc igemm launch +
+    head_loss_kernel on the same minibatch: the whole flat gradient, the loss and the priorities
+    (the fold's output layer is fp32 on the stored bf16 h; the head kernel's bf16 MFMA fragments)."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.models.network import Network
+    B = 32
+    kind = 'atari' if extra.startswith('cnn:') else 'nature'
+    extra = extra[4:] if extra.startswith('cnn:') else extra
+    outs = []
+    for fold in (True, False):
+        cfg = preset(kind, 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 %s' % extra)
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        g = torch.Generator(device=DEV).manual_seed(4)
+        net.online.flat.normal_(0.0, 0.03, generator=g)
+        net.target.flat.normal_(0.0, 0.03, generator=g)
+        net.refresh_packed()
+        batch = {
+            'states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
+            'next_states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
+            'actions': torch.randint(0, 6, (B,), dtype=torch.int32, device=DEV, generator=g),
+            'rewards': torch.randn(B, device=DEV, generator=g) * 5.0,
+            'dones': (torch.rand(B, device=DEV, generator=g) < 0.2).float(),
+            'gammas': torch.full((B,), 0.99, device=DEV),
+        }
+        ex = net.executor
+        ex.fold_head = fold
+        grad = torch.zeros_like(net.online.flat)
+        loss, prio = ex.loss_and_grad(net.online.flat, net.target.flat, batch, grad, None, None)
+        torch.cuda.synchronize()
+        outs.append((float(loss), prio.clone(), grad.clone(), net.layout))
+    (la, pa, ga, lay), (lb, pb, gb, _) = outs
+    assert abs(la - lb) / abs(lb) < 5e-3, (la, lb)
+    # |TD| per sample: both heads round differently (bf16 output-layer fragments vs fp32), an
+    # error on the scale of Q, not of each |TD|
+    torch.testing.assert_close(pa, pb, rtol=0, atol=2e-2 * float(pb.abs().max()))
+    for n in lay.names:
+        o, k = lay.offsets[n], lay.numel(n)
+        x, y = ga[o:o + k].double(), gb[o:o + k].double()
+        assert float((x - y).norm() / (y.norm() + 1e-30)) < 2e-2, n
 
 
 @pytest.mark.parametrize('extra', ['', RAINBOW])
