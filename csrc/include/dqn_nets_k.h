@@ -139,6 +139,12 @@ struct FoldArgs {
   int32_t* cnt;
   int Mpad, ngroups, nlearn;
   int64_t* prof;             // optional: s_memrealtime stamps [block][8] (scripts/probe_fold.py)
+  // spin (every block of the launch resident at once): the online instance's blocks wait for
+  // their group's dQ (tail -> dqg fp32 [Mpad][32] + epoch word dq_epoch[group], never reset) and
+  // each writes its own 16x16 dH tile; else the tail computes the group's whole dH
+  int spin;
+  float* dqg;
+  int32_t* dq_epoch;
 };
 
 // One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =

@@ -64,6 +64,9 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   const int HID = h.HID, HH = h.dueling ? 2 * HID : HID;
   const int m_base = blockIdx.x * 16, nt = blockIdx.y;
   const int Mi = actor_inst ? h.act_E : a.M;   // valid rows of this instance
+  const bool dh_tile = f.spin && !actor_inst && inst == 0;   // this block writes its own dH tile
+  int e0 = 0;                                   // the group's dQ epoch before this launch's tail
+  if (dh_tile) e0 = __hip_atomic_load(f.dq_epoch + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ActorPre pre{};
   const bool frames_duty = actor_inst && nt < h.act_E;
   if (frames_duty) pre = actor_prefetch(h.actor);   // (before the arrival: the tail advances it)
@@ -186,8 +189,53 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   }
   __syncthreads();
   if (frames_duty) actor_env_frames(h.actor, nt, pre);       // env nt's new frame(s): rng only
-  if (!S.flag) return;
-  if (tid == 0) {                                            // acquire: every block's writes
+  // dH tile of this block from the group's dQ rows: (dQ W2^T)[rows][the tile's 16 units] * (h > 0)
+  auto dh_from = [&](const float (*dq)[33]) {
+    if (tid < 256) {
+      const int r = tid >> 4, j = tid & 15;
+      if (r < min(16, a.M - m_base)) {
+        float sacc;
+        if (vtile) {
+          sacc = dq[r][A] * S.w2t[j];
+        } else {
+          sacc = 0.f;
+          if constexpr (AT > 0) {
+#pragma unroll
+            for (int i = 0; i < AT; ++i) sacc += dq[r][i] * S.w2t[j * AT + i];
+          } else {
+            for (int i = 0; i < A; ++i) sacc += dq[r][i] * S.w2t[j * A + i];
+          }
+        }
+        reinterpret_cast<act_t*>(h.dh)[(int64_t)(m_base + r) * HH + nt * 16 + j] =
+            (act_t)((float)S.hv[r][j] > 0.f ? sacc * kLossScale : 0.f);
+      }
+    }
+  };
+  if (!S.flag) {
+    if (!dh_tile) return;
+    // wait for the group's tail to publish dQ (every block of the launch is resident: spin mode)
+    // (no acquire fence here: an L2 invalidation per waiting block costs the next launches their
+    //  cached weights; the dQ rows are read with agent-scope loads, coherent like the stores)
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(f.dq_epoch + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;    // 1 s: never hang
+      }
+    }
+    __syncthreads();
+    const int nr = min(16, a.M - m_base);
+    for (int t = tid; t < 16 * A1; t += kFoldThreads) {
+      const int r = t / A1, c = t - r * A1;
+      S.dq[r][c] = r < nr ? __hip_atomic_load(f.dqg + (int64_t)(m_base + r) * 32 + c, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : 0.f;
+    }
+    __syncthreads();
+    dh_from(S.dq);
+    return;
+  }
+  if (tid == 0) {                     // acquire: the other blocks' partial slots (and h rows)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(f.cnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -203,7 +251,7 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   constexpr int kHc = 2 * kFoldMaxHid * 16 / 8 / kFoldThreads;   // chunks per thread (<= 4)
   const act_t* h0 = reinterpret_cast<const act_t*>(h.h[0]);
   bfx8 hvr[kHc];
-  if (!actor_inst) {
+  if (!actor_inst && !f.spin) {
 #pragma unroll
     for (int u = 0; u < kHc; ++u) {
       const int t = tid + u * kFoldThreads, r = t / nch;
@@ -306,6 +354,23 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   }
   FOLD_MARK(5);
   __syncthreads();
+  if (f.spin) {
+    // publish the group's dQ rows (write-through), then its epoch: the online blocks waiting on it
+    // write their dH tiles (this block too, when it is one of them)
+    const int g = (int)blockIdx.x;
+    for (int t = tid; t < nrows * A1; t += kFoldThreads) {
+      const int r = t / A1, c = t - r * A1;
+      __hip_atomic_store(f.dqg + (int64_t)(m_base + r) * 32 + c, S.dq[r][c], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int e = __hip_atomic_load(f.dq_epoch + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(f.dq_epoch + g, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (dh_tile) dh_from(S.dq);
+  }
   for (int t = tid; t < nrows * 64; t += kFoldThreads) {
     const int r = t >> 6, c = t & 63;
     const float g = c < A ? S.dq[r][c] : (c == 32 && h.dueling ? S.dq[r][A] : 0.f);
@@ -316,6 +381,7 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   // ---- dH[row][k] = (sum_i dQ[row][i] W[k][i]) * (h > 0) (dueling: value units dV wv[k]) over the
   //      group's online h rows (8 units per thread)
   act_t* dh = reinterpret_cast<act_t*>(h.dh);
+  if (!f.spin) {
 #pragma unroll
   for (int u = 0; u < kHc; ++u) {
     const int t = tid + u * kFoldThreads;
@@ -346,6 +412,7 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     }
     *reinterpret_cast<bfx8*>(dh + o) = out;
   }
+  }
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     FOLD_MARK(6);
@@ -364,6 +431,19 @@ int launch_fc_head(const ConvArgs& a, const HeadArgs& h, const FoldArgs& f, hipS
       (f.nlearn != 2 && f.nlearn != 3) || ninst > kMaxInst)
     return -1;
   const dim3 grid((a.M + 15) / 16, a.N / 16, ninst);
+  // spin mode needs every block resident at once (2 per CU by LDS): one per CU, conservatively
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  if (f.spin && (int)(grid.x * grid.y * grid.z) > cus) {
+    FoldArgs g = f;
+    g.spin = 0;
+    return launch_fc_head(a, h, g, st);
+  }
+  if (f.spin && (f.dqg == nullptr || f.dq_epoch == nullptr)) return -1;
 #define FOLD(AT) hipLaunchKernelGGL(fc_head_kernel<AT>, grid, dim3(kFoldThreads), 0, st, a, h, f)
   switch (h.A) {
     case 2: FOLD(2); break;

@@ -298,7 +298,8 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
              std::vector<int64_t> io, std::vector<int64_t> qp, std::vector<int64_t> actor, std::vector<double> actor_f,
              int64_t act_h, std::vector<int64_t> fold, int64_t prof) {
   dqn::ConvArgs a = conv_args(in, w, bias, out, {}, std::vector<double>(in.size(), 1.0), dims);
-  TORCH_CHECK(flts.size() == 1 && qp.size() == 2 && fold.size() == 4, "fc_head: flts = [delta], qp, fold");
+  TORCH_CHECK(flts.size() == 1 && qp.size() == 2 && (fold.size() == 4 || fold.size() == 6),
+              "fc_head: flts = [delta], qp, fold = [qacc, cnt, Mpad, nlearn(, dqg, dq_epoch)]");
   dqn::HeadArgs hd = head_args(ints, h, hw, hb, hwv, hbv, io, {}, {}, {}, actor, actor_f, act_h);
   TORCH_CHECK(!hd.infer, "fc_head: training launches only");
   hd.delta = (float)flts[0];
@@ -311,6 +312,11 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
   f.nlearn = (int)fold[3];
   f.ngroups = (a.M + 15) / 16;
   f.prof = P<int64_t*>(prof);
+  if (fold.size() == 6) {      // spin mode: the online blocks write their own dH tiles
+    f.spin = 1;
+    f.dqg = P<float*>(fold[4]);
+    f.dq_epoch = P<int32_t*>(fold[5]);
+  }
   TORCH_CHECK(f.qacc && f.cnt && (f.nlearn == 2 || f.nlearn == 3), "fc_head: fold buffers, 2-3 learner instances");
   TORCH_CHECK((int)in.size() == f.nlearn + (hd.act_E > 0 ? 1 : 0) && out.size() == in.size() && bias.size() == in.size() &&
                   w.size() == in.size(), "fc_head: one fc input / weights / bias / output per instance");

@@ -863,7 +863,9 @@ class HipExecutor:
         if ws is None:
             mpad = (B + 15) // 16 * 16
             ws = {'q': torch.zeros(4 * mpad * 32 * (self.HH // 16), dtype=torch.float32, device=dev),
-                  'cnt': torch.zeros(mpad // 16 + 2, dtype=torch.int32, device=dev), 'mpad': mpad}
+                  'cnt': torch.zeros(mpad // 16 + 2, dtype=torch.int32, device=dev), 'mpad': mpad,
+                  'dqg': torch.zeros(mpad * 32, dtype=torch.float32, device=dev),
+                  'epoch': torch.zeros(mpad // 16 + 2, dtype=torch.int32, device=dev)}
             self._ws[key] = ws
         return ws
 
@@ -879,7 +881,8 @@ class HipExecutor:
                               [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0],
                               ints, [self.delta], [ws['h'][i].data_ptr() for i in range(nlearn)], w, b, wv, bv, io,
                               [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()], actor, actor_f, act_h,
-                              [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn],
+                              [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn, fw['dqg'].data_ptr(),
+                               fw['epoch'].data_ptr()],
                               self.fold_prof.data_ptr() if self.fold_prof is not None else 0)
 
     def _head_ptrs(self, flats):

@@ -504,8 +504,10 @@ def test_per_fused_in_optimizer_equals_separate_launches(extra):
     from dist_dqn_amd.replay import DeviceReplay
     outs = []
     for fuse in (0, 2):
+        # (--det_wgrad: bit-reproducible conv weight gradients, so the two runs' priorities -- and
+        #  with them the prioritized minibatches -- can only differ through the sampling paths)
         cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 '
-                     '--fuse_sampling=%d %s' % (fuse, extra))
+                     '--det_wgrad=1 --fuse_sampling=%d %s' % (fuse, extra))
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)
         rep.fill_synthetic(4096, 6, seed=5)
@@ -557,8 +559,10 @@ def test_fused_acting_per_insert_in_optimizer(extra):
     from dist_dqn_amd.replay import DeviceReplay
     outs = []
     for defer in (False, True):
+        # (--det_wgrad: bit-reproducible conv weight gradients: the runs' priorities can only
+        #  differ through the insert paths)
         cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --replay_memory_capacity=4096 '
-                     '--fuse_sampling=2 ' + extra)
+                     '--det_wgrad=1 --fuse_sampling=2 ' + extra)
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=5, prioritized=True)
         rep.fill_synthetic(4096, 6, seed=5)

@@ -316,19 +316,21 @@ def test_head_kernels_match_pure_torch_loss(extra, fold):
         assert torch.equal(ws['dh'][:B * ex.HH], dh_bits) and torch.equal(ws['dq16'][:B * width], dq_bits)
 
 
-@pytest.mark.parametrize('extra', ['', '--double_dqn --loss=huber', '--dueling --double_dqn', 'cnn:--dueling'])
-def test_folded_head_gradient_matches_separate_head(extra):
+@pytest.mark.parametrize('extra,B', [('', 32), ('--double_dqn --loss=huber', 32), ('--dueling --double_dqn', 32),
+                                     ('cnn:--dueling', 32), ('--dueling', 256)])
+def test_folded_head_gradient_matches_separate_head(extra, B):
     """One launch for fc + output layer + TD loss + dQ / dH (fc_head.hip) vs the fc igemm launch +
     head_loss_kernel on the same minibatch: the whole flat gradient, the loss and the priorities
-    (the fold's output layer is fp32 on the stored bf16 h; the head kernel's bf16 MFMA fragments)."""
+    (the fold's output layer is fp32 on the stored bf16 h; the head kernel's bf16 MFMA fragments).
+    B = 32: every block resident, the online blocks write their own dH tiles after the group's tail
+    publishes dQ (spin mode); B = 256: more blocks than CUs, the tails write the whole dH."""
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.models.network import Network
-    B = 32
     kind = 'atari' if extra.startswith('cnn:') else 'nature'
     extra = extra[4:] if extra.startswith('cnn:') else extra
     outs = []
     for fold in (True, False):
-        cfg = preset(kind, 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 %s' % extra)
+        cfg = preset(kind, 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 --minibatch_size=%d %s' % (B, extra))
         net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
         g = torch.Generator(device=DEV).manual_seed(4)
         net.online.flat.normal_(0.0, 0.03, generator=g)
