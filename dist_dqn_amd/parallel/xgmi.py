@@ -116,10 +116,21 @@ class XgmiAllReduce:
             raise RuntimeError('xgmi all-reduce setup failed on some rank (here: %s)' % (err,))
         ctx.barrier()           # every peer's signal words are zero before anyone signals
 
+    @property
+    def max_blocks(self) -> int:
+        """Blocks per call. Every rank's blocks spin on their peers' flags, so all W ranks' calls
+        must be resident at once. One GPU per rank: up to XGMI_MAX_BLOCKS (256). Several ranks on
+        ONE GPU (the rehearsals): 128 / W, so the W kernels fit together -- at W = 8 with 104 blocks
+        per rank a rank's wait timed out after 10 s on a peer block that never ran (error word:
+        all-gather phase, peer 2, block 192; round 4), i.e. starvation, not the protocol."""
+        if self.ctx.world_size <= max(1, torch.cuda.device_count()):
+            return self.ext.XGMI_MAX_BLOCKS
+        return max(8, 128 // self.ctx.world_size)
+
     def blocks_for(self, n: int) -> int:
-        # ~2 float4 vectors per thread of each slice; all blocks co-resident (<= 256)
+        # ~2 float4 vectors per thread of each slice; all blocks co-resident
         sv = n // 4 // self.ctx.world_size
-        return max(1, min(self.ext.XGMI_MAX_BLOCKS, (sv + 511) // 512))
+        return max(1, min(self.max_blocks, (sv + 511) // 512))
 
     def allgather2(self, srcs, outs, nbytes):
         """out[s][q * nbytes[s] : (q + 1) * nbytes[s]] = rank q's src[s] (raw device pointers, 16-byte
@@ -128,7 +139,7 @@ class XgmiAllReduce:
         assert self.gather_cap > 0, 'no gather channel'
         ch = self.channels[-1]
         nv = (int(nbytes[0]) + int(nbytes[1])) // 16
-        blocks = max(1, min(self.ext.XGMI_MAX_BLOCKS, (nv + 255) // 256))
+        blocks = max(1, min(self.max_blocks, (nv + 255) // 256))
         self.ext.xgmi_allgather([int(v) for v in srcs], [int(v) for v in outs], [int(v) for v in nbytes], ch.data,
                                 ch.sig, ch.seq_ptr, ch.err_ptr, self.gather_cap, self.ctx.rank, self.ctx.world_size,
                                 blocks, self.ctx.device.index)
@@ -147,7 +158,7 @@ class XgmiAllReduce:
                                          ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.gather_cap, self.ctx.rank,
                                          self.ctx.world_size)
         nv = (int(nbytes[0]) + int(nbytes[1])) // 16
-        blocks = max(1, min(self.ext.XGMI_MAX_BLOCKS, (nv + 255) // 256))
+        blocks = max(1, min(self.max_blocks, (nv + 255) // 256))
         cache[key] = (host.to(self.ctx.device), blocks)
         return cache[key]
 
@@ -241,8 +252,9 @@ class XgmiAllReduce:
             self.self_test_log.append(('exception', repr(e)))
             ok = False
         if not ok:
-            log.warning('xgmi all-reduce self-test failed on rank %d: (channel, call, wrong values, error word) %s',
-                        r, self.self_test_log)
+            log.warning('xgmi all-reduce self-test failed on rank %d: (channel, call, wrong values, error word) %s; '
+                        'first timed-out waits %s; blocks per call %d', r, self.self_test_log, self.error_info(),
+                        self.blocks_for(n))
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.ctx.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return int(flag) == 1

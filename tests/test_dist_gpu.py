@@ -49,6 +49,10 @@ def _run_ranks(target, args, world=2, timeout=100):
 def _setup(rank, world, port):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0', DQN_DIST_BACKEND='gloo')
+    if world > 4:
+        # 8 ranks (+ this test process) on ONE GPU: 2 hardware queues each keeps every rank's
+        # queues mapped at once (their spinning peer waits need all ranks running together)
+        os.environ['GPU_MAX_HW_QUEUES'] = '2'
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -151,6 +155,7 @@ def _worker_xgmi(rank, world, port, wire, concurrent, errq):
 def test_xgmi_allreduce_ranks_one_gpu(world, wire, concurrent):
     """The peer-to-peer kernel (IPC-mapped fine-grained buffers) against exact sums, at the
     world sizes the node runs (the WC = 2 / 4 / 8 instantiations, the 8-peer gather)."""
+    _gpu_free_parent(world)
     _run_ranks(_worker_xgmi, (wire, concurrent), world=world, timeout=100 + 20 * world)
 
 
@@ -251,6 +256,7 @@ def _worker(rank, world, port, network, extra, errq):
     (8, 'nature', '--allreduce=xgmi ' + RAINBOW_DP)])
 def test_dp_learner_ranks_one_gpu(world, network, extra):
     """(--allreduce=rccl means the process group's collective: gloo in this rehearsal.)"""
+    _gpu_free_parent(world)
     _run_ranks(_worker, (network, extra), world=world, timeout=100 + 25 * world)
 
 
@@ -419,6 +425,41 @@ def _worker_bigbatch(rank, world, port, extra, out, errq):
         raise
 
 
+def _worker_bigbatch_ref(rank, world, port, extra, W, out, errq):
+    """The single-process W*B reference step, in a child too: the test process itself never
+    opens a GPU context here (see _gpu_free_parent)."""
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from dist_dqn_amd.learner import Learner
+        dev = torch.device('cuda', 0)
+        cfg, net, rep = _big_batch_net(BIG_CFG + extra, 32 * W, 1, 0, dev)
+        w0 = net.online.flat.clone()
+        ln = Learner(net, rep, cfg)
+        ln.step()
+        torch.cuda.synchronize()
+        torch.save({'w0': w0.cpu(), 'w1': net.online.flat.cpu(), 'step': int(net.global_step),
+                    'names': list(net.layout.names),
+                    'spans': [(net.layout.offsets[n], net.layout.numel(n)) for n in net.layout.names]}, out)
+    except BaseException as e:  # noqa: BLE001 - report to the parent
+        import traceback
+        errq.put('reference: %s\n%s' % (e, traceback.format_exc()))
+        raise
+
+
+def _gpu_free_parent(world):
+    """8 ranks on ONE GPU need the test process itself to hold no GPU context: with it they are
+    9 GPU processes, and round 4's diagnostics showed the resulting starvation -- the W=8 self-test
+    of the second big-batch case (after the first case's reference had opened a context here)
+    timed out with every wait pointing at one never-run block (ranks 1, 2: reduce-scatter, peer 0
+    block 6, flag 2 of 3; the others all-gather on peer 1), while the same case passed first in a
+    fresh process. The full GPU suite opens a context in earlier modules: skip there, run the
+    module on its own (scripts/gpu_r4_dist.sh) for the 8-rank evidence."""
+    if world >= 8 and torch.cuda.is_initialized():
+        pytest.skip('8 ranks + a GPU-holding test process on one device: run this module in a fresh '
+                    'process (scripts/gpu_r4_dist.sh)')
+
+
 @pytest.mark.parametrize('world,extra', [
     (2, '--allreduce=xgmi'),                           # low-rank fc exchange into the fused optimizer
     (2, '--allreduce=xgmi --lowrank_dense=0'),         # full all-reduce of the flat gradient
@@ -430,22 +471,26 @@ def _worker_bigbatch(rank, world, port, extra, out, errq):
     (8, '--allreduce=xgmi'),
     (8, '--allreduce=xgmi --dueling')])
 def test_dp_step_equals_big_batch_step(tmp_path, world, extra):
-    from dist_dqn_amd.learner import Learner
+    _gpu_free_parent(world)
     out = str(tmp_path / 'dp.pt')
     _run_ranks(_worker_bigbatch, (extra, out), world=world, timeout=100 + 25 * world)
     dp = torch.load(out, weights_only=True)
-    dev = torch.device('cuda', 0)
-    B = 32 * world
     ex = ' '.join(a for a in extra.split() if not a.startswith('--allreduce') and not a.startswith('--lowrank'))
-    cfg, net, rep = _big_batch_net(BIG_CFG + ex, B, 1, 0, dev)
-    assert torch.equal(net.online.flat.cpu(), dp['w0']), 'different initial parameters'
-    ln = Learner(net, rep, cfg)
-    ln.step()
-    torch.cuda.synchronize()
-    assert int(net.global_step) == dp['step'] == 1
-    big = net.online.flat.cpu() - dp['w0']
+    ref = str(tmp_path / 'big.pt')
+    _run_ranks(_worker_bigbatch_ref, (ex, world, ref), world=1, timeout=200)
+    bb = torch.load(ref, weights_only=True)
+    assert torch.equal(bb['w0'], dp['w0']), 'different initial parameters'
+    assert bb['step'] == dp['step'] == 1
+    big = bb['w1'] - dp['w0']
     small = dp['w1'] - dp['w0']
-    lay = net.layout
+
+    class _Lay:
+        names = bb['names']
+        offsets = {n: o for n, (o, _) in zip(bb['names'], bb['spans'])}
+
+        def numel(self, n):
+            return dict(zip(bb['names'], bb['spans']))[n][1]
+    lay = _Lay()
     for name in lay.names:
         o, n = lay.offsets[name], lay.numel(name)
         a, b = small[o:o + n].double(), big[o:o + n].double()
