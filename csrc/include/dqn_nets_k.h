@@ -145,6 +145,25 @@ struct FoldArgs {
   int spin;
   float* dqg;
   int32_t* dq_epoch;
+  float* zero_ptr;           // side duty: block 0 zeroes [zero_ptr, +zero_n) (the step's dgrad-chain
+  int zero_n;                // counters; 16-byte aligned, zero_n % 4 == 0)
+};
+
+// The Nature dgrad chain in ONE launch (qnet.hip dgrad_chain_kernel): block ranges run
+//   stage 0  fc dgrad        dz3 = (dH W_fc^T) * (x3 > 0)      (+ the fc dgrad's side duties)
+//   stage 1  conv3 dgrad     dz2 = dgrad(dz3) * (x2 > 0)
+//   stage 2  conv2 dgrad     dz1 = parity-class dgrad(dz2) * (x1 > 0)
+// in dispatch order; a stage-1 block waits for the stage-0 row groups of its samples, a stage-2
+// block for the stage-1 blocks of its sample (counters in cnt, one per 32 ints: [gx0] row groups |
+// [B] samples | [1] error flag; zeroed by the step's fc forward launch). Stage 0 / 1 outputs are full 128-byte
+// lines per block row, stored write-through.
+struct ChainArgs {
+  ConvArgs a[3];
+  int n0, n1, n2;            // blocks per stage
+  int gx0, gy0;              // stage-0 grid (16-sample row groups, 64-column tiles)
+  int rows1;                 // stage-1 output rows per sample
+  int B;
+  int32_t* cnt;
 };
 
 // One tensor of the noisy-net parameter mix (rainbow.hip): eff[mu_off + k*N + n] =
@@ -235,6 +254,9 @@ enum LayerKind {
 void launch_pack(const float* src, void* dst, const dqn::PackJob* jobs_dev, int njobs, int max_threads,
                  void* dst2, const int64_t* step, int freq, hipStream_t st);
 int launch_igemm(int kind, const dqn::ConvArgs& a, int ninst, hipStream_t st);
+// -1: shapes outside the chained kernel (Nature fc / conv3 / conv2 dgrad, B <= 1024)
+int launch_dgrad_chain(const dqn::ConvArgs& a0, const dqn::ConvArgs& a1, const dqn::ConvArgs& a2, int32_t* cnt, int B,
+                       hipStream_t st);
 int launch_wgrad(int kind, const dqn::ConvArgs& a, const dqn::WgradArgs& g, hipStream_t st);
 int launch_wgrad_group(dqn::WgradGroup G, hipStream_t st);
 // Plans G for the fused weight-gradient range of a split optimizer update (optim.hip kModeWg):

@@ -58,6 +58,9 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
                       : nullptr;
 #define FOLD_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memrealtime()
   FOLD_MARK(0);
+  if (f.zero_ptr != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+    for (int t = threadIdx.x; t < f.zero_n / 4; t += blockDim.x)
+      reinterpret_cast<float4*>(f.zero_ptr)[t] = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool actor_inst = h.act_E > 0 && inst == f.nlearn;
   if (actor_inst && blockIdx.x > 0) return;     // the actors' E <= 16 rows: row group 0 only
   const int A = AT > 0 ? AT : h.A, A1 = A + 1;

@@ -70,26 +70,39 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ src
   if (sync) *reinterpret_cast<bfx8*>(dst2 + o) = v;
 }
 
+// Write-through (agent-scope) store of one act_t of an MFMA C/D tile: 32-bit stores, 16-bit types
+// pair with the adjacent column held by lane ^ 1 (both lanes of a pair are active together: same
+// row, N even). For outputs another block of the same launch reads after a counter.
+DQN_DEV void store_wt(act_t* p, act_t v, int lane) {
+#if DQN_ACT_F32
+  (void)lane;
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#else
+  const uint32_t mine = (uint32_t)__builtin_bit_cast(uint16_t, v);
+  const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+  if ((lane & 1) == 0)
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), mine | (other << 16), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
 // ============================================================ implicit GEMM
 // Block = WM x WN x KSPLIT waves (4 or 8); wave tile = (MT*16) x (NT*16).
 // EPI: 0 = scale*acc + bias, ReLU, bf16 out; 1 = scale*acc + bias, fp32 out (no ReLU);
 //      2 = acc * (mask > 0), bf16 out (ReLU backward through the layer input).
-template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U = 4>
-__global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
+// Body of one block (bx, by, bz) of a virtual (gx, gy, gz) GEMM grid: shared by igemm_kernel and
+// the chained dgrad launch (dgrad_chain.hip). WT: the EPI 2 output leaves as write-through 32-bit
+// stores (agent scope: another block of the same launch reads it after a counter).
+template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U = 4, bool WT = false>
+DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int gy, int gz) {
   static_assert(WM * WN * KSPLIT == 4 || WM * WN * KSPLIT == 8, "4 or 8 waves per block");
   __shared__ float red[KSPLIT > 1 ? WM * WN * (KSPLIT - 1) * MT * NT * 256 : 1];
-  if (a.gth != nullptr && (int)blockIdx.z == a.gth_z) {
-    // side duty: the low-rank DP all-gather (its own grid.z slice; every block of it returns
-    // here, uniformly, before any barrier of the GEMM body)
-    const int gb = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    if (gb < a.gth_blocks) xgmi_gather_block(*reinterpret_cast<const XgmiGatherArgs*>(a.gth), gb, a.gth_blocks);
-    return;
-  }
-  const int inst = blockIdx.z;
+  const int inst = bz;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wk = wave % KSPLIT, wn = (wave / KSPLIT) % WN, wm = wave / (KSPLIT * WN);
-  const int m_base = blockIdx.x * (WM * MT * 16) + wm * MT * 16;
-  const int nt_base = blockIdx.y * (WN * NT) + wn * NT;
+  const int m_base = bx * (WM * MT * 16) + wm * MT * 16;
+  const int nt_base = by * (WN * NT) + wn * NT;
   const int K32 = (a.K + 31) / 32;
   const bfx8* __restrict__ Bp = reinterpret_cast<const bfx8*>(a.w[inst]);
 
@@ -147,8 +160,8 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   }
   // noise duty (every thread of the block, before the split-K waves retire)
   if (a.nz_out0 != nullptr) {
-    const int nblk = gridDim.x * gridDim.y * (gridDim.z - (a.gth != nullptr ? 1 : 0));   // (GEMM blocks only)
-    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int nblk = gx * gy * gz;                                  // (GEMM blocks only)
+    const int blk = (bz * gy + by) * gx + bx;
     const int nq = ((a.nz_out1 != nullptr ? 2 : 1) * a.nz_n + 3) / 4;
     const int nt = blockDim.x, tq = (int)threadIdx.x;
     const uint64_t seed = (uint64_t)a.nz_rng[0], ctr = (uint64_t)a.nz_rng[1];
@@ -180,12 +193,12 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   // side duties of the launch (ConvArgs aux): zero a gradient range (the conv weight gradients
   // accumulate into it with atomics later in the step) and sum the head's per-tile loss partials
   if (a.zero_ptr != nullptr) {
-    const int nblk = gridDim.x * gridDim.y * (gridDim.z - (a.gth != nullptr ? 1 : 0));   // (GEMM blocks only)
-    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int nblk = gx * gy * gz;                                  // (GEMM blocks only)
+    const int blk = (bz * gy + by) * gx + bx;
     float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
     for (int t = blk * 64 + lane; t < a.zero_n / 4; t += nblk * 64) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (a.loss_parts != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+  if (a.loss_parts != nullptr && bx == 0 && by == 0 && bz == 0) {
     const float v = lane < a.nparts ? a.loss_parts[lane] : 0.f;
     const float sl = wave_sum(v);
     if (lane == 0) a.loss_out[0] = sl * a.loss_mul;
@@ -211,12 +224,28 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
           reinterpret_cast<act_t*>(a.out[inst])[o] = (act_t)v;
         } else if constexpr (EPI == 1) {
           reinterpret_cast<float*>(a.out[inst])[o] = v * scale + bv;
-        } else {
+        } else if constexpr (!WT) {
           reinterpret_cast<act_t*>(a.out[inst])[o] = (act_t)(mk[i][j][r] > 0.f ? v : 0.f);
+        } else {
+          const act_t q = (act_t)(mk[i][j][r] > 0.f ? v : 0.f);
+          store_wt(reinterpret_cast<act_t*>(a.out[inst]) + o, q, lane);
         }
       }
     }
   }
+}
+
+template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U = 4>
+__global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
+  if (a.gth != nullptr && (int)blockIdx.z == a.gth_z) {
+    // side duty: the low-rank DP all-gather (its own grid.z slice; every block of it returns
+    // here, uniformly, before any barrier of the GEMM body)
+    const int gb = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    if (gb < a.gth_blocks) xgmi_gather_block(*reinterpret_cast<const XgmiGatherArgs*>(a.gth), gb, a.gth_blocks);
+    return;
+  }
+  igemm_body<LD, MT, NT, WM, WN, KSPLIT, EPI, U>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y,
+                                                 gridDim.z - (a.gth != nullptr ? 1 : 0));
 }
 
 // ===================================================== stride-2 dgrad by parity
@@ -229,14 +258,13 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
 // N (2 n-tiles) x the class's K in two halves (4 waves); the epilogue scatters the rows back
 // to NHWC with the ReLU mask of the layer input.
 template <int COUT, int KH, int KW>
-__global__ void __launch_bounds__(256) dgrad_s2_kernel(ConvArgs a) {
+DQN_DEV void dgrad_s2_body(const ConvArgs& a, int bx, int inst) {
   static_assert(KH % 2 == 0 && KW % 2 == 0 && COUT % 32 == 0, "2x2 tap classes, 32-deep k-steps");
   constexpr int CK = COUT / 32;                            // k-steps per tap
   constexpr int KSC = (KH / 2) * (KW / 2) * CK;            // the class's k-steps (8)
   constexpr int KHALF = KSC / 2;
-  const int inst = blockIdx.z;
   const int PH = a.IH / 2, PW = a.IW / 2, crow = PH * PW, cmt = (crow + 15) / 16;
-  int blk = blockIdx.x;
+  int blk = bx;
   const int mt = blk % cmt;
   blk /= cmt;
   const int cls = blk & 3, b = blk >> 2, cy = cls >> 1, cx = cls & 1;
@@ -284,6 +312,11 @@ __global__ void __launch_bounds__(256) dgrad_s2_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     if (orow[i] >= 0) out[orow[i] * a.ldo + n] = (act_t)(mk[i] > 0.f ? acc[i] : 0.f);
+}
+
+template <int COUT, int KH, int KW>
+__global__ void __launch_bounds__(256) dgrad_s2_kernel(ConvArgs a) {
+  dgrad_s2_body<COUT, KH, KW>(a, blockIdx.x, blockIdx.z);
 }
 
 // ================================================================ weight grad
@@ -991,6 +1024,67 @@ __global__ void __launch_bounds__(kHeadThreads) head_loss_kernel(HeadArgs a) {
 
 using namespace dqn;
 
+// ================================================================ dgrad chain
+// (ChainArgs, dqn_nets_k.h) The three dgrad GEMMs of the Nature backward in one launch: a stage
+// waits for its own inputs only (row group / sample counters), so the launch boundaries between
+// them -- drain + ramp, ~2-3 us each -- become overlap. Producers' outputs are write-through
+// full lines, and a consumer reads a line only after its counter says every writer finished, so
+// its L2 cannot hold an older copy of it (L2 is invalidated at kernel start).
+// counters: one per 128-byte line (kChainStride ints), so the pollers of one counter never share
+// a line with another counter's arrivals
+constexpr int kChainStride = 32;
+
+DQN_DEV void chain_arrive(int32_t* c, int n) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's write-through stores done
+  __syncthreads();
+  if (threadIdx.x < n)
+    __hip_atomic_fetch_add(c + threadIdx.x * kChainStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+DQN_DEV void chain_wait(const int32_t* c, int want, int32_t* err) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(8);                             // (~0.2 us: light on the counter's line)
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {    // 1 s: flag it, never hang
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) dgrad_chain_kernel(ChainArgs c) {
+  int b = blockIdx.x;
+  int32_t* c0 = c.cnt;                                      // stage-0 row groups
+  int32_t* c1 = c.cnt + c.gx0 * kChainStride;               // stage-1 samples
+  int32_t* err = c1 + c.B * kChainStride;
+  if (b < c.n0) {
+    const int bx = b % c.gx0, by = b / c.gx0;
+    igemm_body<DenseLoader, 1, 2, 1, 2, 2, 2, 8, true>(c.a[0], bx, by, 0, c.gx0, c.gy0, 1);
+    chain_arrive(c0 + bx * kChainStride, 1);
+    return;
+  }
+  b -= c.n0;
+  if (b < c.n1) {
+    const int m0 = b * 16, m1 = min(m0 + 15, c.a[1].M - 1);
+    const int s0 = m0 / c.rows1, s1 = m1 / c.rows1;
+    chain_wait(c0 + (s0 / 16) * kChainStride, c.gy0, err);
+    if (s1 / 16 != s0 / 16) chain_wait(c0 + (s1 / 16) * kChainStride, c.gy0, err);
+    igemm_body<DgradLoader<64, 3, 3, 1>, 1, 2, 1, 2, 2, 2, 9, true>(c.a[1], b, 0, 0, c.n1, 1, 1);
+    if (c.n2 > 0) chain_arrive(c1 + s0 * kChainStride, s1 - s0 + 1);
+    return;
+  }
+  b -= c.n1;
+  const ConvArgs& a2 = c.a[2];
+  const int cmt = ((a2.IH / 2) * (a2.IW / 2) + 15) / 16;
+  const int s = (b / cmt) >> 2;                                  // dgrad_s2_body's block order
+  const int need = (s * c.rows1 + c.rows1 - 1) / 16 - (s * c.rows1) / 16 + 1;
+  chain_wait(c1 + s * kChainStride, need, err);
+  dgrad_s2_body<64, 4, 4>(a2, b, 0);
+}
+
 // ------------------------------------------------------------------ launchers
 void launch_pack(const float* src, void* dst, const PackJob* jobs_dev, int njobs, int max_threads, void* dst2,
                  const int64_t* step, int freq, hipStream_t st) {
@@ -1044,6 +1138,35 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
       IGEMM_LAUNCH_U(NatD2, 1, 2, 2, 1, 2, 2, 8); return 0;     // 32 k-steps
     default: return -1;
   }
+}
+
+int launch_dgrad_chain(const ConvArgs& a0, const ConvArgs& a1, const ConvArgs& a2, int32_t* cnt, int B,
+                       hipStream_t st) {
+  // stage 0: dense dgrad, 16-row x 64-column tiles (full 128-byte lines of dz3 per block row)
+  // stage 1: conv3 dgrad (64 input channels = one 128-byte line per row)
+  // stage 2: conv2 dgrad by parity classes (the conditions of launch_igemm's D2 fast path)
+  // (a2.out == nullptr: two stages -- the conv2 dgrad stays its own launch, where its 52-VGPR blocks
+  //  run 8 per SIMD instead of the chain's 3)
+  const bool s2 = a2.out[0] != nullptr;
+  if (cnt == nullptr || B < 1 || B > 1024 || a0.M != B || a0.N % 64 != 0 || a1.N != 64 || a1.M % B != 0 ||
+      a1.in[0] != a0.out[0] || a1.zero_ptr != nullptr || a1.loss_parts != nullptr || a0.gth != nullptr)
+    return -1;
+  if (s2 && (a2.N16 != 2 || a2.IH % 2 != 0 || a2.IW % 2 != 0 || a2.pad_t != 0 || a2.pad_l != 0 ||
+             2 * a2.OH + 2 != a2.IH || 2 * a2.OW + 2 != a2.IW || a2.M != B * a2.IH * a2.IW ||
+             a2.in[0] != a1.out[0] || a2.zero_ptr != nullptr || a2.loss_parts != nullptr))
+    return -1;
+  ChainArgs c{};
+  c.a[0] = a0; c.a[1] = a1; c.a[2] = a2;
+  c.gx0 = (B + 15) / 16;
+  c.gy0 = a0.N / 64;
+  c.n0 = c.gx0 * c.gy0;
+  c.n1 = (a1.M + 15) / 16;
+  c.rows1 = a1.M / B;
+  c.n2 = s2 ? B * 4 * (((a2.IH / 2) * (a2.IW / 2) + 15) / 16) : 0;
+  c.B = B;
+  c.cnt = cnt;
+  hipLaunchKernelGGL(dgrad_chain_kernel, dim3(c.n0 + c.n1 + c.n2), dim3(256), 0, st, c);
+  return 0;
 }
 
 #define WGRAD_LAUNCH(LD, MC, KB, NB)                                                                   \

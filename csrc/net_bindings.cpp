@@ -79,6 +79,31 @@ void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::v
   TORCH_CHECK(launch_igemm((int)kind, a, (int)in.size(), cur_stream()) == 0, "unknown igemm kind ", kind);
 }
 
+// The Nature dgrad chain in one launch (qnet.hip dgrad_chain_kernel): the fc dgrad (with its aux
+// side duties, as igemm), the conv3 dgrad and the conv2 parity dgrad; cnt: int32 counters, one per
+// 32 ints ((ceil(B / 16) + B + 1) * 32, zeroed by the step's fc forward launch)
+void dgrad_chain(int64_t in0, int64_t w0, int64_t out0, int64_t mask0, std::vector<int64_t> dims0,
+                 std::vector<int64_t> aux0, std::vector<double> aux_f0, int64_t w1, int64_t out1, int64_t mask1,
+                 std::vector<int64_t> dims1, int64_t w2, int64_t out2, int64_t mask2, std::vector<int64_t> dims2,
+                 int64_t cnt, int64_t B) {
+  dqn::ConvArgs a0 = conv_args({in0}, {w0}, {}, {out0}, {mask0}, {1.0}, dims0);
+  TORCH_CHECK((aux0.size() == 5 || aux0.size() == 9) && aux_f0.size() == 1 && aux0[0] % 16 == 0 && aux0[1] % 4 == 0 &&
+                  aux0[3] <= 64, "dgrad_chain aux = [zero_ptr, zero_n, loss_parts, nparts, loss_out(, noise)]");
+  a0.zero_ptr = P<float*>(aux0[0]); a0.zero_n = (int)aux0[1];
+  a0.loss_parts = P<const float*>(aux0[2]); a0.nparts = (int)aux0[3]; a0.loss_out = P<float*>(aux0[4]);
+  a0.loss_mul = (float)aux_f0[0];
+  if (aux0.size() == 9) {
+    TORCH_CHECK(aux0[5] != 0 && aux0[7] >= 1 && aux0[8] != 0, "dgrad_chain noise duty: out0, n, rng");
+    a0.nz_out0 = P<float*>(aux0[5]); a0.nz_out1 = P<float*>(aux0[6]); a0.nz_n = (int)aux0[7];
+    a0.nz_rng = P<const int64_t*>(aux0[8]);
+  }
+  TORCH_CHECK(a0.loss_parts == nullptr || a0.loss_out != nullptr, "dgrad_chain aux: loss output");
+  dqn::ConvArgs a1 = conv_args({out0}, {w1}, {}, {out1}, {mask1}, {1.0}, dims1);
+  dqn::ConvArgs a2 = conv_args({out1}, {w2}, {}, {out2}, {mask2}, {1.0}, dims2);   // out2 = 0: two stages
+  TORCH_CHECK(launch_dgrad_chain(a0, a1, a2, P<int32_t*>(cnt), (int)B, cur_stream()) == 0,
+              "dgrad_chain: shapes outside the chained kernel");
+}
+
 void wgrad(int64_t kind, int64_t in, std::vector<int64_t> dims, int64_t dz, int64_t ldz, int64_t dw, int64_t db,
            int64_t dw2, int64_t db2, int64_t nsplit, int64_t N, int64_t MC, int64_t KB, int64_t NB, double scale,
            bool atomic, int64_t mloop, bool db_zero) {
@@ -298,8 +323,8 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
              std::vector<int64_t> io, std::vector<int64_t> qp, std::vector<int64_t> actor, std::vector<double> actor_f,
              int64_t act_h, std::vector<int64_t> fold, int64_t prof) {
   dqn::ConvArgs a = conv_args(in, w, bias, out, {}, std::vector<double>(in.size(), 1.0), dims);
-  TORCH_CHECK(flts.size() == 1 && qp.size() == 2 && (fold.size() == 4 || fold.size() == 6),
-              "fc_head: flts = [delta], qp, fold = [qacc, cnt, Mpad, nlearn(, dqg, dq_epoch)]");
+  TORCH_CHECK(flts.size() == 1 && qp.size() == 2 && (fold.size() == 4 || fold.size() == 6 || fold.size() == 8),
+              "fc_head: flts = [delta], qp, fold = [qacc, cnt, Mpad, nlearn(, dqg, dq_epoch(, zero_ptr, zero_n))]");
   dqn::HeadArgs hd = head_args(ints, h, hw, hb, hwv, hbv, io, {}, {}, {}, actor, actor_f, act_h);
   TORCH_CHECK(!hd.infer, "fc_head: training launches only");
   hd.delta = (float)flts[0];
@@ -312,10 +337,15 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
   f.nlearn = (int)fold[3];
   f.ngroups = (a.M + 15) / 16;
   f.prof = P<int64_t*>(prof);
-  if (fold.size() == 6) {      // spin mode: the online blocks write their own dH tiles
+  if (fold.size() >= 6 && fold[4] != 0) {     // spin mode: the online blocks write their own dH tiles
     f.spin = 1;
     f.dqg = P<float*>(fold[4]);
     f.dq_epoch = P<int32_t*>(fold[5]);
+  }
+  if (fold.size() == 8 && fold[6] != 0) {      // zero duty (the step's dgrad-chain counters)
+    TORCH_CHECK(fold[6] % 16 == 0 && fold[7] % 4 == 0, "fc_head: zero range 16-byte aligned, n % 4 == 0");
+    f.zero_ptr = P<float*>(fold[6]);
+    f.zero_n = (int)fold[7];
   }
   TORCH_CHECK(f.qacc && f.cnt && (f.nlearn == 2 || f.nlearn == 3), "fc_head: fold buffers, 2-3 learner instances");
   TORCH_CHECK((int)in.size() == f.nlearn + (hd.act_E > 0 ? 1 : 0) && out.size() == in.size() && bias.size() == in.size() &&
@@ -434,6 +464,7 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("dw"), pybind11::arg("db"), pybind11::arg("dw2"), pybind11::arg("db2"), pybind11::arg("nsplit"), pybind11::arg("N"), pybind11::arg("MC"),
         pybind11::arg("KB"), pybind11::arg("NB"), pybind11::arg("scale"), pybind11::arg("atomic"), pybind11::arg("mloop") = 1,
         pybind11::arg("db_zero") = false);
+  m.def("qnet_dgrad_chain", &dgrad_chain);
   m.def("qnet_fc_head", &fc_head, pybind11::arg("inp"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("out"), pybind11::arg("dims"), pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("hw"), pybind11::arg("hb"), pybind11::arg("hwv"), pybind11::arg("hbv"), pybind11::arg("io"),

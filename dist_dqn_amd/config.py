@@ -186,6 +186,10 @@ def build_parser() -> argparse.ArgumentParser:
     a('--fold_head', default=1, type=int,
       help='HIP executor, scalar heads: fc forward + output layer + TD loss + dQ / dH (+ the fused acting '
            'step) in ONE launch (csrc/kernels/fc_head.hip) instead of the fc launch + the head launch')
+    a('--chain_dgrad', default=0, type=int,
+      help='HIP executor, Nature net: 1 = the fc and conv3 data gradients in ONE launch whose stages wait on '
+           'per-sample counters (dgrad_chain_kernel; 2: the conv2 dgrad too); 0 (default: measured faster) = '
+           'separate launches')
     a('--fuse_fc_wgrad', default=1, type=int,
       help='HIP executor (16-bit builds): form the fc weight gradient (X^T dH, rank <= B) inside the '
            'fused optimizer launch instead of writing and re-reading it as an fp32 gradient')
@@ -299,6 +303,7 @@ class Config:
     fuse_sampling: int = 2
     fuse_fc_wgrad: int = 1
     fold_head: int = 1
+    chain_dgrad: int = 0
     fuse_wgrad_update: int = 1
     det_wgrad: int = 0
     summary_secs: float = 120.0

@@ -95,6 +95,8 @@ class Learner:
         ex = network.executor
         if hasattr(ex, 'fold_head'):
             ex.fold_head = bool(int(getattr(config, 'fold_head', 1)))
+        if hasattr(ex, 'chain_dgrad'):
+            ex.chain_dgrad = int(getattr(config, 'chain_dgrad', 0))
         # the fc weight / bias gradient formed inside the fused optimizer launch from the fc input
         # rows and dH rows (executor.can_defer_fc): no fp32 fc gradient round trip through HBM.
         # Under DP only with the low-rank exchange (the rows are then every rank's)

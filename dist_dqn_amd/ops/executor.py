@@ -104,6 +104,11 @@ class HipExecutor:
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self.fold_head = True       # training: fc forward + scalar head in one launch (fc_head.hip)
+        # fc + conv3 dgrads in one launch (dgrad_chain_kernel; 2: + conv2). Opt-in: measured 12.1 us vs
+        # 4.96 + 5.16 us for the two launches (the waits and the write-through stores cost more than the
+        # launch boundary saves; 14.34k / 13.99k / 14.50k steps/s for 1 / 2 / 0, profiles/r4_dgrad_chain_ab.jsonl)
+        self.chain_dgrad = 0
+        self._fc_zero = None        # int32 counters the next fc forward launch zeroes (the chain's)
         self.grouped_wgrad = True   # every layer's weight gradient in ONE launch after the dgrad chain
         # (round 2 measured the fc + output-layer members on a parallel graph branch beside the dgrad
         # chain: 12.0k -> 9.9k steps/s, the captured fork / join costs more than the overlap gains)
@@ -845,10 +850,12 @@ class HipExecutor:
 
     def _fc_fwd(self, packs, flats, ws, B, ninst):
         fcb = [p.data_ptr() + self.esz * self.poff['fc/bias'] for p in packs]
+        z = self._fc_zero                  # (the step's dgrad-chain counters: zeroed by this launch)
         self.ext.qnet_igemm(_KIND['DFWD'], [ws['x3'][i].data_ptr() for i in range(ninst)],
                             [p.data_ptr() + self.esz * self.poff['fc/fwd'] for p in packs], fcb,
                             [ws['h'][i].data_ptr() for i in range(ninst)], [], [1.0] * ninst,
-                            [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0])
+                            [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0],
+                            [z.data_ptr(), z.numel(), 0, 0, 0] if z is not None else [], [1.0] if z is not None else [])
 
     def can_fold_head(self, B: int, E: int = 0) -> bool:
         """Whether the training step's fc forward and scalar head run as ONE launch
@@ -882,7 +889,8 @@ class HipExecutor:
                               ints, [self.delta], [ws['h'][i].data_ptr() for i in range(nlearn)], w, b, wv, bv, io,
                               [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()], actor, actor_f, act_h,
                               [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn, fw['dqg'].data_ptr(),
-                               fw['epoch'].data_ptr()],
+                               fw['epoch'].data_ptr()] +
+                              ([self._fc_zero.data_ptr(), self._fc_zero.numel()] if self._fc_zero is not None else []),
                               self.fold_prof.data_ptr() if self.fold_prof is not None else 0)
 
     def _head_ptrs(self, flats):
@@ -1004,22 +1012,45 @@ class HipExecutor:
         head kernel wrote dH; C51: dH = (dout16 [W | Wv]^T) * (h > 0) is one more igemm launch
         before it, over the head's dL/dlogits rows. draw_noise = (out0, out1, rng): the launch
         also draws the next noisy-net samples (see ``loss_and_grad``)."""
-        F, HH = self.FLAT, self.HH
-        dh = ws['dh'].data_ptr()
         if self.dist and not dh_done:
             self._c51_dh(ws, B, po)
+        dh, pk, dz3, x3, dims, aux, aux_f = self._fc_dgrad_args(ws, B, po, zero, draw_noise)
+        if gather is not None:          # (device XgmiGatherArgs ptr, blocks): the low-rank all-gather duty
+            aux += [int(gather[0]), int(gather[1])]
+        self.ext.qnet_igemm(_KIND['DDGRAD'], [dh], [pk], [], [dz3], [x3], [1.0], dims, aux, aux_f)
+
+    def _fc_dgrad_args(self, ws, B, po, zero=(), draw_noise=None):
+        """(dH, packed W_fc dgrad fragments, dz3, x3 mask, dims, aux, aux_f) of the fc dgrad launch:
+        aux = the side duties (zero the conv gradient range, sum the loss partials, draw noise)."""
+        F, HH = self.FLAT, self.HH
         pk = po.data_ptr() + self.esz * self.poff['fc/dgrad']
-        x3, dz3 = ws['x3'][0].data_ptr(), ws['dz3'].data_ptr()
         zp, zn = (zero[0], zero[1]) if zero else (0, 0)
         aux = [zp, zn, ws['loss_parts'].data_ptr(), self._loss_parts(B), ws['loss'].data_ptr()]
         if draw_noise is not None:
             o0, o1, rng = draw_noise
             assert o0.dtype == torch.float32 and (o1 is None or o1.numel() == o0.numel()) and rng.dtype == torch.int64
             aux += [o0.data_ptr(), o1.data_ptr() if o1 is not None else 0, o0.numel(), rng.data_ptr()]
-        if gather is not None:          # (device XgmiGatherArgs ptr, blocks): the low-rank all-gather duty
-            aux += [int(gather[0]), int(gather[1])]
-        self.ext.qnet_igemm(_KIND['DDGRAD'], [dh], [pk], [], [dz3], [x3], [1.0],
-                            [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0], aux, [1.0 / B])
+        return (ws['dh'].data_ptr(), pk, ws['dz3'].data_ptr(), ws['x3'][0].data_ptr(),
+                [B, F, HH, F // 16, F, 0, 0, 0, 0, 0, 0], aux, [1.0 / B])
+
+    def can_chain_dgrad(self, B: int) -> bool:
+        """Whether the Nature backward's fc / conv3 / conv2 dgrads run as ONE launch
+        (qnet.hip dgrad_chain_kernel): 16-bit or fp32 builds, the grouped-wgrad path, one stream."""
+        return (self.chain_dgrad and self.arch.network == 'nature' and self.grouped_wgrad and not self.two_stream
+                and B <= 1024 and self.FLAT % 64 == 0 and self.arch.convs[2].cin == 64)
+
+    def chain_error(self, B, dev) -> bool:
+        """True if a dgrad-chain stage gave up waiting for its inputs (host sync)."""
+        return int(self._chain_ws(B, dev)[((B + 15) // 16 + B) * 32]) != 0
+
+    def _chain_ws(self, B, dev):
+        key = ('chain', B, dev.index if dev.index is not None else 0)
+        t = self._ws.get(key)
+        if t is None:
+            n = ((B + 15) // 16 + B + 1) * 32         # one counter per 128-byte line
+            t = torch.zeros(n, dtype=torch.int32, device=dev)
+            self._ws[key] = t
+        return t
 
     def _head_wgrad_members(self, ws, B, h0, hgrads):
         """Grouped-wgrad members of the output layer: dW = h^T dZ (dueling: advantage stream over
@@ -1134,6 +1165,11 @@ class HipExecutor:
             assert self.fused_trunk and frames is not None, 'deferred sampling needs the fused trunk'
         sample = (spec, ninst) if spec is not None else None
         fold = self.can_fold_head(B, 0 if acting is None else E)
+        # the fc / conv3 / conv2 dgrads as one launch (single-process grouped-wgrad path); its
+        # counters are zeroed by this step's fc forward launch
+        chain = (self.can_chain_dgrad(B) and not split and lowrank is None and B <= 32
+                 and self.arch.network == 'nature')
+        self._fc_zero = self._chain_ws(B, dev) if chain else None
         if acting is None:
             self._fwd_trunk(xs, packs, flats, ws, B, ninst, frames=frames, sample=sample, fc=not fold)
         else:
@@ -1173,6 +1209,7 @@ class HipExecutor:
             self._head(hints, [ws['h'][i].data_ptr() for i in range(ninst)], w, b, wv, bv, hio,
                        *self._head_packs(packs), [],          # (the conv grad range is zeroed by the fc dgrad)
                        hactor, hactor_f, act_h=act_h, ws=ws)
+        self._fc_zero = None                # (consumed by this step's fc forward launch)
         # ---- backward (online instance 0 only)
         c1, c2, c3 = self.arch.convs
         (h1, w1), (h2, w2), (h3, w3) = c1.out_hw, c2.out_hw, c3.out_hw
@@ -1267,18 +1304,30 @@ class HipExecutor:
                 # dense weight gradients now (they need only dh, dQ and x3 / h): the dense range is final
                 ext.qnet_wgrad_group(members[3:], dims[3:], scales[3:])
                 members, dims, scales = members[:3], dims[:3], scales[:3]
-            else:
+            elif not chain:
                 fc_dgrad()
+            d3 = [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3, 0, 0]
+            d2 = [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2, 0, 0]
 
             def tail():
-                ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [],
-                               [ws['dz2'].data_ptr()], [x2], [1.0],
-                               [B * h2 * w2, c3.cin, c3.k * c3.k * c3.cout, c3.cin // 16, c3.cin, h2, w2, h3, w3,
-                                0, 0])
-                ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [],
-                               [ws['dz1'].data_ptr()], [x1], [1.0],
-                               [B * h1 * w1, c2.cin, c2.k * c2.k * c2.cout, c2.cin // 16, c2.cin, h1, w1, h2, w2,
-                                0, 0])
+                if chain:
+                    # fc dgrad (+ its side duties) -> conv3 dgrad -> conv2 dgrad: ONE launch
+                    if self.dist:                   # C51: dH = dlogits [W | Wv]^T * (h > 0) first
+                        self._c51_dh(ws, B, po)
+                    dh, pk, dz3, x3m, dims0, aux0, auxf0 = self._fc_dgrad_args(ws, B, po, zero, draw_noise)
+                    three = self.chain_dgrad >= 2       # (2: the conv2 dgrad inside the chain too)
+                    ext.qnet_dgrad_chain(dh, pk, dz3, x3m, dims0, aux0, auxf0, pko('conv3/dgrad'),
+                                         ws['dz2'].data_ptr(), x2, d3, pko('conv2/dgrad'),
+                                         ws['dz1'].data_ptr() if three else 0, x1, d2,
+                                         self._chain_ws(B, dev).data_ptr(), B)
+                    if not three:
+                        ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [],
+                                       [ws['dz1'].data_ptr()], [x1], [1.0], d2)
+                else:
+                    ext.qnet_igemm(_KIND['D3'], [ws['dz3'].data_ptr()], [pko('conv3/dgrad')], [],
+                                   [ws['dz2'].data_ptr()], [x2], [1.0], d3)
+                    ext.qnet_igemm(_KIND['D2'], [ws['dz2'].data_ptr()], [pko('conv2/dgrad')], [],
+                                   [ws['dz1'].data_ptr()], [x1], [1.0], d2)
                 if dwg:                 # the next update_and_pack runs the group beside the fc update
                     self._wg_pending = (members, dims, scales)
                 else:

@@ -420,3 +420,48 @@ def test_det_wgrad_conv_update_matches_fp32_oracle():
         assert cos > 0.98 and abs(ratio - 1.0) < 0.05, (n, cos, ratio)
         seen += 1
     assert seen == 6
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', RAINBOW])
+def test_dgrad_chain_matches_separate_launches(extra):
+    """fc dgrad -> conv3 dgrad (-> conv2 dgrad) in ONE launch (dgrad_chain_kernel: stages wait on
+    per-sample counters, producers store write-through) vs the three launches: the same dz3 / dz2 /
+    dz1 bit for bit (same GEMMs, same split-K order) over two steps, and the same gradients."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.models.network import Network
+    B = 32
+    outs = []
+    for chain in (1, 2, 0):
+        cfg = preset('nature', 'Pong-v0', '--seed=3 --backend=hip --dtype=bf16 %s' % extra)
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+        g = torch.Generator(device=DEV).manual_seed(4)
+        net.online.flat.normal_(0.0, 0.03, generator=g)
+        net.target.flat.normal_(0.0, 0.03, generator=g)
+        net.refresh_packed()
+        ex = net.executor
+        ex.chain_dgrad = chain                  # (opt-in: the default is 0, measured faster)
+        assert bool(ex.can_chain_dgrad(B)) == bool(chain)
+        res = []
+        for it in range(2):
+            batch = {
+                'states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
+                'next_states': torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device=DEV, generator=g),
+                'actions': torch.randint(0, 6, (B,), dtype=torch.int32, device=DEV, generator=g),
+                'rewards': torch.randn(B, device=DEV, generator=g) * 5.0,
+                'dones': (torch.rand(B, device=DEV, generator=g) < 0.2).float(),
+                'gammas': torch.full((B,), 0.99, device=DEV),
+            }
+            grad = torch.zeros_like(net.online.flat)
+            noise, tnoise = (net.noise, net.noise_target) if ex.noisy else (None, None)
+            loss, _ = ex.loss_and_grad(net.online.flat, net.target.flat, batch, grad, noise, tnoise)
+            torch.cuda.synchronize()
+            ws = ex._workspace(B, DEV)
+            res.append((ws['dz3'].clone(), ws['dz2'].clone(), ws['dz1'].clone(), float(loss), grad.clone()))
+        if chain:
+            assert not ex.chain_error(B, DEV)
+        outs.append(res)
+    for run in outs[:2]:                      # the 2-stage and the 3-stage chain vs separate launches
+        for (a3, a2, a1, la, ga), (b3, b2, b1, lb, gb) in zip(run, outs[2]):
+            assert torch.equal(a3, b3) and torch.equal(a2, b2) and torch.equal(a1, b1)
+            assert la == lb
+            torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-7)
