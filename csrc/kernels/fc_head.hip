@@ -43,6 +43,7 @@ struct FoldLds {
   float w2[kFoldMaxHid * kFoldMaxA + kFoldMaxHid];   // tail: online output layer (+ value column)
   float q[3][17][33];                          // tail: Q rows per instance (+ the bias row)
   float dq[16][33];                            // tail: dQ rows (| dV at A)
+  int32_t pst[16][4];                          // actor tail: the envs' frame stacks
   int flag;
 };
 
@@ -70,9 +71,15 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   const bool dh_tile = f.spin && !actor_inst && inst == 0;   // this block writes its own dH tile
   int e0 = 0;                                   // the group's dQ epoch before this launch's tail
   if (dh_tile) e0 = __hip_atomic_load(f.dq_epoch + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ActorPre pre{};
   const bool frames_duty = actor_inst && nt < h.act_E;
-  if (frames_duty) pre = actor_prefetch(h.actor);   // (before the arrival: the tail advances it)
+  // the frame duty's rng / cursor words (before the arrival: the tail advances them); scalars,
+  // not an ActorPre (whose per-thread stack array put 88 bytes per lane in scratch)
+  int64_t pf0 = 0, pseed = 0, pctr = 0;
+  if (frames_duty) {
+    pf0 = h.actor.cursor[1];
+    pseed = h.actor.rng[0];
+    pctr = h.actor.rng[1];
+  }
   // the tile's 16 rows of the output layer (advantage / plain [16][A], or the 16 value weights),
   // staged now: their loads complete under the k-loop instead of after it
   const int wi = actor_inst ? 0 : inst;        // output-layer weights of the instance
@@ -191,7 +198,13 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     FOLD_MARK(3);
   }
   __syncthreads();
-  if (frames_duty) actor_env_frames(h.actor, nt, pre);       // env nt's new frame(s): rng only
+  if (frames_duty) {                                         // env nt's new frame(s): rng only
+    ActorPre pre{};
+    pre.f0 = pf0;
+    pre.seed = (uint64_t)pseed;
+    pre.ctr = (uint64_t)pctr;
+    actor_env_frames(h.actor, nt, pre);
+  }
   // dH tile of this block from the group's dQ rows: (dQ W2^T)[rows][the tile's 16 units] * (h > 0)
   auto dh_from = [&](const float (*dq)[33]) {
     if (tid < 256) {
@@ -308,10 +321,12 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     // ---- fused acting: decision + replay append per env, state advance, PER insert
     const ActorArgs& x = h.actor;
     const ActorPre p = actor_prefetch(x);
+    // (env e's stack through LDS: a pointer into the private ActorPre::st would put it in scratch)
+    if (tid < x.E)
+      for (int c2 = 0; c2 < 4; ++c2) S.pst[tid][c2] = p.st[c2];
     for (int e = tid; e < x.E; e += kFoldThreads) {
       int fs, rs;
-      actor_env_step(x, S.q[0][e], e, p.t0, p.f0, p.eps0, p.eps_min, p.decay, p.seed, p.ctr, fs, rs,
-                     e == tid ? p.st : nullptr);
+      actor_env_step(x, S.q[0][e], e, p.t0, p.f0, p.eps0, p.eps_min, p.decay, p.seed, p.ctr, fs, rs, S.pst[e]);
     }
     if (tid == 0) actor_advance(x, p.t0, p.f0, p.size0, p.eps0, p.eps_min, p.decay, p.ctr, p.frames_done);
     if (x.tsum != nullptr)

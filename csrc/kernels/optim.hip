@@ -171,7 +171,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   // WG: the launch also computes the grouped weight gradients (tiles after the lead block)
   const bool wgm = wg != nullptr && ff.x != nullptr && op >= 0;
   if (wg != nullptr && !wgm) return;      // (binding checks: a WG launch needs FcFuse rows and an update)
-  (void)wg_jobs;                          // (WG: fc jobs first, then the jobs waiting on a range)
+  (void)wg_jobs;                          // (WG: fc jobs first, then one block per job waiting on a range)
   // + the lead block (sampler / closer) + the weight-gradient tiles
   L.grid = (njobs < cap ? njobs : cap) + (L.smp.size != nullptr || L.per.sum != nullptr || wgm ? 1 : 0) +
            (wgm ? wg_blocks : 0);

@@ -26,7 +26,10 @@ struct OptHP {
   // (ready: a dependent job's wait is over / the sampler's draw is done)
   int64_t* prof;
 };
-constexpr int kProfPhases = 16, kTlBlocks = 4096, kTilePhBlocks = 512;   // (+ [8] tile phases per wgrad block)
+constexpr int kProfPhases = 16, kTlBlocks = 4096, kTilePhBlocks = 512;
+// (two fc jobs per block of a WG launch would halve its 785 fc blocks -- they reach the CUs over
+//  ~4 us, behind the weight-gradient tiles -- but a second inlined job raised the launch from 97
+//  to 168 VGPRs, 3 waves / SIMD; measured round 4, not kept)   // (+ [8] tile phases per wgrad block)
 
 // Contraction is pinned off in the update math so every kernel that inlines it
 // (optim_kernel's float4 loop, optim_pack_kernel's tiles) rounds identically:
@@ -179,6 +182,20 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 // (128 VGPRs: no spills in the item body, occupancy is moot) and a returning arrival ticket per
 // block -- the last block to arrive closes the launch, nobody polls.
 constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8, kModeWg = 16, kModeFew = 32;
+
+// A static LDS buffer only in the instantiations that use one (ALLOC; TAG keeps two buffers of one
+// size apart): the WG launches must carry no static LDS (see smem below).
+template <bool ALLOC, size_t N, int TAG>
+struct OptShm {
+  DQN_DEV static unsigned char* get() {
+    __shared__ __attribute__((aligned(16))) unsigned char b[N];
+    return b;
+  }
+};
+template <size_t N, int TAG>
+struct OptShm<false, N, TAG> {
+  DQN_DEV static unsigned char* get() { return nullptr; }
+};
 template <int OP, int MODE>
 __global__ void __launch_bounds__(kPackThreads, (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? 8 : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
@@ -209,8 +226,11 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // LDS: the sampler block's scratch (the update items exchange through DPP); WG launches carve
   // everything (weight-gradient staging, FcFuse staging) from the dynamic buffer instead
   constexpr size_t kSmpLds = sizeof(SampleLds) > sizeof(SumtreeLds) ? sizeof(SampleLds) : sizeof(SumtreeLds);
-  __shared__ __attribute__((aligned(16))) unsigned char smem[WG ? 16 : kSmpLds];
   extern __shared__ __attribute__((aligned(16))) unsigned char opt_dyn[];
+  // (WG: no static LDS at all -- with even a few static bytes the 40 KB dynamic buffer became
+  //  41.5 KB per block, 3 blocks per CU instead of 4, and the fc jobs queued behind the tiles;
+  //  the lead block's sampler uses the dynamic buffer, which no tile of it needs)
+  unsigned char* smem = WG ? opt_dyn : OptShm<!WG, kSmpLds, 0>::get();
   int64_t* tl = (h.prof != nullptr && threadIdx.x == 0 && blockIdx.x < kTlBlocks) ? h.prof + kProfPhases + 3 * blockIdx.x
                                                                                     : nullptr;
   if (tl) { tl[0] = (int64_t)__builtin_amdgcn_s_memrealtime(); tl[1] = 0; tl[2] = 0; }
@@ -298,8 +318,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   }
   OPT_MARK(1);
 #if !DQN_ACT_F32
-  __shared__ __attribute__((aligned(16))) unsigned char fcl_s[FC && !WG ? kFcLds : 16];
-  unsigned char* fcl = WG ? opt_dyn : fcl_s;
+  unsigned char* fcl = WG ? opt_dyn : OptShm<!WG, FC ? kFcLds : 16, 1>::get();
   // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
   // this thread's 8-element piece of fc operand rows m0 .. m0 + 31 of the item's 32 (k) x 64 (n)
   // tile: t < 128 a piece of an x row, 128 <= t < 384 one of a dh row
@@ -664,18 +683,15 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         // after every tile in the grid, so the tiles are resident or done: the wait ends)
         const int d = jobs[wid].dep;
         if (d >= 0) {
-          __shared__ int wg_wait_err;
           if (threadIdx.x == 0) {
             const int m = d / kWgSlots;
             const int want = wg->nblk[m] / wg->gy[m];        // tiles per K-range
             const int32_t* c = wg->done + kTicketStride * (kMaxWgradMembers + d);
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            wg_wait_err = 0;
             while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
               __builtin_amdgcn_s_sleep(2);
               if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s: flag, do not hang
                 ticket[kErrFlag] = 1;
-                wg_wait_err = 1;
                 break;
               }
             }
@@ -683,7 +699,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
           __syncthreads();
-          (void)wg_wait_err;
         }
       }
 #endif

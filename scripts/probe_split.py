@@ -104,8 +104,12 @@ def main():
     ex._wg_plans = {}
     plan, nwg, jobs, nfc, _ = ex._wg_plan(wg, net.grad, dev)
     if os.environ.get('DQN_OPT_PROF'):
-        out['timeline_us'] = timeline(ex, plan, nwg, jf, nfc, nint, lambda: launch(jobs, fca, plan.data_ptr(), nwg,
+        out['timeline_us'] = timeline(ex, plan, nwg, jobs, nfc, nint, lambda: launch(jobs, fca, plan.data_ptr(), nwg,
                                                                                  sample=smp))
+        # the fc jobs alone (no tiles, no lead block's sampler): their start spread = how fast the
+        # launch gets its blocks onto the CUs
+        t = timeline_fc_only(ex, nfc, lambda: launch(jf, fca))
+        out['timeline_fc_only_us'] = t
         out['timeline_wgrad_only_us'] = timeline(ex, plan, nwg, jf[:nint], 1, nint,
                                                  lambda: launch(jobs, fca, plan.data_ptr(), nwg, nj=1))
         # phases inside the tiles of that launch (us after each tile's start): staged chunk 0 |
@@ -123,6 +127,20 @@ def main():
         out['tile_phases_us'] = {'first_conv1_tiles': rows[:3],
                                  'median_all': [med([r[i] for r in rows]) for i in range(6)]}
     print(json.dumps(out))
+
+
+def timeline_fc_only(ex, nfc, fn):
+    """Start / duration / end percentiles of the blocks of a launch of fc jobs only."""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    t = ex.ext.optim_timeline(nfc + 1)
+    st = [t[3 * b] for b in range(nfc + 1) if t[3 * b]]
+    t0 = min(st)
+    pct = lambda v: [round(sorted(v)[int(q * (len(v) - 1))], 2) for q in (0.0, 0.25, 0.5, 0.75, 1.0)]
+    rows = [(t[3 * b], t[3 * b + 2]) for b in range(nfc + 1) if t[3 * b]]
+    return {'start': pct([(a - t0) / 100.0 for a, _ in rows]), 'dur': pct([(e - a) / 100.0 for a, e in rows]),
+            'end': pct([(e - t0) / 100.0 for _, e in rows]), 'blocks': len(rows)}
 
 
 def timeline(ex, plan, nwg, jobs, nfc, nint, fn):
