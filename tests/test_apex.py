@@ -86,6 +86,25 @@ def test_ingest_service_under_thread_sanitizer(tmp_path):
     assert 'errors 0' in run.stdout, run.stdout
 
 
+@pytest.mark.skipif(shutil.which('g++') is None, reason='needs g++')
+def test_inference_service_under_thread_sanitizer(tmp_path):
+    """The native inference service's core (csrc/host/infer_core.h, the code the GPU binding
+    runs) on a fake device: actor threads' mailbox requests answered through late "H2D / graph /
+    D2H" ops on a stream thread, stats polled during the run, stop."""
+    exe = str(tmp_path / 'infer_stress')
+    src = [os.path.join(ROOT, 'csrc', 'host', f) for f in ('tests/infer_stress.cpp', 'mailbox.cpp')]
+    r = subprocess.run(['g++', '-std=c++17', '-O1', '-g', '-fsanitize=thread', '-I' + os.path.join(ROOT, 'csrc'),
+                        '-o', exe] + src + ['-lpthread'], capture_output=True, text=True)
+    if r.returncode != 0 and 'tsan' in (r.stderr + r.stdout).lower():
+        pytest.skip('ThreadSanitizer runtime unavailable')
+    assert r.returncode == 0, r.stderr
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, TSAN_OPTIONS='halt_on_error=1'))
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert 'ThreadSanitizer' not in run.stderr, run.stderr
+    assert 'errors 0' in run.stdout, run.stdout
+
+
 def test_apex_epsilons():
     e = apex_epsilons(8)
     assert e[0] == pytest.approx(0.4) and e[-1] == pytest.approx(0.4 ** 8)
