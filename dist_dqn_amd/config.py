@@ -183,6 +183,9 @@ def build_parser() -> argparse.ArgumentParser:
            '2 = the previous step\'s optimizer launch draws it (one extra block, off the critical path)')
     a('--summary_secs', default=120.0, type=float,
       help='chief: seconds between global_step/sec summaries (TF Supervisor step counter: 120)')
+    a('--ps_timeout_s', default=60.0, type=float,
+      help='async PS over xGMI: a worker pull that waits longer for the server flags an error (the '
+           'learner raises at its next device check) instead of hanging')
     a('--fold_head', default=1, type=int,
       help='HIP executor, scalar heads: fc forward + output layer + TD loss + dQ / dH (+ the fused acting '
            'step) in ONE launch (csrc/kernels/fc_head.hip) instead of the fc launch + the head launch')
@@ -303,6 +306,7 @@ class Config:
     fuse_sampling: int = 2
     fuse_fc_wgrad: int = 1
     fold_head: int = 1
+    ps_timeout_s: float = 60.0
     chain_dgrad: int = 0
     fuse_wgrad_update: int = 1
     det_wgrad: int = 0

@@ -523,7 +523,7 @@ def make_ps_server(ctx: DistContext, network, config):
 def make_ps_client(ctx: DistContext, flat: torch.Tensor, config):
     if ps_transport(ctx, config) == 'xgmi':
         try:
-            return XgmiPSClient(ctx, flat)
+            return XgmiPSClient(ctx, flat, timeout_s=float(getattr(config, 'ps_timeout_s', 60.0)))
         except RuntimeError as e:
             log.warning('async PS over xgmi unavailable (%s): torch.distributed p2p instead', e)
     return AsyncPSClient(ctx, flat)

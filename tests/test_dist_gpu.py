@@ -354,6 +354,58 @@ def test_async_ps_hip_learners_one_gpu(transport):
     _run_ranks(_worker_async_ps, (transport,), world=3, timeout=150)
 
 
+def _worker_ps_stall(rank, world, port, errq):
+    """The server answers 2 pushes, then stops answering (a stalled / dead PS): the worker's pull
+    times out on the device (2 s) and the learner's next device check raises instead of training
+    on un-pulled parameters."""
+    try:
+        _setup(rank, world, port)
+        from dist_dqn_amd.config import preset
+        from dist_dqn_amd.learner import Learner
+        from dist_dqn_amd.models.network import Network
+        from dist_dqn_amd.parallel import broadcast_state, init_distributed
+        from dist_dqn_amd.parallel.async_ps import make_ps_client, make_ps_server
+        from dist_dqn_amd.replay import DeviceReplay
+        cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=5 --backend=hip --replay_memory_capacity=2048 '
+                     '--async_ps --ps_transport=xgmi --ps_timeout_s=2 --allreduce_check_steps=1 --hip_graph=0')
+        ctx = init_distributed(cfg, device='cuda')
+        net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
+        broadcast_state(ctx, net)
+        if rank == 0:
+            srv = make_ps_server(ctx, net, cfg)
+            assert srv.serve(max_updates=2) == 2
+            dist.barrier()                                  # (the worker saw its error)
+            srv.close()
+        else:
+            rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
+            rep.fill_synthetic(2048, 6, seed=rank)
+            ps = make_ps_client(ctx, net.online.flat, cfg)
+            ps.pull(net.online.flat, net.global_step)
+            net.refresh_packed()
+            ln = Learner(net, rep, cfg, ctx, ps_client=ps)
+            raised = None
+            for _ in range(5):
+                try:
+                    ln.step()
+                except RuntimeError as e:
+                    raised = str(e)
+                    break
+            assert raised is not None and 'parameter server' in raised, raised
+            assert ln.train_steps <= 4, ln.train_steps
+            torch.cuda.synchronize()
+            ps.close()
+            dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 - report to the parent
+        import traceback
+        errq.put('rank %d: %s\n%s' % (rank, e, traceback.format_exc()))
+        raise
+
+
+def test_async_ps_worker_raises_when_the_server_stalls():
+    _run_ranks(_worker_ps_stall, (), world=2, timeout=150)
+
+
 # ------------------------------------------------------- DP == the big-batch step
 # The reference's synchronous mode aggregates the replicas' gradients into ONE update
 # (SyncReplicasOptimizer, /root/reference/src/network.py:186-202): W ranks with B samples each
