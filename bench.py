@@ -59,9 +59,10 @@ def main():
                          'rainbow = C51 + noisy nets + dueling + double + PER + Adam')
     ap.add_argument('--fuse_acting', type=int, default=1,
                     help='run the device actors\' step inside the learner step\'s launches when possible')
-    ap.add_argument('--graph_steps', type=int, default=8,
+    ap.add_argument('--graph_steps', type=int, default=16,
                     help='SGD steps per HIP-graph launch (Learner.step_many: the same per-step work, one host '
-                         'launch per G steps -- the inter-graph gap is amortised); 1 = one graph per step')
+                         'launch per G steps -- the inter-graph gap is amortised); 1 = one graph per step '
+                         '(profiles/r4_graph_steps.txt: 16 / 32 measured 0.5-1%% above 8)')
     args = ap.parse_args()
 
     import shlex

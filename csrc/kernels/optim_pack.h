@@ -266,10 +266,10 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     if (m < 0 || threadIdx.x != 0) return;
     const int32_t* dc = wg->done + kTicketStride * m;
     const int want = wg->nblk[m];
-    int spins = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 23)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s: flag, do not hang
         ticket[kErrFlag] = 1;
         break;
       }
@@ -740,15 +740,17 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     const int j = threadIdx.x;
     const int want = ((int)gridDim.x - j + kTicketSubs - 1) / kTicketSubs - (j == 0 ? 1 : 0);
     int32_t* c = cnt + kTicketStride * j;
-    int spins = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
       __builtin_amdgcn_s_sleep(4);
-      if (++spins > (1 << 22)) {                          // >> any launch: flag, do not hang
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s (>> any launch): flag, do not hang
         ticket[kErrFlag] = 1;
         break;
       }
     }
-    __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // consume exactly this launch's arrivals (not a reset to 0): after a timeout the late arrivals
+    // cancel the deficit instead of counting toward -- and closing early -- the next launch
+    __hip_atomic_fetch_add(c, -want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   OPT_MARK(3);

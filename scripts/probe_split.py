@@ -64,8 +64,10 @@ def main():
             int(opt.layout.reg_end), 1.0, net.global_step, hps)
     p, pt = ex.packed(net.online.flat), ex.packed(net.target.flat)
     fca = [int(fc[0]), int(fc[1]), int(fc[2]), ex.FLAT, ex.HH]
-    spec = rep.next_sample_spec(32)
-    smp = list(spec['spec']) + [int(spec['B'])] if spec['kind'] == 'uniform' else []
+    smp = []                              # (prioritized: the sampler block runs the PER step instead)
+    if not cfg.prioritized_replay:
+        spec = rep.next_sample_spec(32)
+        smp = list(spec['spec']) + [int(spec['B'])] if spec['kind'] == 'uniform' else []
     op = kernel_op(opt)
 
     def launch(jobs, fcx, wgp=0, nb=0, sample=(), nj=None):

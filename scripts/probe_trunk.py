@@ -21,12 +21,12 @@ for B, ninst in ((4, 1), (32, 2), (32, 3), (256, 1)):
     sl = torch.randint(0, 1000, (B, 4), dtype=torch.int32, device=dev)
     ex.trunk_prof = torch.zeros(ninst * B * 16, dtype=torch.int64, device=dev)
     for _ in range(20):
-        ex._fwd_trunk([sl] * ninst, [p] * ninst, [f] * ninst, ws, B, ninst, frames=frames)
+        ex._fwd_trunk([sl] * ninst, [p] * ninst, [f] * ninst, ws, B, ninst, frames=frames, fc=False)
     torch.cuda.synchronize()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     st.record()
     for _ in range(50):
-        ex._fwd_trunk([sl] * ninst, [p] * ninst, [f] * ninst, ws, B, ninst, frames=frames)
+        ex._fwd_trunk([sl] * ninst, [p] * ninst, [f] * ninst, ws, B, ninst, frames=frames, fc=False)
     en.record()
     torch.cuda.synchronize()
     t = ex.trunk_prof.view(-1, 16)[:, [0, 1, 2, 6, 8, 9, 10]].double()
@@ -43,7 +43,7 @@ for B, ninst in ((4, 1), (32, 2), (32, 3), (256, 1)):
         span = max(span, float((tx[:, -1] - tx[:, 0].min()).max()))
         skew.append(tx[:, 0] - tx[:, 0].min())
     s0 = torch.cat(skew)
-    print('B=%d ninst=%d  trunk+fc %.2f us/call | block cycles %.0f: %s | span %.0f, start offsets p50 %.0f max %.0f'
+    print('B=%d ninst=%d  trunk %.2f us/call | block cycles %.0f: %s | span %.0f, start offsets p50 %.0f max %.0f'
           % (B, ninst, st.elapsed_time(en) * 1e3 / 50, sum(d), ' '.join('%s %.0f' % kv for kv in zip(names, d)),
              span, float(s0.median()), float(s0.max())))
 ex.trunk_prof = None
