@@ -20,7 +20,6 @@ kernels of csrc/kernels/cnn.hip (`HipCnnExecutor`). `simple` uses torch.
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -397,7 +396,8 @@ class HipExecutor:
         final at launch start; one block each), then every other job grouped by the member tile
         range that completes its gradient -- (member, 64-row K-range) for weight tiles, the
         member's K-range-0 tiles for its bias; each such job's block (after every tile in the grid)
-        waits for its range's count (UpdJob.dep = member * WG_SLOTS + slot)."""
+        waits for its range's count (UpdJob.dep = member * WG_SLOTS + slot). Noisy nets put those
+        jobs first, before the fc jobs."""
         members, dims, scales = wg
         key = (tuple(tuple(m) for m in members), tuple(tuple(d) for d in dims), tuple(scales), grad.data_ptr(),
                self.wg_conv_chunks, dev)
@@ -430,12 +430,18 @@ class HipExecutor:
                 else:
                     slot = ext.WG_SLOTS - 1
                 groups.setdefault((mi, slot), []).append(list(it))
-            table, deps = list(fcj), []
+            # range-dependent jobs right after the tiles (their waits end when the tiles do) or at the
+            # end of the grid: first measured +1.2% for noisy nets, whose fc jobs run ~10 us each and
+            # kept them queued to ~45 us; -0.2..-1.0% for the plain nets (profiles/r4_dep_first_ab.txt)
+            dep_first = self.noisy
+            table, deps = ([] if dep_first else list(fcj)), []
             for (mi, slot), its in sorted(groups.items()):
                 deps.append([mi, slot, len(table), len(its)])
                 for it in its:                 # the job's block waits for that range's tiles
                     it[21] = mi * ext.WG_SLOTS + slot
                 table += its
+            if dep_first:
+                table += fcj
             host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
             jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
             pl = (host.to(dev), int(total), jobs, len(fcj), done)
@@ -530,14 +536,15 @@ class HipExecutor:
         M rows split into 128-row chunks, ``mloop`` consecutive chunks per chunk group summed in
         registers in a fixed order, each group's [K][N] weights + [N] bias stored plainly into
         its own partial slice; the optimizer's conv jobs then sum the slices in ascending order.
-        Same result on every run (and every rank) for the same inputs. ``DQN_DET_GROUPS`` caps
-        the partial slices per layer (fewer: fewer bytes summed, longer wgrad blocks)."""
+        Same result on every run (and every rank) for the same inputs. At most 26 partial slices
+        per layer (the round-3 sweep's best: fewer slices sum fewer bytes but lengthen the wgrad
+        blocks, profiles/r3_det_wgrad.md)."""
         key = (B, dev.index if dev.index is not None else 0)
         pl = self._det.get(key)
         if pl is not None:
             return pl
         lay = self.layout
-        cap = max(1, int(os.environ.get('DQN_DET_GROUPS', '26')))
+        cap = 26
         info, base = {}, 0
         for c in self.arch.convs:
             h, w = c.conv_hw
@@ -1279,7 +1286,7 @@ class HipExecutor:
                 seg = ([x3, ws['dh'].data_ptr()], [lw['x'].data_ptr(), lw['dh'].data_ptr()],
                        [B * F * self.esz, B * HH * self.esz])
                 ga = None
-                if lowrank.get('gather_args') is not None and os.environ.get('DQN_LR_FUSED_GATHER', '1') == '1':
+                if lowrank.get('gather_args') is not None:
                     dev_args, nblk = lowrank['gather_args'](*seg)      # (cached by the transport)
                     ga = (dev_args.data_ptr(), nblk)
                     self._fc_dgrad(ws, B, po, zero, draw_noise, dh_done=True, gather=ga)

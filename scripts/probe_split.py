@@ -30,6 +30,9 @@ def main():
     iters = 200
     if args[:1] == ['--iters']:
         iters, args = int(args[1]), args[2:]
+    real_only = args[:1] == ['--real-only']     # only the learner's own launch (e.g. Rainbow's noisy / PER args)
+    if real_only:
+        args = args[1:]
     dev = torch.device('cuda', 0)
     cfg = preset('nature', 'Pong-v0', '--seed=0 --dtype=bf16 --replay_memory_capacity=65536 ' + ' '.join(args))
     net = Network.create_network(cfg, (84, 84, 4), 6, device=dev)
@@ -88,6 +91,13 @@ def main():
         return round(a.elapsed_time(b) * 1000.0 / iters, 2)
 
     out = {'wg_blocks': nwg, 'fc_jobs': nfc, 'jobs': jobs.numel() // nint}
+    if os.environ.get('DQN_OPT_PROF'):
+        # the learner's own update launch (its real noise / PER / target-mix arguments), eager step
+        for _ in range(3):
+            out['timeline_real_us'] = timeline(ex, plan, nwg, jobs, nfc, nint, learner.step)
+    if real_only:
+        print(json.dumps(out))
+        return
     out['wgrad_group'] = timeit(lambda: ex.ext.qnet_wgrad_group(members, dims, scales))
     out['F'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg, sample=smp))
     out['F_nosampler'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg))
