@@ -245,11 +245,18 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   const int nwork = (int)gridDim.x - (extra ? 1 : 0) - wg0;
   const int wid = (int)blockIdx.x - (extra ? 1 : 0) - wg0;      // work index of an update block
   float lr_t = h.lr;
+  // the step words, read once at launch start: block 0's closing step writes their successors from
+  // these registers (a load -> store round trip there sat on the launch's critical path); nothing
+  // else writes them during the launch
+  float b1p = 1.f, b2p = 1.f;
   if constexpr (OP == 3) {
-    const float b1p = beta_pow[0], b2p = beta_pow[1];
+    b1p = beta_pow[0];
+    b2p = beta_pow[1];
     lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   }
-  const bool sync = UPD && tgt != nullptr && step != nullptr && ((step[0] + 1) % tfreq) == 0;
+  const int64_t step_now = UPD && step != nullptr ? step[0] : 0;
+  const int64_t rng_now = UPD && noise_rng != nullptr ? noise_rng[1] : 0;   // (FEW: any block may close)
+  const bool sync = UPD && tgt != nullptr && step != nullptr && ((step_now + 1) % tfreq) == 0;
   const bool psync = sync && tgt_packed != nullptr;
   constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7;   // second slot written
   const bool wtwo = OP != 7 || ticket[kSlotFlag] != 0;                         // (momentum-0 RMSProp: flagged)
@@ -762,12 +769,12 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   }
 #endif
   if (threadIdx.x == 0) {
-    if (step) step[0] += 1;
+    if (step) step[0] = step_now + 1;
     if constexpr (OP == 3) {
-      beta_pow[0] *= h.b1;
-      beta_pow[1] *= h.b2;
+      beta_pow[0] = b1p * h.b1;
+      beta_pow[1] = b2p * h.b2;
     }
-    if (noise_rng != nullptr) noise_rng[1] += 1;        // (the drawing launch completed before this one)
+    if (noise_rng != nullptr) noise_rng[1] = rng_now + 1;   // (the drawing launch completed before this one)
   }
   // every other block consumed gnoise before its arrival add: block 0 may overwrite it now --
   // float4 pieces, every load of a round issued before its stores (a load -> store chain per
