@@ -1062,7 +1062,7 @@ __global__ void __launch_bounds__(256) dgrad_chain_kernel(ChainArgs c) {
   int32_t* err = c1 + c.B * kChainStride;
   if (b < c.n0) {
     const int bx = b % c.gx0, by = b / c.gx0;
-    igemm_body<DenseLoader, 1, 2, 1, 2, 2, 2, 8, true>(c.a[0], bx, by, 0, c.gx0, c.gy0, 1);
+    igemm_body<DenseLoader, 1, 1, 1, 1, 4, 2, DQN_ACT_F32 ? 2 : 4, true>(c.a[0], bx, by, 0, c.gx0, c.gy0, 1);
     chain_arrive(c0 + bx * kChainStride, 1);
     return;
   }
@@ -1124,7 +1124,10 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 8, 0, 13); return 0;
     case L_DENSE_FWD_F32: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 1, 13); return 0;
     // ---- backward data, ReLU mask of the layer input
-    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 2, 2, 2, 8); return 0;   // K 512-1024
+    // K 512-1024: 16 x 16 blocks, split-K 4 (2x the blocks of 16 x 32 split-K 2; A/B interleaved on one
+    // box: flagship +0.2-0.3%, dd +0.7-2.0%, Rainbow +0.7-1.1%, profiles/r4_fc_dgrad_tiles_ab.txt). The
+    // dgrad chain's fc stage uses the same tiling (bit-identical to this launch).
+    case L_DENSE_DGRAD: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 4, 2, 4); return 0;
     case L_NAT_CONV3_DGRAD: IGEMM_LAUNCH_U(NatD3, 1, 2, 1, 2, 2, 2, 9); return 0;     // 18 k-steps, 16 x 64 blocks
     case L_NAT_CONV2_DGRAD:
       // parity-class dgrad (8 k-steps of real taps instead of 32 with 3/4 zeros); the generic
@@ -1158,7 +1161,7 @@ int launch_dgrad_chain(const ConvArgs& a0, const ConvArgs& a1, const ConvArgs& a
   ChainArgs c{};
   c.a[0] = a0; c.a[1] = a1; c.a[2] = a2;
   c.gx0 = (B + 15) / 16;
-  c.gy0 = a0.N / 64;
+  c.gy0 = a0.N / 16;
   c.n0 = c.gx0 * c.gy0;
   c.n1 = (a1.M + 15) / 16;
   c.rows1 = a1.M / B;
