@@ -1121,7 +1121,12 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     case L_NAT_CONV3_FWD: IGEMM_LAUNCH(NatC3, 1, 4, 2, 1, 2, 0); return 0;       // K 576: split-K 2
     // K 3136 = 98 k-steps, split-K 8: one 13-step load batch per wave; 16-row blocks so the
     // B=32 step spreads over 2x the CUs (each block's L2->CU bytes are the bound, not MFMA)
-    case L_DENSE_FWD_RELU: IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 8, 0, 13); return 0;
+    case L_DENSE_FWD_RELU:
+      // 32-row blocks once 16-row blocks would exceed one per CU (Rainbow's 2 x 64 x 3 = 384:
+      // +0.5-1.3%, profiles/r4_fc_fwd_tiles_ab.txt; at <= 256 blocks, e.g. the unfolded flagship's
+      // 192, the 16-row blocks measured 4% faster in round 3)
+      if (((a.M + 15) / 16) * ((a.N + 15) / 16) * ninst > 256) { IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 0, 13); return 0; }
+      IGEMM_LAUNCH_U(DenseLoader, 1, 1, 1, 1, 8, 0, 13); return 0;
     case L_DENSE_FWD_F32: IGEMM_LAUNCH_U(DenseLoader, 2, 1, 1, 1, 8, 1, 13); return 0;
     // ---- backward data, ReLU mask of the layer input
     // K 512-1024: 16 x 16 blocks, split-K 4 (2x the blocks of 16 x 32 split-K 2; A/B interleaved on one
