@@ -39,6 +39,40 @@ VARIANTS = {
 }
 
 
+def relaunch(n: int) -> int:
+    """Run this benchmark as ``n`` ranks (one per GPU) under torch.distributed.run and return the
+    worst rank's exit code; rank 0's JSON line reaches stdout unchanged. Refuses loudly when the
+    node has fewer than ``n`` GPUs, unless DQN_DIST_BACKEND=gloo asks for a one-GPU rehearsal
+    (ranks sharing a device, process group over gloo, data over the in-graph xgmi kernels)."""
+    import socket
+    import subprocess
+    shared_ok = os.environ.get('DQN_DIST_BACKEND') == 'gloo'
+    ndev = torch.cuda.device_count()
+    if ndev < n and not shared_ok:
+        print('bench: --gpus %d needs %d GPUs, this node has %d (one rank per GPU; DQN_DIST_BACKEND=gloo '
+              'rehearses several ranks on one GPU)' % (n, n, ndev), file=sys.stderr, flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % n,
+           '--master-addr=127.0.0.1', '--master-port=%d' % port, os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def timed_split(steps: int, g_max: int):
+    """(G, graph launches, single steps) for the timed region: G = the largest step count per graph
+    launch in [4, g_max] that divides ``steps`` (no single-step graphs mixed into the timing), else
+    g_max with the remainder as single steps (reported)."""
+    if g_max <= 1:
+        return 1, 0, steps
+    for g in range(g_max, 3, -1):
+        if steps % g == 0:
+            return g, steps // g, 0
+    return g_max, steps // g_max, steps % g_max
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -64,12 +98,23 @@ def main():
                          'launch per G steps -- the inter-graph gap is amortised); 1 = one graph per step '
                          '(profiles/r4_graph_steps.txt: 16 / 32 measured 0.5-1%% above 8)')
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
+    # --gpus N > 1 started without a launcher: relaunch N ranks under torch.distributed.run as a
+    # CHILD process, before anything touches the GPU (device_count() does not initialise it here)
+    if 'RANK' not in os.environ and args.gpus > 1:
+        return relaunch(args.gpus)
+    world_env = int(os.environ.get('WORLD_SIZE', '1'))
+    if world_env != args.gpus:
+        print('bench: --gpus %d but the launcher started %d rank(s); pass --gpus equal to --nproc-per-node'
+              % (args.gpus, world_env), file=sys.stderr, flush=True)
+        return 2
 
-    import shlex
     from dist_dqn_amd.config import preset
     from dist_dqn_amd.learner import Learner
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.parallel import broadcast_state, check_state_equal, init_distributed
+    from dist_dqn_amd.parallel.dist import device_id
     from dist_dqn_amd.replay import DeviceReplay
 
     cfg = preset('nature' if args.network == 'nature' else 'atari', 'Pong-v0',
@@ -81,6 +126,10 @@ def main():
     ctx = init_distributed(cfg, device='cuda')
     dev = ctx.device
     assert dev.type == 'cuda', 'bench.py needs a GPU'
+    if ctx.enabled and ctx.ranks_share_gpu() and ctx.backend != 'gloo':
+        print('bench: ranks share a GPU (%s); one rank per GPU is required (DQN_DIST_BACKEND=gloo for a '
+              'one-GPU rehearsal)' % ctx.device_ids(), file=sys.stderr, flush=True)
+        return 2
     net = Network.create_network(cfg, (84, 84, 4), args.actions, num_replicas=ctx.world_size, device=dev)
     net.target.copy_from(net.online)
     net.refresh_packed()
@@ -105,7 +154,8 @@ def main():
     # G steps per graph launch (Learner.step_many) when the whole step is one in-graph body (fused or
     # no acting; one process, or DP with in-graph xgmi collectives). Whether G > 1 pays is decided
     # by a start-up probe (below), identically on every rank.
-    G_max = max(1, args.graph_steps) if (actor is None or fused) and args.graph else 1
+    # G_max divides --steps when it can (timed_split), so the timed region is G-step launches only
+    G_max = timed_split(args.steps, max(1, args.graph_steps))[0] if (actor is None or fused) and args.graph else 1
 
     def run(n, G):
         if G > 1:
@@ -138,14 +188,22 @@ def main():
     if G_max > 1 and not learner.can_step_many():
         G_max = 1
     if G_max > 1:
+        failed = 0
         try:
             learner.step_many(G_max)            # captures the G-step graph outside the timed region
         except RuntimeError as e:               # (capture refused): one graph per step instead
-            print('bench: %d-step graph unavailable (%s); one graph per step' % (G_max, e), file=sys.stderr,
+            print('bench: rank %d: %d-step graph unavailable (%s)' % (ctx.rank, G_max, e), file=sys.stderr,
                   flush=True)
             torch.cuda.synchronize(dev)
+            failed = 1
+        # every rank falls back together (DP: each step is a collective, so the ranks' step
+        # sequences must stay identical); a rank whose capture succeeded ran G steps, the others
+        # catch up with single steps
+        if ctx.ctrl_allreduce_max(failed):
+            for _ in range(G_max if failed else 0):
+                step()
             G_max = 1
-            step()                              # host step state restored by step_many: one clean step
+            print('bench: one graph per step (a G-step capture failed on some rank)', file=sys.stderr, flush=True)
     # probe (untimed, identical decision on every rank: MAX-reduced times): G = 1 vs G = G_max
     probe_steps = 4 * G_max if G_max > 1 else 16
     t_g1 = timed(lambda: run(probe_steps, 1))
@@ -154,6 +212,7 @@ def main():
         t_gm = timed(lambda: run(probe_steps, G_max))
         G = G_max if t_gm < t_g1 else 1
     ms_g1 = 1000.0 * t_g1 / probe_steps
+    G, n_launch, n_single = timed_split(args.steps, G)
     ctx.barrier()
     torch.cuda.synchronize(dev)
     frames0 = actor.env_frames if actor is not None else 0
@@ -177,6 +236,7 @@ def main():
     # (outside the timed region) every replica tensor must still be bit-identical to rank 0's
     eq = check_state_equal(ctx, net)
     replicas_equal = all(eq.values())
+    dev_ids = ctx.device_ids() if ctx.enabled else [device_id(dev)]
     if ctx.rank == 0:
         sps = args.steps * ctx.world_size / el
         out = {
@@ -192,6 +252,7 @@ def main():
                        'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
                        'frames_per_state': 4, 'optimizer': cfg.optimizer + '(tf)', 'executor': net.executor.name,
                        'hip_graph': bool(args.graph), 'steps_per_graph_launch': G,
+                       'timed_launches': {'graph_launches_of_G': n_launch, 'single_step_graphs': n_single},
                        'graph_steps_probe': {'candidates': sorted({1, G_max}), 'probe_steps': probe_steps,
                                              'ms_per_step_g1': round(ms_g1, 4)},
                        'actor_envs': args.actor_envs,
@@ -201,6 +262,8 @@ def main():
                        'final_loss': loss,
                        'allreduce': learner.reducer.mode if ctx.enabled else None,
                        'allreduce_probe_us': learner.reducer.timings or None,
+                       'xgmi_vs_rccl_max_rel': (learner.reducer.timings or {}).get('xgmi_vs_rccl_max_rel'),
+                       'rank_devices': dev_ids, 'ranks_share_gpu': len(set(dev_ids)) < len(dev_ids),
                        'lowrank_dense': learner._lowrank is not None,
                        'allreduce_ranges': learner._ar_ranges or None,
                        'allreduce_peer_timeouts': not xgmi_ok,
@@ -220,8 +283,9 @@ def main():
     if not replicas_equal or not xgmi_ok:
         print('bench: replicas diverged (%s) or an xgmi peer wait timed out (%s)'
               % (sorted(k for k, v in eq.items() if not v), not xgmi_ok), file=sys.stderr, flush=True)
-        sys.exit(3)
+        return 3
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

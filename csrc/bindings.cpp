@@ -293,8 +293,9 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   TORCH_CHECK(ticket.numel() >= 2, "optim_pack: ticket[1] is the slot flag word");
   if (wg != 0) {
     TORCH_CHECK(wg_blocks >= 1 && wg_blocks <= 16384 && !fc.empty() && op >= 0 && part == 0 && (wg % 16) == 0 &&
-                    wg_jobs >= 1 && wg_jobs <= jobs.numel() / upd_job_ints(),
-                "optim_pack wg: needs fc rows and an update, no partials; 1 <= wg_jobs <= jobs");
+                    wg_jobs >= 0 && wg_jobs <= jobs.numel() / upd_job_ints(),
+                "optim_pack wg: needs fc rows and an update, no partials; 0 <= wg_jobs <= jobs (the leading fc "
+                "jobs interleaved with the tiles; 0 = tiles first)");
   }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];

@@ -147,6 +147,10 @@ struct FoldArgs {
   int32_t* dq_epoch;
   float* zero_ptr;           // side duty: block 0 zeroes [zero_ptr, +zero_n) (the step's dgrad-chain
   int zero_n;                // counters; 16-byte aligned, zero_n % 4 == 0)
+  // spin mode: a dH-tile block whose dQ wait expires (1 s) stores 0x1000000 | group here and skips
+  // its dH write instead of using stale dQ (read by Learner._device_checks). dq_epoch[ngroups + 1].
+  int32_t* err;
+  int dbg_no_publish;        // test hook (DQN_DEBUG_FOLD_NO_PUBLISH): the tails never publish dQ
 };
 
 // The Nature dgrad chain in ONE launch (qnet.hip dgrad_chain_kernel): block ranges run

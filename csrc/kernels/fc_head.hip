@@ -45,6 +45,7 @@ struct FoldLds {
   float dq[16][33];                            // tail: dQ rows (| dV at A)
   int32_t pst[16][4];                          // actor tail: the envs' frame stacks
   int flag;
+  int timed_out;                               // dH-tile block: the dQ wait expired
 };
 
 template <int AT>
@@ -234,12 +235,19 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     //  cached weights; the dQ rows are read with agent-scope loads, coherent like the stores)
     if (tid == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      S.timed_out = 0;
       while (__hip_atomic_load(f.dq_epoch + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e0) {
         __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;    // 1 s: never hang
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {      // 1 s: never hang, never
+          S.timed_out = 1;                                                 // train on stale dQ
+          if (f.err != nullptr)
+            __hip_atomic_store(f.err, 0x1000000 | (int)blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
       }
     }
     __syncthreads();
+    if (S.timed_out) return;             // flagged: the learner's device check raises
     const int nr = min(16, a.M - m_base);
     for (int t = tid; t < 16 * A1; t += kFoldThreads) {
       const int r = t / A1, c = t - r * A1;
@@ -372,7 +380,7 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
   }
   FOLD_MARK(5);
   __syncthreads();
-  if (f.spin) {
+  if (f.spin && !f.dbg_no_publish) {
     // publish the group's dQ rows (write-through), then its epoch: the online blocks waiting on it
     // write their dH tiles (this block too, when it is one of them)
     const int g = (int)blockIdx.x;

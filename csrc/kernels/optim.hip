@@ -171,7 +171,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   // WG: the launch also computes the grouped weight gradients (tiles after the lead block)
   const bool wgm = wg != nullptr && ff.x != nullptr && op >= 0;
   if (wg != nullptr && !wgm) return;      // (binding checks: a WG launch needs FcFuse rows and an update)
-  (void)wg_jobs;                          // (WG: fc jobs first, then one block per job waiting on a range)
+  // wg_jobs > 0 (WG): the table's first wg_jobs jobs (the fc jobs) interleave with the tiles
   // + the lead block (sampler / closer) + the weight-gradient tiles
   L.grid = (njobs < cap ? njobs : cap) + (L.smp.size != nullptr || L.per.sum != nullptr || wgm ? 1 : 0) +
            (wgm ? wg_blocks : 0);
@@ -193,6 +193,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   L.noise = noise; L.eff = eff; L.gnoise = gnoise; L.noise_dst = noise_dst; L.noise_n = noise_n;
   L.tnoise = tnoise; L.teff = teff; L.tpk = reinterpret_cast<act_t*>(tpk); L.noise_rng = noise_rng; L.ff = ff;
   L.part = part; L.wg = reinterpret_cast<const WgradGroup*>(wg); L.wg_blocks = wgm ? wg_blocks : 0;
+  L.wg_mix = wgm && wg_jobs > 0 && wg_jobs <= njobs ? wg_jobs : 0;
   switch (op) {
     case -1: optim_pack_op<-1>(L); break;
     case 0: optim_pack_op<0>(L); break;

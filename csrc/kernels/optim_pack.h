@@ -205,7 +205,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
                   int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
                   float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff,
-                  const float* __restrict__ part, const WgradGroup* __restrict__ wg, int wg_blocks) {
+                  const float* __restrict__ part, const WgradGroup* __restrict__ wg, int wg_blocks, int wg_mix) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
@@ -243,7 +243,26 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
   const bool sampler = smp_on && blockIdx.x == 0;
   const int nwork = (int)gridDim.x - (extra ? 1 : 0) - wg0;
-  const int wid = (int)blockIdx.x - (extra ? 1 : 0) - wg0;      // work index of an update block
+  // block roles after the lead block. WG: the weight-gradient tiles [0, wg_blocks) and the job table
+  // (wg_mix > 0: its first wg_mix jobs -- the fc jobs, independent of the tiles -- interleaved with
+  // the tiles over the first wg_blocks + wg_mix positions, Bresenham-spaced: the latency-bound tiles
+  // and the bandwidth-bound fc jobs share the CUs from the launch start instead of the tiles holding
+  // most slots for their whole span; the range-dependent jobs stay after every tile)
+  int wgb = -1;                                               // this block's tile (WG), else -1
+  int wid = (int)blockIdx.x - (extra ? 1 : 0) - wg0;          // work index of an update block
+  if constexpr (WG) {
+    const int p = (int)blockIdx.x - 1;
+    const int S = wg_blocks + wg_mix;
+    if (p >= 0 && wg_mix > 0 && p < S) {
+      const int q = p * wg_blocks / S, q1 = (p + 1) * wg_blocks / S;
+      if (q1 > q) { wgb = q; wid = -1; } else { wid = p - q; }
+    } else if (p >= 0 && p < wg_blocks) {
+      wgb = p;
+      wid = -1;
+    } else {
+      wid = p - wg_blocks;
+    }
+  }
   float lr_t = h.lr;
   // the step words, read once at launch start: block 0's closing step writes their successors from
   // these registers (a load -> store round trip there sat on the launch's critical path); nothing
@@ -654,7 +673,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   };
 #if !DQN_ACT_F32
   if constexpr (WG) {
-    const int b = (int)blockIdx.x - 1;
+    const int b = wgb;
     if (b >= 0 && b < wg_blocks) {
       // ---- a weight-gradient tile, counted on its (member, K-range) when done (the last tile of a
       //      range ran that range's jobs serially: ~4 of them, 8-15 us each, measured; the jobs
@@ -810,7 +829,7 @@ struct OptPackLaunch {
   const UpdJob* jobs; int njobs; act_t* packed; float* tgt; act_t* tgt_packed; int tfreq;
   const float* noise; float* eff; const float* gnoise; float* noise_dst; int noise_n;
   TrunkSample smp; PerStep per; const float* tnoise; float* teff; act_t* tpk; int64_t* noise_rng; FcFuse ff;
-  const float* part; const WgradGroup* wg; int wg_blocks;
+  const float* part; const WgradGroup* wg; int wg_blocks; int wg_mix;
 };
 
 template <int N>
@@ -822,7 +841,8 @@ void optim_pack_op(const OptPackLaunch& L) {
 #define OPM(M) hipLaunchKernelGGL((optim_pack_kernel<N, M>), dim3(L.grid), dim3(kPackThreads), L.dyn, L.st, L.w, L.g, \
                                   L.s0, L.s1, L.beta_pow, L.step, L.ticket, L.h, L.jobs, L.njobs, L.packed, L.tgt, \
                                   L.tgt_packed, L.tfreq, L.noise, L.eff, L.gnoise, L.noise_dst, L.noise_n, L.smp, L.per, \
-                                  L.tnoise, L.teff, L.tpk, L.noise_rng, L.ff, L.part, L.wg, L.wg_blocks)
+                                  L.tnoise, L.teff, L.tpk, L.noise_rng, L.ff, L.part, L.wg, L.wg_blocks, \
+                                  L.wg_mix)
   if constexpr (N < 0) {
     OPM(kModeNoisy);                                    // mix + pack only (noisy nets)
   } else {

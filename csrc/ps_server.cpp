@@ -68,6 +68,18 @@ class PsServer {
 
   void request_stop() { stop_.store(true, std::memory_order_relaxed); }
 
+  // Quiesce for a consistent host-side read of the PS state (a checkpoint snapshot): the thread
+  // stops launching at the top of its loop, drains the PS stream and acknowledges; pushes that
+  // arrive meanwhile stay in their push words and are answered after resume(). Returns once
+  // paused (or once the thread has exited). Called with the GIL released.
+  void pause() {
+    pause_req_.store(true, std::memory_order_release);
+    while (running_ && !done_.load() && !paused_.load(std::memory_order_acquire))
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  void resume() { pause_req_.store(false, std::memory_order_release); }
+  int64_t pauses() const { return pauses_.load(); }
+
   // join (GIL released by the binding); returns the number of applied pushes
   int64_t wait() {
     if (running_) {
@@ -101,6 +113,14 @@ class PsServer {
       int nactive = nw_;
       const auto t0 = std::chrono::steady_clock::now();
       while (nactive > 0 && !(max_updates_ > 0 && updates_.load() >= max_updates_)) {
+        if (pause_req_.load(std::memory_order_acquire)) {
+          HIPCK(hipStreamSynchronize(stream_));            // every launched update has landed
+          paused_.store(true, std::memory_order_release);
+          pauses_.fetch_add(1);
+          while (pause_req_.load(std::memory_order_acquire))
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+          paused_.store(false, std::memory_order_release);
+        }
         bool got = false;
         for (int w = 1; w <= nw_; ++w) {
           if (!active[w]) continue;
@@ -147,7 +167,8 @@ class PsServer {
   int stopped_workers_ = 0;
   double busy_s_ = 0.0;
   std::atomic<int64_t> updates_{0};
-  std::atomic<bool> stop_{false}, done_{false};
+  std::atomic<bool> stop_{false}, done_{false}, pause_req_{false}, paused_{false};
+  std::atomic<int64_t> pauses_{0};
   bool running_ = false;
   std::thread th_;
   std::string err_;
@@ -161,6 +182,9 @@ void register_ps_server(pybind11::module_& m) {
       .def("set_graphs", &PsServer::set_graphs)
       .def("start", &PsServer::start)
       .def("request_stop", &PsServer::request_stop)
+      .def("pause", &PsServer::pause, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("resume", &PsServer::resume)
+      .def("pauses", &PsServer::pauses)
       .def("wait", &PsServer::wait, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("updates", &PsServer::updates)
       .def("running", &PsServer::running)

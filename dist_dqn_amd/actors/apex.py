@@ -738,7 +738,13 @@ class ApexTrainer:
                     # together, once every rank's replay shard holds `start` transitions (one
                     # control-plane max per pre-start iteration: the ranks' collective sequences
                     # stay matched, and no in-graph xgmi wait spins on a peer still filling)
-                    started = ready = ctx.ctrl_allreduce_max(0 if ready else 1) == 0
+                    # (a stop asked for before the first step -- signal, time budget, dead actors --
+                    # rides in the same max: 2 = some rank wants to stop, every rank leaves together)
+                    v = ctx.ctrl_allreduce_max(2 if supervisor.stop_requested() else (0 if ready else 1))
+                    if v >= 2:
+                        log.info('apex: stop agreed before the first SGD step')
+                        break
+                    started = ready = v == 0
                 if ready:
                     if self.learn_t0 is None:
                         self.learn_t0, self.learn_frames0 = time.time(), self.pool.frames

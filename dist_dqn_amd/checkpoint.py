@@ -19,6 +19,7 @@ JSON sidecar with epsilon and training_steps.
 """
 from __future__ import annotations
 
+import contextlib
 import glob
 import json
 import os
@@ -133,6 +134,10 @@ class CheckpointManager:
         _MANAGERS.add(self)
         self._write_error: Optional[BaseException] = None
         self.last_path: Optional[str] = None
+        # optional context-manager factory held around the snapshot copies when another host
+        # thread updates the parameters on its own stream (the native async-PS server: its
+        # updates pause, so parameters, slots and global_step come from one update)
+        self.quiesce = None
 
     def restore(self) -> Optional[str]:
         path = latest_checkpoint(self.logdir)
@@ -170,7 +175,11 @@ class CheckpointManager:
         with self._lock:
             self._last = now
             self.wait()                  # one write in flight at a time
-            snap, ev = self.network.snapshot() if hasattr(self.network, 'snapshot') else (None, None)
+            quiesce = self.quiesce
+            with (quiesce() if quiesce is not None else contextlib.nullcontext()):
+                snap, ev = self.network.snapshot() if hasattr(self.network, 'snapshot') else (None, None)
+                if quiesce is not None and ev is not None:
+                    ev.synchronize()     # the copies land before the quiesced writer resumes
             if self._armed:
                 opt.request_slots(False)
                 self._armed = False

@@ -191,12 +191,19 @@ def _probe_graph_steps(ctx, learner, G_max: int) -> int:
         learner.step()
     if not learner.can_step_many():
         return 1
+    failed = 0
     try:
         learner.step_many(G_max)             # capture the G-step graph outside the timing
     except RuntimeError as e:
-        log.warning('%d-step graph unavailable (%s); one graph per step', G_max, e)
+        log.warning('rank %d: %d-step graph unavailable (%s)', ctx.rank, G_max, e)
         torch.cuda.synchronize(dev)
-        learner.step()
+        failed = 1
+    # agreed fallback: under DP every step is a collective, so all ranks drop to G = 1 together,
+    # and a rank whose capture failed makes up the G steps its peers just ran
+    if ctx.ctrl_allreduce_max(failed):
+        for _ in range(G_max if failed else 0):
+            learner.step()
+        log.warning('one graph per step (a %d-step capture failed on some rank)', G_max)
         return 1
 
     def timed(fn):

@@ -499,6 +499,11 @@ class Learner:
         t = getattr(self.net.optimizer, 'ticket', None)
         if t is not None and t.is_cuda and t.numel() > 2 and int(t[2].item()) != 0:
             raise RuntimeError('fused optimizer: an end-of-launch arrival wait gave up (step %d)' % self.train_steps)
+        fe = getattr(self.net.executor, 'fold_errors', None)
+        errs = fe() if fe is not None else []
+        if errs:
+            raise RuntimeError('folded head: a dH block\'s wait for its group\'s dQ expired (groups %s, step %d); '
+                               'its dH tile was not written' % ([e & 0xffff for e in errs], self.train_steps))
 
     def update_target_now(self, tau: float = 1.0):
         """Unconditional target sync (reference `_update_target_network` at init, `dqn_agent.py:50`)."""

@@ -20,6 +20,7 @@ kernels of csrc/kernels/cnn.hip (`HipCnnExecutor`). `simple` uses torch.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -444,7 +445,10 @@ class HipExecutor:
                 table += fcj
             host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
             jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
-            pl = (host.to(dev), int(total), jobs, len(fcj), done)
+            # fc jobs interleaved with the tiles (they lead the table unless dep_first); DQN_WG_MIX=0: the
+            # tiles first, as round 4
+            mix = 0 if dep_first or os.environ.get('DQN_WG_MIX', '1') == '0' else len(fcj)
+            pl = (host.to(dev), int(total), jobs, mix, done)
             self._wg_plans[key] = pl
         return pl
 
@@ -882,6 +886,18 @@ class HipExecutor:
                   'epoch': torch.zeros(mpad // 16 + 2, dtype=torch.int32, device=dev)}
             self._ws[key] = ws
         return ws
+
+    def fold_errors(self) -> list:
+        """Error words of the folded head launches (host sync): 0x1000000 | group for a dH-tile
+        block whose wait for its group's dQ expired (fc_head.hip; the block skipped its dH write).
+        The word is the epoch buffer's last entry (ngroups + 1) and is never cleared."""
+        out = []
+        for key, ws in self._ws.items():
+            if isinstance(key, tuple) and key and key[0] == 'fold':
+                v = int(ws['epoch'][ws['mpad'] // 16 + 1].item())
+                if v:
+                    out.append(v)
+        return out
 
     def _fc_head(self, packs, ws, B, nlearn, ints, w, b, wv, bv, io, actor, actor_f, act_h, dev):
         """fc forward of every instance (learners', then the fused actors') + the scalar head's

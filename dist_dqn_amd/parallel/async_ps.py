@@ -32,6 +32,7 @@ since that worker last saw it. Without the flag each worker keeps its own replic
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import time
 from typing import Dict, Optional
@@ -420,6 +421,17 @@ class XgmiPSServer:
             srv.set_graphs(w, ga.raw_cuda_graph_exec(), gs.raw_cuda_graph_exec())
         srv.start(int(max_updates), 1)
         last = 0
+        ck = getattr(supervisor, 'ckpt', None)
+
+        @contextlib.contextmanager
+        def paused():
+            srv.pause()                       # the server thread drains its stream and waits
+            try:
+                yield
+            finally:
+                srv.resume()
+        if ck is not None:
+            ck.quiesce = paused               # periodic saves read one update's consistent state
         try:
             while srv.running():
                 if supervisor is not None:
@@ -431,7 +443,10 @@ class XgmiPSServer:
                         srv.request_stop()
                 time.sleep(1e-3)
         finally:
+            if ck is not None:
+                ck.quiesce = None
             self.updates = srv.wait()
+        self.pauses = int(srv.pauses())
         _, per, stopped, busy = srv.stats()
         self.per_worker = {w: int(per[w]) for w in self.workers}
         self.stopped_workers = int(stopped)

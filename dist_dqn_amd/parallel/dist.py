@@ -55,6 +55,31 @@ class DistContext:
         dist.broadcast_object_list(box, src=src, group=self.ctrl_group)
         return box[0]
 
+    def ctrl_all_gather_object(self, obj) -> list:
+        """[rank 0's obj, rank 1's obj, ...] on every rank (control plane)."""
+        if not self.enabled:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.ctrl_group)
+        return out
+
+    def device_ids(self) -> list:
+        """Every rank's physical device id (`device_id`), gathered over the control plane (cached)."""
+        ids = self.__dict__.get('_device_ids')
+        if ids is None:
+            ids = self.ctrl_all_gather_object(device_id(self.device))
+            self.__dict__['_device_ids'] = ids
+        return ids
+
+    def ranks_share_gpu(self) -> bool:
+        """True when two or more ranks drive the same physical GPU (the one-GPU rehearsals). Decided
+        from the gathered PCI ids, so every rank computes the same answer whatever its visible device
+        set (``HIP_VISIBLE_DEVICES`` per rank gives device_count() == 1 on every rank of a real node)."""
+        if not self.enabled or self.device.type != 'cuda':
+            return False
+        ids = self.device_ids()
+        return len(set(ids)) < len(ids)
+
     @property
     def enabled(self) -> bool:
         return self.world_size > 1
@@ -65,6 +90,18 @@ class DistContext:
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
+
+
+def device_id(dev: torch.device) -> str:
+    """Physical identity of a device: 'pci:<domain>:<bus>:<device>' (plus the uuid when the
+    runtime reports one) for a GPU, 'cpu' otherwise."""
+    if dev.type != 'cuda':
+        return 'cpu'
+    p = torch.cuda.get_device_properties(dev)
+    pci = 'pci:%04x:%02x:%02x' % (getattr(p, 'pci_domain_id', 0), getattr(p, 'pci_bus_id', 0),
+                                  getattr(p, 'pci_device_id', 0))
+    uuid = str(getattr(p, 'uuid', '') or '')
+    return pci + ('/' + uuid if uuid else '')
 
 
 def _from_cluster_flags(config):
@@ -92,28 +129,54 @@ def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600) ->
     if device == 'auto':
         device = getattr(config, 'device', 'auto') if config is not None else 'auto'
     use_gpu = (device in ('auto', 'cuda')) and torch.cuda.is_available()
-    if use_gpu:
-        ndev = torch.cuda.device_count()
-        dev = torch.device('cuda', local_rank % max(ndev, 1))
-        torch.cuda.set_device(dev)
-    else:
-        dev = torch.device('cpu')
     backend = 'none'
     if world > 1:
         backend = 'nccl' if use_gpu else 'gloo'
         # DQN_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks on ONE
         # device (RCCL refuses two ranks per GPU; gloo stages CUDA tensors through the host)
         backend = os.environ.get('DQN_DIST_BACKEND', backend)
-        if not dist.is_initialized():
-            kw = dict(backend=backend, rank=rank, world_size=world,
-                      timeout=datetime.timedelta(seconds=timeout_s))
-            if use_gpu and backend == 'nccl':
-                kw['device_id'] = dev
-            dist.init_process_group(**kw)
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        if backend == 'nccl' and local_rank >= ndev:
+            # RCCL needs one GPU per rank: say so here instead of a "Duplicate GPU" abort later
+            raise RuntimeError('rank %d (local rank %d) has no GPU of its own: %d visible device(s) for %d ranks '
+                               'per node. Launch at most one rank per GPU, or set DQN_DIST_BACKEND=gloo to '
+                               'rehearse several ranks on one GPU.' % (rank, local_rank, ndev, world))
+        dev = torch.device('cuda', local_rank % max(ndev, 1))
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device('cpu')
+    if world > 1 and not dist.is_initialized():
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if use_gpu and backend == 'nccl':
+            kw['device_id'] = dev
+        dist.init_process_group(**kw)
     ctrl = None
     if world > 1 and backend != 'gloo':
         ctrl = dist.new_group(backend='gloo', timeout=datetime.timedelta(seconds=timeout_s))
-    return DistContext(rank, world, local_rank, dev, backend, ctrl)
+    ctx = DistContext(rank, world, local_rank, dev, backend, ctrl)
+    if world > 1:
+        first_contact(ctx)
+    return ctx
+
+
+def first_contact(ctx: DistContext):
+    """The first collective on the data backend: a 4-element SUM of rank-stamped values on the
+    rank's own device, checked exactly. It runs right after the process group forms and BEFORE any
+    xgmi / IPC setup, so a broken RCCL install, a duplicate device or a wrong topology fails
+    here with its own message instead of inside the transport probe or the first SGD step."""
+    W = ctx.world_size
+    t = torch.tensor([1.0, float(ctx.rank), float(ctx.rank * ctx.rank), 3.0], device=ctx.device)
+    try:
+        dist.all_reduce(t)
+        got = t.cpu().tolist()
+    except Exception as e:  # noqa: BLE001
+        raise RuntimeError('first %s collective failed on rank %d of %d (device %s, %s): %s'
+                           % (ctx.backend, ctx.rank, W, ctx.device, device_id(ctx.device), e)) from e
+    want = [float(W), W * (W - 1) / 2.0, (W - 1) * W * (2 * W - 1) / 6.0, 3.0 * W]
+    if got != want:
+        raise RuntimeError('first %s collective returned %s on rank %d, expected %s'
+                           % (ctx.backend, got, ctx.rank, want))
 
 
 def shutdown(ctx: Optional[DistContext] = None):

@@ -82,6 +82,9 @@ class XgmiAllReduce:
         self.ext = _ext.load(required=True)
         assert hasattr(self.ext, 'XGMI_MAX_BLOCKS'), 'extension built without the xGMI all-reduce'
         self.ctx = ctx
+        # several ranks on one physical GPU? Decided from the gathered PCI ids (one collective, the
+        # same answer on every rank), not from this rank's visible device count
+        self.shared_gpu = ctx.ranks_share_gpu()
         self.bf16 = wire_dtype == 'bf16'
         self.cap = (int(capacity) + 63) // 64 * 64
         esz = 2 if self.bf16 else 4
@@ -123,7 +126,7 @@ class XgmiAllReduce:
         ONE GPU (the rehearsals): 128 / W, so the W kernels fit together -- at W = 8 with 104 blocks
         per rank a rank's wait timed out after 10 s on a peer block that never ran (error word:
         all-gather phase, peer 2, block 192; round 4), i.e. starvation, not the protocol."""
-        if self.ctx.world_size <= max(1, torch.cuda.device_count()):
+        if not self.shared_gpu:
             return self.ext.XGMI_MAX_BLOCKS
         return max(8, 128 // self.ctx.world_size)
 

@@ -111,6 +111,35 @@ def test_checkpoint_roundtrip_tf_names(tmp_path):
     assert s1.keys() == s2.keys() and all(torch.equal(s1[k], s2[k]) for k in s1)
 
 
+def test_checkpoint_manager_snapshots_inside_quiesce(tmp_path):
+    """A manager with a quiesce hook (the native async-PS server's pause) takes its snapshot while
+    the hook is held, and the written checkpoint holds that state."""
+    cfg = _cfg(tmp_path, '--network=simple', '--optimizer=rmsprop')
+    net = Network.create_network(cfg, (4,), 2)
+    mgr = ckpt.CheckpointManager(str(tmp_path), net, save_secs=600, async_write=False)
+    events = []
+    orig = net.snapshot
+
+    def snap():
+        events.append('snapshot')
+        return orig()
+    net.snapshot = snap
+
+    import contextlib
+
+    @contextlib.contextmanager
+    def quiesce():
+        events.append('pause')
+        net.global_step.fill_(7)          # the paused writer's last update
+        yield
+        events.append('resume')
+        net.global_step.fill_(8)          # updates continue after the snapshot
+    mgr.quiesce = quiesce
+    path = mgr.maybe_save(force=True)
+    assert events == ['pause', 'snapshot', 'resume']
+    assert int(ckpt.load(path)['global_step']) == 7
+
+
 def test_checkpoint_retention(tmp_path):
     t = {'w': torch.zeros(2)}
     for s in range(6):

@@ -110,6 +110,20 @@ def test_apex_world2_actor_death_is_a_coordinated_stop(tmp_path):
         n.startswith('model.ckpt-%d' % s) for n in os.listdir(logdir)), os.listdir(logdir)
 
 
+@pytest.mark.timeout(300)
+def test_apex_world2_time_budget_ends_before_the_first_step(tmp_path):
+    """The replay never reaches replay_start_size (larger than its capacity), so no rank ever
+    takes a first step; --apex_seconds must still end BOTH ranks (the stop request rides in the
+    pre-start readiness reduction) instead of spinning forever."""
+    logdir = str(tmp_path)
+    args = _args(logdir, '--max_train_steps=1000000', '--apex_seconds=4')
+    args = [a for a in args if not a.startswith('--replay_start_size')] + ['--replay_start_size=10000000']
+    rcs = _launch(2, logdir, args, timeout=200)
+    assert rcs == [0, 0], (rcs, _log(logdir, 0), _log(logdir, 1))
+    done = [_records(logdir, r, 'done')[-1] for r in range(2)]
+    assert all(d['training_steps'] == 0 for d in done), done
+
+
 def _gpu_args(logdir, *extra):
     import shlex
     from dist_dqn_amd.config import dqn_params_for_env

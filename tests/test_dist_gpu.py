@@ -277,9 +277,50 @@ def test_bench_ranks_replicas_equal(tmp_path, world):
     line = [ln for ln in out.stdout.splitlines() if ln.startswith('{')][-1]
     d = json.loads(line)
     assert d['n_gpus'] == world and d['config']['world_size'] == world
-    assert d['graph_steps'] in (1, 16) and d['ms_per_step_g1'] > 0
+    assert d['graph_steps'] in (1, 10) and d['ms_per_step_g1'] > 0        # 10: the largest G <= 16 dividing 20
     assert d['config']['replicas_equal'] is True and d['config']['replicas_diverged'] == []
     assert d['config']['dist_backend'] == 'gloo'
+
+
+def test_bench_gpus_flag_launches_ranks_itself(tmp_path):
+    """`python bench.py --gpus 2` with NO launcher: bench.py relaunches itself under
+    torch.distributed.run as 2 ranks (here sharing cuda:0 over gloo), rank 0's line reports
+    n_gpus == 2, both ranks' device ids, bit-equal replicas and a timed region of G-step
+    launches only."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK')}
+    env.update(DQN_DIST_BACKEND='gloo', OMP_NUM_THREADS='4')
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '20', '--warmup', '5',
+           '--replay', '20000']
+    out = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=200)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, out.stdout                  # rank 0 only
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['config']['world_size'] == 2
+    assert d['config']['replicas_equal'] is True
+    assert len(d['config']['rank_devices']) == 2 and d['config']['ranks_share_gpu'] is True
+    tl = d['config']['timed_launches']
+    assert tl['graph_launches_of_G'] * d['graph_steps'] + tl['single_step_graphs'] == 20
+
+
+def test_bench_gpus_more_than_the_node_has_fails_loudly():
+    """`--gpus 8` on a one-GPU box (no gloo rehearsal asked for) must refuse with a message and a
+    non-zero exit, never run one rank and print n_gpus 1."""
+    import subprocess
+    import sys
+    if torch.cuda.device_count() >= 8:
+        pytest.skip('node has 8 GPUs')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'DQN_DIST_BACKEND')}
+    out = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '8', '--steps', '4'],
+                         env=env, cwd=root, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
+    assert 'needs 8 GPUs' in out.stderr
 
 
 def _worker_async_ps(rank, world, port, transport, errq):
@@ -352,6 +393,90 @@ def _worker_async_ps(rank, world, port, transport, errq):
 @pytest.mark.parametrize('transport', ['p2p', 'xgmi'])
 def test_async_ps_hip_learners_one_gpu(transport):
     _run_ranks(_worker_async_ps, (transport,), world=3, timeout=150)
+
+
+class _QuiesceProbeSupervisor:
+    """Stands in for the RunSupervisor on the PS rank: every new update count triggers a
+    'checkpoint' that reads the PS state inside the checkpoint manager's quiesce hook and checks
+    that nothing moves while it is held (parameters, every optimizer slot, global_step)."""
+
+    def __init__(self, net):
+        import types
+        self.net = net
+        self.reads = []
+        self.ckpt = types.SimpleNamespace(quiesce=None)
+
+    def on_train_step(self, u):
+        import time
+        q = self.ckpt.quiesce
+        assert q is not None, 'native serve did not install the quiesce hook'
+        if len(self.reads) >= 6:
+            return
+        with q():
+            net = self.net
+            g0 = int(net.global_step)
+            p0 = net.online.flat.clone()
+            s0 = [s.clone() for s in net.optimizer.slots]
+            torch.cuda.synchronize()
+            time.sleep(0.005)                        # workers keep pushing meanwhile
+            torch.cuda.synchronize()
+            moved = (int(net.global_step) != g0 or not torch.equal(p0, net.online.flat)
+                     or any(not torch.equal(a, b) for a, b in zip(s0, net.optimizer.slots)))
+            self.reads.append((g0, moved))
+
+    def should_stop(self):
+        return False
+
+
+def _worker_async_ps_quiesce(rank, world, port, errq):
+    """Native xgmi PS serve with periodic 'checkpoints': the server thread pauses (drains its stream)
+    around each snapshot, so a save reads ONE update's parameters, slots and global_step."""
+    try:
+        _setup(rank, world, port)
+        from dist_dqn_amd.config import preset
+        from dist_dqn_amd.learner import Learner
+        from dist_dqn_amd.models.network import Network
+        from dist_dqn_amd.parallel import broadcast_state, init_distributed
+        from dist_dqn_amd.parallel.async_ps import make_ps_client, make_ps_server
+        from dist_dqn_amd.replay import DeviceReplay
+        cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=5 --backend=hip --replay_memory_capacity=2048 '
+                     '--async_ps --ps_transport=xgmi')
+        ctx = init_distributed(cfg, device='cuda')
+        net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
+        broadcast_state(ctx, net)
+        steps = 40
+        if rank == 0:
+            srv = make_ps_server(ctx, net, cfg)
+            sup = _QuiesceProbeSupervisor(net)
+            n = srv.serve(supervisor=sup)
+            assert n == steps * (world - 1)
+            assert sup.reads and not any(m for _, m in sup.reads), sup.reads
+            assert srv.pauses >= len(sup.reads), (srv.pauses, len(sup.reads))
+            assert sup.ckpt.quiesce is None                     # removed when serving ends
+            dist.barrier()
+            srv.close()
+        else:
+            rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
+            rep.fill_synthetic(2048, 6, seed=rank)
+            ps = make_ps_client(ctx, net.online.flat, cfg)
+            ps.pull(net.online.flat, net.global_step)
+            net.refresh_packed()
+            ln = Learner(net, rep, cfg, ctx, ps_client=ps)
+            for _ in range(steps):
+                ln.step()
+            torch.cuda.synchronize()
+            assert ps.check()
+            ps.close()
+            dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 - report to the parent
+        import traceback
+        errq.put('rank %d: %s\n%s' % (rank, e, traceback.format_exc()))
+        raise
+
+
+def test_async_ps_native_serve_quiesces_for_checkpoints():
+    _run_ranks(_worker_async_ps_quiesce, (), world=3, timeout=150)
 
 
 def _worker_ps_stall(rank, world, port, errq):

@@ -319,6 +319,25 @@ def test_head_kernels_match_pure_torch_loss(extra, fold):
         assert torch.equal(ws['dh'][:B * ex.HH], dh_bits) and torch.equal(ws['dq16'][:B * width], dq_bits)
 
 
+def test_folded_head_dq_wait_timeout_raises(monkeypatch):
+    """Spin-mode fold with the tails' dQ publish switched off (DQN_DEBUG_FOLD_NO_PUBLISH, read at
+    launch): every waiting dH block gives up after 1 s, skips its dH write and sets the fold's
+    error word, and the learner's device check raises instead of training on stale dQ."""
+    net, learner = _learner('', True)
+    learner.step()                                   # a normal step: no error word
+    torch.cuda.synchronize()
+    learner._device_checks()
+    assert net.executor.fold_errors() == []
+    monkeypatch.setenv('DQN_DEBUG_FOLD_NO_PUBLISH', '1')
+    learner.step()
+    torch.cuda.synchronize()
+    monkeypatch.delenv('DQN_DEBUG_FOLD_NO_PUBLISH')
+    errs = net.executor.fold_errors()
+    assert errs and all(e >> 24 == 1 for e in errs), errs
+    with pytest.raises(RuntimeError, match='folded head'):
+        learner._device_checks()
+
+
 @pytest.mark.parametrize('extra,B', [('', 32), ('--double_dqn --loss=huber', 32), ('--dueling --double_dqn', 32),
                                      ('cnn:--dueling', 32), ('--dueling', 256)])
 def test_folded_head_gradient_matches_separate_head(extra, B):
