@@ -31,6 +31,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+VARIANT_DTYPE = {'rainbow': 'fp16'}
 METRIC = "learner SGD steps/sec + env frames/sec, Atari Nature-CNN DQN at 1/2/4/8 MI355X"
 VARIANTS = {
     'dqn': '',
@@ -80,7 +81,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--network', default='nature')
     ap.add_argument('--batch', type=int, default=32)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp16', 'fp32'])
+    ap.add_argument('--dtype', default=None, choices=['bf16', 'fp16', 'fp32'],
+                    help='compute dtype (default: the variant\'s BASELINE config -- bf16, Rainbow fp16)')
     ap.add_argument('--backend', default='auto', choices=['auto', 'hip', 'torch'])
     ap.add_argument('--replay', type=int, default=1000000, help='replay capacity (the Atari preset: 1M transitions)')
     ap.add_argument('--actions', type=int, default=6)
@@ -98,6 +100,8 @@ def main():
                          'launch per G steps -- the inter-graph gap is amortised); 1 = one graph per step '
                          '(profiles/r4_graph_steps.txt: 16 / 32 measured 0.5-1%% above 8)')
     args = ap.parse_args()
+    if args.dtype is None:             # BASELINE.json config 5: "Rainbow ... fp16 conv MFMA path"
+        args.dtype = VARIANT_DTYPE.get(args.variant, 'bf16')
     if args.gpus < 1:
         ap.error('--gpus must be >= 1')
     # --gpus N > 1 started without a launcher: relaunch N ranks under torch.distributed.run as a

@@ -259,8 +259,12 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     dh_from(S.dq);
     return;
   }
-  if (tid == 0) {                     // acquire: the other blocks' partial slots (and h rows)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (tid == 0) {
+    // spin mode reads only the partial-Q slots of this launch, and those with agent-scope (sc1)
+    // loads after the counter add returned (the producers stored them sc1): no acquire fence, whose
+    // L1 invalidate costs ~1.7 us on this chain (MI355X_MICROARCH.md, coherence table). Otherwise
+    // the tail also reads the other blocks' h rows with plain loads: acquire first.
+    if (!f.spin || f.fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(f.cnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -297,12 +301,15 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
       if (r < nrows && (c < A || h.dueling)) {
         const float* p = f.qacc + (((int64_t)(i0 + i) * f.Mpad + m_base + r) * 32 + c) * NT;
         const int lo = h.dueling ? (c < A ? half : 0) : 0, hi = h.dueling ? (c < A ? NT : half) : NT;
-        for (int u = lo; u < hi; u += 4) {
-          const float4 x = *reinterpret_cast<const float4*>(p + u);
-          v += x.x;
-          v += x.y;
-          v += x.z;
-          v += x.w;
+        for (int u = lo; u < hi; u += 4) {        // (sc1 loads, in tile order)
+          const float x0 = __hip_atomic_load(p + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float x1 = __hip_atomic_load(p + u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float x2 = __hip_atomic_load(p + u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float x3 = __hip_atomic_load(p + u + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v += x0;
+          v += x1;
+          v += x2;
+          v += x3;
         }
       }
       S.q[i][r][c] = v;

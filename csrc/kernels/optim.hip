@@ -128,7 +128,7 @@ static int grid_for_ticket(int n4) {
 void launch_optimizer_step(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow,
                            int64_t* step, int32_t* ticket, const float* hp9, float lr, float reg, int reg_end,
                            float grad_scale, int n, float* tgt, int tfreq, hipStream_t st) {
-  OptHP h;
+  OptHP h{};
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
@@ -161,6 +161,8 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
   h.prof = optim_prof_buffer();
+  static const int dep_fence = getenv("DQN_FENCE_TAILS") != nullptr ? 1 : 0;
+  h.dep_fence = dep_fence;
   // one block per job up to max_grid (grid-stride beyond it); block 0 (+1 sampler block when the
   // launch draws the next minibatch) closes the launch once every other block has arrived
   const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};

@@ -21,6 +21,7 @@ struct OptHP {
   float lr, reg, grad_scale;
   float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
   int reg_end;
+  int dep_fence;             // A/B knob (DQN_FENCE_TAILS=1): dependent jobs acquire-fence + plain loads
   // probe launches only (DQN_OPT_PROF=1, nullptr otherwise): [0, 16) s_memtime phase stamps of
   // blocks 0 and 1, then per block [start, ready, end] s_memrealtime (100 MHz) for blocks < kTlBlocks
   // (ready: a dependent job's wait is over / the sampler's draw is done)
@@ -300,8 +301,8 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (no acquire fence: the waiter reads nothing the member wrote -- it only must not overwrite
+    //  the slot tables before the member's reads completed, which its count follows)
     if (tl) tl[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #else
     (void)m;
@@ -432,6 +433,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // UNCONDITIONAL load issued in one batch: out-of-range threads read the job's first element
   // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
   // vmcnt wait between loads and serialise the item on memory latency.)
+  bool gsc1 = false;             // WG dependent job: its gradient is read with sc1 loads
   auto item = [&](const UpdJob& jb, auto al_c, auto nz_c, auto dg_c) {
     // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read
     constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value, DG = decltype(dg_c)::value;
@@ -495,7 +497,14 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     if constexpr (NZ) {
       ld(W, so, ws);
       if constexpr (UPD) {
-        if constexpr (!DG) ld(G, so, gs);
+        if constexpr (!DG) {
+          if (gsc1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gs[j] = __hip_atomic_load(G + so + ix[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            ld(G, so, gs);
+          }
+        }
         if constexpr (ONE) ld(S0, so, as);
         if constexpr (TWO_LD) ld(S1, so, bs);
       }
@@ -563,7 +572,12 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
           for (int j = 0; j < 4; ++j) g[j] += pv[j];
         }
       } else if (!fcj) {
-        ld(G, mo, g);
+        if (gsc1) {                                       // produced in this launch (see the dep wait)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[j] = __hip_atomic_load(G + mo + ix[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          ld(G, mo, g);
+        }
       }
     }
     // ---- update
@@ -721,10 +735,16 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                 break;
               }
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the tiles' atomics are visible
+            // (no acquire fence: the item reads this gradient with agent-scope sc1 loads, and the
+            //  tiles produced it by memory-side atomics / sc1 stores; the fence's L1 invalidate cost
+            //  ~1.7 us on the launch's critical path)
+          }
+          if (h.dep_fence && threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
           __syncthreads();
+          gsc1 = !h.dep_fence;
         }
       }
 #endif

@@ -269,8 +269,12 @@ class HipExecutor:
         self._wg_pending = None
         self._wg_plans: Dict[tuple, tuple] = {}
         # 128-row chunks per conv weight-gradient tile of the fused launch (summed in registers, one
-        # set of fp32 atomics per tile)
-        self.wg_conv_chunks = 2
+        # set of fp32 atomics per tile; DQN_WG_CHUNKS: measured 2 > 4 > 8, gpurun_out/r5c)
+        self.wg_conv_chunks = int(os.environ.get('DQN_WG_CHUNKS', '2'))
+        # fc jobs interleaved with the weight-gradient tiles in that launch (optim_pack.h wg_mix): measured
+        # 14.8k -> 13.6k SGD steps/s on the flagship (the tiles, on the critical path, then finish later;
+        # gpurun_out/r5a/ab.jsonl), so off unless DQN_WG_MIX=1
+        self.wg_mix = os.environ.get('DQN_WG_MIX', '0') == '1'
         # (job table, partial buffer ptr) of a step whose conv weight gradients the next
         # update_and_pack sums from the grouped wgrad's deterministic partials
         self._parts_pending = None
@@ -445,10 +449,7 @@ class HipExecutor:
                 table += fcj
             host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
             jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
-            # fc jobs interleaved with the tiles (they lead the table unless dep_first); DQN_WG_MIX=0: the
-            # tiles first, as round 4
-            mix = 0 if dep_first or os.environ.get('DQN_WG_MIX', '1') == '0' else len(fcj)
-            pl = (host.to(dev), int(total), jobs, mix, done)
+            pl = (host.to(dev), int(total), jobs, len(fcj), done)
             self._wg_plans[key] = pl
         return pl
 
@@ -497,7 +498,7 @@ class HipExecutor:
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             target_noise, teff, tpk, noise_rng, fcargs, 0, wg=plan.data_ptr(), wg_blocks=nwg,
-                            wg_jobs=nfc)
+                            wg_jobs=nfc if self.wg_mix and not self.noisy else 0)
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:

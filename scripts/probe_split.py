@@ -76,7 +76,7 @@ def main():
     def launch(jobs, fcx, wgp=0, nb=0, sample=(), nj=None):
         ex.ext.optim_pack(op, *base, jobs, p, net.target.flat, pt, 1 << 30, ex.opt_max_grid, None, None, None, None,
                           list(sample), [], [], None, None, None, None, fcx, 0, wg=wgp, wg_blocks=nb,
-                          wg_jobs=nfc if nj is None else nj)
+                          wg_jobs=0 if nj is None else nj)
 
     def timeit(fn):
         for _ in range(10):
@@ -136,8 +136,16 @@ def main():
         bounds, lo = [], 0
         for m in members:
             pass
+        # per member (the timeline's ready word holds a tile's member id)
+        tlv = ex.ext.optim_timeline(1 + len(rows))
+        per = {}
+        for b, r in enumerate(rows):
+            per.setdefault(int(tlv[3 * (b + 1) + 1]), []).append(r)
         out['tile_phases_us'] = {'first_conv1_tiles': rows[:3],
-                                 'median_all': [med([r[i] for r in rows]) for i in range(6)]}
+                                 'median_all': [med([r[i] for r in rows]) for i in range(6)],
+                                 'median_by_member': {str(m): {'n': len(v), 'phases': [med([r[i] for r in v])
+                                                                                         for i in range(6)]}
+                                                      for m, v in sorted(per.items())}}
     print(json.dumps(out))
 
 

@@ -631,10 +631,10 @@ def _gpu_free_parent(world):
     timed out with every wait pointing at one never-run block (ranks 1, 2: reduce-scatter, peer 0
     block 6, flag 2 of 3; the others all-gather on peer 1), while the same case passed first in a
     fresh process. The full GPU suite opens a context in earlier modules: skip there, run the
-    module on its own (scripts/gpu_r4_dist.sh) for the 8-rank evidence."""
+    module on its own (scripts/gpu_dp.sh) for the 8-rank evidence."""
     if world >= 8 and torch.cuda.is_initialized():
         pytest.skip('8 ranks + a GPU-holding test process on one device: run this module in a fresh '
-                    'process (scripts/gpu_r4_dist.sh)')
+                    'process (scripts/gpu_dp.sh)')
 
 
 @pytest.mark.parametrize('world,extra', [
