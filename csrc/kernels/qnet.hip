@@ -1253,7 +1253,8 @@ constexpr int kGrpMC256 = 0x40;
   case L_NAT_CONV2_FWD + OFF: group_member<NatC2, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;    \
   case L_NAT_CONV3_FWD + OFF: group_member<NatC3, MC, 64, 64>(G.a[i], G.g[i], b, G.gx[i], G.gy[i], glds); break;
 // (<= 128 VGPRs: 4 waves / SIMD, the 4 blocks / CU the conv members' LDS allows)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) wgrad_group_kernel(WgradGroup Gv) {
+// (fp32 build: 3 waves / EU -- at 4 the 128-VGPR cap spilled 20 B / lane to scratch)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DQN_ACT_F32 ? 3 : 4))) wgrad_group_kernel(WgradGroup Gv) {
   extern __shared__ __attribute__((aligned(16))) act_t glds[];
   // members are read straight from the kernel-argument segment (the group is the only, offset-0
   // argument): indexing the by-value parameter with the runtime member index otherwise lets the

@@ -151,7 +151,10 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   for (int mt = 0; mt < (R2 + 15) / 16; ++mt) p2r[mt] = kTrunkP2[pv][mt * 16 + row];
 #pragma unroll
   for (int mt = 0; mt < (R3 + 15) / 16; ++mt) p3r[mt] = kTrunkP3[pv][mt * 16 + row];
-  bfx8 w1r[2][K1 / 32], w2r[K2 / 64];
+#if !DQN_ACT_F32
+  bfx8 w1r[2][K1 / 32];
+#endif
+  bfx8 w2r[K2 / 64];
   const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
   bfx8 w1s[2];
   {
@@ -159,8 +162,10 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
     const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
     w1s[0] = W1[tid];
     w1s[1] = W1[tid + 512];
+#if !DQN_ACT_F32
 #pragma unroll
     for (int j = 0; j < K2 / 64; ++j) w2r[j] = W2[((hi * (K2 / 64) + j) * 4 + nq) * 64 + lane];
+#endif
   }
   static_assert((K1 / 32) * 2 * 64 == 2 * 512, "two conv1 fragments per thread");
   // The MFMAs below run transposed (weights as the A operand): lane l then holds 4
@@ -195,11 +200,13 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   wl1[tid] = w1s[0];
   wl1[tid + 512] = w1s[1];
   __syncthreads();
+#if !DQN_ACT_F32
 #pragma unroll
   for (int ks = 0; ks < K1 / 32; ++ks) {
     w1r[0][ks] = wl1[(ks * 2 + 0) * 64 + lane];
     w1r[1][ks] = wl1[(ks * 2 + 1) * 64 + lane];
   }
+#endif
   TRUNK_MARK(1);
 
   // ---------------------------------------------------------------- conv1 -> act1 (+x1)
@@ -226,8 +233,15 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
       for (int ks = 0; ks < K1 / 32; ++ks) {              // k = (kh*8 + kw)*4 + c, kh = ks
+#if DQN_ACT_F32
+        // fp32 build: the weight fragments (32 B per lane each) stay in LDS and are read per k-step:
+        // held in registers (128 VGPRs) they pushed the kernel past 256 VGPRs into scratch spills
+        c0 = tmfma(wl1[(ks * 2 + 0) * 64 + lane], fa[ks], c0);
+        c1 = tmfma(wl1[(ks * 2 + 1) * 64 + lane], fa[ks], c1);
+#else
         c0 = tmfma(w1r[0][ks], fa[ks], c0);
         c1 = tmfma(w1r[1][ks], fa[ks], c1);
+#endif
       }
       const int p = mt * 16 + row;
       if (p < np1) {
@@ -244,8 +258,17 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
   }
   // conv3 fragments into the registers conv1 released (latency hidden by conv2)
   bfx8 w3r[K3 / 64];
+#if DQN_ACT_F32
+  // fp32 build (2x the fragment registers): conv2's weights now, conv3's after conv2's MFMAs
+  {
+    const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
+#pragma unroll
+    for (int j = 0; j < K2 / 64; ++j) w2r[j] = W2[((hi * (K2 / 64) + j) * 4 + nq) * 64 + lane];
+  }
+#else
 #pragma unroll
   for (int j = 0; j < K3 / 64; ++j) w3r[j] = W3[((hi * (K3 / 64) + j) * 4 + nq) * 64 + lane];
+#endif
   __syncthreads();
   TRUNK_MARK(2);
   // ---------------------------------------------------------------- conv2 -> act2 (+x2)
@@ -266,6 +289,21 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       }
     };
     f32x4 acc2[MTX];
+#if DQN_ACT_F32
+    // fp32 build: one operand buffer (the double buffer is 128 VGPRs of fp32 fragments); the LDS
+    // latency it hid is small against the 64 fp32 MFMAs of an m-tile
+    bfx8 fa1[KH];
+#pragma unroll
+    for (int mt = 0; mt < MTX; ++mt) {
+      if (mt >= MT) break;                                // block-uniform
+      load2(fa1, mt);
+      acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < KH; ++j) acc2[mt] = tmfma(w2r[j], fa1[j], acc2[mt]);
+    }
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) w3r[j] = W3[((hi * (K3 / 64) + j) * 4 + nq) * 64 + lane];
+#else
     bfx8 fa[2][KH];
     load2(fa[0], 0);
 #pragma unroll
@@ -278,6 +316,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int j = 0; j < KH; ++j) acc2[mt] = tmfma(w2r[j], fa[mt & 1][j], acc2[mt]);
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     if (hi == 1) {
 #pragma unroll
       for (int mt = 0; mt < MTX; ++mt)
@@ -319,6 +358,17 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       }
     };
     f32x4 acc[MT];
+#if DQN_ACT_F32
+    bfx8 fa1[KJ];                                         // (fp32: single-buffered, as conv2)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      if (mt >= mtn) break;                               // block-uniform
+      load3(fa1, mt);
+      acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < KJ; ++j) acc[mt] = tmfma(w3r[j], fa1[j], acc[mt]);
+    }
+#else
     bfx8 fa[2][KJ];
     load3(fa[0], 0);
 #pragma unroll
@@ -331,6 +381,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int j = 0; j < KJ; ++j) acc[mt] = tmfma(w3r[j], fa[mt & 1][j], acc[mt]);
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     TRUNK_MARK(8);
     // k-half exchange: hi waves park fp32 partials in the (dead) input region
     if (hi == 1) {

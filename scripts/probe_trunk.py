@@ -11,7 +11,8 @@ from dist_dqn_amd.config import preset
 from dist_dqn_amd.models.network import Network
 
 dev = torch.device('cuda', 0)
-cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=0 --backend=hip')
+DTYPE = sys.argv[1] if len(sys.argv) > 1 else 'bf16'          # python scripts/probe_trunk.py [bf16|fp16|fp32]
+cfg = preset('nature', 'Pong-v0', '--dtype=%s --seed=0 --backend=hip' % DTYPE)
 net = Network.create_network(cfg, (84, 84, 4), 6, device=dev)
 ex = net.executor
 p, f = ex.packed(net.online.flat), net.online.flat
