@@ -438,18 +438,22 @@ class HipExecutor:
             # range-dependent jobs right after the tiles (their waits end when the tiles do) or at the
             # end of the grid: first measured +1.2% for noisy nets, whose fc jobs run ~10 us each and
             # kept them queued to ~45 us; -0.2..-1.0% for the plain nets (profiles/r4_dep_first_ab.txt)
-            dep_first = self.noisy
-            table, deps = ([] if dep_first else list(fcj)), []
+            # DQN_DEP_AT=n: the dependent jobs after the first n fc jobs (A/B of the grid order). Noisy
+            # nets: after 300 of their ~1.6k fc jobs (+1-2% Rainbow over right after the tiles,
+            # gpurun_out/r5j, r5k); plain nets: at the end (0 / 200 / 400 / 600 measured the same)
+            lead = min(300, len(fcj)) if self.noisy else len(fcj)
+            if os.environ.get('DQN_DEP_AT'):
+                lead = max(0, min(len(fcj), int(os.environ['DQN_DEP_AT'])))
+            table, deps = list(fcj[:lead]), []
             for (mi, slot), its in sorted(groups.items()):
                 deps.append([mi, slot, len(table), len(its)])
                 for it in its:                 # the job's block waits for that range's tiles
                     it[21] = mi * ext.WG_SLOTS + slot
                 table += its
-            if dep_first:
-                table += fcj
+            table += fcj[lead:]
             host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
             jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
-            pl = (host.to(dev), int(total), jobs, len(fcj), done)
+            pl = (host.to(dev), int(total), jobs, len(fcj), done, lead)
             self._wg_plans[key] = pl
         return pl
 
@@ -467,7 +471,7 @@ class HipExecutor:
         wg, self._wg_pending = self._wg_pending, None
         fcargs = self._take_fc(fc)
         assert fcargs, 'deferred weight gradients need the fused fc gradient (defer_fc)'
-        plan, nwg, jobs, nfc, _ = self._wg_plan(wg, grad, dev)
+        plan, nwg, jobs, nfc, _, lead = self._wg_plan(wg, grad, dev)
         hp = opt.hp
         s0 = opt.slots[0] if len(opt.slots) > 0 else flat
         s1 = opt.slots[1] if len(opt.slots) > 1 else flat
@@ -498,7 +502,7 @@ class HipExecutor:
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             target_noise, teff, tpk, noise_rng, fcargs, 0, wg=plan.data_ptr(), wg_blocks=nwg,
-                            wg_jobs=nfc if self.wg_mix and not self.noisy else 0)
+                            wg_jobs=lead if self.wg_mix else 0)
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:

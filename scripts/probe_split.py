@@ -58,7 +58,7 @@ def main():
     opt = net.optimizer
     hp = opt.hp
     hps = [float(hp[k]) for k in ('momentum', 'rho', 'rms_mom', 'rms_eps', 'b1', 'b2', 'adam_eps', 'ad_rho', 'ad_eps')]
-    plan, nwg, jobs, nfc, _ = ex._wg_plan(wg, net.grad, dev)
+    plan, nwg, jobs, nfc, _, _ = ex._wg_plan(wg, net.grad, dev)
     nint = ex.ext.UPD_JOB_INTS
     jf = jobs[:nfc * nint]
     s0 = opt.slots[0] if opt.slots else net.online.flat
@@ -109,12 +109,12 @@ def main():
     for cc in (1, 4):                     # chunks per conv tile (the executor's default: 2)
         ex.wg_conv_chunks = cc
         ex._wg_plans = {}
-        pl2, n2, j2, _, _ = ex._wg_plan(wg, net.grad, dev)
+        pl2, n2, j2, _, _, _ = ex._wg_plan(wg, net.grad, dev)
         out['F_chunks%d' % cc] = timeit(lambda: launch(j2, fca, pl2.data_ptr(), n2, sample=smp))
         out['wg_blocks_chunks%d' % cc] = n2
     ex.wg_conv_chunks = 2
     ex._wg_plans = {}
-    plan, nwg, jobs, nfc, _ = ex._wg_plan(wg, net.grad, dev)
+    plan, nwg, jobs, nfc, _, _ = ex._wg_plan(wg, net.grad, dev)
     if os.environ.get('DQN_OPT_PROF'):
         out['timeline_us'] = timeline(ex, plan, nwg, jobs, nfc, nint, lambda: launch(jobs, fca, plan.data_ptr(), nwg,
                                                                                  sample=smp))
