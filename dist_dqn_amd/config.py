@@ -209,6 +209,10 @@ def build_parser() -> argparse.ArgumentParser:
     a('--max_to_keep', default=5, type=int)
     a('--save_agent_state', action='store_true', help='Checkpoint epsilon/step sidecar')
     a('--async_ps', action='store_true', help='Emulate async parameter-server updates')
+    a('--ps_pipeline', default=0, type=int,
+      help='async PS over xGMI: 1 = a worker takes the PS answer to its PREVIOUS push, then pushes this '
+           'step\'s gradient and goes on (one more step of staleness, within the reference\'s Hogwild '
+           'semantics; no per-step round trip to the server); 0 = push, then wait for this push\'s answer')
     a('--ps_transport', default='auto', choices=['auto', 'p2p', 'xgmi'],
       help='--async_ps transport: one-sided xGMI peer memory (GPU; replicated targets) or '
            'torch.distributed point-to-point; auto = xgmi when available')
@@ -316,6 +320,7 @@ class Config:
     save_agent_state: bool = False
     async_ps: bool = False
     ps_transport: str = 'auto'
+    ps_pipeline: int = 0
     max_train_steps: int = 0
     allreduce_check_steps: int = 1000
     stop_sync_steps: int = 10

@@ -320,6 +320,27 @@ class Learner:
         """The async parameter server answered STOP (no more pushes are accepted)."""
         return self.ps is not None and self.ps.stopped
 
+    def _ps_in_graph(self) -> bool:
+        """The PS exchange (push / pull kernels with device-side sequence numbers) and the repack
+        ride in the step's HIP graph: the xgmi transport with replicated targets."""
+        return (self.ps is not None and getattr(self.ps, 'in_graph', False)
+                and not bool(self.config.disable_target_replication))
+
+    def _ps_exchange_kernels(self):
+        """The graph-capturable part of the exchange: push + pull launches, then the repack."""
+        self.ps.exchange_kernels(self.net.grad, self.net.online.flat, self.net.global_step)
+        self.net._repack()
+
+    def _ps_after_graph(self):
+        """Host side of an in-graph exchange: the push count and the LOCAL target cadence
+        (reference `dqn_agent.py:143,215-222`), eager after the replay (stream order)."""
+        self.ps.pushes += 1
+        due = self.tau >= 1.0 and (self.train_steps + 1) % max(1, self.config.target_update_freq) == 0
+        if self.tau < 1.0:
+            self.update_target_now(self.tau)
+        elif due:
+            self.update_target_now()
+
     def _ps_exchange(self):
         """Async-PS worker: push grads, pull the PS parameters, repack; target cadence on
         the LOCAL train-step count (reference `dqn_agent.py:143,215-222`). With
@@ -366,9 +387,15 @@ class Learner:
         s.wait_stream(torch.cuda.current_stream(self.device))
         g_pre, g_post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
-            if self.ps is not None:          # post-exchange work is host-driven (eager)
+            if self.ps is not None:
+                # xgmi transport: the whole worker step (gradient, push, pull, repack) is ONE graph;
+                # otherwise the post-exchange work is host-driven (eager)
+                inside = self._ps_in_graph()
                 with torch.cuda.graph(g_pre, stream=s, capture_error_mode=_CAPTURE_MODE):
                     self._sample_and_grad()
+                    if inside:
+                        self._run_tail()
+                        self._ps_exchange_kernels()
                 self._graphs = (g_pre,)
             elif self.ctx.enabled and self.reducer.in_graph:
                 # the whole DP step: ONE graph
@@ -466,7 +493,10 @@ class Learner:
                 self._capture()      # records only; the replay below runs the step
             self._graphs[0].replay()
             if self.ps is not None:
-                self._ps_exchange()
+                if self._ps_in_graph():
+                    self._ps_after_graph()
+                else:
+                    self._ps_exchange()
             elif len(self._graphs) > 1:
                 g_tail = self._graphs[2]
                 if g_tail is not None:

@@ -467,7 +467,7 @@ class XgmiPSClient:
     transport = 'xgmi'
 
     def __init__(self, ctx: DistContext, flat: torch.Tensor, shared: Optional[_PSShared] = None,
-                 timeout_s: float = 60.0):
+                 timeout_s: float = 60.0, pipeline: bool = False):
         assert ctx.enabled and ctx.rank >= 1
         self.ctx, self.w = ctx, ctx.rank
         self.n = flat.numel()
@@ -483,6 +483,9 @@ class XgmiPSClient:
         self.pushes = 0
         self.target_updated = False
         self._host_pushes = 1
+        # pipelined exchange (--ps_pipeline): take the answer to the previous push, then push; the
+        # server answered it while this worker computed the gradient, so the wait is usually over
+        self.pipeline = bool(pipeline)
 
     @property
     def stopped(self) -> bool:
@@ -501,16 +504,39 @@ class XgmiPSClient:
                  sync_target: bool = False, target: Optional[torch.Tensor] = None) -> bool:
         if self.stopped:
             return False
-        self.sh.ext.ps_push(grad, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
-        self._pull(flat, global_step)
+        self.exchange_kernels(grad, flat, global_step)
         self.pushes += 1
         return True
+
+    # the push / pull launches keep their sequence numbers on the device: a captured graph replays them
+    in_graph = True
+
+    def exchange_kernels(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
+        '''The exchange's launches only (graph-capturable; after a STOP answer the pull copies nothing
+        and the push lands in a slot the server no longer reads).'''
+        if self.pipeline:
+            # answer to push k-1 -> parameters (this step's gradient is computed already: stream
+            # order), then push k into the slot the server has finished reading (it answered k-1)
+            self._pull(flat, global_step)
+            self.sh.ext.ps_push(grad, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
+        else:
+            self.sh.ext.ps_push(grad, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
+            self._pull(flat, global_step)
+
+    def flush(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
+        '''Pipelined exchange: take the answer to the last push (the parameters after it).'''
+        if self.pipeline and not self.stopped:
+            self._pull(flat, global_step)
 
     def check(self) -> bool:
         """False if a pull timed out waiting for the PS (host sync)."""
         return int(self._err[0]) == 0
 
     def close(self):
+        if self.pipeline and not self.stopped and self.pushes > 0:
+            # the server must answer the last gradient push before BYE replaces it in the push word
+            scratch = torch.empty(self.n, dtype=torch.float32, device=self._seq.device)
+            self._pull(scratch, None)
         if not self.stopped:
             self.sh.ext.ps_push(self._empty, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, _BYE,
                                 self._ticket)
@@ -538,7 +564,8 @@ def make_ps_server(ctx: DistContext, network, config):
 def make_ps_client(ctx: DistContext, flat: torch.Tensor, config):
     if ps_transport(ctx, config) == 'xgmi':
         try:
-            return XgmiPSClient(ctx, flat, timeout_s=float(getattr(config, 'ps_timeout_s', 60.0)))
+            return XgmiPSClient(ctx, flat, timeout_s=float(getattr(config, 'ps_timeout_s', 60.0)),
+                                pipeline=bool(getattr(config, 'ps_pipeline', 0)))
         except RuntimeError as e:
             log.warning('async PS over xgmi unavailable (%s): torch.distributed p2p instead', e)
     return AsyncPSClient(ctx, flat)
