@@ -10,8 +10,8 @@
 // worker's stream with no host synchronisation (graph-capturable):
 //   ps_push_kernel   grad -> PS slot (peer stores), then the last block publishes
 //                    push word = (seq << 4) | kind with a system-scope release
-//   ps_pull_kernel   every block waits for done word >= (seq << 4) (system-scope acquire,
-//                    bounded), then snapshot -> local flat and the int64 global step
+//   ps_wait_kernel   one block waits for done word >= (seq << 4) (system-scope acquire, bounded)
+//   ps_copy_kernel   then snapshot -> local flat and the int64 global step
 // PS, per arrival (host loop): the fused optimizer reads the gradient slot in place, then
 //   ps_publish_kernel  flat -> that worker's snapshot, step, then done word = (seq << 4) | st
 #include "common.h"
@@ -50,50 +50,41 @@ ps_push_kernel(const float4* __restrict__ grad, float4* __restrict__ slot, long 
   }
 }
 
-// wait for the PS's answer to push number seq[0], then snapshot -> flat (+ the global step);
-// status kPsStop: the PS stopped, nothing is copied and stopped[0] is set. Block 0 (dispatched
-// first, so always resident) polls the host-shared done word and opens a device-local gate
-// (gate[0] = seq, gate[1] = status) the other blocks poll in L2, so only one thread per worker
-// reads host memory. A wait longer than timeout_ns sets err[0] (checked by the host) instead of
-// spinning forever.
-__global__ void __launch_bounds__(kPsThreads)
-ps_pull_kernel(float4* __restrict__ flat, const float4* __restrict__ snap, long n4, int64_t* step,
-               const int64_t* snap_step, const uint64_t* done_word, const int64_t* seq, int64_t* gate,
-               int32_t* err, int32_t* stopped, long long timeout_ns) {
-  __shared__ int s_ok;
-  if (threadIdx.x == 0) {
-    const int64_t want = seq[0];
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t limit = (uint64_t)(timeout_ns / 10);       // 100 MHz counter
-    int ok = 1;
-    if (blockIdx.x == 0) {
-      uint64_t v = ld_acquire_sys(done_word);
-      while ((int64_t)(v >> 4) < want) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) { ok = 0; break; }
-        __builtin_amdgcn_s_sleep(8);
-        v = ld_acquire_sys(done_word);
-      }
-      const int64_t st = ok ? (int64_t)(v & 15) : -1;
-      if (!ok) err[0] = 1;
-      if (st == (int64_t)kPsStop) stopped[0] = 1;
-      __hip_atomic_store(gate + 1, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gate, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      ok = st == 0;
-    } else {
-      while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > limit + 100000000ull) { ok = 0; break; }   // (+1 s)
-        __builtin_amdgcn_s_sleep(4);
-      }
-      if (ok) ok = __hip_atomic_load(gate + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-      else err[0] = 1;
-    }
-    s_ok = ok;
+// Wait for the PS's answer to push number seq[0] in ONE block (ps_wait_kernel), then copy the
+// snapshot -> flat (+ the global step) with the whole grid (ps_copy_kernel), in stream order. (A
+// single kernel whose every block spun on the answer kept ~512 spinning workgroups on the GPU for
+// the whole server round trip -- the other workers' and the server's kernels waited behind them:
+// 153 us per pull, profiles/r5_async_ps_trace.md.) Status kPsStop: the PS stopped, nothing is
+// copied and stopped[0] is set. A wait longer than timeout_ns sets err[0] (checked by the host)
+// instead of spinning forever. gate[1] = the answer's status for the copy kernel (-1: timed out).
+__global__ void __launch_bounds__(64)
+ps_wait_kernel(const uint64_t* done_word, const int64_t* seq, int64_t* gate, int32_t* err, int32_t* stopped,
+               long long timeout_ns) {
+  if (threadIdx.x != 0) return;
+  const int64_t want = seq[0];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t limit = (uint64_t)(timeout_ns / 10);       // 100 MHz counter
+  int ok = 1;
+  uint64_t v = ld_acquire_sys(done_word);
+  while ((int64_t)(v >> 4) < want) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > limit) { ok = 0; break; }
+    __builtin_amdgcn_s_sleep(8);
+    v = ld_acquire_sys(done_word);
   }
-  __syncthreads();
-  if (!s_ok) return;
+  const int64_t st = ok ? (int64_t)(v & 15) : -1;
+  if (!ok) err[0] = 1;
+  if (st == (int64_t)kPsStop) stopped[0] = 1;
+  gate[1] = st;
+  gate[0] = want;
+}
+
+__global__ void __launch_bounds__(kPsThreads)
+ps_copy_kernel(float4* __restrict__ flat, const float4* __restrict__ snap, long n4, int64_t* step,
+               const int64_t* snap_step, const int64_t* gate) {
+  if (gate[1] != 0) return;                                 // stopped / timed out: nothing to copy
   for (long i = (long)blockIdx.x * kPsThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kPsThreads)
     flat[i] = snap[i];
-  if (blockIdx.x == 0 && threadIdx.x == 0) step[0] = snap_step[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && step != nullptr) step[0] = snap_step[0];
 }
 
 // PS: flat -> worker snapshot (+ step), then done word = value (system-scope release, last block).
@@ -140,9 +131,9 @@ void launch_ps_pull(float* flat, const float* snap, long n, int64_t* step, const
                     const uint64_t* done_word, const int64_t* seq, int64_t* gate, int32_t* err, int32_t* stopped,
                     long long timeout_ns, hipStream_t st) {
   const long n4 = n / 4;
-  hipLaunchKernelGGL(dqn::ps_pull_kernel, dim3(dqn::ps_grid(n4)), dim3(dqn::kPsThreads), 0, st,
-                     reinterpret_cast<float4*>(flat), reinterpret_cast<const float4*>(snap), n4, step, snap_step,
-                     done_word, seq, gate, err, stopped, timeout_ns);
+  hipLaunchKernelGGL(dqn::ps_wait_kernel, dim3(1), dim3(64), 0, st, done_word, seq, gate, err, stopped, timeout_ns);
+  hipLaunchKernelGGL(dqn::ps_copy_kernel, dim3(dqn::ps_grid(n4)), dim3(dqn::kPsThreads), 0, st,
+                     reinterpret_cast<float4*>(flat), reinterpret_cast<const float4*>(snap), n4, step, snap_step, gate);
 }
 
 void launch_ps_publish(float* snap, const float* flat, long n, int64_t* snap_step, const int64_t* step,
