@@ -215,7 +215,7 @@ class Network:
         return 0, end
 
     def apply_grads(self, grad_scale: float = 1.0, target_freq: Optional[int] = None, next_sample=None,
-                    grad: Optional[torch.Tensor] = None) -> bool:
+                    grad: Optional[torch.Tensor] = None, repack: bool = True) -> bool:
         """Optimizer step (global_step += 1 inside it) + executor repack.
 
         target_freq: also do the hard target sync (target <- online when the new
@@ -224,7 +224,9 @@ class Network:
         still owes the target update (``hard_target_update``). next_sample: ``(spec, B)`` — the
         fused launch also draws the next uniform minibatch (only honoured when it returns True).
         grad: the gradient buffer to apply (default ``self.grad``; the xgmi parameter server passes
-        a worker's peer-written slot)."""
+        a worker's peer-written slot). repack=False (the parameter server, which never runs the
+        network): the optimizer step only; the caller calls ``refresh_packed`` before the packed
+        copies are used again."""
         ex = self.executor
         g = self.grad if grad is None else grad
         fuse = (target_freq is not None and self.online.flat.is_cuda and self.optimizer.backend != 'torch'
@@ -260,7 +262,8 @@ class Network:
                           freq=int(target_freq))
             return True
         self.optimizer.step(self.online.flat, g, grad_scale, self.global_step)
-        self._repack()
+        if repack:
+            self._repack()
         return False
 
     def _repack(self):

@@ -381,7 +381,7 @@ class XgmiPSServer:
                     self.stopped_workers += 1
                     continue
                 # arrival-order apply, the gradient read in place from the worker's slot
-                self.net.apply_grads(1.0, grad=self._grads[w])
+                self.net.apply_grads(1.0, grad=self._grads[w], repack=False)
                 self._publish(w, s)
                 self.updates += 1
                 self.per_worker[w] += 1
@@ -391,6 +391,7 @@ class XgmiPSServer:
                 time.sleep(idle_sleep)
         torch.cuda.synchronize(self.net.online.flat.device)
         self.busy_s = time.perf_counter() - t_busy
+        self.net.refresh_packed()             # (updates ran without the repack)
         return self.updates
 
     def _serve_native(self, max_updates: int, supervisor) -> int:
@@ -406,9 +407,10 @@ class XgmiPSServer:
             for w in self.workers:
                 ga, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga, stream=s, capture_error_mode='thread_local'):
-                    # arrival-order apply, the gradient read in place from worker w's slot; the
-                    # answer's push number comes from w's push word (the kernel echoes it)
-                    net.apply_grads(1.0, grad=self._grads[w])
+                    # arrival-order apply, the gradient read in place from worker w's slot (no
+                    # repack: the server never runs the network); the answer's push number comes
+                    # from w's push word (the kernel echoes it)
+                    net.apply_grads(1.0, grad=self._grads[w], repack=False)
                     ext.ps_publish(sh.snap(w), net.online.flat, sh.snap_step(w), net.global_step, sh.done_word(w), 0,
                                    self._ticket, self.n, echo=sh.push_word(w))
                 with torch.cuda.graph(gs, stream=s, capture_error_mode='thread_local'):
@@ -452,6 +454,7 @@ class XgmiPSServer:
         self.stopped_workers = int(stopped)
         self.busy_s = float(busy)
         torch.cuda.current_stream(dev).wait_stream(s)
+        self.net.refresh_packed()             # (updates ran without the repack)
         torch.cuda.synchronize(dev)
         return self.updates
 
