@@ -323,7 +323,7 @@ def test_bench_gpus_more_than_the_node_has_fails_loudly():
     assert 'needs 8 GPUs' in out.stderr
 
 
-def _worker_async_ps(rank, world, port, transport, errq):
+def _worker_async_ps(rank, world, port, transport, errq, pipeline=0):
     """--async_ps on the GPU: rank 0 is the parameter server (HIP fused optimizer on its HBM
     copy), ranks 1..world-1 run the HIP Nature-CNN learner against it (push gradient, pull
     parameters + int64 global_step). Three ranks share cuda:0 over gloo (p2p: the messages;
@@ -338,7 +338,7 @@ def _worker_async_ps(rank, world, port, transport, errq):
         from dist_dqn_amd.parallel.async_ps import make_ps_client, make_ps_server
         from dist_dqn_amd.replay import DeviceReplay
         cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=5 --backend=hip --replay_memory_capacity=2048 '
-                     '--async_ps --target_update_freq=3 --ps_transport=%s' % transport)
+                     '--async_ps --target_update_freq=3 --ps_transport=%s --ps_pipeline=%d' % (transport, pipeline))
         ctx = init_distributed(cfg, device='cuda')
         net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
         assert net.executor.name.startswith('hip'), net.executor.name
@@ -373,8 +373,14 @@ def _worker_async_ps(rank, world, port, transport, errq):
             torch.cuda.synchronize()
             assert torch.isfinite(ln.loss).all()
             assert ps.pushes == steps
-            assert seen == sorted(seen) and len(set(seen)) == steps, seen    # the PS step only moves forward
-            assert all(1 <= s <= steps * (world - 1) for s in seen), seen
+            if pipeline:
+                # each step takes the answer to the PREVIOUS push: the first one is the initial
+                # parameters (step 0), and the PS step still only moves forward
+                assert seen == sorted(seen) and seen[0] == 0, seen
+                assert all(0 <= s < steps * (world - 1) for s in seen), seen
+            else:
+                assert seen == sorted(seen) and len(set(seen)) == steps, seen    # the PS step only moves forward
+                assert all(1 <= s <= steps * (world - 1) for s in seen), seen
             if transport == 'xgmi':
                 assert ps.check()
                 ps.close()
@@ -393,6 +399,16 @@ def _worker_async_ps(rank, world, port, transport, errq):
 @pytest.mark.parametrize('transport', ['p2p', 'xgmi'])
 def test_async_ps_hip_learners_one_gpu(transport):
     _run_ranks(_worker_async_ps, (transport,), world=3, timeout=150)
+
+
+def _worker_async_ps_pipelined(rank, world, port, errq):
+    _worker_async_ps(rank, world, port, 'xgmi', errq, pipeline=1)
+
+
+def test_async_ps_pipelined_hip_learners_one_gpu():
+    """--ps_pipeline=1 (xgmi): every push is still applied exactly once in arrival order, the server's
+    step counts them all, and the workers' parameters lag one answer behind."""
+    _run_ranks(_worker_async_ps_pipelined, (), world=3, timeout=150)
 
 
 class _QuiesceProbeSupervisor:
