@@ -260,11 +260,11 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     return;
   }
   if (tid == 0) {
-    // spin mode reads only the partial-Q slots of this launch, and those with agent-scope (sc1)
-    // loads after the counter add returned (the producers stored them sc1): no acquire fence, whose
-    // L1 invalidate costs ~1.7 us on this chain (MI355X_MICROARCH.md, coherence table). Otherwise
-    // the tail also reads the other blocks' h rows with plain loads: acquire first.
-    if (!f.spin || f.fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // acquire, then plain loads of the partial-Q slots (and, not spin, the other blocks' h rows).
+    // DQN_SC1_TAILS=1 (spin mode): no fence, the slots read with 16-byte sc1 loads after the counter
+    // add returned (the producers stored them sc1) -- measured 0.3-0.6 us SLOWER than the fence on
+    // this kernel (round 5, gpurun_out/r5v), so off by default
+    if (!f.spin || !f.sc1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(f.cnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -294,22 +294,26 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
     // Q rows: every (instance, row, column) sums its tiles' partial slots in tile order (dueling:
     // advantage columns over the advantage tiles, the value column over the value tiles), + bias
     const int NT = (int)gridDim.y, half = h.dueling ? NT / 2 : 0;
+    // the slots through a buffer descriptor: 16-byte sc1 loads (buffer_load_dwordx4 ... sc1) bypass
+    // this CU's L1 like the scalar agent-scope loads, at a quarter of their instructions (4-byte
+    // atomic loads cost the dueling fold ~4.6 us: round-5 trace, gpurun_out/r5u)
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+        f.qacc, (short)0, (int)(4 * (int64_t)(f.nlearn + 1) * f.Mpad * 32 * NT), 0x00020000);
+    typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
     if (tid < ni * 32) S.q[tid >> 5][16][tid & 31] = pb;          // (row 16: the bias row)
     for (int t = tid; t < ni * 16 * A1; t += kFoldThreads) {
       const int i = t / (16 * A1), rem = t - i * 16 * A1, r = rem / A1, c = rem - r * A1;
       float v = 0.f;
       if (r < nrows && (c < A || h.dueling)) {
-        const float* p = f.qacc + (((int64_t)(i0 + i) * f.Mpad + m_base + r) * 32 + c) * NT;
+        const int pb0 = 4 * (int)((((int64_t)(i0 + i) * f.Mpad + m_base + r) * 32 + c) * NT);   // byte offset
         const int lo = h.dueling ? (c < A ? half : 0) : 0, hi = h.dueling ? (c < A ? NT : half) : NT;
-        for (int u = lo; u < hi; u += 4) {        // (sc1 loads, in tile order)
-          const float x0 = __hip_atomic_load(p + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const float x1 = __hip_atomic_load(p + u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const float x2 = __hip_atomic_load(p + u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const float x3 = __hip_atomic_load(p + u + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          v += x0;
-          v += x1;
-          v += x2;
-          v += x3;
+        for (int u = lo; u < hi; u += 4) {        // (summed in tile order)
+          const float4 x = f.sc1 ? __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(qrs, pb0 + 4 * u, 0, 16))
+                                 : *reinterpret_cast<const float4*>(f.qacc + pb0 / 4 + u);
+          v += x.x;
+          v += x.y;
+          v += x.z;
+          v += x.w;
         }
       }
       S.q[i][r][c] = v;

@@ -475,6 +475,21 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         for (int j = 0; j < 4; ++j) v[j] = base[off + ix[j]];
       }
     };
+    // sc1 (L1-bypassing) loads of bytes other workgroups of this launch produced: 16 B per lane through
+    // a buffer descriptor where the 4 values are contiguous (one buffer_load_dwordx4 ... sc1), else 4 B each
+    auto sc1_ld = [&](const float* base, int64_t off, float* v) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
+                                                                          0x7ffffff0, 0x00020000);
+      if constexpr (AL) {
+        typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+        const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4 * (off + ix[0])), 0, 16));
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (off + ix[j])), 0, 16));
+      }
+    };
     auto st = [&](float* base, int64_t off, const float* v) {
       if constexpr (AL) {
         if (ok[0]) {
@@ -499,8 +514,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       if constexpr (UPD) {
         if constexpr (!DG) {
           if (gsc1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) gs[j] = __hip_atomic_load(G + so + ix[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sc1_ld(G, so, gs);
           } else {
             ld(G, so, gs);
           }
@@ -573,8 +587,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         }
       } else if (!fcj) {
         if (gsc1) {                                       // produced in this launch (see the dep wait)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) g[j] = __hip_atomic_load(G + mo + ix[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sc1_ld(G, mo, g);
         } else {
           ld(G, mo, g);
         }

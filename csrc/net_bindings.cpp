@@ -343,7 +343,7 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
     f.dq_epoch = P<int32_t*>(fold[5]);
     f.err = f.dq_epoch + f.ngroups + 1;       // the epoch buffer holds ngroups + 2 words
     f.dbg_no_publish = std::getenv("DQN_DEBUG_FOLD_NO_PUBLISH") != nullptr ? 1 : 0;
-    f.fence = std::getenv("DQN_FENCE_TAILS") != nullptr ? 1 : 0;
+    f.sc1 = std::getenv("DQN_SC1_TAILS") != nullptr ? 1 : 0;
   }
   if (fold.size() == 8 && fold[6] != 0) {      // zero duty (the step's dgrad-chain counters)
     TORCH_CHECK(fold[6] % 16 == 0 && fold[7] % 4 == 0, "fc_head: zero range 16-byte aligned, n % 4 == 0");
