@@ -307,13 +307,23 @@ __global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadA
       if (r < nrows && (c < A || h.dueling)) {
         const int pb0 = 4 * (int)((((int64_t)(i0 + i) * f.Mpad + m_base + r) * 32 + c) * NT);   // byte offset
         const int lo = h.dueling ? (c < A ? half : 0) : 0, hi = h.dueling ? (c < A ? NT : half) : NT;
-        for (int u = lo; u < hi; u += 4) {        // (summed in tile order)
-          const float4 x = f.sc1 ? __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(qrs, pb0 + 4 * u, 0, 16))
-                                 : *reinterpret_cast<const float4*>(f.qacc + pb0 / 4 + u);
-          v += x.x;
-          v += x.y;
-          v += x.z;
-          v += x.w;
+        if (f.sc1) {                              // (summed in tile order)
+          for (int u = lo; u < hi; u += 4) {
+            const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(qrs, pb0 + 4 * u, 0, 16));
+            v += x.x;
+            v += x.y;
+            v += x.z;
+            v += x.w;
+          }
+        } else {
+          const float* p = f.qacc + pb0 / 4;
+          for (int u = lo; u < hi; u += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(p + u);
+            v += x.x;
+            v += x.y;
+            v += x.z;
+            v += x.w;
+          }
         }
       }
       S.q[i][r][c] = v;
