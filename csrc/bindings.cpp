@@ -511,6 +511,26 @@ void ps_push(torch::Tensor grad, int64_t slot, int64_t push_word, torch::Tensor 
                  cur_stream());
 }
 
+// --ps_lowrank: the push as up to 6 pieces (raw device pointers, 16-byte aligned, lengths % 16 == 0)
+void ps_push_segs(std::vector<int64_t> src, std::vector<int64_t> dst, std::vector<int64_t> nbytes, int64_t push_word,
+                  torch::Tensor seq, int64_t kind, torch::Tensor ticket) {
+  CHECK_T(seq, torch::kInt64); CHECK_T(ticket, torch::kInt32);
+  TORCH_CHECK(src.size() == dst.size() && src.size() == nbytes.size() && push_word && kind >= 0 && kind < 16,
+              "ps_push_segs args");
+  std::vector<const void*> s(src.size());
+  std::vector<void*> d(dst.size());
+  std::vector<long> nb(nbytes.size());
+  for (size_t k = 0; k < src.size(); ++k) {
+    s[k] = reinterpret_cast<const void*>(src[k]);
+    d[k] = reinterpret_cast<void*>(dst[k]);
+    nb[k] = (long)nbytes[k];
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(seq.device());
+  TORCH_CHECK(launch_ps_push_segs(s.data(), d.data(), nb.data(), (int)src.size(), reinterpret_cast<uint64_t*>(push_word),
+                                  ptr<int64_t>(seq), (int)kind, ptr<int32_t>(ticket), cur_stream()) == 0,
+              "ps_push_segs: 1..6 pieces, 16-byte aligned, lengths % 16 == 0");
+}
+
 // seq: int64 [2] = (push number, gate number) device words of this worker
 void ps_pull(torch::Tensor flat, int64_t snap, torch::Tensor step, int64_t snap_step, int64_t done_word,
              torch::Tensor seq, torch::Tensor gate, torch::Tensor err, torch::Tensor stopped, int64_t timeout_ns) {
@@ -712,6 +732,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("host_unregister", &host_unregister);
   m.def("tensor_from_ptr", &tensor_from_ptr);
   m.def("ps_push", &ps_push);
+  m.def("ps_push_segs", &ps_push_segs);
   m.def("ps_pull", &ps_pull);
   m.def("ps_publish", &ps_publish, pybind11::arg("snap"), pybind11::arg("flat"), pybind11::arg("snap_step"),
         pybind11::arg("step"), pybind11::arg("done_word"), pybind11::arg("value"), pybind11::arg("ticket"),

@@ -126,6 +126,8 @@ int launch_xgmi_allgather(const dqn::XgmiGatherArgs& a, int blocks, hipStream_t 
 // Asynchronous parameter server over xGMI peer memory, csrc/kernels/async_ps.hip.
 void launch_ps_push(const float* grad, float* slot, long n, uint64_t* push_word, int64_t* seq, int kind,
                     int32_t* ticket, hipStream_t st);
+int launch_ps_push_segs(const void* const* src, void* const* dst, const long* nbytes, int n, uint64_t* push_word,
+                        int64_t* seq, int kind, int32_t* ticket, hipStream_t st);
 void launch_ps_pull(float* flat, const float* snap, long n, int64_t* step, const int64_t* snap_step,
                     const uint64_t* done_word, const int64_t* seq, int64_t* gate, int32_t* err, int32_t* stopped,
                     long long timeout_ns, hipStream_t st);

@@ -50,6 +50,41 @@ ps_push_kernel(const float4* __restrict__ grad, float4* __restrict__ slot, long 
   }
 }
 
+// Segmented push (--ps_lowrank): up to kPsSegs (src, dst, 16-byte-multiple length) pieces -- the flat
+// gradient outside the fc weight tensors, and the fc layer's factors (its input rows X and dL/dh rows,
+// rank <= B) written into the fc weight region of the slot -- then the push word as ps_push_kernel.
+constexpr int kPsSegs = 6;
+struct PsSegs {
+  const float4* src[kPsSegs];
+  float4* dst[kPsSegs];
+  long n4[kPsSegs];          // float4 vectors per piece
+  long start[kPsSegs + 1];   // prefix sums of n4
+  int n;
+};
+
+__global__ void __launch_bounds__(kPsThreads)
+ps_push_segs_kernel(PsSegs sg, uint64_t* push_word, int64_t* seq, int kind, int32_t* ticket) {
+  const long total = sg.start[sg.n];
+  for (long i = (long)blockIdx.x * kPsThreads + threadIdx.x; i < total; i += (long)gridDim.x * kPsThreads) {
+    int k = 0;
+    while (k + 1 < sg.n && i >= sg.start[k + 1]) ++k;
+    const long j = i - sg.start[k];
+    sg.dst[k][j] = sg.src[k][j];
+  }
+  __threadfence_system();                   // this thread's peer stores, before its block's arrival
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (int)gridDim.x - 1) {
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t s = seq[0] + 1;
+      seq[0] = s;
+      __threadfence_system();
+      st_release_sys(push_word, ((uint64_t)s << 4) | (uint64_t)kind);
+    }
+  }
+}
+
 // Wait for the PS's answer to push number seq[0] in ONE block (ps_wait_kernel), then copy the
 // snapshot -> flat (+ the global step) with the whole grid (ps_copy_kernel), in stream order. (A
 // single kernel whose every block spun on the answer kept ~512 spinning workgroups on the GPU for
@@ -142,4 +177,23 @@ void launch_ps_publish(float* snap, const float* flat, long n, int64_t* snap_ste
   hipLaunchKernelGGL(dqn::ps_publish_kernel, dim3(flat != nullptr ? dqn::ps_grid(n4) : 1), dim3(dqn::kPsThreads),
                      0, st, reinterpret_cast<float4*>(snap), reinterpret_cast<const float4*>(flat), n4, snap_step,
                      step, done_word, value, ticket, echo);
+}
+
+int launch_ps_push_segs(const void* const* src, void* const* dst, const long* nbytes, int n, uint64_t* push_word,
+                        int64_t* seq, int kind, int32_t* ticket, hipStream_t st) {
+  if (n < 1 || n > dqn::kPsSegs) return -1;
+  dqn::PsSegs sg{};
+  sg.n = n;
+  sg.start[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    if (nbytes[k] % 16 != 0 || (reinterpret_cast<uintptr_t>(src[k]) & 15) || (reinterpret_cast<uintptr_t>(dst[k]) & 15))
+      return -2;
+    sg.src[k] = reinterpret_cast<const float4*>(src[k]);
+    sg.dst[k] = reinterpret_cast<float4*>(dst[k]);
+    sg.n4[k] = nbytes[k] / 16;
+    sg.start[k + 1] = sg.start[k] + sg.n4[k];
+  }
+  hipLaunchKernelGGL(dqn::ps_push_segs_kernel, dim3(dqn::ps_grid(sg.start[n])), dim3(dqn::kPsThreads), 0, st, sg,
+                     push_word, seq, kind, ticket);
+  return 0;
 }

@@ -33,7 +33,10 @@ namespace dqn {
 constexpr int kFoldThreads = 512;
 constexpr int kFoldMaxA = 18;                  // Atari's full action set
 constexpr int kFoldMaxHid = 512;
-constexpr int kFoldU = DQN_ACT_F32 ? 7 : 13;   // k-steps per load batch (fp32: twice the VGPRs each)
+// k-steps per load batch (fp32: twice the VGPRs each). kFoldU1: one block per CU (the whole K slice of a
+// wave in one batch); kFoldU2: two blocks per CU (<= 128 VGPRs), for grids above the CU count -- the
+// dueling net's 2 x 64 x 3 = 384 blocks, which otherwise lost the spin mode (all blocks resident)
+constexpr int kFoldU1 = DQN_ACT_F32 ? 7 : 13, kFoldU2 = DQN_ACT_F32 ? 4 : 8;
 
 struct FoldLds {
   float red[7 * 256];                          // split-K partial tiles of waves 1..7
@@ -48,8 +51,8 @@ struct FoldLds {
   int timed_out;                               // dH-tile block: the dQ wait expired
 };
 
-template <int AT>
-__global__ void __launch_bounds__(kFoldThreads) fc_head_kernel(ConvArgs a, HeadArgs h, FoldArgs f) {
+template <int AT, int kFoldU>
+__global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_head_kernel(ConvArgs a, HeadArgs h, FoldArgs f) {
   __shared__ __attribute__((aligned(16))) FoldLds S;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int inst = blockIdx.z;
@@ -478,20 +481,28 @@ int launch_fc_head(const ConvArgs& a, const HeadArgs& h, const FoldArgs& f, hipS
       (f.nlearn != 2 && f.nlearn != 3) || ninst > kMaxInst)
     return -1;
   const dim3 grid((a.M + 15) / 16, a.N / 16, ninst);
-  // spin mode needs every block resident at once (2 per CU by LDS): one per CU, conservatively
+  // spin mode needs every block resident at once: one per CU with the one-batch k-loop, two per CU
+  // (LDS 58 KB, <= 128 VGPRs) with the two-batch variant; beyond that the tails write the whole dH
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   }
-  if (f.spin && (int)(grid.x * grid.y * grid.z) > cus) {
+  const int nblk = (int)(grid.x * grid.y * grid.z);
+  static const bool two_ok = getenv("DQN_FOLD_TWO_PER_CU") == nullptr || atoi(getenv("DQN_FOLD_TWO_PER_CU")) != 0;
+  const bool two = two_ok && nblk > cus && nblk <= 2 * cus;
+  if (f.spin && nblk > (two ? 2 * cus : cus)) {
     FoldArgs g = f;
     g.spin = 0;
     return launch_fc_head(a, h, g, st);
   }
   if (f.spin && (f.dqg == nullptr || f.dq_epoch == nullptr)) return -1;
-#define FOLD(AT) hipLaunchKernelGGL(fc_head_kernel<AT>, grid, dim3(kFoldThreads), 0, st, a, h, f)
+#define FOLD(AT)                                                                                             \
+  do {                                                                                                      \
+    if (two) hipLaunchKernelGGL((fc_head_kernel<AT, kFoldU2>), grid, dim3(kFoldThreads), 0, st, a, h, f);   \
+    else hipLaunchKernelGGL((fc_head_kernel<AT, kFoldU1>), grid, dim3(kFoldThreads), 0, st, a, h, f);       \
+  } while (0)
   switch (h.A) {
     case 2: FOLD(2); break;
     case 3: FOLD(3); break;

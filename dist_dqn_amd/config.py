@@ -213,6 +213,9 @@ def build_parser() -> argparse.ArgumentParser:
       help='async PS over xGMI: 1 = a worker takes the PS answer to its PREVIOUS push, then pushes this '
            'step\'s gradient and goes on (one more step of staleness, within the reference\'s Hogwild '
            'semantics; no per-step round trip to the server); 0 = push, then wait for this push\'s answer')
+    a('--ps_lowrank', default=1, type=int,
+      help='async PS over xGMI: push the fc weight gradient as its factors (fc input rows + dL/dh rows, rank '
+           '<= B; the server forms it in its fused optimizer launch) instead of the 6.4 MB gradient')
     a('--ps_transport', default='auto', choices=['auto', 'p2p', 'xgmi'],
       help='--async_ps transport: one-sided xGMI peer memory (GPU; replicated targets) or '
            'torch.distributed point-to-point; auto = xgmi when available')
@@ -321,6 +324,7 @@ class Config:
     async_ps: bool = False
     ps_transport: str = 'auto'
     ps_pipeline: int = 0
+    ps_lowrank: int = 1
     max_train_steps: int = 0
     allreduce_check_steps: int = 1000
     stop_sync_steps: int = 10

@@ -125,6 +125,14 @@ class Learner:
                 self._ar_ranges = ranges
         if self.ctx.enabled and self._lowrank is None:
             self._defer_fc = False         # (an all-reduced fc gradient must exist in the flat buffer)
+        # async PS over xgmi (--ps_lowrank): the fc gradient is pushed as its factors (the server forms
+        # it in its fused optimizer launch); the plan is the server's too (same config, same net)
+        self._ps_lowrank = None
+        if ps_client is not None and hasattr(ps_client, 'lowrank'):
+            from .parallel.async_ps import ps_lowrank_plan
+            ps_client.lowrank = self._ps_lowrank = ps_lowrank_plan(network, config)
+            if self._ps_lowrank is not None:
+                self._defer_fc = True
         # conv weight gradients as deterministic chunk-group partials summed inside the fused
         # optimizer launch (executor.can_det_wgrad): one process only (DP all-reduces the flat
         # gradient, whose conv range then must hold the sums)
@@ -326,9 +334,19 @@ class Learner:
         return (self.ps is not None and getattr(self.ps, 'in_graph', False)
                 and not bool(self.config.disable_target_replication))
 
+    def _ps_fc_rows(self):
+        """Low-rank push: the deferred fc gradient's factor rows (taken off the executor: no local
+        optimizer step consumes them)."""
+        if self._ps_lowrank is None:
+            return None
+        ex = self.net.executor
+        fc, ex._fc_pending = ex._fc_pending, None
+        assert fc is not None, 'low-rank push: compute_grads(defer_fc=True) left no fc rows'
+        return fc[0], fc[1]
+
     def _ps_exchange_kernels(self):
         """The graph-capturable part of the exchange: push + pull launches, then the repack."""
-        self.ps.exchange_kernels(self.net.grad, self.net.online.flat, self.net.global_step)
+        self.ps.exchange_kernels(self.net.grad, self.net.online.flat, self.net.global_step, self._ps_fc_rows())
         self.net._repack()
 
     def _ps_after_graph(self):
@@ -349,8 +367,9 @@ class Learner:
         own = bool(self.config.disable_target_replication)
         due = self.tau >= 1.0 and (self.train_steps + 1) % max(1, self.config.target_update_freq) == 0
         with trace('ps.exchange'):
+            kw = {'fc_rows': self._ps_fc_rows()} if self._ps_lowrank is not None else {}
             ok = self.ps.exchange(self.net.grad, self.net.online.flat, self.net.global_step,
-                                  sync_target=own and due, target=self.net.target.flat if own else None)
+                                  sync_target=own and due, target=self.net.target.flat if own else None, **kw)
         if not ok:
             return
         self.net._repack()

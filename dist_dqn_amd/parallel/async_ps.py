@@ -224,6 +224,43 @@ _BYE = 15                             # push kind: the worker leaves
 _STOP_STATUS = 1                      # done status: the PS stopped
 
 
+def ps_lowrank_plan(network, config) -> Optional[dict]:
+    """--ps_lowrank (xgmi transport): the fc weight gradient travels as its factors -- the fc input
+    rows X [B][F] and the dL/dh rows [B][HH] (act_t), rank <= B -- written into the slot where the
+    fc weight gradient would be, instead of the 6.4 MB gradient (Nature, B = 32: ~0.56 MB pushed in all
+    with the rest of the flat gradient). The server's fused optimizer launch forms dW = X^T dH from
+    them (the single-process learner's FcFuse path), so the update is the same arithmetic. The same
+    plan on every rank (decided from the config and the architecture). None when not applicable
+    (noisy / distributional heads, B > 32, no fused fc path in this build)."""
+    if not int(getattr(config, 'ps_lowrank', 1)):
+        return None
+    ex = network.executor
+    B = int(config.minibatch_size)
+    if (not hasattr(ex, 'can_defer_fc') or getattr(ex, 'noisy', False) or getattr(ex, 'dist', False)
+            or not ex.can_defer_fc(B, True) or not hasattr(ex, 'update_and_pack')):
+        return None
+    lay = network.layout
+    holes = sorted((lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in lay.names if n.endswith('fcl/w'))
+    if not holes:
+        return None
+    esz = 2                                                   # act_t rows (16-bit builds: FcFuse)
+    xbytes = B * int(ex.FLAT) * esz
+    dbytes = B * int(ex.HH) * esz
+    if xbytes % 16 or dbytes % 16 or 4 * (holes[0][1] - holes[0][0]) < xbytes + dbytes:
+        return None
+    keep, lo = [], 0                                          # the flat ranges outside the fc weights
+    for a, b in holes:
+        if a > lo:
+            keep.append((lo, a))
+        lo = b
+    if lo < lay.total:
+        keep.append((lo, lay.total))
+    if len(keep) + 2 > 6 or any((b - a) % 4 for a, b in keep):
+        return None
+    return {'B': B, 'keep': keep, 'x_off': 4 * holes[0][0], 'dh_off': 4 * holes[0][0] + xbytes,
+            'xbytes': xbytes, 'dbytes': dbytes}
+
+
 class _PSShared:
     """Rank 0's fine-grained HBM region ([W-1] gradient slots, [W-1] parameter snapshots, [W-1]
     int64 step words) exported over IPC, and the shared host control page, mapped by every rank."""
@@ -332,6 +369,7 @@ class XgmiPSServer:
         assert not getattr(network.config, 'disable_target_replication', False), \
             'the xgmi PS transport keeps replicated targets (use --ps_transport=p2p)'
         self.ctx, self.net = ctx, network
+        self.lowrank = ps_lowrank_plan(network, network.config)
         self.n = network.online.flat.numel()
         self.sh = shared or _PSShared(ctx, self.n)
         self.workers = list(range(1, ctx.world_size))
@@ -342,6 +380,18 @@ class XgmiPSServer:
         self.per_worker = {w: 0 for w in self.workers}
         self.stopped_workers = 0
         self.busy_s = 0.0
+
+    def _apply(self, w: int):
+        """Arrival-order update from worker w's slot, read in place (no repack: the server never runs
+        the network). Low-rank pushes: the fused optimizer launch forms the fc gradient from the
+        factors in the slot."""
+        net = self.net
+        if self.lowrank is None:
+            net.apply_grads(1.0, grad=self._grads[w], repack=False)
+            return
+        base, lr = self.sh.slot(w), self.lowrank
+        net.executor.update_and_pack(net.optimizer, net.online.flat, self._grads[w], 1.0, net.global_step,
+                                     fc=(base + lr['x_off'], base + lr['dh_off'], lr['B']))
 
     def _publish(self, w: int, seq: int, status: int = 0):
         st = status == 0
@@ -381,7 +431,7 @@ class XgmiPSServer:
                     self.stopped_workers += 1
                     continue
                 # arrival-order apply, the gradient read in place from the worker's slot
-                self.net.apply_grads(1.0, grad=self._grads[w], repack=False)
+                self._apply(w)
                 self._publish(w, s)
                 self.updates += 1
                 self.per_worker[w] += 1
@@ -410,7 +460,7 @@ class XgmiPSServer:
                     # arrival-order apply, the gradient read in place from worker w's slot (no
                     # repack: the server never runs the network); the answer's push number comes
                     # from w's push word (the kernel echoes it)
-                    net.apply_grads(1.0, grad=self._grads[w], repack=False)
+                    self._apply(w)
                     ext.ps_publish(sh.snap(w), net.online.flat, sh.snap_step(w), net.global_step, sh.done_word(w), 0,
                                    self._ticket, self.n, echo=sh.push_word(w))
                 with torch.cuda.graph(gs, stream=s, capture_error_mode='thread_local'):
@@ -470,7 +520,7 @@ class XgmiPSClient:
     transport = 'xgmi'
 
     def __init__(self, ctx: DistContext, flat: torch.Tensor, shared: Optional[_PSShared] = None,
-                 timeout_s: float = 60.0, pipeline: bool = False):
+                 timeout_s: float = 60.0, pipeline: bool = False, lowrank: Optional[dict] = None):
         assert ctx.enabled and ctx.rank >= 1
         self.ctx, self.w = ctx, ctx.rank
         self.n = flat.numel()
@@ -489,6 +539,7 @@ class XgmiPSClient:
         # pipelined exchange (--ps_pipeline): take the answer to the previous push, then push; the
         # server answered it while this worker computed the gradient, so the wait is usually over
         self.pipeline = bool(pipeline)
+        self.lowrank = lowrank                # ps_lowrank_plan: push the fc factors, not the fc gradient
 
     @property
     def stopped(self) -> bool:
@@ -504,27 +555,41 @@ class XgmiPSClient:
         self._pull(flat, global_step)
 
     def exchange(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None,
-                 sync_target: bool = False, target: Optional[torch.Tensor] = None) -> bool:
+                 sync_target: bool = False, target: Optional[torch.Tensor] = None, fc_rows=None) -> bool:
         if self.stopped:
             return False
-        self.exchange_kernels(grad, flat, global_step)
+        self.exchange_kernels(grad, flat, global_step, fc_rows)
         self.pushes += 1
         return True
 
     # the push / pull launches keep their sequence numbers on the device: a captured graph replays them
     in_graph = True
 
-    def exchange_kernels(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
+    def exchange_kernels(self, grad: torch.Tensor, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None,
+                         fc_rows=None):
         '''The exchange's launches only (graph-capturable; after a STOP answer the pull copies nothing
-        and the push lands in a slot the server no longer reads).'''
+        and the push lands in a slot the server no longer reads). fc_rows (low-rank push): device
+        pointers (X rows, dL/dh rows) of the deferred fc gradient.'''
         if self.pipeline:
             # answer to push k-1 -> parameters (this step's gradient is computed already: stream
             # order), then push k into the slot the server has finished reading (it answered k-1)
             self._pull(flat, global_step)
-            self.sh.ext.ps_push(grad, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
+            self._push(grad, fc_rows)
         else:
-            self.sh.ext.ps_push(grad, self.sh.slot(self.w), self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
+            self._push(grad, fc_rows)
             self._pull(flat, global_step)
+
+    def _push(self, grad, fc_rows):
+        slot = self.sh.slot(self.w)
+        if self.lowrank is None:
+            self.sh.ext.ps_push(grad, slot, self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
+            return
+        assert fc_rows is not None, 'low-rank push: the learner defers the fc gradient'
+        lr, g = self.lowrank, grad.data_ptr()
+        src = [g + 4 * a for a, _ in lr['keep']] + [int(fc_rows[0]), int(fc_rows[1])]
+        dst = [slot + 4 * a for a, _ in lr['keep']] + [slot + lr['x_off'], slot + lr['dh_off']]
+        nb = [4 * (b - a) for a, b in lr['keep']] + [lr['xbytes'], lr['dbytes']]
+        self.sh.ext.ps_push_segs(src, dst, nb, self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
 
     def flush(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
         '''Pipelined exchange: take the answer to the last push (the parameters after it).'''
@@ -564,11 +629,12 @@ def make_ps_server(ctx: DistContext, network, config):
     return AsyncPSServer(ctx, network)
 
 
-def make_ps_client(ctx: DistContext, flat: torch.Tensor, config):
+def make_ps_client(ctx: DistContext, flat: torch.Tensor, config, network=None):
     if ps_transport(ctx, config) == 'xgmi':
         try:
             return XgmiPSClient(ctx, flat, timeout_s=float(getattr(config, 'ps_timeout_s', 60.0)),
-                                pipeline=bool(getattr(config, 'ps_pipeline', 0)))
+                                pipeline=bool(getattr(config, 'ps_pipeline', 0)),
+                                lowrank=ps_lowrank_plan(network, config) if network is not None else None)
         except RuntimeError as e:
             log.warning('async PS over xgmi unavailable (%s): torch.distributed p2p instead', e)
     return AsyncPSClient(ctx, flat)
