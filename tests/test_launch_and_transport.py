@@ -189,3 +189,48 @@ def test_failed_gather_self_test_keeps_allreduce_but_no_gather(monkeypatch, fake
     _FakeXgmi.gather_ok = False
     r = _reducer(monkeypatch, t_x=10.0, t_r=20.0, gather_bytes=4096)
     assert isinstance(r._setup_xgmi('auto'), _FakeXgmi) and not r.can_gather
+
+
+# ------------------------------------------------------------------ async PS low-rank push plan
+class _StubEx:
+    FLAT, HH, noisy, dist = 3136, 512, False, False
+
+    def __init__(self, HH=512):
+        self.HH = HH
+
+    def can_defer_fc(self, B, sigma_grads=False):
+        return B <= 32
+
+    def update_and_pack(self, *a, **k):
+        pass
+
+
+@pytest.mark.parametrize('dueling', [False, True])
+def test_ps_lowrank_plan_pushes_everything_but_the_fc_weights(dueling):
+    """--ps_lowrank: the pushed pieces cover the flat buffer outside the fc weight tensors exactly,
+    and the fc factor rows (X [B][3136], dL/dh [B][HH], 16-bit) fit where the first fc weight
+    gradient would be."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.parallel.async_ps import ps_lowrank_plan
+    cfg = preset('nature', 'Pong-v0', '--device=cpu --backend=torch --async_ps' + (' --dueling' if dueling else ''))
+    net = Network.create_network(cfg, (84, 84, 4), 6)
+    net.executor = _StubEx(1024 if dueling else 512)
+    plan = ps_lowrank_plan(net, cfg)
+    lay = net.layout
+    fcw = [(lay.offsets[n], lay.offsets[n] + lay.numel(n)) for n in lay.names if n.endswith('fcl/w')]
+    covered = sorted(plan['keep'] + fcw)
+    assert covered[0][0] == 0 and covered[-1][1] == lay.total
+    assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))          # no gap, no overlap
+    B = cfg.minibatch_size
+    assert plan['x_off'] == 4 * fcw[0][0] and plan['xbytes'] == B * 3136 * 2
+    assert plan['dh_off'] == plan['x_off'] + plan['xbytes'] and plan['dbytes'] == B * (1024 if dueling else 512) * 2
+    assert plan['dh_off'] + plan['dbytes'] <= 4 * fcw[0][1]
+    pushed = sum(4 * (b - a) for a, b in plan['keep']) + plan['xbytes'] + plan['dbytes']
+    assert pushed < 4 * lay.total / 8                       # > 8x fewer bytes than the full gradient
+    # not applicable: flag off, noisy heads, minibatch beyond the fused path
+    assert ps_lowrank_plan(net, cfg.replace(ps_lowrank=0)) is None
+    net.executor.noisy = True
+    assert ps_lowrank_plan(net, cfg) is None
+    net.executor.noisy = False
+    assert ps_lowrank_plan(net, cfg.replace(minibatch_size=64)) is None
