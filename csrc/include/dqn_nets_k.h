@@ -52,6 +52,11 @@ struct ConvArgs {
   // data parallelism, low-rank exchange: the blocks of grid.z == gth_z run the xgmi all-gather of
   // the fc factors (the first gth_blocks of them; args: a device XgmiGatherArgs) beside the GEMM
   const void* gth; int gth_blocks, gth_z;
+  // noisy nets, factorised target fc forward (fz_w2 != null; dense forward kind only): instance
+  // fz_inst computes relu(scale * (X Wmu + f(eps_out) * ((X * f(eps_in)) Wsigma)) + bias) from the
+  // mu fragments in w[fz_inst] and the sigma fragments in fz_w2 (f(x) = sgn(x) sqrt|x|; eps from
+  // fz_noise, column halves [0, fz_nsplit) / [fz_nsplit, N) with their own eps_in / eps_out offsets)
+  const void* fz_w2; const float* fz_noise; int fz_inst, fz_nsplit; int fz_ein[2], fz_eout[2];
 };
 
 struct WgradArgs {
@@ -240,6 +245,7 @@ struct WgradGroup {
   // tile runs once that slot's gradient is complete (a contiguous range of the launch's job table)
   int32_t* done;
   int slots_member;
+  int prefetch;              // fused tiles: both chunks' loads issued up front (DQN_WG_PREFETCH, default 1)
   int dep_first[kMaxWgradMembers][16 + 1], dep_count[kMaxWgradMembers][16 + 1];
 };
 constexpr int kWgSlots = 16 + 1;            // K-ranges (<= 16) + the bias

@@ -22,6 +22,10 @@ struct OptHP {
   float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
   int reg_end;
   int dep_fence;             // A/B knob (DQN_FENCE_TAILS=1): dependent jobs acquire-fence + plain loads
+  // noisy nets, factorised target fc (UpdJob.eff bit 1): the target's packed fc weights hold mu
+  // fragments and this buffer (the packed layout) its sigma fragments, written only when they change
+  // (a sync step, or a mix-only call on the target); the target forward mixes the noise in itself
+  void* tsg;
   // probe launches only (DQN_OPT_PROF=1, nullptr otherwise): [0, 16) s_memtime phase stamps of
   // blocks 0 and 1, then per block [start, ready, end] s_memrealtime (100 MHz) for blocks < kTlBlocks
   // (ready: a dependent job's wait is over / the sampler's draw is done)
@@ -138,7 +142,8 @@ struct UpdJob {
   // and the packed / eff values are mu + sigma * f(noise[ein + k]) f(noise[eout + n])
   // (ein < 0: f = 1, biases; elem chunks: eout already offset to the chunk start)
   int sig_off, ein_off, eout_off;
-  int eff;                       // 1: also store the effective fp32 value at eff[src index]
+  int eff;                       // bit 0: also store the effective fp32 value at eff[src index];
+                                 // bit 1: factorised target tile (OptHP.tsg), no per-step target mix
   // fc weight tile / fc bias chunk whose gradient the launch forms from FcFuse rows: the
   // tensor's first column in dH (-1: read the flat gradient)
   int fc_col;
@@ -504,6 +509,10 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
     };
     const int64_t mo = jb.src_off, so = NZ ? jb.sig_off : jb.src_off;
+    // factorised target tile: the target's mu / sigma fragments only change at a sync (or in a
+    // mix-only call on the target itself), so no per-step target loads / mix / pack for it
+    const bool tfj = NZ && !elem && (jb.eff & 2) != 0 && h.tsg != nullptr;
+    const bool tmj = tmix && !tfj;
     float w[4], a[4], b[4], ws[4], gs[4], as[4], bs[4], tw[4], tws[4], e[4], te[4];
     // ---- every load of the item, issued before any math
     ld(W, mo, w);
@@ -525,7 +534,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     // the target's mu / sigma in the same batch (one memory round trip per item: the extra
     // VGPRs keep the same 2 blocks / CU, the block is 8 waves and the budget 128 VGPRs)
-    if (tmix) {
+    if (tmj) {
       ld(tgt, mo, tw);
       if constexpr (NZ) ld(tgt, so, tws);
     }
@@ -551,13 +560,13 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       for (int j = 0; j < 4; ++j) {
         const int oi = jb.eout_off + (ok[j] ? n + j : 0);
         no[j] = noise[oi]; go[j] = DG ? gn[oi] : 1.f;
-        if (tmix) to[j] = tnoise[oi];
+        if (tmj) to[j] = tnoise[oi];
       }
-      if (tmix) ti = tnoise[hin ? ki : 0];
+      if (tmj) ti = tnoise[hin ? ki : 0];
       if (hin) { nin = fnz(ni); gin = fnz(gi); }
 #pragma unroll
       for (int j = 0; j < 4; ++j) { nout[j] = fnz(no[j]); gout[j] = fnz(go[j]); }
-      if (tmix) {
+      if (tmj) {
         if (hin) tin = fnz(ti);
 #pragma unroll
         for (int j = 0; j < 4; ++j) tout[j] = fnz(to[j]);
@@ -617,18 +626,18 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       e[j] = w[j];
-      if constexpr (NZ) e[j] = w[j] + ws[j] * nin * nout[j];
-    }
-    if (tmix) {
+      if constexpr (NZ) e[j] = (tfj && !UPD) ? w[j] : w[j] + ws[j] * nin * nout[j];   // (mix-only on a
+    }                                                     //  factorised target: mu fragments)
+    if (tmj) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float mu = sync ? w[j] : tw[j];
         te[j] = mu;
         if constexpr (NZ) te[j] = mu + (sync ? ws[j] : tws[j]) * tin * tout[j];
       }
-      if (jb.eff) st(teff, mo, te);
+      if (jb.eff & 1) st(teff, mo, te);
     }
-    if (jb.eff) st(eff, mo, e);
+    if (jb.eff & 1) st(eff, mo, e);
     if (elem) {
       if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
         float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
@@ -679,7 +688,20 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     };
     OPT_MARK(7);
     emit(e, packed, psync ? tgt_packed : nullptr, true);
-    if (tmix) emit(te, tpk, nullptr, false);              // (the target runs forward only)
+    if (tmj) emit(te, tpk, nullptr, false);               // (the target runs forward only)
+    if constexpr (NZ) {
+      if (tfj) {
+        act_t* sg = reinterpret_cast<act_t*>(h.tsg);
+        if constexpr (UPD) {
+          if (tmix && sync) {                             // the target just became this mu / sigma
+            emit(w, tpk, nullptr, false);
+            emit(ws, sg, nullptr, false);
+          }
+        } else {
+          emit(ws, sg, nullptr, false);                   // (mix-only: `packed` got the mu fragments)
+        }
+      }
+    }
   };
   using T_ = std::true_type;
   using F_ = std::false_type;

@@ -94,10 +94,18 @@ DQN_DEV void store_wt(act_t* p, act_t v, int lane) {
 // Body of one block (bx, by, bz) of a virtual (gx, gy, gz) GEMM grid: shared by igemm_kernel and
 // the chained dgrad launch (dgrad_chain.hip). WT: the EPI 2 output leaves as write-through 32-bit
 // stores (agent scope: another block of the same launch reads it after a counter).
-template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U = 4, bool WT = false>
-DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int gy, int gz) {
+// FZ: the factorised noisy forward of ConvArgs.fz_* (a second accumulator over the sigma fragments
+// with the A fragments scaled by f(eps_in), staged in LDS; f(eps_out) joins in the epilogue).
+// dblk / dnblk (>= 0 / > 0): this block's index / the block count for the side duties when the
+// launch's grid is not the (gx, gy, gz) of this body (fc_fwd_fz_kernel)
+constexpr int kFzMaxK = 4096;
+template <class LD, int MT, int NT, int WM, int WN, int KSPLIT, int EPI, int U = 4, bool WT = false, bool FZ = false>
+DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int gy, int gz, int dblk = -1,
+                        int dnblk = 0) {
   static_assert(WM * WN * KSPLIT == 4 || WM * WN * KSPLIT == 8, "4 or 8 waves per block");
-  __shared__ float red[KSPLIT > 1 ? WM * WN * (KSPLIT - 1) * MT * NT * 256 : 1];
+  static_assert(!FZ || (EPI == 0 && WM * WN == 1), "factorised forward: dense forward tiles");
+  __shared__ float red[KSPLIT > 1 ? (FZ ? 2 : 1) * WM * WN * (KSPLIT - 1) * MT * NT * 256 : 1];
+  __shared__ float fin_s[FZ ? kFzMaxK : 1];
   const int inst = bz;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wk = wave % KSPLIT, wn = (wave / KSPLIT) % WN, wm = wave / (KSPLIT * WN);
@@ -106,11 +114,17 @@ DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int g
   const int K32 = (a.K + 31) / 32;
   const bfx8* __restrict__ Bp = reinterpret_cast<const bfx8*>(a.w[inst]);
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[MT][NT], acc2[FZ ? MT : 1][FZ ? NT : 1];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) {
+      acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (FZ) acc2[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  // FZ: the block's column half (its eps_in / eps_out segment; nsplit % 16 == 0, NT == 1)
+  const int fzh = FZ && nt_base * 16 >= a.fz_nsplit ? 1 : 0;
+  const bfx8* __restrict__ Bp2 = reinterpret_cast<const bfx8*>(FZ ? a.fz_w2 : nullptr);
 
   // each lane owns row (lane & 15) of every m-tile and k-group (lane >> 4)
   LD ld[MT];
@@ -142,26 +156,62 @@ DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int g
   // predicated (zero fragments) instead of falling back to one step at a time;
   // a U that covers the wave's whole K range pays the load latency once.
   for (int ks = ks_lo; ks < ks_hi; ks += U) {
-    bfx8 af[U][MT], bf[U][NT];
+    bfx8 af[U][MT], bf[U][NT], bf2[FZ ? U : 1][FZ ? NT : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool kok = ks + u < ks_hi;
 #pragma unroll
       for (int i = 0; i < MT; ++i) af[u][i] = kok ? ld[i].frag((ks + u) * 32 + kg) : zero8();
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bf[u][j] = kok ? Bp[((int64_t)(ks + u) * a.N16 + nt_base + j) * 64 + lane] : zero8();
+      for (int j = 0; j < NT; ++j) {
+        const int64_t bo = ((int64_t)(ks + u) * a.N16 + nt_base + j) * 64 + lane;
+        bf[u][j] = kok ? Bp[bo] : zero8();
+        if constexpr (FZ) bf2[u][j] = kok ? Bp2[bo] : zero8();
+      }
+    }
+    if constexpr (FZ) {
+      // f(eps_in) of the whole K into LDS while the fragments above are in flight (every wave
+      // has exactly one first batch: the host checks K32 >= KSPLIT); [K, K32 * 32) = 0
+      if (ks == ks_lo) {
+        const float* ein = a.fz_noise + a.fz_ein[fzh];
+        for (int k = (int)threadIdx.x; k < K32 * 32; k += (int)blockDim.x) {
+          const float x = k < a.K ? ein[k] : 0.f;
+          fin_s[k] = copysignf(sqrtf(fabsf(x)), x);
+        }
+        __syncthreads();
+      }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      float fv[8];
+      if constexpr (FZ) {
+        // (a batch step past the wave's range reads the first k-step: its A fragment is zero, and
+        //  LDS past the staged K could hold NaN patterns)
+        const int kf = (ks + u < ks_hi ? ks + u : ks_lo) * 32 + kg;
+        const float4 f0 = *reinterpret_cast<const float4*>(fin_s + kf);
+        const float4 f1 = *reinterpret_cast<const float4*>(fin_s + kf + 4);
+        fv[0] = f0.x; fv[1] = f0.y; fv[2] = f0.z; fv[3] = f0.w; fv[4] = f1.x; fv[5] = f1.y; fv[6] = f1.z; fv[7] = f1.w;
+      }
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MT; ++i) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[u][i], bf[u][j], acc[i][j]);
+        if constexpr (FZ) {
+          bfx8 as;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) as[q] = (act_t)((float)af[u][i][q] * fv[q]);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc2[i][j] = mfma16(as, bf2[u][j], acc2[i][j]);
+        }
+      }
+    }
   }
+  // side-duty block index / count (GEMM blocks only)
+  const int dn = dnblk > 0 ? dnblk : gx * gy * gz;
+  const int db = dnblk > 0 ? dblk : (bz * gy + by) * gx + bx;
   // noise duty (every thread of the block, before the split-K waves retire)
   if (a.nz_out0 != nullptr) {
-    const int nblk = gx * gy * gz;                                  // (GEMM blocks only)
-    const int blk = (bz * gy + by) * gx + bx;
+    const int nblk = dn, blk = db;
     const int nq = ((a.nz_out1 != nullptr ? 2 : 1) * a.nz_n + 3) / 4;
     const int nt = blockDim.x, tq = (int)threadIdx.x;
     const uint64_t seed = (uint64_t)a.nz_rng[0], ctr = (uint64_t)a.nz_rng[1];
@@ -170,14 +220,17 @@ DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int g
   if constexpr (KSPLIT > 1) {
     // waves wk > 0 hand partial tiles to wk == 0 through LDS
     const int slot = ((wm * WN + wn) * (KSPLIT - 1));
+    constexpr int kHalf = WM * WN * (KSPLIT - 1) * MT * NT * 256;     // (FZ: acc2 partials after acc's)
     if (wk > 0) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+          for (int r = 0; r < 4; ++r) {
             red[(((slot + wk - 1) * MT + i) * NT + j) * 256 + r * 64 + lane] = acc[i][j][r];
+            if constexpr (FZ) red[kHalf + (((slot + wk - 1) * MT + i) * NT + j) * 256 + r * 64 + lane] = acc2[i][j][r];
+          }
     }
     __syncthreads();
     if (wk != 0) return;
@@ -188,17 +241,19 @@ DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int g
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += red[(((slot + s) * MT + i) * NT + j) * 256 + r * 64 + lane];
+          for (int r = 0; r < 4; ++r) {
+            acc[i][j][r] += red[(((slot + s) * MT + i) * NT + j) * 256 + r * 64 + lane];
+            if constexpr (FZ) acc2[i][j][r] += red[kHalf + (((slot + s) * MT + i) * NT + j) * 256 + r * 64 + lane];
+          }
   }
   // side duties of the launch (ConvArgs aux): zero a gradient range (the conv weight gradients
   // accumulate into it with atomics later in the step) and sum the head's per-tile loss partials
   if (a.zero_ptr != nullptr) {
-    const int nblk = gx * gy * gz;                                  // (GEMM blocks only)
-    const int blk = (bz * gy + by) * gx + bx;
+    const int nblk = dn, blk = db;
     float4* z4 = reinterpret_cast<float4*>(a.zero_ptr);
     for (int t = blk * 64 + lane; t < a.zero_n / 4; t += nblk * 64) z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (a.loss_parts != nullptr && bx == 0 && by == 0 && bz == 0) {
+  if (a.loss_parts != nullptr && db == 0) {
     const float v = lane < a.nparts ? a.loss_parts[lane] : 0.f;
     const float sl = wave_sum(v);
     if (lane == 0) a.loss_out[0] = sl * a.loss_mul;
@@ -211,6 +266,11 @@ DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int g
     const int n = (nt_base + j) * 16 + (lane & 15);
     if (n >= a.N) continue;
     const float bv = (EPI == 2 || bias == nullptr) ? 0.f : bias[n];
+    float fo = 0.f;                                                 // FZ: f(eps_out[n])
+    if constexpr (FZ) {
+      const float x = a.fz_noise[a.fz_eout[fzh] + n - (fzh ? a.fz_nsplit : 0)];
+      fo = copysignf(sqrtf(fabsf(x)), x);
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -218,6 +278,7 @@ DQN_DEV void igemm_body(const ConvArgs& a, int bx, int by, int bz, int gx, int g
         const int m = m_base + i * 16 + 4 * (lane >> 4) + r;
         if (m >= a.M) continue;
         float v = acc[i][j][r];
+        if constexpr (FZ) v += fo * acc2[i][j][r];
         const int64_t o = (int64_t)m * a.ldo + n;
         if constexpr (EPI == 0) {
           v = fmaxf(v * scale + bv, 0.f);
@@ -246,6 +307,23 @@ __global__ void __launch_bounds__(512) igemm_kernel(ConvArgs a) {
   }
   igemm_body<LD, MT, NT, WM, WN, KSPLIT, EPI, U>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y,
                                                  gridDim.z - (a.gth != nullptr ? 1 : 0));
+}
+
+// Dense forward with a factorised noisy instance (ConvArgs.fz_*): grid (2, N/16, ninst). The
+// factorised instance runs 16-row blocks (bx = row block: its blocks stream two B operands, so half
+// the A rows keep their L2->CU bytes at the plain blocks'), every other instance the 32-row tiles
+// of L_DENSE_FWD_RELU on bx == 0 (bx == 1 exits). Side duties over the active blocks.
+template <int U>
+__global__ void __launch_bounds__(512) fc_fwd_fz_kernel(ConvArgs a) {
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z, gy = gridDim.y, gz = gridDim.z;
+  const int nact = gy * (gz + 1);
+  if (bz == a.fz_inst) {
+    igemm_body<DenseLoader, 1, 1, 1, 1, 8, 0, U, false, true>(a, bx, by, bz, 2, gy, gz, gy * (gz - 1) + by * 2 + bx,
+                                                             nact);
+  } else if (bx == 0) {
+    igemm_body<DenseLoader, 2, 1, 1, 1, 8, 0, U>(a, 0, by, bz, 1, gy, gz, (bz - (bz > a.fz_inst ? 1 : 0)) * gy + by,
+                                                 nact);
+  }
 }
 
 // ===================================================== stride-2 dgrad by parity
@@ -1122,6 +1200,11 @@ int launch_igemm(int kind, const ConvArgs& a, int ninst, hipStream_t st) {
     // K 3136 = 98 k-steps, split-K 8: one 13-step load batch per wave; 16-row blocks so the
     // B=32 step spreads over 2x the CUs (each block's L2->CU bytes are the bound, not MFMA)
     case L_DENSE_FWD_RELU:
+      if (a.fz_w2 != nullptr) {     // factorised noisy instance (host-checked: M <= 32, N % 16 == 0)
+        if (a.gth != nullptr || a.M > 32 || a.fz_inst < 0 || a.fz_inst >= ninst) return -2;
+        hipLaunchKernelGGL((fc_fwd_fz_kernel<kLoadBatch(13)>), dim3(2, a.N16, ninst), dim3(512), 0, st, a);
+        return 0;
+      }
       // 32-row blocks once 16-row blocks would exceed one per CU (Rainbow's 2 x 64 x 3 = 384:
       // +0.5-1.3%, profiles/r4_fc_fwd_tiles_ab.txt; at <= 256 blocks, e.g. the unfolded flagship's
       // 192, the 16-row blocks measured 4% faster in round 3)
@@ -1338,6 +1421,8 @@ int wgrad_fused_plan(WgradGroup& G, int conv_chunks) {
 #else
   int total = 0;
   G.slots_member = -1;
+  static const int prefetch = getenv("DQN_WG_PREFETCH") == nullptr || atoi(getenv("DQN_WG_PREFETCH")) != 0;
+  G.prefetch = prefetch;
   for (int i = 0; i < G.n; ++i) {
     int MC, KB, NB;
     if (!fused_wgrad_tiles(G.kind[i], MC, KB, NB) || G.g[i].part != nullptr) return -1;

@@ -82,6 +82,29 @@ struct ConvLoader {
       return *reinterpret_cast<const bfx8*>(base + ((int64_t)iy * IW + ix) * CIN + ci);
     }
   }
+  // fetch / conv: frag split at the u8 -> act_t conversion, so a caller can issue several chunks'
+  // loads before it first touches their data (the fused weight-gradient tiles)
+  struct RawU8 { uint32_t lo, hi; };
+  using Raw = typename std::conditional<sizeof(Tin) == 1, RawU8, bfx8>::type;
+  DQN_DEV Raw fetch(int k0) const {
+    if constexpr (sizeof(Tin) == 1) {
+      Raw v{0u, 0u};
+      if (!ok) return v;
+      const int kh = k0 / (KW * CIN), kw = (k0 - kh * (KW * CIN)) / CIN;
+      const int iy = iy0 + kh, ix = ix0 + kw;
+      if (iy >= 0 && iy < IH) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(base + (int64_t)iy * IW * CIN);
+        if (ix >= 0 && ix < IW) v.lo = row[ix];
+        if (ix + 1 >= 0 && ix + 1 < IW) v.hi = row[ix + 1];
+      }
+      return v;
+    } else {
+      return frag(k0);
+    }
+  }
+  DQN_DEV static bfx8 conv(const Raw& v) {
+    if constexpr (sizeof(Tin) == 1) return u8x8_to_bf(v.lo, v.hi); else return v;
+  }
 };
 
 // conv1 straight from the replay's frame ring: row m = (b, oy, ox), k = (kh, kw, c)
@@ -136,6 +159,35 @@ struct FrameLoader {
     }
     return r;
   }
+  // fetch / conv (see ConvLoader): frame c's pixel pair (ix, ix + 1) as the 16 bits of v[c]
+  struct Raw { uint32_t v[4]; };
+  DQN_DEV Raw fetch(int k0) const {
+    Raw w{{0u, 0u, 0u, 0u}};
+    if (!ok) return w;
+    const int kh = k0 / (KW * 4), kw = (k0 - kh * (KW * 4)) / 4;
+    const int iy = iy0 + kh, ix = ix0 + kw;
+    if (iy < 0 || iy >= IH) return w;
+    const int off = iy * IW + ix;
+    const bool in0 = ix >= 0 && ix < IW, in1 = ix + 1 >= 0 && ix + 1 < IW;
+    if (in0 && in1 && ((off & 1) == 0)) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w.v[c] = *reinterpret_cast<const uint16_t*>(fb[c] + off);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        w.v[c] = (in0 ? (uint32_t)fb[c][off] : 0u) | (in1 ? (uint32_t)fb[c][off + 1] << 8 : 0u);
+    }
+    return w;
+  }
+  DQN_DEV static bfx8 conv(const Raw& w) {
+    bfx8 r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      r[c] = (act_t)(float)(w.v[c] & 0xffu);
+      r[4 + c] = (act_t)(float)(w.v[c] >> 8);
+    }
+    return r;
+  }
 };
 
 // dgrad gather: row m = (b, iy, ix) of the conv INPUT, k = (kh, kw, co);
@@ -181,6 +233,9 @@ struct DenseLoader {
     if (!ok) return zero8();
     return *reinterpret_cast<const bfx8*>(row + k0);
   }
+  using Raw = bfx8;
+  DQN_DEV Raw fetch(int k0) const { return frag(k0); }
+  DQN_DEV static bfx8 conv(const Raw& v) { return v; }
 };
 
 #if DQN_ACT_F32
@@ -217,7 +272,7 @@ DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
 // stores when g.atomic == 0: one group covers M). Staging as the 16-bit wgrad_block: row-major
 // [m][k] / [m][n] tiles with the slot swizzle, operands through transposed LDS reads. LDS:
 // WgradTile<MC, KB, NB>::lds_bytes. Every thread of the block calls it (2 barriers per chunk).
-template <class LD, int MC, int KB, int NB, int NTH>
+template <class LD, int MC, int KB, int NB, int NTH, bool PF = true>
 DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, int nper, act_t* lds,
                         int64_t* ph = nullptr) {
   // ph (probe launches): s_memrealtime at tile start | each chunk staged | each chunk's MFMAs done |
@@ -239,17 +294,16 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   const int nch = min(nchunks, c0 + nper) - c0;
   const bool dob = g.db != nullptr && by == 0;
   const int r = tid % MC, p = tid / MC;
-  bfx8 va[GA], vz[GZ];
-  auto load = [&](int c) {
+  // two chunk slots in registers: both chunks' loads are issued before either is converted / staged
+  // (the u8 conv1 loaders convert inside frag(), and the frame loader's addresses depend on a
+  // slot-table load: chunk by chunk, the tile paid ~4 dependent round trips for its 2 chunks)
+  using Raw = typename LD::Raw;
+  Raw ra0[GA], ra1[GA];
+  bfx8 vz0[GZ], vz1[GZ];
+  auto fetch_z = [&](int c, bfx8* vz) {
     const int m = (c0 + c) * MC + r;
     const bool mok = m < a.M;
     const act_t* dz = reinterpret_cast<const act_t*>(g.dz) + (int64_t)(mok ? m : 0) * g.ldz + n_lo;
-    LD ld(a, 0, m);
-#pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int k0 = k_lo + (p + i * TPR) * 8;
-      va[i] = sel8(k0 < a.K, ld.frag(min(k0, a.K - 8)));          // (clamped: no branch per load)
-    }
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
@@ -257,22 +311,28 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
       vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
     }
   };
+  auto fetch_a = [&](const LD& ld, Raw* ra) {
+#pragma unroll
+    for (int i = 0; i < GA; ++i) ra[i] = ld.fetch(min(k_lo + (p + i * TPR) * 8, a.K - 8));   // (clamped)
+  };
+  auto stage = [&](int c, const Raw* ra, const bfx8* vz) {
+    if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int k0 = k_lo + (p + i * TPR) * 8;
+      *reinterpret_cast<bfx8*>(At + r * SA + (((p + i * TPR) * 8) ^ wsw(r))) = sel8(k0 < a.K, LD::conv(ra[i]));
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[i];
+    __syncthreads();
+  };
   const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
   constexpr int NTt = NB / 16;
   f32x4 acc[PERW];
 #pragma unroll
   for (int i = 0; i < PERW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
-  load(0);
-  for (int c = 0; c < nch; ++c) {
-    if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
-#pragma unroll
-    for (int i = 0; i < GA; ++i) *reinterpret_cast<bfx8*>(At + r * SA + (((p + i * TPR) * 8) ^ wsw(r))) = va[i];
-#pragma unroll
-    for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[i];
-    __syncthreads();
-    WG_MARK(1 + 2 * c);
-    if (c + 1 < nch) load(c + 1);                // in flight under this chunk's MFMAs
+  auto compute = [&]() {
     if (dob && tid < NB) {
 #pragma unroll 8
       for (int q = 0; q < MC; ++q) dbs += (float)Zt[q * SZ + (tid ^ wsw(q))];
@@ -290,7 +350,43 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
         acc[i] = mfma16(af, bf, acc[i]);
       }
     }
+  };
+  {
+    // loaders of both chunks first (the frame loader's slot-table loads), then the dZ rows, then the A
+    // fragments: waiting for chunk 0's data leaves chunk 1's loads in flight
+    // (!PF: the A/B baseline -- chunk c + 1's loads issued after chunk c is staged)
+    const LD l0(a, 0, c0 * MC + r);
+    fetch_z(0, vz0);
+    if (PF && nch > 1) fetch_z(1, vz1);
+    if constexpr (PF) {
+      const LD l1(a, 0, (c0 + 1) * MC + r);
+      fetch_a(l0, ra0);
+      if (nch > 1) fetch_a(l1, ra1);
+    } else {
+      fetch_a(l0, ra0);
+    }
+  }
+  // chunk j's data lives in slot j & 1; PF refills a slot two chunks ahead, !PF one ahead
+  auto refill = [&](int j, Raw* ra, bfx8* vz) {
+    if (j < nch) {
+      const LD l(a, 0, (c0 + j) * MC + r);
+      fetch_z(j, vz);
+      fetch_a(l, ra);
+    }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    stage(c, ra0, vz0);
+    WG_MARK(1 + 2 * c);
+    if constexpr (PF) refill(c + 2, ra0, vz0); else refill(c + 1, ra1, vz1);
+    compute();
     WG_MARK(2 + 2 * c);
+    if (c + 1 < nch) {
+      stage(c + 1, ra1, vz1);
+      WG_MARK(3 + 2 * c);
+      if constexpr (PF) refill(c + 3, ra1, vz1); else refill(c + 2, ra0, vz0);
+      compute();
+      WG_MARK(4 + 2 * c);
+    }
   }
   const bool atomic = g.atomic != 0;
   if (dob && tid < NB) {
@@ -351,14 +447,20 @@ DQN_DEV int fused_wgrad_block(const WgradGroup& G, int b, act_t* lds, int64_t* p
   const int bx = b % gx, rr = b / gx, by = rr % gy, bz = rr / gy;
   const ConvArgs& a = G.a[i];
   const WgradArgs& g = G.g[i];
+#define WG_TILE(LD, MC_, KB_, NB_)                                                                 \
+  do {                                                                                              \
+    if (G.prefetch) wgrad_tile<LD, MC_, KB_, NB_, NTH, true>(a, g, bx, by, bz, g.mloop, lds, ph);   \
+    else wgrad_tile<LD, MC_, KB_, NB_, NTH, false>(a, g, bx, by, bz, g.mloop, lds, ph);             \
+  } while (0)
   switch (G.kind[i]) {
-    case L_NAT_CONV1_FWD: wgrad_tile<FwC1, kFusedWgMC, 64, 32, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
-    case L_NAT_CONV1_FRAMES: wgrad_tile<FwF1, kFusedWgMC, 64, 32, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
-    case L_NAT_CONV2_FWD: wgrad_tile<FwC2, kFusedWgMC, 64, 64, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
-    case L_NAT_CONV3_FWD: wgrad_tile<FwC3, kFusedWgMC, 64, 64, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
-    case L_HEAD_WGRAD: wgrad_tile<DenseLoader, 64, 64, 64, NTH>(a, g, bx, by, bz, g.mloop, lds, ph); break;
+    case L_NAT_CONV1_FWD: WG_TILE(FwC1, kFusedWgMC, 64, 32); break;
+    case L_NAT_CONV1_FRAMES: WG_TILE(FwF1, kFusedWgMC, 64, 32); break;
+    case L_NAT_CONV2_FWD: WG_TILE(FwC2, kFusedWgMC, 64, 64); break;
+    case L_NAT_CONV3_FWD: WG_TILE(FwC3, kFusedWgMC, 64, 64); break;
+    case L_HEAD_WGRAD: WG_TILE(DenseLoader, 64, 64, 64); break;
     default: break;
   }
+#undef WG_TILE
   return i * 256 + by;                           // (member, K-range) of the tile
 }
 #endif

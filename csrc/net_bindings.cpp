@@ -50,8 +50,23 @@ dqn::ConvArgs conv_args(const std::vector<int64_t>& in, const std::vector<int64_
 // with aux_f = [loss_mul]: the launch's side duties (ConvArgs)
 void igemm(int64_t kind, std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_t> bias,
            std::vector<int64_t> out, std::vector<int64_t> mask, std::vector<double> scale, std::vector<int64_t> dims,
-           std::vector<int64_t> aux, std::vector<double> aux_f) {
+           std::vector<int64_t> aux, std::vector<double> aux_f, std::vector<int64_t> fz) {
   dqn::ConvArgs a = conv_args(in, w, bias, out, mask, scale, dims);
+  // fz = [] or [instance, sigma fragments, noise, nsplit, ein0, eout0, ein1, eout1]: the dense forward's
+  // factorised noisy instance (qnet.hip fc_fwd_fz_kernel)
+  if (!fz.empty()) {
+    TORCH_CHECK(kind == dqn::L_DENSE_FWD_RELU && fz.size() == 8 && fz[0] >= 0 && fz[0] < (int64_t)in.size() && fz[1] != 0 &&
+                    fz[2] != 0 && fz[1] % 16 == 0 && a.M >= 1 && a.M <= 32 && a.N % 16 == 0 && a.N16 == a.N / 16 &&
+                    a.K % 32 == 0 && a.K >= 8 * 32 && a.K <= 4096 && fz[3] % 16 == 0 && fz[3] >= 16 && fz[3] <= a.N &&
+                    fz[4] >= 0 && fz[5] >= 0 && fz[6] >= 0 && fz[7] >= 0,
+                "igemm fz: dense forward, [inst, w2, noise, nsplit % 16, ein0, eout0, ein1, eout1], M <= 32, "
+                "N % 16 == 0, K % 32 == 0, 256 <= K <= 4096");
+    a.fz_inst = (int)fz[0];
+    a.fz_w2 = P<const void*>(fz[1]);
+    a.fz_noise = P<const float*>(fz[2]);
+    a.fz_nsplit = (int)fz[3];
+    a.fz_ein[0] = (int)fz[4]; a.fz_eout[0] = (int)fz[5]; a.fz_ein[1] = (int)fz[6]; a.fz_eout[1] = (int)fz[7];
+  }
   if (!aux.empty()) {
     // + optional noise duty [out0, out1, n, rng]: the next noisy-net samples at the stream's counter
     // + optional gather duty [gth (device XgmiGatherArgs), gth_blocks] at the end
@@ -462,7 +477,8 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("max_threads"), pybind11::arg("dst2") = 0, pybind11::arg("step") = 0, pybind11::arg("freq") = 1);
   m.def("qnet_igemm", &igemm, pybind11::arg("kind"), pybind11::arg("inp"), pybind11::arg("w"), pybind11::arg("bias"),
         pybind11::arg("out"), pybind11::arg("mask"), pybind11::arg("scale"), pybind11::arg("dims"),
-        pybind11::arg("aux") = std::vector<int64_t>{}, pybind11::arg("aux_f") = std::vector<double>{});
+        pybind11::arg("aux") = std::vector<int64_t>{}, pybind11::arg("aux_f") = std::vector<double>{},
+        pybind11::arg("fz") = std::vector<int64_t>{});
   m.def("qnet_wgrad", &wgrad, pybind11::arg("kind"), pybind11::arg("in"), pybind11::arg("dims"), pybind11::arg("dz"), pybind11::arg("ldz"),
         pybind11::arg("dw"), pybind11::arg("db"), pybind11::arg("dw2"), pybind11::arg("db2"), pybind11::arg("nsplit"), pybind11::arg("N"), pybind11::arg("MC"),
         pybind11::arg("KB"), pybind11::arg("NB"), pybind11::arg("scale"), pybind11::arg("atomic"), pybind11::arg("mloop") = 1,

@@ -105,6 +105,10 @@ class Network:
                                           device=self.device)
             self.executor.draw_noise(self.noise, self.noise_target, self.noise_rng)
             self.executor.premix(self.online.flat, self.noise)
+            # the target runs forward only: its fc layer may keep mu / sigma fragments and mix the
+            # noise in its forward (HipExecutor.set_factorised)
+            if hasattr(self.executor, 'set_factorised'):
+                self.executor.set_factorised(self.target.flat)
             self.executor.premix(self.target.flat, self.noise_target)
 
     # -------------------------------------------------------------- factory

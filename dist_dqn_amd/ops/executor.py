@@ -98,6 +98,19 @@ class HipExecutor:
         # C51 dL/dlogits rows (dout16 [B][KD]): logits at [0, NO), dueling value at [VO, VO + atoms)
         self.c51_VO = (self.NO + 31) // 32 * 32
         self.c51_KD = self.c51_VO + ((self.atoms + 31) // 32 * 32 if self.dueling else 0)
+        # noisy C51 nets: a flat marked with ``set_factorised`` (the learner's target) keeps its fc
+        # weights packed as separate mu / sigma fragments that change only at a target sync; its fc
+        # forward mixes the per-step noise itself (qnet.hip fc_fwd_fz_kernel: X Wmu + f(eps_out) *
+        # ((X * f(eps_in)) Wsigma)), so the optimizer launch neither reads the target's fc weights nor
+        # re-packs them every step (~10 bytes / fc weight of its ~60). Opt-in (DQN_TFACT=1): measured
+        # on Rainbow, the optimizer launch 58.4 -> 53.2 us but the fc forward 10.5 -> 20.0 us (the
+        # target's fragments, written only at a sync, are read cold from HBM, twice the bytes), so
+        # 7.29k -> 7.04k SGD steps/s on one box (gpurun_out/r5aa, r5ab)
+        self.tfact = (self.noisy and self.dist and dtype != 'fp32' and arch.network == 'nature'
+                      and os.environ.get('DQN_TFACT', '0') == '1')
+        self._fact: Dict[int, torch.Tensor] = {}      # flat ptr -> sigma fragments (packed layout)
+        self._fact_pk: Dict[int, int] = {}            # packed ptr -> flat ptr (factorised flats)
+        self._fz_noise: Dict[int, torch.Tensor] = {}  # flat ptr -> the noise its packed fc bias holds
         self._plan_packing()
         self._packed: Dict[int, torch.Tensor] = {}
         self._ws: Dict[Tuple[int, int], dict] = {}
@@ -238,7 +251,8 @@ class HipExecutor:
         for src, f in sorted(fwd.items()):
             d = dg.get(src)
             so, ei, eo = nz.get(src, (-1, -1, -1))
-            eff = int(self.noisy and src not in fc_w)
+            # eff bit 0: store the fp32 effective values; bit 1: factorised target fc tile (tfact)
+            eff = int(self.noisy and src not in fc_w) | (2 if self.tfact and src in fc_w else 0)
             fcc = fc_col.get(src, -1)
             assert fcc < 0 or (f.K % 8 == 0 and f.N % 8 == 0)
             for k0 in range(0, f.K, 32):
@@ -312,13 +326,30 @@ class HipExecutor:
         if noise is None:
             noise = d[3]
         assert noise.numel() >= d[3].numel() and noise.dtype == torch.float32
+        k = flat.data_ptr()
+        tsg = self._fact.get(k)
+        if tsg is not None:          # factorised flat: p gets the mu fragments, tsg the sigma ones
+            self._fz_noise[k] = noise
         self.ext.optim_pack(-1, flat, flat, flat, flat, d[0], d[1], 0.0, 0.0, 0, 1.0, d[2], [0.0] * 9,
                             self._upd_jobs(dev), p, None, None, 1, self.opt_max_grid, noise, eff, None, None, [], [],
-                            [], None, None, None, None, [], 0)
+                            [], None, None, None, None, [], 0, tsg=tsg.data_ptr() if tsg is not None else 0)
 
     def draw_noise(self, out0: torch.Tensor, out1: Optional[torch.Tensor], rng: torch.Tensor):
         """Standard normals into out0 (and out1) from the device Philox state ``rng`` (one launch)."""
         self.ext.noise_normal(out0, out1, rng)
+
+    def set_factorised(self, flat: torch.Tensor) -> bool:
+        """Mark ``flat`` (a target net: forward only) for the factorised noisy fc forward (see
+        ``tfact``); its packed copy is re-made by the next ``premix`` / ``effective``. Returns whether
+        it applies to this executor."""
+        if not self.tfact:
+            return False
+        k = flat.data_ptr()
+        if k not in self._fact:
+            self._fact[k] = torch.zeros(self.packed_elems, dtype=self.act_dtype, device=flat.device)
+            self._fact_pk[self._packed_for(k, flat).data_ptr()] = k
+            self._bound.pop(k, None)
+        return True
 
     def premix(self, flat: torch.Tensor, noise: torch.Tensor):
         """Bind ``noise`` to ``flat``: its packed / eff buffers now hold the effective weights
@@ -387,12 +418,34 @@ class HipExecutor:
                              if next_sample is not None and next_sample['kind'] == 'uniform' else []),
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
-                            target_noise, teff, tpk, noise_rng, self._take_fc(fc), part)
+                            target_noise, teff, tpk, noise_rng, self._take_fc(fc), part, tsg=self._tsg_arg(target, target_noise))
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:
                 self._bound[target.data_ptr()] = target_noise
         return True
+
+    def prepare_update(self, opt, flat: torch.Tensor):
+        """Allocate what ``update_and_pack`` creates on first use (the device job table, the
+        optimizer's arrival ticket, the packed buffer), so a first call inside a graph capture does
+        no host-to-device copy."""
+        dev = flat.device
+        self._upd_jobs(dev)
+        if getattr(opt, 'ticket', None) is None or opt.ticket.device != dev or opt.ticket.numel() < 17 * 32:
+            opt.ticket = torch.zeros(17 * 32, dtype=torch.int32, device=dev)
+        self.packed(flat)
+
+    def _tsg_arg(self, target, target_noise) -> int:
+        """The optimizer launch's factorised-target argument: the target's sigma fragments (written at
+        a sync step) when the launch mixes a factorised target under ``target_noise`` (now its bias
+        noise, which the target forward reads), else 0."""
+        if target is None or target_noise is None:
+            return 0
+        tsg = self._fact.get(target.data_ptr())
+        if tsg is None:
+            return 0
+        self._fz_noise[target.data_ptr()] = target_noise
+        return tsg.data_ptr()
 
     def _wg_plan(self, wg, grad, dev):
         """The fused weight-gradient launch plan for these members (fixed workspace pointers: built
@@ -502,7 +555,7 @@ class HipExecutor:
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             target_noise, teff, tpk, noise_rng, fcargs, 0, wg=plan.data_ptr(), wg_blocks=nwg,
-                            wg_jobs=lead if self.wg_mix else 0)
+                            wg_jobs=lead if self.wg_mix else 0, tsg=self._tsg_arg(target, target_noise))
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:
@@ -602,6 +655,12 @@ class HipExecutor:
             if d.noisy:
                 dense[d.name] = (d, noff)
                 noff += d.fin + d.fout
+        # (eps_in, eps_out) offsets of the fc layer(s) in fc/fwd column order (factorised forward)
+        fcn = ['value/fcl', 'advantage/fcl'] if self.dueling else ['fcl', 'fcl']
+        if all(n in dense for n in fcn):
+            self._fz_offs = [(dense[n][1], dense[n][1] + dense[n][0].fin) for n in fcn]
+        elif self.tfact:
+            self.tfact = False
         for name in lay.names:
             kind = lay.kinds[name]
             if kind not in ('w', 'b'):
@@ -871,7 +930,24 @@ class HipExecutor:
                             [p.data_ptr() + self.esz * self.poff['fc/fwd'] for p in packs], fcb,
                             [ws['h'][i].data_ptr() for i in range(ninst)], [], [1.0] * ninst,
                             [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0],
-                            [z.data_ptr(), z.numel(), 0, 0, 0] if z is not None else [], [1.0] if z is not None else [])
+                            [z.data_ptr(), z.numel(), 0, 0, 0] if z is not None else [], [1.0] if z is not None else [],
+                            fz=self._fz_args(packs[:ninst], B))
+
+    def _fz_args(self, packs, B) -> list:
+        """The fc forward's factorised instance (``set_factorised``): [inst, sigma fragments, noise,
+        nsplit, eps_in / eps_out offsets of both column halves], or [] when no instance is."""
+        if not self._fact_pk:
+            return []
+        idx = [i for i, p in enumerate(packs) if p.data_ptr() in self._fact_pk]
+        if not idx:
+            return []
+        assert len(idx) == 1 and B <= 32, 'factorised fc forward: one instance, B <= 32'
+        k = self._fact_pk[packs[idx[0]].data_ptr()]
+        noise = self._fz_noise.get(k)
+        assert noise is not None, 'factorised target: not mixed yet (premix / effective first)'
+        (e0, o0), (e1, o1) = self._fz_offs
+        return [idx[0], self._fact[k].data_ptr() + self.esz * self.poff['fc/fwd'], noise.data_ptr(),
+                self.HID if self.dueling else self.HH, e0, o0, e1, o1]
 
     def can_fold_head(self, B: int, E: int = 0) -> bool:
         """Whether the training step's fc forward and scalar head run as ONE launch

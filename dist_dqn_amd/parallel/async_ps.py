@@ -449,6 +449,8 @@ class XgmiPSServer:
         dev = net.online.flat.device
         for w in self.workers:                # initial pull (push number 1): the PS parameters
             self._publish(w, 1)
+        if self.lowrank is not None:          # (no first-use allocations inside the capture)
+            net.executor.prepare_update(net.optimizer, net.online.flat)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         graphs = {}

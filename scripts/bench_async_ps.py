@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, transport, steps, q, pipeline=0):
+def _rank(rank, world, port, transport, steps, q, pipeline=0, lowrank=1):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0', DQN_DIST_BACKEND='gloo')
     sys.path.insert(0, ROOT)
@@ -39,7 +39,7 @@ def _rank(rank, world, port, transport, steps, q, pipeline=0):
     from dist_dqn_amd.parallel.async_ps import make_ps_client, make_ps_server
     from dist_dqn_amd.replay import DeviceReplay
     cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=5 --backend=hip --replay_memory_capacity=20000 '
-                 '--async_ps --ps_transport=%s --ps_pipeline=%d' % (transport, pipeline))
+                 '--async_ps --ps_transport=%s --ps_pipeline=%d --ps_lowrank=%d' % (transport, pipeline, lowrank))
     ctx = init_distributed(cfg, device='cuda')
     net = Network.create_network(cfg, (84, 84, 4), 6, num_replicas=world, device=ctx.device)
     broadcast_state(ctx, net)
@@ -85,13 +85,14 @@ def main():
     ap.add_argument('--workers', type=int, default=2)
     ap.add_argument('--steps', type=int, default=300, help='SGD steps (pushes) per worker')
     ap.add_argument('--pipeline', type=int, default=0, help='--ps_pipeline: take the previous push\'s answer, then push')
+    ap.add_argument('--lowrank', type=int, default=1, help='--ps_lowrank: push the fc factors, not the fc gradient')
     args = ap.parse_args()
     import multiprocessing as mp
     ctx = mp.get_context('spawn')
     q = ctx.SimpleQueue()
     world = args.workers + 1
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, args.transport, args.steps, q, args.pipeline)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, args.transport, args.steps, q, args.pipeline, args.lowrank)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -105,7 +106,7 @@ def main():
     ps = [r for r in res if r[0] == 'ps']
     wk = [r for r in res if r[0] == 'worker']
     out = {'transport': args.transport, 'workers': args.workers, 'steps_per_worker': args.steps,
-           'pipeline': args.pipeline,
+           'pipeline': args.pipeline, 'lowrank': args.lowrank,
            'ps_updates': ps[0][1] if ps else None, 'ps_wall_s': round(ps[0][2], 3) if ps else None,
            'ps_updates_per_sec': round(ps[0][1] / ps[0][2], 1) if ps else None,
            'worker_sgd_steps_per_sec': [round(n / el, 1) for _, n, el in wk],

@@ -457,6 +457,42 @@ def test_rainbow_learner_keeps_online_premixed():
     assert _rel(net.q_values(x), oracle.q_values(net.online.flat, x, net.noise)) < 2e-2
 
 
+@pytest.mark.parametrize('dtype', ['bf16', 'fp16'])
+def test_rainbow_factorised_target_tracks_syncs(dtype, monkeypatch):
+    """Rainbow's target keeps separate mu / sigma fc fragments (written only at a sync) and mixes
+    its per-step noise in the fc forward (qnet.hip fc_fwd_fz_kernel): over graph-replayed steps
+    that cross two fused hard syncs, its Q-values match the fp32 oracle on the target's master
+    weights under the target noise after every step."""
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.learner import Learner
+    from dist_dqn_amd.models.executor import TorchExecutor
+    from dist_dqn_amd.models.network import Network
+    from dist_dqn_amd.replay import DeviceReplay
+    monkeypatch.setenv('DQN_TFACT', '1')                  # (opt-in: see HipExecutor.tfact)
+    cfg = preset('nature', 'Pong-v0', '--seed=4 --backend=hip --dtype=%s --replay_memory_capacity=4096 '
+                 '--target_update_freq=3 %s' % (dtype, RAINBOW))
+    net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
+    ex = net.executor
+    assert ex.tfact and net.target.flat.data_ptr() in ex._fact
+    rep = DeviceReplay(4096, (84, 84), 4, device=DEV, seed=6)
+    rep.fill_synthetic(4096, 6, seed=6)
+    ln = Learner(net, rep, cfg, use_graph=True)
+    oracle = TorchExecutor(net.arch, net.layout, input_scale=cfg.input_scale, loss=cfg.loss, oracle=True,
+                           huber_delta=cfg.huber_delta, double_dqn=cfg.double_dqn)
+    x = torch.randint(0, 256, (16, 84, 84, 4), dtype=torch.uint8, device=DEV)
+    t0 = net.target.flat.clone()
+    for i in range(7):
+        ln.step()
+        torch.cuda.synchronize()
+        q = net.target_q_values(x)
+        q_ref = oracle.q_values(net.target.flat, x, net.noise_target)
+        assert _rel(q, q_ref) < 2e-2, (i, _rel(q, q_ref))
+    assert int(net.global_step) == 7 and not torch.equal(t0, net.target.flat)
+    # after the step-6 sync the target's master equals the online net as it was then; one more
+    # update moved the online net on
+    assert not torch.equal(net.online.flat, net.target.flat)
+
+
 @pytest.mark.parametrize('extra,acting', [('', False), ('--double_dqn', False), ('', True)])
 def test_fused_sampling_equals_sampler_launch(extra, acting):
     """Uniform minibatch drawn by an extra block of the previous step's optimizer launch
