@@ -245,7 +245,6 @@ struct WgradGroup {
   // tile runs once that slot's gradient is complete (a contiguous range of the launch's job table)
   int32_t* done;
   int slots_member;
-  int prefetch;              // fused tiles: both chunks' loads issued up front (DQN_WG_PREFETCH, default 1)
   int dep_first[kMaxWgradMembers][16 + 1], dep_count[kMaxWgradMembers][16 + 1];
 };
 constexpr int kWgSlots = 16 + 1;            // K-ranges (<= 16) + the bias

@@ -240,12 +240,60 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   int64_t* tl = (h.prof != nullptr && threadIdx.x == 0 && blockIdx.x < kTlBlocks) ? h.prof + kProfPhases + 3 * blockIdx.x
                                                                                     : nullptr;
   if (tl) { tl[0] = (int64_t)__builtin_amdgcn_s_memrealtime(); tl[1] = 0; tl[2] = 0; }
+  int32_t* cnt = ticket + kTicketStride;        // end-of-launch arrival counters (see the closing step)
+#if !DQN_ACT_F32
+  // ---- a weight-gradient tile, counted on its (member, K-range) when done (the last tile of a
+  //      range ran that range's jobs serially: ~4 of them, 8-15 us each, measured; the jobs
+  //      now wait in blocks of their own at the end of the grid and run in parallel)
+  auto wg_tile_run = [&](int b) {
+    int64_t* ph = (h.prof != nullptr && b < kTilePhBlocks) ? h.prof + kProfPhases + 3 * kTlBlocks + 8 * b : nullptr;
+    const int mb = fused_wgrad_block<kPackThreads>(*wg, b, reinterpret_cast<act_t*>(opt_dyn), ph);
+    const int m = mb >> 8, by = mb & 255;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's atomics / write-through stores done
+    if (ph != nullptr && threadIdx.x == 0) ph[7] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (tl) { tl[1] = m; tl[2] = (int64_t)__builtin_amdgcn_s_memrealtime(); }
+      // count the tile on its (member, K-range) and -- K-range 0 -- the member's bias range; the
+      // jobs of a range wait for its count in their own blocks (end of the grid), in parallel
+      __hip_atomic_fetch_add(wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + by), 1,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (by == 0)
+        __hip_atomic_fetch_add(wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + kWgSlots - 1), 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // (member-level count: the sampler waits for the frame-slot reader)
+      __hip_atomic_fetch_add(wg->done + kTicketStride * m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  if constexpr (WG && !FEW) {
+    // tiles first, ahead of the launch-start reads below (the step / rng / slot-flag words): every
+    // scalar load there is waited for in order (s_waitcnt lgkmcnt(0)), ~3 us of dependent round
+    // trips before a tile issued its first operand load (probe_split timeline: tile blocks ran
+    // 9.0 us of which 5.6 us inside the tile)
+    // (the block roles of the WG grid, as below: wg_mix > 0 interleaves the first wg_mix jobs)
+    const int p = (int)blockIdx.x - 1, S = wg_blocks + wg_mix;
+    int tb = -1;
+    if (p >= 0 && wg_mix > 0 && p < S) {
+      const int q = p * wg_blocks / S, q1 = (p + 1) * wg_blocks / S;
+      if (q1 > q) tb = q;
+    } else if (p >= 0 && p < wg_blocks) {
+      tb = p;
+    }
+    if (tb >= 0) {
+      wg_tile_run(tb);
+      __syncthreads();
+      if (threadIdx.x == 0)                     // the end-of-launch arrival (see the closing step)
+        __hip_atomic_fetch_add(cnt + kTicketStride * (blockIdx.x & (kTicketSubs - 1)), 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+#endif
   // block 0 leads (the sampler when the launch draws the next minibatch; always in WG launches,
   // whose block 0 then only closes the launch)
   const bool smp_on = smp.size != nullptr || per.sum != nullptr;
   const bool extra = smp_on || WG;
   const int wg0 = WG ? wg_blocks : 0;
-  int32_t* cnt = ticket + kTicketStride;        // end-of-launch arrival counters (see the closing step)
   // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
   const bool sampler = smp_on && blockIdx.x == 0;
   const int nwork = (int)gridDim.x - (extra ? 1 : 0) - wg0;
@@ -254,16 +302,15 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // the tiles over the first wg_blocks + wg_mix positions, Bresenham-spaced: the latency-bound tiles
   // and the bandwidth-bound fc jobs share the CUs from the launch start instead of the tiles holding
   // most slots for their whole span; the range-dependent jobs stay after every tile)
-  int wgb = -1;                                               // this block's tile (WG), else -1
+  // (the tile blocks themselves returned at the top of the kernel)
   int wid = (int)blockIdx.x - (extra ? 1 : 0) - wg0;          // work index of an update block
   if constexpr (WG) {
     const int p = (int)blockIdx.x - 1;
     const int S = wg_blocks + wg_mix;
     if (p >= 0 && wg_mix > 0 && p < S) {
       const int q = p * wg_blocks / S, q1 = (p + 1) * wg_blocks / S;
-      if (q1 > q) { wgb = q; wid = -1; } else { wid = p - q; }
+      wid = q1 > q ? -1 : p - q;
     } else if (p >= 0 && p < wg_blocks) {
-      wgb = p;
       wid = -1;
     } else {
       wid = p - wg_blocks;
@@ -722,30 +769,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   };
 #if !DQN_ACT_F32
   if constexpr (WG) {
-    const int b = wgb;
-    if (b >= 0 && b < wg_blocks) {
-      // ---- a weight-gradient tile, counted on its (member, K-range) when done (the last tile of a
-      //      range ran that range's jobs serially: ~4 of them, 8-15 us each, measured; the jobs
-      //      now wait in blocks of their own at the end of the grid and run in parallel)
-      int64_t* ph = (h.prof != nullptr && b < kTilePhBlocks) ? h.prof + kProfPhases + 3 * kTlBlocks + 8 * b : nullptr;
-      const int mb = fused_wgrad_block<kPackThreads>(*wg, b, reinterpret_cast<act_t*>(opt_dyn), ph);
-      const int m = mb >> 8, by = mb & 255;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's atomics / write-through stores done
-      if (ph != nullptr && threadIdx.x == 0) ph[7] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        if (tl) { tl[1] = m; tl[2] = (int64_t)__builtin_amdgcn_s_memrealtime(); }
-        // count the tile on its (member, K-range) and -- K-range 0 -- the member's bias range; the
-        // jobs of a range wait for its count in their own blocks (end of the grid), in parallel
-        __hip_atomic_fetch_add(wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + by), 1,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (by == 0)
-          __hip_atomic_fetch_add(wg->done + kTicketStride * (kMaxWgradMembers + m * kWgSlots + kWgSlots - 1), 1,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // (member-level count: the sampler waits for the frame-slot reader)
-        __hip_atomic_fetch_add(wg->done + kTicketStride * m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    // (the tile blocks ran wg_tile_run at the top of the kernel and returned)
   }
 #endif
   if constexpr (FC) {

@@ -1421,8 +1421,6 @@ int wgrad_fused_plan(WgradGroup& G, int conv_chunks) {
 #else
   int total = 0;
   G.slots_member = -1;
-  static const int prefetch = getenv("DQN_WG_PREFETCH") == nullptr || atoi(getenv("DQN_WG_PREFETCH")) != 0;
-  G.prefetch = prefetch;
   for (int i = 0; i < G.n; ++i) {
     int MC, KB, NB;
     if (!fused_wgrad_tiles(G.kind[i], MC, KB, NB) || G.g[i].part != nullptr) return -1;

@@ -99,6 +99,13 @@ class PsServer {
     std::vector<int64_t> per(per_.begin(), per_.end());
     return pybind11::make_tuple(updates_.load(), per, (int64_t)stopped_workers_, busy_s_);
   }
+  // seconds since serving started at every kMarkEvery-th launched update (steady-state rate windows);
+  // after wait()
+  std::vector<double> marks() const {
+    if (running_) throw std::runtime_error("PsServer.marks() before wait()");
+    return marks_;
+  }
+  static constexpr int kMarkEvery = 64;
 
  private:
   uint64_t push_word(int w) const {
@@ -143,7 +150,8 @@ class PsServer {
           }
           HIPCK(hipGraphLaunch(apply_[w], stream_));       // arrival order: one stream
           per_[w] += 1;
-          updates_.fetch_add(1, std::memory_order_relaxed);
+          if ((updates_.fetch_add(1, std::memory_order_relaxed) + 1) % kMarkEvery == 0)
+            marks_.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         }
         if (!got) std::this_thread::sleep_for(std::chrono::microseconds(2));
       }
@@ -166,6 +174,7 @@ class PsServer {
   uint64_t seen0_ = 1;
   int stopped_workers_ = 0;
   double busy_s_ = 0.0;
+  std::vector<double> marks_;
   std::atomic<int64_t> updates_{0};
   std::atomic<bool> stop_{false}, done_{false}, pause_req_{false}, paused_{false};
   std::atomic<int64_t> pauses_{0};
@@ -188,5 +197,6 @@ void register_ps_server(pybind11::module_& m) {
       .def("wait", &PsServer::wait, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("updates", &PsServer::updates)
       .def("running", &PsServer::running)
-      .def("stats", &PsServer::stats);
+      .def("stats", &PsServer::stats)
+      .def("marks", &PsServer::marks);
 }

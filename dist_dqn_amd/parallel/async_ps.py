@@ -501,6 +501,7 @@ class XgmiPSServer:
                 ck.quiesce = None
             self.updates = srv.wait()
         self.pauses = int(srv.pauses())
+        self.marks = list(srv.marks()) if hasattr(srv, 'marks') else []   # (s at every 64th update)
         _, per, stopped, busy = srv.stats()
         self.per_worker = {w: int(per[w]) for w in self.workers}
         self.stopped_workers = int(stopped)

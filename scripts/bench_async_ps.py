@@ -49,7 +49,13 @@ def _rank(rank, world, port, transport, steps, q, pipeline=0, lowrank=1):
         n = srv.serve()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        q.put(('ps', n, el))
+        # steady state: the native server's update timestamps (every 64th), middle half of the run
+        mk = getattr(srv, 'marks', [])
+        steady = None
+        if len(mk) >= 8:
+            i0, i1 = len(mk) // 4, 3 * len(mk) // 4
+            steady = 64 * (i1 - i0) / (mk[i1] - mk[i0])
+        q.put(('ps', n, el, steady))
         if hasattr(srv, 'close'):
             dist.barrier()
             srv.close()
@@ -104,11 +110,14 @@ def main():
     while not q.empty():
         res.append(q.get())
     ps = [r for r in res if r[0] == 'ps']
+    steady = ps[0][3] if ps and len(ps[0]) > 3 else None
     wk = [r for r in res if r[0] == 'worker']
     out = {'transport': args.transport, 'workers': args.workers, 'steps_per_worker': args.steps,
            'pipeline': args.pipeline, 'lowrank': args.lowrank,
            'ps_updates': ps[0][1] if ps else None, 'ps_wall_s': round(ps[0][2], 3) if ps else None,
            'ps_updates_per_sec': round(ps[0][1] / ps[0][2], 1) if ps else None,
+           # (the rate above includes the workers' start-up: replay fill, learner build, graph capture)
+           'ps_updates_per_sec_steady': round(steady, 1) if steady else None,
            'worker_sgd_steps_per_sec': [round(n / el, 1) for _, n, el in wk],
            'exitcodes': [p.exitcode for p in procs], 'gpus': 1,
            'note': 'all ranks share one MI355X (gloo setup); the workers run the HIP Nature-CNN learner'}
