@@ -150,7 +150,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
                 std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
                 c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng, std::vector<int64_t> fc,
-                int64_t part, int64_t wg, int64_t wg_blocks, int64_t wg_jobs, int64_t tsg) {
+                int64_t part, int64_t wg, int64_t wg_blocks, int64_t wg_jobs, int64_t tsg, bool no_pack) {
   // wg / wg_blocks: the launch also computes the grouped weight gradients -- a device WgradGroup
   // (qnet_wgrad_plan) whose wg_blocks tiles follow the lead block; jobs with dep >= 0 wait for
   // their member (needs fc: the launch forms the fc gradients from FcFuse rows)
@@ -170,6 +170,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   // op -1: no optimizer update, only the (noisy) mix + pack of w (noise / eff given)
   // tsg: 0 or the sigma-fragment buffer (packed layout) of a factorised target (UpdJob.eff bit 1):
   //   update calls with tnoise write it at a sync step, mix-only calls on that target every time
+  // no_pack: update only (no packed fragments / copies; the async-PS server)
   CHECK_T(w, torch::kFloat32); CHECK_T(grad, torch::kFloat32); CHECK_T(s0, torch::kFloat32);
   CHECK_T(s1, torch::kFloat32); CHECK_T(beta_pow, torch::kFloat32); CHECK_T(ticket, torch::kInt32);
   CHECK_T(step, torch::kInt64); CHECK_T(jobs, torch::kInt32); CHECK_T(packed, DQN_ACT_F32 ? torch::kFloat32 : DQN_ACT_F16 ? torch::kHalf : torch::kBFloat16);
@@ -308,7 +309,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
                     per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, fc.empty() ? nullptr : &ff,
                     reinterpret_cast<const float*>(part), reinterpret_cast<const void*>(wg), (int)wg_blocks,
-                    (int)wg_jobs, reinterpret_cast<void*>(tsg), cur_stream());
+                    (int)wg_jobs, reinterpret_cast<void*>(tsg), no_pack ? 1 : 0, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {
@@ -768,7 +769,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("noise_dst"), pybind11::arg("sample"), pybind11::arg("per_p"), pybind11::arg("per_f"),
         pybind11::arg("tnoise"), pybind11::arg("teff"), pybind11::arg("tpk"), pybind11::arg("noise_rng"),
         pybind11::arg("fc"), pybind11::arg("part"), pybind11::arg("wg") = 0, pybind11::arg("wg_blocks") = 0,
-        pybind11::arg("wg_jobs") = 0, pybind11::arg("tsg") = 0);
+        pybind11::arg("wg_jobs") = 0, pybind11::arg("tsg") = 0, pybind11::arg("no_pack") = false);
   m.def("noise_normal", &noise_normal);
   m.attr("UPD_JOB_INTS") = upd_job_ints();
   m.def("optim_prof", []() {

@@ -59,7 +59,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
                        int64_t* noise_rng, const FcFuse* fc, const float* part, const void* wg, int wg_blocks,
-                       int wg_jobs, void* tsg, hipStream_t st);
+                       int wg_jobs, void* tsg, int no_pack, hipStream_t st);
 // 1 when this build's optimizer launch can form the fc weight gradient itself (16-bit builds)
 int optim_fc_fuse();
 // probe launches (DQN_OPT_PROF=1): per-block [start, ready, end] s_memrealtime stamps of the last launch

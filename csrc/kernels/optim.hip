@@ -154,7 +154,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
                        int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
                        void* tpk, int64_t* noise_rng, const FcFuse* fc, const float* part, const void* wg,
-                       int wg_blocks, int wg_jobs, void* tsg, hipStream_t st) {
+                       int wg_blocks, int wg_jobs, void* tsg, int no_pack, hipStream_t st) {
   OptPackLaunch L{};
   OptHP& h = L.h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
@@ -164,6 +164,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   static const int dep_fence = getenv("DQN_FENCE_TAILS") != nullptr ? 1 : 0;
   h.dep_fence = dep_fence;
   h.tsg = tsg;
+  h.no_pack = no_pack;
   // one block per job up to max_grid (grid-stride beyond it); block 0 (+1 sampler block when the
   // launch draws the next minibatch) closes the launch once every other block has arrived
   const FcFuse ff = (fc != nullptr && optim_fc_fuse()) ? *fc : FcFuse{nullptr, nullptr, 0, 0, 0};

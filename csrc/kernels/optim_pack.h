@@ -26,6 +26,9 @@ struct OptHP {
   // fragments and this buffer (the packed layout) its sigma fragments, written only when they change
   // (a sync step, or a mix-only call on the target); the target forward mixes the noise in itself
   void* tsg;
+  // 1: update only, no packed fragments / fp32 copies written (the async-PS server, which never
+  // runs the network: it re-packs once when serving ends)
+  int no_pack;
   // probe launches only (DQN_OPT_PROF=1, nullptr otherwise): [0, 16) s_memtime phase stamps of
   // blocks 0 and 1, then per block [start, ready, end] s_memrealtime (100 MHz) for blocks < kTlBlocks
   // (ready: a dependent job's wait is over / the sampler's draw is done)
@@ -169,8 +172,9 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 
 // MODE bits: kModeNoisy (noisy jobs in the work list), kModeTmix (+ the target's mix + pack),
 // kModePer (the sampler block runs the prioritized sum-tree path). Paths a mode excludes are
-// not instantiated: their registers would cost the plain nets occupancy (mode 0: 8 waves / SIMD,
-// so every block of the Nature-CNN work list is resident at once).
+// not instantiated: their registers would cost the plain nets occupancy. Mode 0: 5 waves / SIMD
+// (at 8 it spilled 120 B / lane to scratch: 16.1 -> 12.8 us alone, scripts/probe_optim.py,
+// gpurun_out/r5ae); the fc-only mode stays at 8 (its 52 B spill measured 2.5 % faster than 6 waves).
 // kModeFc: some jobs form their gradient from FcFuse rows (16-bit builds).
 // kModeWg (16-bit builds): the launch also computes the grouped weight gradients. Grid: [the lead
 // block: sampler + closer] [the WgradGroup's tiles (device memory, wgrad_dev.h)] [the jobs whose
@@ -203,7 +207,7 @@ struct OptShm<false, N, TAG> {
   DQN_DEV static unsigned char* get() { return nullptr; }
 };
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? (DQN_ACT_F32 ? 4 : 8) : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+__global__ void __launch_bounds__(kPackThreads, (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? (DQN_ACT_F32 ? 4 : (MODE & kModeFc) ? 8 : 5) : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
@@ -686,7 +690,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     }
     if (jb.eff & 1) st(eff, mo, e);
     if (elem) {
-      if (jb.fwd_off >= 0) {                              // fp32 copy inside the packed buffer
+      if (jb.fwd_off >= 0 && !h.no_pack) {                // fp32 copy inside the packed buffer
         float* pf = reinterpret_cast<float*>(packed + jb.fwd_off) + n;
         float* tf = psync ? reinterpret_cast<float*>(tgt_packed + jb.fwd_off) + n : nullptr;
         float* mf = tmix ? reinterpret_cast<float*>(tpk + jb.fwd_off) + n : nullptr;
@@ -734,7 +738,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
     };
     OPT_MARK(7);
-    emit(e, packed, psync ? tgt_packed : nullptr, true);
+    if (!h.no_pack) emit(e, packed, psync ? tgt_packed : nullptr, true);
     if (tmj) emit(te, tpk, nullptr, false);               // (the target runs forward only)
     if constexpr (NZ) {
       if (tfj) {

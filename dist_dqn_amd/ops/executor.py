@@ -366,7 +366,7 @@ class HipExecutor:
                         noise: Optional[torch.Tensor] = None, grad_noise: Optional[torch.Tensor] = None,
                         noise_dst: Optional[torch.Tensor] = None, next_sample=None,
                         target_noise: Optional[torch.Tensor] = None, noise_rng: Optional[torch.Tensor] = None,
-                        fc=None):
+                        fc=None, pack: bool = True):
         """Optimizer step + repack in ONE launch (+ the hard target sync under the device
         predicate when ``target`` is given). Noisy nets: ``noise`` (the next sample for this
         flat) is mixed in and bound (see ``premix``); the target's packed copy is not written
@@ -381,9 +381,11 @@ class HipExecutor:
         samples ``loss_and_grad(draw_noise=...)`` drew this step; the last block advances its
         counter. ``fc``: the pending fused fc weight gradient of ``loss_and_grad(defer_fc=True)``
         (default: taken from this executor; the launch forms dW = X^T dH and the fc bias gradient
-        from those rows instead of reading them from ``grad``). Returns True."""
+        from those rows instead of reading them from ``grad``). ``pack=False``: the update only, no packed
+        fragments written (a caller that never runs the network until it repacks). Returns True."""
         from ..optim import kernel_op
         dev = flat.device
+        assert pack or (self._wg_pending is None and not self.noisy), 'pack=False: plain fused update only'
         if self._wg_pending is not None:
             return self._update_split(opt, flat, grad, grad_scale, global_step, target, target_freq, noise, grad_noise,
                                       noise_dst, next_sample, target_noise, noise_rng, fc)
@@ -418,7 +420,8 @@ class HipExecutor:
                              if next_sample is not None and next_sample['kind'] == 'uniform' else []),
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
-                            target_noise, teff, tpk, noise_rng, self._take_fc(fc), part, tsg=self._tsg_arg(target, target_noise))
+                            target_noise, teff, tpk, noise_rng, self._take_fc(fc), part, tsg=self._tsg_arg(target, target_noise),
+                            no_pack=not pack)
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:

@@ -391,7 +391,7 @@ class XgmiPSServer:
             return
         base, lr = self.sh.slot(w), self.lowrank
         net.executor.update_and_pack(net.optimizer, net.online.flat, self._grads[w], 1.0, net.global_step,
-                                     fc=(base + lr['x_off'], base + lr['dh_off'], lr['B']))
+                                     fc=(base + lr['x_off'], base + lr['dh_off'], lr['B']), pack=False)
 
     def _publish(self, w: int, seq: int, status: int = 0):
         st = status == 0

@@ -307,6 +307,70 @@ def test_bench_gpus_flag_launches_ranks_itself(tmp_path):
     assert tl['graph_launches_of_G'] * d['graph_steps'] + tl['single_step_graphs'] == 20
 
 
+def _worker_rccl_one_rank(rank, world, port, errq):
+    """A real RCCL (backend 'nccl') process group of ONE rank: RCCL refuses two ranks on one GPU, so
+    this is the only RCCL run a one-GPU box allows. The context is forced 'enabled' so the data
+    parallel code takes its RCCL branches: first contact, the bucketed fp32 and bf16-wire all-reduce,
+    the async range all-reduce of the overlapped backward, the state broadcast, and learner steps
+    whose gradient all-reduce is RCCL's."""
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1', LOCAL_RANK='0')
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from dist_dqn_amd.config import preset
+        from dist_dqn_amd.learner import Learner
+        from dist_dqn_amd.models.network import Network
+        from dist_dqn_amd.parallel.dist import DistContext, first_contact
+        from dist_dqn_amd.parallel.dp import GradAllReducer, broadcast_state
+        from dist_dqn_amd.replay import DeviceReplay
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+        assert dist.get_backend() == 'nccl'
+        ctrl = dist.new_group(backend='gloo')
+
+        class _Ctx(DistContext):
+            enabled = property(lambda self: True)
+        ctx = _Ctx(0, 1, 0, dev, 'nccl', ctrl)
+        first_contact(ctx)                                  # checked 4-element RCCL all-reduce
+        g = torch.Generator(device=dev).manual_seed(1)
+        flat = torch.randn(3 * 1024 * 1024 + 12, device=dev, generator=g)
+        ref = flat.clone()
+        red = GradAllReducer(ctx, flat, bucket_mb=2.0, mode='rccl')
+        assert red.xgmi is None and len(red.buckets) > 1, red.buckets
+        red.allreduce()                                     # one rank: the sum is the value itself
+        assert torch.equal(flat, ref)
+        h = [red.allreduce_range_async(0, 1000), red.allreduce_range_async(1000, flat.numel())]
+        red.wait_all(h)
+        assert torch.equal(flat, ref)
+        red16 = GradAllReducer(ctx, flat, bucket_mb=2.0, mode='rccl', wire_dtype='bf16')
+        red16.allreduce()                                   # bf16 wire: rounded once
+        assert torch.equal(flat, ref.to(torch.bfloat16).float())
+        cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=3 --backend=hip --replay_memory_capacity=4096 '
+                     '--allreduce=rccl')
+        net = Network.create_network(cfg, (84, 84, 4), 6, device=dev)
+        broadcast_state(ctx, net)
+        rep = DeviceReplay(4096, (84, 84), 4, device=dev, seed=3)
+        rep.fill_synthetic(4096, 6, seed=3)
+        ln = Learner(net, rep, cfg, ctx)
+        assert ln.reducer.xgmi is None and ln.reducer.ctx is ctx
+        p0 = net.online.flat.clone()
+        for _ in range(4):
+            ln.step()
+        torch.cuda.synchronize()
+        assert int(net.global_step) == 4 and torch.isfinite(net.online.flat).all()
+        assert not torch.equal(p0, net.online.flat)
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+        errq.put('rank %d: %s\n%s' % (rank, e, traceback.format_exc()))
+        raise
+
+
+def test_rccl_one_rank_data_parallel_paths():
+    _run_ranks(_worker_rccl_one_rank, (), world=1, timeout=150)
+
+
 def test_bench_gpus_more_than_the_node_has_fails_loudly():
     """`--gpus 8` on a one-GPU box (no gloo rehearsal asked for) must refuse with a message and a
     non-zero exit, never run one rank and print n_gpus 1."""
