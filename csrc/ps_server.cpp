@@ -18,6 +18,8 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <immintrin.h>
+#include <sched.h>
 #include <vector>
 
 namespace {
@@ -119,6 +121,7 @@ class PsServer {
       std::vector<char> active(nw_ + 1, 1);
       int nactive = nw_;
       const auto t0 = std::chrono::steady_clock::now();
+      uint32_t idle = 0;
       while (nactive > 0 && !(max_updates_ > 0 && updates_.load() >= max_updates_)) {
         if (pause_req_.load(std::memory_order_acquire)) {
           HIPCK(hipStreamSynchronize(stream_));            // every launched update has landed
@@ -153,7 +156,14 @@ class PsServer {
           if ((updates_.fetch_add(1, std::memory_order_relaxed) + 1) % kMarkEvery == 0)
             marks_.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         }
-        if (!got) std::this_thread::sleep_for(std::chrono::microseconds(2));
+        // idle: spin (a 2 us sleep_for slept ~60 us under the kernel's timer slack -- a push then waited
+        // that long to be seen); a yield every 256 empty polls keeps the core shareable
+        if (!got) {
+          _mm_pause();
+          if ((++idle & 255) == 0) sched_yield();
+        } else {
+          idle = 0;
+        }
       }
       HIPCK(hipStreamSynchronize(stream_));
       busy_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
