@@ -324,18 +324,25 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // the step words, read once at launch start: block 0's closing step writes their successors from
   // these registers (a load -> store round trip there sat on the launch's critical path); nothing
   // else writes them during the launch
+  // ... read in ONE batch of unconditional scalar loads (null pointers swapped for a valid word whose
+  // value is then ignored): loaded one by one behind their null checks, each cost a pointer load, a
+  // wait, the value load and another wait -- several round trips before a job issued its first load
+  const int64_t* step_p = step != nullptr ? step : reinterpret_cast<const int64_t*>(ticket);
+  const int64_t* rng_p = noise_rng != nullptr ? noise_rng + 1 : step_p;
+  const int64_t step_raw = step_p[0], rng_raw = rng_p[0];
+  const int32_t flag_raw = ticket[kSlotFlag];
   float b1p = 1.f, b2p = 1.f;
   if constexpr (OP == 3) {
     b1p = beta_pow[0];
     b2p = beta_pow[1];
     lr_t = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   }
-  const int64_t step_now = UPD && step != nullptr ? step[0] : 0;
-  const int64_t rng_now = UPD && noise_rng != nullptr ? noise_rng[1] : 0;   // (FEW: any block may close)
+  const int64_t step_now = UPD && step != nullptr ? step_raw : 0;
+  const int64_t rng_now = UPD && noise_rng != nullptr ? rng_raw : 0;         // (FEW: any block may close)
   const bool sync = UPD && tgt != nullptr && step != nullptr && ((step_now + 1) % tfreq) == 0;
   const bool psync = sync && tgt_packed != nullptr;
   constexpr bool TWO = OP == 2 || OP == 3 || OP == 5 || OP == 6 || OP == 7;   // second slot written
-  const bool wtwo = OP != 7 || ticket[kSlotFlag] != 0;                         // (momentum-0 RMSProp: flagged)
+  const bool wtwo = OP != 7 || flag_raw != 0;                                  // (momentum-0 RMSProp: flagged)
   constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
   constexpr bool ONE = UPD && OP != 0;
   const int t = threadIdx.x;
