@@ -73,6 +73,24 @@ __global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_he
   const int m_base = blockIdx.x * 16, nt = blockIdx.y;
   const int Mi = actor_inst ? h.act_E : a.M;   // valid rows of this instance
   const bool dh_tile = f.spin && !actor_inst && inst == 0;   // this block writes its own dH tile
+  // ---- h tile operands: the first k batch is issued BEFORE the loads below (output-layer rows,
+  //      biases, TD inputs, epoch / actor words): the LDS staging of those waits for its data, and
+  //      with the fragments issued after it the block paid two round trips before its first MFMA
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  DenseLoader ld(a, inst, m_base + (lane & 15));
+  const bfx8* __restrict__ Bp = reinterpret_cast<const bfx8*>(a.w[inst]);
+  const int K32 = (a.K + 31) / 32, kg = 8 * (lane >> 4);
+  const int ks_lo = (K32 * wave) / 8, ks_hi = (K32 * (wave + 1)) / 8;
+  bfx8 af[kFoldU], bf[kFoldU];
+  auto load_batch = [&](int ks) {
+#pragma unroll
+    for (int u = 0; u < kFoldU; ++u) {
+      const bool kok = ks + u < ks_hi;
+      af[u] = kok ? ld.frag((ks + u) * 32 + kg) : zero8();
+      bf[u] = kok ? Bp[((int64_t)(ks + u) * a.N16 + nt) * 64 + lane] : zero8();
+    }
+  };
+  load_batch(ks_lo);
   int e0 = 0;                                   // the group's dQ epoch before this launch's tail
   if (dh_tile) e0 = __hip_atomic_load(f.dq_epoch + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool frames_duty = actor_inst && nt < h.act_E;
@@ -109,24 +127,11 @@ __global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_he
     if (h.wts != nullptr) tw = h.wts[b];
   }
 
-  // ---- h tile: split-K over 8 waves (igemm_kernel's Dense 1x1x1x1x8 tiling)
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  {
-    DenseLoader ld(a, inst, m_base + (lane & 15));
-    const bfx8* __restrict__ Bp = reinterpret_cast<const bfx8*>(a.w[inst]);
-    const int K32 = (a.K + 31) / 32, kg = 8 * (lane >> 4);
-    const int ks_lo = (K32 * wave) / 8, ks_hi = (K32 * (wave + 1)) / 8;
-    for (int ks = ks_lo; ks < ks_hi; ks += kFoldU) {
-      bfx8 af[kFoldU], bf[kFoldU];
+  // ---- h tile: split-K over 8 waves (igemm_kernel's Dense 1x1x1x1x8 tiling); batch 1 is in flight
+  for (int ks = ks_lo; ks < ks_hi; ks += kFoldU) {
+    if (ks != ks_lo) load_batch(ks);
 #pragma unroll
-      for (int u = 0; u < kFoldU; ++u) {
-        const bool kok = ks + u < ks_hi;
-        af[u] = kok ? ld.frag((ks + u) * 32 + kg) : zero8();
-        bf[u] = kok ? Bp[((int64_t)(ks + u) * a.N16 + nt) * 64 + lane] : zero8();
-      }
-#pragma unroll
-      for (int u = 0; u < kFoldU; ++u) acc = mfma16(af[u], bf[u], acc);
-    }
+    for (int u = 0; u < kFoldU; ++u) acc = mfma16(af[u], bf[u], acc);
   }
   if (wave > 0) {
 #pragma unroll
