@@ -283,8 +283,10 @@ class HipExecutor:
         self._wg_pending = None
         self._wg_plans: Dict[tuple, tuple] = {}
         # 128-row chunks per conv weight-gradient tile of the fused launch (summed in registers, one
-        # set of fp32 atomics per tile; DQN_WG_CHUNKS: measured 2 > 4 > 8, gpurun_out/r5c)
-        self.wg_conv_chunks = int(os.environ.get('DQN_WG_CHUNKS', '2'))
+        # set of fp32 atomics per tile; DQN_WG_CHUNKS). With both chunks' loads issued up front
+        # (wgrad_tile's two-slot ring): 3 > 2 > 4 on the flagship (15.33k / 15.04k / 14.76k), 3 = 2 on
+        # Rainbow (profiles/r5_late_ab.md); before the ring 2 > 4 > 8 (gpurun_out/r5c)
+        self.wg_conv_chunks = int(os.environ.get('DQN_WG_CHUNKS', '3'))
         # fc jobs interleaved with the weight-gradient tiles in that launch (optim_pack.h wg_mix): measured
         # 14.8k -> 13.6k SGD steps/s on the flagship (the tiles, on the critical path, then finish later;
         # gpurun_out/r5a/ab.jsonl), so off unless DQN_WG_MIX=1

@@ -106,13 +106,13 @@ def main():
     # (the previous single launch reads every gradient from the flat buffer: fc jobs as well)
     jall = ex._upd_jobs(dev)
     out['fused_old'] = timeit(lambda: launch(jall, fca, sample=smp))
-    for cc in (1, 4):                     # chunks per conv tile (the executor's default: 2)
+    for cc in (2, 4):                     # chunks per conv tile (the executor default: 3)
         ex.wg_conv_chunks = cc
         ex._wg_plans = {}
         pl2, n2, j2, _, _, _ = ex._wg_plan(wg, net.grad, dev)
         out['F_chunks%d' % cc] = timeit(lambda: launch(j2, fca, pl2.data_ptr(), n2, sample=smp))
         out['wg_blocks_chunks%d' % cc] = n2
-    ex.wg_conv_chunks = 2
+    ex.wg_conv_chunks = int(os.environ.get("DQN_WG_CHUNKS", "3"))
     ex._wg_plans = {}
     plan, nwg, jobs, nfc, _, _ = ex._wg_plan(wg, net.grad, dev)
     if os.environ.get('DQN_OPT_PROF'):
