@@ -497,9 +497,10 @@ class HipExecutor:
             # end of the grid: first measured +1.2% for noisy nets, whose fc jobs run ~10 us each and
             # kept them queued to ~45 us; -0.2..-1.0% for the plain nets (profiles/r4_dep_first_ab.txt)
             # DQN_DEP_AT=n: the dependent jobs after the first n fc jobs (A/B of the grid order). Noisy
-            # nets: after 300 of their ~1.6k fc jobs (+1-2% Rainbow over right after the tiles,
-            # gpurun_out/r5j, r5k); plain nets: at the end (0 / 200 / 400 / 600 measured the same)
-            lead = min(300, len(fcj)) if self.noisy else len(fcj)
+            # nets: after 500 of their ~1.6k fc jobs (round 5: 300 was +1-2% over right after the tiles,
+            # gpurun_out/r5j, r5k; with the earlier-finishing tiles 500 beat 300 in 4 of 4 rounds,
+            # +0.3-1.0%, profiles/r5_late_ab.md); plain nets: at the end (0 / 150 / 400 measured no better)
+            lead = min(500, len(fcj)) if self.noisy else len(fcj)
             if os.environ.get('DQN_DEP_AT'):
                 lead = max(0, min(len(fcj), int(os.environ['DQN_DEP_AT'])))
             table, deps = list(fcj[:lead]), []
