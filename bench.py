@@ -99,7 +99,13 @@ def main():
                     help='SGD steps per HIP-graph launch (Learner.step_many: the same per-step work, one host '
                          'launch per G steps -- the inter-graph gap is amortised); 1 = one graph per step '
                          '(profiles/r4_graph_steps.txt: 16 / 32 measured 0.5-1%% above 8)')
+    ap.add_argument('--dp_path', type=int, default=0,
+                    help='1 (one GPU only): run the data-parallel step at W = 1 -- a one-rank RCCL group with every '
+                         'DP code path on (in-graph xgmi gather + in-launch gradient exchange): the per-rank cost of '
+                         'the multi-GPU step without peers')
     args = ap.parse_args()
+    if args.dp_path and args.gpus != 1:
+        ap.error('--dp_path is the one-rank probe of the DP step (--gpus 1)')
     if args.dtype is None:             # BASELINE.json config 5: "Rainbow ... fp16 conv MFMA path"
         args.dtype = VARIANT_DTYPE.get(args.variant, 'bf16')
     if args.gpus < 1:
@@ -127,7 +133,7 @@ def main():
                                                     args.update_freq, VARIANTS[args.variant] + ' ' + args.extra))
     if args.network not in ('nature', 'cnn'):
         cfg = cfg.replace(network=args.network)
-    ctx = init_distributed(cfg, device='cuda')
+    ctx = init_distributed(cfg, device='cuda', force_dp=bool(args.dp_path))
     dev = ctx.device
     assert dev.type == 'cuda', 'bench.py needs a GPU'
     if ctx.enabled and ctx.ranks_share_gpu() and ctx.backend != 'gloo':
@@ -253,7 +259,8 @@ def main():
             'samples_per_sec': round(sps * args.batch, 1),
             'config': {'model': 'nature-cnn' if args.network == 'nature' else args.network,
                        'global_batch': args.batch * ctx.world_size, 'seq_len': None,
-                       'parallelism': 'dp%d' % ctx.world_size, 'per_gpu_batch': args.batch,
+                       'parallelism': 'dp%d' % ctx.world_size + (' (DP step forced at one rank)' if ctx.force_dp else ''),
+                       'per_gpu_batch': args.batch,
                        'frames_per_state': 4, 'optimizer': cfg.optimizer + '(tf)', 'executor': net.executor.name,
                        'hip_graph': bool(args.graph), 'steps_per_graph_launch': G,
                        'timed_launches': {'graph_launches_of_G': n_launch, 'single_step_graphs': n_single},
@@ -269,6 +276,7 @@ def main():
                        'xgmi_vs_rccl_max_rel': (learner.reducer.timings or {}).get('xgmi_vs_rccl_max_rel'),
                        'rank_devices': dev_ids, 'ranks_share_gpu': len(set(dev_ids)) < len(dev_ids),
                        'lowrank_dense': learner._lowrank is not None,
+                       'dp_fused_update': bool(getattr(learner, '_dp_fused', False)),
                        'allreduce_ranges': learner._ar_ranges or None,
                        'allreduce_peer_timeouts': not xgmi_ok,
                        'world_size': ctx.world_size, 'dist_backend': ctx.backend,

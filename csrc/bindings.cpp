@@ -150,10 +150,13 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                 c10::optional<torch::Tensor> noise_dst, std::vector<int64_t> sample, std::vector<int64_t> per_p,
                 std::vector<double> per_f, c10::optional<torch::Tensor> tnoise, c10::optional<torch::Tensor> teff,
                 c10::optional<torch::Tensor> tpk, c10::optional<torch::Tensor> noise_rng, std::vector<int64_t> fc,
-                int64_t part, int64_t wg, int64_t wg_blocks, int64_t wg_jobs, int64_t tsg, bool no_pack) {
+                int64_t part, int64_t wg, int64_t wg_blocks, std::vector<int64_t> dp, int64_t tsg, bool no_pack) {
   // wg / wg_blocks: the launch also computes the grouped weight gradients -- a device WgradGroup
   // (qnet_wgrad_plan) whose wg_blocks tiles follow the lead block; jobs with dep >= 0 wait for
   // their member (needs fc: the launch forms the fc gradients from FcFuse rows)
+  // dp: [] or [device DpExchange (xgmi_dpx_args), first, n, blocks] (WG launches under data
+  //   parallelism): the job table's dependent jobs [first, first + n) sum their gradient over every
+  //   rank inside the launch, run by `blocks` blocks
   // part: 0 or the base of the grouped conv wgrad's partial buffer (jobs with part_n > 0 sum it)
   // fc: [] or [x ptr, dh ptr, M, ldx, ldh]: the launch forms the fc weight / bias gradient of the
   // jobs carrying a dH column from those act_t rows (optim.hip FcFuse) instead of reading `grad`
@@ -295,10 +298,17 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
   }
   TORCH_CHECK(ticket.numel() >= 2, "optim_pack: ticket[1] is the slot flag word");
   if (wg != 0) {
-    TORCH_CHECK(wg_blocks >= 1 && wg_blocks <= 16384 && !fc.empty() && op >= 0 && part == 0 && (wg % 16) == 0 &&
-                    wg_jobs >= 0 && wg_jobs <= jobs.numel() / upd_job_ints(),
-                "optim_pack wg: needs fc rows and an update, no partials; 0 <= wg_jobs <= jobs (the leading fc "
-                "jobs interleaved with the tiles; 0 = tiles first)");
+    TORCH_CHECK(wg_blocks >= 1 && wg_blocks <= 16384 && !fc.empty() && op >= 0 && part == 0 && (wg % 16) == 0,
+                "optim_pack wg: needs fc rows and an update, no partials");
+  }
+  dqn::DpLaunch dpl{nullptr, 0, 0, 0};
+  if (!dp.empty()) {
+    const int64_t nj = jobs.numel() / upd_job_ints();
+    TORCH_CHECK(wg != 0 && dp.size() == 4 && dp[0] != 0 && (dp[0] % 16) == 0 && dp[2] >= 1 &&
+                    dp[2] <= dqn::kDpxMaxSlots && dp[1] >= 0 && dp[1] + dp[2] <= nj && dp[3] >= 1 && dp[3] <= dp[2],
+                "optim_pack dp: [device DpExchange, first, n, blocks] with a WG launch, the dependent jobs inside "
+                "the table, 1 <= blocks <= n <= DPX_MAX_SLOTS");
+    dpl = dqn::DpLaunch{P<const dqn::DpExchange*>(dp[0]), (int)dp[1], (int)dp[2], (int)dp[3]};
   }
   float h[9];
   for (int i = 0; i < 9; ++i) h[i] = (float)hp[i];
@@ -309,7 +319,7 @@ void optim_pack(int64_t op, torch::Tensor w, torch::Tensor grad, torch::Tensor s
                     tgtp, (int)target_freq, (int)max_grid, nz, ef, gnz, ndst, nn, sample.empty() ? nullptr : &smp,
                     per_p.empty() ? nullptr : &per, tnz, tef, tpkp, nrng, fc.empty() ? nullptr : &ff,
                     reinterpret_cast<const float*>(part), reinterpret_cast<const void*>(wg), (int)wg_blocks,
-                    (int)wg_jobs, reinterpret_cast<void*>(tsg), no_pack ? 1 : 0, cur_stream());
+                    dp.empty() ? nullptr : &dpl, reinterpret_cast<void*>(tsg), no_pack ? 1 : 0, cur_stream());
 }
 
 void noise_normal(torch::Tensor out0, c10::optional<torch::Tensor> out1, torch::Tensor rng) {
@@ -682,6 +692,29 @@ torch::Tensor xgmi_gather_args(std::vector<int64_t> srcs, std::vector<int64_t> o
   return out;
 }
 
+// the DpExchange bytes (CPU uint8) of an exchange channel: every rank's inbox / signal-word base
+// (peer-mapped), this rank's per-slot counters and error word; the fused update launch reads them
+// from device memory (copied there by the caller)
+torch::Tensor xgmi_dpx_args(std::vector<int64_t> inbox, std::vector<int64_t> sig, int64_t seq, int64_t err,
+                            int64_t rank, int64_t world, int64_t slots, int64_t cap) {
+  TORCH_CHECK(world >= 1 && world <= dqn::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi dpx: rank/world");
+  TORCH_CHECK((int64_t)inbox.size() == world && (int64_t)sig.size() == world && seq && err, "xgmi dpx: pointers");
+  TORCH_CHECK(slots >= 1 && slots <= dqn::kDpxMaxSlots && 2 * world * slots * (int64_t)dqn::kDpxSlotElems <= cap,
+              "xgmi dpx: slots exceed the channel's inbox");
+  dqn::DpExchange x{};
+  for (int i = 0; i < world; ++i) {
+    TORCH_CHECK(inbox[i] && sig[i] && (inbox[i] & 15) == 0, "xgmi dpx: null / misaligned peer pointer");
+    x.inbox[i] = reinterpret_cast<float*>(inbox[i]);
+    x.sig[i] = reinterpret_cast<uint32_t*>(sig[i]);
+  }
+  x.seq = reinterpret_cast<uint32_t*>(seq);
+  x.err = reinterpret_cast<int*>(err);
+  x.rank = (int)rank; x.world = (int)world; x.slots = (int)slots;
+  auto out = torch::empty({(int64_t)sizeof(x)}, torch::kUInt8);
+  std::memcpy(out.data_ptr(), &x, sizeof(x));
+  return out;
+}
+
 // ---------------------------------------------------------------- fused MLP
 // ints: [L, A, P, Hs, Ds, sw, B, double, huber, fin x4, fout x4, act x4, w_off x4, b_off x4]
 // ptrs: [w_on, w_tg, x, xn, act, rew, done, gam, wts, loss, prio, grad, q_out] (0 = unused)
@@ -749,6 +782,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("bf16"), pybind11::arg("blocks"), pybind11::arg("ranges") = std::vector<int64_t>{});
   m.def("xgmi_allgather", &xgmi_allgather);
   m.def("xgmi_gather_args", &xgmi_gather_args);
+  m.def("xgmi_dpx_args", &xgmi_dpx_args);
+  m.attr("DPX_MAX_SLOTS") = dqn::kDpxMaxSlots;
+  m.attr("DPX_SLOT_ELEMS") = dqn::kDpxSlotElems;
   m.attr("XGMI_MAX_BLOCKS") = dqn::kXgmiMaxBlocks;
   m.attr("XGMI_SIG_WORDS") = dqn::kXgmiMaxRanks * dqn::kXgmiMaxBlocks;
   m.def("replay_gather_frames", &replay_gather_frames);
@@ -769,7 +805,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("noise_dst"), pybind11::arg("sample"), pybind11::arg("per_p"), pybind11::arg("per_f"),
         pybind11::arg("tnoise"), pybind11::arg("teff"), pybind11::arg("tpk"), pybind11::arg("noise_rng"),
         pybind11::arg("fc"), pybind11::arg("part"), pybind11::arg("wg") = 0, pybind11::arg("wg_blocks") = 0,
-        pybind11::arg("wg_jobs") = 0, pybind11::arg("tsg") = 0, pybind11::arg("no_pack") = false);
+        pybind11::arg("dp") = std::vector<int64_t>{}, pybind11::arg("tsg") = 0, pybind11::arg("no_pack") = false);
   m.def("noise_normal", &noise_normal);
   m.attr("UPD_JOB_INTS") = upd_job_ints();
   m.def("optim_prof", []() {

@@ -53,13 +53,15 @@ struct FcFuse {
   const void* dh;
   int M, ldx, ldh;
 };
+// dp: nullptr or a dqn::DpLaunch (WG launches under data parallelism: the dependent jobs exchange
+// their gradients with every rank inside the launch, see DpExchange below)
 void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, float* beta_pow, int64_t* step,
                        int32_t* ticket, const float* hp9, float lr, float reg, int reg_end, float grad_scale,
                        const void* jobs, int njobs, void* packed, float* tgt, void* tgt_packed, int tfreq, int max_grid,
                        const float* noise, float* eff, const float* gnoise, float* noise_dst, int noise_n,
                        const dqn::TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff, void* tpk,
                        int64_t* noise_rng, const FcFuse* fc, const float* part, const void* wg, int wg_blocks,
-                       int wg_jobs, void* tsg, int no_pack, hipStream_t st);
+                       const void* dp, void* tsg, int no_pack, hipStream_t st);
 // 1 when this build's optimizer launch can form the fc weight gradient itself (16-bit builds)
 int optim_fc_fuse();
 // probe launches (DQN_OPT_PROF=1): per-block [start, ready, end] s_memrealtime stamps of the last launch
@@ -122,6 +124,29 @@ struct XgmiGatherArgs {
 };
 }  // namespace dqn
 int launch_xgmi_allgather(const dqn::XgmiGatherArgs& a, int blocks, hipStream_t st);
+namespace dqn {
+// Data-parallel exchange INSIDE the fused weight-gradient + update launch (optim_pack.h kModeDp):
+// every update job whose gradient the launch's own weight-gradient tiles produce (conv layers,
+// output layer) pushes its 2048-value gradient slot into every rank's inbox, raises its flag in
+// every rank's signal words, waits for all ranks' flags and sums the W slots in rank order
+// (bit-identical on every rank), then updates. No all-reduce launch between backward and update.
+constexpr int kDpxMaxSlots = 1024;     // dependent update jobs per launch (signal words per source rank)
+constexpr int kDpxSlotElems = 2048;    // one job's gradient: a 32 x 64 tile or a <= 2048-element chunk
+struct DpExchange {
+  float* inbox[kXgmiMaxRanks];     // every rank's inbox, peer-mapped: [2 parities][world][slots][kDpxSlotElems]
+  uint32_t* sig[kXgmiMaxRanks];    // every rank's signal words [kXgmiMaxRanks (source)][kDpxMaxSlots]
+  uint32_t* seq;                   // this rank's per-slot call counters [kDpxMaxSlots]
+  int* err;                        // [4]: the first timed-out wait (phase kXgmiPhaseDpx), 0 = none
+  int rank, world, slots;          // slots: inbox capacity in jobs per source rank
+};
+// launch-time view: the device descriptor + where the dependent jobs sit in the job table
+// ([first, first + n)) and how many blocks run them (blocks < n: each block takes jobs
+// first + b, first + b + blocks, ... in order -- ranks sharing one GPU in the rehearsals)
+struct DpLaunch {
+  const DpExchange* x;
+  int first, n, blocks;
+};
+}  // namespace dqn
 
 // Asynchronous parameter server over xGMI peer memory, csrc/kernels/async_ps.hip.
 void launch_ps_push(const float* grad, float* slot, long n, uint64_t* push_word, int64_t* seq, int kind,

@@ -154,15 +154,13 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
                        int max_grid, const float* noise, float* eff, const float* gnoise, float* noise_dst,
                        int noise_n, const TrunkSample* smp, const PerStep* per, const float* tnoise, float* teff,
                        void* tpk, int64_t* noise_rng, const FcFuse* fc, const float* part, const void* wg,
-                       int wg_blocks, int wg_jobs, void* tsg, int no_pack, hipStream_t st) {
+                       int wg_blocks, const void* dp, void* tsg, int no_pack, hipStream_t st) {
   OptPackLaunch L{};
   OptHP& h = L.h;
   h.lr = lr; h.reg = reg; h.grad_scale = grad_scale; h.reg_end = reg_end;
   h.momentum = hp9[0]; h.rho = hp9[1]; h.rms_mom = hp9[2]; h.rms_eps = hp9[3];
   h.b1 = hp9[4]; h.b2 = hp9[5]; h.adam_eps = hp9[6]; h.ad_rho = hp9[7]; h.ad_eps = hp9[8];
   h.prof = optim_prof_buffer();
-  static const int dep_fence = getenv("DQN_FENCE_TAILS") != nullptr ? 1 : 0;
-  h.dep_fence = dep_fence;
   h.tsg = tsg;
   h.no_pack = no_pack;
   // one block per job up to max_grid (grid-stride beyond it); block 0 (+1 sampler block when the
@@ -175,13 +173,19 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   // WG: the launch also computes the grouped weight gradients (tiles after the lead block)
   const bool wgm = wg != nullptr && ff.x != nullptr && op >= 0;
   if (wg != nullptr && !wgm) return;      // (binding checks: a WG launch needs FcFuse rows and an update)
-  // wg_jobs > 0 (WG): the table's first wg_jobs jobs (the fc jobs) interleave with the tiles
+  // DP (WG under data parallelism): the dependent jobs run in dp->blocks blocks
+  const DpLaunch dpl = (wgm && dp != nullptr) ? *reinterpret_cast<const DpLaunch*>(dp) : DpLaunch{nullptr, 0, 0, 0};
+  if (dp != nullptr && (dpl.x == nullptr || dpl.blocks < 1 || dpl.blocks > dpl.n || dpl.first < 0 ||
+                        dpl.first + dpl.n > njobs || dpl.n > kDpxMaxSlots))
+    return;                               // (binding checks)
+  const int nblk_jobs = dpl.x != nullptr ? njobs - dpl.n + dpl.blocks : njobs;
   // + the lead block (sampler / closer) + the weight-gradient tiles
-  L.grid = (njobs < cap ? njobs : cap) + (L.smp.size != nullptr || L.per.sum != nullptr || wgm ? 1 : 0) +
+  L.grid = (nblk_jobs < cap ? nblk_jobs : cap) + (L.smp.size != nullptr || L.per.sum != nullptr || wgm ? 1 : 0) +
            (wgm ? wg_blocks : 0);
   // (a noisy net always passes its noise sample; plain nets pass none)
   L.mode = (noise != nullptr ? kModeNoisy : 0) | (tnoise != nullptr ? kModeTmix : 0) |
-           (L.per.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0) | (wgm ? kModeWg : 0);
+           (L.per.sum != nullptr ? kModePer : 0) | (ff.x != nullptr && op >= 0 ? kModeFc : 0) | (wgm ? kModeWg : 0) |
+           (dpl.x != nullptr ? kModeDp : 0);
   // few work blocks (16-bit builds, the common optimizers): no spills, returning-ticket close
   L.few = !DQN_ACT_F32 && !wgm && ff.x == nullptr && njobs <= 256 && (op == 0 || op == 3 || op == 7);
 #if DQN_ACT_F32
@@ -197,7 +201,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
   L.noise = noise; L.eff = eff; L.gnoise = gnoise; L.noise_dst = noise_dst; L.noise_n = noise_n;
   L.tnoise = tnoise; L.teff = teff; L.tpk = reinterpret_cast<act_t*>(tpk); L.noise_rng = noise_rng; L.ff = ff;
   L.part = part; L.wg = reinterpret_cast<const WgradGroup*>(wg); L.wg_blocks = wgm ? wg_blocks : 0;
-  L.wg_mix = wgm && wg_jobs > 0 && wg_jobs <= njobs ? wg_jobs : 0;
+  L.dp = dpl;
   switch (op) {
     case -1: optim_pack_op<-1>(L); break;
     case 0: optim_pack_op<0>(L); break;

@@ -13,6 +13,7 @@
 #include "sample_dev.h"
 #include "sumtree_dev.h"
 #include "wgrad_dev.h"
+#include "xgmi_dev.h"
 #include "../include/dqn_kernels.h"
 
 namespace dqn {
@@ -21,7 +22,6 @@ struct OptHP {
   float lr, reg, grad_scale;
   float momentum, rho, rms_mom, rms_eps, b1, b2, adam_eps, ad_rho, ad_eps;
   int reg_end;
-  int dep_fence;             // A/B knob (DQN_FENCE_TAILS=1): dependent jobs acquire-fence + plain loads
   // noisy nets, factorised target fc (UpdJob.eff bit 1): the target's packed fc weights hold mu
   // fragments and this buffer (the packed layout) its sigma fragments, written only when they change
   // (a sync step, or a mix-only call on the target); the target forward mixes the noise in itself
@@ -191,7 +191,9 @@ DQN_DEV void upd4(float* w, const float* g, float* a, float* b, int64_t k0flat, 
 // kModeFew: a launch of few work blocks (the second launch of a split update): 4 waves / SIMD
 // (128 VGPRs: no spills in the item body, occupancy is moot) and a returning arrival ticket per
 // block -- the last block to arrive closes the launch, nobody polls.
-constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8, kModeWg = 16, kModeFew = 32;
+// kModeDp (with kModeWg, data parallelism): the dependent jobs sum their gradient slots over every rank
+// inside the launch (DpExchange, dqn_kernels.h): no all-reduce launch between backward and update.
+constexpr int kModeNoisy = 1, kModeTmix = 2, kModePer = 4, kModeFc = 8, kModeWg = 16, kModeFew = 32, kModeDp = 64;
 
 // A static LDS buffer only in the instantiations that use one (ALLOC; TAG keeps two buffers of one
 // size apart): the WG launches must carry no static LDS (see smem below).
@@ -207,7 +209,7 @@ struct OptShm<false, N, TAG> {
   DQN_DEV static unsigned char* get() { return nullptr; }
 };
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? (DQN_ACT_F32 ? 4 : (MODE & kModeFc) ? 8 : 5) : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+__global__ void __launch_bounds__(kPackThreads, (MODE & kModeDp) ? 4 : (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? (DQN_ACT_F32 ? 4 : (MODE & kModeFc) ? 8 : 5) : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,
@@ -215,7 +217,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                   float* __restrict__ eff, const float* __restrict__ gnoise, float* __restrict__ noise_dst,
                   int noise_n, TrunkSample smp, PerStep per, const float* __restrict__ tnoise,
                   float* __restrict__ teff, act_t* __restrict__ tpk, int64_t* __restrict__ noise_rng, FcFuse ff,
-                  const float* __restrict__ part, const WgradGroup* __restrict__ wg, int wg_blocks, int wg_mix) {
+                  const float* __restrict__ part, const WgradGroup* __restrict__ wg, int wg_blocks, DpLaunch dp) {
   // OP < 0: no optimizer update, only (noisy mix +) pack of W into `packed` / `eff`.
   // gnoise (noisy nets): the sample the forward used; sigma's gradient is then derived here,
   // dL/dsigma = dL/dW_eff * f(gnoise_in) f(gnoise_out) from the mu-slot gradient (identical
@@ -231,6 +233,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   constexpr bool FC = (MODE & kModeFc) != 0 && !DQN_ACT_F32 && OP >= 0;
   constexpr bool WG = (MODE & kModeWg) != 0 && !DQN_ACT_F32 && OP >= 0;
   constexpr bool FEW = (MODE & kModeFew) != 0 && OP >= 0;
+  constexpr bool DP = WG && (MODE & kModeDp) != 0;
   // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
   const bool tmix = TMIX && UPD && tnoise != nullptr && tgt != nullptr;
   // LDS: the sampler block's scratch (the update items exchange through DPP); WG launches carve
@@ -274,16 +277,10 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     // scalar load there is waited for in order (s_waitcnt lgkmcnt(0)), ~3 us of dependent round
     // trips before a tile issued its first operand load (probe_split timeline: tile blocks ran
     // 9.0 us of which 5.6 us inside the tile)
-    // (the block roles of the WG grid, as below: wg_mix > 0 interleaves the first wg_mix jobs)
-    const int p = (int)blockIdx.x - 1, S = wg_blocks + wg_mix;
-    int tb = -1;
-    if (p >= 0 && wg_mix > 0 && p < S) {
-      const int q = p * wg_blocks / S, q1 = (p + 1) * wg_blocks / S;
-      if (q1 > q) tb = q;
-    } else if (p >= 0 && p < wg_blocks) {
-      tb = p;
-    }
-    if (tb >= 0) {
+    // (block roles of the WG grid: the lead block, the tiles [1, 1 + wg_blocks), then the job blocks;
+    //  round 5 measured the fc jobs interleaved with the tiles: 14.8k -> 13.6k SGD steps/s, removed)
+    const int tb = (int)blockIdx.x - 1;
+    if (tb >= 0 && tb < wg_blocks) {
       wg_tile_run(tb);
       __syncthreads();
       if (threadIdx.x == 0)                     // the end-of-launch arrival (see the closing step)
@@ -301,25 +298,11 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // the sampler is block 0: dispatched first, so its serial chain overlaps the whole update
   const bool sampler = smp_on && blockIdx.x == 0;
   const int nwork = (int)gridDim.x - (extra ? 1 : 0) - wg0;
-  // block roles after the lead block. WG: the weight-gradient tiles [0, wg_blocks) and the job table
-  // (wg_mix > 0: its first wg_mix jobs -- the fc jobs, independent of the tiles -- interleaved with
-  // the tiles over the first wg_blocks + wg_mix positions, Bresenham-spaced: the latency-bound tiles
-  // and the bandwidth-bound fc jobs share the CUs from the launch start instead of the tiles holding
-  // most slots for their whole span; the range-dependent jobs stay after every tile)
-  // (the tile blocks themselves returned at the top of the kernel)
-  int wid = (int)blockIdx.x - (extra ? 1 : 0) - wg0;          // work index of an update block
-  if constexpr (WG) {
-    const int p = (int)blockIdx.x - 1;
-    const int S = wg_blocks + wg_mix;
-    if (p >= 0 && wg_mix > 0 && p < S) {
-      const int q = p * wg_blocks / S, q1 = (p + 1) * wg_blocks / S;
-      wid = q1 > q ? -1 : p - q;
-    } else if (p >= 0 && p < wg_blocks) {
-      wid = -1;
-    } else {
-      wid = p - wg_blocks;
-    }
-  }
+  // block roles after the lead block. WG: the weight-gradient tiles [0, wg_blocks) (they returned at
+  // the top of the kernel), then the job table, one job per block (DP: the dependent jobs
+  // [dp.first, dp.first + dp.n) run in dp.blocks blocks)
+  const int wid = WG ? ((int)blockIdx.x - 1 < wg_blocks ? -1 : (int)blockIdx.x - 1 - wg_blocks)
+                     : (int)blockIdx.x - (extra ? 1 : 0) - wg0;      // work index of an update block
   float lr_t = h.lr;
   // the step words, read once at launch start: block 0's closing step writes their successors from
   // these registers (a load -> store round trip there sat on the launch's critical path); nothing
@@ -345,7 +328,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   const bool wtwo = OP != 7 || flag_raw != 0;                                  // (momentum-0 RMSProp: flagged)
   constexpr bool TWO_LD = TWO && OP != 7;                                      // ... and read
   constexpr bool ONE = UPD && OP != 0;
-  const int t = threadIdx.x;
+  int t = threadIdx.x;            // (DP job loop: re-derived per job, see there)
   int64_t* prof = (h.prof != nullptr && t == 0 && blockIdx.x < 2) ? h.prof + 8 * blockIdx.x : nullptr;
 #define OPT_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memtime()
   OPT_MARK(0);
@@ -497,6 +480,92 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
   // vmcnt wait between loads and serialise the item on memory latency.)
   bool gsc1 = false;             // WG dependent job: its gradient is read with sc1 loads
+  // ---- DP: the cross-rank sum of dependent job `dslot`'s gradient (this thread's 4 values g[]).
+  // Push: my values into row `rank` of every rank's inbox (remote xGMI stores, posted), publish
+  // (system-scope fence + release flag store into every rank's signal word of this slot), wait for
+  // every rank's flag in my own signal words (local polls, bounded), then sum the W rows of my inbox
+  // in rank order: the same bytes in the same order on every rank, so the replicas stay
+  // bit-identical. Inbox parity alternates per call of a slot: a rank reaches call k + 2 of a slot
+  // only after every rank flagged call k + 1, i.e. finished reading call k (stream order).
+  int dslot = -1;
+  float gdp[4] = {0.f, 0.f, 0.f, 0.f};
+  auto dp_sum = [&](float* g) {
+    if constexpr (DP) {
+      const DpExchange& X = *dp.x;
+      const int W = X.world, r = X.rank;
+      const uint32_t k = X.seq[dslot];
+      const long stride = (long)X.slots * kDpxSlotElems;                  // one source rank's rows
+      const long base = (long)(k & 1u) * W * stride + (long)dslot * kDpxSlotElems + 4 * t;
+      const float4 v = make_float4(g[0], g[1], g[2], g[3]);
+      for (int q = 0; q < W; ++q) {
+        const int d = r + q < W ? r + q : r + q - W;                      // (peers staggered across links)
+        *reinterpret_cast<float4*>(X.inbox[d] + base + (long)r * stride) = v;
+      }
+      __threadfence_system();
+      __syncthreads();
+      if (t < W) store_rel(X.sig[t] + r * kDpxMaxSlots + dslot, k + 1u);
+      if (t < W) {
+        const uint32_t* f = X.sig[r] + t * kDpxMaxSlots + dslot;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t seen;
+        while ((int32_t)((seen = load_acq(f)) - (k + 1u)) < 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kXgmiTimeoutTicks) {   // flag, do not hang
+            const int code = (int)(0x80000000u | ((uint32_t)kXgmiPhaseDpx << 24) | ((uint32_t)t << 16) | (uint32_t)dslot);
+            if (atomicCAS(X.err, 0, code) == 0) {
+              X.err[1] = (int)(k + 1u);
+              X.err[2] = (int)seen;
+              X.err[3] = (int)k;
+            }
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");                   // system scope, every thread
+      const float* in = X.inbox[r] + base;
+      float4 acc = *reinterpret_cast<const float4*>(in);
+      for (int q0 = 1; q0 < W; q0 += 2) {                               // 2 rows in flight, summed in order
+        float4 x[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          x[u] = *reinterpret_cast<const float4*>(in + (long)(q0 + u < W ? q0 + u : 0) * stride);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (q0 + u >= W) break;
+          acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
+        }
+      }
+      g[0] = acc.x; g[1] = acc.y; g[2] = acc.z; g[3] = acc.w;
+      if (t == 0) X.seq[dslot] = k + 1u;             // (every thread read it before the barriers)
+    } else {
+      (void)g;
+    }
+  };
+  // dependent job jb's summed gradient into gdp (this thread's 4 values in the item's thread map),
+  // before the item issues its own loads: nothing else is live across the exchange's waits
+  auto dp_grad = [&](const UpdJob& jb) {
+    int64_t d0;
+    bool ok[4];
+    if (jb.kind == 1) {
+      d0 = 4 * t;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ok[j] = 4 * t + j < jb.K;
+    } else {
+      const int wv = t >> 6, l = t & 63;
+      const int k = jb.k0 + (wv >> 1) * 8 + (l & 7), n = jb.n0 + (wv & 1) * 32 + (l >> 3) * 4;
+      d0 = (int64_t)k * jb.N + n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ok[j] = k < jb.K && n + j < jb.N;
+    }
+    // (sc1: produced by this launch's tiles, see dep_wait; out-of-range lanes read element 0)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G + jb.src_off), (short)0,
+                                                                        0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      gdp[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (ok[j] ? d0 + j : 0)), 0, 16));
+    dp_sum(gdp);
+  };
   auto item = [&](const UpdJob& jb, auto al_c, auto nz_c, auto dg_c) {
     // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read
     constexpr bool AL = decltype(al_c)::value, NZ = decltype(nz_c)::value, DG = decltype(dg_c)::value;
@@ -654,7 +723,16 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
         }
       } else if (!fcj) {
         if (gsc1) {                                       // produced in this launch (see the dep wait)
-          sc1_ld(G, mo, g);
+          if constexpr (DP) {
+            if (dslot >= 0) {                             // block-uniform: the sum over every rank, formed
+#pragma unroll                                            // before the item's loads (dp_grad)
+              for (int j = 0; j < 4; ++j) g[j] = gdp[j];
+            } else {
+              sc1_ld(G, mo, g);
+            }
+          } else {
+            sc1_ld(G, mo, g);
+          }
         } else {
           ld(G, mo, g);
         }
@@ -783,41 +861,64 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     // (the tile blocks ran wg_tile_run at the top of the kernel and returned)
   }
 #endif
+  // a job whose gradient a weight-gradient range of this launch produces (its blocks come after every
+  // tile in the grid, so the tiles are resident or done: the wait ends)
+  auto dep_wait = [&](int d) {
+#if !DQN_ACT_F32
+    if constexpr (WG) {
+      if (threadIdx.x == 0) {
+        const int m = d / kWgSlots;
+        const int want = wg->nblk[m] / wg->gy[m];        // tiles per K-range
+        const int32_t* c = wg->done + kTicketStride * (kMaxWgradMembers + d);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          __builtin_amdgcn_s_sleep(2);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s: flag, do not hang
+            ticket[kErrFlag] = 1;
+            break;
+          }
+        }
+        // (no acquire fence: the item reads this gradient with agent-scope sc1 loads, and the
+        //  tiles produced it by memory-side atomics / sc1 stores; the fence's L1 invalidate cost
+        //  ~1.7 us on the launch's critical path)
+      }
+      __syncthreads();
+      gsc1 = true;
+    }
+#else
+    (void)d;
+#endif
+  };
   if constexpr (FC) {
     // one job per block (the launcher sizes the grid for it): no job loop, so no per-thread loop
     // invariants are hoisted and kept live across the fc barriers
-    if (wid >= 0 && wid < njobs) {
-#if !DQN_ACT_F32
-      if constexpr (WG) {
-        // a job whose gradient a weight-gradient range of this launch produces (its blocks come
-        // after every tile in the grid, so the tiles are resident or done: the wait ends)
-        const int d = jobs[wid].dep;
-        if (d >= 0) {
-          if (threadIdx.x == 0) {
-            const int m = d / kWgSlots;
-            const int want = wg->nblk[m] / wg->gy[m];        // tiles per K-range
-            const int32_t* c = wg->done + kTicketStride * (kMaxWgradMembers + d);
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-              __builtin_amdgcn_s_sleep(2);
-              if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s: flag, do not hang
-                ticket[kErrFlag] = 1;
-                break;
-              }
-            }
-            // (no acquire fence: the item reads this gradient with agent-scope sc1 loads, and the
-            //  tiles produced it by memory-side atomics / sc1 stores; the fence's L1 invalidate cost
-            //  ~1.7 us on the launch's critical path)
-          }
-          if (h.dep_fence && threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          __syncthreads();
-          gsc1 = !h.dep_fence;
+    if constexpr (DP) {
+      // job-table positions: [0, first) one job per block, [first, first + blocks) the dependent-job
+      // blocks (each runs jobs first + b, first + b + blocks, ... in order: every rank's block b
+      // waits on the same slots in the same order), then the rest of the table one per block
+      // (one call site of the item: a second one cost ~50 VGPRs)
+      const bool dblk = wid >= dp.first && wid < dp.first + dp.blocks;
+      const int j0 = wid < dp.first || dblk ? wid : wid - dp.blocks + dp.n;
+      const int j1 = dblk ? dp.first + dp.n : j0 + 1, js = dblk ? dp.blocks : 1;
+      for (int ji = j0; wid >= 0 && ji < j1 && ji < njobs; ji += js) {
+        // (t opaque per job: the item's thread-map values are recomputed instead of hoisted out of the
+        //  loop and kept live across it -- +17 VGPRs and scratch spills otherwise)
+        asm volatile("" : "+v"(t));
+        const int d = jobs[ji].dep;
+        if (d >= 0) dep_wait(d);
+        if (dblk) {
+          DQN_ASSERT(d >= 0 && ji - dp.first < dp.x->slots);
+          dslot = ji - dp.first;
+          dp_grad(jobs[ji]);
         }
+        run(ji);
+        if (dblk) __syncthreads();                        // (the next job's exchange reuses the slots)
       }
-#endif
+    } else if (wid >= 0 && wid < njobs) {
+      if constexpr (WG) {
+        const int d = jobs[wid].dep;
+        if (d >= 0) dep_wait(d);
+      }
       run(wid);
     }
   } else {
@@ -919,7 +1020,7 @@ struct OptPackLaunch {
   const UpdJob* jobs; int njobs; act_t* packed; float* tgt; act_t* tgt_packed; int tfreq;
   const float* noise; float* eff; const float* gnoise; float* noise_dst; int noise_n;
   TrunkSample smp; PerStep per; const float* tnoise; float* teff; act_t* tpk; int64_t* noise_rng; FcFuse ff;
-  const float* part; const WgradGroup* wg; int wg_blocks; int wg_mix;
+  const float* part; const WgradGroup* wg; int wg_blocks; DpLaunch dp;
 };
 
 template <int N>
@@ -932,7 +1033,7 @@ void optim_pack_op(const OptPackLaunch& L) {
                                   L.s0, L.s1, L.beta_pow, L.step, L.ticket, L.h, L.jobs, L.njobs, L.packed, L.tgt, \
                                   L.tgt_packed, L.tfreq, L.noise, L.eff, L.gnoise, L.noise_dst, L.noise_n, L.smp, L.per, \
                                   L.tnoise, L.teff, L.tpk, L.noise_rng, L.ff, L.part, L.wg, L.wg_blocks, \
-                                  L.wg_mix)
+                                  L.dp)
   if constexpr (N < 0) {
     OPM(kModeNoisy);                                    // mix + pack only (noisy nets)
   } else {
@@ -958,6 +1059,9 @@ void optim_pack_op(const OptPackLaunch& L) {
         case 12: OPM(12); break; case 13: OPM(13); break; case 15: OPM(15); break;
         case 24: OPM(24); break; case 25: OPM(25); break; case 27: OPM(27); break;
         case 28: OPM(28); break; case 29: OPM(29); break; case 31: OPM(31); break;
+        // data parallelism: the WG modes with the in-launch gradient exchange
+        case 88: OPM(88); break; case 89: OPM(89); break; case 91: OPM(91); break;
+        case 92: OPM(92); break; case 93: OPM(93); break; case 95: OPM(95); break;
         default: break;
       }
     }

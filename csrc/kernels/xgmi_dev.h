@@ -27,7 +27,8 @@ DQN_DEV void signal_all(const XgmiArgs& a, int b, uint32_t val) {
 // Which wait of which call timed out (the error word's first report wins; err[1..3] then hold the
 // expected flag value, the value last seen and the call's per-block counter):
 //   err[0] = 1 << 31 | phase << 24 | peer << 16 | block
-constexpr int kXgmiPhaseReduceScatter = 1, kXgmiPhaseAllGather = 2, kXgmiPhaseGather = 3;
+// (kXgmiPhaseDpx: the in-launch gradient exchange of the fused update, optim_pack.h; block = job slot)
+constexpr int kXgmiPhaseReduceScatter = 1, kXgmiPhaseAllGather = 2, kXgmiPhaseGather = 3, kXgmiPhaseDpx = 4;
 
 // wait until every peer raised flag >= val for block b; false on timeout
 DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val, int phase) {

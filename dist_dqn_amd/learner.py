@@ -109,9 +109,18 @@ class Learner:
                 and getattr(config, 'overlap_allreduce', True) and hasattr(ex, 'lowrank_spec')
                 and getattr(config, 'allreduce_dtype', 'fp32') == 'fp32'):
             lr = ex.lowrank_spec(B, sigma_fused=network.fuses_sigma_grads(tfreq), fused_fc=self._defer_fc)
+        # data parallelism, fused step: the conv / output-layer weight gradients run inside the update
+        # launch as in one process, and its dependent update jobs sum them over the ranks in-launch (the
+        # xgmi transport's exchange channel, optim_pack.h kModeDp): no all-reduce launch, no separate
+        # weight-gradient launch. Needs the low-rank fc exchange (the fc gradient is then formed from
+        # every rank's rows inside the same launch).
+        fuse_wu = int(getattr(config, 'fuse_wgrad_update', 1))
+        want_dpx = bool(lr is not None and self._defer_fc and fuse_wu and hasattr(ex, 'can_defer_wgrad')
+                        and ex.can_defer_wgrad(B, sg) and config.allreduce in ('xgmi', 'auto'))
+        nslots = sum(1 for it in ex.upd_items if it[20] < 0) if want_dpx else 0
         self.reducer = GradAllReducer(self.ctx, network.grad, config.grad_bucket_mb,
                                       'rccl' if ps_client is not None else config.allreduce, config.allreduce_dtype,
-                                      gather_bytes=lr['gather_bytes'] if lr else 0)
+                                      gather_bytes=lr['gather_bytes'] if lr else 0, exchange_slots=nslots)
         self._lowrank = None
         self._ar_ranges = []
         if lr and self.reducer.in_graph and self.reducer.can_gather:
@@ -140,11 +149,18 @@ class Learner:
                                and network.fuses_update(tfreq) and hasattr(ex, 'can_det_wgrad')
                                and ex.can_det_wgrad(B))
         # the grouped conv / output-layer weight gradients run in the leading blocks of the fused
-        # update's first launch, beside the fc update (executor.can_defer_wgrad): one process only
-        # (DP all-reduces those gradients between the backward and the update)
-        self._defer_wgrad = bool(not self.ctx.enabled and ps_client is None and self._defer_fc
-                                 and not self._det_wgrad and int(getattr(config, 'fuse_wgrad_update', 1))
+        # update's first launch, beside the fc update (executor.can_defer_wgrad): one process, or data
+        # parallelism with the in-launch exchange (above)
+        dp_fused = bool(self.ctx.enabled and want_dpx and self._lowrank is not None
+                        and getattr(self.reducer.xgmi, 'dpx', None) is not None)
+        self._defer_wgrad = bool(((not self.ctx.enabled and ps_client is None) or dp_fused) and self._defer_fc
+                                 and not self._det_wgrad and fuse_wu
                                  and hasattr(ex, 'can_defer_wgrad') and ex.can_defer_wgrad(B, sg))
+        self._dp_fused = dp_fused and self._defer_wgrad
+        if self._dp_fused:
+            self._ar_ranges = []           # (nothing left for an all-reduce launch)
+        if hasattr(ex, 'dp_exchange'):
+            ex.dp_exchange = self.reducer.xgmi if self._dp_fused else None
         self.train_steps = 0           # reference DQNAgent.training_steps (host-side mirror)
         if use_graph is None:
             use_graph = bool(config.hip_graph) and self.device.type == 'cuda'
@@ -212,7 +228,7 @@ class Learner:
         if self._split:
             loss, prio, self._tail = self.net.compute_grads(batch, acting=acting, split=True, sigma_grads=sg,
                                                             lowrank=self._lowrank, defer_fc=self._defer_fc,
-                                                            det_wgrad=self._det_wgrad)
+                                                            det_wgrad=self._det_wgrad, defer_wgrad=self._defer_wgrad)
         else:
             loss, prio = self.net.compute_grads(batch, acting=acting, sigma_grads=sg, defer_fc=self._defer_fc,
                                                 det_wgrad=self._det_wgrad, defer_wgrad=self._defer_wgrad)
@@ -297,6 +313,11 @@ class Learner:
         overlap saves (round 2 measured the dense range on a side stream beside the conv backward:
         slower)."""
         total = self.net.grad.numel()
+        if self._dp_fused:
+            # the fused update launch sums every other gradient over the ranks itself (its dependent
+            # jobs' in-launch exchange) and forms the fc gradient from the all-gathered rows: no launch
+            self._run_tail()
+            return
         if self._lowrank is not None and self._tail is not None:
             # the fc weight gradient is already the global sum (formed from the all-gathered
             # factors on the tail's joined branch): reduce only the remaining ranges

@@ -287,10 +287,10 @@ class HipExecutor:
         # (wgrad_tile's two-slot ring): 3 > 2 > 4 on the flagship (15.33k / 15.04k / 14.76k), 3 = 2 on
         # Rainbow (profiles/r5_late_ab.md); before the ring 2 > 4 > 8 (gpurun_out/r5c)
         self.wg_conv_chunks = int(os.environ.get('DQN_WG_CHUNKS', '3'))
-        # fc jobs interleaved with the weight-gradient tiles in that launch (optim_pack.h wg_mix): measured
-        # 14.8k -> 13.6k SGD steps/s on the flagship (the tiles, on the critical path, then finish later;
-        # gpurun_out/r5a/ab.jsonl), so off unless DQN_WG_MIX=1
-        self.wg_mix = os.environ.get('DQN_WG_MIX', '0') == '1'
+        # data parallelism (learner.py): the transport whose exchange channel the fused update launch
+        # uses to sum the dependent jobs' gradients over every rank (parallel/xgmi.py dpx_launch); None:
+        # one process
+        self.dp_exchange = None
         # (job table, partial buffer ptr) of a step whose conv weight gradients the next
         # update_and_pack sums from the grouped wgrad's deterministic partials
         self._parts_pending = None
@@ -512,7 +512,8 @@ class HipExecutor:
             table += fcj[lead:]
             host, total = ext.qnet_wgrad_plan(members, dims, scales, done, deps, conv_chunks=self.wg_conv_chunks)
             jobs = torch.tensor([v for it in table for v in it], dtype=torch.int32, device=dev)
-            pl = (host.to(dev), int(total), jobs, len(fcj), done, lead)
+            # (the dependent jobs: table positions [lead, lead + ndep))
+            pl = (host.to(dev), int(total), jobs, len(fcj), done, lead, len(table) - len(fcj))
             self._wg_plans[key] = pl
         return pl
 
@@ -530,7 +531,9 @@ class HipExecutor:
         wg, self._wg_pending = self._wg_pending, None
         fcargs = self._take_fc(fc)
         assert fcargs, 'deferred weight gradients need the fused fc gradient (defer_fc)'
-        plan, nwg, jobs, nfc, _, lead = self._wg_plan(wg, grad, dev)
+        plan, nwg, jobs, nfc, _, lead, ndep = self._wg_plan(wg, grad, dev)
+        # data parallelism: the dependent jobs sum their gradient over every rank inside the launch
+        dp = self.dp_exchange.dpx_launch(lead, ndep) if self.dp_exchange is not None else []
         hp = opt.hp
         s0 = opt.slots[0] if len(opt.slots) > 0 else flat
         s1 = opt.slots[1] if len(opt.slots) > 1 else flat
@@ -561,7 +564,7 @@ class HipExecutor:
                             (list(next_sample['p']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             (list(next_sample['f']) if next_sample is not None and next_sample['kind'] == 'per' else []),
                             target_noise, teff, tpk, noise_rng, fcargs, 0, wg=plan.data_ptr(), wg_blocks=nwg,
-                            wg_jobs=lead if self.wg_mix else 0, tsg=self._tsg_arg(target, target_noise))
+                            dp=dp, tsg=self._tsg_arg(target, target_noise))
         if self.noisy:
             self._bound[flat.data_ptr()] = noise_dst if noise_dst is not None else noise
             if target_noise is not None:
@@ -572,8 +575,11 @@ class HipExecutor:
         """True when ``loss_and_grad(defer_fc=True, defer_wgrad=True)`` at this batch leaves the
         grouped conv / output-layer weight gradients to the next ``update_and_pack`` (which then
         runs them beside the fc update, ``_update_split``): the Nature trunk's grouped-wgrad path
-        in the 16-bit builds, one process (no all-reduce between the gradients and the update)."""
-        return self.can_defer_fc(B, sigma_grads) and self.arch.network == 'nature' and not (self.noisy and sigma_grads)
+        in the 16-bit builds. Under data parallelism only with ``dp_exchange`` set (the launch sums
+        those gradients over the ranks itself) and the low-rank fc exchange."""
+        # (the reference `cnn` too: its conv members are the same three fused tile kinds -- 8x8/4, 4x4/2,
+        #  3x3/1 -- with SAME padding in their ConvArgs, conv2 / conv3 reading the pooled activations)
+        return self.can_defer_fc(B, sigma_grads) and not (self.noisy and sigma_grads)
 
     def _take_fc(self, fc=None):
         if fc is None:
@@ -1335,8 +1341,11 @@ class HipExecutor:
         if self.arch.network == 'cnn':
             defer = bool(defer_fc) and self.can_defer_fc(B, gnoise is not None)
             assert defer or not defer_fc, 'defer_fc: not available for this executor / batch'
+            dwg = bool(defer_wgrad)
+            assert not dwg or (defer and not split and self.can_defer_wgrad(B, gnoise is not None)), \
+                'defer_wgrad (cnn): needs defer_fc, one process'
             out = self._cnn_backward(ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, gnoise, dev, fc_dgrad,
-                                     hmembers, hdims, defer=defer)
+                                     hmembers, hdims, defer=defer, defer_wgrad=dwg)
             return out + (None,) if split else out
         x1, x2, x3 = ws['x1'][0].data_ptr(), ws['x2'][0].data_ptr(), ws['x3'][0].data_ptr()
         mc_fc = (B + 31) // 32 * 32
@@ -1369,8 +1378,9 @@ class HipExecutor:
             defer = bool(defer_fc) and self.can_defer_fc(B, gnoise is not None)
             assert defer or not defer_fc, 'defer_fc: not available for this executor / batch'
             dwg = bool(defer_wgrad)
-            assert not dwg or (defer and not det and not split and self.can_defer_wgrad(B, gnoise is not None)), \
-                'defer_wgrad: needs defer_fc, one process, no det_wgrad'
+            assert not dwg or (defer and not det and self.can_defer_wgrad(B, gnoise is not None)
+                               and (not split or (lowrank is not None and self.dp_exchange is not None))), \
+                'defer_wgrad: needs defer_fc, no det_wgrad; under DP the low-rank exchange and dp_exchange'
             if defer and not (split and lowrank is not None):
                 # the optimizer launch forms dW_fc = x3^T dH from this rank's rows
                 self._fc_pending = (x3, ws['dh'].data_ptr(), B)
@@ -1533,7 +1543,7 @@ class HipCnnExecutor(HipExecutor):
             self._fc_fwd(packs, flats, ws, B, ninst)
 
     def _cnn_backward(self, ws, B, s, frames, po, g, fw, fb, fw2, fb2, grad_out, noise, dev, fc_dgrad,
-                      hmembers=(), hdims=(), defer=False):
+                      hmembers=(), hdims=(), defer=False, defer_wgrad=False):
         ext = self.ext
         F, HH, H = self.FLAT, self.HH, self.HID
         pko = lambda key: po.data_ptr() + self.esz * self.poff[key]
@@ -1568,7 +1578,11 @@ class HipCnnExecutor(HipExecutor):
             dims.append([B, HH, F, 0, 0, 0, 0, 0, 0, 0, 0])
         members += list(hmembers)
         dims += list(hdims)
-        ext.qnet_wgrad_group(members, dims, [self.input_scale] + [1.0] * (len(members) - 1))
+        scales = [self.input_scale] + [1.0] * (len(members) - 1)
+        if defer_wgrad:                 # the next update_and_pack runs the group beside the fc update
+            self._wg_pending = (members, dims, scales)
+        else:
+            ext.qnet_wgrad_group(members, dims, scales)
         if self.noisy and noise is not None:
             ext.qnet_noisy_grad(grad_out.data_ptr(), noise.data_ptr(), self._noisy_jobs_on(dev).data_ptr(),
                                 len(self.noisy_jobs), self._noisy_max)

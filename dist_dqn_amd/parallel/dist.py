@@ -34,6 +34,9 @@ class DistContext:
     # gloo). Stop agreement, restored-path/sidecar broadcast and replica fingerprints go here,
     # as CPU tensors, so they never queue behind (or synchronise with) the GPU stream.
     ctrl_group: object = None
+    # a one-rank process group that still takes every data-parallel code path (the W = 1 probe of
+    # the DP step: bench.py --dp_path, tests): collectives over one rank are the identity
+    force_dp: bool = False
 
     @property
     def is_chief(self) -> bool:
@@ -82,7 +85,7 @@ class DistContext:
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force_dp
 
     def barrier(self):
         if self.enabled:
@@ -114,7 +117,9 @@ def _from_cluster_flags(config):
     return dict(rank=config.task_id, world=len(hosts), addr=host, port=port, local_rank=config.gpu_id)
 
 
-def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600) -> DistContext:
+def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600, force_dp: bool = False) -> DistContext:
+    """``force_dp`` (one process only): form a one-rank process group anyway and report the context
+    enabled, so the data-parallel step runs at W = 1 (its collectives are the identity)."""
     env_world = int(os.environ.get('WORLD_SIZE', '1'))
     cl = _from_cluster_flags(config) if config is not None and env_world == 1 else None
     if env_world > 1:
@@ -130,32 +135,46 @@ def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600) ->
         device = getattr(config, 'device', 'auto') if config is not None else 'auto'
     use_gpu = (device in ('auto', 'cuda')) and torch.cuda.is_available()
     backend = 'none'
-    if world > 1:
+    force_dp = bool(force_dp) and world == 1
+    if force_dp:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if 'MASTER_PORT' not in os.environ:
+            import socket
+            with socket.socket() as sk:
+                sk.bind(('127.0.0.1', 0))
+                os.environ['MASTER_PORT'] = str(sk.getsockname()[1])
+    if world > 1 or force_dp:
         backend = 'nccl' if use_gpu else 'gloo'
         # DQN_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks on ONE
         # device (RCCL refuses two ranks per GPU; gloo stages CUDA tensors through the host)
         backend = os.environ.get('DQN_DIST_BACKEND', backend)
     if use_gpu:
         ndev = torch.cuda.device_count()
-        if backend == 'nccl' and local_rank >= ndev:
-            # RCCL needs one GPU per rank: say so here instead of a "Duplicate GPU" abort later
-            raise RuntimeError('rank %d (local rank %d) has no GPU of its own: %d visible device(s) for %d ranks '
-                               'per node. Launch at most one rank per GPU, or set DQN_DIST_BACKEND=gloo to '
-                               'rehearse several ranks on one GPU.' % (rank, local_rank, ndev, world))
-        dev = torch.device('cuda', local_rank % max(ndev, 1))
+        if ndev == 0:
+            raise RuntimeError('rank %d: no visible GPU' % rank)
+        # (local_rank % ndev: a rank that sees only its own GPU -- per-rank HIP_VISIBLE_DEVICES, SLURM
+        # --gpus-per-task=1, the reference's --gpu_id flags -- has local rank 1..N-1 but one device.
+        # Real sharing of one physical GPU is decided after the group exists, from the PCI ids.)
+        dev = torch.device('cuda', local_rank % ndev)
         torch.cuda.set_device(dev)
     else:
         dev = torch.device('cpu')
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_dp) and not dist.is_initialized():
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if use_gpu and backend == 'nccl':
             kw['device_id'] = dev
         dist.init_process_group(**kw)
     ctrl = None
-    if world > 1 and backend != 'gloo':
+    if (world > 1 or force_dp) and backend != 'gloo':
         ctrl = dist.new_group(backend='gloo', timeout=datetime.timedelta(seconds=timeout_s))
-    ctx = DistContext(rank, world, local_rank, dev, backend, ctrl)
-    if world > 1:
+    ctx = DistContext(rank, world, local_rank, dev, backend, ctrl, force_dp)
+    if world > 1 and use_gpu and backend == 'nccl' and ctx.ranks_share_gpu():
+        # RCCL needs one GPU per rank: say so here (every rank computes the same answer from the
+        # gathered PCI ids) instead of a "Duplicate GPU detected" abort at the first collective
+        raise RuntimeError('rank %d (local rank %d, %s): ranks share a physical GPU (%s). Launch at most one '
+                           'rank per GPU, or set DQN_DIST_BACKEND=gloo to rehearse several ranks on one GPU.'
+                           % (rank, local_rank, device_id(dev), ctx.device_ids()))
+    if ctx.enabled:
         first_contact(ctx)
     return ctx
 

@@ -37,7 +37,7 @@ log = logging.getLogger(__name__)
 
 class GradAllReducer:
     def __init__(self, ctx: DistContext, flat_grad: torch.Tensor, bucket_mb: float = 64.0,
-                 mode: str = 'auto', wire_dtype: str = 'fp32', gather_bytes: int = 0):
+                 mode: str = 'auto', wire_dtype: str = 'fp32', gather_bytes: int = 0, exchange_slots: int = 0):
         self.ctx = ctx
         self.flat = flat_grad
         n = flat_grad.numel()
@@ -55,6 +55,9 @@ class GradAllReducer:
         self.xgmi = None
         self.timings = {}
         self.gather_bytes = int(gather_bytes)
+        # > 0: the xgmi transport also carries the fused update's in-launch exchange channel
+        # (learner.py: the conv / output-layer gradients summed inside the update launch)
+        self.exchange_slots = int(exchange_slots)
         self.can_gather = False       # the xgmi transport carries a working all-gather channel
         if ctx.enabled and flat_grad.is_cuda and mode in ('xgmi', 'auto'):
             self.xgmi = self._setup_xgmi(mode)
@@ -65,7 +68,8 @@ class GradAllReducer:
         from .xgmi import XgmiAllReduce
         n = self.flat.numel()
         try:
-            x = XgmiAllReduce(self.ctx, n, self.wire_dtype, gather_bytes=self.gather_bytes)
+            x = XgmiAllReduce(self.ctx, n, self.wire_dtype, gather_bytes=self.gather_bytes,
+                              exchange_slots=self.exchange_slots)
         except Exception as e:  # noqa: BLE001
             if mode == 'xgmi':
                 raise

@@ -35,11 +35,13 @@ _SIG_BYTES = 64 * 1024          # >= XGMI_SIG_WORDS * 4, keeps staging 64 KB ali
 
 
 class _Channel:
-    def __init__(self, ext, ctx: DistContext, cap: int, esz: int):
+    def __init__(self, ext, ctx: DistContext, cap: int, esz: int, nseq: int = 0):
         self.ext = ext
         self.cap = cap
         self.base = ext.xgmi_alloc(_SIG_BYTES + 2 * cap * esz)
-        self.seq_err = torch.zeros(ext.XGMI_MAX_BLOCKS + 4, dtype=torch.int32, device=ctx.device)
+        # per-block (exchange: per-slot) call counters, then the 4-word error record
+        self.nseq = int(nseq or ext.XGMI_MAX_BLOCKS)
+        self.seq_err = torch.zeros(self.nseq + 4, dtype=torch.int32, device=ctx.device)
         self.opened: List[int] = []
         self.sig: List[int] = []
         self.data: List[int] = []
@@ -62,7 +64,11 @@ class _Channel:
 
     @property
     def err_ptr(self) -> int:
-        return self.seq_err.data_ptr() + 4 * self.ext.XGMI_MAX_BLOCKS
+        return self.seq_err.data_ptr() + 4 * self.nseq
+
+    @property
+    def err_words(self) -> torch.Tensor:
+        return self.seq_err[self.nseq:self.nseq + 4]
 
     def close(self):
         for p in self.opened:
@@ -77,7 +83,7 @@ class XgmiAllReduce:
     """Sum of an fp32 GPU tensor across the ranks of ``ctx`` (in place, current stream)."""
 
     def __init__(self, ctx: DistContext, capacity: int, wire_dtype: str = 'fp32', channels: int = 2,
-                 gather_bytes: int = 0):
+                 gather_bytes: int = 0, exchange_slots: int = 0):
         assert ctx.enabled and ctx.device.type == 'cuda'
         self.ext = _ext.load(required=True)
         assert hasattr(self.ext, 'XGMI_MAX_BLOCKS'), 'extension built without the xGMI all-reduce'
@@ -96,10 +102,21 @@ class XgmiAllReduce:
         # gather_bytes > 0: one more channel (byte staging) for `allgather2` -- the low-rank
         # exchange of the dense layer's factors (learner.py)
         self.gather_cap = (int(gather_bytes) + 255) // 256 * 256
+        # exchange_slots > 0: one more channel (per-job inboxes) for the fused update's in-launch
+        # gradient exchange under data parallelism (optim_pack.h kModeDp, `dpx_launch`)
+        self.dpx_slots = int(exchange_slots)
+        assert self.dpx_slots <= self.ext.DPX_MAX_SLOTS, 'exchange: too many dependent update jobs'
+        self.dpx = None
+        self.gch = None
         try:
             self.channels = [_Channel(self.ext, ctx, self.cap, esz) for _ in range(channels)]
             if self.gather_cap > 0:
-                self.channels.append(_Channel(self.ext, ctx, self.gather_cap, 1))
+                self.gch = _Channel(self.ext, ctx, self.gather_cap, 1)
+                self.channels.append(self.gch)
+            if self.dpx_slots > 0:
+                self.dpx = _Channel(self.ext, ctx, ctx.world_size * self.dpx_slots * self.ext.DPX_SLOT_ELEMS, 4,
+                                    nseq=self.ext.DPX_MAX_SLOTS)
+                self.channels.append(self.dpx)
             handles = [self.ext.xgmi_ipc_handle(ch.base) for ch in self.channels]
         except Exception as e:  # noqa: BLE001
             err = e
@@ -140,7 +157,7 @@ class XgmiAllReduce:
         aligned, sizes % 16 == 0), for both segments in ONE launch on the current stream (the gather
         channel: its own signals and staging, so it may run beside the all-reduce channels)."""
         assert self.gather_cap > 0, 'no gather channel'
-        ch = self.channels[-1]
+        ch = self.gch
         nv = (int(nbytes[0]) + int(nbytes[1])) // 16
         blocks = max(1, min(self.max_blocks, (nv + 255) // 256))
         self.ext.xgmi_allgather([int(v) for v in srcs], [int(v) for v in outs], [int(v) for v in nbytes], ch.data,
@@ -156,7 +173,7 @@ class XgmiAllReduce:
         cache = self.__dict__.setdefault('_gather_args', {})
         if key in cache:
             return cache[key]
-        ch = self.channels[-1]
+        ch = self.gch
         host = self.ext.xgmi_gather_args([int(v) for v in srcs], [int(v) for v in outs], [int(v) for v in nbytes],
                                          ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.gather_cap, self.ctx.rank,
                                          self.ctx.world_size)
@@ -164,6 +181,11 @@ class XgmiAllReduce:
         blocks = max(1, min(self.max_blocks, (nv + 255) // 256))
         cache[key] = (host.to(self.ctx.device), blocks)
         return cache[key]
+
+    @property
+    def n_reduce_channels(self) -> int:
+        """The all-reduce channels (the gather / exchange channels follow them)."""
+        return len(self.channels) - (1 if self.gather_cap > 0 else 0) - (1 if self.dpx is not None else 0)
 
     def self_test_gather(self) -> bool:
         """Gather rank-stamped bytes twice (both staging parities), check every slot, agree."""
@@ -207,17 +229,35 @@ class XgmiAllReduce:
 
     def failed_channels(self) -> list:
         """Indices of the channels whose error word is set (host sync)."""
-        return [c for c, ch in enumerate(self.channels) if int(ch.seq_err[self.ext.XGMI_MAX_BLOCKS]) != 0]
+        return [c for c, ch in enumerate(self.channels) if int(ch.err_words[0]) != 0]
 
-    _PHASES = {1: 'reduce-scatter (phase A)', 2: 'all-gather (phase B)', 3: 'gather'}
+    def dpx_launch(self, first: int, n: int) -> list:
+        """The ``dp`` argument of a fused update launch whose job table holds its ``n`` dependent jobs
+        at [first, first + n): [device DpExchange, first, n, blocks]. One GPU per rank: one block per
+        job. Ranks sharing ONE GPU (the rehearsals): every rank's dependent blocks spin on their peers,
+        so at most 64 / W blocks per rank take the jobs in turn (the peers' blocks stay schedulable)."""
+        assert self.dpx is not None, 'no exchange channel'
+        assert 1 <= n <= self.dpx_slots, ('exchange: %d dependent jobs, channel sized for %d' % (n, self.dpx_slots))
+        key = (int(first), int(n))
+        cache = self.__dict__.setdefault('_dpx_args', {})
+        if key not in cache:
+            if 'dev' not in cache:
+                ch = self.dpx
+                host = self.ext.xgmi_dpx_args(ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.ctx.rank,
+                                              self.ctx.world_size, self.dpx_slots, ch.cap)
+                cache['dev'] = host.to(self.ctx.device)
+            blocks = n if not self.shared_gpu else max(1, min(n, 64 // self.ctx.world_size))
+            cache[key] = [cache['dev'].data_ptr(), int(first), int(n), int(blocks)]
+        return cache[key]
+
+    _PHASES = {1: 'reduce-scatter (phase A)', 2: 'all-gather (phase B)', 3: 'gather', 4: 'update exchange'}
 
     def error_info(self) -> list:
         """Per failed channel, the FIRST timed-out wait: {'channel', 'phase', 'peer', 'block',
         'expected', 'seen', 'call'} (host sync; xgmi_dev.h wait_all)."""
         out = []
-        M = self.ext.XGMI_MAX_BLOCKS
         for c, ch in enumerate(self.channels):
-            w = [int(v) for v in ch.seq_err[M:M + 4].tolist()]
+            w = [int(v) for v in ch.err_words.tolist()]
             if w[0] == 0:
                 continue
             code = w[0] & 0xffffffff
@@ -228,7 +268,7 @@ class XgmiAllReduce:
 
     def check(self) -> bool:
         """False if any block of any launch so far timed out waiting for a peer (host sync)."""
-        return all(int(ch.seq_err[self.ext.XGMI_MAX_BLOCKS]) == 0 for ch in self.channels)
+        return all(int(ch.err_words[0]) == 0 for ch in self.channels)
 
     def self_test(self, n: int) -> bool:
         """Reduce rank-dependent integers (exact in fp32 and bf16) on every channel, three
@@ -240,14 +280,14 @@ class XgmiAllReduce:
         # per (channel, call): values off the exact sum, error word after the call (why a test failed)
         self.self_test_log = []
         try:
-            for c in range(len(self.channels) - (1 if self.gather_cap > 0 else 0)):
+            for c in range(self.n_reduce_channels):
                 for call in range(3):
                     x = (idx % 7) + (r + 1) * (call + 1)
                     expect = W * (idx % 7) + (call + 1) * W * (W + 1) / 2
                     self.allreduce(x, channel=c)
                     torch.cuda.synchronize(self.ctx.device)
                     wrong = int((x != expect).sum())
-                    self.self_test_log.append((c, call, wrong, int(self.channels[c].seq_err[self.ext.XGMI_MAX_BLOCKS])))
+                    self.self_test_log.append((c, call, wrong, int(self.channels[c].err_words[0])))
                     ok = ok and wrong == 0
             ok = ok and self.check()
         except Exception as e:  # noqa: BLE001 - any failure means "do not use this transport"

@@ -4,7 +4,6 @@ step, timed alone (HIP events over back-to-back launches):
   wgrad_group      the grouped weight-gradient launch it replaces (256-row chunks)
   F                the fused launch: lead block, weight-gradient tiles, fc jobs, dependent jobs
   F_nosampler      the same without the next-minibatch block
-  F_wgrad_only     the weight-gradient tiles + one fc job
   F_fc_only        the fc jobs alone (FcFuse launch, no weight-gradient tiles)
   fused_old        the previous update launch (every job, sampler block; gradients read)
 
@@ -58,7 +57,7 @@ def main():
     opt = net.optimizer
     hp = opt.hp
     hps = [float(hp[k]) for k in ('momentum', 'rho', 'rms_mom', 'rms_eps', 'b1', 'b2', 'adam_eps', 'ad_rho', 'ad_eps')]
-    plan, nwg, jobs, nfc, _, _ = ex._wg_plan(wg, net.grad, dev)
+    plan, nwg, jobs, nfc = ex._wg_plan(wg, net.grad, dev)[:4]
     nint = ex.ext.UPD_JOB_INTS
     jf = jobs[:nfc * nint]
     s0 = opt.slots[0] if opt.slots else net.online.flat
@@ -73,10 +72,9 @@ def main():
         smp = list(spec['spec']) + [int(spec['B'])] if spec['kind'] == 'uniform' else []
     op = kernel_op(opt)
 
-    def launch(jobs, fcx, wgp=0, nb=0, sample=(), nj=None):
+    def launch(jobs, fcx, wgp=0, nb=0, sample=()):
         ex.ext.optim_pack(op, *base, jobs, p, net.target.flat, pt, 1 << 30, ex.opt_max_grid, None, None, None, None,
-                          list(sample), [], [], None, None, None, None, fcx, 0, wg=wgp, wg_blocks=nb,
-                          wg_jobs=0 if nj is None else nj)
+                          list(sample), [], [], None, None, None, None, fcx, 0, wg=wgp, wg_blocks=nb)
 
     def timeit(fn):
         for _ in range(10):
@@ -101,7 +99,6 @@ def main():
     out['wgrad_group'] = timeit(lambda: ex.ext.qnet_wgrad_group(members, dims, scales))
     out['F'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg, sample=smp))
     out['F_nosampler'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg))
-    out['F_wgrad_only'] = timeit(lambda: launch(jobs, fca, plan.data_ptr(), nwg, nj=1))
     out['F_fc_only'] = timeit(lambda: launch(jf, fca))
     # (the previous single launch reads every gradient from the flat buffer: fc jobs as well)
     jall = ex._upd_jobs(dev)
@@ -109,12 +106,12 @@ def main():
     for cc in (2, 4):                     # chunks per conv tile (the executor default: 3)
         ex.wg_conv_chunks = cc
         ex._wg_plans = {}
-        pl2, n2, j2, _, _, _ = ex._wg_plan(wg, net.grad, dev)
+        pl2, n2, j2 = ex._wg_plan(wg, net.grad, dev)[:3]
         out['F_chunks%d' % cc] = timeit(lambda: launch(j2, fca, pl2.data_ptr(), n2, sample=smp))
         out['wg_blocks_chunks%d' % cc] = n2
-    ex.wg_conv_chunks = int(os.environ.get("DQN_WG_CHUNKS", "3"))
+    ex.wg_conv_chunks = 3
     ex._wg_plans = {}
-    plan, nwg, jobs, nfc, _, _ = ex._wg_plan(wg, net.grad, dev)
+    plan, nwg, jobs, nfc = ex._wg_plan(wg, net.grad, dev)[:4]
     if os.environ.get('DQN_OPT_PROF'):
         out['timeline_us'] = timeline(ex, plan, nwg, jobs, nfc, nint, lambda: launch(jobs, fca, plan.data_ptr(), nwg,
                                                                                  sample=smp))
@@ -122,8 +119,6 @@ def main():
         # launch gets its blocks onto the CUs
         t = timeline_fc_only(ex, nfc, lambda: launch(jf, fca))
         out['timeline_fc_only_us'] = t
-        out['timeline_wgrad_only_us'] = timeline(ex, plan, nwg, jf[:nint], 1, nint,
-                                                 lambda: launch(jobs, fca, plan.data_ptr(), nwg, nj=1))
         # phases inside the tiles of that launch (us after each tile's start): staged chunk 0 |
         # chunk 0 MFMAs | staged chunk 1 | chunk 1 MFMAs | results issued | drained
         ph = ex.ext.optim_tile_phases(min(nwg, 512))

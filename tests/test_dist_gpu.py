@@ -205,8 +205,11 @@ def _worker(rank, world, port, network, extra, errq):
                 # no noisy layers, fp32 wire); overlap=0 is the full all-reduce it is compared with
                 lowrank = bool(overlap) and network == 'nature' and 'bf16' not in extra
                 assert (ln._lowrank is not None) == lowrank, (overlap, extra)
-                # ... and then feeds the fused optimizer (fc dW from the W*B gathered rows)
+                # ... and then feeds the fused optimizer (fc dW from the W*B gathered rows), whose launch
+                # also runs the conv / output-layer weight gradients and sums them over the ranks
+                # itself (in-launch exchange: no all-reduce launch)
                 assert ln._defer_fc == lowrank, (overlap, extra)
+                assert ln._dp_fused == lowrank and ln._defer_wgrad == lowrank, (overlap, extra)
             elif overlap and network == 'nature':
                 assert ln._graphs is not None and ln._graphs[2] is not None, 'no split graph captured'
             outs[overlap] = net.online.flat.clone()
@@ -369,6 +372,66 @@ def _worker_rccl_one_rank(rank, world, port, errq):
 
 def test_rccl_one_rank_data_parallel_paths():
     _run_ranks(_worker_rccl_one_rank, (), world=1, timeout=150)
+
+
+def _worker_dp_fused_one_rank(rank, world, port, extra, errq):
+    """The fused DP step at W = 1 (``init_distributed(force_dp=True)``: a one-rank RCCL group, every DP
+    code path on): the fc gather side duty, the weight-gradient tiles inside the update launch and
+    its in-launch exchange, all in ONE graph per G steps. Against a one-process learner from the
+    same init on the same minibatches: the same parameters (to the conv wgrad's fp32-atomic order)."""
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'DQN_DIST_BACKEND'):
+            os.environ.pop(k, None)
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from dist_dqn_amd.config import preset
+        from dist_dqn_amd.learner import Learner
+        from dist_dqn_amd.models.network import Network
+        from dist_dqn_amd.parallel import init_distributed
+        from dist_dqn_amd.replay import DeviceReplay
+        cfg = preset('nature', 'Pong-v0', '--dtype=bf16 --seed=3 --backend=hip --replay_memory_capacity=4096 '
+                     '--allreduce=xgmi ' + extra)
+        ctx = init_distributed(cfg, device='cuda', force_dp=True)
+        assert ctx.enabled and ctx.world_size == 1 and ctx.backend == 'nccl'
+        outs, losses = [], []
+        for dp in (True, False):
+            net = Network.create_network(cfg, (84, 84, 4), 6, device=ctx.device)
+            rep = DeviceReplay(4096, (84, 84), 4, device=ctx.device, seed=3,
+                               prioritized=cfg.prioritized_replay)
+            rep.fill_synthetic(4096, 6, seed=3)
+            ln = Learner(net, rep, cfg, ctx if dp else None)
+            if dp:
+                assert ln._dp_fused and ln._defer_wgrad and ln.reducer.mode == 'xgmi', \
+                    (ln._dp_fused, ln._defer_wgrad, ln.reducer.mode)
+                assert ln.reducer.xgmi.dpx is not None and ln.can_step_many()
+            else:
+                assert not ln.ctx.enabled and ln._defer_wgrad
+            for _ in range(3):                          # eager warm-up, then the one-step graph
+                ln.step()
+            ln.step_many(4)                             # a 4-step graph (the bench's shape)
+            torch.cuda.synchronize()
+            assert int(net.global_step) == 7
+            if dp:
+                ln.reducer.check()
+                ln._device_checks()
+            losses.append(float(ln.loss))
+            outs.append(net.online.flat.clone())
+        assert all(torch.isfinite(o).all() for o in outs)
+        if cfg.optimizer == 'adam':
+            assert float(torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=0)) > 0.9999
+        else:
+            torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-6)
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+        errq.put('rank %d: %s\n%s' % (rank, e, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize('extra', ['', '--dueling --double_dqn --loss=huber', RAINBOW_DP])
+def test_dp_fused_step_one_rank_matches_one_process(extra):
+    _run_ranks(_worker_dp_fused_one_rank, (extra,), world=1, timeout=200)
 
 
 def test_bench_gpus_more_than_the_node_has_fails_loudly():

@@ -109,7 +109,7 @@ class _FakeXgmi:
     gather_ok = True
     closed = 0
 
-    def __init__(self, ctx, n, wire, gather_bytes=0):
+    def __init__(self, ctx, n, wire, gather_bytes=0, exchange_slots=0):
         if _FakeXgmi.raise_in_ctor:
             raise RuntimeError('ipc mapping refused')
 
