@@ -31,12 +31,16 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-VARIANT_DTYPE = {'rainbow': 'fp16'}
+# (ref: the reference's own Q-network and preset -- `cnn` (SAME convs + max-pools, FC256), the atari
+#  preset of scripts/dqn_params.sh:24-42 (RMSProp 2.5e-4, B = 32, no input scaling) -- in the reference's
+#  fp32 by default)
+VARIANT_DTYPE = {'rainbow': 'fp16', 'ref': 'fp32'}
 METRIC = "learner SGD steps/sec + env frames/sec, Atari Nature-CNN DQN at 1/2/4/8 MI355X"
 VARIANTS = {
     'dqn': '',
     'dd': '--dueling --double_dqn --loss=huber',
     'rainbow': '--dueling --double_dqn --distributional --noisy --prioritized_replay --optimizer=adam --lr=0.0000625',
+    'ref': '',
 }
 
 
@@ -92,7 +96,8 @@ def main():
     ap.add_argument('--extra', default='', help='extra config flags, e.g. "--dueling --double_dqn"')
     ap.add_argument('--variant', default='dqn', choices=sorted(VARIANTS),
                     help='algorithm variant (BASELINE.json configs): dqn = Nature DQN, dd = Double+Dueling+Huber, '
-                         'rainbow = C51 + noisy nets + dueling + double + PER + Adam')
+                         'rainbow = C51 + noisy nets + dueling + double + PER + Adam, ref = the reference\'s own '
+                         '`cnn` Q-network on its atari preset (fp32 by default)')
     ap.add_argument('--fuse_acting', type=int, default=1,
                     help='run the device actors\' step inside the learner step\'s launches when possible')
     ap.add_argument('--graph_steps', type=int, default=16,
@@ -106,6 +111,8 @@ def main():
     args = ap.parse_args()
     if args.dp_path and args.gpus != 1:
         ap.error('--dp_path is the one-rank probe of the DP step (--gpus 1)')
+    if args.variant == 'ref':
+        args.network = 'cnn'
     if args.dtype is None:             # BASELINE.json config 5: "Rainbow ... fp16 conv MFMA path"
         args.dtype = VARIANT_DTYPE.get(args.variant, 'bf16')
     if args.gpus < 1:

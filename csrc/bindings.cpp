@@ -699,7 +699,8 @@ torch::Tensor xgmi_dpx_args(std::vector<int64_t> inbox, std::vector<int64_t> sig
                             int64_t rank, int64_t world, int64_t slots, int64_t cap) {
   TORCH_CHECK(world >= 1 && world <= dqn::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi dpx: rank/world");
   TORCH_CHECK((int64_t)inbox.size() == world && (int64_t)sig.size() == world && seq && err, "xgmi dpx: pointers");
-  TORCH_CHECK(slots >= 1 && slots <= dqn::kDpxMaxSlots && 2 * world * slots * (int64_t)dqn::kDpxSlotElems <= cap,
+  // (cap: the channel's elements per parity; the kernel addresses [2 parities][world][slots][elems])
+  TORCH_CHECK(slots >= 1 && slots <= dqn::kDpxMaxSlots && world * slots * (int64_t)dqn::kDpxSlotElems <= cap,
               "xgmi dpx: slots exceed the channel's inbox");
   dqn::DpExchange x{};
   for (int i = 0; i < world; ++i) {

@@ -156,7 +156,7 @@ struct FoldArgs {
   // its dH write instead of using stale dQ (read by Learner._device_checks). dq_epoch[ngroups + 1].
   int32_t* err;
   int dbg_no_publish;        // test hook (DQN_DEBUG_FOLD_NO_PUBLISH): the tails never publish dQ
-  int sc1;                   // A/B knob (DQN_SC1_TAILS=1): spin-mode tails read the slots sc1, no fence
+  int two_per_cu;            // spin mode may run two blocks per CU (KernelTuning.fold_two_per_cu)
 };
 
 // The Nature dgrad chain in ONE launch (qnet.hip dgrad_chain_kernel): block ranges run

@@ -255,8 +255,9 @@ __global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_he
       }
     }
     __syncthreads();
-    if (S.timed_out) return;             // flagged: the learner's device check raises
-    const int nr = min(16, a.M - m_base);
+    // timed out (flagged: the learner's device check raises): the tile is written as ZEROS -- the
+    // group then adds nothing to this step's gradient, instead of the previous step's stale dH
+    const int nr = S.timed_out ? 0 : min(16, a.M - m_base);
     for (int t = tid; t < 16 * A1; t += kFoldThreads) {
       const int r = t / A1, c = t - r * A1;
       S.dq[r][c] = r < nr ? __hip_atomic_load(f.dqg + (int64_t)(m_base + r) * 32 + c, __ATOMIC_RELAXED,
@@ -269,10 +270,8 @@ __global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_he
   }
   if (tid == 0) {
     // acquire, then plain loads of the partial-Q slots (and, not spin, the other blocks' h rows).
-    // DQN_SC1_TAILS=1 (spin mode): no fence, the slots read with 16-byte sc1 loads after the counter
-    // add returned (the producers stored them sc1) -- measured 0.3-0.6 us SLOWER than the fence on
-    // this kernel (round 5, gpurun_out/r5v), so off by default
-    if (!f.spin || !f.sc1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // (round 5 measured sc1 slot loads without the fence 0.3-0.6 us slower, gpurun_out/r5v: removed)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(f.cnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -302,12 +301,6 @@ __global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_he
     // Q rows: every (instance, row, column) sums its tiles' partial slots in tile order (dueling:
     // advantage columns over the advantage tiles, the value column over the value tiles), + bias
     const int NT = (int)gridDim.y, half = h.dueling ? NT / 2 : 0;
-    // the slots through a buffer descriptor: 16-byte sc1 loads (buffer_load_dwordx4 ... sc1) bypass
-    // this CU's L1 like the scalar agent-scope loads, at a quarter of their instructions (4-byte
-    // atomic loads cost the dueling fold ~4.6 us: round-5 trace, gpurun_out/r5u)
-    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
-        f.qacc, (short)0, (int)(4 * (int64_t)(f.nlearn + 1) * f.Mpad * 32 * NT), 0x00020000);
-    typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
     if (tid < ni * 32) S.q[tid >> 5][16][tid & 31] = pb;          // (row 16: the bias row)
     for (int t = tid; t < ni * 16 * A1; t += kFoldThreads) {
       const int i = t / (16 * A1), rem = t - i * 16 * A1, r = rem / A1, c = rem - r * A1;
@@ -315,23 +308,13 @@ __global__ void __launch_bounds__(kFoldThreads, kFoldU == kFoldU2 ? 4 : 2) fc_he
       if (r < nrows && (c < A || h.dueling)) {
         const int pb0 = 4 * (int)((((int64_t)(i0 + i) * f.Mpad + m_base + r) * 32 + c) * NT);   // byte offset
         const int lo = h.dueling ? (c < A ? half : 0) : 0, hi = h.dueling ? (c < A ? NT : half) : NT;
-        if (f.sc1) {                              // (summed in tile order)
-          for (int u = lo; u < hi; u += 4) {
-            const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(qrs, pb0 + 4 * u, 0, 16));
-            v += x.x;
-            v += x.y;
-            v += x.z;
-            v += x.w;
-          }
-        } else {
-          const float* p = f.qacc + pb0 / 4;
-          for (int u = lo; u < hi; u += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(p + u);
-            v += x.x;
-            v += x.y;
-            v += x.z;
-            v += x.w;
-          }
+        const float* p = f.qacc + pb0 / 4;         // (summed in tile order)
+        for (int u = lo; u < hi; u += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(p + u);
+          v += x.x;
+          v += x.y;
+          v += x.z;
+          v += x.w;
         }
       }
       S.q[i][r][c] = v;
@@ -495,8 +478,7 @@ int launch_fc_head(const ConvArgs& a, const HeadArgs& h, const FoldArgs& f, hipS
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   }
   const int nblk = (int)(grid.x * grid.y * grid.z);
-  static const bool two_ok = getenv("DQN_FOLD_TWO_PER_CU") == nullptr || atoi(getenv("DQN_FOLD_TWO_PER_CU")) != 0;
-  const bool two = two_ok && nblk > cus && nblk <= 2 * cus;
+  const bool two = f.two_per_cu && nblk > cus && nblk <= 2 * cus;
   if (f.spin && nblk > (two ? 2 * cus : cus)) {
     FoldArgs g = f;
     g.spin = 0;

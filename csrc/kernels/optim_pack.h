@@ -481,30 +481,32 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // vmcnt wait between loads and serialise the item on memory latency.)
   bool gsc1 = false;             // WG dependent job: its gradient is read with sc1 loads
   // ---- DP: the cross-rank sum of dependent job `dslot`'s gradient (this thread's 4 values g[]).
-  // Push: my values into row `rank` of every rank's inbox (remote xGMI stores, posted), publish
-  // (system-scope fence + release flag store into every rank's signal word of this slot), wait for
-  // every rank's flag in my own signal words (local polls, bounded), then sum the W rows of my inbox
-  // in rank order: the same bytes in the same order on every rank, so the replicas stay
-  // bit-identical. Inbox parity alternates per call of a slot: a rank reaches call k + 2 of a slot
-  // only after every rank flagged call k + 1, i.e. finished reading call k (stream order).
+  // Push: my values into row `rank` of every PEER's inbox (remote xGMI stores, posted), publish
+  // (system-scope fence + release flag store into every peer's signal word of this slot), wait for
+  // every peer's flag in my own signal words (local polls, bounded), then sum the W rows in rank
+  // order -- the peers' from my inbox, mine from registers: the same bytes in the same order on every
+  // rank, so the replicas stay bit-identical (W = 1: nothing to exchange). Inbox parity alternates
+  // per call of a slot: a rank reaches call k + 2 of a slot only after every peer flagged call k + 1,
+  // i.e. finished reading call k (stream order).
   int dslot = -1;
   float gdp[4] = {0.f, 0.f, 0.f, 0.f};
   auto dp_sum = [&](float* g) {
     if constexpr (DP) {
       const DpExchange& X = *dp.x;
       const int W = X.world, r = X.rank;
+      if (W == 1) return;                                                 // (the sum of one row)
       const uint32_t k = X.seq[dslot];
       const long stride = (long)X.slots * kDpxSlotElems;                  // one source rank's rows
       const long base = (long)(k & 1u) * W * stride + (long)dslot * kDpxSlotElems + 4 * t;
       const float4 v = make_float4(g[0], g[1], g[2], g[3]);
-      for (int q = 0; q < W; ++q) {
+      for (int q = 1; q < W; ++q) {
         const int d = r + q < W ? r + q : r + q - W;                      // (peers staggered across links)
         *reinterpret_cast<float4*>(X.inbox[d] + base + (long)r * stride) = v;
       }
       __threadfence_system();
       __syncthreads();
-      if (t < W) store_rel(X.sig[t] + r * kDpxMaxSlots + dslot, k + 1u);
-      if (t < W) {
+      if (t < W && t != r) store_rel(X.sig[t] + r * kDpxMaxSlots + dslot, k + 1u);
+      if (t < W && t != r) {
         const uint32_t* f = X.sig[r] + t * kDpxMaxSlots + dslot;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t seen;
@@ -524,12 +526,14 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");                   // system scope, every thread
       const float* in = X.inbox[r] + base;
-      float4 acc = *reinterpret_cast<const float4*>(in);
+      float4 acc = r == 0 ? v : *reinterpret_cast<const float4*>(in);
       for (int q0 = 1; q0 < W; q0 += 2) {                               // 2 rows in flight, summed in order
         float4 x[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-          x[u] = *reinterpret_cast<const float4*>(in + (long)(q0 + u < W ? q0 + u : 0) * stride);
+        for (int u = 0; u < 2; ++u) {
+          const int q = q0 + u < W ? q0 + u : 0;
+          x[u] = q == r ? v : *reinterpret_cast<const float4*>(in + (long)q * stride);
+        }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           if (q0 + u >= W) break;

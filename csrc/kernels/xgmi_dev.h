@@ -61,10 +61,11 @@ DQN_DEV bool wait_all(const XgmiArgs& a, int b, uint32_t val, int phase) {
 
 
 // All-gather of two segments (one signal per call): A  my segments -> my staging, signal
-// "A done" (k + 1); C  every rank's chunk b -> out[s] + q * bytes[s]. Block b of every rank
-// handles chunk b of the concatenated payload, so it waits only for block b of its peers.
-// Staging alternates parity per call: a rank writes parity p again at call k + 2 only after
-// every peer signalled A of call k + 1, i.e. finished reading call k (its C of call k).
+// "A done" (k + 1); C  every PEER's chunk b -> out[s] + q * bytes[s] from its staging, my own chunk
+// straight from my segments (no round trip through the uncached staging; W = 1: no staging, no
+// signal at all). Block b of every rank handles chunk b of the concatenated payload, so it waits
+// only for block b of its peers. Staging alternates parity per call: a rank writes parity p again
+// at call k + 2 only after every peer signalled A of call k + 1, i.e. finished reading call k.
 DQN_DEV void xgmi_gather_block(const XgmiGatherArgs& g, int b, int G) {
   const XgmiArgs& a = g.x;
   const int t = threadIdx.x, NT = blockDim.x;
@@ -79,16 +80,18 @@ DQN_DEV void xgmi_gather_block(const XgmiGatherArgs& g, int b, int G) {
   DQN_ASSERT(16 * nv <= a.cap && b < kXgmiMaxBlocks);
   const uint4* s0 = reinterpret_cast<const uint4*>(g.src[0]);
   const uint4* s1 = reinterpret_cast<const uint4*>(g.src[1]);
-  uint4* mine = stage(r);
-  for (long v = lo + t; v < hi; v += NT) mine[v] = v < v0 ? s0[v] : s1[v - v0];
-  signal_all(a, b, k + 1u);
-  if (!wait_all(a, b, k + 1u, kXgmiPhaseGather)) return;
   uint4* o0 = reinterpret_cast<uint4*>(g.out[0]);
   uint4* o1 = reinterpret_cast<uint4*>(g.out[1]);
+  if (W > 1) {
+    uint4* mine = stage(r);
+    for (long v = lo + t; v < hi; v += NT) mine[v] = v < v0 ? s0[v] : s1[v - v0];
+    signal_all(a, b, k + 1u);
+    if (!wait_all(a, b, k + 1u, kXgmiPhaseGather)) return;
+  }
   for (long v = lo + t; v < hi; v += NT) {
     for (int d = 0; d < W; ++d) {
-      const int q = (r + d) % W;                      // stagger peers across links
-      const uint4 x = stage(q)[v];
+      const int q = (r + d) % W;                      // stagger peers across links (d = 0: my own rows)
+      const uint4 x = d == 0 ? (v < v0 ? s0[v] : s1[v - v0]) : stage(q)[v];
       if (v < v0) o0[(long)q * v0 + v] = x;
       else o1[(long)q * v1 + (v - v0)] = x;
     }

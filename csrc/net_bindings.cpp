@@ -336,7 +336,8 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
              std::vector<int64_t> dims, std::vector<int64_t> ints, std::vector<double> flts, std::vector<int64_t> h,
              std::vector<int64_t> hw, std::vector<int64_t> hb, std::vector<int64_t> hwv, std::vector<int64_t> hbv,
              std::vector<int64_t> io, std::vector<int64_t> qp, std::vector<int64_t> actor, std::vector<double> actor_f,
-             int64_t act_h, std::vector<int64_t> fold, int64_t prof) {
+             int64_t act_h, std::vector<int64_t> fold, int64_t prof, bool two_per_cu) {
+  // two_per_cu: spin mode may run two blocks per CU (the executor's KernelTuning.fold_two_per_cu)
   dqn::ConvArgs a = conv_args(in, w, bias, out, {}, std::vector<double>(in.size(), 1.0), dims);
   TORCH_CHECK(flts.size() == 1 && qp.size() == 2 && (fold.size() == 4 || fold.size() == 6 || fold.size() == 8),
               "fc_head: flts = [delta], qp, fold = [qacc, cnt, Mpad, nlearn(, dqg, dq_epoch(, zero_ptr, zero_n))]");
@@ -352,13 +353,13 @@ void fc_head(std::vector<int64_t> in, std::vector<int64_t> w, std::vector<int64_
   f.nlearn = (int)fold[3];
   f.ngroups = (a.M + 15) / 16;
   f.prof = P<int64_t*>(prof);
+  f.two_per_cu = two_per_cu ? 1 : 0;
   if (fold.size() >= 6 && fold[4] != 0) {     // spin mode: the online blocks write their own dH tiles
     f.spin = 1;
     f.dqg = P<float*>(fold[4]);
     f.dq_epoch = P<int32_t*>(fold[5]);
     f.err = f.dq_epoch + f.ngroups + 1;       // the epoch buffer holds ngroups + 2 words
     f.dbg_no_publish = std::getenv("DQN_DEBUG_FOLD_NO_PUBLISH") != nullptr ? 1 : 0;
-    f.sc1 = std::getenv("DQN_SC1_TAILS") != nullptr ? 1 : 0;
   }
   if (fold.size() == 8 && fold[6] != 0) {      // zero duty (the step's dgrad-chain counters)
     TORCH_CHECK(fold[6] % 16 == 0 && fold[7] % 4 == 0, "fc_head: zero range 16-byte aligned, n % 4 == 0");
@@ -488,7 +489,7 @@ void register_net_ops(pybind11::module_& m) {
         pybind11::arg("out"), pybind11::arg("dims"), pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("hw"), pybind11::arg("hb"), pybind11::arg("hwv"), pybind11::arg("hbv"), pybind11::arg("io"),
         pybind11::arg("qp"), pybind11::arg("actor"), pybind11::arg("actor_f"), pybind11::arg("act_h"),
-        pybind11::arg("fold"), pybind11::arg("prof") = 0);
+        pybind11::arg("fold"), pybind11::arg("prof") = 0, pybind11::arg("two_per_cu") = true);
   m.def("qnet_head_loss", &head_loss, pybind11::arg("ints"), pybind11::arg("flts"), pybind11::arg("h"),
         pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"), pybind11::arg("io"),
         pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("qp"), pybind11::arg("actor"),

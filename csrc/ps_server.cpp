@@ -79,7 +79,13 @@ class PsServer {
     while (running_ && !done_.load() && !paused_.load(std::memory_order_acquire))
       std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
-  void resume() { pause_req_.store(false, std::memory_order_release); }
+  // returns once the thread has left its pause (or exited): a pause() right after this cannot see
+  // the previous pause's stale paused_ == true and return while the thread goes on launching
+  void resume() {
+    pause_req_.store(false, std::memory_order_release);
+    while (running_ && !done_.load() && paused_.load(std::memory_order_acquire))
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
   int64_t pauses() const { return pauses_.load(); }
 
   // join (GIL released by the binding); returns the number of applied pushes

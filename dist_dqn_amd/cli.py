@@ -71,7 +71,7 @@ def run_worker(config: Config):
         ps = None
         if config.async_ps and ctx.enabled:
             from .parallel.async_ps import make_ps_client
-            ps = make_ps_client(ctx, network.online.flat, config)
+            ps = make_ps_client(ctx, network.online.flat, config, network=network)
             # start from the PS parameters (and the PS-owned target under --disable_target_replication)
             ps.pull(network.online.flat, network.global_step,
                     target=network.target.flat if config.disable_target_replication else None)
@@ -95,6 +95,7 @@ def run_worker(config: Config):
             agent.train(config.num_episodes, config.max_steps_per_episode, sv)
         finally:
             if session is not None and session.ps is not None:
+                session.finish_ps()
                 session.ps.close()
         if coordinated and config.replica_check:
             _replica_check(ctx, network, metrics, agent.training_steps)

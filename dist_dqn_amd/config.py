@@ -204,6 +204,9 @@ def build_parser() -> argparse.ArgumentParser:
       help='HIP executor (one process, 16-bit builds): conv weight gradients as deterministic '
            'chunk-group partials summed in a fixed order by the fused optimizer launch (no fp32 '
            'atomics: bit-reproducible steps; measured 79.6 vs 71.4 us per flagship step, so opt-in)')
+    a('--kernel_tuning', default='',
+      help='HIP executor tuning constants, "key=value,..." (ops/tuning.py KernelTuning: wg_conv_chunks, '
+           'dep_at, fold_two_per_cu, tfact); empty = the measured defaults')
     a('--checkpoint_secs', default=600, type=float,
       help='chief: seconds between periodic checkpoints (reference Supervisor: 600; <= 0 disables)')
     a('--max_to_keep', default=5, type=int)
@@ -317,6 +320,7 @@ class Config:
     chain_dgrad: int = 0
     fuse_wgrad_update: int = 1
     det_wgrad: int = 0
+    kernel_tuning: str = ''
     summary_secs: float = 120.0
     checkpoint_secs: float = 600
     max_to_keep: int = 5

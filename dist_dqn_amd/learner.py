@@ -138,9 +138,10 @@ class Learner:
         # it in its fused optimizer launch); the plan is the server's too (same config, same net)
         self._ps_lowrank = None
         if ps_client is not None and hasattr(ps_client, 'lowrank'):
-            from .parallel.async_ps import ps_lowrank_plan
-            ps_client.lowrank = self._ps_lowrank = ps_lowrank_plan(network, config)
+            # (decided in make_ps_client and checked against the server's plan on every rank)
+            self._ps_lowrank = ps_client.lowrank
             if self._ps_lowrank is not None:
+                assert self._defer_fc or ex.can_defer_fc(B, True), 'low-rank push needs the fused fc path'
                 self._defer_fc = True
         # conv weight gradients as deterministic chunk-group partials summed inside the fused
         # optimizer launch (executor.can_det_wgrad): one process only (DP all-reduces the flat
@@ -401,6 +402,14 @@ class Learner:
                 self.net.executor.repack(self.net.target.flat)
         elif due:
             self.update_target_now()
+
+    def finish_ps(self):
+        """--async_ps worker, end of training: with --ps_pipeline the local parameters are one PS
+        answer behind; take the answer to the last push and repack, so end-of-run evaluation, metrics
+        and state use the server's parameters (before ``ps.close()``)."""
+        fl = getattr(self.ps, 'flush', None)
+        if fl is not None and fl(self.net.online.flat, self.net.global_step):
+            self.net._repack()
 
     def _broadcast_owned_target(self):
         """Sync DP + --disable_target_replication: rank 0 owns the target (reference: target

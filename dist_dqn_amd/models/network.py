@@ -62,7 +62,9 @@ def make_executor(arch: ArchSpec, layout, config, device: torch.device):
         if supports(arch):
             # --dtype: bf16 / fp16 (16-bit MFMA builds) or fp32 (the reference's precision: the
             # fp32-MFMA build of the same kernels, _C_f32)
-            return make_hip_executor(arch, layout, dtype=config.dtype, **kw)
+            from ..ops.tuning import KernelTuning
+            return make_hip_executor(arch, layout, dtype=config.dtype,
+                                     tuning=KernelTuning.parse(getattr(config, 'kernel_tuning', '')), **kw)
         if backend == 'hip':
             raise RuntimeError('HIP executor does not support %s' % (arch,))
         log.warning('HIP conv executor does not support this architecture (network=%s input=%s atoms=%s); '

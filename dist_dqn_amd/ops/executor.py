@@ -67,7 +67,7 @@ class HipExecutor:
     consumes_slots = True       # conv1 reads the replay frame ring through [B, 4] slot tables
 
     def __init__(self, arch, layout, dtype: str = 'bf16', input_scale: float = 1.0, loss: str = 'mse',
-                 huber_delta: float = 1.0, double_dqn: bool = False):
+                 huber_delta: float = 1.0, double_dqn: bool = False, tuning=None):
         assert supports(arch), 'HIP executor: unsupported architecture'
         # fp16 (--dtype=fp16) / fp32 (--dtype=fp32, the reference's training precision): the same
         # kernels built with -DDQN_F16 (fp16 MFMA, static loss scale inside the kernels) or
@@ -80,6 +80,8 @@ class HipExecutor:
         self.fs = 4 // self.esz                  # act_t slots of one fp32 value inside the packed buffer
         self.ext = _ext.load(required=True, variant={'bf16': '', 'fp16': 'f16', 'fp32': 'f32'}[dtype])
         self.arch, self.layout = arch, layout
+        from .tuning import KernelTuning
+        self.tuning = tuning if tuning is not None else KernelTuning()
         self.input_scale = float(input_scale)
         self.huber = loss == 'huber'
         self.delta = float(huber_delta)
@@ -102,12 +104,12 @@ class HipExecutor:
         # weights packed as separate mu / sigma fragments that change only at a target sync; its fc
         # forward mixes the per-step noise itself (qnet.hip fc_fwd_fz_kernel: X Wmu + f(eps_out) *
         # ((X * f(eps_in)) Wsigma)), so the optimizer launch neither reads the target's fc weights nor
-        # re-packs them every step (~10 bytes / fc weight of its ~60). Opt-in (DQN_TFACT=1): measured
-        # on Rainbow, the optimizer launch 58.4 -> 53.2 us but the fc forward 10.5 -> 20.0 us (the
-        # target's fragments, written only at a sync, are read cold from HBM, twice the bytes), so
+        # re-packs them every step (~10 bytes / fc weight of its ~60). Opt-in (KernelTuning.tfact):
+        # measured on Rainbow, the optimizer launch 58.4 -> 53.2 us but the fc forward 10.5 -> 20.0 us
+        # (the target's fragments, written only at a sync, are read cold from HBM, twice the bytes), so
         # 7.29k -> 7.04k SGD steps/s on one box (gpurun_out/r5aa, r5ab)
         self.tfact = (self.noisy and self.dist and dtype != 'fp32' and arch.network == 'nature'
-                      and os.environ.get('DQN_TFACT', '0') == '1')
+                      and bool(self.tuning.tfact))
         self._fact: Dict[int, torch.Tensor] = {}      # flat ptr -> sigma fragments (packed layout)
         self._fact_pk: Dict[int, int] = {}            # packed ptr -> flat ptr (factorised flats)
         self._fz_noise: Dict[int, torch.Tensor] = {}  # flat ptr -> the noise its packed fc bias holds
@@ -282,11 +284,8 @@ class HipExecutor:
         # next update_and_pack computes in its first launch (loss_and_grad(defer_wgrad=True))
         self._wg_pending = None
         self._wg_plans: Dict[tuple, tuple] = {}
-        # 128-row chunks per conv weight-gradient tile of the fused launch (summed in registers, one
-        # set of fp32 atomics per tile; DQN_WG_CHUNKS). With both chunks' loads issued up front
-        # (wgrad_tile's two-slot ring): 3 > 2 > 4 on the flagship (15.33k / 15.04k / 14.76k), 3 = 2 on
-        # Rainbow (profiles/r5_late_ab.md); before the ring 2 > 4 > 8 (gpurun_out/r5c)
-        self.wg_conv_chunks = int(os.environ.get('DQN_WG_CHUNKS', '3'))
+        # 128-row chunks per conv weight-gradient tile of the fused launch (KernelTuning.wg_conv_chunks)
+        self.wg_conv_chunks = int(self.tuning.wg_conv_chunks)
         # data parallelism (learner.py): the transport whose exchange channel the fused update launch
         # uses to sum the dependent jobs' gradients over every rank (parallel/xgmi.py dpx_launch); None:
         # one process
@@ -495,14 +494,12 @@ class HipExecutor:
                 groups.setdefault((mi, slot), []).append(list(it))
             # range-dependent jobs right after the tiles (their waits end when the tiles do) or at the
             # end of the grid: first measured +1.2% for noisy nets, whose fc jobs run ~10 us each and
-            # kept them queued to ~45 us; -0.2..-1.0% for the plain nets (profiles/r4_dep_first_ab.txt)
-            # DQN_DEP_AT=n: the dependent jobs after the first n fc jobs (A/B of the grid order). Noisy
-            # nets: after 500 of their ~1.6k fc jobs (round 5: 300 was +1-2% over right after the tiles,
-            # gpurun_out/r5j, r5k; with the earlier-finishing tiles 500 beat 300 in 4 of 4 rounds,
-            # +0.3-1.0%, profiles/r5_late_ab.md); plain nets: at the end (0 / 150 / 400 measured no better)
+            # kept them queued to ~45 us; -0.2..-1.0% for the plain nets (profiles/r4_dep_first_ab.txt).
+            # KernelTuning.dep_at = n: after the first n fc jobs; -1: noisy nets after 500 of their ~1.6k
+            # fc jobs (+0.3-1.0% over 300, profiles/r5_late_ab.md), plain nets at the end
             lead = min(500, len(fcj)) if self.noisy else len(fcj)
-            if os.environ.get('DQN_DEP_AT'):
-                lead = max(0, min(len(fcj), int(os.environ['DQN_DEP_AT'])))
+            if self.tuning.dep_at >= 0:
+                lead = max(0, min(len(fcj), int(self.tuning.dep_at)))
             table, deps = list(fcj[:lead]), []
             for (mi, slot), its in sorted(groups.items()):
                 deps.append([mi, slot, len(table), len(its)])
@@ -1007,7 +1004,8 @@ class HipExecutor:
                               [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn, fw['dqg'].data_ptr(),
                                fw['epoch'].data_ptr()] +
                               ([self._fc_zero.data_ptr(), self._fc_zero.numel()] if self._fc_zero is not None else []),
-                              self.fold_prof.data_ptr() if self.fold_prof is not None else 0)
+                              self.fold_prof.data_ptr() if self.fold_prof is not None else 0,
+                              two_per_cu=bool(self.tuning.fold_two_per_cu))
 
     def _head_ptrs(self, flats):
         lay = self.layout

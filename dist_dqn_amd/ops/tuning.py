@@ -1,0 +1,51 @@
+"""Tuning constants of the HIP executor's launches (``--kernel_tuning``).
+
+One documented place for the knobs that earlier rounds read from the environment inside the
+launch path (DQN_WG_CHUNKS, DQN_DEP_AT, DQN_FOLD_TWO_PER_CU, DQN_TFACT). They are now fixed when
+the executor is built, from the run configuration:
+
+    --kernel_tuning "wg_conv_chunks=3,dep_at=-1,fold_two_per_cu=1,tfact=0"
+
+Every default is the measured best on MI355X; the measurements are cited per field. Knobs that
+lost their A/B (fc jobs interleaved with the weight-gradient tiles, acquire-fenced dependent jobs,
+sc1 slot loads in the head fold) were removed from the kernels instead.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+
+@dataclasses.dataclass(frozen=True)
+class KernelTuning:
+    # 128-row chunks per conv weight-gradient tile of the fused wgrad + update launch (summed in
+    # registers, one set of fp32 atomics per tile). Round 5 with the two-slot load ring: 3 > 2 > 4 on
+    # the flagship (15.33k / 15.04k / 14.76k SGD steps/s), 3 = 2 on Rainbow (profiles/r5_late_ab.md)
+    wg_conv_chunks: int = 3
+    # grid position of the range-dependent update jobs of that launch: after the first ``dep_at`` fc
+    # jobs; -1 = the measured policy (noisy nets: after 500 of their ~1.6k fc jobs, +0.3-1.0 % over
+    # 300 in 4 of 4 rounds; plain nets: at the end, 0 / 150 / 400 measured no better)
+    dep_at: int = -1
+    # head fold (fc_head.hip) in spin mode may run two blocks per CU when one per CU cannot hold
+    # the grid (dueling / 3-instance launches; round 5, commit 69b1367)
+    fold_two_per_cu: int = 1
+    # noisy C51 nets: the target keeps separate mu / sigma fc fragments written only at a sync and
+    # mixes its noise inside the fc forward. Measured slower (optimizer 58.4 -> 53.2 us but the fc
+    # forward 10.5 -> 20.0 us: 7.29k -> 7.04k SGD steps/s, profiles/r5_late_ab.md), so opt-in
+    tfact: int = 0
+
+    @classmethod
+    def parse(cls, spec: str = '') -> 'KernelTuning':
+        """``"key=value,key=value"`` (empty: the defaults); unknown keys raise."""
+        kw = {}
+        names = {f.name for f in dataclasses.fields(cls)}
+        for part in (spec or '').replace(' ', '').split(','):
+            if not part:
+                continue
+            k, _, v = part.partition('=')
+            if k not in names:
+                raise ValueError('--kernel_tuning: unknown key %r (known: %s)' % (k, sorted(names)))
+            kw[k] = int(v)
+        t = cls(**kw)
+        if t.wg_conv_chunks < 1 or t.wg_conv_chunks > 8:
+            raise ValueError('--kernel_tuning: wg_conv_chunks in [1, 8]')
+        return t

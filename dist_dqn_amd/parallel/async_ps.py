@@ -255,10 +255,22 @@ def ps_lowrank_plan(network, config) -> Optional[dict]:
         lo = b
     if lo < lay.total:
         keep.append((lo, lay.total))
-    if len(keep) + 2 > 6 or any((b - a) % 4 for a, b in keep):
+    # (16-byte pieces: every kept range's start and length, and the factor slot's start, % 4 elements)
+    if len(keep) + 2 > 6 or any((b - a) % 4 or a % 4 for a, b in keep) or holes[0][0] % 4:
         return None
     return {'B': B, 'keep': keep, 'x_off': 4 * holes[0][0], 'dh_off': 4 * holes[0][0] + xbytes,
             'xbytes': xbytes, 'dbytes': dbytes}
+
+
+def _agree_lowrank(ctx: DistContext, plan: Optional[dict]):
+    """The server and every worker must push / read the fc gradient the same way (factor rows or the
+    fp32 gradient): gather every rank's plan over the control plane and fail on every rank together
+    if they differ (a mismatch would read 16-bit factor rows as an fp32 gradient, or the reverse)."""
+    key = None if plan is None else sorted((k, tuple(map(tuple, v)) if k == 'keep' else v) for k, v in plan.items())
+    plans = ctx.ctrl_all_gather_object(key)
+    if any(p != plans[0] for p in plans):
+        raise ValueError('async PS: the low-rank push plan differs across ranks (%s); pass the network to '
+                         'make_ps_client and use the same --ps_lowrank / --minibatch_size everywhere' % (plans,))
 
 
 class _PSShared:
@@ -372,6 +384,7 @@ class XgmiPSServer:
         self.lowrank = ps_lowrank_plan(network, network.config)
         self.n = network.online.flat.numel()
         self.sh = shared or _PSShared(ctx, self.n)
+        _agree_lowrank(ctx, self.lowrank)
         self.workers = list(range(1, ctx.world_size))
         dev = network.online.flat.device
         self._grads = {w: self.sh.ext.tensor_from_ptr(self.sh.slot(w), self.n, dev.index or 0) for w in self.workers}
@@ -542,7 +555,9 @@ class XgmiPSClient:
         # pipelined exchange (--ps_pipeline): take the answer to the previous push, then push; the
         # server answered it while this worker computed the gradient, so the wait is usually over
         self.pipeline = bool(pipeline)
+        self._flushed_at = -1                 # push count whose answer flush() took
         self.lowrank = lowrank                # ps_lowrank_plan: push the fc factors, not the fc gradient
+        _agree_lowrank(ctx, lowrank)          # (the server's plan, checked on every rank)
 
     @property
     def stopped(self) -> bool:
@@ -594,18 +609,24 @@ class XgmiPSClient:
         nb = [4 * (b - a) for a, b in lr['keep']] + [lr['xbytes'], lr['dbytes']]
         self.sh.ext.ps_push_segs(src, dst, nb, self.sh.push_word(self.w), self._seq, PUSH, self._ticket)
 
-    def flush(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None):
-        '''Pipelined exchange: take the answer to the last push (the parameters after it).'''
-        if self.pipeline and not self.stopped:
+    def flush(self, flat: torch.Tensor, global_step: Optional[torch.Tensor] = None) -> bool:
+        '''Pipelined exchange: take the answer to the last push (the parameters after it) into
+        ``flat`` -- a worker's parameters otherwise lag one PS answer behind at the end of training
+        (Learner.finish_ps). Returns whether it pulled.'''
+        if self.pipeline and not self.stopped and self.pushes > 0 and self._flushed_at != self.pushes:
             self._pull(flat, global_step)
+            self._flushed_at = self.pushes
+            return True
+        return False
 
     def check(self) -> bool:
         """False if a pull timed out waiting for the PS (host sync)."""
         return int(self._err[0]) == 0
 
     def close(self):
-        if self.pipeline and not self.stopped and self.pushes > 0:
+        if self.pipeline and not self.stopped and self.pushes > 0 and self._flushed_at != self.pushes:
             # the server must answer the last gradient push before BYE replaces it in the push word
+            # (unless flush() already took that answer)
             scratch = torch.empty(self.n, dtype=torch.float32, device=self._seq.device)
             self._pull(scratch, None)
         if not self.stopped:
@@ -633,6 +654,8 @@ def make_ps_server(ctx: DistContext, network, config):
 
 
 def make_ps_client(ctx: DistContext, flat: torch.Tensor, config, network=None):
+    """``network``: the worker's Network -- its low-rank push plan is decided here and checked
+    against the server's (required for the xgmi transport's --ps_lowrank)."""
     if ps_transport(ctx, config) == 'xgmi':
         try:
             return XgmiPSClient(ctx, flat, timeout_s=float(getattr(config, 'ps_timeout_s', 60.0)),

@@ -62,7 +62,7 @@ def _rank(rank, world, port, transport, steps, q, pipeline=0, lowrank=1):
     else:
         rep = DeviceReplay(20000, (84, 84), 4, device=ctx.device, seed=rank)
         rep.fill_synthetic(20000, 6, seed=rank)
-        ps = make_ps_client(ctx, net.online.flat, cfg)
+        ps = make_ps_client(ctx, net.online.flat, cfg, network=net)
         ps.pull(net.online.flat, net.global_step)
         net.refresh_packed()
         ln = Learner(net, rep, cfg, ctx, ps_client=ps)

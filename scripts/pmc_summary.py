@@ -1,5 +1,6 @@
 """Summarise rocprofv3 --pmc counter CSVs (scripts/profile_counters.sh) per kernel:
-MFMA bf16 FLOPs and busy %, LDS bank-conflict rate, HBM bytes, achieved rates."""
+MFMA FLOPs per type (bf16 / fp16 / fp32: SQ_INSTS_VALU_MFMA_MOPS_* count 512 FLOPs each) and busy %,
+LDS bank-conflict rate, HBM bytes, achieved rates."""
 import collections
 import csv
 import glob
@@ -27,8 +28,8 @@ def short(k):
     return (k[:70] + '...') if len(k) > 73 else k
 
 
-print('| kernel | dispatches | time ms | bf16 MFMA GFLOP | MFMA TFLOP/s | MFMA busy % of kernel | LDS conflict % '
-      '| HBM read MB | HBM write MB | HBM GB/s |')
+print('| kernel | dispatches | time ms | MFMA GFLOP bf16 / fp16 / fp32 | MFMA TFLOP/s | MFMA busy % of kernel '
+      '| LDS conflict % | HBM read MB | HBM write MB | HBM GB/s |')
 print('|---|---|---|---|---|---|---|---|---|---|')
 rows = sorted(vals.items(), key=lambda kv: -dur.get(kv[0], 0.0))
 for k, c in rows:
@@ -36,7 +37,8 @@ for k, c in rows:
         continue
     n = len({d for p, d in calls[k] if 'pass1' in p}) or 1
     t = dur.get(k, 0.0)
-    fl = c.get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0.0) * 512
+    fb, fh, ff = (c.get('SQ_INSTS_VALU_MFMA_MOPS_' + x, 0.0) * 512 for x in ('BF16', 'F16', 'F32'))
+    fl = fb + fh + ff
     busy = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0)
     gui = c.get('GRBM_GUI_ACTIVE', 0.0)
     mfma_pct = 100.0 * busy / (gui * 4 * 256) if gui else 0.0       # 4 SIMDs x 256 CUs
@@ -44,5 +46,5 @@ for k, c in rows:
     conf = 100.0 * c.get('SQ_LDS_BANK_CONFLICT', 0.0) / lds if lds else 0.0
     rd, wr = c.get('FETCH_SIZE', 0.0) / 1024, c.get('WRITE_SIZE', 0.0) / 1024     # KB -> MB
     bw = (rd + wr) / 1024 / t if t else 0.0
-    print('| %s | %d | %.3f | %.3f | %.2f | %.1f | %.1f | %.2f | %.2f | %.0f |' % (
-        short(k), n, t * 1e3, fl / 1e9, fl / t / 1e12 if t else 0.0, mfma_pct, conf, rd, wr, bw))
+    print('| %s | %d | %.3f | %.3f / %.3f / %.3f | %.2f | %.1f | %.1f | %.2f | %.2f | %.0f |' % (
+        short(k), n, t * 1e3, fb / 1e9, fh / 1e9, ff / 1e9, fl / t / 1e12 if t else 0.0, mfma_pct, conf, rd, wr, bw))

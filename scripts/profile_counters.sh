@@ -11,7 +11,9 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 ARGS=${BENCH_ARGS:-"--steps 60 --warmup 10"}
 i=0
-for group in "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" \
+# (pass 1: MFMA ops of every type the builds use -- bf16 (_C), fp16 (_C_f16: Rainbow), fp32 (_C_f32) --
+#  6 SQ + 1 GRBM counters, within one pass's 8 SQ / 2 GRBM)
+for group in "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" \
              "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS" \
              "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i + 1))

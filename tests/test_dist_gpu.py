@@ -404,11 +404,12 @@ def _worker_dp_fused_one_rank(rank, world, port, extra, errq):
             if dp:
                 assert ln._dp_fused and ln._defer_wgrad and ln.reducer.mode == 'xgmi', \
                     (ln._dp_fused, ln._defer_wgrad, ln.reducer.mode)
-                assert ln.reducer.xgmi.dpx is not None and ln.can_step_many()
+                assert ln.reducer.xgmi.dpx is not None
             else:
                 assert not ln.ctx.enabled and ln._defer_wgrad
             for _ in range(3):                          # eager warm-up, then the one-step graph
                 ln.step()
+            assert ln.can_step_many()
             ln.step_many(4)                             # a 4-step graph (the bench's shape)
             torch.cuda.synchronize()
             assert int(net.global_step) == 7
@@ -488,7 +489,7 @@ def _worker_async_ps(rank, world, port, transport, errq, pipeline=0):
         else:
             rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
             rep.fill_synthetic(2048, 6, seed=rank)
-            ps = make_ps_client(ctx, net.online.flat, cfg)
+            ps = make_ps_client(ctx, net.online.flat, cfg, network=net)
             assert getattr(ps, 'transport', 'p2p') == transport, ps
             ps.pull(net.online.flat, net.global_step)
             net.refresh_packed()
@@ -601,7 +602,7 @@ def _worker_async_ps_quiesce(rank, world, port, errq):
         else:
             rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
             rep.fill_synthetic(2048, 6, seed=rank)
-            ps = make_ps_client(ctx, net.online.flat, cfg)
+            ps = make_ps_client(ctx, net.online.flat, cfg, network=net)
             ps.pull(net.online.flat, net.global_step)
             net.refresh_packed()
             ln = Learner(net, rep, cfg, ctx, ps_client=ps)
@@ -647,7 +648,7 @@ def _worker_ps_stall(rank, world, port, errq):
         else:
             rep = DeviceReplay(2048, (84, 84), 4, device=ctx.device, seed=rank)
             rep.fill_synthetic(2048, 6, seed=rank)
-            ps = make_ps_client(ctx, net.online.flat, cfg)
+            ps = make_ps_client(ctx, net.online.flat, cfg, network=net)
             ps.pull(net.online.flat, net.global_step)
             net.refresh_packed()
             ln = Learner(net, rep, cfg, ctx, ps_client=ps)

@@ -468,9 +468,8 @@ def test_rainbow_factorised_target_tracks_syncs(dtype, monkeypatch):
     from dist_dqn_amd.models.executor import TorchExecutor
     from dist_dqn_amd.models.network import Network
     from dist_dqn_amd.replay import DeviceReplay
-    monkeypatch.setenv('DQN_TFACT', '1')                  # (opt-in: see HipExecutor.tfact)
     cfg = preset('nature', 'Pong-v0', '--seed=4 --backend=hip --dtype=%s --replay_memory_capacity=4096 '
-                 '--target_update_freq=3 %s' % (dtype, RAINBOW))
+                 '--target_update_freq=3 --kernel_tuning=tfact=1 %s' % (dtype, RAINBOW))   # (opt-in)
     net = Network.create_network(cfg, (84, 84, 4), 6, device=DEV)
     ex = net.executor
     assert ex.tfact and net.target.flat.data_ptr() in ex._fact

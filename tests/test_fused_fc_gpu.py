@@ -321,7 +321,7 @@ def test_head_kernels_match_pure_torch_loss(extra, fold):
 
 def test_folded_head_dq_wait_timeout_raises(monkeypatch):
     """Spin-mode fold with the tails' dQ publish switched off (DQN_DEBUG_FOLD_NO_PUBLISH, read at
-    launch): every waiting dH block gives up after 1 s, skips its dH write and sets the fold's
+    launch): every waiting dH block gives up after 1 s, writes a zero dH tile and sets the fold's
     error word, and the learner's device check raises instead of training on stale dQ."""
     net, learner = _learner('', True)
     learner.step()                                   # a normal step: no error word
@@ -334,6 +334,10 @@ def test_folded_head_dq_wait_timeout_raises(monkeypatch):
     monkeypatch.delenv('DQN_DEBUG_FOLD_NO_PUBLISH')
     errs = net.executor.fold_errors()
     assert errs and all(e >> 24 == 1 for e in errs), errs
+    # the waiting blocks wrote ZERO dH tiles (no stale previous-step rows): only the groups' tails
+    # (one block per 16-row group) wrote their own tile
+    dh = net.executor._workspace(learner.B, net.device)['dh'].float()
+    assert float((dh == 0).float().mean()) > 0.9, float((dh == 0).float().mean())
     with pytest.raises(RuntimeError, match='folded head'):
         learner._device_checks()
 

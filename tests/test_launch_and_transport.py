@@ -234,3 +234,55 @@ def test_ps_lowrank_plan_pushes_everything_but_the_fc_weights(dueling):
     assert ps_lowrank_plan(net, cfg) is None
     net.executor.noisy = False
     assert ps_lowrank_plan(net, cfg.replace(minibatch_size=64)) is None
+
+
+def _worker_agree_plan(rank, world, port, differ, q):
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        from dist_dqn_amd.parallel import init_distributed
+        from dist_dqn_amd.parallel.async_ps import _agree_lowrank
+        ctx = init_distributed(None, device='cpu')
+        plan = {'B': 32, 'keep': [(0, 64), (128, 256)], 'x_off': 256, 'dh_off': 512, 'xbytes': 64, 'dbytes': 32}
+        if differ and rank == 1:
+            plan = None                              # e.g. a worker built without the network
+        try:
+            _agree_lowrank(ctx, plan)
+            raised = False
+        except ValueError:
+            raised = True
+        assert raised == bool(differ), (rank, raised)
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put('rank %d: %r' % (rank, e))
+
+
+@pytest.mark.parametrize('differ', [False, True])
+def test_async_ps_lowrank_plan_agreement(differ):
+    """The xgmi PS server and its workers must agree on the low-rank push plan: identical plans pass,
+    a worker without one fails on EVERY rank (ValueError, no fallback) instead of corrupting the
+    parameters (the server would read 16-bit factor rows as an fp32 gradient)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_agree_plan, args=(r, 2, port, differ, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    errs = []
+    while not q.empty():
+        errs.append(q.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in ps)
+
+
+def test_kernel_tuning_parse():
+    from dist_dqn_amd.config import preset
+    from dist_dqn_amd.ops.tuning import KernelTuning
+    assert KernelTuning.parse('') == KernelTuning()
+    t = KernelTuning.parse('wg_conv_chunks=2, dep_at=300,tfact=1')
+    assert (t.wg_conv_chunks, t.dep_at, t.fold_two_per_cu, t.tfact) == (2, 300, 1, 1)
+    with pytest.raises(ValueError):
+        KernelTuning.parse('wg_mix=1')              # removed knob: refused, not ignored
+    cfg = preset('nature', 'Pong-v0', '--kernel_tuning=dep_at=0')
+    assert KernelTuning.parse(cfg.kernel_tuning).dep_at == 0
