@@ -716,6 +716,17 @@ torch::Tensor xgmi_dpx_args(std::vector<int64_t> inbox, std::vector<int64_t> sig
   return out;
 }
 
+// one call of the exchange self-test over the channel described by `args` (xgmi_dpx_args bytes, CPU)
+void xgmi_dpx_selftest(torch::Tensor args, torch::Tensor out, int64_t slots, int64_t call) {
+  TORCH_CHECK(args.numel() == (int64_t)sizeof(dqn::DpExchange) && !args.is_cuda(), "dpx selftest: args bytes");
+  CHECK_T(out, torch::kFloat32);
+  dqn::DpExchange x;
+  std::memcpy(&x, args.data_ptr(), sizeof(x));
+  TORCH_CHECK(slots >= 1 && slots <= x.slots && out.numel() >= slots * (int64_t)dqn::kDpxSlotElems, "dpx selftest: slots");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  TORCH_CHECK(launch_dpx_selftest(x, ptr<float>(out), (int)slots, (int)call, cur_stream()) == 0, "dpx selftest launch");
+}
+
 // ---------------------------------------------------------------- fused MLP
 // ints: [L, A, P, Hs, Ds, sw, B, double, huber, fin x4, fout x4, act x4, w_off x4, b_off x4]
 // ptrs: [w_on, w_tg, x, xn, act, rew, done, gam, wts, loss, prio, grad, q_out] (0 = unused)
@@ -784,6 +795,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_allgather", &xgmi_allgather);
   m.def("xgmi_gather_args", &xgmi_gather_args);
   m.def("xgmi_dpx_args", &xgmi_dpx_args);
+  m.def("xgmi_dpx_selftest", &xgmi_dpx_selftest);
   m.attr("DPX_MAX_SLOTS") = dqn::kDpxMaxSlots;
   m.attr("DPX_SLOT_ELEMS") = dqn::kDpxSlotElems;
   m.attr("XGMI_MAX_BLOCKS") = dqn::kXgmiMaxBlocks;

@@ -147,6 +147,8 @@ struct DpLaunch {
   int first, n, blocks;
 };
 }  // namespace dqn
+// the exchange protocol's self-test (xgmi_ar.hip): slots blocks of rank-stamped values, sums -> out
+int launch_dpx_selftest(const dqn::DpExchange& x, float* out, int slots, int call, hipStream_t st);
 
 // Asynchronous parameter server over xGMI peer memory, csrc/kernels/async_ps.hip.
 void launch_ps_push(const float* grad, float* slot, long n, uint64_t* push_word, int64_t* seq, int kind,

@@ -221,6 +221,7 @@ struct CnnFwdArgs {
   act_t* x3[kMaxInst];                                        // [B][256] pooled fc inputs
   int M[kMaxInst];                                             // valid samples per instance
   float scale;
+  int64_t* prof;             // probe only (scripts/probe_cnn.py): [block][8] s_memrealtime stamps
 };
 
 struct CnnBwdArgs {
@@ -228,6 +229,7 @@ struct CnnBwdArgs {
   const act_t* a1; const act_t* a2; const act_t* a3;   // post-ReLU pre-pool activations
   const void* w3d; const void* w2d;           // packed conv3 / conv2 dgrad fragments
   act_t* dz1; act_t* dz2; act_t* dz3;      // d(conv pre-activation) for the wgrads
+  int64_t* prof;             // probe only (scripts/probe_cnn.py): [block][8] s_memrealtime stamps
 };
 
 // Grouped weight-gradient launch (qnet.hip): up to 4 independent layers.

@@ -54,6 +54,10 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   const int b = blockIdx.x, inst = blockIdx.y;
   if (a.M[inst] > 0 && b >= a.M[inst]) return;          // (fused actor instance: E < B samples)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // probe stamps: 0 start, 1 input staged, 2 conv1, 3 pool1, 4 conv2, 5 pool2, 6 conv3, 7 end
+  int64_t* prof = (a.prof != nullptr && tid == 0) ? a.prof + 8 * ((int64_t)inst * gridDim.x + b) : nullptr;
+#define CNN_MARK(i) if (prof) prof[i] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  CNN_MARK(0);
   const int l16 = lane & 15, kg = 8 * (lane >> 4), cq = 4 * (lane >> 4);
   const bool keep = inst == 0 && a.a1 != nullptr;
 
@@ -120,6 +124,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     }
   }
   __syncthreads();
+  CNN_MARK(1);
 
   // ---- conv1 (8x8/4 SAME) -> a1 = ReLU(scale*acc + b); both n-tiles per wave
   {
@@ -151,6 +156,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
       }
     }
   }
+  CNN_MARK(2);
   // conv2 / conv3 fragments now (latency overlaps pool1)
   bfx8 w2r[K2 / 32];
   {
@@ -180,6 +186,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     *reinterpret_cast<bfx8*>(p1p + (y * P1W + x) * LP1 + c8) = tz8();
   }
   __syncthreads();
+  CNN_MARK(3);
 
   // ---- conv2 (4x4/2 SAME) -> a2: wave = n-tile (wave & 3), m-tiles {wave>>2, +2}
   {
@@ -203,6 +210,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
       }
     }
   }
+  CNN_MARK(4);
   bfx8 w3r[K3 / 64];
   {
     const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
@@ -229,6 +237,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     *reinterpret_cast<bfx8*>(p2p + (y * P2W + x) * LP2 + c8) = tz8();
   }
   __syncthreads();
+  CNN_MARK(5);
 
   // ---- conv3 (3x3/1 SAME) -> a3: wave = (n-tile, k-half), partials exchanged in LDS
   {
@@ -250,6 +259,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     if (hi == 0) {
       c = unpark(red, nq, lane, c);
       if (ok) {
+        CNN_MARK(6);
         const pk4_t v = pack4(c + f4(bias3));
         *reinterpret_cast<pk4_t*>(a3 + p * L3 + nq * 16 + cq) = v;
         if (keep) *reinterpret_cast<pk4_t*>(a.a3 + (int64_t)b * R3 * N3 + p * N3 + nq * 16 + cq) = v;
@@ -269,26 +279,39 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     }
     *reinterpret_cast<bfx8*>(a.x3[inst] + (int64_t)b * Q3 * Q3 * N3 + pix * N3 + c8) = m;
   }
+  CNN_MARK(7);
 }
 
 // ======================================================================= backward
-// position (y, x) of a pre-pool map is the argmax of its 2x2/2 window (first max in
-// row-major order over the valid cells) for channel c?
-DQN_DEV bool is_argmax(const act_t* act, int OW, int OH, int L, int y, int x, int c) {
-  const int y0 = y & ~1, x0 = x & ~1;
-  float best = -INFINITY;
-  int by = y0, bx = x0;
+// Window-major pool backward (one thread = one 2x2/2 window x 8 channels): the window's valid cells of
+// the pre-pool map `act` (LDS, L elements per pixel) are read once, the first max in row-major order
+// over the valid cells (the oracle's max_pool2d routing) per channel gets d = dp[window][c] where that
+// maximum is > 0 (ReLU), every other cell 0. (Round 5 ran one thread per pre-pool element, each
+// re-reading its whole window: pool1's backward alone took ~10 us of the launch, scripts/probe_cnn.py.)
+// out[dy * 2 + dx]: the cells' 8 values; valid[]: the cell is inside the map.
+template <int OH, int OW, int L>
+DQN_DEV void pool_bwd8(const act_t* act, const float* dpw, int py, int px, int c8, bfx8* out, bool* valid) {
+  bfx8 v[4];
 #pragma unroll
-  for (int dy = 0; dy < 2; ++dy)
+  for (int i = 0; i < 4; ++i) {
+    const int y = 2 * py + (i >> 1), x = 2 * px + (i & 1);
+    valid[i] = y < OH && x < OW;
+    v[i] = valid[i] ? *reinterpret_cast<const bfx8*>(act + (y * OW + x) * L + c8) : tz8();
+  }
+  const float4 d0 = *reinterpret_cast<const float4*>(dpw + c8), d1 = *reinterpret_cast<const float4*>(dpw + c8 + 4);
+  const float d[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
 #pragma unroll
-    for (int dx = 0; dx < 2; ++dx) {
-      const int yy = y0 + dy, xx = x0 + dx;
-      if (yy < OH && xx < OW) {
-        const float v = (float)act[(yy * OW + xx) * L + c];
-        if (v > best) { best = v; by = yy; bx = xx; }
-      }
+  for (int j = 0; j < 8; ++j) {
+    float best = -INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = (float)v[i][j];
+      if (valid[i] && f > best) { best = f; bi = i; }
     }
-  return by == y && bx == x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i][j] = (act_t)((i == bi && best > 0.f) ? d[j] : 0.f);
+  }
 }
 
 __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
@@ -304,107 +327,171 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4 * 256];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, kg = 8 * (lane >> 4);
+  // probe stamps: 0 start, 1 loads, 2 pool3, 3 conv3 dgrad, 4 pool2, 5 conv2 dgrad, 6 a1 staged, 7 end
+  int64_t* prof = (a.prof != nullptr && tid == 0) ? a.prof + 8 * (int64_t)b : nullptr;
+  CNN_MARK(0);
   const act_t* ga1 = a.a1 + (int64_t)b * R1 * N1;
   const act_t* ga2 = a.a2 + (int64_t)b * R2 * N2;
   const act_t* ga3 = a.a3 + (int64_t)b * R3 * N3;
-  for (int t = tid; t < R1 * N1 / 8; t += 512)
-    reinterpret_cast<bfx8*>(a1s)[t] = reinterpret_cast<const bfx8*>(ga1)[t];
+  // every global load of the kernel that does not depend on its own results, issued up front in one
+  // batch: a1 (needed only by the last stage: held in registers until then, so the first stages wait
+  // for a2 / a3 / dp3 alone), the conv3 dgrad fragments of this wave, the first conv2 dgrad batch
+  // (issued after conv3 below). Round 5 issued them stage by stage: the conv2 dgrad alone waited on
+  // 8 dependent L2 round trips per wave (23.7 us for the launch, profiles/r6_kernel_stats_ref_bf16_v1.md).
+  constexpr int NA1 = (R1 * N1 / 8 + 511) / 512;
+  bfx8 a1r[NA1];
+#pragma unroll
+  for (int j = 0; j < NA1; ++j) {
+    const int t = tid + 512 * j;
+    a1r[j] = t < R1 * N1 / 8 ? reinterpret_cast<const bfx8*>(ga1)[t] : tz8();
+  }
+  const int nq3 = wave & 3, hi3 = wave >> 2;
+  bfx8 w3r[K3 / 64];
+  {
+    const bfx8* W = reinterpret_cast<const bfx8*>(a.w3d);
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) w3r[j] = W[((hi3 * (K3 / 64) + j) * 4 + nq3) * 64 + lane];
+  }
   for (int t = tid; t < R2 * N2 / 8; t += 512)
     reinterpret_cast<bfx8*>(a2s)[t] = reinterpret_cast<const bfx8*>(ga2)[t];
   if (tid < R3 * N3 / 8) reinterpret_cast<bfx8*>(a3s)[tid] = reinterpret_cast<const bfx8*>(ga3)[tid];
   if (tid < Q3 * Q3 * N3) dp3s[tid] = (float)a.dp3[(int64_t)b * Q3 * Q3 * N3 + tid];
   __syncthreads();
+  CNN_MARK(1);
 
-  // ---- pool3 backward + ReLU mask -> dz3 (LDS + global)
-  for (int t = tid; t < R3 * N3; t += 512) {
-    const int p = t / N3, c = t - p * N3, y = p / O3, x = p - y * O3;
-    const float av = (float)a3s[p * N3 + c];
-    float d = 0.f;
-    if (av > 0.f && is_argmax(a3s, O3, O3, N3, y, x, c)) d = dp3s[((y >> 1) * Q3 + (x >> 1)) * N3 + c];
-    dz3s[p * L3 + c] = (act_t)d;
-    a.dz3[(int64_t)b * R3 * N3 + t] = (act_t)d;
+  // ---- pool3 backward + ReLU mask -> dz3 (LDS + global): window-major, 8 channels per thread
+  if (tid < Q3 * Q3 * (N3 / 8)) {
+    const int w = tid / (N3 / 8), c8 = (tid - w * (N3 / 8)) * 8, py = w / Q3, px = w - py * Q3;
+    bfx8 o[4];
+    bool ok[4];
+    pool_bwd8<O3, O3, N3>(a3s, dp3s + w * N3, py, px, c8, o, ok);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!ok[i]) continue;
+      const int p = (2 * py + (i >> 1)) * O3 + 2 * px + (i & 1);
+      *reinterpret_cast<bfx8*>(dz3s + p * L3 + c8) = o[i];
+      *reinterpret_cast<bfx8*>(a.dz3 + (int64_t)b * R3 * N3 + p * N3 + c8) = o[i];
+    }
   }
   __syncthreads();
+  CNN_MARK(2);
 
-  // ---- conv3 dgrad -> dp2 [9][64]: A gathers dz3 (SAME pad 1, stride 1), B = packed dgrad
+  // ---- conv3 dgrad -> dp2 [9][64]: A gathers dz3 (SAME pad 1, stride 1), B = packed dgrad (w3r)
   {
-    const int nq = wave & 3, hi = wave >> 2;
-    const bfx8* W = reinterpret_cast<const bfx8*>(a.w3d);
     const int m = l16;
     const int iy = m / O3, ix = m - iy * O3;
     f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < K3 / 64; ++j) {
-      const int ks = hi * (K3 / 64) + j, tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+      const int ks = hi3 * (K3 / 64) + j, tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
       const int oy = iy + 1 - kh, ox = ix + 1 - kw, co = (ks & 1) * 32 + kg;
       const bool ok = m < R3 && oy >= 0 && oy < O3 && ox >= 0 && ox < O3;
       const bfx8 af = ok ? *reinterpret_cast<const bfx8*>(dz3s + (oy * O3 + ox) * L3 + co) : tz8();
-      c = tmfma(af, W[(ks * 4 + nq) * 64 + lane], c);
+      c = tmfma(af, w3r[j], c);
     }
-    if (hi == 1) park(red, nq, lane, c);
+    if (hi3 == 1) park(red, nq3, lane, c);
     __syncthreads();
-    if (hi == 0) {
-      c = unpark(red, nq, lane, c);
+    if (hi3 == 0) {
+      c = unpark(red, nq3, lane, c);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int mm = 4 * (lane >> 4) + r;
-        if (mm < R3) dp2[mm * N2 + nq * 16 + l16] = c[r];
+        if (mm < R3) dp2[mm * N2 + nq3 * 16 + l16] = c[r];
       }
     }
   }
+  // conv2 dgrad operands: wave w owns n-tile nt = w & 1 of the m-tiles w >> 1 and (w >> 1) + 4 -- the
+  // two tasks share their B fragments, loaded once per 8-deep batch, the next batch in flight (16-bit
+  // builds: double-buffered) while this one's MFMAs run; batch 0 issued now, under pool2's work
+  const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2d);
+  const int nt2 = wave & 1, mtA = wave >> 1;
+  constexpr int NB2 = DQN_ACT_F32 ? 1 : 2;                 // B batches in registers
+  bfx8 bf[NB2][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) bf[0][u] = W2[(u * 2 + nt2) * 64 + lane];
   __syncthreads();
+  CNN_MARK(3);
 
-  // ---- pool2 backward + mask -> dz2
-  for (int t = tid; t < R2 * N2; t += 512) {
-    const int p = t / N2, c = t - p * N2, y = p / O2, x = p - y * O2;
-    const float av = (float)a2s[p * N2 + c];
-    float d = 0.f;
-    if (av > 0.f && is_argmax(a2s, O2, O2, N2, y, x, c)) d = dp2[((y >> 1) * Q2 + (x >> 1)) * N2 + c];
-    dz2s[p * L2 + c] = (act_t)d;
-    a.dz2[(int64_t)b * R2 * N2 + t] = (act_t)d;
+  // ---- pool2 backward + mask -> dz2 (window-major)
+  if (tid < Q2 * Q2 * (N2 / 8)) {
+    const int w = tid / (N2 / 8), c8 = (tid - w * (N2 / 8)) * 8, py = w / Q2, px = w - py * Q2;
+    bfx8 o[4];
+    bool ok[4];
+    pool_bwd8<O2, O2, N2>(a2s, dp2 + w * N2, py, px, c8, o, ok);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!ok[i]) continue;
+      const int p = (2 * py + (i >> 1)) * O2 + 2 * px + (i & 1);
+      *reinterpret_cast<bfx8*>(dz2s + p * L2 + c8) = o[i];
+      *reinterpret_cast<bfx8*>(a.dz2 + (int64_t)b * R2 * N2 + p * N2 + c8) = o[i];
+    }
   }
   __syncthreads();
+  CNN_MARK(4);
 
   // ---- conv2 dgrad -> dp1 [121][32]: 8 m-tiles x 2 n-tiles, K = 16 taps x 64 (32 k-steps)
   {
-    const bfx8* W = reinterpret_cast<const bfx8*>(a.w2d);
-    for (int task = wave; task < 16; task += 8) {
-      const int mt = task >> 1, nt = task & 1;
-      const int m = mt * 16 + l16;
-      const int iy = m / Q1, ix = m - iy * Q1;
-      f32x4 c = {0.f, 0.f, 0.f, 0.f};
-      for (int k8 = 0; k8 < 32; k8 += 8) {
-        bfx8 af[8], bf[8];
+    f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = cA;
+    const int mA = mtA * 16 + l16, mB = (mtA + 4) * 16 + l16;
+    const int iyA = mA / Q1, ixA = mA - iyA * Q1, iyB = mB / Q1, ixB = mB - iyB * Q1;
+    auto gather = [&](int m, int iy, int ix, int ks) -> bfx8 {
+      const int tap = ks >> 1, kh = tap >> 2, kw = tap & 3, co = (ks & 1) * 32 + kg;
+      const int ny = iy + 1 - kh, nx = ix + 1 - kw;              // SAME pad_t = pad_l = 1, stride 2
+      const bool ok = m < Q1 * Q1 && ny >= 0 && nx >= 0 && !(ny & 1) && !(nx & 1) && (ny >> 1) < O2 &&
+                      (nx >> 1) < O2;
+      return ok ? *reinterpret_cast<const bfx8*>(dz2s + ((ny >> 1) * O2 + (nx >> 1)) * L2 + co) : tz8();
+    };
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int ks = k8 + u, tap = ks >> 1, kh = tap >> 2, kw = tap & 3, co = (ks & 1) * 32 + kg;
-          const int ny = iy + 1 - kh, nx = ix + 1 - kw;           // SAME pad_t = pad_l = 1, stride 2
-          const bool ok = m < Q1 * Q1 && ny >= 0 && nx >= 0 && !(ny & 1) && !(nx & 1) && (ny >> 1) < O2 &&
-                          (nx >> 1) < O2;
-          af[u] = ok ? *reinterpret_cast<const bfx8*>(dz2s + ((ny >> 1) * O2 + (nx >> 1)) * L2 + co) : tz8();
-          bf[u] = W[(ks * 2 + nt) * 64 + lane];
-        }
+    for (int q = 0; q < 4; ++q) {                           // 4 batches of 8 k-steps
+      const int cur = NB2 == 2 ? (q & 1) : 0;
+      if (NB2 == 1 && q > 0) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) c = tmfma(af[u], bf[u], c);
+        for (int u = 0; u < 8; ++u) bf[0][u] = W2[((8 * q + u) * 2 + nt2) * 64 + lane];
+      }
+      if (NB2 == 2 && q + 1 < 4) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bf[(q + 1) & (NB2 - 1)][u] = W2[((8 * (q + 1) + u) * 2 + nt2) * 64 + lane];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mm = mt * 16 + 4 * (lane >> 4) + r;
-        if (mm < Q1 * Q1) dp1[mm * N1 + nt * 16 + l16] = c[r];
+      for (int u = 0; u < 8; ++u) {
+        const int ks = 8 * q + u;
+        cA = tmfma(gather(mA, iyA, ixA, ks), bf[cur][u], cA);
+        cB = tmfma(gather(mB, iyB, ixB, ks), bf[cur][u], cB);
       }
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ma = mtA * 16 + 4 * (lane >> 4) + r, mb = (mtA + 4) * 16 + 4 * (lane >> 4) + r;
+      if (ma < Q1 * Q1) dp1[ma * N1 + nt2 * 16 + l16] = cA[r];
+      if (mb < Q1 * Q1) dp1[mb * N1 + nt2 * 16 + l16] = cB[r];
+    }
+  }
+  CNN_MARK(5);
+  // a1 into LDS for the last stage (its loads were issued at the kernel start)
+#pragma unroll
+  for (int j = 0; j < NA1; ++j) {
+    const int t = tid + 512 * j;
+    if (t < R1 * N1 / 8) reinterpret_cast<bfx8*>(a1s)[t] = a1r[j];
   }
   __syncthreads();
+  CNN_MARK(6);
 
   // ---- pool1 backward + mask -> dz1 (global only: the conv1 wgrad input)
   act_t* gdz1 = a.dz1 + (int64_t)b * R1 * N1;
-  for (int t = tid; t < R1 * N1; t += 512) {
-    const int p = t / N1, c = t - p * N1, y = p / O1, x = p - y * O1;
-    const float av = (float)a1s[p * N1 + c];
-    float d = 0.f;
-    if (av > 0.f && is_argmax(a1s, O1, O1, N1, y, x, c)) d = dp1[((y >> 1) * Q1 + (x >> 1)) * N1 + c];
-    gdz1[t] = (act_t)d;
+  for (int t = tid; t < Q1 * Q1 * (N1 / 8); t += 512) {      // (window-major: 484 items, one round)
+    const int w = t / (N1 / 8), c8 = (t - w * (N1 / 8)) * 8, py = w / Q1, px = w - py * Q1;
+    bfx8 o[4];
+    bool ok[4];
+    pool_bwd8<O1, O1, N1>(a1s, dp1 + w * N1, py, px, c8, o, ok);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!ok[i]) continue;
+      const int p = (2 * py + (i >> 1)) * O1 + 2 * px + (i & 1);
+      *reinterpret_cast<bfx8*>(gdz1 + p * N1 + c8) = o[i];
+    }
   }
+  CNN_MARK(7);
+#undef CNN_MARK
 }
 
 }  // namespace dqn

@@ -480,70 +480,19 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // (clamped address) and discard it. (Per-thread predicated loads put a branch and a full
   // vmcnt wait between loads and serialise the item on memory latency.)
   bool gsc1 = false;             // WG dependent job: its gradient is read with sc1 loads
-  // ---- DP: the cross-rank sum of dependent job `dslot`'s gradient (this thread's 4 values g[]).
-  // Push: my values into row `rank` of every PEER's inbox (remote xGMI stores, posted), publish
-  // (system-scope fence + release flag store into every peer's signal word of this slot), wait for
-  // every peer's flag in my own signal words (local polls, bounded), then sum the W rows in rank
-  // order -- the peers' from my inbox, mine from registers: the same bytes in the same order on every
-  // rank, so the replicas stay bit-identical (W = 1: nothing to exchange). Inbox parity alternates
-  // per call of a slot: a rank reaches call k + 2 of a slot only after every peer flagged call k + 1,
-  // i.e. finished reading call k (stream order).
+  // ---- DP: the cross-rank sum of dependent job `dslot`'s gradient slot (xgmi_dev.h dpx_sum: push to
+  // every peer's inbox, flag, wait, sum in rank order -- bit-identical on every rank)
   int dslot = -1;
   float gdp[4] = {0.f, 0.f, 0.f, 0.f};
-  auto dp_sum = [&](float* g) {
+  // (live: this thread holds an element of the job -- the others neither push nor read: a 32 x 64
+  //  tile of the output layer holds 32 x A values, e.g. 6 of 64 columns)
+  auto dp_sum = [&](float* g, bool live) {
     if constexpr (DP) {
-      const DpExchange& X = *dp.x;
-      const int W = X.world, r = X.rank;
-      if (W == 1) return;                                                 // (the sum of one row)
-      const uint32_t k = X.seq[dslot];
-      const long stride = (long)X.slots * kDpxSlotElems;                  // one source rank's rows
-      const long base = (long)(k & 1u) * W * stride + (long)dslot * kDpxSlotElems + 4 * t;
-      const float4 v = make_float4(g[0], g[1], g[2], g[3]);
-      for (int q = 1; q < W; ++q) {
-        const int d = r + q < W ? r + q : r + q - W;                      // (peers staggered across links)
-        *reinterpret_cast<float4*>(X.inbox[d] + base + (long)r * stride) = v;
-      }
-      __threadfence_system();
-      __syncthreads();
-      if (t < W && t != r) store_rel(X.sig[t] + r * kDpxMaxSlots + dslot, k + 1u);
-      if (t < W && t != r) {
-        const uint32_t* f = X.sig[r] + t * kDpxMaxSlots + dslot;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t seen;
-        while ((int32_t)((seen = load_acq(f)) - (k + 1u)) < 0) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > kXgmiTimeoutTicks) {   // flag, do not hang
-            const int code = (int)(0x80000000u | ((uint32_t)kXgmiPhaseDpx << 24) | ((uint32_t)t << 16) | (uint32_t)dslot);
-            if (atomicCAS(X.err, 0, code) == 0) {
-              X.err[1] = (int)(k + 1u);
-              X.err[2] = (int)seen;
-              X.err[3] = (int)k;
-            }
-            break;
-          }
-        }
-      }
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");                   // system scope, every thread
-      const float* in = X.inbox[r] + base;
-      float4 acc = r == 0 ? v : *reinterpret_cast<const float4*>(in);
-      for (int q0 = 1; q0 < W; q0 += 2) {                               // 2 rows in flight, summed in order
-        float4 x[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int q = q0 + u < W ? q0 + u : 0;
-          x[u] = q == r ? v : *reinterpret_cast<const float4*>(in + (long)q * stride);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (q0 + u >= W) break;
-          acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
-        }
-      }
+      const float4 acc = dpx_sum(*dp.x, dslot, t, make_float4(g[0], g[1], g[2], g[3]), live);
       g[0] = acc.x; g[1] = acc.y; g[2] = acc.z; g[3] = acc.w;
-      if (t == 0) X.seq[dslot] = k + 1u;             // (every thread read it before the barriers)
     } else {
       (void)g;
+      (void)live;
     }
   };
   // dependent job jb's summed gradient into gdp (this thread's 4 values in the item's thread map),
@@ -568,7 +517,7 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       gdp[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (ok[j] ? d0 + j : 0)), 0, 16));
-    dp_sum(gdp);
+    dp_sum(gdp, ok[0] || ok[1] || ok[2] || ok[3]);
   };
   auto item = [&](const UpdJob& jb, auto al_c, auto nz_c, auto dg_c) {
     // DG: dL/dsigma is derived from the mu-slot gradient (gnoise given), not read

@@ -154,6 +154,19 @@ __global__ __launch_bounds__(kThreads) void xgmi_allgather_kernel(XgmiGatherArgs
   xgmi_gather_block(g, blockIdx.x, gridDim.x);
 }
 
+// Self-test of the update exchange (xgmi_dev.h dpx_sum), the exact protocol of the fused update's
+// dependent jobs: block = slot, 512 threads x 4 values, v = rank-stamped small integers (exact in
+// fp32), the sum written to out[slot][2048]; thread t of a slot is live unless (t + slot) % 7 == 0
+// (dead lanes neither push nor read, as the partial tiles' outside lanes).
+__global__ __launch_bounds__(512) void dpx_selftest_kernel(DpExchange x, float* out, int call) {
+  const int s = blockIdx.x, t = threadIdx.x;
+  const float base = (float)((s * 512 + t) % 97 + call);
+  const float4 v = make_float4(base + x.rank, base + 2 * x.rank, base + 3 * x.rank, base + 4 * x.rank);
+  const bool live = (t + s) % 7 != 0;
+  const float4 r = dpx_sum(x, s, t, v, live);
+  if (live) reinterpret_cast<float4*>(out + (long)s * kDpxSlotElems)[t] = r;
+}
+
 }  // namespace
 
 }  // namespace dqn
@@ -163,6 +176,12 @@ int launch_xgmi_allgather(const dqn::XgmiGatherArgs& g, int blocks, hipStream_t 
   if (blocks < 1 || blocks > dqn::kXgmiMaxBlocks || a.world < 1 || a.world > dqn::kXgmiMaxRanks) return 1;
   if (g.bytes[0] % 16 != 0 || g.bytes[1] % 16 != 0 || g.bytes[0] + g.bytes[1] > a.cap) return 2;
   hipLaunchKernelGGL(dqn::xgmi_allgather_kernel, dim3(blocks), dim3(dqn::kThreads), 0, st, g);
+  return 0;
+}
+
+int launch_dpx_selftest(const dqn::DpExchange& x, float* out, int slots, int call, hipStream_t st) {
+  if (slots < 1 || slots > x.slots || x.world < 1 || x.world > dqn::kXgmiMaxRanks) return 1;
+  hipLaunchKernelGGL(dqn::dpx_selftest_kernel, dim3(slots), dim3(512), 0, st, x, out, call);
   return 0;
 }
 

@@ -100,4 +100,67 @@ DQN_DEV void xgmi_gather_block(const XgmiGatherArgs& g, int b, int G) {
 }
 
 
+// The data-parallel exchange of the fused update launch (optim_pack.h kModeDp) for one job slot: this
+// thread's 4 values v of the slot's gradient are pushed into row `rank` of every PEER's inbox (remote
+// xGMI stores, posted), published (system-scope fence + release flag store into every peer's signal
+// word of the slot), then every peer's flag is awaited in my own signal words (local polls, bounded:
+// the error word on expiry, no hang) and the W rows are summed in rank order -- the peers' from my
+// inbox, mine from registers: the same bytes in the same order on every rank, so the replicas stay
+// bit-identical. W = 1: v itself, no traffic. Inbox parity alternates per call of a slot: a rank
+// reaches call k + 2 of a slot only after every peer flagged call k + 1, i.e. finished reading call k
+// (stream order). Every thread of the block calls it (two barriers); `live`: this thread holds an
+// element (the others neither push nor read).
+DQN_DEV float4 dpx_sum(const DpExchange& X, int slot, int t, float4 v, bool live) {
+  const int W = X.world, r = X.rank;
+  if (W == 1) return v;
+  const uint32_t k = X.seq[slot];
+  const long stride = (long)X.slots * kDpxSlotElems;                    // one source rank's rows
+  const long base = (long)(k & 1u) * W * stride + (long)slot * kDpxSlotElems + 4 * t;
+  if (live) {
+    for (int q = 1; q < W; ++q) {
+      const int d = r + q < W ? r + q : r + q - W;                      // (peers staggered across links)
+      *reinterpret_cast<float4*>(X.inbox[d] + base + (long)r * stride) = v;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (t < W && t != r) store_rel(X.sig[t] + r * kDpxMaxSlots + slot, k + 1u);
+  if (t < W && t != r) {
+    const uint32_t* f = X.sig[r] + t * kDpxMaxSlots + slot;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t seen;
+    while ((int32_t)((seen = load_acq(f)) - (k + 1u)) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kXgmiTimeoutTicks) {
+        const int code = (int)(0x80000000u | ((uint32_t)kXgmiPhaseDpx << 24) | ((uint32_t)t << 16) | (uint32_t)slot);
+        if (atomicCAS(X.err, 0, code) == 0) {
+          X.err[1] = (int)(k + 1u);
+          X.err[2] = (int)seen;
+          X.err[3] = (int)k;
+        }
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");                     // system scope, every thread
+  const float* in = X.inbox[r] + base;
+  float4 acc = (r == 0 || !live) ? v : *reinterpret_cast<const float4*>(in);
+  for (int q0 = 1; q0 < W; q0 += 2) {                                 // 2 rows in flight, summed in order
+    float4 x[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + u < W ? q0 + u : 0;
+      x[u] = (q == r || !live) ? v : *reinterpret_cast<const float4*>(in + (long)q * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (q0 + u >= W) break;
+      acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
+    }
+  }
+  if (t == 0) X.seq[slot] = k + 1u;                 // (every thread read it before the barriers)
+  return acc;
+}
+
 }  // namespace dqn

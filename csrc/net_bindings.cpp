@@ -266,7 +266,7 @@ std::tuple<torch::Tensor, int64_t> wgrad_plan(std::vector<std::vector<int64_t>> 
 
 // ptrs (4 per group): slots, states, w1, w2, w3, b1, b2, b3, x3, then a1, p1, a2, p2, a3; M as in trunk
 void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale,
-             std::vector<int64_t> M) {
+             std::vector<int64_t> M, int64_t prof) {
   constexpr int I = dqn::kMaxInst;
   TORCH_CHECK(ptrs.size() == 9 * I + 5 && ninst >= 1 && ninst <= I && B >= 1 && M.size() <= (size_t)I, "cnn_fwd args");
   dqn::CnnFwdArgs a{};
@@ -287,19 +287,21 @@ void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst
   }
   a.a1 = P<act_t*>(ptrs[9 * I + 0]); a.p1 = P<act_t*>(ptrs[9 * I + 1]); a.a2 = P<act_t*>(ptrs[9 * I + 2]);
   a.p2 = P<act_t*>(ptrs[9 * I + 3]); a.a3 = P<act_t*>(ptrs[9 * I + 4]);
+  a.prof = P<int64_t*>(prof);
   TORCH_CHECK(a.a1 == nullptr || (a.p1 && a.a2 && a.p2 && a.a3), "cnn_fwd: keep all activations or none");
   a.scale = (float)scale;
   launch_cnn_fwd(a, (int)B, (int)ninst, cur_stream());
 }
 
 // ptrs: dp3, a1, a2, a3, w3d, w2d, dz1, dz2, dz3
-void cnn_bwd(std::vector<int64_t> ptrs, int64_t B) {
+void cnn_bwd(std::vector<int64_t> ptrs, int64_t B, int64_t prof) {
   TORCH_CHECK(ptrs.size() == 9 && B >= 1, "cnn_bwd args");
   for (auto p : ptrs) TORCH_CHECK(p != 0, "cnn_bwd: null pointer");
   dqn::CnnBwdArgs a{};
   a.dp3 = P<const act_t*>(ptrs[0]); a.a1 = P<const act_t*>(ptrs[1]); a.a2 = P<const act_t*>(ptrs[2]);
   a.a3 = P<const act_t*>(ptrs[3]); a.w3d = P<const void*>(ptrs[4]); a.w2d = P<const void*>(ptrs[5]);
   a.dz1 = P<act_t*>(ptrs[6]); a.dz2 = P<act_t*>(ptrs[7]); a.dz3 = P<act_t*>(ptrs[8]);
+  a.prof = P<int64_t*>(prof);
   launch_cnn_bwd(a, (int)B, cur_stream());
 }
 
@@ -500,8 +502,9 @@ void register_net_ops(pybind11::module_& m) {
   m.attr("WG_COUNTERS") = (int)dqn::kWgCounters;
   m.attr("WG_SLOTS") = (int)dqn::kWgSlots;
   m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
-        pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{});
-  m.def("qnet_cnn_bwd", &cnn_bwd);
+        pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{},
+        pybind11::arg("prof") = 0);
+  m.def("qnet_cnn_bwd", &cnn_bwd, pybind11::arg("ptrs"), pybind11::arg("B"), pybind11::arg("prof") = 0);
   m.def("qnet_c51_head", &c51_head, pybind11::arg("ints"), pybind11::arg("dist"), pybind11::arg("flts"),
         pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),
         pybind11::arg("io"), pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),

@@ -97,6 +97,11 @@ class Learner:
             ex.fold_head = bool(int(getattr(config, 'fold_head', 1)))
         if hasattr(ex, 'chain_dgrad'):
             ex.chain_dgrad = int(getattr(config, 'chain_dgrad', 0))
+        if hasattr(ex, 'fold_spin') and self.ctx.enabled and self.ctx.ranks_share_gpu():
+            # several ranks on ONE GPU (rehearsal): no intra-launch spin waits besides the collectives'
+            # own (bounded, co-residency-sized) ones -- a fold tail starved by another rank's spinning
+            # blocks expired its waiters and zeroed their dH (round 6, W = 4 big-batch rehearsal)
+            ex.fold_spin = False
         # the fc weight / bias gradient formed inside the fused optimizer launch from the fc input
         # rows and dH rows (executor.can_defer_fc): no fp32 fc gradient round trip through HBM.
         # Under DP only with the low-rank exchange (the rows are then every rank's)
@@ -153,7 +158,7 @@ class Learner:
         # update's first launch, beside the fc update (executor.can_defer_wgrad): one process, or data
         # parallelism with the in-launch exchange (above)
         dp_fused = bool(self.ctx.enabled and want_dpx and self._lowrank is not None
-                        and getattr(self.reducer.xgmi, 'dpx', None) is not None)
+                        and getattr(self.reducer, 'can_exchange', False))
         self._defer_wgrad = bool(((not self.ctx.enabled and ps_client is None) or dp_fused) and self._defer_fc
                                  and not self._det_wgrad and fuse_wu
                                  and hasattr(ex, 'can_defer_wgrad') and ex.can_defer_wgrad(B, sg))

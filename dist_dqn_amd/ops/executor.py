@@ -119,6 +119,10 @@ class HipExecutor:
         self.two_stream = False
         self.fused_trunk = True     # conv1..conv3 in one per-sample kernel (trunk.hip)
         self.fold_head = True       # training: fc forward + scalar head in one launch (fc_head.hip)
+        # the fold's spin mode (its dH-tile blocks wait for their group's tail: every block resident);
+        # off when several processes share the GPU (the one-GPU DP rehearsals: another rank's spinning
+        # collective blocks can hold the CUs a tail needs -- the waits then expire, learner.py)
+        self.fold_spin = True
         # fc + conv3 dgrads in one launch (dgrad_chain_kernel; 2: + conv2). Opt-in: measured 12.1 us vs
         # 4.96 + 5.16 us for the two launches (the waits and the write-through stores cost more than the
         # launch boundary saves; 14.34k / 13.99k / 14.50k steps/s for 1 / 2 / 0, profiles/r4_dgrad_chain_ab.jsonl)
@@ -132,6 +136,7 @@ class HipExecutor:
         self.trunk_prof = None      # int64 [ninst*B*8] phase-timestamp buffer (scripts/probe_trunk.py)
         self.head_prof = None       # int64 [32] head phase stamps (scripts/probe_head.py)
         self.fold_prof = None       # int64 [blocks * 8] fused fc + head stamps (scripts/probe_fold.py)
+        self.cnn_prof = None        # (fwd, bwd) int64 [blocks * 8] cnn kernel stamps (scripts/probe_cnn.py)
         self._events = {}
 
     # ------------------------------------------------------------ packing
@@ -1001,8 +1006,8 @@ class HipExecutor:
                               [B, self.HH, self.FLAT, self.HH // 16, self.HH, 0, 0, 0, 0, 0, 0],
                               ints, [self.delta], [ws['h'][i].data_ptr() for i in range(nlearn)], w, b, wv, bv, io,
                               [ws['loss_parts'].data_ptr(), ws['dq16'].data_ptr()], actor, actor_f, act_h,
-                              [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn, fw['dqg'].data_ptr(),
-                               fw['epoch'].data_ptr()] +
+                              [fw['q'].data_ptr(), fw['cnt'].data_ptr(), fw['mpad'], nlearn,
+                               fw['dqg'].data_ptr() if self.fold_spin else 0, fw['epoch'].data_ptr()] +
                               ([self._fc_zero.data_ptr(), self._fc_zero.numel()] if self._fc_zero is not None else []),
                               self.fold_prof.data_ptr() if self.fold_prof is not None else 0,
                               two_per_cu=bool(self.tuning.fold_two_per_cu))
@@ -1535,8 +1540,9 @@ class HipCnnExecutor(HipExecutor):
         ptrs = (pad(slots) + pad(states) + pad(pk('conv1/fwd')) + pad(pk('conv2/fwd')) + pad(pk('conv3/fwd'))
                 + pad(bias('conv1/b')) + pad(bias('conv2/b')) + pad(bias('conv3/b'))
                 + pad([ws['x3'][i].data_ptr() for i in range(ninst)]) + keep)
+        prof = self.cnn_prof[0].data_ptr() if self.cnn_prof is not None and keep_acts else 0
         self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale,
-                              list(M))
+                              list(M), prof=prof)
         if fc:
             self._fc_fwd(packs, flats, ws, B, ninst)
 
@@ -1551,7 +1557,8 @@ class HipCnnExecutor(HipExecutor):
         # pool / ReLU / conv dgrad chain per sample -> d(conv pre-activations)
         ext.qnet_cnn_bwd([ws['dz3'].data_ptr(), ws['a1'].data_ptr(), ws['a2'].data_ptr(), ws['a3'].data_ptr(),
                           pko('conv3/dgrad'), pko('conv2/dgrad'), ws['dc1'].data_ptr(), ws['dc2'].data_ptr(),
-                          ws['dc3'].data_ptr()], B)
+                          ws['dc3'].data_ptr()], B,
+                         prof=self.cnn_prof[1].data_ptr() if self.cnn_prof is not None else 0)
         c1, c2, c3 = self.arch.convs
         t1, _, l1, _ = c1.pads()
         t2, _, l2, _ = c2.pads()

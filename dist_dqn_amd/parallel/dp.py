@@ -59,6 +59,7 @@ class GradAllReducer:
         # (learner.py: the conv / output-layer gradients summed inside the update launch)
         self.exchange_slots = int(exchange_slots)
         self.can_gather = False       # the xgmi transport carries a working all-gather channel
+        self.can_exchange = False     # ... and a working in-launch update-exchange channel
         if ctx.enabled and flat_grad.is_cuda and mode in ('xgmi', 'auto'):
             self.xgmi = self._setup_xgmi(mode)
         self.mode = 'xgmi' if self.xgmi is not None else 'rccl'
@@ -85,6 +86,11 @@ class GradAllReducer:
             self.can_gather = x.self_test_gather()
             if not self.can_gather:
                 log.warning('xgmi all-gather failed its self-test; dense gradients all-reduced in full')
+        # the fused update's in-launch exchange channel: its own protocol self-test (a failure keeps
+        # the transport, without the fused DP step: the learner then all-reduces between launches)
+        self.can_exchange = bool(self.exchange_slots > 0 and x.self_test_dpx())
+        if self.exchange_slots > 0 and not self.can_exchange:
+            log.warning('xgmi update-exchange failed its self-test; the DP step keeps a separate all-reduce')
         agree = self._cross_check(x)
         if not agree:
             x.close()

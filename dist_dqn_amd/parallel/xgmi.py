@@ -242,13 +242,45 @@ class XgmiAllReduce:
         cache = self.__dict__.setdefault('_dpx_args', {})
         if key not in cache:
             if 'dev' not in cache:
-                ch = self.dpx
-                host = self.ext.xgmi_dpx_args(ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.ctx.rank,
-                                              self.ctx.world_size, self.dpx_slots, ch.cap)
-                cache['dev'] = host.to(self.ctx.device)
+                cache['dev'] = self._dpx_host().to(self.ctx.device)
             blocks = n if not self.shared_gpu else max(1, min(n, 64 // self.ctx.world_size))
             cache[key] = [cache['dev'].data_ptr(), int(first), int(n), int(blocks)]
         return cache[key]
+
+    def _dpx_host(self) -> torch.Tensor:
+        ch = self.dpx
+        return self.ext.xgmi_dpx_args(ch.data, ch.sig, ch.seq_ptr, ch.err_ptr, self.ctx.rank, self.ctx.world_size,
+                                      self.dpx_slots, ch.cap)
+
+    def self_test_dpx(self) -> bool:
+        """The fused update's in-launch exchange protocol (xgmi_dev.h dpx_sum) over this channel: every
+        slot, three calls (both inbox parities, then again), rank-stamped integers summed exactly, dead
+        lanes skipped; agreed across ranks. The learner uses the fused DP step only when it passes."""
+        ok = self.dpx is not None
+        W, dev = self.ctx.world_size, self.ctx.device
+        n, E = self.dpx_slots, self.ext.DPX_SLOT_ELEMS
+        try:
+            if ok:
+                host = self._dpx_host()
+                t = torch.arange(n * 512, device=dev).view(n, 512)
+                s_idx = torch.arange(n, device=dev).view(n, 1)
+                live = ((t % 512 + s_idx) % 7 != 0).view(n, 512, 1).expand(n, 512, 4)
+                j = torch.arange(1, 5, device=dev, dtype=torch.float32).view(1, 1, 4)
+                for call in range(3):
+                    out = torch.zeros(n * E, dtype=torch.float32, device=dev)
+                    self.ext.xgmi_dpx_selftest(host, out, n, call)
+                    torch.cuda.synchronize(dev)
+                    base = ((t % 97) + call).float().view(n, 512, 1)
+                    want = W * base + j * (W * (W - 1) / 2.0)
+                    got = out.view(n, 512, 4)
+                    ok = ok and bool(torch.equal(got[live], want[live]))
+                ok = ok and self.check()
+        except Exception as e:  # noqa: BLE001
+            log.warning('xgmi update-exchange self-test raised: %s', e)
+            ok = False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag) == 1
 
     _PHASES = {1: 'reduce-scatter (phase A)', 2: 'all-gather (phase B)', 3: 'gather', 4: 'update exchange'}
 
