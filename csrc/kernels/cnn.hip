@@ -85,6 +85,25 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     }
   }
   const int nq = wave & 3, hi = wave >> 2;
+  // conv2 / conv3 fragments: issued before pool1 / pool2 (their latency partly overlaps those
+  // stages). Issuing them with the input loads instead delayed the input staging by ~1.2 us and the
+  // whole forward by ~0.3 us (scripts/probe_cnn.py, round 6), so kept per stage.
+  constexpr bool kEarlyW = false;
+  bfx8 w2r[K2 / 32], w3r[K3 / 64];
+  auto load_w2 = [&]() {
+    const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
+#pragma unroll
+    for (int ks = 0; ks < K2 / 32; ++ks) w2r[ks] = W2[(ks * 4 + nq) * 64 + lane];
+  };
+  auto load_w3 = [&]() {
+    const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) w3r[j] = W3[((hi * (K3 / 64) + j) * 4 + nq) * 64 + lane];
+  };
+  if constexpr (kEarlyW) {
+    load_w2();
+    load_w3();
+  }
   bfx8 w1r[2][K1 / 32];
   {
     const bfx8* W1 = reinterpret_cast<const bfx8*>(a.w1[inst]);
@@ -157,13 +176,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     }
   }
   CNN_MARK(2);
-  // conv2 / conv3 fragments now (latency overlaps pool1)
-  bfx8 w2r[K2 / 32];
-  {
-    const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2[inst]);
-#pragma unroll
-    for (int ks = 0; ks < K2 / 32; ++ks) w2r[ks] = W2[(ks * 4 + nq) * 64 + lane];
-  }
+  if constexpr (!kEarlyW) load_w2();
   __syncthreads();
 
   // ---- pool1 (SAME 21 -> 11, bottom/right window cut) -> padded p1 (zero border)
@@ -211,12 +224,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     }
   }
   CNN_MARK(4);
-  bfx8 w3r[K3 / 64];
-  {
-    const bfx8* W3 = reinterpret_cast<const bfx8*>(a.w3[inst]);
-#pragma unroll
-    for (int j = 0; j < K3 / 64; ++j) w3r[j] = W3[((hi * (K3 / 64) + j) * 4 + nq) * 64 + lane];
-  }
+  if constexpr (!kEarlyW) load_w3();
   __syncthreads();
 
   // ---- pool2 (6 -> 3) -> padded p2

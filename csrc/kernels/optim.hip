@@ -188,11 +188,7 @@ void launch_optim_pack(int op, float* w, const float* g, float* s0, float* s1, f
            (dpl.x != nullptr ? kModeDp : 0);
   // few work blocks (16-bit builds, the common optimizers): no spills, returning-ticket close
   L.few = !DQN_ACT_F32 && !wgm && ff.x == nullptr && njobs <= 256 && (op == 0 || op == 3 || op == 7);
-#if DQN_ACT_F32
-  L.dyn = 0;
-#else
   L.dyn = wgm ? (size_t)kFusedWgLds : 0;
-#endif
   L.st = st;
   L.w = w; L.g = g; L.s0 = s0; L.s1 = s1; L.beta_pow = beta_pow; L.step = step; L.ticket = ticket;
   L.jobs = reinterpret_cast<const UpdJob*>(jobs); L.njobs = njobs;
@@ -235,7 +231,7 @@ int optim_timeline_read(int64_t* out, int nblocks) {
     (void)hipMemcpy(out, b + kProfPhases, 3 * (size_t)nblocks * sizeof(int64_t), hipMemcpyDeviceToHost);
   return nblocks;
 }
-int optim_fc_fuse() { return DQN_ACT_F32 ? 0 : 1; }
+int optim_fc_fuse() { return 1; }   // (every build since round 6: the fp32 FcFuse / fused tiles)
 
 void launch_target_update(float* dst, const float* src, float tau, const int64_t* step, int freq, int n,
                           float* dst2, const float* src2, int n2, hipStream_t st) {

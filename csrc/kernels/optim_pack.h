@@ -116,25 +116,25 @@ constexpr int kSlotFlag = 1;
 // expected -- the learner's periodic check reads it)
 constexpr int kErrFlag = 2;
 
-#if !DQN_ACT_F32
 // Fused fc weight gradient (FcFuse): a 32 (k) x 64 (n) update tile's dW = X^T dH over M rows,
 // 32-row chunks staged ROW-major in LDS (strides + 16 elements: conflict-free transposed reads,
 // as the grouped wgrad), wave w owning the 16 x 16 sub-tile (k: w >> 2, n: w & 3) as dW^T =
 // dH^T X on one v_mfma_f32_16x16x32 per chunk (lane: one k, 4 consecutive n), then through
 // an fp32 LDS tile into the update's own thread map (row r, 4 consecutive n).
-constexpr int kFcSX = 32 + 16, kFcSH = 64 + 16, kFcRS = 64 + 4;
-constexpr int kFcLds = 32 * kFcRS * 4;          // >= staging (32 * (SX + SH) * 2 B) and 4 x 512 fp32
-static_assert(32 * (kFcSX + kFcSH) * 2 <= kFcLds && 4 * 512 * 4 <= kFcLds, "fc LDS plan");
-#endif
+// (fp32 build: the same 32-row chunks staged row-major, each MFMA operand lane reading its 8 rows of
+//  one column with strided 4-byte reads: row strides of 34 / 66 floats put a read's 4 lane groups
+//  (rows 8 g + j) 16 banks apart -- conflict-free)
+constexpr int kFcSX = DQN_ACT_F32 ? 32 + 2 : 32 + 16, kFcSH = DQN_ACT_F32 ? 64 + 2 : 64 + 16, kFcRS = 64 + 4;
+constexpr int kFcStage = 32 * (kFcSX + kFcSH) * (int)sizeof(act_t);
+constexpr int kFcLds = kFcStage > 32 * kFcRS * 4 ? kFcStage : 32 * kFcRS * 4;   // staging, fp32 dW tile, 4 x 512 fp32
+static_assert(4 * 512 * 4 <= kFcLds, "fc LDS plan");
 
-#if !DQN_ACT_F32
 // dynamic LDS of a WG launch: the largest fused weight-gradient tile and the FcFuse staging
 constexpr int kFusedWgLds = (int)WgradTile<kFusedWgMC, 64, 64>::lds_bytes > kFcLds ? (int)WgradTile<kFusedWgMC, 64, 64>::lds_bytes
                                                                                     : kFcLds;
 static_assert(kFusedWgLds <= 40 * 1024, "WG launch LDS: 4 blocks / CU");
 static_assert((int)WgradTile<64, 64, 64>::lds_bytes <= kFusedWgLds && (int)WgradTile<kFusedWgMC, 64, 32>::lds_bytes <= kFusedWgLds,
               "every fused tile fits");
-#endif
 
 struct UpdJob {
   int kind;                      // 0 = tile, 1 = elementwise chunk
@@ -230,8 +230,8 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // sample into teff / tpk (the target's eff / packed buffers): no separate target mix launch.
   constexpr bool UPD = OP >= 0;
   constexpr bool TMIX = (MODE & kModeTmix) != 0, NZOK = (MODE & kModeNoisy) != 0, PEROK = (MODE & kModePer) != 0;
-  constexpr bool FC = (MODE & kModeFc) != 0 && !DQN_ACT_F32 && OP >= 0;
-  constexpr bool WG = (MODE & kModeWg) != 0 && !DQN_ACT_F32 && OP >= 0;
+  constexpr bool FC = (MODE & kModeFc) != 0 && OP >= 0;
+  constexpr bool WG = (MODE & kModeWg) != 0 && OP >= 0;
   constexpr bool FEW = (MODE & kModeFew) != 0 && OP >= 0;
   constexpr bool DP = WG && (MODE & kModeDp) != 0;
   // (TMIX is a template flag: the target-mix registers cost the plain nets occupancy)
@@ -248,7 +248,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
                                                                                     : nullptr;
   if (tl) { tl[0] = (int64_t)__builtin_amdgcn_s_memrealtime(); tl[1] = 0; tl[2] = 0; }
   int32_t* cnt = ticket + kTicketStride;        // end-of-launch arrival counters (see the closing step)
-#if !DQN_ACT_F32
   // ---- a weight-gradient tile, counted on its (member, K-range) when done (the last tile of a
   //      range ran that range's jobs serially: ~4 of them, 8-15 us each, measured; the jobs
   //      now wait in blocks of their own at the end of the grid and run in parallel)
@@ -289,7 +288,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       return;
     }
   }
-#endif
   // block 0 leads (the sampler when the launch draws the next minibatch; always in WG launches,
   // whose block 0 then only closes the launch)
   const bool smp_on = smp.size != nullptr || per.sum != nullptr;
@@ -335,7 +333,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   // WG: thread 0 polls member m's done counter (bounded: a lost arrival flags the error word
   // instead of hanging), then acquires; the caller's barrier releases the block's other waves
   auto wg_wait = [&](int m) {
-#if !DQN_ACT_F32
     if (m < 0 || threadIdx.x != 0) return;
     const int32_t* dc = wg->done + kTicketStride * m;
     const int want = wg->nblk[m];
@@ -350,9 +347,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     // (no acquire fence: the waiter reads nothing the member wrote -- it only must not overwrite
     //  the slot tables before the member's reads completed, which its count follows)
     if (tl) tl[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-#else
-    (void)m;
-#endif
   };
   if (PEROK && sampler && per.sum != nullptr) {
     // prioritized: this step's priorities into the tree (one wave), then the next step's
@@ -390,7 +384,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     if (tl) tl[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
   OPT_MARK(1);
-#if !DQN_ACT_F32
   unsigned char* fcl = WG ? opt_dyn : OptShm<!WG, FC ? kFcLds : 16, 1>::get();
   // dW of this thread's 4 values (tile row k, columns n..n+3 of the item map) from the FcFuse rows
   // this thread's 8-element piece of fc operand rows m0 .. m0 + 31 of the item's 32 (k) x 64 (n)
@@ -426,18 +419,38 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     const int lr = lx ? (t >> 2) : ((t - 128) >> 3);
     const int lc = lx ? 8 * (t & 3) : 8 * ((t - 128) & 7);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#if !DQN_ACT_F32
     const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
     const act_t* ph = Hs + (4 * gq + rq) * kFcSH + nt * 16 + cp;
     const act_t* px = Xs + (4 * gq + rq) * kFcSX + kt * 16 + cp;
+#endif
     for (int m0 = 0; m0 < ff.M; m0 += 32) {
       const bfx8 v = m0 == 0 ? v0 : fc_load(jb, m0);
       __syncthreads();                 // previous chunk's operand reads / previous item's R reads done
+#if DQN_ACT_F32
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (lx) Xs[lr * kFcSX + lc + j] = v[j];
+        else if (lh) Hs[lr * kFcSH + lc + j] = v[j];
+      }
+      __syncthreads();
+      // A = dh^T (rows n), B = x (columns k): lane (row = lane & 15, g = lane >> 4) holds chunk rows
+      // 8 g .. 8 g + 7 of its column (the fp32 k32 operand layout, dqn_act.h)
+      bfx8 af, bfm;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        af[j] = Hs[(8 * (lane >> 4) + j) * kFcSH + nt * 16 + (lane & 15)];
+        bfm[j] = Xs[(8 * (lane >> 4) + j) * kFcSX + kt * 16 + (lane & 15)];
+      }
+      acc = DQN_MFMA16_BUILTIN(af, bfm, acc, 0, 0, 0);
+#else
       if (lx) *reinterpret_cast<bfx8*>(Xs + lr * kFcSX + lc) = v;
       else if (lh) *reinterpret_cast<bfx8*>(Hs + lr * kFcSH + lc) = v;
       __syncthreads();
       // A = dh^T (rows n), B = x (columns k); the same row permutation on both operands
       acc = DQN_MFMA16_BUILTIN(join_tr(lds_tr16(ph), lds_tr16(ph + 16 * kFcSH)),
                                join_tr(lds_tr16(px), lds_tr16(px + 16 * kFcSX)), acc, 0, 0, 0);
+#endif
     }
     __syncthreads();                   // operand reads done before R overwrites the staging
     // acc[r] = dW[k = kt * 16 + (lane & 15)][n = nt * 16 + 4 * (lane >> 4) + r]
@@ -472,7 +485,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       g[j] = ((R[i] + R[512 + i]) + (R[1024 + i] + R[1536 + i])) * kInvLossScale;
     }
   };
-#endif
   // One job item = a 32x64 tile (or a 2048-element chunk) updated by 4 consecutive elements per
   // thread. The body is instantiated per (AL = 16-byte aligned float4 rows, NZ = noisy) so that
   // every global load of the item (mu / sigma / grad / slots / target / noise factors) is an
@@ -621,11 +633,9 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
     // the fc tile's first 32 operand rows (L2 / MALL) join the batch: fc_tile_grad then waits on
     // one round trip instead of issuing its own after the batch has drained
     bfx8 fx0;
-#if !DQN_ACT_F32
     if constexpr (FC && UPD) {
       if (fcj && !elem) fx0 = fc_load(jb, 0);
     }
-#endif
     // factorised-noise factors (loaded with the item's batch, before the fc gradient: a separate
     // round trip after it cost Rainbow's items ~1 us each): f(eps_in[k]) (1 for biases / chunks) and f(eps_out[n + j])
     float nin = 1.f, nout[4] = {1.f, 1.f, 1.f, 1.f}, gin = 1.f, gout[4] = {1.f, 1.f, 1.f, 1.f};
@@ -653,7 +663,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
     }
     if constexpr (UPD) {
-#if !DQN_ACT_F32
       // fused fc weight / bias gradient (block-uniform), formed while the item's HBM loads
       // above are in flight (its X / dH rows are L2-resident)
       if constexpr (FC) {
@@ -663,7 +672,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
           OPT_MARK(6);
         }
       }
-#endif
       if (part != nullptr && jb.part_n > 0) {
         // fixed-order sum of the chunk-group partials (block-uniform branch), 4 loads in flight
         float pv[4];
@@ -809,15 +817,12 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       }
     }
   };
-#if !DQN_ACT_F32
   if constexpr (WG) {
     // (the tile blocks ran wg_tile_run at the top of the kernel and returned)
   }
-#endif
   // a job whose gradient a weight-gradient range of this launch produces (its blocks come after every
   // tile in the grid, so the tiles are resident or done: the wait ends)
   auto dep_wait = [&](int d) {
-#if !DQN_ACT_F32
     if constexpr (WG) {
       if (threadIdx.x == 0) {
         const int m = d / kWgSlots;
@@ -838,9 +843,6 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       __syncthreads();
       gsc1 = true;
     }
-#else
-    (void)d;
-#endif
   };
   if constexpr (FC) {
     // one job per block (the launcher sizes the grid for it): no job loop, so no per-thread loop
@@ -924,13 +926,11 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
   }
   __syncthreads();
   OPT_MARK(3);
-#if !DQN_ACT_F32
   if constexpr (WG) {            // every block has arrived: the sampler / range waits are over
     for (int t = threadIdx.x; t < kMaxWgradMembers + wg->n * kWgSlots; t += blockDim.x)
       if (t < wg->n || t >= kMaxWgradMembers)
         __hip_atomic_store(wg->done + kTicketStride * t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#endif
   if (threadIdx.x == 0) {
     if (step) step[0] = step_now + 1;
     if constexpr (OP == 3) {
@@ -993,7 +993,16 @@ void optim_pack_op(const OptPackLaunch& L) {
 #if DQN_ACT_F32
     switch (L.mode) {
       case 0: OPM(0); break; case 1: OPM(1); break; case 3: OPM(3); break;
-      case 4: OPM(4); break; case 5: OPM(5); break; default: OPM(7); break;
+      case 4: OPM(4); break; case 5: OPM(5); break; case 7: OPM(7); break;
+      // the fused fc weight gradient / weight-gradient + update / DP exchange modes (round 6: the
+      // fp32 build's FcFuse and fused tiles)
+      case 8: OPM(8); break; case 9: OPM(9); break; case 11: OPM(11); break;
+      case 12: OPM(12); break; case 13: OPM(13); break; case 15: OPM(15); break;
+      case 24: OPM(24); break; case 25: OPM(25); break; case 27: OPM(27); break;
+      case 28: OPM(28); break; case 29: OPM(29); break; case 31: OPM(31); break;
+      case 88: OPM(88); break; case 89: OPM(89); break; case 91: OPM(91); break;
+      case 92: OPM(92); break; case 93: OPM(93); break; case 95: OPM(95); break;
+      default: break;
     }
 #else
     constexpr bool kFew = N == 0 || N == 3 || N == 7;   // (the common optimizers' few-block variants)

@@ -411,7 +411,7 @@ __global__ void __launch_bounds__(256) dgrad_s2_kernel(ConvArgs a) {
 #if DQN_ACT_F32
 template <class LD, int MC, int KB, int NB>
 DQN_DEV void wgrad_block(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, act_t* lds) {
-  constexpr int LR = MC + 8;
+  constexpr int LR = WgradTile<MC, KB, NB>::LR;
   constexpr int TPR = 256 / MC;                  // threads per staged row
   constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
   constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / 4, KSTEPS = MC / 32;
@@ -681,7 +681,7 @@ DQN_DEV void wgrad_block_det(const ConvArgs& a, const WgradArgs& g, int bx, int 
 // store 0 into the bias gradient (ranks != 0: the caller's all-reduce then sums it once).
 template <class LD, int MC, int KB, int NB>
 DQN_DEV void wgrad_block_multi(const ConvArgs& a, const WgradArgs& g, int by, int bz, act_t* lds) {
-  constexpr int LR = MC + 8;                     // fp32 build: [k][m] / [n][m] rows
+  constexpr int LR = MC + 8;                     // [k][m] / [n][m] rows (every build: see WgradTile)
   constexpr int SA = KB + 16, SZ = NB + 16;      // 16-bit builds: row-major [m][k] / [m][n] (see WgradTile)
   constexpr int TPR = 256 / MC;
   constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
@@ -1370,7 +1370,7 @@ static bool wgrad_tiles(int kind, int& MC, int& KB, int& NB, size_t& lds) {
     default: return false;
   }
 #if DQN_ACT_F32
-  lds = (size_t)(KB + NB) * (MC + 8) * sizeof(act_t);
+  lds = (size_t)(KB + NB) * (MC + kF32Pad) * sizeof(act_t);   // WgradTile<...>::lds_bytes
 #else
   lds = (size_t)MC * (KB + 16 + NB + 16) * sizeof(act_t);      // WgradTile<...>::lds_bytes
 #endif
@@ -1414,11 +1414,6 @@ int launch_wgrad_group(WgradGroup G, hipStream_t st) {
 }
 
 int wgrad_fused_plan(WgradGroup& G, int conv_chunks) {
-#if DQN_ACT_F32
-  (void)G;
-  (void)conv_chunks;
-  return -1;
-#else
   int total = 0;
   G.slots_member = -1;
   for (int i = 0; i < G.n; ++i) {
@@ -1435,7 +1430,6 @@ int wgrad_fused_plan(WgradGroup& G, int conv_chunks) {
     total += G.nblk[i];
   }
   return total;
-#endif
 }
 
 void launch_head_loss(const HeadArgs& a, hipStream_t st) {

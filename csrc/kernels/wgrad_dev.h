@@ -239,9 +239,14 @@ struct DenseLoader {
 };
 
 #if DQN_ACT_F32
+// fp32 build: the chunk is staged TRANSPOSED ([k][m] and [n][m], m contiguous) so a lane's 8
+// consecutive m values are two ds_read_b128. Rows of MC + 4 floats: a 16-lane read phase (rows
+// 0..15 of one k / n group) then starts on 16 distinct 4-bank groups (MC + 8 put rows r and r + 8
+// on the same banks: ~36 % bank conflicts in the fp32 grouped wgrad, profiles/r6_pmc_dqn_fp32.md).
+constexpr int kF32Pad = 4;
 template <int MC, int KB, int NB>
 struct WgradTile {
-  static constexpr int LR = MC + 8;
+  static constexpr int LR = MC + kF32Pad;
   static constexpr size_t lds_bytes = (size_t)(KB + NB) * LR * sizeof(act_t);
 };
 #else
@@ -264,7 +269,6 @@ DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
 #endif
 
 
-#if !DQN_ACT_F32
 // ------------------------------------------------------------- fused-launch tile
 // One weight-gradient tile (K-range by, N-range bz) over chunk group bx = nper consecutive
 // MC-row chunks of M, run by NTH threads: the chunks are summed in registers (chunk c + 1's
@@ -272,6 +276,8 @@ DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
 // stores when g.atomic == 0: one group covers M). Staging as the 16-bit wgrad_block: row-major
 // [m][k] / [m][n] tiles with the slot swizzle, operands through transposed LDS reads. LDS:
 // WgradTile<MC, KB, NB>::lds_bytes. Every thread of the block calls it (2 barriers per chunk).
+// (fp32 build: the chunk staged transposed, WgradTile's fp32 layout; when NB / 8 < the threads per
+//  row -- conv1's 32 columns with 64-row chunks -- only the first NB / 8 thread groups load dZ)
 template <class LD, int MC, int KB, int NB, int NTH, bool PF = true>
 DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, int nper, act_t* lds,
                         int64_t* ph = nullptr) {
@@ -280,14 +286,22 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
 #define WG_MARK(i) if (ph != nullptr && threadIdx.x == 0 && (i) < 7) ph[i] = (int64_t)__builtin_amdgcn_s_memrealtime()
   WG_MARK(0);
   using Tl = WgradTile<MC, KB, NB>;
-  constexpr int SA = Tl::SA, SZ = Tl::SZ;
   constexpr int NW = NTH / 64, TPR = NTH / MC;
-  constexpr int GA = KB / 8 / TPR, GZ = NB / 8 / TPR;
+  constexpr int GA = KB / 8 / TPR;
+  constexpr bool ZPART = NB / 8 < TPR;           // (fewer dZ fragments per row than threads per row)
+  constexpr int GZ = ZPART ? 1 : NB / 8 / TPR;
   constexpr int TILES = (KB / 16) * (NB / 16), PERW = TILES / NW, KSTEPS = MC / 32;
-  static_assert(NTH % MC == 0 && GA >= 1 && GZ >= 1 && GA * TPR * 8 == KB && GZ * TPR * 8 == NB &&
+  static_assert(NTH % MC == 0 && GA >= 1 && GA * TPR * 8 == KB && (ZPART || GZ * TPR * 8 == NB) &&
                 TILES % NW == 0 && NB <= NTH, "fused wgrad tiling");
+#if DQN_ACT_F32
+  constexpr int LR = Tl::LR;
+  act_t* At = lds;                               // [KB][LR]: A transposed, m contiguous
+  act_t* Zt = lds + KB * LR;                     // [NB][LR]
+#else
+  constexpr int SA = Tl::SA, SZ = Tl::SZ;
   act_t* At = lds;                               // [MC][SA]
   act_t* Zt = lds + MC * SA;                     // [MC][SZ]
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int k_lo = by * KB, n_lo = bz * NB;
   const int nchunks = (a.M + MC - 1) / MC, c0 = bx * nper;
@@ -307,8 +321,9 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
-      const int cz = (n_lo + c8 < g.N ? n_lo + c8 : 0) - n_lo;     // masked groups read column 0
-      vz[i] = sel8(mok && n_lo + c8 < g.N, *reinterpret_cast<const bfx8*>(dz + cz));
+      const bool zok = (!ZPART || c8 < NB) && n_lo + c8 < g.N;
+      const int cz = (zok ? n_lo + c8 : 0) - n_lo;                  // masked groups read column 0
+      vz[i] = sel8(mok && zok, *reinterpret_cast<const bfx8*>(dz + cz));
     }
   };
   auto fetch_a = [&](const LD& ld, Raw* ra) {
@@ -317,6 +332,23 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   };
   auto stage = [&](int c, const Raw* ra, const bfx8* vz) {
     if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
+#if DQN_ACT_F32
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int c8 = (p + i * TPR) * 8, k0 = k_lo + c8;
+      const bfx8 v = sel8(k0 < a.K, LD::conv(ra[i]));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + r] = v[j];
+    }
+#pragma unroll
+    for (int i = 0; i < GZ; ++i) {
+      const int c8 = (p + i * TPR) * 8;
+      if (!ZPART || c8 < NB) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[i][j];
+      }
+    }
+#else
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int k0 = k_lo + (p + i * TPR) * 8;
@@ -324,6 +356,7 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
     }
 #pragma unroll
     for (int i = 0; i < GZ; ++i) *reinterpret_cast<bfx8*>(Zt + r * SZ + (((p + i * TPR) * 8) ^ wsw(r))) = vz[i];
+#endif
     __syncthreads();
   };
   const int gq = lane >> 4, rq = (lane >> 2) & 3, cp = 4 * (lane & 3);
@@ -333,6 +366,25 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   for (int i = 0; i < PERW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
   auto compute = [&]() {
+#if DQN_ACT_F32
+    if (dob && tid < NB) {
+      const act_t* zr = Zt + tid * LR;
+#pragma unroll 8
+      for (int q = 0; q < MC; ++q) dbs += (float)zr[q];
+    }
+    const int kg = 8 * (lane >> 4), row = lane & 15;
+#pragma unroll
+    for (int i = 0; i < PERW; ++i) {
+      const int tile = wave + NW * i;
+      const int kt = tile / NTt, nt = tile - kt * NTt;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * LR + 32 * s + kg);
+        const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * LR + 32 * s + kg);
+        acc[i] = mfma16(af, bf, acc[i]);
+      }
+    }
+#else
     if (dob && tid < NB) {
 #pragma unroll 8
       for (int q = 0; q < MC; ++q) dbs += (float)Zt[q * SZ + (tid ^ wsw(q))];
@@ -350,6 +402,7 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
         acc[i] = mfma16(af, bf, acc[i]);
       }
     }
+#endif
   };
   {
     // loaders of both chunks first (the frame loader's slot-table loads), then the dZ rows, then the A
@@ -418,10 +471,10 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
 #undef WG_MARK
 }
 
-// The fused launch's tiles per member kind (NTH = 512 threads, 128-row chunks, <= 40 KB of
-// LDS: the optimizer blocks beside them keep 4 blocks / CU). Returns false for a kind the fused
-// launch does not run.
-constexpr int kFusedWgMC = 128;
+// The fused launch's tiles per member kind (NTH = 512 threads, 128-row chunks -- 64 in the fp32
+// build, whose staging is twice the bytes --, <= 40 KB of LDS: the optimizer blocks beside them keep
+// 4 blocks / CU). Returns false for a kind the fused launch does not run.
+constexpr int kFusedWgMC = DQN_ACT_F32 ? 64 : 128;
 DQN_DEV_HOST_INLINE bool fused_wgrad_tiles(int kind, int& MC, int& KB, int& NB) {
   switch (kind) {
     case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = kFusedWgMC; KB = 64; NB = 32; return true;
@@ -461,6 +514,5 @@ DQN_DEV int fused_wgrad_block(const WgradGroup& G, int b, act_t* lds, int64_t* p
 #undef WG_TILE
   return i * 256 + by;                           // (member, K-range) of the tile
 }
-#endif
 
 }  // namespace dqn

@@ -290,7 +290,7 @@ class HipExecutor:
         self._wg_pending = None
         self._wg_plans: Dict[tuple, tuple] = {}
         # 128-row chunks per conv weight-gradient tile of the fused launch (KernelTuning.wg_conv_chunks)
-        self.wg_conv_chunks = int(self.tuning.wg_conv_chunks)
+        self.wg_conv_chunks = self.tuning.conv_chunks(self.arch.network, self.compute_dtype)
         # data parallelism (learner.py): the transport whose exchange channel the fused update launch
         # uses to sum the dependent jobs' gradients over every rank (parallel/xgmi.py dpx_launch); None:
         # one process

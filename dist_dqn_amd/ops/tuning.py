@@ -17,10 +17,13 @@ import dataclasses
 
 @dataclasses.dataclass(frozen=True)
 class KernelTuning:
-    # 128-row chunks per conv weight-gradient tile of the fused wgrad + update launch (summed in
-    # registers, one set of fp32 atomics per tile). Round 5 with the two-slot load ring: 3 > 2 > 4 on
-    # the flagship (15.33k / 15.04k / 14.76k SGD steps/s), 3 = 2 on Rainbow (profiles/r5_late_ab.md)
-    wg_conv_chunks: int = 3
+    # row chunks (128 rows; 64 in the fp32 build) per conv weight-gradient tile of the fused wgrad +
+    # update launch (summed in registers, one set of fp32 atomics per tile). -1 = the measured best
+    # per net and build: Nature 384 rows per tile -- bf16 3 > 2 > 4 on the flagship (15.33k / 15.04k /
+    # 14.76k SGD steps/s, profiles/r5_late_ab.md), fp32 6 x 64 (9.52k vs 9.33k at 3, round 6) --; the
+    # reference `cnn` 256 rows -- bf16 2 > 1 > 3 > 6 (17.71k / 15.89k / 16.67k / 14.61k,
+    # profiles/r6_ab_wg_chunks.jsonl)
+    wg_conv_chunks: int = -1
     # grid position of the range-dependent update jobs of that launch: after the first ``dep_at`` fc
     # jobs; -1 = the measured policy (noisy nets: after 500 of their ~1.6k fc jobs, +0.3-1.0 % over
     # 300 in 4 of 4 rounds; plain nets: at the end, 0 / 150 / 400 measured no better)
@@ -46,6 +49,13 @@ class KernelTuning:
                 raise ValueError('--kernel_tuning: unknown key %r (known: %s)' % (k, sorted(names)))
             kw[k] = int(v)
         t = cls(**kw)
-        if t.wg_conv_chunks < 1 or t.wg_conv_chunks > 8:
-            raise ValueError('--kernel_tuning: wg_conv_chunks in [1, 8]')
+        if t.wg_conv_chunks != -1 and not 1 <= t.wg_conv_chunks <= 8:
+            raise ValueError('--kernel_tuning: wg_conv_chunks -1 (auto) or in [1, 8]')
         return t
+
+    def conv_chunks(self, network: str, dtype: str) -> int:
+        """Row chunks per fused conv weight-gradient tile (``wg_conv_chunks``, -1 resolved)."""
+        if self.wg_conv_chunks > 0:
+            return self.wg_conv_chunks
+        rows = 256 if network == 'cnn' else 384
+        return rows // (64 if dtype == 'fp32' else 128)

@@ -282,6 +282,10 @@ def test_kernel_tuning_parse():
     assert KernelTuning.parse('') == KernelTuning()
     t = KernelTuning.parse('wg_conv_chunks=2, dep_at=300,tfact=1')
     assert (t.wg_conv_chunks, t.dep_at, t.fold_two_per_cu, t.tfact) == (2, 300, 1, 1)
+    auto = KernelTuning()                           # -1: the measured best per net / build
+    assert (auto.conv_chunks('nature', 'bf16'), auto.conv_chunks('nature', 'fp32'), auto.conv_chunks('cnn', 'bf16'),
+            auto.conv_chunks('cnn', 'fp32')) == (3, 6, 2, 4)
+    assert t.conv_chunks('cnn', 'fp32') == 2
     with pytest.raises(ValueError):
         KernelTuning.parse('wg_mix=1')              # removed knob: refused, not ignored
     cfg = preset('nature', 'Pong-v0', '--kernel_tuning=dep_at=0')

@@ -57,7 +57,7 @@ def _build(variant, acting, dtype='bf16'):
 
 @pytest.mark.parametrize('variant,acting,dtype', [('dqn', False, 'bf16'), ('dqn', True, 'bf16'), ('dd', True, 'bf16'),
                                                   ('rainbow', True, 'bf16'), ('ref', True, 'bf16'),
-                                                  ('ref', True, 'fp32')])
+                                                  ('ref', True, 'fp32'), ('dqn', True, 'fp32')])
 def test_production_step_matches_fp32_oracle_every_tensor(variant, acting, dtype):
     """(fp32: the reference's precision, held to the fp32 build's tolerances: cosine > 0.9999, norm
     within 0.2 %.)"""
