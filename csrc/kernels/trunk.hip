@@ -197,8 +197,23 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       }
     }
   }
+#if DQN_ACT_F32
+  // fp32 fragments are 32 B per lane: stored as two 16-byte planes (lane-contiguous), so a wave's
+  // b128 reads of one plane are conflict-free (lane-interleaved 32-byte entries put lanes l and l + 8
+  // of a 16-lane read phase on the same banks: 2-way conflicts on every weight read of conv1)
+  {
+    float4* wp = reinterpret_cast<float4*>(wl1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 512 * h, f = e >> 6, l = e & 63;
+      wp[(2 * f) * 64 + l] = make_float4(w1s[h][0], w1s[h][1], w1s[h][2], w1s[h][3]);
+      wp[(2 * f + 1) * 64 + l] = make_float4(w1s[h][4], w1s[h][5], w1s[h][6], w1s[h][7]);
+    }
+  }
+#else
   wl1[tid] = w1s[0];
   wl1[tid + 512] = w1s[1];
+#endif
   __syncthreads();
 #if !DQN_ACT_F32
 #pragma unroll
@@ -236,8 +251,15 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
 #if DQN_ACT_F32
         // fp32 build: the weight fragments (32 B per lane each) stay in LDS and are read per k-step:
         // held in registers (128 VGPRs) they pushed the kernel past 256 VGPRs into scratch spills
-        c0 = tmfma(wl1[(ks * 2 + 0) * 64 + lane], fa[ks], c0);
-        c1 = tmfma(wl1[(ks * 2 + 1) * 64 + lane], fa[ks], c1);
+        const float4* wp = reinterpret_cast<const float4*>(wl1);
+        auto wfrag = [&](int f) {
+          const float4 lo = wp[(2 * f) * 64 + lane], hi4 = wp[(2 * f + 1) * 64 + lane];
+          bfx8 v;
+          v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi4.x; v[5] = hi4.y; v[6] = hi4.z; v[7] = hi4.w;
+          return v;
+        };
+        c0 = tmfma(wfrag(ks * 2 + 0), fa[ks], c0);
+        c1 = tmfma(wfrag(ks * 2 + 1), fa[ks], c1);
 #else
         c0 = tmfma(w1r[0][ks], fa[ks], c0);
         c1 = tmfma(w1r[1][ks], fa[ks], c1);
