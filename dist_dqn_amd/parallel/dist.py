@@ -168,6 +168,10 @@ def init_distributed(config=None, device: str = 'auto', timeout_s: int = 600, fo
     if (world > 1 or force_dp) and backend != 'gloo':
         ctrl = dist.new_group(backend='gloo', timeout=datetime.timedelta(seconds=timeout_s))
     ctx = DistContext(rank, world, local_rank, dev, backend, ctrl, force_dp)
+    if ctx.enabled and use_gpu:
+        # gathered HERE, on every rank, and cached: a later ranks_share_gpu() is then never a
+        # collective that only some ranks reach (the --async_ps server builds no Learner)
+        ctx.device_ids()
     if world > 1 and use_gpu and backend == 'nccl' and ctx.ranks_share_gpu():
         # RCCL needs one GPU per rank: say so here (every rank computes the same answer from the
         # gathered PCI ids) instead of a "Duplicate GPU detected" abort at the first collective

@@ -9,6 +9,7 @@ non-overlapped single-collective path and across replicas.
 """
 import os
 import socket
+import time
 
 import pytest
 import torch
@@ -31,10 +32,13 @@ def _run_ranks(target, args, world=2, timeout=100):
     errq = ctx.SimpleQueue()
     port = _free_port()
     procs = [ctx.Process(target=target, args=(r, world, port) + tuple(args) + (errq,)) for r in range(world)]
+    # (a hung rank dumps its Python stacks shortly before the deadline: _setup)
+    os.environ['DQN_TEST_STACK_DUMP_S'] = str(max(5, timeout - 10))
     for p in procs:
         p.start()
+    deadline = time.monotonic() + timeout          # one deadline for all ranks, not one per join
     for p in procs:
-        p.join(timeout=timeout)
+        p.join(timeout=max(0.0, deadline - time.monotonic()))
     alive = [p for p in procs if p.is_alive()]
     for p in alive:
         p.kill()
@@ -53,7 +57,9 @@ def _setup(rank, world, port):
         # 8 ranks (+ this test process) on ONE GPU: 2 hardware queues each keeps every rank's
         # queues mapped at once (their spinning peer waits need all ranks running together)
         os.environ['GPU_MAX_HW_QUEUES'] = '2'
+    import faulthandler
     import sys
+    faulthandler.dump_traceback_later(float(os.environ.get('DQN_TEST_STACK_DUMP_S', '90')), exit=False)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
