@@ -278,7 +278,7 @@ DQN_DEV int wsw(int row) { return ((row >> 2) & 1) << 3; }
 // WgradTile<MC, KB, NB>::lds_bytes. Every thread of the block calls it (2 barriers per chunk).
 // (fp32 build: the chunk staged transposed, WgradTile's fp32 layout; when NB / 8 < the threads per
 //  row -- conv1's 32 columns with 64-row chunks -- only the first NB / 8 thread groups load dZ)
-template <class LD, int MC, int KB, int NB, int NTH, bool PF = true>
+template <class LD, int MC, int KB, int NB, int NTH, int PF = 2>
 DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, int bz, int nper, act_t* lds,
                         int64_t* ph = nullptr) {
   // ph (probe launches): s_memrealtime at tile start | each chunk staged | each chunk's MFMAs done |
@@ -307,13 +307,20 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   const int nchunks = (a.M + MC - 1) / MC, c0 = bx * nper;
   const int nch = min(nchunks, c0 + nper) - c0;
   const bool dob = g.db != nullptr && by == 0;
-  const int r = tid % MC, p = tid / MC;
+#if DQN_ACT_F32
+  const int r = tid % MC, p = tid / MC;          // (transposed staging: consecutive lanes, consecutive m)
+#else
+  // thread -> (row r, piece p): the TPR threads of a row adjacent, so a wave's 16-byte loads cover
+  // whole 64-byte runs of 16 rows (row-major NHWC / dZ rows) instead of 16 bytes of 64 rows each: 4x
+  // fewer cache-line requests through the CU's address unit per load instruction
+  const int r = tid / TPR, p = tid % TPR;
+#endif
   // two chunk slots in registers: both chunks' loads are issued before either is converted / staged
   // (the u8 conv1 loaders convert inside frag(), and the frame loader's addresses depend on a
   // slot-table load: chunk by chunk, the tile paid ~4 dependent round trips for its 2 chunks)
   using Raw = typename LD::Raw;
-  Raw ra0[GA], ra1[GA];
-  bfx8 vz0[GZ], vz1[GZ];
+  Raw ra0[GA], ra1[GA], ra2[GA];
+  bfx8 vz0[GZ], vz1[GZ], vz2[GZ];
   auto fetch_z = [&](int c, bfx8* vz) {
     const int m = (c0 + c) * MC + r;
     const bool mok = m < a.M;
@@ -405,21 +412,28 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
 #endif
   };
   {
-    // loaders of both chunks first (the frame loader's slot-table loads), then the dZ rows, then the A
-    // fragments: waiting for chunk 0's data leaves chunk 1's loads in flight
-    // (!PF: the A/B baseline -- chunk c + 1's loads issued after chunk c is staged)
+    // loaders of the first PF chunks first (the frame loader's slot-table loads), then the dZ rows, then
+    // the A fragments: waiting for chunk 0's data leaves the later chunks' loads in flight
+    // (PF = 1: the A/B baseline -- chunk c + 1's loads issued after chunk c is staged; PF = 3: a
+    //  three-chunk tile waits on ONE memory round trip instead of two)
     const LD l0(a, 0, c0 * MC + r);
     fetch_z(0, vz0);
-    if (PF && nch > 1) fetch_z(1, vz1);
-    if constexpr (PF) {
+    if (PF >= 2 && nch > 1) fetch_z(1, vz1);
+    if (PF >= 3 && nch > 2) fetch_z(2, vz2);
+    if constexpr (PF >= 2) {
       const LD l1(a, 0, (c0 + 1) * MC + r);
       fetch_a(l0, ra0);
       if (nch > 1) fetch_a(l1, ra1);
+      if constexpr (PF >= 3) {
+        const LD l2(a, 0, (c0 + 2) * MC + r);
+        if (nch > 2) fetch_a(l2, ra2);
+      }
     } else {
       fetch_a(l0, ra0);
     }
   }
-  // chunk j's data lives in slot j & 1; PF refills a slot two chunks ahead, !PF one ahead
+  // chunk j's data lives in slot j % PF (PF = 1: slots j & 1, refilled one chunk ahead); a slot is
+  // refilled PF chunks ahead right after it is staged
   auto refill = [&](int j, Raw* ra, bfx8* vz) {
     if (j < nch) {
       const LD l(a, 0, (c0 + j) * MC + r);
@@ -427,18 +441,40 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
       fetch_a(l, ra);
     }
   };
-  for (int c = 0; c < nch; c += 2) {
-    stage(c, ra0, vz0);
-    WG_MARK(1 + 2 * c);
-    if constexpr (PF) refill(c + 2, ra0, vz0); else refill(c + 1, ra1, vz1);
-    compute();
-    WG_MARK(2 + 2 * c);
-    if (c + 1 < nch) {
-      stage(c + 1, ra1, vz1);
-      WG_MARK(3 + 2 * c);
-      if constexpr (PF) refill(c + 3, ra1, vz1); else refill(c + 2, ra0, vz0);
+  if constexpr (PF >= 3) {
+    for (int c = 0; c < nch; c += 3) {
+      stage(c, ra0, vz0);
+      WG_MARK(1 + 2 * c);
+      refill(c + 3, ra0, vz0);
       compute();
-      WG_MARK(4 + 2 * c);
+      WG_MARK(2 + 2 * c);
+      if (c + 1 < nch) {
+        stage(c + 1, ra1, vz1);
+        WG_MARK(3 + 2 * c);
+        refill(c + 4, ra1, vz1);
+        compute();
+        WG_MARK(4 + 2 * c);
+      }
+      if (c + 2 < nch) {
+        stage(c + 2, ra2, vz2);
+        refill(c + 5, ra2, vz2);
+        compute();
+      }
+    }
+  } else {
+    for (int c = 0; c < nch; c += 2) {
+      stage(c, ra0, vz0);
+      WG_MARK(1 + 2 * c);
+      if constexpr (PF >= 2) refill(c + 2, ra0, vz0); else refill(c + 1, ra1, vz1);
+      compute();
+      WG_MARK(2 + 2 * c);
+      if (c + 1 < nch) {
+        stage(c + 1, ra1, vz1);
+        WG_MARK(3 + 2 * c);
+        if constexpr (PF >= 2) refill(c + 3, ra1, vz1); else refill(c + 2, ra0, vz0);
+        compute();
+        WG_MARK(4 + 2 * c);
+      }
     }
   }
   const bool atomic = g.atomic != 0;
@@ -475,6 +511,10 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
 // build, whose staging is twice the bytes --, <= 40 KB of LDS: the optimizer blocks beside them keep
 // 4 blocks / CU). Returns false for a kind the fused launch does not run.
 constexpr int kFusedWgMC = DQN_ACT_F32 ? 64 : 128;
+#ifndef DQN_WG_PREFETCH
+#define DQN_WG_PREFETCH 2
+#endif
+constexpr int kWgPrefetch = DQN_WG_PREFETCH;
 DQN_DEV_HOST_INLINE bool fused_wgrad_tiles(int kind, int& MC, int& KB, int& NB) {
   switch (kind) {
     case L_NAT_CONV1_FWD: case L_NAT_CONV1_FRAMES: MC = kFusedWgMC; KB = 64; NB = 32; return true;
@@ -500,9 +540,10 @@ DQN_DEV int fused_wgrad_block(const WgradGroup& G, int b, act_t* lds, int64_t* p
   const int bx = b % gx, rr = b / gx, by = rr % gy, bz = rr / gy;
   const ConvArgs& a = G.a[i];
   const WgradArgs& g = G.g[i];
-// (both chunks' loads up front: the fused launch 23.5 -> 23.0 us alone, scripts/probe_split.py,
-//  gpurun_out/r5ab; the one-ahead order stays as wgrad_tile<..., false>)
-#define WG_TILE(LD, MC_, KB_, NB_) wgrad_tile<LD, MC_, KB_, NB_, NTH, true>(a, g, bx, by, bz, g.mloop, lds, ph)
+// (two chunks' loads up front: the fused launch 23.5 -> 23.0 us alone, scripts/probe_split.py,
+//  gpurun_out/r5ab; the one-ahead order stays as wgrad_tile<..., 1>. kWgPrefetch chunks up front:
+//  DQN_WG_PREFETCH at build time, default 2)
+#define WG_TILE(LD, MC_, KB_, NB_) wgrad_tile<LD, MC_, KB_, NB_, NTH, kWgPrefetch>(a, g, bx, by, bz, g.mloop, lds, ph)
   switch (G.kind[i]) {
     case L_NAT_CONV1_FWD: WG_TILE(FwC1, kFusedWgMC, 64, 32); break;
     case L_NAT_CONV1_FRAMES: WG_TILE(FwF1, kFusedWgMC, 64, 32); break;
