@@ -209,7 +209,7 @@ struct OptShm<false, N, TAG> {
   DQN_DEV static unsigned char* get() { return nullptr; }
 };
 template <int OP, int MODE>
-__global__ void __launch_bounds__(kPackThreads, (MODE & kModeDp) ? 4 : (MODE & kModeWg) ? 3 : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? (DQN_ACT_F32 ? 4 : (MODE & kModeFc) ? 8 : 5) : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
+__global__ void __launch_bounds__(kPackThreads, (MODE & kModeDp) ? 4 : (MODE & kModeWg) ? (kWgPrefetch >= 3 ? 4 : 3) : (MODE & kModeFew) ? 4 : (MODE & ~kModeFc) == 0 ? (DQN_ACT_F32 ? 4 : (MODE & kModeFc) ? 8 : 5) : (((MODE & (kModeTmix | kModeNoisy)) || !(OP == -1 || OP == 0 || OP == 3 || OP == 7)) ? 1 : 6))
 optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ S0, float* __restrict__ S1,
                   float* __restrict__ beta_pow, int64_t* __restrict__ step, int32_t* __restrict__ ticket, OptHP h,
                   const UpdJob* __restrict__ jobs, int njobs, act_t* __restrict__ packed, float* __restrict__ tgt,

@@ -244,6 +244,10 @@ struct DenseLoader {
 // 0..15 of one k / n group) then starts on 16 distinct 4-bank groups (MC + 8 put rows r and r + 8
 // on the same banks: ~36 % bank conflicts in the fp32 grouped wgrad, profiles/r6_pmc_dqn_fp32.md).
 constexpr int kF32Pad = 4;
+// fused-tile staging swizzle: row kr (a k or n index) of the transposed chunk stores m at column
+// m ^ fsw(kr) -- a multiple of 4 below 32, so 4-aligned m groups stay contiguous (float4 reads) and m
+// stays inside its 32-aligned half
+DQN_DEV int fsw(int kr) { return 4 * ((kr >> 3) & 7); }
 template <int MC, int KB, int NB>
 struct WgradTile {
   static constexpr int LR = MC + kF32Pad;
@@ -307,14 +311,11 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   const int nchunks = (a.M + MC - 1) / MC, c0 = bx * nper;
   const int nch = min(nchunks, c0 + nper) - c0;
   const bool dob = g.db != nullptr && by == 0;
-#if DQN_ACT_F32
-  const int r = tid % MC, p = tid / MC;          // (transposed staging: consecutive lanes, consecutive m)
-#else
   // thread -> (row r, piece p): the TPR threads of a row adjacent, so a wave's 16-byte loads cover
   // whole 64-byte runs of 16 rows (row-major NHWC / dZ rows) instead of 16 bytes of 64 rows each: 4x
-  // fewer cache-line requests through the CU's address unit per load instruction
+  // fewer cache-line requests through the CU's address unit per load instruction (fused launch
+  // 22.7 -> 21.3 us, bf16). fp32: the transposed staging then swizzles m by k (fsw below)
   const int r = tid / TPR, p = tid % TPR;
-#endif
   // two chunk slots in registers: both chunks' loads are issued before either is converted / staged
   // (the u8 conv1 loaders convert inside frag(), and the frame loader's addresses depend on a
   // slot-table load: chunk by chunk, the tile paid ~4 dependent round trips for its 2 chunks)
@@ -340,19 +341,21 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   auto stage = [&](int c, const Raw* ra, const bfx8* vz) {
     if (c > 0) __syncthreads();                  // the previous chunk's LDS reads are done
 #if DQN_ACT_F32
+    // (row c8 + j of the transposed tile holds m = r at column r ^ fsw(c8): the 8 piece-lanes of a
+    //  row m write 8 k rows 8 * LR words apart -- 2 bank groups -- at distinct columns)
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int c8 = (p + i * TPR) * 8, k0 = k_lo + c8;
       const bfx8 v = sel8(k0 < a.K, LD::conv(ra[i]));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + r] = v[j];
+      for (int j = 0; j < 8; ++j) At[(c8 + j) * LR + (r ^ fsw(c8))] = v[j];
     }
 #pragma unroll
     for (int i = 0; i < GZ; ++i) {
       const int c8 = (p + i * TPR) * 8;
       if (!ZPART || c8 < NB) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + r] = vz[i][j];
+        for (int j = 0; j < 8; ++j) Zt[(c8 + j) * LR + (r ^ fsw(c8))] = vz[i][j];
       }
     }
 #else
@@ -376,18 +379,29 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
 #if DQN_ACT_F32
     if (dob && tid < NB) {
       const act_t* zr = Zt + tid * LR;
+      const int zs = fsw(tid);
 #pragma unroll 8
-      for (int q = 0; q < MC; ++q) dbs += (float)zr[q];
+      for (int q = 0; q < MC; ++q) dbs += (float)zr[q ^ zs];        // (m order)
     }
     const int kg = 8 * (lane >> 4), row = lane & 15;
+    // 8 consecutive m of one k / n row: two 4-float groups, each contiguous under the swizzle
+    auto rd8 = [&](const act_t* base, int kr, int m0) {
+      const act_t* rp = base + kr * LR;
+      const int sw = fsw(kr);
+      const float4 lo = *reinterpret_cast<const float4*>(rp + (m0 ^ sw));
+      const float4 hi = *reinterpret_cast<const float4*>(rp + ((m0 + 4) ^ sw));
+      bfx8 v;
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      return v;
+    };
 #pragma unroll
     for (int i = 0; i < PERW; ++i) {
       const int tile = wave + NW * i;
       const int kt = tile / NTt, nt = tile - kt * NTt;
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
-        const bfx8 af = *reinterpret_cast<const bfx8*>(At + (kt * 16 + row) * LR + 32 * s + kg);
-        const bfx8 bf = *reinterpret_cast<const bfx8*>(Zt + (nt * 16 + row) * LR + 32 * s + kg);
+        const bfx8 af = rd8(At, kt * 16 + row, 32 * s + kg);
+        const bfx8 bf = rd8(Zt, nt * 16 + row, 32 * s + kg);
         acc[i] = mfma16(af, bf, acc[i]);
       }
     }
