@@ -219,10 +219,6 @@ struct CnnFwdArgs {
   const float* b1[kMaxInst]; const float* b2[kMaxInst]; const float* b3[kMaxInst];
   act_t* a1; act_t* p1; act_t* a2; act_t* p2; act_t* a3;  // instance 0, for the backward
   act_t* x3[kMaxInst];                                        // [B][256] pooled fc inputs
-  // [B][441][32] conv1 outputs of each instance made by cnn_conv1_kernel (the conv1 split: several
-  // workgroups per sample); nullptr = the fused kernel runs conv1 itself. Instance 0 keeping its
-  // activations: c1[0] == a1
-  act_t* c1[kMaxInst];
   int M[kMaxInst];                                             // valid samples per instance
   float scale;
   int64_t* prof;             // probe only (scripts/probe_cnn.py): [block][8] s_memrealtime stamps
@@ -280,7 +276,7 @@ int launch_wgrad_group(dqn::WgradGroup G, hipStream_t st);
 // summed in registers per tile, one set of fp32 atomics per group) and atomic flag. Returns the
 // total block count, or -1 when a member kind has no fused tile (16-bit builds only).
 int wgrad_fused_plan(dqn::WgradGroup& G, int conv_chunks);
-void launch_cnn_fwd(const dqn::CnnFwdArgs& a, int B, int ninst, int conv1_split, hipStream_t st);
+void launch_cnn_fwd(const dqn::CnnFwdArgs& a, int B, int ninst, hipStream_t st);
 void launch_cnn_bwd(const dqn::CnnBwdArgs& a, int B, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
 // -1: shape outside the fused kernel's range (A <= 18, HID <= 512, E <= 16, 2-3 learner instances)

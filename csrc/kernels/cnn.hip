@@ -60,15 +60,12 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   CNN_MARK(0);
   const int l16 = lane & 15, kg = 8 * (lane >> 4), cq = 4 * (lane >> 4);
   const bool keep = inst == 0 && a.a1 != nullptr;
-  // conv1 already made by cnn_conv1_kernel (several workgroups per sample): start from its output
-  act_t* const pre = a.c1[inst];
 
   // ---- input loads first (4 pixels x 4 channels per task), then weights / biases
   constexpr int NT = HW / 4;
   uint32_t in[4][4];
   const bool slot_path = a.slots[inst] != nullptr;
-  if (pre != nullptr) {
-  } else if (slot_path) {
+  if (slot_path) {
     const int4 sl = reinterpret_cast<const int4*>(a.slots[inst])[b];
     const uint32_t* f0 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW);
     const uint32_t* f1 = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW);
@@ -108,7 +105,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     load_w3();
   }
   bfx8 w1r[2][K1 / 32];
-  if (pre == nullptr) {
+  {
     const bfx8* W1 = reinterpret_cast<const bfx8*>(a.w1[inst]);
 #pragma unroll
     for (int ks = 0; ks < K1 / 32; ++ks) {
@@ -116,19 +113,13 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
       w1r[1][ks] = W1[(ks * 2 + 1) * 64 + lane];
     }
   }
-  const float4 bias1a = pre == nullptr ? *reinterpret_cast<const float4*>(a.b1[inst] + cq) : float4{};
-  const float4 bias1b = pre == nullptr ? *reinterpret_cast<const float4*>(a.b1[inst] + 16 + cq) : float4{};
+  const float4 bias1a = *reinterpret_cast<const float4*>(a.b1[inst] + cq);
+  const float4 bias1b = *reinterpret_cast<const float4*>(a.b1[inst] + 16 + cq);
   const float4 bias2 = *reinterpret_cast<const float4*>(a.b2[inst] + nq * 16 + cq);
   const float4 bias3 = *reinterpret_cast<const float4*>(a.b3[inst] + nq * 16 + cq);
 
-  if (pre != nullptr) {
-    // conv1 output of this sample ([441][32], post-ReLU) into the padded-row a1 tile
-    const bfx8* src = reinterpret_cast<const bfx8*>(pre + (int64_t)b * R1 * N1);
-    for (int t = tid; t < R1 * N1 / 8; t += 512)
-      *reinterpret_cast<bfx8*>(a1 + (t / (N1 / 8)) * L1 + (t % (N1 / 8)) * 8) = src[t];
-  }
   // ---- zero-padded bf16 NHWC image: interior from the loads, 2-pixel zero border
-  for (int t = tid; pre == nullptr && t < 4 * XW + 4 * IH; t += 512) {       // 688 border pixels
+  for (int t = tid; t < 4 * XW + 4 * IH; t += 512) {       // 688 border pixels
     int y, x;
     if (t < 4 * XW) { const int r = t / XW; y = r < 2 ? r : r + IH; x = t - r * XW; }
     else { const int u = t - 4 * XW, r = u / 4, c = u - r * 4; y = r + XP; x = c < 2 ? c : c + IH; }
@@ -137,7 +128,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int t = tid + 512 * j;
-    if (t >= NT || pre != nullptr) continue;
+    if (t >= NT) continue;
     const int y = (4 * t) / IH, x = 4 * t - y * IH;          // 4 consecutive pixels of one row
     in_t* dst = xin + ((y + XP) * XW + x + XP) * 4;
     if (slot_path) {
@@ -155,7 +146,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   CNN_MARK(1);
 
   // ---- conv1 (8x8/4 SAME) -> a1 = ReLU(scale*acc + b); both n-tiles per wave
-  if (pre == nullptr) {
+  {
     const float scale = a.scale;
     const int kw = kg >> 2;
     act_t* ga1 = keep ? a.a1 + (int64_t)b * R1 * N1 : nullptr;
@@ -297,106 +288,6 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
     *reinterpret_cast<bfx8*>(a.x3[inst] + (int64_t)b * Q3 * Q3 * N3 + pix * N3 + c8) = m;
   }
   CNN_MARK(7);
-}
-
-// ================================================================ conv1 split
-// conv1 of the forward with S workgroups per sample (grid B x ninst x S): workgroup s stages only
-// the padded input rows its ceil(21 / S) output rows read and writes its slice of the post-ReLU
-// conv1 output to c1[inst] ([B][441][32]); cnn_fwd_kernel then starts from it (CnnFwdArgs.c1).
-// One workgroup per sample held conv1 on 68 CUs of 256: MFMA-bound there in the fp32 build (~15 us
-// of the 37 us forward, scripts/probe_cnn.py).
-constexpr int kCnnC1MaxRows = 6;                              // output rows per workgroup (S >= 4)
-__global__ void __launch_bounds__(512) cnn_conv1_kernel(CnnFwdArgs a, int S) {
-  using namespace cnn;
-  __shared__ __attribute__((aligned(16))) in_t xs[(4 * kCnnC1MaxRows + 4) * XW * 4];
-  const int b = blockIdx.x, inst = blockIdx.y, s = blockIdx.z;
-  if (a.M[inst] > 0 && b >= a.M[inst]) return;
-  const int RB = (O1 + S - 1) / S, oy0 = s * RB, oy1 = min(O1, oy0 + RB);
-  if (oy0 >= oy1 || RB > kCnnC1MaxRows) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l16 = lane & 15, kg = 8 * (lane >> 4), cq = 4 * (lane >> 4);
-  const int nrow = 4 * (oy1 - oy0) + 4;                       // padded rows [4 oy0, 4 oy0 + nrow)
-  const int y0 = 4 * oy0 - XP;                                // image row of padded row 0 (may be < 0)
-  const int ya = max(0, y0), yb = min(IH, y0 + nrow);
-  constexpr int TPR = IH / 4;                                 // 4-pixel tasks per image row
-  const int ntask = (yb - ya) * TPR;
-  // input loads first (<= 2 tasks per thread), then the weights
-  uint32_t in[2][4];
-  const bool slot_path = a.slots[inst] != nullptr;
-  const int4 sl = slot_path ? reinterpret_cast<const int4*>(a.slots[inst])[b] : int4{0, 0, 0, 0};
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int t = tid + 512 * j;
-    if (t >= ntask) continue;
-    const int g = ya * TPR + t;                               // 4-pixel group index in the image
-    if (slot_path) {
-      in[j][0] = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.x * HW)[g];
-      in[j][1] = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.y * HW)[g];
-      in[j][2] = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.z * HW)[g];
-      in[j][3] = reinterpret_cast<const uint32_t*>(a.frames + (int64_t)sl.w * HW)[g];
-    } else {
-      const uint4 v = reinterpret_cast<const uint4*>(a.states[inst] + (int64_t)b * HW * 4)[g];
-      in[j][0] = v.x; in[j][1] = v.y; in[j][2] = v.z; in[j][3] = v.w;
-    }
-  }
-  bfx8 w1r[2][K1 / 32];
-  {
-    const bfx8* W1 = reinterpret_cast<const bfx8*>(a.w1[inst]);
-#pragma unroll
-    for (int ks = 0; ks < K1 / 32; ++ks) {
-      w1r[0][ks] = W1[(ks * 2 + 0) * 64 + lane];
-      w1r[1][ks] = W1[(ks * 2 + 1) * 64 + lane];
-    }
-  }
-  const float4 bias1a = *reinterpret_cast<const float4*>(a.b1[inst] + cq);
-  const float4 bias1b = *reinterpret_cast<const float4*>(a.b1[inst] + 16 + cq);
-  // zero padding: the 2 + 2 border columns of every padded row, and whole rows outside the image
-  for (int t = tid; t < nrow * XW; t += 512) {
-    const int r = t / XW, x = t - r * XW, y = y0 + r;
-    if (y < 0 || y >= IH || x < XP || x >= XP + IH)
-      *reinterpret_cast<uint2*>(xs + (r * XW + x) * 4) = make_uint2(0u, 0u);
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int t = tid + 512 * j;
-    if (t >= ntask) continue;
-    const int y = ya + t / TPR, x = 4 * (t % TPR);
-    in_t* dst = xs + ((y - y0) * XW + x + XP) * 4;
-    if (slot_path) {
-      planes_to_lds(in[j][0], in[j][1], in[j][2], in[j][3], dst);
-    } else {
-      uint32_t c[4];
-#pragma unroll
-      for (int ch = 0; ch < 4; ++ch)
-        c[ch] = ((in[j][0] >> 8 * ch) & 0xffu) | (((in[j][1] >> 8 * ch) & 0xffu) << 8) |
-                (((in[j][2] >> 8 * ch) & 0xffu) << 16) | (((in[j][3] >> 8 * ch) & 0xffu) << 24);
-      planes_to_lds(c[0], c[1], c[2], c[3], dst);
-    }
-  }
-  __syncthreads();
-  const float scale = a.scale;
-  const int kw = kg >> 2;
-  act_t* out = a.c1[inst] + (int64_t)b * R1 * N1;
-  const int p0 = oy0 * O1, np = (oy1 - oy0) * O1;
-  for (int mt = wave; mt < (np + 15) / 16; mt += 8) {
-    const int q = mt * 16 + l16;
-    const bool ok = q < np;
-    const int p = p0 + (ok ? q : 0), oy = p / O1, ox = p - oy * O1;
-    const in_t* base = xs + (((oy - oy0) * 4) * XW + ox * 4 + kw) * 4;
-    bfx8 fa[K1 / 32];
-#pragma unroll
-    for (int ks = 0; ks < K1 / 32; ++ks) fa[ks] = ok ? ld_in8(base + ks * XW * 4) : tz8();
-    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-    for (int ks = 0; ks < K1 / 32; ++ks) {
-      c0 = tmfma(w1r[0][ks], fa[ks], c0);
-      c1 = tmfma(w1r[1][ks], fa[ks], c1);
-    }
-    if (ok) {
-      *reinterpret_cast<pk4_t*>(out + p * N1 + cq) = pack4(c0 * scale + f4(bias1a));
-      *reinterpret_cast<pk4_t*>(out + p * N1 + 16 + cq) = pack4(c1 * scale + f4(bias1b));
-    }
-  }
 }
 
 // ======================================================================= backward
@@ -615,9 +506,7 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
 
 using namespace dqn;
 
-void launch_cnn_fwd(const CnnFwdArgs& a, int B, int ninst, int conv1_split, hipStream_t st) {
-  if (conv1_split > 0)
-    hipLaunchKernelGGL(cnn_conv1_kernel, dim3(B, ninst, conv1_split), dim3(512), 0, st, a, conv1_split);
+void launch_cnn_fwd(const CnnFwdArgs& a, int B, int ninst, hipStream_t st) {
   hipLaunchKernelGGL(cnn_fwd_kernel, dim3(B, ninst), dim3(512), 0, st, a);
 }
 

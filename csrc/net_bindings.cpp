@@ -266,7 +266,7 @@ std::tuple<torch::Tensor, int64_t> wgrad_plan(std::vector<std::vector<int64_t>> 
 
 // ptrs (4 per group): slots, states, w1, w2, w3, b1, b2, b3, x3, then a1, p1, a2, p2, a3; M as in trunk
 void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst, double scale,
-             std::vector<int64_t> M, int64_t prof, std::vector<int64_t> c1, int64_t conv1_split) {
+             std::vector<int64_t> M, int64_t prof) {
   constexpr int I = dqn::kMaxInst;
   TORCH_CHECK(ptrs.size() == 9 * I + 5 && ninst >= 1 && ninst <= I && B >= 1 && M.size() <= (size_t)I, "cnn_fwd args");
   dqn::CnnFwdArgs a{};
@@ -290,16 +290,7 @@ void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst
   a.prof = P<int64_t*>(prof);
   TORCH_CHECK(a.a1 == nullptr || (a.p1 && a.a2 && a.p2 && a.a3), "cnn_fwd: keep all activations or none");
   a.scale = (float)scale;
-  // conv1 split: c1 = one [B][441][32] buffer per instance (instance 0 keeping its activations: a1),
-  // conv1_split workgroups per sample (4..21: <= 6 output rows each)
-  TORCH_CHECK(c1.empty() == (conv1_split == 0) && (c1.empty() || (c1.size() == (size_t)ninst &&
-              conv1_split >= 4 && conv1_split <= 21)), "cnn_fwd: c1 buffers and conv1_split 4..21 go together");
-  for (size_t i = 0; i < c1.size(); ++i) {
-    a.c1[i] = P<act_t*>(c1[i]);
-    TORCH_CHECK(a.c1[i] != nullptr && (i != 0 || a.a1 == nullptr || a.c1[0] == a.a1),
-                "cnn_fwd: c1[0] must be the kept a1 buffer");
-  }
-  launch_cnn_fwd(a, (int)B, (int)ninst, (int)conv1_split, cur_stream());
+  launch_cnn_fwd(a, (int)B, (int)ninst, cur_stream());
 }
 
 // ptrs: dp3, a1, a2, a3, w3d, w2d, dz1, dz2, dz3
@@ -512,7 +503,7 @@ void register_net_ops(pybind11::module_& m) {
   m.attr("WG_SLOTS") = (int)dqn::kWgSlots;
   m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
         pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{},
-        pybind11::arg("prof") = 0, pybind11::arg("c1") = std::vector<int64_t>{}, pybind11::arg("conv1_split") = 0);
+        pybind11::arg("prof") = 0);
   m.def("qnet_cnn_bwd", &cnn_bwd, pybind11::arg("ptrs"), pybind11::arg("B"), pybind11::arg("prof") = 0);
   m.def("qnet_c51_head", &c51_head, pybind11::arg("ints"), pybind11::arg("dist"), pybind11::arg("flts"),
         pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),

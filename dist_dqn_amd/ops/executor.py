@@ -1516,7 +1516,6 @@ class HipCnnExecutor(HipExecutor):
             'x3': torch.zeros(4, B * self.FLAT, **bf),
             'h': torch.zeros(4, B * self.HH, **bf),
             'a1': torch.zeros(B * 441 * 32, **bf), 'p1': torch.zeros(B * 121 * 32, **bf),
-            'c1': torch.zeros(4, B * 441 * 32, **bf),    # conv1 split outputs (instances that keep no a1)
             'a2': torch.zeros(B * 36 * 64, **bf), 'p2': torch.zeros(B * 9 * 64, **bf),
             'a3': torch.zeros(B * 9 * 64, **bf),
             'dh': torch.zeros(B * self.HH, **bf), 'dz3': torch.zeros(B * self.FLAT, **bf),
@@ -1542,13 +1541,8 @@ class HipCnnExecutor(HipExecutor):
                 + pad(bias('conv1/b')) + pad(bias('conv2/b')) + pad(bias('conv3/b'))
                 + pad([ws['x3'][i].data_ptr() for i in range(ninst)]) + keep)
         prof = self.cnn_prof[0].data_ptr() if self.cnn_prof is not None and keep_acts else 0
-        split = self.tuning.cnn_split(self.compute_dtype)
-        c1 = []
-        if split:                           # conv1 in its own launch, `split` workgroups per sample
-            c1 = [ws['a1'].data_ptr() if keep_acts else ws['c1'][0].data_ptr()] + \
-                 [ws['c1'][i].data_ptr() for i in range(1, ninst)]
         self.ext.qnet_cnn_fwd(frames.data_ptr() if frames is not None else 0, ptrs, B, ninst, self.input_scale,
-                              list(M), prof=prof, c1=c1, conv1_split=split)
+                              list(M), prof=prof)
         if fc:
             self._fc_fwd(packs, flats, ws, B, ninst)
 

@@ -35,9 +35,6 @@ class KernelTuning:
     # mixes its noise inside the fc forward. Measured slower (optimizer 58.4 -> 53.2 us but the fc
     # forward 10.5 -> 20.0 us: 7.29k -> 7.04k SGD steps/s, profiles/r5_late_ab.md), so opt-in
     tfact: int = 0
-    # reference `cnn` forward: conv1 in a launch of its own with this many workgroups per sample
-    # (4..21; 0 = inside the fused per-sample kernel). -1 = the measured best per build
-    cnn_conv1_split: int = -1
 
     @classmethod
     def parse(cls, spec: str = '') -> 'KernelTuning':
@@ -54,15 +51,7 @@ class KernelTuning:
         t = cls(**kw)
         if t.wg_conv_chunks != -1 and not 1 <= t.wg_conv_chunks <= 8:
             raise ValueError('--kernel_tuning: wg_conv_chunks -1 (auto) or in [1, 8]')
-        if t.cnn_conv1_split not in (-1, 0) and not 4 <= t.cnn_conv1_split <= 21:
-            raise ValueError('--kernel_tuning: cnn_conv1_split -1 (auto), 0 or in [4, 21]')
         return t
-
-    def cnn_split(self, dtype: str) -> int:
-        """Workgroups per sample of the cnn conv1 launch (0: conv1 inside the fused forward)."""
-        if self.cnn_conv1_split >= 0:
-            return self.cnn_conv1_split
-        return 4 if dtype == 'fp32' else 0
 
     def conv_chunks(self, network: str, dtype: str) -> int:
         """Row chunks per fused conv weight-gradient tile (``wg_conv_chunks``, -1 resolved)."""

@@ -66,19 +66,6 @@ def test_q_values_match_oracle(extra):
     assert _rel(q, q_ref) < (1e-4 if F32 in extra else 2e-2)
 
 
-@pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
-def test_cnn_conv1_split_equals_fused(dtype):
-    """Reference cnn: conv1 in its own launch with 4 / 7 workgroups per sample (KernelTuning
-    cnn_conv1_split) gives the fused forward's Q-values exactly (same per-output MFMA order)."""
-    qs = []
-    for split in (0, 4, 7):
-        net, _, batch = _setup('cnn:--dtype=%s --kernel_tuning=cnn_conv1_split=%d' % (dtype, split))
-        assert net.executor.tuning.cnn_split(dtype) == split
-        qs.append(net.q_values(batch['states']))
-    for q in qs[1:]:
-        torch.testing.assert_close(q, qs[0], rtol=0, atol=0)
-
-
 @pytest.mark.parametrize('extra,B,weighted', [('', 32, False), ('--dueling --double_dqn --loss=huber', 32, True),
                                              ('', 7, False), ('--double_dqn', 64, False),
                                              ('--distributional', 32, False), ('--noisy', 32, False),

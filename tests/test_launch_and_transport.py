@@ -286,10 +286,6 @@ def test_kernel_tuning_parse():
     assert (auto.conv_chunks('nature', 'bf16'), auto.conv_chunks('nature', 'fp32'), auto.conv_chunks('cnn', 'bf16'),
             auto.conv_chunks('cnn', 'fp32')) == (3, 6, 2, 4)
     assert t.conv_chunks('cnn', 'fp32') == 2
-    assert (auto.cnn_split('fp32'), auto.cnn_split('bf16')) == (4, 0)
-    assert KernelTuning.parse('cnn_conv1_split=7').cnn_split('bf16') == 7
-    with pytest.raises(ValueError):
-        KernelTuning.parse('cnn_conv1_split=3')     # <= 6 conv1 output rows per workgroup
     with pytest.raises(ValueError):
         KernelTuning.parse('wg_mix=1')              # removed knob: refused, not ignored
     cfg = preset('nature', 'Pong-v0', '--kernel_tuning=dep_at=0')
