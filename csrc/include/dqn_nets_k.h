@@ -277,7 +277,7 @@ int launch_wgrad_group(dqn::WgradGroup G, hipStream_t st);
 // total block count, or -1 when a member kind has no fused tile (16-bit builds only).
 int wgrad_fused_plan(dqn::WgradGroup& G, int conv_chunks);
 void launch_cnn_fwd(const dqn::CnnFwdArgs& a, int B, int ninst, hipStream_t st);
-void launch_cnn_bwd(const dqn::CnnBwdArgs& a, int B, hipStream_t st);
+void launch_cnn_bwd(const dqn::CnnBwdArgs& a, int B, int parts, hipStream_t st);
 void launch_head_loss(const dqn::HeadArgs& a, hipStream_t st);
 // -1: shape outside the fused kernel's range (A <= 18, HID <= 512, E <= 16, 2-3 learner instances)
 int launch_fc_head(const dqn::ConvArgs& a, const dqn::HeadArgs& h, const dqn::FoldArgs& f, hipStream_t st);

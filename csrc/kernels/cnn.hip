@@ -335,8 +335,13 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4 * 256];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, kg = 8 * (lane >> 4);
+  // two workgroups per sample (gridDim.y == 2): both run the cheap stages up to dz2 (part 0 writes
+  // dz3 / dz2), then each takes half of the conv2 dgrad m-tiles and their pool1 windows -- one
+  // workgroup per sample held the 32-sample backward on 32 CUs, the conv2 dgrad MFMA-bound there
+  // in the fp32 build (16 of its 30 us, scripts/probe_cnn.py)
+  const int part = blockIdx.y, nparts = gridDim.y;
   // probe stamps: 0 start, 1 loads, 2 pool3, 3 conv3 dgrad, 4 pool2, 5 conv2 dgrad, 6 a1 staged, 7 end
-  int64_t* prof = (a.prof != nullptr && tid == 0) ? a.prof + 8 * (int64_t)b : nullptr;
+  int64_t* prof = (a.prof != nullptr && tid == 0 && part == 0) ? a.prof + 8 * (int64_t)b : nullptr;
   CNN_MARK(0);
   const act_t* ga1 = a.a1 + (int64_t)b * R1 * N1;
   const act_t* ga2 = a.a2 + (int64_t)b * R2 * N2;
@@ -378,7 +383,7 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
       if (!ok[i]) continue;
       const int p = (2 * py + (i >> 1)) * O3 + 2 * px + (i & 1);
       *reinterpret_cast<bfx8*>(dz3s + p * L3 + c8) = o[i];
-      *reinterpret_cast<bfx8*>(a.dz3 + (int64_t)b * R3 * N3 + p * N3 + c8) = o[i];
+      if (part == 0) *reinterpret_cast<bfx8*>(a.dz3 + (int64_t)b * R3 * N3 + p * N3 + c8) = o[i];
     }
   }
   __syncthreads();
@@ -412,7 +417,9 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   // two tasks share their B fragments, loaded once per 8-deep batch, the next batch in flight (16-bit
   // builds: double-buffered) while this one's MFMAs run; batch 0 issued now, under pool2's work
   const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2d);
-  const int nt2 = wave & 1, mtA = wave >> 1;
+  // (one part: m-tiles w >> 1 and (w >> 1) + 4 per wave; two parts: m-tile 4 part + (w >> 1) only)
+  const int nt2 = wave & 1, mtA = (wave >> 1) + 4 * part;
+  const bool twom = nparts == 1;
   constexpr int NB2 = DQN_ACT_F32 ? 1 : 2;                 // B batches in registers
   bfx8 bf[NB2][8];
 #pragma unroll
@@ -431,7 +438,7 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
       if (!ok[i]) continue;
       const int p = (2 * py + (i >> 1)) * O2 + 2 * px + (i & 1);
       *reinterpret_cast<bfx8*>(dz2s + p * L2 + c8) = o[i];
-      *reinterpret_cast<bfx8*>(a.dz2 + (int64_t)b * R2 * N2 + p * N2 + c8) = o[i];
+      if (part == 0) *reinterpret_cast<bfx8*>(a.dz2 + (int64_t)b * R2 * N2 + p * N2 + c8) = o[i];
     }
   }
   __syncthreads();
@@ -464,14 +471,14 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
       for (int u = 0; u < 8; ++u) {
         const int ks = 8 * q + u;
         cA = tmfma(gather(mA, iyA, ixA, ks), bf[cur][u], cA);
-        cB = tmfma(gather(mB, iyB, ixB, ks), bf[cur][u], cB);
+        if (twom) cB = tmfma(gather(mB, iyB, ixB, ks), bf[cur][u], cB);
       }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ma = mtA * 16 + 4 * (lane >> 4) + r, mb = (mtA + 4) * 16 + 4 * (lane >> 4) + r;
       if (ma < Q1 * Q1) dp1[ma * N1 + nt2 * 16 + l16] = cA[r];
-      if (mb < Q1 * Q1) dp1[mb * N1 + nt2 * 16 + l16] = cB[r];
+      if (twom && mb < Q1 * Q1) dp1[mb * N1 + nt2 * 16 + l16] = cB[r];
     }
   }
   CNN_MARK(5);
@@ -486,7 +493,9 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
 
   // ---- pool1 backward + mask -> dz1 (global only: the conv1 wgrad input)
   act_t* gdz1 = a.dz1 + (int64_t)b * R1 * N1;
-  for (int t = tid; t < Q1 * Q1 * (N1 / 8); t += 512) {      // (window-major: 484 items, one round)
+  // (this part's windows: the dp1 rows its conv2 dgrad m-tiles made -- 64 per part of two)
+  const int w_lo = nparts == 1 ? 0 : 64 * part, w_hi = nparts == 1 ? Q1 * Q1 : min(Q1 * Q1, 64 * part + 64);
+  for (int t = tid + w_lo * (N1 / 8); t < w_hi * (N1 / 8); t += 512) {      // (window-major, one round)
     const int w = t / (N1 / 8), c8 = (t - w * (N1 / 8)) * 8, py = w / Q1, px = w - py * Q1;
     bfx8 o[4];
     bool ok[4];
@@ -510,6 +519,6 @@ void launch_cnn_fwd(const CnnFwdArgs& a, int B, int ninst, hipStream_t st) {
   hipLaunchKernelGGL(cnn_fwd_kernel, dim3(B, ninst), dim3(512), 0, st, a);
 }
 
-void launch_cnn_bwd(const CnnBwdArgs& a, int B, hipStream_t st) {
-  hipLaunchKernelGGL(cnn_bwd_kernel, dim3(B), dim3(512), 0, st, a);
+void launch_cnn_bwd(const CnnBwdArgs& a, int B, int parts, hipStream_t st) {
+  hipLaunchKernelGGL(cnn_bwd_kernel, dim3(B, parts == 2 ? 2 : 1), dim3(512), 0, st, a);
 }

@@ -294,15 +294,15 @@ void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst
 }
 
 // ptrs: dp3, a1, a2, a3, w3d, w2d, dz1, dz2, dz3
-void cnn_bwd(std::vector<int64_t> ptrs, int64_t B, int64_t prof) {
-  TORCH_CHECK(ptrs.size() == 9 && B >= 1, "cnn_bwd args");
+void cnn_bwd(std::vector<int64_t> ptrs, int64_t B, int64_t prof, int64_t parts) {
+  TORCH_CHECK(ptrs.size() == 9 && B >= 1 && (parts == 1 || parts == 2), "cnn_bwd args (parts 1 or 2)");
   for (auto p : ptrs) TORCH_CHECK(p != 0, "cnn_bwd: null pointer");
   dqn::CnnBwdArgs a{};
   a.dp3 = P<const act_t*>(ptrs[0]); a.a1 = P<const act_t*>(ptrs[1]); a.a2 = P<const act_t*>(ptrs[2]);
   a.a3 = P<const act_t*>(ptrs[3]); a.w3d = P<const void*>(ptrs[4]); a.w2d = P<const void*>(ptrs[5]);
   a.dz1 = P<act_t*>(ptrs[6]); a.dz2 = P<act_t*>(ptrs[7]); a.dz3 = P<act_t*>(ptrs[8]);
   a.prof = P<int64_t*>(prof);
-  launch_cnn_bwd(a, (int)B, cur_stream());
+  launch_cnn_bwd(a, (int)B, (int)parts, cur_stream());
 }
 
 // Scalar head. qp = [loss_parts, dq16]: per-16-sample-tile loss partials (training; summed by
@@ -504,7 +504,8 @@ void register_net_ops(pybind11::module_& m) {
   m.def("qnet_cnn_fwd", &cnn_fwd, pybind11::arg("frames"), pybind11::arg("ptrs"), pybind11::arg("B"),
         pybind11::arg("ninst"), pybind11::arg("scale"), pybind11::arg("M") = std::vector<int64_t>{},
         pybind11::arg("prof") = 0);
-  m.def("qnet_cnn_bwd", &cnn_bwd, pybind11::arg("ptrs"), pybind11::arg("B"), pybind11::arg("prof") = 0);
+  m.def("qnet_cnn_bwd", &cnn_bwd, pybind11::arg("ptrs"), pybind11::arg("B"), pybind11::arg("prof") = 0,
+        pybind11::arg("parts") = 1);
   m.def("qnet_c51_head", &c51_head, pybind11::arg("ints"), pybind11::arg("dist"), pybind11::arg("flts"),
         pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("wv"), pybind11::arg("bv"),
         pybind11::arg("io"), pybind11::arg("pw"), pybind11::arg("pwv"), pybind11::arg("zero"), pybind11::arg("actor"),

@@ -1558,7 +1558,8 @@ class HipCnnExecutor(HipExecutor):
         ext.qnet_cnn_bwd([ws['dz3'].data_ptr(), ws['a1'].data_ptr(), ws['a2'].data_ptr(), ws['a3'].data_ptr(),
                           pko('conv3/dgrad'), pko('conv2/dgrad'), ws['dc1'].data_ptr(), ws['dc2'].data_ptr(),
                           ws['dc3'].data_ptr()], B,
-                         prof=self.cnn_prof[1].data_ptr() if self.cnn_prof is not None else 0)
+                         prof=self.cnn_prof[1].data_ptr() if self.cnn_prof is not None else 0,
+                         parts=self.tuning.cnn_parts(self.compute_dtype))
         c1, c2, c3 = self.arch.convs
         t1, _, l1, _ = c1.pads()
         t2, _, l2, _ = c2.pads()

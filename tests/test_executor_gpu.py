@@ -122,6 +122,25 @@ def test_loss_and_grad_match_oracle(extra, B, weighted):
         assert cos > cmin and abs(ratio - 1.0) < tol, (name, cos, ratio)
 
 
+@pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
+def test_cnn_backward_two_parts_equals_one(dtype):
+    """Reference cnn backward with two workgroups per sample (KernelTuning cnn_bwd_parts=2, the
+    default: the conv2 dgrad m-tiles and pool1 windows split) == one workgroup per sample: the same
+    d(conv pre-activation) buffers bit for bit, the same gradient up to the wgrad atomics' order."""
+    outs = []
+    for parts in (1, 2):
+        net, _, batch = _setup('cnn:--dtype=%s --kernel_tuning=cnn_bwd_parts=%d' % (dtype, parts))
+        assert net.executor.tuning.cnn_parts(dtype) == parts
+        g = torch.zeros_like(net.online.flat)
+        net.executor.loss_and_grad(net.online.flat, net.target.flat, batch, g, net.noise, net.noise_target)
+        torch.cuda.synchronize()
+        ws = net.executor._workspace(32, DEV)
+        outs.append((g.clone(), [ws[k].clone() for k in ('dc1', 'dc2', 'dc3')]))
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-3, atol=1e-6)
+
+
 @pytest.mark.parametrize('dtype', ['bf16', 'fp16'])
 def test_learner_step_graph_equals_eager(dtype):
     """HIP-graph replay of the full SGD step == the same step run eagerly."""
