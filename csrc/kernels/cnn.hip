@@ -335,10 +335,11 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4 * 256];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, kg = 8 * (lane >> 4);
-  // two workgroups per sample (gridDim.y == 2): both run the cheap stages up to dz2 (part 0 writes
-  // dz3 / dz2), then each takes half of the conv2 dgrad m-tiles and their pool1 windows -- one
+  // two or four workgroups per sample (gridDim.y): all run the cheap stages up to dz2 (part 0 writes
+  // dz3 / dz2), then each takes its share of the conv2 dgrad m-tiles and their pool1 windows -- one
   // workgroup per sample held the 32-sample backward on 32 CUs, the conv2 dgrad MFMA-bound there
-  // in the fp32 build (16 of its 30 us, scripts/probe_cnn.py)
+  // in the fp32 build (16 of its 30 us, scripts/probe_cnn.py). Four parts: ref fp32 9.1k -> 10.6k,
+  // bf16 17.4k -> 18.6k SGD steps/s (KernelTuning.cnn_bwd_parts)
   const int part = blockIdx.y, nparts = gridDim.y;
   // probe stamps: 0 start, 1 loads, 2 pool3, 3 conv3 dgrad, 4 pool2, 5 conv2 dgrad, 6 a1 staged, 7 end
   int64_t* prof = (a.prof != nullptr && tid == 0 && part == 0) ? a.prof + 8 * (int64_t)b : nullptr;
@@ -417,13 +418,17 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
   // two tasks share their B fragments, loaded once per 8-deep batch, the next batch in flight (16-bit
   // builds: double-buffered) while this one's MFMAs run; batch 0 issued now, under pool2's work
   const bfx8* W2 = reinterpret_cast<const bfx8*>(a.w2d);
-  // (one part: m-tiles w >> 1 and (w >> 1) + 4 per wave; two parts: m-tile 4 part + (w >> 1) only)
-  const int nt2 = wave & 1, mtA = (wave >> 1) + 4 * part;
+  // (one part: m-tiles w >> 1 and (w >> 1) + 4 per wave; two parts: m-tile 4 part + (w >> 1) only;
+  //  four parts: m-tile 2 part + ((w >> 1) & 1), the K range halved over w >> 2, partials met in LDS)
+  const int nt2 = wave & 1;
+  const int mtA = nparts == 4 ? 2 * part + ((wave >> 1) & 1) : (wave >> 1) + 4 * part;
+  const int kh2 = nparts == 4 ? wave >> 2 : 0;
+  const int q0 = 2 * kh2, q1 = nparts == 4 ? q0 + 2 : 4;   // this wave's 8-deep k-step batches
   const bool twom = nparts == 1;
   constexpr int NB2 = DQN_ACT_F32 ? 1 : 2;                 // B batches in registers
   bfx8 bf[NB2][8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) bf[0][u] = W2[(u * 2 + nt2) * 64 + lane];
+  for (int u = 0; u < 8; ++u) bf[0][u] = W2[((8 * q0 + u) * 2 + nt2) * 64 + lane];
   __syncthreads();
   CNN_MARK(3);
 
@@ -458,12 +463,13 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
     };
 #pragma unroll
     for (int q = 0; q < 4; ++q) {                           // 4 batches of 8 k-steps
+      if (q < q0 || q >= q1) continue;
       const int cur = NB2 == 2 ? (q & 1) : 0;
-      if (NB2 == 1 && q > 0) {
+      if (NB2 == 1 && q > q0) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) bf[0][u] = W2[((8 * q + u) * 2 + nt2) * 64 + lane];
       }
-      if (NB2 == 2 && q + 1 < 4) {
+      if (NB2 == 2 && q + 1 < q1) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) bf[(q + 1) & (NB2 - 1)][u] = W2[((8 * (q + 1) + u) * 2 + nt2) * 64 + lane];
       }
@@ -474,10 +480,15 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
         if (twom) cB = tmfma(gather(mB, iyB, ixB, ks), bf[cur][u], cB);
       }
     }
+    if (nparts == 4) {                                      // the two K halves of each task
+      if (kh2 == 1) park(red, wave & 3, lane, cA);
+      __syncthreads();
+      if (kh2 == 0) cA = unpark(red, wave & 3, lane, cA);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ma = mtA * 16 + 4 * (lane >> 4) + r, mb = (mtA + 4) * 16 + 4 * (lane >> 4) + r;
-      if (ma < Q1 * Q1) dp1[ma * N1 + nt2 * 16 + l16] = cA[r];
+      if (kh2 == 0 && ma < Q1 * Q1) dp1[ma * N1 + nt2 * 16 + l16] = cA[r];
       if (twom && mb < Q1 * Q1) dp1[mb * N1 + nt2 * 16 + l16] = cB[r];
     }
   }
@@ -493,8 +504,8 @@ __global__ void __launch_bounds__(512) cnn_bwd_kernel(CnnBwdArgs a) {
 
   // ---- pool1 backward + mask -> dz1 (global only: the conv1 wgrad input)
   act_t* gdz1 = a.dz1 + (int64_t)b * R1 * N1;
-  // (this part's windows: the dp1 rows its conv2 dgrad m-tiles made -- 64 per part of two)
-  const int w_lo = nparts == 1 ? 0 : 64 * part, w_hi = nparts == 1 ? Q1 * Q1 : min(Q1 * Q1, 64 * part + 64);
+  // (this part's windows: the dp1 rows its conv2 dgrad m-tiles made -- 128 / nparts per part)
+  const int w_lo = (128 / nparts) * part, w_hi = min(Q1 * Q1, w_lo + 128 / nparts);
   for (int t = tid + w_lo * (N1 / 8); t < w_hi * (N1 / 8); t += 512) {      // (window-major, one round)
     const int w = t / (N1 / 8), c8 = (t - w * (N1 / 8)) * 8, py = w / Q1, px = w - py * Q1;
     bfx8 o[4];
@@ -520,5 +531,5 @@ void launch_cnn_fwd(const CnnFwdArgs& a, int B, int ninst, hipStream_t st) {
 }
 
 void launch_cnn_bwd(const CnnBwdArgs& a, int B, int parts, hipStream_t st) {
-  hipLaunchKernelGGL(cnn_bwd_kernel, dim3(B, parts == 2 ? 2 : 1), dim3(512), 0, st, a);
+  hipLaunchKernelGGL(cnn_bwd_kernel, dim3(B, (parts == 2 || parts == 4) ? parts : 1), dim3(512), 0, st, a);
 }

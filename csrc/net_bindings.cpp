@@ -295,7 +295,7 @@ void cnn_fwd(int64_t frames, std::vector<int64_t> ptrs, int64_t B, int64_t ninst
 
 // ptrs: dp3, a1, a2, a3, w3d, w2d, dz1, dz2, dz3
 void cnn_bwd(std::vector<int64_t> ptrs, int64_t B, int64_t prof, int64_t parts) {
-  TORCH_CHECK(ptrs.size() == 9 && B >= 1 && (parts == 1 || parts == 2), "cnn_bwd args (parts 1 or 2)");
+  TORCH_CHECK(ptrs.size() == 9 && B >= 1 && (parts == 1 || parts == 2 || parts == 4), "cnn_bwd args (parts 1, 2, 4)");
   for (auto p : ptrs) TORCH_CHECK(p != 0, "cnn_bwd: null pointer");
   dqn::CnnBwdArgs a{};
   a.dp3 = P<const act_t*>(ptrs[0]); a.a1 = P<const act_t*>(ptrs[1]); a.a2 = P<const act_t*>(ptrs[2]);

@@ -35,8 +35,10 @@ class KernelTuning:
     # mixes its noise inside the fc forward. Measured slower (optimizer 58.4 -> 53.2 us but the fc
     # forward 10.5 -> 20.0 us: 7.29k -> 7.04k SGD steps/s, profiles/r5_late_ab.md), so opt-in
     tfact: int = 0
-    # reference `cnn` backward: workgroups per sample (1 or 2: the conv2 dgrad m-tiles and pool1 windows
-    # split over two); -1 = the measured best per build
+    # reference `cnn` backward: workgroups per sample (1, 2 or 4: the conv2 dgrad m-tiles and pool1
+    # windows split over them; 4 also halves each wave's K range). -1 = 4, the measured best in both
+    # builds: fp32 9.13k / 9.98k / 10.56k, bf16 17.41k / 17.99k / 18.61k SGD steps/s for 1 / 2 / 4
+    # (`--variant ref`, profiles/r6_ab_cnn_bwd_parts.jsonl)
     cnn_bwd_parts: int = -1
 
     @classmethod
@@ -54,15 +56,15 @@ class KernelTuning:
         t = cls(**kw)
         if t.wg_conv_chunks != -1 and not 1 <= t.wg_conv_chunks <= 8:
             raise ValueError('--kernel_tuning: wg_conv_chunks -1 (auto) or in [1, 8]')
-        if t.cnn_bwd_parts not in (-1, 1, 2):
-            raise ValueError('--kernel_tuning: cnn_bwd_parts -1 (auto), 1 or 2')
+        if t.cnn_bwd_parts not in (-1, 1, 2, 4):
+            raise ValueError('--kernel_tuning: cnn_bwd_parts -1 (auto), 1, 2 or 4')
         return t
 
     def cnn_parts(self, dtype: str) -> int:
         """Workgroups per sample of the reference cnn's fused backward (``cnn_bwd_parts``, -1 resolved)."""
         if self.cnn_bwd_parts > 0:
             return self.cnn_bwd_parts
-        return 2
+        return 4
 
     def conv_chunks(self, network: str, dtype: str) -> int:
         """Row chunks per fused conv weight-gradient tile (``wg_conv_chunks``, -1 resolved)."""

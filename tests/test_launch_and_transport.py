@@ -287,9 +287,9 @@ def test_kernel_tuning_parse():
             auto.conv_chunks('cnn', 'fp32')) == (3, 6, 2, 4)
     assert t.conv_chunks('cnn', 'fp32') == 2
     assert (auto.cnn_parts('fp32'), auto.cnn_parts('bf16'), KernelTuning.parse('cnn_bwd_parts=1').cnn_parts('fp32')) \
-        == (2, 2, 1)
+        == (4, 4, 1)
     with pytest.raises(ValueError):
-        KernelTuning.parse('cnn_bwd_parts=3')
+        KernelTuning.parse('cnn_bwd_parts=3')  # (1, 2 or 4)
     with pytest.raises(ValueError):
         KernelTuning.parse('wg_mix=1')              # removed knob: refused, not ignored
     cfg = preset('nature', 'Pong-v0', '--kernel_tuning=dep_at=0')
