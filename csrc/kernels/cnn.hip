@@ -146,6 +146,60 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
   CNN_MARK(1);
 
   // ---- conv1 (8x8/4 SAME) -> a1 = ReLU(scale*acc + b); both n-tiles per wave
+#if DQN_ACT_F32
+  // fp32 build: the uint8 input is exact in bf16, so each fp32 weight fragment runs as three bf16
+  // fragments (split3_bf16, fused_util.h): 3 bf16 MFMAs instead of 8 fp32 ones per k-step. A wave's
+  // m-tiles (4) share each split, made once per k-step.
+  {
+    const float scale = a.scale;
+    const int kw = kg >> 2;
+    act_t* ga1 = keep ? a.a1 + (int64_t)b * R1 * N1 : nullptr;
+    constexpr int NMT = (R1 + 15) / 16, MTW = (NMT + 7) / 8;
+    f32x4 c0[MTW], c1[MTW];
+    int off[MTW];
+    bool okm[MTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const int mt = wave + 8 * i, p = mt * 16 + l16;
+      okm[i] = mt < NMT && p < R1;
+      const int q = okm[i] ? p : 0, oy = q / O1, ox = q - oy * O1;
+      off[i] = ((oy * 4) * XW + ox * 4 + kw) * 4;
+      c0[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c1[i] = c0[i];
+    }
+#pragma unroll
+    for (int ks = 0; ks < K1 / 32; ++ks) {
+      b16x8 h0, m0, l0, h1, m1, l1;
+      split3_bf16(w1r[0][ks], h0, m0, l0);
+      split3_bf16(w1r[1][ks], h1, m1, l1);
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        if (wave + 8 * i >= NMT) continue;                  // (wave-uniform)
+        b16x8 x;
+        if (okm[i]) {
+          x = *reinterpret_cast<const b16x8*>(xin + off[i] + ks * XW * 4);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.f;
+        }
+        c0[i] = mfma3_bf16(h0, m0, l0, x, c0[i]);
+        c1[i] = mfma3_bf16(h1, m1, l1, x, c1[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      if (!okm[i]) continue;
+      const int p = (wave + 8 * i) * 16 + l16;
+      const pk4_t v0 = pack4(c0[i] * scale + f4(bias1a)), v1 = pack4(c1[i] * scale + f4(bias1b));
+      *reinterpret_cast<pk4_t*>(a1 + p * L1 + cq) = v0;
+      *reinterpret_cast<pk4_t*>(a1 + p * L1 + 16 + cq) = v1;
+      if (ga1 != nullptr) {
+        *reinterpret_cast<pk4_t*>(ga1 + p * N1 + cq) = v0;
+        *reinterpret_cast<pk4_t*>(ga1 + p * N1 + 16 + cq) = v1;
+      }
+    }
+  }
+#else
   {
     const float scale = a.scale;
     const int kw = kg >> 2;
@@ -175,6 +229,7 @@ __global__ void __launch_bounds__(512) cnn_fwd_kernel(CnnFwdArgs a) {
       }
     }
   }
+#endif
   CNN_MARK(2);
   if constexpr (!kEarlyW) load_w2();
   __syncthreads();

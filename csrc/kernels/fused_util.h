@@ -71,6 +71,30 @@ DQN_DEV void planes_to_lds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, i
   reinterpret_cast<uint4*>(dst)[1] = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
+#if DQN_ACT_F32
+// fp32 build, layers whose input is exact in bf16 (conv1: the uint8 frames): the fp32 weight fragment
+// as three bf16 fragments whose sum is exactly the fp32 value (8 + 8 + 8 significand bits), so three
+// bf16 MFMAs (16x16x32) give products that are exact in fp32 and fp32 accumulation -- the fp32
+// convolution up to summation order -- instead of eight fp32 MFMAs (16x16x4) per 32-deep k-step.
+typedef __attribute__((ext_vector_type(8))) __bf16 b16x8;
+DQN_DEV void split3_bf16(const bfx8& v, b16x8& h, b16x8& m, b16x8& l) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 hj = (__bf16)v[j];
+    const float r1 = v[j] - (float)hj;
+    const __bf16 mj = (__bf16)r1;
+    h[j] = hj;
+    m[j] = mj;
+    l[j] = (__bf16)(r1 - (float)mj);
+  }
+}
+DQN_DEV f32x4 mfma3_bf16(const b16x8& h, const b16x8& m, const b16x8& l, const b16x8& x, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(l, x, c, 0, 0, 0);      // (small terms first)
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, x, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, x, c, 0, 0, 0);
+}
+#endif
+
 // K-split partial-sum exchange: waves of k-half 1 park their fp32 accumulators
 // in LDS, waves of k-half 0 add them after the barrier.
 DQN_DEV void park(float* red, int slot, int lane, const f32x4& acc) {

@@ -239,6 +239,59 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       for (int ks = 0; ks < K1 / 32; ++ks) f[ks] = ld_in8(base + ks * IW * 4);
     };
     const int MT = (np1 + 15) / 16;                       // 25 m-tiles whole, 18 / 15 per part
+#if DQN_ACT_F32
+    // fp32 build: the frames are exact in bf16, so each fp32 weight fragment (LDS) runs as three bf16
+    // fragments (split3_bf16, fused_util.h): 3 bf16 MFMAs per k-step instead of 8 fp32 ones. k-step
+    // outer, the wave's m-tiles inner: one split per k-step and n-tile, shared by the m-tiles.
+    constexpr int MTW = (R1 / 16 + 7) / 8;
+    f32x4 c0[MTW], c1[MTW];
+    const in_t* base[MTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const int p = min((wave + 8 * i) * 16 + row, np1 - 1), oy = p / O1, ox = p - oy * O1;   // (tail clamped)
+      base[i] = xin + ((oy * 4) * IW + ox * 4 + kw) * 4;
+      c0[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c1[i] = c0[i];
+    }
+    // (the fp32 weight fragments, 32 B per lane each, stay in LDS and are read per k-step: held in
+    //  registers -- 128 VGPRs -- they pushed the kernel past 256 VGPRs into scratch spills)
+    const float4* wp = reinterpret_cast<const float4*>(wl1);
+    auto wfrag = [&](int f) {
+      const float4 lo = wp[(2 * f) * 64 + lane], hi4 = wp[(2 * f + 1) * 64 + lane];
+      bfx8 v;
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi4.x; v[5] = hi4.y; v[6] = hi4.z; v[7] = hi4.w;
+      return v;
+    };
+#pragma unroll
+    for (int ks = 0; ks < K1 / 32; ++ks) {              // k = (kh*8 + kw)*4 + c, kh = ks
+      b16x8 h0, m0, l0, h1, m1, l1;
+      split3_bf16(wfrag(ks * 2 + 0), h0, m0, l0);
+      split3_bf16(wfrag(ks * 2 + 1), h1, m1, l1);
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        if (wave + 8 * i >= MT) continue;                 // wave-uniform
+        const b16x8 x = *reinterpret_cast<const b16x8*>(base[i] + ks * IW * 4);
+        c0[i] = mfma3_bf16(h0, m0, l0, x, c0[i]);
+        c1[i] = mfma3_bf16(h1, m1, l1, x, c1[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const int mt = wave + 8 * i;
+      if (mt >= MT) break;                                // wave-uniform
+      const int p = mt * 16 + row;
+      if (p < np1) {
+        const pk4_t v0 = pack4(c0[i] * scale + f4(bias1a)), v1 = pack4(c1[i] * scale + f4(bias1b));
+        *reinterpret_cast<pk4_t*>(act1 + p * L1 + cq) = v0;
+        *reinterpret_cast<pk4_t*>(act1 + p * L1 + 16 + cq) = v1;
+        const int oy = p / O1;
+        if (x1 != nullptr && oy >= c1o && oy < c1e) {   // conv2 wgrad input + ReLU mask (owned rows)
+          *reinterpret_cast<pk4_t*>(x1 + p * N1 + cq) = v0;
+          *reinterpret_cast<pk4_t*>(x1 + p * N1 + 16 + cq) = v1;
+        }
+      }
+    }
+#else
 #pragma unroll
     for (int i = 0; i < (R1 / 16 + 7) / 8; ++i) {
       const int mt = wave + 8 * i;
@@ -248,22 +301,8 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
       for (int ks = 0; ks < K1 / 32; ++ks) {              // k = (kh*8 + kw)*4 + c, kh = ks
-#if DQN_ACT_F32
-        // fp32 build: the weight fragments (32 B per lane each) stay in LDS and are read per k-step:
-        // held in registers (128 VGPRs) they pushed the kernel past 256 VGPRs into scratch spills
-        const float4* wp = reinterpret_cast<const float4*>(wl1);
-        auto wfrag = [&](int f) {
-          const float4 lo = wp[(2 * f) * 64 + lane], hi4 = wp[(2 * f + 1) * 64 + lane];
-          bfx8 v;
-          v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi4.x; v[5] = hi4.y; v[6] = hi4.z; v[7] = hi4.w;
-          return v;
-        };
-        c0 = tmfma(wfrag(ks * 2 + 0), fa[ks], c0);
-        c1 = tmfma(wfrag(ks * 2 + 1), fa[ks], c1);
-#else
         c0 = tmfma(w1r[0][ks], fa[ks], c0);
         c1 = tmfma(w1r[1][ks], fa[ks], c1);
-#endif
       }
       const int p = mt * 16 + row;
       if (p < np1) {
@@ -277,6 +316,7 @@ __global__ void __launch_bounds__(512) trunk_fwd_kernel(TrunkArgs a) {
         }
       }
     }
+#endif
   }
   // conv3 fragments into the registers conv1 released (latency hidden by conv2)
   bfx8 w3r[K3 / 64];
