@@ -19,10 +19,12 @@ import dataclasses
 class KernelTuning:
     # row chunks (128 rows; 64 in the fp32 build) per conv weight-gradient tile of the fused wgrad +
     # update launch (summed in registers, one set of fp32 atomics per tile). -1 = the measured best
-    # per net and build: Nature 384 rows per tile -- bf16 3 > 2 > 4 on the flagship (15.33k / 15.04k /
-    # 14.76k SGD steps/s, profiles/r5_late_ab.md), fp32 6 x 64 (9.52k vs 9.33k at 3, round 6) --; the
-    # reference `cnn` 256 rows -- bf16 2 > 1 > 3 > 6 (17.71k / 15.89k / 16.67k / 14.61k,
-    # profiles/r6_ab_wg_chunks.jsonl)
+    # per net and build: Nature bf16 3 x 128 rows -- 3 > 2 > 4 on the flagship (15.33k / 15.04k /
+    # 14.76k SGD steps/s, profiles/r5_late_ab.md; again after the round-6 tile loads: 15.40-15.55k /
+    # 15.06-15.09k / 14.97k) --, Nature fp32 4 x 64 (10.13-10.19k vs 9.91k at 6, 10.14k at 5, 9.92-9.96k
+    # at 3, 9.47k at 2, profiles/r6_ab_wg_chunks_late.jsonl); the reference `cnn` 256 rows -- bf16 2 > 3
+    # (18.52k / 17.43k; round 6 earlier: 2 > 1 > 3 > 6, profiles/r6_ab_wg_chunks.jsonl), fp32 4 > 3 > 6 > 2
+    # (11.66-11.67k / 11.45k / 10.75k / 10.80k)
     wg_conv_chunks: int = -1
     # grid position of the range-dependent update jobs of that launch: after the first ``dep_at`` fc
     # jobs; -1 = the measured policy (noisy nets: after 500 of their ~1.6k fc jobs, +0.3-1.0 % over
@@ -70,5 +72,6 @@ class KernelTuning:
         """Row chunks per fused conv weight-gradient tile (``wg_conv_chunks``, -1 resolved)."""
         if self.wg_conv_chunks > 0:
             return self.wg_conv_chunks
-        rows = 256 if network == 'cnn' else 384
-        return rows // (64 if dtype == 'fp32' else 128)
+        if dtype == 'fp32':
+            return 4                                   # (4 x 64 rows, both nets)
+        return 2 if network == 'cnn' else 3

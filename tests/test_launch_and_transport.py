@@ -284,7 +284,7 @@ def test_kernel_tuning_parse():
     assert (t.wg_conv_chunks, t.dep_at, t.fold_two_per_cu, t.tfact) == (2, 300, 1, 1)
     auto = KernelTuning()                           # -1: the measured best per net / build
     assert (auto.conv_chunks('nature', 'bf16'), auto.conv_chunks('nature', 'fp32'), auto.conv_chunks('cnn', 'bf16'),
-            auto.conv_chunks('cnn', 'fp32')) == (3, 6, 2, 4)
+            auto.conv_chunks('cnn', 'fp32')) == (3, 4, 2, 4)
     assert t.conv_chunks('cnn', 'fp32') == 2
     assert (auto.cnn_parts('fp32'), auto.cnn_parts('bf16'), KernelTuning.parse('cnn_bwd_parts=1').cnn_parts('fp32')) \
         == (4, 4, 1)
