@@ -156,16 +156,6 @@ def timeline_fc_only(ex, nfc, fn):
     rows = [(t[3 * b], t[3 * b + 2]) for b in range(nfc + 1) if t[3 * b]]
     out = {'start': pct([(a - t0) / 100.0 for a, _ in rows]), 'dur': pct([(e - a) / 100.0 for a, e in rows]),
            'end': pct([(e - t0) / 100.0 for _, e in rows]), 'blocks': len(rows)}
-    if hasattr(ex.ext, 'optim_job_phases'):
-        jp = ex.ext.optim_job_phases(nfc + 1)
-        ph = []
-        for b in range(1, nfc + 1):
-            s = jp[8 * b: 8 * b + 5]
-            if all(s) and t[3 * b] and t[3 * b + 2]:
-                ph.append([(s[0] - t[3 * b]) / 100.0] + [(s[i + 1] - s[i]) / 100.0 for i in range(4)]
-                          + [(t[3 * b + 2] - s[4]) / 100.0])
-        if ph:
-            out['fc_job_phases_p50'] = [round(sorted(c)[len(c) // 2], 2) for c in zip(*ph)]
     return out
 
 
@@ -194,23 +184,6 @@ def timeline(ex, plan, nwg, jobs, nfc, nint, fn):
         tl['fc_jobs'] = {'start': pct([us(t[3 * b]) for b in fcb]), 'dur': pct([(t[3 * b + 2] - t[3 * b]) / 100.0
                                                                                 for b in fcb]),
                          'end': pct([us(t[3 * b + 2]) for b in fcb])}
-        # the fc jobs' item phases (optim_pack.h kJobPhOff): block start -> item entry (descriptor) ->
-        # operand rows staged (load batch arrived) -> fc gradient formed -> update stores issued ->
-        # item end (fragments emitted) -> block end (arrival)
-        if hasattr(ex.ext, 'optim_job_phases'):
-            jp = ex.ext.optim_job_phases(ngrid)
-            rows = []
-            for b in fcb:
-                s = jp[8 * b: 8 * b + 5]
-                if all(s) and t[3 * b] and t[3 * b + 2]:
-                    rows.append([(s[0] - t[3 * b]) / 100.0] + [(s[i + 1] - s[i]) / 100.0 for i in range(4)]
-                                + [(t[3 * b + 2] - s[4]) / 100.0])
-            if rows:
-                tl['fc_job_phases_us'] = {
-                    'names': ['start->entry', 'entry->staged', 'staged->grad', 'grad->stores', 'stores->end',
-                              'end->arrive'],
-                    'p50': [round(sorted(c)[len(c) // 2], 2) for c in zip(*rows)],
-                    'p90': [round(sorted(c)[int(0.9 * (len(c) - 1))], 2) for c in zip(*rows)], 'n': len(rows)}
         dep = range(1 + nwg + nfc, ngrid)
         if len(dep):
             tl['dep_jobs'] = {'start': pct([us(t[3 * b]) for b in dep]), 'ready': pct([us(t[3 * b + 1]) for b in dep]),
