@@ -314,8 +314,18 @@ DQN_DEV void wgrad_tile(const ConvArgs& a, const WgradArgs& g, int bx, int by, i
   // thread -> (row r, piece p): the TPR threads of a row adjacent, so a wave's 16-byte loads cover
   // whole 64-byte runs of 16 rows (row-major NHWC / dZ rows) instead of 16 bytes of 64 rows each: 4x
   // fewer cache-line requests through the CU's address unit per load instruction (fused launch
-  // 22.7 -> 21.3 us, bf16). fp32: the transposed staging then swizzles m by k (fsw below)
+  // 22.7 -> 21.3 us, bf16). fp32: the transposed staging then swizzles m by k (fsw below).
+  // 16-bit builds: the 4 rows of one 16-lane ds_write_b128 pass are rows {0,2,4,6} / {1,3,5,7} (+8) of
+  // the wave's 16: at 160-byte row strides rows 0 and 3 share banks (2-way conflicts, 22 % of the
+  // launch's LDS cycles, profiles/r6_pmc_final_dqn.md); rows 0, 2, 4, 6 start on disjoint 16-bank windows
+#if DQN_ACT_F32
   const int r = tid / TPR, p = tid % TPR;
+#else
+  static_assert(TPR != 4 || MC % 16 == 0, "row interleave: 16-row waves");
+  const int q16 = (tid & 63) / TPR, pass = q16 >> 2;
+  const int r = TPR == 4 ? (tid >> 6) * 16 + (pass >> 1) * 8 + (q16 & 3) * 2 + (pass & 1) : tid / TPR;
+  const int p = tid % TPR;
+#endif
   // two chunk slots in registers: both chunks' loads are issued before either is converted / staged
   // (the u8 conv1 loaders convert inside frag(), and the frame loader's addresses depend on a
   // slot-table load: chunk by chunk, the tile paid ~4 dependent round trips for its 2 chunks)
