@@ -428,10 +428,14 @@ optim_pack_kernel(float* __restrict__ W, const float* __restrict__ G, float* __r
       const bfx8 v = m0 == 0 ? v0 : fc_load(jb, m0);
       __syncthreads();                 // previous chunk's operand reads / previous item's R reads done
 #if DQN_ACT_F32
+      // (8-byte stores: the padded row strides keep even float offsets; 8 scalar stores per row piece
+      //  put the fp32 launch's LDS bank conflicts at 31 %, profiles/r6_pmc_final_ref_fp32.md)
+      {
+        float* dst = lx ? Xs + lr * kFcSX + lc : Hs + lr * kFcSH + lc;
+        if (lx || lh) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (lx) Xs[lr * kFcSX + lc + j] = v[j];
-        else if (lh) Hs[lr * kFcSH + lc + j] = v[j];
+          for (int j = 0; j < 8; j += 2) *reinterpret_cast<float2*>(dst + j) = make_float2(v[j], v[j + 1]);
+        }
       }
       __syncthreads();
       // A = dh^T (rows n), B = x (columns k): lane (row = lane & 15, g = lane >> 4) holds chunk rows
